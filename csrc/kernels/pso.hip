@@ -1,0 +1,56 @@
+// Fused PSO tell (K7): pbest select + velocity/position update + clip in one pass.
+// rp / rg are regenerated from Philox counters (element index = row*d + col, the
+// same words evoxmi.ops.random.uniform produces), so no (N, d) noise is stored.
+// Each thread owns 4 consecutive elements = one Philox block per key.
+#include "evoxmi_common.h"
+
+namespace {
+
+__global__ void __launch_bounds__(256) pso_kernel(const float* __restrict__ pop, const float* __restrict__ vel,
+                                                  const float* __restrict__ lbl, const float* __restrict__ lbf,
+                                                  const float* __restrict__ fit, const float* __restrict__ gbl,
+                                                  const int64_t* __restrict__ kp, const int64_t* __restrict__ kg,
+                                                  float w, float phip, float phig, const float* __restrict__ lb,
+                                                  const float* __restrict__ ub, float* __restrict__ opop,
+                                                  float* __restrict__ ovel, float* __restrict__ olbl,
+                                                  float* __restrict__ olbf, int N, int D) {
+  uint32_t p0, p1, g0, g1;
+  evx::load_key(kp, p0, p1);
+  evx::load_key(kg, g0, g1);
+  const int64_t total = (int64_t)N * D;
+  const int64_t nb = (total + 3) >> 2;
+  for (int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; b < nb; b += (int64_t)gridDim.x * blockDim.x) {
+    evx::u4 wp = evx::philox_block((uint64_t)b, p0, p1);
+    evx::u4 wg = evx::philox_block((uint64_t)b, g0, g1);
+    uint32_t rpw[4] = {wp.x, wp.y, wp.z, wp.w};
+    uint32_t rgw[4] = {wg.x, wg.y, wg.z, wg.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int64_t i = (b << 2) + j;
+      if (i >= total) break;
+      int r = (int)(i / D), c = (int)(i - (int64_t)r * D);
+      float x = pop[i];
+      bool better = lbf[r] > fit[r];
+      float lb_loc = better ? x : lbl[i];
+      float v = w * vel[i] + phip * evx::u24(rpw[j]) * (lb_loc - x) + phig * evx::u24(rgw[j]) * (gbl[c] - x);
+      float nx = fminf(fmaxf(x + v, lb[c]), ub[c]);
+      opop[i] = nx;
+      ovel[i] = v;
+      olbl[i] = lb_loc;
+      if (c == 0) olbf[r] = fminf(lbf[r], fit[r]);
+    }
+  }
+}
+
+}  // namespace
+
+void evx_pso_update(const float* pop, const float* vel, const float* lbl, const float* lbf, const float* fit,
+                    const float* gbl, const int64_t* kp, const int64_t* kg, float w, float phip, float phig,
+                    const float* lb, const float* ub, float* opop, float* ovel, float* olbl, float* olbf, int N, int D,
+                    hipStream_t s) {
+  int64_t nb = ((int64_t)N * D + 3) / 4;
+  int grid = (int)((nb + 255) / 256);
+  if (grid > 8192) grid = 8192;
+  if (grid < 1) grid = 1;
+  pso_kernel<<<grid, 256, 0, s>>>(pop, vel, lbl, lbf, fit, gbl, kp, kg, w, phip, phig, lb, ub, opop, ovel, olbl, olbf, N, D);
+}

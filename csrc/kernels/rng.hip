@@ -1,0 +1,44 @@
+// Philox4x32-10 bulk generation (uniform / normal) — K1 of SURVEY §2.10.
+// One thread = one Philox block = 4 outputs, stored as one 16-B float4 (coalesced
+// 1 KiB per wave-instruction).  The key is read from device memory so the launch
+// is hipGraph-capturable (no host round-trip for the key).
+#include "evoxmi_common.h"
+
+namespace {
+
+template <int DIST>
+__global__ void __launch_bounds__(256) philox_fill_kernel(float* __restrict__ out, int64_t n,
+                                                          const int64_t* __restrict__ key, int64_t block_offset) {
+  uint32_t k0, k1;
+  evx::load_key(key, k0, k1);
+  const int64_t nb = (n + 3) >> 2;
+  for (int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; b < nb; b += (int64_t)gridDim.x * blockDim.x) {
+    evx::u4 w = evx::philox_block((uint64_t)(b + block_offset), k0, k1);
+    float4 v;
+    if (DIST == 0) {
+      v = make_float4(evx::u24(w.x), evx::u24(w.y), evx::u24(w.z), evx::u24(w.w));
+    } else {
+      v = evx::normal4(w);
+    }
+    const int64_t i = b << 2;
+    if (i + 3 < n) {
+      *reinterpret_cast<float4*>(out + i) = v;
+    } else {
+      float t[4] = {v.x, v.y, v.z, v.w};
+      for (int j = 0; j < 4 && i + j < n; ++j) out[i + j] = t[j];
+    }
+  }
+}
+
+}  // namespace
+
+void evx_philox_fill(float* out, int64_t n, const int64_t* key, int dist, int64_t elem_offset, hipStream_t s) {
+  const int64_t nb = (n + 3) >> 2;
+  int grid = (int)((nb + 255) / 256);
+  if (grid > 4096) grid = 4096;
+  if (grid < 1) grid = 1;
+  if (dist == 0)
+    philox_fill_kernel<0><<<grid, 256, 0, s>>>(out, n, key, elem_offset >> 2);
+  else
+    philox_fill_kernel<1><<<grid, 256, 0, s>>>(out, n, key, elem_offset >> 2);
+}

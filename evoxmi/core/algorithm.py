@@ -1,0 +1,39 @@
+"""Algorithm base class (reference ``src/evox/core/algorithm.py:10-90``).
+
+``ask(state) -> (population, state)`` proposes candidates, ``tell(state, fitness)
+-> state`` consumes their (minimisation-oriented) fitness.  ``init_ask`` /
+``init_tell`` are optional: when overridden, the workflow uses them at
+generation 0 (the first population may differ in size from later ones).
+"""
+from typing import Tuple
+
+import torch
+
+from .module import Stateful
+from .state import State
+
+
+class Algorithm(Stateful):
+    """Base class for all algorithms."""
+
+    def init_ask(self, state: State) -> Tuple[torch.Tensor, State]:
+        return None, State()
+
+    def init_tell(self, state: State, fitness: torch.Tensor) -> State:
+        return State()
+
+    def ask(self, state: State) -> Tuple[torch.Tensor, State]:
+        return torch.zeros(0), State()
+
+    def tell(self, state: State, fitness: torch.Tensor) -> State:
+        return State()
+
+
+def algorithm_has_init_ask(algorithm: Algorithm, state: State = None) -> bool:
+    """True when ``algorithm`` overrides ``init_ask`` (reference ``utils/common.py:15-19``).
+
+    The reference probes the method with ``eval_shape``; without a tracer we inspect
+    the class hierarchy instead, which gives the same answer for every algorithm
+    that follows the base-class contract (``init_ask`` returning ``None`` = absent).
+    """
+    return type(algorithm).init_ask is not Algorithm.init_ask

@@ -1,0 +1,171 @@
+"""Evaluation monitor (reference ``src/evox/monitors/eval_monitor.py:16-215``).
+
+Same public API (``get_best_fitness``, ``get_topk_solutions``, ``get_pf_fitness``,
+``get_history``, ``plot``, ``flush`` ...).  MI355X-first execution: the reference
+ships top-k rows to the host through ``io_callback`` every generation; here the
+top-k merge (SO) and the Pareto archive (MO) stay **device resident** and are
+computed with stream-ordered device ops only — ``post_eval`` never synchronises
+the host with the GPU, so it does not stall the generation pipeline (and works
+with graph replay, which hands it the graph's static output buffers).  Host
+copies happen only when a getter is called.
+"""
+from __future__ import annotations
+
+import warnings
+
+import torch
+
+from ..core import Monitor
+
+
+def _apply_dir(x, od):
+    if isinstance(od, torch.Tensor):
+        return x * od.to(x.device)
+    return x if od == 1 else x * od
+
+
+class EvalMonitor(Monitor):
+    def __init__(self, full_fit_history=True, full_sol_history=False, topk=1, calc_pf=False, history_to_host=False):
+        super().__init__()
+        self.full_fit_history = full_fit_history
+        self.full_sol_history = full_sol_history
+        self.topk = topk
+        self.calc_pf = calc_pf
+        self.history_to_host = history_to_host
+        self.fitness_history = []
+        self.solution_history = []
+        self.topk_fitness = None
+        self.topk_solutions = None
+        self.pf_solutions = None
+        self.pf_fitness = None
+        self.latest_solution = None
+        self.latest_fitness = None
+        self.eval_count = 0
+        self.opt_direction = 1
+
+    def hooks(self):
+        return ["post_eval"]
+
+    def set_opt_direction(self, opt_direction):
+        self.opt_direction = opt_direction
+
+    def _keep(self, x):
+        if x is None:
+            return None
+        if self.history_to_host and x.is_cuda:
+            h = torch.empty(x.shape, dtype=x.dtype, pin_memory=True)
+            h.copy_(x, non_blocking=True)
+            return h
+        return x.detach().clone()
+
+    def post_eval(self, _state, cand_sol, _transformed, fitness):
+        self.eval_count += int(fitness.shape[0])
+        if fitness.ndim == 1:
+            self.record_fit_single_obj(cand_sol, fitness)
+        else:
+            self.record_fit_multi_obj(cand_sol, fitness)
+
+    def record_fit_single_obj(self, cand_sol, fitness):
+        if self.full_sol_history:
+            self.solution_history.append(self._keep(cand_sol))
+        if self.full_fit_history:
+            self.fitness_history.append(self._keep(fitness))
+        n = fitness.shape[0]
+        k = min(self.topk, n)
+        if cand_sol is not None and cand_sol.shape[0] != n:
+            cand_sol = None  # distributed generic path: rows are sharded
+        if k == 1:
+            i = torch.argmin(fitness)
+            fit = fitness[i : i + 1] if False else fitness.index_select(0, i.reshape(1))
+            sol = cand_sol.index_select(0, i.reshape(1)) if cand_sol is not None else None
+            if self.topk_fitness is None:
+                self.topk_fitness, self.topk_solutions = fit.clone(), (sol.clone() if sol is not None else None)
+            else:
+                better = fit < self.topk_fitness  # device-side select, no host sync
+                self.topk_fitness = torch.where(better, fit, self.topk_fitness)
+                if sol is not None and self.topk_solutions is not None:
+                    self.topk_solutions = torch.where(better[:, None], sol, self.topk_solutions)
+        else:
+            vals, idx = torch.topk(fitness, k, largest=False, sorted=True)
+            sols = cand_sol.index_select(0, idx) if cand_sol is not None else None
+            if self.topk_fitness is not None:
+                vals = torch.cat([self.topk_fitness, vals])
+                if sols is not None and self.topk_solutions is not None:
+                    sols = torch.cat([self.topk_solutions, sols], 0)
+                v2, i2 = torch.topk(vals, k, largest=False, sorted=True)
+                vals = v2
+                if sols is not None:
+                    sols = sols.index_select(0, i2)
+            self.topk_fitness, self.topk_solutions = vals, sols
+
+    def record_fit_multi_obj(self, cand_sol, fitness):
+        from ..operators.selection.non_dominate import non_dominated_sort
+
+        if self.full_sol_history:
+            self.solution_history.append(self._keep(cand_sol))
+        if self.full_fit_history:
+            self.fitness_history.append(self._keep(fitness))
+        if self.calc_pf:
+            pf_f = fitness if self.pf_fitness is None else torch.cat([self.pf_fitness, fitness], 0)
+            pf_s = cand_sol if self.pf_solutions is None else torch.cat([self.pf_solutions, cand_sol], 0)
+            rank = non_dominated_sort(pf_f)
+            keep = rank == 0
+            self.pf_fitness = pf_f[keep]
+            self.pf_solutions = pf_s[keep]
+        self.latest_fitness = fitness.detach().clone()
+        self.latest_solution = cand_sol.detach().clone() if cand_sol is not None else None
+
+    # ---------------------------------------------------------------- getters
+    def get_latest_fitness(self):
+        return _apply_dir(self.latest_fitness, self.opt_direction)
+
+    def get_latest_solution(self):
+        return self.latest_solution
+
+    def get_pf_fitness(self):
+        return _apply_dir(self.pf_fitness, self.opt_direction)
+
+    def get_pf_solutions(self):
+        return self.pf_solutions
+
+    def get_topk_fitness(self):
+        return _apply_dir(self.topk_fitness, self.opt_direction)
+
+    def get_topk_solutions(self):
+        return self.topk_solutions
+
+    def get_best_solution(self):
+        return None if self.topk_solutions is None else self.topk_solutions[0]
+
+    def get_best_fitness(self):
+        if self.topk_fitness is None:
+            warnings.warn("trying to get info from a monitor with no recorded data")
+            return None
+        return _apply_dir(self.topk_fitness[0], self.opt_direction)
+
+    def get_history(self):
+        return [_apply_dir(f, self.opt_direction) for f in self.fitness_history]
+
+    def plot(self, problem_pf=None, **kwargs):
+        from ..vis_tools import plot
+
+        if not self.fitness_history:
+            warnings.warn("No fitness history recorded, return None")
+            return None
+        h = [f.cpu() for f in self.get_history()]
+        n_objs = 1 if h[0].ndim == 1 else h[0].shape[1]
+        if n_objs == 1:
+            return plot.plot_obj_space_1d(h, **kwargs)
+        if n_objs == 2:
+            return plot.plot_obj_space_2d(h, problem_pf, **kwargs)
+        if n_objs == 3:
+            return plot.plot_obj_space_3d(h, problem_pf, **kwargs)
+        warnings.warn("Not supported yet.")
+        return None
+
+    def flush(self):
+        if torch.cuda.is_available() and torch.cuda.is_initialized():
+            torch.cuda.synchronize()
+
+    def close(self):
+        self.flush()

@@ -1,0 +1,313 @@
+"""The standard single-/multi-GPU workflow.
+
+Parity: reference ``src/evox/workflows/std_workflow.py`` — one generation per
+``step`` with the hook order
+
+``pre_step → pre_ask → ask|init_ask → post_ask → sol_transforms → pre_eval →
+evaluate → ×opt_direction → post_eval → fit_transforms → pre_tell →
+tell|init_tell → post_tell → generation += 1 → post_step``
+
+(``std_workflow.py:129-199``); ``init_ask``/``init_tell`` are used at generation 0
+when the algorithm overrides them (``:203-213``).
+
+MI355X-first execution model (replaces ``jax.jit`` / ``pmap``):
+
+* ``graph=True`` captures one full generation (ask, evaluation, tell — every HIP
+  kernel and, in distributed mode, the RCCL collectives) into a **hipGraph** via
+  ``torch.cuda.CUDAGraph`` on a side stream and replays it, so a generation costs
+  one graph launch instead of dozens of host-side kernel launches.  The state
+  returned in graph mode aliases the workflow's static buffers (clone to keep a
+  snapshot).  Monitor hooks that consume the step's tensors are replayed on the
+  host after each graph launch with the graph's static output buffers, so
+  monitors need not be capture-safe.
+* ``enable_distributed(state)`` turns the workflow into an SPMD program with one
+  process per GPU (``torch.distributed``; backend ``nccl`` = RCCL over xGMI on
+  MI355X, ``gloo`` on CPU).  The algorithm state is replicated; every rank
+  evaluates a balanced slice of the population and the fitness slices are
+  all-gathered (reference ``std_workflow.py:311-345``, without its dropped
+  remainder rows).  Algorithms that implement the sharded protocol
+  (``ask_sharded``/``tell_sharded``, e.g. :class:`~evoxmi.algorithms.CMAES`)
+  generate only their own rows and all-reduce partial statistics instead.
+"""
+from __future__ import annotations
+
+import warnings
+from typing import Callable, List, Optional, Union
+
+import torch
+
+from ..core import Algorithm, Monitor, Problem, State, Workflow, use_state
+from ..core.algorithm import algorithm_has_init_ask
+from ..core.state import tree_flatten, tree_map
+from ..utils.common import parse_opt_direction
+
+HOOKS = ("pre_step", "pre_ask", "post_ask", "pre_eval", "post_eval", "pre_tell", "post_tell", "post_step")
+
+
+class StdWorkflow(Workflow):
+    def __init__(
+        self,
+        algorithm: Algorithm,
+        problem: Union[Problem, List[Problem]],
+        monitors: List[Monitor] = (),
+        opt_direction: Union[str, List[str]] = "min",
+        sol_transforms: List[Callable] = (),
+        fit_transforms: List[Callable] = (),
+        pop_transform: Optional[Callable] = None,
+        jit_problem: bool = True,
+        num_objectives: Optional[int] = None,
+        monitor=None,
+        graph: bool = False,
+        nan_policy: str = "keep",
+    ):
+        super().__init__()
+        self.algorithm = algorithm
+        self.problem = problem
+        self.monitors = list(monitors)
+        if monitor is not None:
+            warnings.warn("`monitor` is deprecated, use `monitors=[...]`", DeprecationWarning)
+            self.monitors = [monitor]
+        self.registered_hooks = {h: [] for h in HOOKS}
+        for m in self.monitors:
+            for h in m.hooks():
+                self.registered_hooks[h].append(m)
+        self.opt_direction = parse_opt_direction(opt_direction)
+        for m in self.monitors:
+            m.set_opt_direction(self.opt_direction)
+        self.sol_transforms = list(sol_transforms)
+        if pop_transform is not None:
+            warnings.warn("`pop_transform` is deprecated, use `sol_transforms`", DeprecationWarning)
+            self.sol_transforms = [pop_transform]
+        self.fit_transforms = list(fit_transforms)
+        self.jit_problem = jit_problem
+        self.num_objectives = num_objectives
+        if jit_problem is False and num_objectives is None:
+            warnings.warn("Using external problem but num_objectives isn't set, assuming to be 1.")
+            self.num_objectives = 1
+        assert nan_policy in ("keep", "inf"), "nan_policy must be 'keep' or 'inf'"
+        self.nan_policy = nan_policy
+        self.graph = graph
+        self._has_init_ask = algorithm_has_init_ask(algorithm)
+        # distributed context
+        self.distributed_step = False
+        self._dist = None
+        # graph-mode bookkeeping
+        self._graph = None
+        self._static = None
+        self._static_out = None
+        self._hook_args = None
+
+    # ------------------------------------------------------------------ state
+    def setup(self, key):
+        return State(generation=0)
+
+    # ------------------------------------------------------------------ core
+    def _opt_dir(self, fitness):
+        od = self.opt_direction
+        if isinstance(od, torch.Tensor):
+            od = od.to(fitness.device)
+            return fitness * od
+        return fitness if od == 1 else fitness * od
+
+    def _evaluate(self, state, transformed):
+        if self.jit_problem:
+            return use_state(self.problem.evaluate)(state, transformed)
+        fitness, state = use_state(self.problem.evaluate)(state, transformed)
+        if not isinstance(fitness, torch.Tensor):
+            fitness = torch.as_tensor(fitness)
+        return fitness.to(torch.float32), state
+
+    def _proto_step(self, is_init: bool, state: State, record=None):
+        for m in self.registered_hooks["pre_ask"]:
+            m.pre_ask(state)
+        alg = self.algorithm
+        sharded = self.distributed_step and self._dist.algorithm_sharded
+        if is_init:
+            ask, tell = alg.init_ask, alg.init_tell
+        else:
+            ask, tell = alg.ask, alg.tell
+        if sharded:
+            d = self._dist
+            ask_s = alg.init_ask_sharded if is_init else alg.ask_sharded
+            cand_sol, state = use_state(ask_s)(state, d)
+        else:
+            cand_sol, state = use_state(ask)(state)
+        for m in self.registered_hooks["post_ask"]:
+            m.post_ask(state, cand_sol)
+
+        if self.distributed_step and not sharded:
+            start, size = self._dist.slice_of(cand_sol.shape[0])
+            local = cand_sol[start : start + size]
+        else:
+            local = cand_sol
+
+        transformed = local
+        for t in self.sol_transforms:
+            transformed = t(transformed)
+        for m in self.registered_hooks["pre_eval"]:
+            m.pre_eval(state, local, transformed)
+
+        fitness, state = self._evaluate(state, transformed)
+        if self.nan_policy == "inf":
+            fitness = torch.nan_to_num(fitness, nan=float("inf"))
+
+        if self.distributed_step:
+            fitness = self._dist.all_gather_rows(fitness, cand_sol.shape[0] if not sharded else self._dist.global_pop)
+
+        fitness = self._opt_dir(fitness)
+        for m in self.registered_hooks["post_eval"]:
+            m.post_eval(state, local, transformed, fitness)
+        tfit = fitness
+        for t in self.fit_transforms:
+            tfit = t(tfit)
+        for m in self.registered_hooks["pre_tell"]:
+            m.pre_tell(state, local, transformed, fitness, tfit)
+        if sharded:
+            tell_s = alg.init_tell_sharded if is_init else alg.tell_sharded
+            state = use_state(tell_s)(state, tfit, self._dist)
+        else:
+            state = use_state(tell)(state, tfit)
+        for m in self.registered_hooks["post_tell"]:
+            m.post_tell(state)
+        if record is not None:
+            record.update(cand_sol=local, transformed=transformed, fitness=fitness, tfit=tfit)
+        return state.update(generation=state.generation + 1)
+
+    def _step_eager(self, state):
+        is_init = self._has_init_ask and state.generation == 0
+        return self._proto_step(bool(is_init), state)
+
+    # ------------------------------------------------------------------ hipGraph path
+    def _hooks_inside_step(self):
+        return any(self.registered_hooks[h] for h in HOOKS[1:-1])
+
+    def _capture(self, state):
+        """Capture one (non-init) generation into a hipGraph."""
+        dev = None
+        for x in tree_flatten(state)[0]:
+            if isinstance(x, torch.Tensor) and x.is_cuda:
+                dev = x.device
+                break
+        if dev is None:
+            raise RuntimeError("graph=True requires the state to live on a GPU")
+        static = tree_map(lambda x: x.clone() if isinstance(x, torch.Tensor) else x, state)
+        # warm-up on a side stream (allocator / lazy init), as required for capture
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        saved_hooks = self.registered_hooks
+        self.registered_hooks = {h: [] for h in HOOKS}
+        try:
+            with torch.cuda.stream(s):
+                self._proto_step(False, tree_map(lambda x: x.clone() if isinstance(x, torch.Tensor) else x, static))
+            torch.cuda.current_stream(dev).wait_stream(s)
+            torch.cuda.synchronize(dev)
+            g = torch.cuda.CUDAGraph()
+            record = {}
+            with torch.cuda.graph(g, stream=s):
+                out = self._proto_step(False, static, record=record)
+                in_leaves, in_spec = tree_flatten(static)
+                out_leaves, out_spec = tree_flatten(out)
+                if in_spec != out_spec:
+                    raise RuntimeError("graph=True: the step changed the state structure; this algorithm is not graph-safe")
+                for a, b in zip(in_leaves, out_leaves):
+                    if isinstance(a, torch.Tensor):
+                        if a.shape != b.shape or a.dtype != b.dtype:
+                            raise RuntimeError("graph=True: a state tensor changed shape/dtype across a step")
+                        if a.data_ptr() != b.data_ptr():
+                            a.copy_(b)
+        finally:
+            self.registered_hooks = saved_hooks
+        # python (non-tensor) leaves must be step-invariant, except the generation counter
+        py_changed = [
+            (a, b)
+            for a, b in zip(in_leaves, out_leaves)
+            if not isinstance(a, torch.Tensor) and a != b
+        ]
+        if len(py_changed) > 1:
+            raise RuntimeError(f"graph=True: host-side state fields change every step {py_changed}; not graph-safe")
+        self._graph = g
+        self._static = static
+        self._hook_args = record
+        return static
+
+    def _step_graph(self, state):
+        if self._graph is None:
+            static = self._capture(state)
+        else:
+            static = self._static
+            if state is not static and state is not self._static_out:
+                # a foreign state (e.g. restored checkpoint): load it into the static buffers
+                for a, b in zip(tree_flatten(static)[0], tree_flatten(state)[0]):
+                    if isinstance(a, torch.Tensor):
+                        a.copy_(b)
+        self._graph.replay()
+        gen = state.generation + 1
+        out = static.update(generation=gen)
+        self._static = out
+        self._static_out = out
+        # post-hoc monitor hooks on the graph's static buffers
+        r = self._hook_args
+        for m in self.registered_hooks["post_ask"]:
+            m.post_ask(out, r["cand_sol"])
+        for m in self.registered_hooks["pre_eval"]:
+            m.pre_eval(out, r["cand_sol"], r["transformed"])
+        for m in self.registered_hooks["post_eval"]:
+            m.post_eval(out, r["cand_sol"], r["transformed"], r["fitness"])
+        for m in self.registered_hooks["pre_tell"]:
+            m.pre_tell(out, r["cand_sol"], r["transformed"], r["fitness"], r["tfit"])
+        for m in self.registered_hooks["post_tell"]:
+            m.post_tell(out)
+        return out
+
+    # ------------------------------------------------------------------ public
+    def step(self, state: State) -> State:
+        for m in self.registered_hooks["pre_step"]:
+            m.pre_step(state)
+        if self.graph and not (self._has_init_ask and state.generation == 0):
+            state = self._step_graph(state)
+        else:
+            state = self._step_eager(state)
+        for m in self.registered_hooks["post_step"]:
+            m.post_step(state)
+        return state
+
+    def valid(self, state: State, metric: str = "loss"):
+        """Evaluate the current proposal in the problem's validation mode (``std_workflow.py:218-234``)."""
+        new_state = use_state(self.problem.valid)(state, metric=metric)
+        pop, new_state = use_state(self.algorithm.ask)(new_state)
+        if self.distributed_step and not self._dist.algorithm_sharded:
+            start, size = self._dist.slice_of(pop.shape[0])
+            pop = pop[start : start + size]
+        for t in self.sol_transforms:
+            pop = t(pop)
+        fitness, _ = use_state(self.problem.evaluate)(new_state, pop)
+        if self.distributed_step:
+            fitness = self._dist.all_gather_rows(fitness, None)
+        return fitness, state
+
+    def enable_distributed(self, state: State, group=None) -> State:
+        """Population-shard this workflow across the ranks of ``torch.distributed``.
+
+        Every rank must call this with an identical state (same key ⇒ identical
+        replicas).  The state is broadcast from rank 0 to make that explicit.
+        """
+        from ..parallel.context import DistContext
+
+        self._dist = DistContext(group=group, algorithm=self.algorithm)
+        self.distributed_step = True
+        state = self._dist.broadcast_state(state)
+        if self._dist.algorithm_sharded:
+            pop_size = getattr(self.algorithm, "pop_size")
+            self._dist.set_global_pop(pop_size)
+        return state
+
+    def enable_multi_devices(self, state: State, devices=None) -> State:
+        """Reference ``std_workflow.py:272-309`` shards along the decision axis with
+        GSPMD.  With one process per GPU that role is played by
+        :class:`evoxmi.parallel.DimShardedProblem`; here we keep the call for API
+        parity and fall back to population sharding when a process group exists."""
+        if not self.jit_problem:
+            raise ValueError("multi-devices with non jit problem isn't currently supported")
+        if torch.distributed.is_available() and torch.distributed.is_initialized():
+            return self.enable_distributed(state)
+        return state
