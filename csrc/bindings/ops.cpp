@@ -6,7 +6,7 @@
 #include <torch/library.h>
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
+#include <c10/core/DeviceGuard.h>
 #include <hip/hip_runtime.h>
 
 #include "evoxmi_launchers.h"
@@ -27,7 +27,7 @@ void check_key(const at::Tensor& key) {
 at::Tensor philox_fill(const at::Tensor& key, int64_t n, int64_t dist, int64_t offset) {
   check_key(key);
   TORCH_CHECK(offset % 4 == 0, "offset must be a multiple of 4");
-  c10::hip::HIPGuard g(key.device());
+  c10::DeviceGuard g(key.device());
   auto out = at::empty({n}, key.options().dtype(at::kFloat));
   if (n > 0) evx_philox_fill(out.data_ptr<float>(), n, key.data_ptr<int64_t>(), (int)dist, offset, cur_stream());
   return out;
@@ -36,7 +36,7 @@ at::Tensor philox_fill(const at::Tensor& key, int64_t n, int64_t dist, int64_t o
 at::Tensor classic_eval(const at::Tensor& X, int64_t func, double a, double b, double c) {
   CHECK_DEV(X); CHECK_F32(X); CHECK_CONTIG(X);
   TORCH_CHECK(X.dim() == 2, "X must be (N, d)");
-  c10::hip::HIPGuard g(X.device());
+  c10::DeviceGuard g(X.device());
   auto out = at::empty({X.size(0)}, X.options());
   if (X.size(0) > 0)
     evx_classic_eval(X.data_ptr<float>(), out.data_ptr<float>(), (int)X.size(0), (int)X.size(1), (int)func, (float)a, (float)b,
@@ -53,7 +53,7 @@ std::vector<at::Tensor> pso_update(const at::Tensor& pop, const at::Tensor& vel,
   const int64_t N = pop.size(0), D = pop.size(1);
   TORCH_CHECK(vel.sizes() == pop.sizes() && lbl.sizes() == pop.sizes(), "shape mismatch");
   TORCH_CHECK(lbf.numel() == N && fit.numel() == N && gbl.numel() == D && lb.numel() == D && ub.numel() == D, "shape mismatch");
-  c10::hip::HIPGuard g(pop.device());
+  c10::DeviceGuard g(pop.device());
   auto opop = at::empty_like(pop), ovel = at::empty_like(pop), olbl = at::empty_like(pop), olbf = at::empty_like(lbf);
   evx_pso_update(pop.data_ptr<float>(), vel.data_ptr<float>(), lbl.data_ptr<float>(), lbf.data_ptr<float>(),
                  fit.data_ptr<float>(), gbl.data_ptr<float>(), kp.data_ptr<int64_t>(), kg.data_ptr<int64_t>(), (float)w,
@@ -62,16 +62,128 @@ std::vector<at::Tensor> pso_update(const at::Tensor& pop, const at::Tensor& vel,
   return {opop, ovel, olbl, olbf};
 }
 
+const float* optf(const c10::optional<at::Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t);
+  return t->data_ptr<float>();
+}
+
+EvxOperand make_operand(const at::Tensor& X, int64_t rc, const c10::optional<at::Tensor>& gather,
+                        const c10::optional<at::Tensor>& sub, int64_t sub_on_k, const c10::optional<at::Tensor>& kscale,
+                        const c10::optional<at::Tensor>& kw, const c10::optional<at::Tensor>& sscale, int64_t sscale_inv) {
+  CHECK_DEV(X); CHECK_F32(X);
+  TORCH_CHECK(X.dim() == 2 && X.stride(1) == 1, "operand must be 2-D with unit inner stride");
+  EvxOperand o{};
+  o.ptr = X.data_ptr<float>();
+  o.ld = X.stride(0);
+  o.rc = (int)rc;
+  o.gather = nullptr;
+  if (gather.has_value() && gather->defined()) {
+    CHECK_DEV(*gather);
+    TORCH_CHECK(gather->scalar_type() == at::kInt && gather->is_contiguous(), "gather must be int32");
+    TORCH_CHECK(rc, "gather only supported for row-contiguous operands");
+    o.gather = gather->data_ptr<int32_t>();
+  }
+  o.sub = optf(sub);
+  o.sub_on_k = (int)sub_on_k;
+  o.kscale = optf(kscale);
+  o.kw = optf(kw);
+  o.sscale = optf(sscale);
+  o.sscale_inv = (int)sscale_inv;
+  return o;
+}
+
+at::Tensor gemm_f32(const at::Tensor& A, int64_t a_rc, const c10::optional<at::Tensor>& a_gather,
+                    const c10::optional<at::Tensor>& a_sub, int64_t a_sub_on_k, const c10::optional<at::Tensor>& a_kscale,
+                    const c10::optional<at::Tensor>& a_kw, const c10::optional<at::Tensor>& a_sscale, int64_t a_sscale_inv,
+                    const at::Tensor& B, int64_t b_rc, const c10::optional<at::Tensor>& b_gather,
+                    const c10::optional<at::Tensor>& b_sub, int64_t b_sub_on_k, const c10::optional<at::Tensor>& b_kscale,
+                    const c10::optional<at::Tensor>& b_kw, const c10::optional<at::Tensor>& b_sscale, int64_t b_sscale_inv,
+                    const c10::optional<at::Tensor>& alpha_ptr, const c10::optional<at::Tensor>& bias_n, double beta,
+                    const c10::optional<at::Tensor>& Cin, int64_t M, int64_t N, int64_t K, int64_t splits, double alpha) {
+  auto ao = make_operand(A, a_rc, a_gather, a_sub, a_sub_on_k, a_kscale, a_kw, a_sscale, a_sscale_inv);
+  auto bo = make_operand(B, b_rc, b_gather, b_sub, b_sub_on_k, b_kscale, b_kw, b_sscale, b_sscale_inv);
+  // shape checks: KC operand is (rows, K); RC operand is (K or gather source, rows)
+  if (!a_rc) { TORCH_CHECK(A.size(0) >= M && A.size(1) >= K, "A shape"); } else { TORCH_CHECK(A.size(1) >= M, "A shape"); }
+  if (!b_rc) { TORCH_CHECK(B.size(0) >= N && B.size(1) >= K, "B shape"); } else { TORCH_CHECK(B.size(1) >= N, "B shape"); }
+  if (a_rc && !ao.gather) TORCH_CHECK(A.size(0) >= K, "A shape");
+  if (b_rc && !bo.gather) TORCH_CHECK(B.size(0) >= K, "B shape");
+  if (a_gather.has_value() && a_gather->defined()) TORCH_CHECK(a_gather->numel() >= K, "gather length");
+  if (b_gather.has_value() && b_gather->defined()) TORCH_CHECK(b_gather->numel() >= K, "gather length");
+  c10::DeviceGuard g(A.device());
+  const int sp = evx_gemm_splits_used((int)K, (int)splits);
+  at::Tensor C = sp > 1 ? at::empty({sp, M, N}, A.options()) : at::empty({M, N}, A.options());
+  const float* cin = nullptr;
+  int64_t ldcin = N;
+  if (Cin.has_value() && Cin->defined()) {
+    TORCH_CHECK(sp == 1, "Cin incompatible with split-K");
+    CHECK_DEV(*Cin); CHECK_F32(*Cin);
+    TORCH_CHECK(Cin->dim() == 2 && Cin->stride(1) == 1 && Cin->size(0) >= M && Cin->size(1) >= N, "Cin shape");
+    cin = Cin->data_ptr<float>();
+    ldcin = Cin->stride(0);
+  }
+  if (M > 0 && N > 0)
+    evx_gemm_f32(ao, bo, C.data_ptr<float>(), N, (int)M, (int)N, (int)K, (int)splits, (float)alpha, optf(alpha_ptr),
+                 optf(bias_n), (float)beta, cin, ldcin, cur_stream());
+  return C;
+}
+
+std::vector<at::Tensor> argsort_f32(const at::Tensor& keys, int64_t descending) {
+  CHECK_DEV(keys); CHECK_F32(keys); CHECK_CONTIG(keys);
+  const int64_t n = keys.numel();
+  TORCH_CHECK(n <= evx_argsort_max_n(), "argsort_f32: n > ", evx_argsort_max_n());
+  c10::DeviceGuard g(keys.device());
+  auto ok = at::empty({n}, keys.options());
+  auto oi = at::empty({n}, keys.options().dtype(at::kInt));
+  if (n > 0) evx_argsort(keys.data_ptr<float>(), (int)n, (int)descending, ok.data_ptr<float>(), oi.data_ptr<int32_t>(), cur_stream());
+  return {ok, oi};
+}
+
+at::Tensor cec_basic(const at::Tensor& Z, int64_t fid, const c10::optional<at::Tensor>& perm, int64_t start, int64_t L,
+                     const c10::optional<at::Tensor>& sub, double scale, const c10::optional<at::Tensor>& Y, int64_t ystart,
+                     int64_t yperm) {
+  CHECK_DEV(Z); CHECK_F32(Z);
+  TORCH_CHECK(Z.dim() == 2 && Z.stride(1) == 1, "Z must be 2-D row-major");
+  const int32_t* pp = nullptr;
+  if (perm.has_value() && perm->defined()) {
+    TORCH_CHECK(perm->scalar_type() == at::kInt && perm->is_contiguous() && perm->numel() >= start + L, "perm");
+    pp = perm->data_ptr<int32_t>();
+  } else {
+    TORCH_CHECK(start + L <= Z.size(1), "segment out of range");
+  }
+  TORCH_CHECK(!yperm || pp, "yperm needs perm");
+  const float* yp = nullptr;
+  int64_t ldy = 0;
+  if (Y.has_value() && Y->defined()) {
+    CHECK_DEV(*Y); CHECK_F32(*Y);
+    TORCH_CHECK(Y->dim() == 2 && Y->stride(1) == 1 && Y->size(0) == Z.size(0) && Y->size(1) >= ystart + L, "Y shape");
+    yp = Y->data_ptr<float>();
+    ldy = Y->stride(0);
+  }
+  c10::DeviceGuard g(Z.device());
+  auto out = at::empty({Z.size(0)}, Z.options());
+  if (Z.size(0) > 0)
+    evx_cec_basic(Z.data_ptr<float>(), Z.stride(0), (int)Z.size(0), (int)fid, pp, (int)start, (int)L, optf(sub), (float)scale,
+                  yp, ldy, (int)ystart, (int)yperm, out.data_ptr<float>(), cur_stream());
+  return out;
+}
+
 }  // namespace
 
 TORCH_LIBRARY(evoxmi, m) {
   m.def("philox_fill(Tensor key, int n, int dist, int offset) -> Tensor");
+  m.def("argsort_f32(Tensor keys, int descending) -> Tensor[]");
+  m.def("cec_basic(Tensor Z, int fid, Tensor? perm, int start, int L, Tensor? sub, float scale, Tensor? Y, int ystart, int yperm) -> Tensor");
   m.def("classic_eval(Tensor X, int func, float a, float b, float c) -> Tensor");
+  m.def("gemm_f32(Tensor A, int a_rc, Tensor? a_gather, Tensor? a_sub, int a_sub_on_k, Tensor? a_kscale, Tensor? a_kw, Tensor? a_sscale, int a_sscale_inv, Tensor B, int b_rc, Tensor? b_gather, Tensor? b_sub, int b_sub_on_k, Tensor? b_kscale, Tensor? b_kw, Tensor? b_sscale, int b_sscale_inv, Tensor? alpha_ptr, Tensor? bias_n, float beta, Tensor? Cin, int M, int N, int K, int splits, float alpha) -> Tensor");
   m.def("pso_update(Tensor pop, Tensor vel, Tensor lbl, Tensor lbf, Tensor fit, Tensor gbl, Tensor kp, Tensor kg, float w, float phip, float phig, Tensor lb, Tensor ub) -> Tensor[]");
 }
 
 TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
   m.impl("philox_fill", &philox_fill);
   m.impl("classic_eval", &classic_eval);
+  m.impl("cec_basic", &cec_basic);
+  m.impl("argsort_f32", &argsort_f32);
+  m.impl("gemm_f32", &gemm_f32);
   m.impl("pso_update", &pso_update);
 }

@@ -9,3 +9,23 @@ void evx_pso_update(const float* pop, const float* vel, const float* lbl, const 
                     const float* gbl, const int64_t* kp, const int64_t* kg, float w, float phip, float phig,
                     const float* lb, const float* ub, float* opop, float* ovel, float* olbl, float* olbf, int N, int D,
                     hipStream_t s);
+
+struct EvxOperand {
+  const float* ptr;
+  int64_t ld;
+  int rc;
+  const int32_t* gather;
+  const float* sub;
+  int sub_on_k;
+  const float* kscale;
+  const float* kw;
+  const float* sscale;
+  int sscale_inv;
+};
+void evx_gemm_f32(EvxOperand a, EvxOperand b, float* C, int64_t ldc, int M, int N, int K, int splits, float alpha,
+                  const float* alpha_ptr, const float* bias_n, float beta, const float* Cin, int64_t ldcin, hipStream_t s);
+int evx_gemm_splits_used(int K, int splits);
+int evx_argsort_max_n();
+void evx_argsort(const float* keys, int n, int descending, float* out_keys, int32_t* out_idx, hipStream_t s);
+void evx_cec_basic(const float* Z, int64_t ld, int N, int fid, const int32_t* perm, int start, int L, const float* sub,
+                   float scale, const float* Y, int64_t ldy, int ystart, int yperm, float* out, hipStream_t s);

@@ -1,0 +1,172 @@
+// CEC2022 basic functions as one wave64-per-row reduction kernel (K6 epilogue stage).
+//
+// z_eff(j) = (Z[row, idx(j)] − sub[idx(j)]) · scale,   idx(j) = perm ? perm[start + j] : start + j
+// for j in [0, L).  Functions that need neighbours (Rosenbrock, Levy, expanded
+// Griewank-Rosenbrock, expanded Schaffer, Schaffer F7) re-read z_eff(j ± 1) — the row
+// is L1/L2 resident, so each element is fetched from HBM once.  The f < 1e-8 clamp and
+// composition weights are applied by the caller.  Function ids match
+// evoxmi/problems/numerical/cec2022.py.
+#include "evoxmi_common.h"
+
+namespace {
+
+constexpr float PI_F = 3.14159265358979323846f;
+
+enum { ZAKHAROV = 0, ROSENBROCK, SCHAFFERF7, RASTRIGIN, LEVY, BENTCIGAR, HGBAT, KATSUURA, ACKLEY, SCHWEFEL, HAPPYCAT,
+       ELLIPTIC, DISCUS, EXPSCHAFFER, EXPGRIEROSEN, GRIEWANK, SPHERE };
+
+struct RowView {
+  const float* z;
+  const int32_t* perm;
+  const float* sub;
+  int start;
+  float scale;
+  __device__ __forceinline__ float operator()(int j) const {
+    int i = perm ? perm[start + j] : start + j;
+    float v = z[i];
+    if (sub) v -= sub[i];
+    return v * scale;
+  }
+};
+
+__global__ void __launch_bounds__(256) cec_basic_kernel(const float* __restrict__ Z, int64_t ld, int N, int fid,
+                                                        const int32_t* __restrict__ perm, int start, int L,
+                                                        const float* __restrict__ sub, float scale,
+                                                        const float* __restrict__ Y, int64_t ldy, int ystart, int yperm,
+                                                        float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= N) return;
+  RowView z{Z + (int64_t)row * ld, perm, sub, start, scale};
+  float a = 0.f, b = 0.f, p = 1.f;
+  const float fL = (float)L;
+  switch (fid) {
+    case ZAKHAROV:
+      for (int j = lane; j < L; j += 64) { float v = z(j); a += v * v; b += 0.5f * (float)(j + 1) * v; }
+      break;
+    case ROSENBROCK:
+      for (int j = lane; j < L - 1; j += 64) {
+        float v = z(j) + 1.f, w = z(j + 1) + 1.f;
+        float t = v * v - w, u = 1.f - v;
+        a += 100.f * t * t + u * u;
+      }
+      break;
+    case SCHAFFERF7:
+      for (int j = lane; j < L - 1; j += 64) {
+        float y0, y1;
+        if (Y) { const float* yr = Y + (int64_t)row * ldy + ystart; y0 = yr[j]; y1 = yr[j + 1]; }
+        else if (yperm) { const float* zr = Z + (int64_t)row * ld; y0 = zr[perm[j]]; y1 = zr[perm[j + 1]]; }
+        else { y0 = z(j); y1 = z(j + 1); }
+        float s = sqrtf(y0 * y0 + y1 * y1);
+        float t = sinf(50.f * powf(s, 0.2f));
+        float r = sqrtf(s);
+        a += r + r * t * t;
+      }
+      break;
+    case RASTRIGIN:
+      for (int j = lane; j < L; j += 64) { float v = z(j) * 0.0512f; a += v * v - 10.f * cosf(2.f * PI_F * v) + 10.f; }
+      break;
+    case LEVY:
+      for (int j = lane; j < L; j += 64) {
+        float w = 1.f + z(j) * 0.25f;
+        if (j == 0) { float s0 = sinf(PI_F * w); a += s0 * s0; }
+        if (j < L - 1) { float s = sinf(PI_F * w + 1.f); a += (w - 1.f) * (w - 1.f) * (1.f + 10.f * s * s); }
+        else { float s = sinf(2.f * PI_F * w); a += (w - 1.f) * (w - 1.f) * (1.f + s * s); }
+      }
+      break;
+    case BENTCIGAR:
+      for (int j = lane; j < L; j += 64) { float v = z(j); a += (j == 0 ? 1.f : 1e6f) * v * v; }
+      break;
+    case HGBAT:
+    case HAPPYCAT:
+      for (int j = lane; j < L; j += 64) { float v = z(j) * 0.05f - 1.f; a += v * v; b += v; }
+      break;
+    case KATSUURA: {
+      const float ex = 10.f / powf(fL, 1.2f);
+      for (int j = lane; j < L; j += 64) {
+        float v = z(j) * 0.05f, temp = 0.f, t1 = 1.f;
+        for (int k = 1; k <= 32; ++k) {
+          t1 *= 2.f;
+          float t2 = t1 * v;
+          temp += fabsf(t2 - floorf(t2 + 0.5f)) / t1;
+        }
+        p *= powf(1.f + (float)(j + 1) * temp, ex);
+      }
+      break;
+    }
+    case ACKLEY:
+      for (int j = lane; j < L; j += 64) { float v = z(j); a += v * v; b += cosf(2.f * PI_F * v); }
+      break;
+    case SCHWEFEL:
+      for (int j = lane; j < L; j += 64) {
+        float v = z(j) * 10.f + 4.209687462275036e2f;
+        if (v > 500.f) {
+          float m = 500.f - fmodf(v, 500.f);
+          float t = (v - 500.f) / 100.f;
+          a += -m * sinf(sqrtf(m)) + t * t / fL;
+        } else if (v < -500.f) {
+          float m = fmodf(fabsf(v), 500.f);
+          float t = (v + 500.f) / 100.f;
+          a += -(-500.f + m) * sinf(sqrtf(500.f - m)) + t * t / fL;
+        } else {
+          a += -v * sinf(sqrtf(fabsf(v)));
+        }
+      }
+      break;
+    case ELLIPTIC:
+      for (int j = lane; j < L; j += 64) { float v = z(j); a += powf(10.f, 6.f * (float)j / (fL - 1.f)) * v * v; }
+      break;
+    case DISCUS:
+      for (int j = lane; j < L; j += 64) { float v = z(j); a += (j == 0 ? 1e6f : 1.f) * v * v; }
+      break;
+    case EXPSCHAFFER:
+      for (int j = lane; j < L; j += 64) {
+        float v = z(j), u = z(j == 0 ? L - 1 : j - 1);
+        float sq = v * v + u * u;
+        float s = sinf(sqrtf(sq));
+        float d = 1.f + 0.001f * sq;
+        a += 0.5f + (s * s - 0.5f) / (d * d);
+      }
+      break;
+    case EXPGRIEROSEN:
+      for (int j = lane; j < L; j += 64) {
+        float v = z(j) * 0.05f + 1.f, w = z(j == L - 1 ? 0 : j + 1) * 0.05f + 1.f;
+        float t1 = v * v - w, t2 = v - 1.f;
+        float temp = 100.f * t1 * t1 + t2 * t2;
+        a += temp * temp / 4000.f - cosf(temp) + 1.f;
+      }
+      break;
+    case GRIEWANK:
+      for (int j = lane; j < L; j += 64) { float v = z(j); a += v * v; p *= cosf(v / sqrtf((float)(j + 1))); }
+      break;
+    default:  // SPHERE
+      for (int j = lane; j < L; j += 64) { float v = z(j); a += v * v; }
+      break;
+  }
+  a = evx::wave_sum(a);
+  b = evx::wave_sum(b);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) p *= __shfl_xor(p, o, 64);
+  if (lane != 0) return;
+  float f;
+  switch (fid) {
+    case ZAKHAROV: f = a + b * b + b * b * b * b; break;
+    case SCHAFFERF7: f = a * a / (fL - 1.f) / (fL - 1.f); break;
+    case HGBAT: f = sqrtf(fabsf(a * a - b * b)) + (0.5f * a + b) / fL + 0.5f; break;
+    case HAPPYCAT: f = powf(fabsf(a - fL), 0.25f) + (0.5f * a + b) / fL + 0.5f; break;
+    case KATSUURA: { float c = 10.f / fL / fL; f = p * c - c; break; }
+    case ACKLEY: f = -20.f * expf(-0.2f * sqrtf(a / fL)) - expf(b / fL) + 20.f + 2.718281828459045f; break;
+    case SCHWEFEL: f = a + 4.189828872724338e2f * fL; break;
+    case GRIEWANK: f = a / 4000.f - p + 1.f; break;
+    default: f = a; break;
+  }
+  out[row] = f;
+}
+
+}  // namespace
+
+void evx_cec_basic(const float* Z, int64_t ld, int N, int fid, const int32_t* perm, int start, int L, const float* sub,
+                   float scale, const float* Y, int64_t ldy, int ystart, int yperm, float* out, hipStream_t s) {
+  dim3 grid((N + 3) / 4);
+  cec_basic_kernel<<<grid, 256, 0, s>>>(Z, ld, N, fid, perm, start, L, sub, scale, Y, ldy, ystart, yperm, out);
+}

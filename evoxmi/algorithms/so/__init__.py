@@ -1,1 +1,2 @@
 from .pso_variants import *  # noqa
+from .es_variants import *  # noqa

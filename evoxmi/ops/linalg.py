@@ -1,0 +1,109 @@
+"""Dense linear algebra on the matrix cores.
+
+``gemm`` is the framework's one general f32 GEMM (``csrc/kernels/gemm_f32.hip``,
+``v_mfma_f32_32x32x2_f32``) with fused operand prologues and a fused epilogue:
+
+    C = alpha·(*alpha_ptr)·Ã B̃ + bias_n[None, :] + beta·Cin
+    Ã[m, k] = (A[m, k] − sub[m|k]) · kscale[k] · kw[k] · sscale
+
+Operands are described by :class:`Operand`; ``rc=False`` means the tensor is
+(rows, K) with K contiguous, ``rc=True`` means (K, rows) with rows contiguous
+(optionally with K-row indirection ``gather``).  ``splits>1`` returns the
+``(splits, M, N)`` split-K partial slabs (deterministic, no atomics).
+
+The CPU branch materialises Ã and B̃ with torch and is the numerics oracle of
+the GPU tests.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from . import _ext
+
+
+@dataclass
+class Operand:
+    t: torch.Tensor
+    rc: bool = False
+    gather: Optional[torch.Tensor] = None
+    sub: Optional[torch.Tensor] = None
+    sub_on_k: bool = False
+    kscale: Optional[torch.Tensor] = None
+    kw: Optional[torch.Tensor] = None
+    sscale: Optional[torch.Tensor] = None
+    sscale_inv: bool = False
+
+    def materialise(self, rows: int, K: int) -> torch.Tensor:
+        """Ã as a dense (rows, K) tensor (CPU reference)."""
+        t = self.t
+        if self.rc:
+            src = t.index_select(0, self.gather.long()) if self.gather is not None else t[:K]
+            X = src[:K, :rows].T
+        else:
+            X = t[:rows, :K]
+        X = X.to(torch.float32)
+        if self.sub is not None:
+            X = X - (self.sub[:K][None, :] if self.sub_on_k else self.sub[:rows][:, None])
+        if self.kscale is not None:
+            X = X * self.kscale[:K][None, :]
+        if self.kw is not None:
+            X = X * self.kw[:K][None, :]
+        if self.sscale is not None:
+            s = self.sscale.reshape(())
+            X = X / s if self.sscale_inv else X * s
+        return X
+
+
+def _c(x):
+    return None if x is None else x.contiguous()
+
+
+def gemm(a: Operand, b: Operand, M: int, N: int, K: int, alpha: float = 1.0, alpha_ptr=None, bias_n=None, beta: float = 0.0,
+         Cin=None, splits: int = 1) -> torch.Tensor:
+    if a.t.is_cuda:
+        g = None if a.gather is None else a.gather.to(torch.int32).contiguous()
+        gb = None if b.gather is None else b.gather.to(torch.int32).contiguous()
+        return _ext.ops().gemm_f32(
+            a.t, int(a.rc), g, _c(a.sub), int(a.sub_on_k), _c(a.kscale), _c(a.kw), _c(a.sscale), int(a.sscale_inv),
+            b.t, int(b.rc), gb, _c(b.sub), int(b.sub_on_k), _c(b.kscale), _c(b.kw), _c(b.sscale), int(b.sscale_inv),
+            _c(alpha_ptr), _c(bias_n), float(beta), Cin, int(M), int(N), int(K), int(splits), float(alpha),
+        )
+    A = a.materialise(M, K)
+    B = b.materialise(N, K)
+    s = alpha * (alpha_ptr.reshape(()) if alpha_ptr is not None else 1.0)
+    if splits > 1:
+        # same slab semantics as the kernel: slice z covers K range [z*kps, (z+1)*kps)
+        kps = -(-K // splits)
+        kps = -(-kps // 16) * 16
+        sl = []
+        for z in range(-(-K // kps)):
+            k0, k1 = z * kps, min(K, (z + 1) * kps)
+            sl.append(s * (A[:, k0:k1] @ B[:, k0:k1].T))
+        out = torch.stack(sl)
+        if bias_n is not None:
+            out = out + bias_n[None, None, :N]
+        return out
+    C = s * (A @ B.T)
+    if bias_n is not None:
+        C = C + bias_n[None, :N]
+    if Cin is not None:
+        C = C + beta * Cin[:M, :N]
+    return C
+
+
+def matmul_nt(A: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
+    """A @ B.T on the matrix cores (A: (M, K), B: (N, K))."""
+    return gemm(Operand(A), Operand(B), A.shape[0], B.shape[0], A.shape[1])
+
+
+def matmul(A: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
+    """A @ B (A: (M, K) K-contiguous; B: (K, N) N-contiguous)."""
+    return gemm(Operand(A), Operand(B, rc=True), A.shape[0], B.shape[1], A.shape[1])
+
+
+def matmul_tn(A: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
+    """A.T @ B (A: (K, M), B: (K, N), both row-major)."""
+    return gemm(Operand(A, rc=True), Operand(B, rc=True), A.shape[1], B.shape[1], A.shape[0])

@@ -131,6 +131,8 @@ def _ext():
 
 def uniform(key, shape=(), dtype=torch.float32, minval=0.0, maxval=1.0, offset: int = 0) -> torch.Tensor:
     """U(minval, maxval) samples (reference ``jax.random.uniform``)."""
+    if offset & 3:
+        return _aligned(lambda k, s, dtype, offset: uniform(k, s, dtype, 0.0, 1.0, offset), key, shape, dtype, offset) * (maxval - minval) + minval
     shape = _as_shape(shape)
     if key.is_cuda and _numel(shape) >= 4096:
         u = _ext().philox_fill(key, _numel(shape), 0, offset).reshape(shape)
@@ -142,12 +144,23 @@ def uniform(key, shape=(), dtype=torch.float32, minval=0.0, maxval=1.0, offset: 
     return u
 
 
+def _aligned(fn, key, shape, dtype, offset):
+    """Support element offsets that are not a multiple of 4 (shard starts)."""
+    shape = _as_shape(shape)
+    lead = offset & 3
+    n = _numel(shape)
+    flat = fn(key, (n + lead,), dtype=dtype, offset=offset - lead)
+    return flat[lead:].reshape(shape)
+
+
 def normal(key, shape=(), dtype=torch.float32, offset: int = 0) -> torch.Tensor:
     """Standard normal samples via Box–Muller on word pairs (0,1) and (2,3).
 
     Element ``4b + j`` uses block ``b``: ``r = sqrt(-2 ln u_{2p})``, ``θ = 2π u_{2p+1}``
     with ``p = j // 2``; ``j`` even takes ``r cos θ``, odd ``r sin θ``.
     """
+    if offset & 3:
+        return _aligned(normal, key, shape, dtype, offset)
     shape = _as_shape(shape)
     n = _numel(shape)
     if key.is_cuda and n >= 4096:
@@ -203,7 +216,7 @@ def permutation(key, x: Union[int, torch.Tensor], axis: int = 0) -> torch.Tensor
     """Random permutation of ``range(x)`` or of ``x`` along ``axis`` (sort of random keys)."""
     if isinstance(x, int):
         n = x
-        perm = torch.argsort(bits(key, (n,)) * 0 + uniform(key, (n,)), stable=True)
+        perm = torch.argsort(uniform(key, (n,)), stable=True)
         return perm
     n = x.shape[axis]
     perm = torch.argsort(uniform(key, (n,)), stable=True).to(x.device)

@@ -1,0 +1,180 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 (or fp64) reference of
+the same op.  Runs on an MI355X (marked gpu)."""
+import math
+
+import pytest
+import torch
+
+from evoxmi import random as rnd
+from evoxmi.ops import _ext
+from evoxmi.ops.linalg import Operand, gemm
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _require_ext():
+    assert _ext.load(), f"evoxmi extension must load on a GPU box: {_ext._ERROR!r}"
+
+
+def _rel(a, b):
+    return ((a.double() - b.double()).abs().max() / (b.double().abs().max() + 1e-30)).item()
+
+
+@pytest.mark.parametrize("a_rc,b_rc", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("M,N,K", [(300, 257, 129), (1000, 1000, 1000), (37, 5, 3)])
+def test_gemm_layouts(a_rc, b_rc, M, N, K):
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(K, M, generator=g) if a_rc else torch.randn(M, K, generator=g)
+    B = torch.randn(K, N, generator=g) if b_rc else torch.randn(N, K, generator=g)
+    ref = gemm(Operand(A, rc=a_rc), Operand(B, rc=b_rc), M, N, K)
+    out = gemm(Operand(A.cuda(), rc=a_rc), Operand(B.cuda(), rc=b_rc), M, N, K).cpu()
+    assert out.shape == ref.shape
+    assert _rel(out, ref) < 1e-5
+
+
+def test_gemm_asymmetric_identity():
+    # A = I with an asymmetric B catches a transposed C-write
+    n = 64
+    I = torch.eye(n)
+    B = torch.arange(n * n, dtype=torch.float32).reshape(n, n)
+    out = gemm(Operand(I.cuda()), Operand(B.cuda()), n, n, n).cpu()
+    assert torch.equal(out, B.T)
+
+
+def test_gemm_prologue_epilogue_gather_split():
+    g = torch.Generator().manual_seed(0)
+    P, d, K = 700, 200, 333
+    X = torch.randn(P, d, generator=g)
+    idx = torch.randperm(P, generator=g)[:K].to(torch.int32)
+    m = torch.randn(d, generator=g)
+    w = torch.rand(K, generator=g)
+    s = torch.tensor([0.7])
+    args = lambda dev: (
+        Operand(X.to(dev), rc=True, gather=idx.to(dev), sub=m.to(dev), kw=w.to(dev), sscale=s.to(dev), sscale_inv=True),
+        Operand(X.to(dev), rc=True, gather=idx.to(dev), sub=m.to(dev), sscale=s.to(dev), sscale_inv=True),
+        d, d, K,
+    )
+    ref = gemm(*args("cpu"), splits=4)
+    out = gemm(*args("cuda"), splits=4).cpu()
+    assert out.shape == ref.shape
+    assert _rel(out.sum(0), ref.sum(0)) < 1e-5
+    # bias + device alpha + k-scale
+    Z = torch.randn(50, 40, generator=g)
+    Bm = torch.randn(30, 40, generator=g)
+    D = torch.rand(40, generator=g)
+    bias = torch.randn(30, generator=g)
+    al = torch.tensor([2.5])
+    r = gemm(Operand(Z, kscale=D), Operand(Bm), 50, 30, 40, alpha_ptr=al, bias_n=bias)
+    o = gemm(Operand(Z.cuda(), kscale=D.cuda()), Operand(Bm.cuda()), 50, 30, 40, alpha_ptr=al.cuda(), bias_n=bias.cuda()).cpu()
+    assert _rel(o, r) < 1e-5
+    assert _rel(r, 2.5 * (Z * D) @ Bm.T + bias) < 1e-5
+
+
+@pytest.mark.parametrize("n", [1, 7, 1000, 10000, 16384])
+def test_argsort(n):
+    from evoxmi.ops.sort import argsort
+
+    x = torch.randn(n)
+    if n > 10:
+        x[3] = x[5]  # tie → index order
+        x[7] = float("nan")
+    k, i = argsort(x.cuda())
+    rk, ri = torch.sort(x, stable=True)
+    assert torch.equal(i.cpu(), ri)
+    assert torch.allclose(k.cpu(), rk, equal_nan=True)
+    k, i = argsort(x.cuda(), descending=True)
+    rk, ri = torch.sort(x, descending=True, stable=True)
+    assert torch.allclose(k.cpu()[~torch.isnan(rk)], rk[~torch.isnan(rk)])
+
+
+@pytest.mark.parametrize("name", ["sphere", "ackley", "rastrigin", "rosenbrock", "griewank", "schwefel", "ellipsoid"])
+@pytest.mark.parametrize("d", [2, 30, 1000])
+def test_classic_kernels(name, d):
+    from evoxmi.problems.numerical import classic
+
+    X = torch.rand(257, d) * 10 - 5
+    fn = getattr(classic, f"{name}_func")
+    if name == "ackley":
+        ref = fn(20.0, 0.2, 2 * math.pi, X.double()).float()
+        out = fn(20.0, 0.2, 2 * math.pi, X.cuda()).cpu()
+    else:
+        ref = fn(X.double()).float()
+        out = fn(X.cuda()).cpu()
+    assert torch.allclose(out, ref, rtol=2e-4, atol=2e-4)
+
+
+@pytest.mark.parametrize("fid", list(range(17)))
+def test_cec_basic_kernels(fid):
+    from evoxmi.problems.numerical import cec2022 as cec
+
+    g = torch.Generator().manual_seed(fid)
+    Z = torch.rand(64, 37, generator=g) * 40 - 20
+    perm = torch.randperm(37, generator=g).to(torch.int32)
+    sub = torch.randn(37, generator=g)
+    for args in [dict(), dict(perm=perm, start=5, length=20), dict(sub=sub, scale=0.5)]:
+        prob = cec.F1_CEC2022()
+        ref = prob._basic(Z.double(), fid, **{k: (v if not isinstance(v, torch.Tensor) or v.dtype != torch.float32 else v.double()) for k, v in args.items()})
+        out = prob._basic(Z.cuda(), fid, **{k: (v.cuda() if isinstance(v, torch.Tensor) else v) for k, v in args.items()}).cpu()
+        assert torch.allclose(out.double(), ref, rtol=1e-3, atol=1e-3), (fid, args, out[:4], ref[:4])
+
+
+@pytest.mark.parametrize("f", list(range(1, 13)))
+@pytest.mark.parametrize("D", [10, 20, 100])
+def test_cec2022_gpu_matches_cpu(f, D):
+    from evoxmi.problems.numerical import CEC2022TestSuit
+
+    p = CEC2022TestSuit.create(f)
+    X = torch.rand(50, D, generator=torch.Generator().manual_seed(f * D)) * 200 - 100
+    ref, _ = p.evaluate(None, X)
+    out, _ = p.evaluate(None, X.cuda())
+    assert torch.allclose(out.cpu(), ref, rtol=2e-3, atol=1e-3), (f, D, out[:3], ref[:3])
+
+
+def test_pso_kernel_matches_cpu():
+    from evoxmi.ops.pso import pso_update
+
+    g = torch.Generator().manual_seed(3)
+    n, d = 100, 13
+    pop, vel, lbl = torch.randn(n, d, generator=g), torch.randn(n, d, generator=g), torch.randn(n, d, generator=g)
+    lbf, fit = torch.randn(n, generator=g), torch.randn(n, generator=g)
+    gbl = torch.randn(d, generator=g)
+    lb, ub = -torch.ones(d) * 2, torch.ones(d) * 2
+    kp, kg = rnd.split(rnd.PRNGKey(5))
+    ref = pso_update(pop, vel, lbl, lbf, fit, gbl, kp, kg, 0.6, 2.5, 0.8, lb, ub)
+    cu = lambda t: t.cuda()
+    out = pso_update(*map(cu, (pop, vel, lbl, lbf, fit, gbl, kp, kg)), 0.6, 2.5, 0.8, cu(lb), cu(ub))
+    for a, b in zip(out, ref):
+        assert torch.allclose(a.cpu(), b, atol=1e-5)
+
+
+def test_cmaes_gpu_converges_sphere():
+    from evoxmi.algorithms import CMAES
+    from evoxmi.monitors import EvalMonitor
+    from evoxmi.problems.numerical import Sphere
+    from evoxmi.workflows import StdWorkflow
+
+    alg = CMAES(torch.tensor([5.0, -10, 15, -20, 25], device="cuda"), init_stdev=0.1, pop_size=10)
+    mon = EvalMonitor()
+    wf = StdWorkflow(alg, Sphere(), monitors=[mon])
+    st = wf.init(rnd.PRNGKey(42, device="cuda"))
+    for _ in range(200):
+        st = wf.step(st)
+    assert mon.get_best_fitness().item() < 0.1
+
+
+def test_cmaes_graph_mode_matches_eager():
+    from evoxmi.algorithms import CMAES
+    from evoxmi.problems.numerical import F1_CEC2022
+    from evoxmi.workflows import StdWorkflow
+
+    d = 64
+    outs = []
+    for graph in (False, True):
+        alg = CMAES(torch.zeros(d, device="cuda"), init_stdev=10.0, pop_size=256)
+        wf = StdWorkflow(alg, F1_CEC2022(), graph=graph)
+        st = wf.init(rnd.PRNGKey(7, device="cuda"))
+        for _ in range(6):
+            st = wf.step(st)
+        outs.append(st.get_child_state("algorithm").mean.clone())
+    assert torch.allclose(outs[0], outs[1], rtol=1e-4, atol=1e-4)
