@@ -168,12 +168,44 @@ at::Tensor cec_basic(const at::Tensor& Z, int64_t fid, const c10::optional<at::T
   return out;
 }
 
+// Runs `sweeps` block-Jacobi sweeps in place on A (np×np) and B (np×np).  All kernels
+// are enqueued on the current stream; convergence is a device flag, so the call is
+// graph-capturable.  Returns [w(np) diag of A, stats(2) = (off², diag²) at the last check].
+std::vector<at::Tensor> jacobi_sweeps(at::Tensor A, at::Tensor B, const at::Tensor& sched, int64_t sweeps, double tol,
+                                      double inner_tol, int64_t max_inner) {
+  CHECK_DEV(A); CHECK_F32(A); CHECK_CONTIG(A); CHECK_DEV(B); CHECK_F32(B); CHECK_CONTIG(B);
+  const int64_t np = A.size(0);
+  TORCH_CHECK(A.dim() == 2 && A.size(1) == np && B.sizes() == A.sizes(), "A, B must be np×np");
+  TORCH_CHECK(np % 32 == 0, "np must be a multiple of 32");
+  const int64_t nb = np / 16;
+  TORCH_CHECK(sched.scalar_type() == at::kInt && sched.is_contiguous() && sched.dim() == 2 && sched.size(0) == nb &&
+                  sched.size(1) == nb, "schedule must be int32 [nb, nb] (row 0: within-block pairing, rows 1..: rounds)");
+  CHECK_DEV(sched);
+  c10::DeviceGuard g(A.device());
+  auto opts = A.options();
+  auto flag = at::zeros({1}, opts.dtype(at::kInt));
+  auto part = at::empty({2 * evx_jacobi_parts()}, opts.dtype(at::kDouble));
+  auto stats = at::zeros({2}, opts.dtype(at::kDouble));
+  auto Vbuf = at::empty({(np / 32) * 32 * 32}, opts);
+  hipStream_t st = cur_stream();
+  const double tol2 = tol * tol;
+  evx_jacobi_check(A.data_ptr<float>(), (int)np, part.data_ptr<double>(), flag.data_ptr<int>(), tol2, stats.data_ptr<double>(), st);
+  for (int64_t sw = 0; sw < sweeps; ++sw) {
+    for (int64_t t = 0; t < nb; ++t)
+      evx_jacobi_round(A.data_ptr<float>(), B.data_ptr<float>(), (int)np, sched.data_ptr<int>() + t * nb, Vbuf.data_ptr<float>(),
+                       flag.data_ptr<int>(), (float)inner_tol, (int)max_inner, t == 0 ? 1 : 0, st);
+    evx_jacobi_check(A.data_ptr<float>(), (int)np, part.data_ptr<double>(), flag.data_ptr<int>(), tol2, stats.data_ptr<double>(), st);
+  }
+  return {A.diagonal().clone(), stats};
+}
+
 }  // namespace
 
 TORCH_LIBRARY(evoxmi, m) {
   m.def("philox_fill(Tensor key, int n, int dist, int offset) -> Tensor");
   m.def("argsort_f32(Tensor keys, int descending) -> Tensor[]");
   m.def("cec_basic(Tensor Z, int fid, Tensor? perm, int start, int L, Tensor? sub, float scale, Tensor? Y, int ystart, int yperm) -> Tensor");
+  m.def("jacobi_sweeps(Tensor A, Tensor B, Tensor sched, int sweeps, float tol, float inner_tol, int max_inner) -> Tensor[]");
   m.def("classic_eval(Tensor X, int func, float a, float b, float c) -> Tensor");
   m.def("gemm_f32(Tensor A, int a_rc, Tensor? a_gather, Tensor? a_sub, int a_sub_on_k, Tensor? a_kscale, Tensor? a_kw, Tensor? a_sscale, int a_sscale_inv, Tensor B, int b_rc, Tensor? b_gather, Tensor? b_sub, int b_sub_on_k, Tensor? b_kscale, Tensor? b_kw, Tensor? b_sscale, int b_sscale_inv, Tensor? alpha_ptr, Tensor? bias_n, float beta, Tensor? Cin, int M, int N, int K, int splits, float alpha) -> Tensor");
   m.def("pso_update(Tensor pop, Tensor vel, Tensor lbl, Tensor lbf, Tensor fit, Tensor gbl, Tensor kp, Tensor kg, float w, float phip, float phig, Tensor lb, Tensor ub) -> Tensor[]");
@@ -182,6 +214,7 @@ TORCH_LIBRARY(evoxmi, m) {
 TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
   m.impl("philox_fill", &philox_fill);
   m.impl("classic_eval", &classic_eval);
+  m.impl("jacobi_sweeps", &jacobi_sweeps);
   m.impl("cec_basic", &cec_basic);
   m.impl("argsort_f32", &argsort_f32);
   m.impl("gemm_f32", &gemm_f32);

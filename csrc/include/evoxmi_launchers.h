@@ -29,3 +29,7 @@ int evx_argsort_max_n();
 void evx_argsort(const float* keys, int n, int descending, float* out_keys, int32_t* out_idx, hipStream_t s);
 void evx_cec_basic(const float* Z, int64_t ld, int N, int fid, const int32_t* perm, int start, int L, const float* sub,
                    float scale, const float* Y, int64_t ldy, int ystart, int yperm, float* out, hipStream_t s);
+void evx_jacobi_round(float* A, float* B, int np, const int* sched_t, float* Vbuf, const int* flag, float inner_tol,
+                      int max_inner, int mode, hipStream_t s);
+void evx_jacobi_check(const float* A, int np, double* part, int* flag, double tol2, double* last_off, hipStream_t s);
+int evx_jacobi_parts();

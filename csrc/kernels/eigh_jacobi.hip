@@ -1,0 +1,277 @@
+// Warm-started two-sided block Jacobi for the symmetric eigenproblem (K4).
+//
+// A (np × np, np = nb·16, nb even) is nearly diagonal (A = Bᵀ C B with the previous
+// generation's eigenbasis B).  One sweep = nb−1 tournament rounds; in round t the nb
+// blocks of 16 indices are paired into nb/2 "pairs" P = (I, J) of 32 indices.
+//
+//  * jacobi_solve : one wave64 per pair.  The 32×32 subproblem S = A[P,P] is loaded
+//    into LDS, symmetrised, and diagonalised with cyclic parallel Jacobi (31 rounds
+//    of 16 rotations per inner sweep, convergence checked per sweep); the accumulated
+//    orthogonal V_P (32×32) goes to global memory.
+//  * jacobi_apply : A ← Jᵀ A J and B ← B J with J = ⊕_P V_P.  Output tile (P,Q) of A
+//    depends only on A[P,Q], V_P and V_Q, so every tile is independent and updated in
+//    place: one wave per 32×32 tile, T = A[P,Q]·V_Q with v_mfma_f32_32x32x2_f32 (16
+//    MFMAs), then V_Pᵀ·T with T taken straight from the accumulator registers as the
+//    B operand (no LDS round trip; the k order is permuted to the accumulator's row
+//    map).  B tiles (32 rows × pair Q) need only the first product.
+//  * jacobi_offnorm / jacobi_flag : Σ off-diagonal² vs tol²·Σ diagonal² → device flag.
+//    Every kernel returns immediately once the flag says "converged", so a fixed
+//    number of sweeps can be captured in a hipGraph without host round trips.
+#include "evoxmi_common.h"
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+namespace {
+
+constexpr int BS = 16;   // block size
+constexpr int PS = 32;   // pair size
+constexpr int LDP = 33;  // padded LDS row
+
+__device__ __forceinline__ int pair_index(const int* __restrict__ sched, int P, int i) {
+  // i in [0, 32): first 16 from block I, next 16 from block J
+  const int blk = sched[2 * P + (i >> 4)];
+  return blk * BS + (i & 15);
+}
+
+// inner circle-method schedule on 32 items: position i in round r
+__device__ __forceinline__ int rr_item(int i, int r) { return i == 0 ? 0 : ((i - 1 + r) % 31) + 1; }
+
+__device__ __forceinline__ void rot_params(float app, float aqq, float apq, float& c, float& s) {
+  c = 1.f;
+  s = 0.f;
+  if (apq != 0.f) {
+    float tau = (aqq - app) / (2.f * apq);
+    float t = copysignf(1.f, tau) / (fabsf(tau) + sqrtf(fmaf(tau, tau, 1.f)));
+    c = rsqrtf(fmaf(t, t, 1.f));
+    s = t * c;
+  }
+}
+
+// 256 threads per 32×32 subproblem: thread t owns the 2×2 block (row pair k = t>>4,
+// col pair l = t&15) of S and the V items (rows 2k, 2k+1 × col pair l).  Each thread
+// computes ONE rotation (its column pair l) from S; the row-pair rotation k is taken
+// from lane (k, k) of the same wave with a cross-lane shuffle.  Per inner round: one
+// LDS read phase, barrier, one LDS write phase, barrier.
+// MODE 0 ("cross"): 16 inner rounds pairing I[x] with J[(x + r) mod 16] — only the
+//   coupling block A_IJ is annihilated; within-block pairs are handled by MODE 1.
+// MODE 1 ("within"): 15 circle-method rounds inside I and inside J simultaneously.
+template <int MODE>
+__global__ void __launch_bounds__(256) jacobi_solve_kernel(const float* __restrict__ A, int np, const int* __restrict__ sched,
+                                                           float* __restrict__ Vout, const int* __restrict__ flag,
+                                                           float tol, int max_inner) {
+  if (flag && *flag) return;
+  __shared__ float S[PS * LDP];
+  __shared__ float V[PS * LDP];
+  __shared__ float red[8];
+  const int t = threadIdx.x;
+  const int P = blockIdx.x;
+  const int blkI = sched[2 * P], blkJ = sched[2 * P + 1];
+  for (int e = t; e < PS * PS; e += 256) {
+    int i = e >> 5, j = e & 31;
+    int gi = (i < 16 ? blkI : blkJ) * BS + (i & 15);
+    int gj = (j < 16 ? blkI : blkJ) * BS + (j & 15);
+    S[i * LDP + j] = A[(int64_t)gi * np + gj];
+    V[i * LDP + j] = (i == j) ? 1.f : 0.f;
+  }
+  __syncthreads();
+  for (int e = t; e < PS * PS; e += 256) {
+    int i = e >> 5, j = e & 31;
+    if (i < j) {
+      float v = 0.5f * (S[i * LDP + j] + S[j * LDP + i]);
+      S[i * LDP + j] = v;
+      S[j * LDP + i] = v;
+    }
+  }
+  __syncthreads();
+  const int k = t >> 4, l = t & 15;
+  const int src_lane = ((k & 3) << 4) | k;  // lane (k, k) inside this wave
+  const int vr0 = 2 * k, vr1 = 2 * k + 1;
+  for (int sweep = 0; sweep < max_inner; ++sweep) {
+    float off = 0.f, dia = 0.f;
+    for (int e = t; e < PS * PS; e += 256) {
+      int i = e >> 5, j = e & 31;
+      float v = S[i * LDP + j];
+      if (i == j) dia += v * v; else off += v * v;
+    }
+    off = evx::wave_sum(off);
+    dia = evx::wave_sum(dia);
+    if ((t & 63) == 0) { red[t >> 6] = off; red[4 + (t >> 6)] = dia; }
+    __syncthreads();
+    off = red[0] + red[1] + red[2] + red[3];
+    dia = red[4] + red[5] + red[6] + red[7];
+    __syncthreads();
+    if (off <= tol * tol * dia || off == 0.f) break;
+    constexpr int ROUNDS = MODE == 0 ? 16 : 15;
+    for (int r = 0; r < ROUNDS; ++r) {
+      int pk, qk, pl, ql;
+      if (MODE == 0) {
+        pk = k; qk = 16 + ((k + r) & 15);
+        pl = l; ql = 16 + ((l + r) & 15);
+      } else {
+        const int kb = (k & 8) << 1, kk = k & 7, lb = (l & 8) << 1, ll = l & 7;
+        pk = kb + (kk == 0 ? 0 : ((kk - 1 + r) % 15) + 1);
+        qk = kb + ((14 - kk + r) % 15) + 1;
+        pl = lb + (ll == 0 ? 0 : ((ll - 1 + r) % 15) + 1);
+        ql = lb + ((14 - ll + r) % 15) + 1;
+      }
+      // ---- read phase
+      float alp = S[pl * LDP + pl], alq = S[ql * LDP + ql], alo = S[pl * LDP + ql];
+      float x00 = S[pk * LDP + pl], x01 = S[pk * LDP + ql], x10 = S[qk * LDP + pl], x11 = S[qk * LDP + ql];
+      float v0a = V[vr0 * LDP + pl], v0b = V[vr0 * LDP + ql];
+      float v1a = V[vr1 * LDP + pl], v1b = V[vr1 * LDP + ql];
+      float cl = 1.f, sl = 0.f;
+      if (alo != 0.f) {
+        float tau = (alq - alp) * __builtin_amdgcn_rcpf(2.f * alo);
+        float tt = copysignf(1.f, tau) * __builtin_amdgcn_rcpf(fabsf(tau) + __builtin_sqrtf(fmaf(tau, tau, 1.f)));
+        cl = __builtin_amdgcn_rsqf(fmaf(tt, tt, 1.f));
+        sl = tt * cl;
+      }
+      const float ck = __shfl(cl, src_lane, 64), sk = __shfl(sl, src_lane, 64);
+      float y00 = ck * x00 - sk * x10, y01 = ck * x01 - sk * x11;
+      float y10 = sk * x00 + ck * x10, y11 = sk * x01 + ck * x11;
+      float o00 = y00 * cl - y01 * sl, o01 = y00 * sl + y01 * cl;
+      float o10 = y10 * cl - y11 * sl, o11 = y10 * sl + y11 * cl;
+      if (k == l) { o01 = 0.f; o10 = 0.f; }
+      __syncthreads();
+      // ---- write phase
+      S[pk * LDP + pl] = o00;
+      S[pk * LDP + ql] = o01;
+      S[qk * LDP + pl] = o10;
+      S[qk * LDP + ql] = o11;
+      V[vr0 * LDP + pl] = v0a * cl - v0b * sl;
+      V[vr0 * LDP + ql] = v0a * sl + v0b * cl;
+      V[vr1 * LDP + pl] = v1a * cl - v1b * sl;
+      V[vr1 * LDP + ql] = v1a * sl + v1b * cl;
+      __syncthreads();
+    }
+  }
+  float* Vo = Vout + (int64_t)P * PS * PS;
+  for (int e = t; e < PS * PS; e += 256) Vo[e] = V[(e >> 5) * LDP + (e & 31)];
+}
+
+// ---------------------------------------------------------------------------------- apply
+// One wave per 32×32 tile; all global loads of the tile and of V_Q / V_P are issued up
+// front (independent registers) so one memory latency covers the whole tile.
+__global__ void __launch_bounds__(256) jacobi_apply_kernel(float* __restrict__ A, float* __restrict__ B, int np,
+                                                           const int* __restrict__ sched, const float* __restrict__ Vp,
+                                                           const int* __restrict__ flag) {
+  if (flag && *flag) return;
+  __shared__ float T0s[4][PS * LDP];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float* T0 = T0s[wv];
+  const int npairs = np / PS;
+  const int tile = blockIdx.x * 4 + wv;
+  const int nA = npairs * npairs;
+  if (tile >= 2 * nA) return;
+  const bool isA = tile < nA;
+  int P = 0, Q, row0 = 0;
+  if (isA) { P = tile / npairs; Q = tile % npairs; }
+  else { int tt = tile - nA; row0 = (tt / npairs) * PS; Q = tt % npairs; }
+  float* M = isA ? A : B;
+  const int h = lane >> 5, c = lane & 31;
+  const int qI = sched[2 * Q], qJ = sched[2 * Q + 1];
+  const int gj = (c < 16 ? qI : qJ) * BS + (c & 15);
+  int pI = 0, pJ = 0;
+  if (isA) { pI = sched[2 * P]; pJ = sched[2 * P + 1]; }
+  // tile gather: iteration it covers rows 2it, 2it+1 (one per half-wave), 32 columns
+  float tv[16];
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const int i = 2 * it + h;
+    const int gi = isA ? ((i < 16 ? pI : pJ) * BS + (i & 15)) : row0 + i;
+    tv[it] = M[(int64_t)gi * np + gj];
+  }
+  const float* VQ = Vp + (int64_t)Q * PS * PS;
+  const float* VP = Vp + (int64_t)P * PS * PS;
+  float bq[16], ap[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) bq[s] = VQ[(2 * s + h) * PS + c];
+  if (isA) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) ap[r] = VP[((r & 3) + 8 * (r >> 2) + 4 * h) * PS + c];
+  }
+#pragma unroll
+  for (int it = 0; it < 16; ++it) T0[(2 * it + h) * LDP + c] = tv[it];
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+  for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(T0[c * LDP + 2 * s + h], bq[s], acc, 0, 0, 0);
+  f32x16 out = acc;
+  if (isA) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) out[r] = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) out = __builtin_amdgcn_mfma_f32_32x32x2f32(ap[r], acc[r], out, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int i = (r & 3) + 8 * (r >> 2) + 4 * h;
+    const int gi = isA ? ((i < 16 ? pI : pJ) * BS + (i & 15)) : row0 + i;
+    M[(int64_t)gi * np + gj] = out[r];
+  }
+}
+
+// ---------------------------------------------------------------------------------- convergence
+__global__ void __launch_bounds__(256) jacobi_offnorm_kernel(const float* __restrict__ A, int np, double* __restrict__ part,
+                                                             const int* __restrict__ flag) {
+  if (flag && *flag) return;
+  __shared__ float scratch[8];
+  double off = 0.0, dia = 0.0;
+  const int64_t total = (int64_t)np * np;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    int i = (int)(e / np), j = (int)(e - (int64_t)i * np);
+    float v = A[e];
+    if (i == j) dia += (double)v * v; else off += (double)v * v;
+  }
+  off = evx::wave_sum_d(off);
+  dia = evx::wave_sum_d(dia);
+  __shared__ double so[4], sd[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) { so[w] = off; sd[w] = dia; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = 0, b = 0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) { a += so[i]; b += sd[i]; }
+    part[2 * blockIdx.x] = a;
+    part[2 * blockIdx.x + 1] = b;
+  }
+  (void)scratch;
+}
+
+__global__ void jacobi_flag_kernel(const double* __restrict__ part, int nparts, int* __restrict__ flag, double tol2,
+                                   double* __restrict__ last_off) {
+  if (*flag) return;
+  double off = 0, dia = 0;
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) { off += part[2 * i]; dia += part[2 * i + 1]; }
+  off = evx::wave_sum_d(off);
+  dia = evx::wave_sum_d(dia);
+  if (threadIdx.x == 0) {
+    if (last_off) { last_off[0] = off; last_off[1] = dia; }
+    if (off <= tol2 * dia) *flag = 1;
+  }
+}
+
+}  // namespace
+
+constexpr int kOffParts = 128;
+
+void evx_jacobi_round(float* A, float* B, int np, const int* sched_t, float* Vbuf, const int* flag, float inner_tol,
+                      int max_inner, int mode, hipStream_t s) {
+  const int npairs = np / PS;
+  if (mode == 0)
+    jacobi_solve_kernel<0><<<npairs, 256, 0, s>>>(A, np, sched_t, Vbuf, flag, inner_tol, max_inner);
+  else
+    jacobi_solve_kernel<1><<<npairs, 256, 0, s>>>(A, np, sched_t, Vbuf, flag, inner_tol, max_inner);
+  const int tiles = 2 * npairs * npairs;
+  jacobi_apply_kernel<<<(tiles + 3) / 4, 256, 0, s>>>(A, B, np, sched_t, Vbuf, flag);
+}
+
+void evx_jacobi_check(const float* A, int np, double* part, int* flag, double tol2, double* last_off, hipStream_t s) {
+  jacobi_offnorm_kernel<<<kOffParts, 256, 0, s>>>(A, np, part, flag);
+  jacobi_flag_kernel<<<1, 64, 0, s>>>(part, kOffParts, flag, tol2, last_off);
+}
+
+int evx_jacobi_parts() { return kOffParts; }

@@ -178,3 +178,37 @@ def test_cmaes_graph_mode_matches_eager():
             st = wf.step(st)
         outs.append(st.get_child_state("algorithm").mean.clone())
     assert torch.allclose(outs[0], outs[1], rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("n", [5, 30, 100, 257, 1000])
+def test_jacobi_cold_eigh(n):
+    from evoxmi.ops import jacobi
+
+    g = torch.Generator().manual_seed(n)
+    X = torch.randn(n, n, generator=g, dtype=torch.float64)
+    C = (X @ X.T / n + torch.eye(n, dtype=torch.float64)).float()
+    w, V = jacobi.eigh(C.cuda())
+    w, V = w.cpu().double(), V.cpu().double()
+    Cd = C.double()
+    rec = (V * w) @ V.T
+    assert ((rec - Cd).norm() / Cd.norm()).item() < 3e-5 * max(1, n / 100) ** 0.5
+    assert ((V.T @ V - torch.eye(n, dtype=torch.float64)).norm() / math.sqrt(n)).item() < 2e-5
+    wr = torch.linalg.eigvalsh(Cd)
+    assert torch.allclose(w, wr, rtol=1e-4, atol=1e-4 * wr.abs().max().item())
+
+
+def test_jacobi_warm_start_converges_fast():
+    from evoxmi.ops import jacobi
+
+    n = 1000
+    g = torch.Generator().manual_seed(0)
+    Q, _ = torch.linalg.qr(torch.randn(n, n, generator=g, dtype=torch.float64))
+    lam = torch.logspace(0, 3, n, dtype=torch.float64)
+    C0 = (Q * lam) @ Q.T
+    Y = torch.randn(2000, n, generator=g, dtype=torch.float64) @ (Q * lam.sqrt()).T
+    C1 = 0.995 * C0 + 0.005 * (Y.T @ Y) / 2000
+    w, B, stats = jacobi.warm_eigh(C1.float().cuda(), Q.float().cuda(), return_stats=True)
+    w, B = w.cpu().double(), B.cpu().double()
+    rec = (B * w) @ B.T
+    assert ((rec - C1).norm() / C1.norm()).item() < 3e-5
+    assert ((B.T @ B - torch.eye(n, dtype=torch.float64)).norm() / math.sqrt(n)).item() < 3e-5
