@@ -199,6 +199,38 @@ std::vector<at::Tensor> jacobi_sweeps(at::Tensor A, at::Tensor B, const at::Tens
   return {A.diagonal().clone(), stats};
 }
 
+at::Tensor philox_words(const at::Tensor& key, int64_t nblocks, int64_t domain, int64_t offset) {
+  check_key(key);
+  c10::DeviceGuard g(key.device());
+  auto out = at::empty({nblocks, 4}, key.options());
+  if (nblocks > 0) evx_philox_words(key.data_ptr<int64_t>(), nblocks, (uint32_t)domain, offset, out.data_ptr<int64_t>(), cur_stream());
+  return out;
+}
+
+// Σ_k w[k] (X[idx[k]] − sub) over the first K (gathered) rows → (D,)
+at::Tensor weighted_rowsum(const at::Tensor& X, const c10::optional<at::Tensor>& idx, const at::Tensor& w,
+                           const c10::optional<at::Tensor>& sub, int64_t K) {
+  CHECK_DEV(X); CHECK_F32(X); CHECK_DEV(w); CHECK_F32(w); CHECK_CONTIG(w);
+  TORCH_CHECK(X.dim() == 2 && X.stride(1) == 1, "X must be row-major 2-D");
+  TORCH_CHECK(w.numel() >= K, "w too short");
+  const int32_t* ip = nullptr;
+  if (idx.has_value() && idx->defined()) {
+    TORCH_CHECK(idx->scalar_type() == at::kInt && idx->is_contiguous() && idx->numel() >= K, "idx");
+    ip = idx->data_ptr<int32_t>();
+  } else {
+    TORCH_CHECK(X.size(0) >= K, "X too short");
+  }
+  const int64_t D = X.size(1);
+  c10::DeviceGuard g(X.device());
+  const int chunks = (int)std::max<int64_t>(1, std::min<int64_t>(64, (K + 63) / 64));
+  auto part = at::empty({chunks, D}, X.options());
+  evx_weighted_rowsum(X.data_ptr<float>(), X.stride(0), ip, w.data_ptr<float>(), optf(sub), (int)K, (int)D, part.data_ptr<float>(),
+                      chunks, cur_stream());
+  return part.sum(0);
+}
+
+void gemm_set_config(int64_t cfg) { evx_gemm_set_config((int)cfg); }
+
 }  // namespace
 
 TORCH_LIBRARY(evoxmi, m) {
@@ -206,14 +238,23 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("argsort_f32(Tensor keys, int descending) -> Tensor[]");
   m.def("cec_basic(Tensor Z, int fid, Tensor? perm, int start, int L, Tensor? sub, float scale, Tensor? Y, int ystart, int yperm) -> Tensor");
   m.def("jacobi_sweeps(Tensor A, Tensor B, Tensor sched, int sweeps, float tol, float inner_tol, int max_inner) -> Tensor[]");
+  m.def("philox_words(Tensor key, int nblocks, int domain, int offset) -> Tensor");
+  m.def("weighted_rowsum(Tensor X, Tensor? idx, Tensor w, Tensor? sub, int K) -> Tensor");
+  m.def("gemm_set_config(int cfg) -> ()");
   m.def("classic_eval(Tensor X, int func, float a, float b, float c) -> Tensor");
   m.def("gemm_f32(Tensor A, int a_rc, Tensor? a_gather, Tensor? a_sub, int a_sub_on_k, Tensor? a_kscale, Tensor? a_kw, Tensor? a_sscale, int a_sscale_inv, Tensor B, int b_rc, Tensor? b_gather, Tensor? b_sub, int b_sub_on_k, Tensor? b_kscale, Tensor? b_kw, Tensor? b_sscale, int b_sscale_inv, Tensor? alpha_ptr, Tensor? bias_n, float beta, Tensor? Cin, int M, int N, int K, int splits, float alpha) -> Tensor");
   m.def("pso_update(Tensor pop, Tensor vel, Tensor lbl, Tensor lbf, Tensor fit, Tensor gbl, Tensor kp, Tensor kg, float w, float phip, float phig, Tensor lb, Tensor ub) -> Tensor[]");
 }
 
+TORCH_LIBRARY_IMPL(evoxmi, CompositeExplicitAutograd, m) {
+  m.impl("gemm_set_config", &gemm_set_config);
+}
+
 TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
   m.impl("philox_fill", &philox_fill);
   m.impl("classic_eval", &classic_eval);
+  m.impl("philox_words", &philox_words);
+  m.impl("weighted_rowsum", &weighted_rowsum);
   m.impl("jacobi_sweeps", &jacobi_sweeps);
   m.impl("cec_basic", &cec_basic);
   m.impl("argsort_f32", &argsort_f32);

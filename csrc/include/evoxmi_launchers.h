@@ -33,3 +33,7 @@ void evx_jacobi_round(float* A, float* B, int np, const int* sched_t, float* Vbu
                       int max_inner, int mode, hipStream_t s);
 void evx_jacobi_check(const float* A, int np, double* part, int* flag, double tol2, double* last_off, hipStream_t s);
 int evx_jacobi_parts();
+void evx_philox_words(const int64_t* key, int64_t nblocks, uint32_t domain, int64_t offset, int64_t* out, hipStream_t s);
+void evx_weighted_rowsum(const float* X, int64_t ldx, const int32_t* idx, const float* w, const float* sub, int K, int D,
+                         float* partial, int chunks, hipStream_t s);
+void evx_gemm_set_config(int cfg);

@@ -42,3 +42,29 @@ void evx_philox_fill(float* out, int64_t n, const int64_t* key, int dist, int64_
   else
     philox_fill_kernel<1><<<grid, 256, 0, s>>>(out, n, key, elem_offset >> 2);
 }
+
+// Raw Philox words for small key-management ops (split / fold_in / bits): one launch
+// instead of ~80 int64 elementwise kernels.  out[b][w] = word w of block (offset + b)
+// with counter (b_lo, b_hi, 0, domain).  Words are stored as int64 (uint32 values).
+namespace {
+__global__ void philox_words_kernel(const int64_t* __restrict__ key, int64_t nblocks, uint32_t domain, int64_t offset,
+                                    int64_t* __restrict__ out) {
+  uint32_t k0, k1;
+  evx::load_key(key, k0, k1);
+  for (int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; b < nblocks; b += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t c = (uint64_t)(b + offset);
+    evx::u4 w = evx::philox4x32_10(evx::u4{(uint32_t)c, (uint32_t)(c >> 32), 0u, domain}, k0, k1);
+    out[4 * b + 0] = w.x;
+    out[4 * b + 1] = w.y;
+    out[4 * b + 2] = w.z;
+    out[4 * b + 3] = w.w;
+  }
+}
+}  // namespace
+
+void evx_philox_words(const int64_t* key, int64_t nblocks, uint32_t domain, int64_t offset, int64_t* out, hipStream_t s) {
+  int grid = (int)((nblocks + 255) / 256);
+  if (grid > 1024) grid = 1024;
+  if (grid < 1) grid = 1;
+  philox_words_kernel<<<grid, 256, 0, s>>>(key, nblocks, domain, offset, out);
+}

@@ -1,62 +1,118 @@
-// Single-workgroup LDS bitonic argsort (K19) for populations up to 16384.
-// Keys are f32 fitness values mapped to order-preserving u32 (NaN → +inf side, i.e.
-// sorted last like torch.sort), packed with the 32-bit index into one u64 so that a
-// single 64-bit compare orders by (key, index): deterministic and equal to a stable
-// sort.  The whole array lives in LDS (16384 x 8 B = 128 KiB of the 160 KiB per CU);
-// 1024 threads, one barrier per bitonic stage, stages with stride < 64 are done with
-// wave shuffles... kept in LDS here for simplicity (≈105 stages at n=16384).
+// Single-workgroup argsort (K19) for populations up to 16384 — register + LDS bitonic.
+//
+// Keys are f32 fitness values mapped to order-preserving u32 and packed with the
+// 32-bit index into one u64, so a single 64-bit compare orders by (key, index):
+// deterministic and identical to a stable sort (torch semantics: NaN is the largest
+// value).  1024 threads each hold E = NP/1024 consecutive elements in registers:
+//   * compare-exchange stages with stride j < E run entirely in registers (the stage
+//     structure is unrolled at compile time so no register is indexed dynamically);
+//   * stages with j ≥ E exchange whole per-thread runs with partner thread t ^ (j/E)
+//     through LDS: one vectorised write (ds_write_b128), barrier, one vectorised read
+//     of the partner's run, barrier.  Runs are padded to 144 B so the ds_read_b128 lane
+//     groups hit distinct banks.
+// At NP = 16384: 55 LDS stages instead of the 105 of an all-LDS bitonic network.
 #include "evoxmi_common.h"
 
 namespace {
 
 __device__ __forceinline__ uint32_t f2ord(float f) {
   uint32_t u = __float_as_uint(f);
-  if (f != f) return 0xFFFFFFFFu;  // NaN last
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
-__device__ __forceinline__ float ord2f(uint32_t o) {
-  uint32_t u = (o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o;
-  return __uint_as_float(u);
+
+template <int E>
+struct Run {
+  unsigned long long v[E];
+};
+
+// in-register compare-exchange for all strides j < E of phase k (e0 = global index of v[0])
+template <int E>
+__device__ __forceinline__ void reg_stages(Run<E>& R, int k, int e0) {
+#pragma unroll
+  for (int j = E / 2; j > 0; j >>= 1) {
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+      if ((r & j) == 0) {
+        const int e = e0 + r;
+        const bool up = (e & k) == 0;
+        unsigned long long a = R.v[r], b = R.v[r + j];
+        const bool sw = (a > b) == up;
+        R.v[r] = sw ? b : a;
+        R.v[r + j] = sw ? a : b;
+      }
+    }
+  }
 }
 
 template <int LOGN>
 __global__ void __launch_bounds__(1024) bitonic_argsort_kernel(const float* __restrict__ keys, int n, int descending,
                                                                float* __restrict__ out_keys, int32_t* __restrict__ out_idx) {
   constexpr int NP = 1 << LOGN;
-  __shared__ unsigned long long s[NP];
-  for (int i = threadIdx.x; i < NP; i += blockDim.x) {
-    unsigned long long v;
+  constexpr int T = 1024;
+  constexpr int E = NP / T;  // 1..16
+  constexpr int RUN_U64 = E < 2 ? E : E + 2;  // pad runs (144 B for E = 16) to spread banks
+  __shared__ unsigned long long s[T * RUN_U64];
+  const int t = threadIdx.x;
+  const int e0 = t * E;
+  Run<E> R;
+#pragma unroll
+  for (int r = 0; r < E; ++r) {
+    const int i = e0 + r;
+    unsigned long long v = 0xFFFFFFFFFFFFFFFFull;
     if (i < n) {
-      float k = keys[i];
-      // torch semantics: NaN is the largest value (last ascending, first descending)
+      const float k = keys[i];
       uint32_t o = (k != k) ? (descending ? 0u : 0xFFFFFFFFu) : f2ord(descending ? -k : k);
       v = ((unsigned long long)o << 32) | (uint32_t)i;
-    } else {
-      v = 0xFFFFFFFFFFFFFFFFull;  // padding sorts last
     }
-    s[i] = v;
+    R.v[r] = v;
   }
-  __syncthreads();
-  for (int k = 2; k <= NP; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int t = threadIdx.x; t < NP / 2; t += blockDim.x) {
-        int i = ((t & ~(j - 1)) << 1) | (t & (j - 1));  // lower element of the pair
-        int p = i | j;
-        bool up = ((i & k) == 0);
-        unsigned long long a = s[i], b = s[p];
-        if ((a > b) == up) {
-          s[i] = b;
-          s[p] = a;
+  // phases k ≤ E: entirely in registers
+#pragma unroll
+  for (int k = 2; k <= E; k <<= 1) {
+#pragma unroll
+    for (int j = k / 2; j > 0; j >>= 1) {
+#pragma unroll
+      for (int r = 0; r < E; ++r) {
+        if ((r & j) == 0) {
+          const bool up = ((e0 + r) & k) == 0;
+          unsigned long long a = R.v[r], b = R.v[r + j];
+          const bool sw = (a > b) == up;
+          R.v[r] = sw ? b : a;
+          R.v[r + j] = sw ? a : b;
         }
+      }
+    }
+  }
+  for (int k = 2 * E; k <= NP; k <<= 1) {
+    for (int j = k >> 1; j >= E; j >>= 1) {
+      const int pt = t ^ (j / E);
+      unsigned long long* mine = s + t * RUN_U64;
+      const unsigned long long* theirs = s + pt * RUN_U64;
+#pragma unroll
+      for (int r = 0; r < E; ++r) mine[r] = R.v[r];
+      __syncthreads();
+      const bool lower = (t & (j / E)) == 0;
+#pragma unroll
+      for (int r = 0; r < E; ++r) {
+        const int e = e0 + r;
+        const bool up = (e & k) == 0;
+        unsigned long long a = R.v[r], b = theirs[r];
+        // lower element keeps min when ascending, upper keeps max
+        const bool take_min = (lower == up);
+        R.v[r] = take_min ? (a < b ? a : b) : (a > b ? a : b);
       }
       __syncthreads();
     }
+    reg_stages<E>(R, k, e0);
   }
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    unsigned long long v = s[i];
-    const int32_t src = (int32_t)(v & 0xFFFFFFFFu);
-    if (out_keys) out_keys[i] = keys[src];
-    out_idx[i] = src;
+#pragma unroll
+  for (int r = 0; r < E; ++r) {
+    const int i = e0 + r;
+    if (i < n) {
+      const int32_t src = (int32_t)(R.v[r] & 0xFFFFFFFFu);
+      if (out_keys) out_keys[i] = keys[src];
+      out_idx[i] = src;
+    }
   }
 }
 

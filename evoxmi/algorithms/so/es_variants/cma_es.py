@@ -33,6 +33,7 @@ from ....core import Algorithm, State
 from ....ops import random as rnd
 from ....ops.eigh import symmetrize_upper, warm_eigh
 from ....ops.linalg import Operand, gemm
+from ....ops.reduce import weighted_rowsum
 from ....ops.sort import argsort, argsort_i32
 
 
@@ -103,8 +104,10 @@ class CMAES(Algorithm):
         d = self.dim
         z = rnd.normal(key, (rows, d), offset=row0 * d)
         if z.is_cuda:
-            # X = mean + σ (Z∘D) Bᵀ : one MFMA GEMM, scaling in the prologue, mean+σ· in the epilogue
-            return gemm(Operand(z, kscale=state.D), Operand(state.B), rows, d, d, alpha_ptr=state.sigma.reshape(1), bias_n=state.mean)
+            # X = mean + σ (Z∘D) Bᵀ = mean + σ Z (B∘D)ᵀ : one prologue-free MFMA GEMM with
+            # mean + σ· fused in the epilogue (σ read from HBM, no host sync)
+            BD = (state.B * state.D).contiguous()
+            return gemm(Operand(z), Operand(BD), rows, d, d, alpha_ptr=state.sigma.reshape(1), bias_n=state.mean)
         return state.mean + state.sigma * (state.D * z) @ state.B.T
 
     def ask(self, state):
@@ -119,10 +122,8 @@ class CMAES(Algorithm):
         if population.is_cuda:
             rows = order_i32 if gather else None
             one_over = state.sigma.reshape(1)
-            # mean: 1×K · K×d, split-K to fill the chip
-            w2 = wvec.reshape(1, -1).contiguous()
-            dm = gemm(Operand(w2), Operand(population, rc=True, gather=rows, sub=state.mean), 1, d, K, splits=64)
-            dm = dm.sum(0).reshape(d) if dm.dim() == 3 else dm.reshape(d)
+            # weighted mean shift: gathered weighted row sum (reduce.hip), deterministic
+            dm = weighted_rowsum(population, rows, wvec, state.mean, K)
             splits = max(1, min(16, K // 256))
             S = gemm(
                 Operand(population, rc=True, gather=rows, sub=state.mean, kw=wvec, sscale=one_over, sscale_inv=True),

@@ -77,7 +77,7 @@ def gemm(a: Operand, b: Operand, M: int, N: int, K: int, alpha: float = 1.0, alp
     if splits > 1:
         # same slab semantics as the kernel: slice z covers K range [z*kps, (z+1)*kps)
         kps = -(-K // splits)
-        kps = -(-kps // 16) * 16
+        kps = -(-kps // 64) * 64
         sl = []
         for z in range(-(-K // kps)):
             k0, k1 = z * kps, min(K, (z + 1) * kps)

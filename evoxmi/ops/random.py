@@ -73,6 +73,10 @@ def philox4x32(c0, c1, c2, c3, k0, k1, rounds: int = 10):
 
 def _blocks(key: torch.Tensor, nblocks: int, domain: int, offset: int = 0):
     dev = key.device
+    if key.is_cuda:
+        # one HIP launch (rng.hip: philox_words) instead of ~80 int64 elementwise kernels
+        w = _ext().ops().philox_words(key.contiguous(), int(nblocks), int(domain), int(offset))
+        return w[:, 0], w[:, 1], w[:, 2], w[:, 3]
     idx = torch.arange(offset, offset + nblocks, dtype=torch.int64, device=dev)
     c0 = idx & MASK32
     c1 = (idx >> 32) & MASK32

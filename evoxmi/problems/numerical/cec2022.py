@@ -203,11 +203,13 @@ class _CEC2022(Problem):
             self._cache[key] = c
         return self._cache[key]
 
-    # ssr: (x − o)·s rotated by M (rows [r0, r0+D) of the stacked rotations)
+    # ssr: z = M (x − o)·s.  The shift is applied before the GEMM (exact zero at the
+    # optimum, as in the reference) and the scale folds into the GEMM epilogue.
     def _ssr(self, X, o, M, s):
         N, D = X.shape
-        sv = torch.full((1,), float(s), dtype=torch.float32, device=X.device)
-        return linalg.gemm(linalg.Operand(X, sub=o, sub_on_k=True, sscale=sv), linalg.Operand(M), N, D, D)
+        if X.is_cuda:
+            return linalg.gemm(linalg.Operand((X - o).contiguous()), linalg.Operand(M), N, D, D, alpha=float(s))
+        return ((X - o) * s) @ M.T
 
     def _basic(self, Z, fid, perm=None, start=0, length=None, sub=None, scale=1.0, ysrc=None, ystart=0):
         """fid on z_eff[:, j] = (Z[:, idx_j] − sub[idx_j])·scale, idx_j = perm[start+j] (or start+j)."""

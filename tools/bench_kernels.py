@@ -26,12 +26,22 @@ dev = torch.device("cuda")
 res = {}
 A = torch.randn(10000, 1000, device=dev)
 B = torch.randn(1000, 1000, device=dev)
-res["gemm_nt_10000x1000x1000_ms"] = t(lambda: gemm(Operand(A), Operand(B), 10000, 1000, 1000))
+from evoxmi.ops import _ext
+ops = _ext.ops()
+D = torch.rand(1000, device=dev)
+for cfg in (-1, 0, 3, 4, 5, 6, 7):
+    ops.gemm_set_config(cfg)
+    res[f"gemm_nt_10000x1000x1000_cfg{cfg}_ms"] = t(lambda: gemm(Operand(A), Operand(B), 10000, 1000, 1000))
+    res[f"gemm_nt_pro_10000x1000x1000_cfg{cfg}_ms"] = t(lambda: gemm(Operand(A, kscale=D), Operand(B), 10000, 1000, 1000))
+    idx0 = torch.randperm(10000, device=dev)[:5000].to(torch.int32)
+    res[f"gemm_tn_gather_split8_cfg{cfg}_ms"] = t(lambda: gemm(Operand(A, rc=True, gather=idx0, sub=D), Operand(A, rc=True, gather=idx0, sub=D), 1000, 1000, 5000, splits=8))
+    res[f"gemm_1024_nn_cfg{cfg}_ms"] = t(lambda: gemm(Operand(B), Operand(B, rc=True), 1000, 1000, 1000))
+ops.gemm_set_config(-1)
 res["torch_mm_10000x1000x1000_ms"] = t(lambda: A @ B.T)
 idx = torch.randperm(10000, device=dev)[:5000].to(torch.int32)
 m = torch.randn(1000, device=dev)
 w = torch.rand(5000, device=dev)
-for sp in (1, 4, 8, 16):
+for sp in (4, 8, 16):
     res[f"gemm_tn_gather_1000x1000x5000_split{sp}_ms"] = t(lambda: gemm(Operand(A, rc=True, gather=idx, sub=m, kw=w), Operand(A, rc=True, gather=idx, sub=m), 1000, 1000, 5000, splits=sp))
 Y = A[:5000]
 res["torch_syrk_ms"] = t(lambda: Y.T @ Y)
