@@ -231,6 +231,54 @@ at::Tensor weighted_rowsum(const at::Tensor& X, const c10::optional<at::Tensor>&
 
 void gemm_set_config(int64_t cfg) { evx_gemm_set_config((int)cfg); }
 
+at::Tensor sbx(const at::Tensor& x, const at::Tensor& keys, double pro_c, double dis_c, int64_t type) {
+  CHECK_DEV(x); CHECK_F32(x); CHECK_CONTIG(x); CHECK_DEV(keys);
+  TORCH_CHECK(x.dim() == 2, "x must be (n, d)");
+  TORCH_CHECK(keys.scalar_type() == at::kLong && keys.is_contiguous() && keys.numel() == 8, "keys must be int64[4,2]");
+  TORCH_CHECK(type == 1 || type == 2, "type must be 1 or 2");
+  const int64_t n = x.size(0), d = x.size(1);
+  c10::DeviceGuard g(x.device());
+  const int64_t rows = type == 1 ? n : n / 2;
+  auto out = at::empty({rows, d}, x.options());
+  if (rows > 0 && d > 0) evx_sbx(x.data_ptr<float>(), out.data_ptr<float>(), (int)n, (int)d, keys.data_ptr<int64_t>(), (float)pro_c, (float)dis_c, (int)type, cur_stream());
+  return out;
+}
+
+at::Tensor pm(const at::Tensor& x, const at::Tensor& lb, const at::Tensor& ub, const at::Tensor& keys, double pro_m, double dis_m, int64_t nm) {
+  CHECK_DEV(x); CHECK_F32(x); CHECK_CONTIG(x); CHECK_DEV(lb); CHECK_F32(lb); CHECK_CONTIG(lb); CHECK_DEV(ub); CHECK_F32(ub); CHECK_CONTIG(ub);
+  TORCH_CHECK(keys.scalar_type() == at::kLong && keys.is_contiguous() && keys.numel() == 4, "keys must be int64[2,2]");
+  TORCH_CHECK(x.dim() == 2 && lb.numel() == x.size(1) && ub.numel() == x.size(1), "shape mismatch");
+  c10::DeviceGuard g(x.device());
+  auto out = at::empty_like(x);
+  if (x.numel() > 0)
+    evx_pm(x.data_ptr<float>(), out.data_ptr<float>(), (int)x.size(0), (int)x.size(1), (int)nm, lb.data_ptr<float>(), ub.data_ptr<float>(),
+           keys.data_ptr<int64_t>(), (float)pro_m, (float)dis_m, cur_stream());
+  return out;
+}
+
+at::Tensor nds(const at::Tensor& f) {
+  CHECK_DEV(f); CHECK_F32(f); CHECK_CONTIG(f);
+  TORCH_CHECK(f.dim() == 2 && f.size(1) >= 1 && f.size(1) <= 8, "fitness must be (n, m) with m <= 8");
+  const int64_t n = f.size(0), nw = (n + 31) / 32;
+  TORCH_CHECK(n <= 65536, "nds: n <= 65536");
+  c10::DeviceGuard g(f.device());
+  auto DT = at::empty({n, nw}, f.options().dtype(at::kInt));
+  auto rank = at::empty({n}, f.options().dtype(at::kInt));
+  auto cnt = at::empty({n}, f.options().dtype(at::kInt));
+  if (n > 0) evx_nds(f.data_ptr<float>(), (int)n, (int)f.size(1), reinterpret_cast<uint32_t*>(DT.data_ptr<int>()), rank.data_ptr<int>(), cnt.data_ptr<int>(), cur_stream());
+  return rank;
+}
+
+at::Tensor dtlz(const at::Tensor& X, int64_t m, int64_t variant) {
+  CHECK_DEV(X); CHECK_F32(X); CHECK_CONTIG(X);
+  TORCH_CHECK(X.dim() == 2 && m >= 2 && m <= 64 && X.size(1) >= m, "dtlz: X must be (n, d) with 2 <= m <= min(d, 64)");
+  TORCH_CHECK(variant >= 1 && variant <= 4, "dtlz: variant 1..4");
+  c10::DeviceGuard g(X.device());
+  auto F = at::empty({X.size(0), m}, X.options());
+  if (X.size(0) > 0) evx_dtlz(X.data_ptr<float>(), F.data_ptr<float>(), (int)X.size(0), (int)X.size(1), (int)m, (int)variant, cur_stream());
+  return F;
+}
+
 }  // namespace
 
 TORCH_LIBRARY(evoxmi, m) {
@@ -241,6 +289,10 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("philox_words(Tensor key, int nblocks, int domain, int offset) -> Tensor");
   m.def("weighted_rowsum(Tensor X, Tensor? idx, Tensor w, Tensor? sub, int K) -> Tensor");
   m.def("gemm_set_config(int cfg) -> ()");
+  m.def("sbx(Tensor x, Tensor keys, float pro_c, float dis_c, int type) -> Tensor");
+  m.def("pm(Tensor x, Tensor lb, Tensor ub, Tensor keys, float pro_m, float dis_m, int nm) -> Tensor");
+  m.def("nds(Tensor f) -> Tensor");
+  m.def("dtlz(Tensor X, int m, int variant) -> Tensor");
   m.def("classic_eval(Tensor X, int func, float a, float b, float c) -> Tensor");
   m.def("gemm_f32(Tensor A, int a_rc, Tensor? a_gather, Tensor? a_sub, int a_sub_on_k, Tensor? a_kscale, Tensor? a_kw, Tensor? a_sscale, int a_sscale_inv, Tensor B, int b_rc, Tensor? b_gather, Tensor? b_sub, int b_sub_on_k, Tensor? b_kscale, Tensor? b_kw, Tensor? b_sscale, int b_sscale_inv, Tensor? alpha_ptr, Tensor? bias_n, float beta, Tensor? Cin, int M, int N, int K, int splits, float alpha) -> Tensor");
   m.def("pso_update(Tensor pop, Tensor vel, Tensor lbl, Tensor lbf, Tensor fit, Tensor gbl, Tensor kp, Tensor kg, float w, float phip, float phig, Tensor lb, Tensor ub) -> Tensor[]");
@@ -253,6 +305,10 @@ TORCH_LIBRARY_IMPL(evoxmi, CompositeExplicitAutograd, m) {
 TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
   m.impl("philox_fill", &philox_fill);
   m.impl("classic_eval", &classic_eval);
+  m.impl("sbx", &sbx);
+  m.impl("pm", &pm);
+  m.impl("nds", &nds);
+  m.impl("dtlz", &dtlz);
   m.impl("philox_words", &philox_words);
   m.impl("weighted_rowsum", &weighted_rowsum);
   m.impl("jacobi_sweeps", &jacobi_sweeps);

@@ -37,3 +37,8 @@ void evx_philox_words(const int64_t* key, int64_t nblocks, uint32_t domain, int6
 void evx_weighted_rowsum(const float* X, int64_t ldx, const int32_t* idx, const float* w, const float* sub, int K, int D,
                          float* partial, int chunks, hipStream_t s);
 void evx_gemm_set_config(int cfg);
+void evx_sbx(const float* x, float* out, int n, int d, const int64_t* keys, float pro_c, float dis_c, int type, hipStream_t s);
+void evx_pm(const float* x, float* out, int n, int d, int nm, const float* lb, const float* ub, const int64_t* keys, float pro_m,
+            float dis_m, hipStream_t s);
+void evx_dtlz(const float* X, float* F, int N, int D, int M, int variant, hipStream_t s);
+void evx_nds(const float* f, int n, int m, uint32_t* DT, int32_t* rank, int32_t* cnt, hipStream_t s);

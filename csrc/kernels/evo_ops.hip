@@ -1,0 +1,88 @@
+// Variation operators as fused elementwise kernels (K11): PlatEMO SBX and polynomial
+// mutation.  Random numbers are regenerated in-register from Philox counters with the
+// same element indexing as evoxmi.ops.random (uniform → u24 of word i%4 of block i/4,
+// randint(0,2) → top bit), so GPU and CPU draw identical streams.
+#include "evoxmi_common.h"
+
+namespace {
+
+__device__ __forceinline__ uint32_t word_at(uint64_t i, uint32_t k0, uint32_t k1) {
+  evx::u4 w = evx::philox_block(i >> 2, k0, k1);
+  const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+  return ws[i & 3];
+}
+
+// keys: 4 consecutive keys (int64[4][2]) = split(key, 4) → mu, b1, b2, b3
+__global__ void __launch_bounds__(256) sbx_kernel(const float* __restrict__ x, float* __restrict__ out, int n, int d,
+                                                  const int64_t* __restrict__ keys, float pro_c, float dis_c, int type) {
+  const int np = n / 2;
+  const int64_t total = (int64_t)np * d;
+  uint32_t km0 = (uint32_t)keys[0], km1 = (uint32_t)keys[1];
+  uint32_t ka0 = (uint32_t)keys[2], ka1 = (uint32_t)keys[3];
+  uint32_t kb0 = (uint32_t)keys[4], kb1 = (uint32_t)keys[5];
+  uint32_t kc0 = (uint32_t)keys[6], kc1 = (uint32_t)keys[7];
+  const float e = 1.f / (dis_c + 1.f);
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int i = (int)(t / d), j = (int)(t - (int64_t)i * d);
+    const float p1 = x[(int64_t)i * d + j], p2 = x[(int64_t)(np + i) * d + j];
+    const float mu = evx::u24(word_at((uint64_t)t, km0, km1));
+    float beta = mu <= 0.5f ? powf(2.f * mu, e) : powf(2.f - 2.f * mu, -e);
+    if (word_at((uint64_t)t, ka0, ka1) >> 31) beta = -beta;
+    if (evx::u24(word_at((uint64_t)t, kb0, kb1)) < 0.5f) beta = 1.f;
+    if (evx::u24(word_at((uint64_t)i, kc0, kc1)) > pro_c) beta = 1.f;
+    const float mid = 0.5f * (p1 + p2), half = 0.5f * (p1 - p2);
+    out[(int64_t)i * d + j] = mid + beta * half;
+    if (type == 1) out[(int64_t)(np + i) * d + j] = mid - beta * half;
+  }
+  if (type == 1 && (n & 1)) {  // odd population: last parent passes through
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < d; j += gridDim.x * blockDim.x)
+      out[(int64_t)(2 * np) * d + j] = x[(int64_t)(n - 1) * d + j];
+  }
+}
+
+// keys: split(key, 2) → site, mu.  Rows beyond the even prefix pass through.
+__global__ void __launch_bounds__(256) pm_kernel(const float* __restrict__ x, float* __restrict__ out, int n, int d, int nm,
+                                                 const float* __restrict__ lb, const float* __restrict__ ub,
+                                                 const int64_t* __restrict__ keys, float pro_m, float dis_m) {
+  const int64_t total = (int64_t)n * d;
+  uint32_t ks0 = (uint32_t)keys[0], ks1 = (uint32_t)keys[1];
+  uint32_t ku0 = (uint32_t)keys[2], ku1 = (uint32_t)keys[3];
+  const float e1 = dis_m + 1.f, inv = 1.f / (dis_m + 1.f);
+  const float pr = pro_m / d;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int i = (int)(t / d), j = (int)(t - (int64_t)i * d);
+    float v = x[t];
+    if (i < nm) {
+      const float lo = lb[j], hi = ub[j], span = hi - lo;
+      v = fmaxf(fminf(v, hi), lo);
+      const bool site = evx::u24(word_at((uint64_t)t, ks0, ks1)) < pr;
+      const float mu = evx::u24(word_at((uint64_t)t, ku0, ku1));
+      if (site) {
+        if (mu <= 0.5f) {
+          const float nrm = (v - lo) / span;
+          v = v + span * (powf(2.f * mu + (1.f - 2.f * mu) * powf(1.f - nrm, e1), inv) - 1.f);
+        } else {
+          const float nrm = (hi - v) / span;
+          v = v + span * (1.f - powf(2.f * (1.f - mu) + 2.f * (mu - 0.5f) * powf(1.f - nrm, e1), inv));
+        }
+      }
+    }
+    out[t] = v;
+  }
+}
+
+int grid_for(int64_t total) {
+  int64_t g = (total + 255) / 256;
+  return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
+}
+
+}  // namespace
+
+void evx_sbx(const float* x, float* out, int n, int d, const int64_t* keys, float pro_c, float dis_c, int type, hipStream_t s) {
+  sbx_kernel<<<grid_for((int64_t)(n / 2) * d), 256, 0, s>>>(x, out, n, d, keys, pro_c, dis_c, type);
+}
+
+void evx_pm(const float* x, float* out, int n, int d, int nm, const float* lb, const float* ub, const int64_t* keys, float pro_m,
+            float dis_m, hipStream_t s) {
+  pm_kernel<<<grid_for((int64_t)n * d), 256, 0, s>>>(x, out, n, d, nm, lb, ub, keys, pro_m, dis_m);
+}

@@ -1,1 +1,2 @@
 from .so import *  # noqa
+from .mo import *  # noqa

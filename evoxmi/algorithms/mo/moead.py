@@ -1,0 +1,167 @@
+"""MOEA/D (reference ``algorithms/mo/moead.py:19-134``).
+
+Semantics kept: Das–Dennis weights with ``pop_size`` overwritten by the number of
+weight vectors, T = ⌈N/10⌉ nearest neighbours, two random neighbours → SBX
+(type 2) + polynomial mutation, default PBI aggregation (``func_name``).
+
+``tell`` — the reference runs a *sequential* ``lax.scan`` over the N offspring,
+each replacing neighbours it improves.  During that scan ``z``, ``z_max`` and the
+weights are fixed, so slot ``s`` only ever compares its *own* current occupant
+with offspring ``i`` (for every ``i`` whose neighbourhood contains ``s``, in
+increasing ``i``) and replaces on strict improvement.  Its final occupant is
+therefore the **first minimiser** of the aggregation over
+``[original, offspring i ∈ revN(s) in order]`` — an exact, order-preserving
+reformulation that evaluates all N·T (slot, offspring) pairs at once and
+reduces per slot (a segmented first-argmin over the reverse-neighbour CSR),
+then gathers only the winning rows.  At N = 16384, d = 10 000 this replaces
+16 384 dependent steps (each moving T rows of 10 000 floats) with one parallel
+pass plus one row gather.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ...core import Algorithm, State
+from ...operators import crossover, mutation
+from ...operators.sampling import UniformSampling
+from ...ops import random as rnd
+from ...utils.common import AggregationFunction
+
+
+def nearest_neighbors(w: torch.Tensor, T: int, chunk: int = 4096) -> torch.Tensor:
+    """T nearest weight vectors of every weight (ties by index, like a stable argsort)."""
+    n = w.shape[0]
+    out = []
+    ww = (w * w).sum(1)
+    for s in range(0, n, chunk):
+        blk = w[s : s + chunk]
+        d2 = (ww[s : s + chunk, None] + ww[None, :] - 2 * blk @ w.T).clamp_min(0)
+        d = torch.sqrt(d2)
+        out.append(torch.argsort(d, dim=1, stable=True)[:, :T])
+    return torch.cat(out, 0)
+
+
+def reverse_neighbors(neighbors: torch.Tensor):
+    """CSR of {i : s ∈ N(i)} for every slot s, with i ascending inside each row."""
+    n, T = neighbors.shape
+    slots = neighbors.reshape(-1)
+    owners = torch.arange(n, device=neighbors.device).repeat_interleave(T)
+    key = slots.to(torch.int64) * n + owners
+    order = torch.argsort(key)
+    rev_owner = owners[order]
+    rev_slot = slots[order]
+    counts = torch.bincount(slots, minlength=n)
+    rowptr = torch.zeros(n + 1, dtype=torch.int64, device=neighbors.device)
+    rowptr[1:] = torch.cumsum(counts, 0)
+    return rowptr, rev_slot, rev_owner
+
+
+def first_argmin_segments(vals: torch.Tensor, seg: torch.Tensor, n_seg: int):
+    """Per segment: (min value, position of its first occurrence) — positions are global."""
+    inf = torch.full((n_seg,), float("inf"), device=vals.device, dtype=vals.dtype)
+    segmin = inf.scatter_reduce(0, seg, vals, reduce="amin", include_self=True)
+    pos = torch.arange(vals.shape[0], device=vals.device)
+    big = torch.full((n_seg,), vals.shape[0], device=vals.device, dtype=torch.int64)
+    cand = torch.where(vals == segmin[seg], pos, torch.full_like(pos, vals.shape[0]))
+    first = big.scatter_reduce(0, seg, cand, reduce="amin", include_self=True)
+    return segmin, first
+
+
+def moead_replace(pop_obj, off_obj, w, z, z_max, agg, rev):
+    """Exact parallel form of the reference's sequential replacement scan.
+
+    Returns (winner offspring index per slot or −1, new objective matrix)."""
+    rowptr, rev_slot, rev_owner = rev
+    n = pop_obj.shape[0]
+    f_old = agg(pop_obj, w, z, z_max)
+    f_new = agg(off_obj[rev_owner], w[rev_slot], z, z_max)
+    segmin, first = first_argmin_segments(f_new, rev_slot, n)
+    better = segmin < f_old
+    has = first < f_new.shape[0]
+    win = torch.where(better & has, rev_owner[first.clamp_max(f_new.shape[0] - 1)], torch.full_like(first, -1))
+    new_obj = torch.where((win >= 0)[:, None], off_obj[win.clamp_min(0)], pop_obj)
+    return win, new_obj
+
+
+class MOEAD(Algorithm):
+    def __init__(self, lb, ub, n_objs, pop_size, func_name="pbi", mutation_op=None, crossover_op=None):
+        super().__init__()
+        self.lb, self.ub = lb, ub
+        self.n_objs = n_objs
+        self.dim = lb.shape[0]
+        self.pop_size = pop_size
+        self.func_name = func_name
+        self.n_neighbor = 0
+        self.mutation = mutation_op if mutation_op is not None else mutation.Polynomial((lb, ub))
+        self.crossover = crossover_op if crossover_op is not None else crossover.SimulatedBinary(type=2)
+        self.sample = UniformSampling(self.pop_size, self.n_objs)
+        self.aggregate_func = AggregationFunction(self.func_name)
+        self._rev = None
+
+    def setup(self, key):
+        key, k1, k2 = rnd.split(key, 3)
+        dev = self.lb.device
+        w, _ = self.sample(k2)
+        w = w.to(dev)
+        self.pop_size = w.shape[0]
+        self.n_neighbor = int(math.ceil(self.pop_size / 10))
+        pop = rnd.uniform(k1, (self.pop_size, self.dim)).to(dev) * (self.ub - self.lb) + self.lb
+        neighbors = nearest_neighbors(w, self.n_neighbor)
+        return State(
+            population=pop,
+            fitness=torch.zeros((self.pop_size, self.n_objs), device=dev),
+            next_generation=pop,
+            weight_vector=w,
+            neighbors=neighbors,
+            z=torch.zeros(self.n_objs, device=dev),
+            key=key,
+        )
+
+    def init_ask(self, state):
+        return state.population, state
+
+    def init_tell(self, state, fitness):
+        return state.update(fitness=fitness, z=fitness.min(0).values)
+
+    def _parents(self, state, key):
+        n, T = state.neighbors.shape
+        # independent permutation of every neighbour row; only the first two columns are used
+        perm = torch.argsort(rnd.uniform(key, (n, T)).to(state.neighbors.device), dim=1, stable=True)[:, :2]
+        return torch.gather(state.neighbors, 1, perm)
+
+    def ask(self, state):
+        key, sub, sel_key, mut_key = rnd.split(state.key, 4)
+        parent = self._parents(state, sub)
+        pop = state.population
+        selected = torch.cat([pop[parent[:, 0]], pop[parent[:, 1]]], 0)
+        off = self.crossover(sel_key, selected)
+        off = self.mutation(mut_key, off)
+        off = torch.clamp(off, self.lb, self.ub)
+        return off, state.update(next_generation=off, key=key)
+
+    def _reverse(self, state):
+        if self._rev is None or self._rev[0].device != state.neighbors.device or self._rev[1].shape[0] != state.neighbors.numel():
+            self._rev = reverse_neighbors(state.neighbors)
+        return self._rev
+
+    def tell(self, state, fitness):
+        z = torch.minimum(state.z, fitness.min(0).values)
+        z_max = state.fitness.max(0).values
+        win, new_obj = moead_replace(state.fitness, fitness, state.weight_vector, z, z_max, self.aggregate_func, self._reverse(state))
+        new_pop = torch.where((win >= 0)[:, None], state.next_generation[win.clamp_min(0)], state.population)
+        return state.update(population=new_pop, fitness=new_obj, z=z)
+
+
+def moead_replace_sequential(pop, pop_obj, off, off_obj, w, z, z_max, neighbors, agg):
+    """Literal transcription of the reference scan (test oracle)."""
+    pop, pop_obj = pop.clone(), pop_obj.clone()
+    for i in range(off.shape[0]):
+        idx = neighbors[i]
+        f_old = agg(pop_obj[idx], w[idx], z, z_max)
+        f_new = agg(off_obj[i][None, :], w[idx], z, z_max)
+        upd = f_old > f_new
+        pop[idx[upd]] = off[i]
+        pop_obj[idx[upd]] = off_obj[i]
+    return pop, pop_obj

@@ -1,0 +1,36 @@
+"""Device non-dominated sort (``nds.hip``) and crowding distance."""
+from __future__ import annotations
+
+import torch
+
+from . import _ext
+
+
+def non_dominated_sort(f: torch.Tensor) -> torch.Tensor:
+    f = f.to(torch.float32).contiguous()
+    if f.shape[0] <= 65536 and f.shape[1] <= 8:
+        return _ext.ops().nds(f)
+    from ..operators.selection.non_dominate import _peel
+    from ..utils.common import dominate_relation
+
+    dom = dominate_relation(f, f)
+    return _peel(dom, dom.sum(0).to(torch.int32))
+
+
+def crowding_distance(costs: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+    """Vectorised over objectives: one batched sort of the (m, n) masked keys."""
+    n, m = costs.shape
+    inf = torch.tensor(float("inf"), device=costs.device, dtype=costs.dtype)
+    nvalid = mask.sum()
+    key = torch.where(mask[:, None], costs, inf).T  # (m, n)
+    order = torch.argsort(key, dim=1, stable=True)
+    sc = torch.gather(costs.T, 1, order)
+    last = (nvalid - 1).clamp_min(0)
+    rng = sc.gather(1, last.expand(m, 1)) - sc[:, :1]
+    d = torch.empty((m, n), dtype=costs.dtype, device=costs.device)
+    if n > 2:
+        d.scatter_(1, order[:, 1:-1], (sc[:, 2:] - sc[:, :-2]) / rng)
+    d.scatter_(1, order[:, :1], inf.expand(m, 1))
+    d.scatter_(1, order.gather(1, last.expand(m, 1)), inf.expand(m, 1))
+    dist = d.sum(0)
+    return torch.where(mask, dist, -inf)

@@ -16,3 +16,8 @@ def cec_basic(Z, fid, perm=None, start=0, L=None, sub=None, scale=1.0, Y=None, y
     p = None if perm is None else perm.to(torch.int32).contiguous()
     s = None if sub is None else sub.contiguous()
     return _ext.ops().cec_basic(Z, int(fid), p, int(start), int(L), s, float(scale), Y, int(ystart), int(yperm))
+
+
+def dtlz(X, m, variant):
+    """Fused DTLZ1–4 objectives (``csrc/kernels/mo_problems.hip``), X: (n, d) f32 on GPU."""
+    return _ext.ops().dtlz(X.contiguous(), int(m), int(variant))

@@ -212,3 +212,76 @@ def test_jacobi_warm_start_converges_fast():
     rec = (B * w) @ B.T
     assert ((rec - C1).norm() / C1.norm()).item() < 3e-5
     assert ((B.T @ B - torch.eye(n, dtype=torch.float64)).norm() / math.sqrt(n)).item() < 3e-5
+
+
+@pytest.mark.parametrize("n,type", [(64, 1), (63, 1), (64, 2), (4096, 1)])
+def test_sbx_kernel_matches_cpu(n, type):
+    from evoxmi.operators.crossover import simulated_binary
+
+    x = torch.rand(n, 37, generator=torch.Generator().manual_seed(n))
+    key = rnd.PRNGKey(11)
+    ref = simulated_binary(key, x, 0.9, 20.0, type)
+    out = simulated_binary(key.cuda(), x.cuda(), 0.9, 20.0, type).cpu()
+    assert out.shape == ref.shape
+    assert torch.allclose(out, ref, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("n", [2, 63, 1000])
+def test_pm_kernel_matches_cpu(n):
+    from evoxmi.operators.mutation import polynomial
+
+    x = torch.rand(n, 29, generator=torch.Generator().manual_seed(n)) * 4 - 2
+    lb, ub = -torch.ones(29), torch.ones(29)
+    key = rnd.PRNGKey(5)
+    ref = polynomial(key, x, (lb, ub), 5.0, 20.0)
+    out = polynomial(key.cuda(), x.cuda(), (lb.cuda(), ub.cuda()), 5.0, 20.0).cpu()
+    assert torch.allclose(out, ref, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("n,m", [(1, 2), (100, 2), (1000, 3), (8192, 3), (300, 5)])
+def test_nds_kernel_matches_cpu(n, m):
+    from evoxmi.operators.selection import non_dominated_sort
+
+    f = torch.rand(n, m, generator=torch.Generator().manual_seed(n))
+    if n > 10:
+        f[5] = f[3]  # duplicates are mutually non-dominated
+    ref = non_dominated_sort(f)
+    out = non_dominated_sort(f.cuda()).cpu()
+    assert torch.equal(out.to(torch.int32), ref.to(torch.int32))
+
+
+def test_crowding_gpu_matches_cpu():
+    from evoxmi.operators.selection import crowding_distance
+
+    f = torch.rand(500, 3, generator=torch.Generator().manual_seed(1))
+    mask = torch.rand(500, generator=torch.Generator().manual_seed(2)) < 0.4
+    ref = crowding_distance(f, mask)
+    out = crowding_distance(f.cuda(), mask.cuda()).cpu()
+    fin = torch.isfinite(ref)
+    assert torch.equal(fin, torch.isfinite(out))
+    assert torch.allclose(out[fin], ref[fin], rtol=1e-5, atol=1e-6)
+    assert torch.equal(out[~fin], ref[~fin])
+
+
+@pytest.mark.parametrize("variant", [1, 2, 3, 4])
+@pytest.mark.parametrize("n,d,m", [(7, 7, 3), (1000, 12, 3), (333, 100, 10)])
+def test_dtlz_fused_kernel(variant, n, d, m):
+    from evoxmi.problems.numerical import DTLZ1, DTLZ2, DTLZ3, DTLZ4
+
+    cls = {1: DTLZ1, 2: DTLZ2, 3: DTLZ3, 4: DTLZ4}[variant]
+    p = cls(d=d, m=m)
+    X = torch.rand(n, d, generator=torch.Generator().manual_seed(n + variant))
+    ref, _ = p.evaluate(None, X)
+    out, _ = p.evaluate(None, X.cuda())
+    assert torch.allclose(out.cpu(), ref, rtol=2e-4, atol=1e-4)
+
+
+def test_maf_on_gpu_matches_cpu():
+    from evoxmi.problems.numerical import maf
+
+    X = torch.rand(64, 12, generator=torch.Generator().manual_seed(3))
+    for i in range(1, 16):
+        p = getattr(maf, f"MaF{i}")(d=12, m=3)
+        ref, _ = p.evaluate(None, X)
+        out, _ = p.evaluate(None, X.cuda())
+        assert torch.allclose(out.cpu(), ref, rtol=1e-4, atol=1e-4), i
