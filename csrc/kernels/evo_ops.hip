@@ -76,6 +76,57 @@ int grid_for(int64_t total) {
   return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
 }
 
+
+// Fused DE trial-vector generation (K10) for every DE variant of the zoo.
+// Row i of the output:
+//   m_j   = Σ_k coef[i,k] · P[idx[i,k], j]            (base + F·(sec−prim) + F·Σ±diffs)
+//   x_j   = P[cur[i], j]
+//   t_j   = bin:   (u(i,j) < CR_i || j == jr_i) ? m_j : x_j
+//           exp:   ((j − jr_i) mod d) < L_i     ? m_j : x_j
+//           arith: x_j + CR_i·(m_j − x_j)
+//   repair: clip to [lb, ub] or LSHADE midpoint ((x + bound)/2)
+// u(i,j) is regenerated from the Philox counter i·d + j (same stream as uniform(key,(R,d))).
+// One thread per element, rows laid out contiguously; coef/idx/row params are broadcast
+// loads that stay in L1/L2.  K ≤ 16.
+__global__ void __launch_bounds__(256) de_trial_kernel(const float* __restrict__ P, const int32_t* __restrict__ idx,
+                                                       const float* __restrict__ coef, int K, const int32_t* __restrict__ cur,
+                                                       const int32_t* __restrict__ mode, const float* __restrict__ CR,
+                                                       const int32_t* __restrict__ jr, const int32_t* __restrict__ L,
+                                                       const int64_t* __restrict__ key, const float* __restrict__ lb,
+                                                       const float* __restrict__ ub, int repair, float* __restrict__ out, int R,
+                                                       int d) {
+  const uint32_t k0 = (uint32_t)key[0], k1 = (uint32_t)key[1];
+  const int64_t total = (int64_t)R * d;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int i = (int)(t / d), j = (int)(t - (int64_t)i * d);
+    float m = 0.f;
+    for (int k = 0; k < K; ++k) {
+      const float c = coef[i * K + k];
+      if (c != 0.f) m = fmaf(c, P[(int64_t)idx[i * K + k] * d + j], m);
+    }
+    const float x = P[(int64_t)cur[i] * d + j];
+    const int md = mode[i];
+    float v;
+    if (md == 0) {
+      const float u = evx::u24(word_at((uint64_t)t, k0, k1));
+      v = (u < CR[i] || j == jr[i]) ? m : x;
+    } else if (md == 1) {
+      int pos = j - jr[i];
+      if (pos < 0) pos += d;
+      v = pos < L[i] ? m : x;
+    } else {
+      v = x + CR[i] * (m - x);
+    }
+    if (repair == 1) {
+      v = fminf(fmaxf(v, lb[j]), ub[j]);
+    } else if (repair == 2) {
+      if (v < lb[j]) v = 0.5f * (x + lb[j]);
+      if (v > ub[j]) v = 0.5f * (x + ub[j]);
+    }
+    out[t] = v;
+  }
+}
+
 }  // namespace
 
 void evx_sbx(const float* x, float* out, int n, int d, const int64_t* keys, float pro_c, float dis_c, int type, hipStream_t s) {
@@ -85,4 +136,12 @@ void evx_sbx(const float* x, float* out, int n, int d, const int64_t* keys, floa
 void evx_pm(const float* x, float* out, int n, int d, int nm, const float* lb, const float* ub, const int64_t* keys, float pro_m,
             float dis_m, hipStream_t s) {
   pm_kernel<<<grid_for((int64_t)n * d), 256, 0, s>>>(x, out, n, d, nm, lb, ub, keys, pro_m, dis_m);
+}
+
+void evx_de_trial(const float* P, const int32_t* idx, const float* coef, int K, const int32_t* cur, const int32_t* mode,
+                  const float* CR, const int32_t* jr, const int32_t* L, const int64_t* key, const float* lb, const float* ub,
+                  int repair, float* out, int R, int d, hipStream_t s) {
+  const int64_t total = (int64_t)R * d;
+  const int grid = (int)std::min<int64_t>((total + 255) / 256, 8192);
+  de_trial_kernel<<<grid, 256, 0, s>>>(P, idx, coef, K, cur, mode, CR, jr, L, key, lb, ub, repair, out, R, d);
 }

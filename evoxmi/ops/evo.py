@@ -19,3 +19,46 @@ def polynomial(key, x, lb, ub, pro_m, dis_m):
     lb = lb.to(device=x.device, dtype=torch.float32).expand(d).contiguous()
     ub = ub.to(device=x.device, dtype=torch.float32).expand(d).contiguous()
     return _ext.ops().pm(x.contiguous(), lb, ub, keys, float(pro_m), float(dis_m), int(nm))
+
+
+_CROSS = {"bin": 0, "exp": 1, "arith": 2}
+_REPAIR = {"none": 0, "clip": 1, "midpoint": 2}
+
+
+def de_trial(key, P, idx, coef, cur, mode, CR, jr, L, lb, ub, repair="clip"):
+    """Fused DE trial vectors (``evo_ops.hip: de_trial_kernel``).
+
+    P: (rows, d) candidate matrix (population, or population ∪ archive);
+    idx/coef: (R, K) gather rows and weights of the mutation vector;
+    cur: (R,) target rows; mode: (R,) 0 = bin, 1 = exp, 2 = arith;
+    CR: (R,) crossover rate (arith: recombination weight); jr: (R,) j_rand (bin) or
+    window start (exp); L: (R,) exp window length; ``key`` seeds u(i, j) exactly as
+    ``uniform(key, (R, d))``.  The CPU branch is the numerics oracle.
+    """
+    R, K = idx.shape
+    d = P.shape[1]
+    rep = _REPAIR[repair] if isinstance(repair, str) else int(repair)
+    dev = P.device
+    lb = torch.as_tensor(lb, dtype=torch.float32, device=dev).expand(d).contiguous()
+    ub = torch.as_tensor(ub, dtype=torch.float32, device=dev).expand(d).contiguous()
+    if P.is_cuda:
+        i32 = lambda t: t.to(device=dev, dtype=torch.int32).contiguous()
+        f32 = lambda t: t.to(device=dev, dtype=torch.float32).contiguous()
+        return _ext.ops().de_trial(P.contiguous(), i32(idx), f32(coef), i32(cur), i32(mode), f32(CR), i32(jr), i32(L),
+                                   key.contiguous(), lb, ub, rep)
+    m = torch.einsum("rk,rkd->rd", coef.to(P.dtype), P[idx.long()])
+    x = P[cur.long()]
+    j = torch.arange(d, device=dev)[None, :]
+    u = rnd.uniform(key, (R, d))
+    bin_mask = (u < CR[:, None]) | (j == jr[:, None])
+    pos = (j - jr[:, None]) % d
+    exp_mask = pos < L[:, None]
+    mode = mode[:, None]
+    v = torch.where(mode == 0, torch.where(bin_mask, m, x),
+                    torch.where(mode == 1, torch.where(exp_mask, m, x), x + CR[:, None] * (m - x)))
+    if rep == 1:
+        v = torch.minimum(torch.maximum(v, lb), ub)
+    elif rep == 2:
+        v = torch.where(v < lb, 0.5 * (x + lb), v)
+        v = torch.where(v > ub, 0.5 * (x + ub), v)
+    return v

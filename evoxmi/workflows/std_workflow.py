@@ -239,7 +239,11 @@ class StdWorkflow(Workflow):
                 # a foreign state (e.g. restored checkpoint): load it into the static buffers
                 for a, b in zip(tree_flatten(static)[0], tree_flatten(state)[0]):
                     if isinstance(a, torch.Tensor):
-                        a.copy_(b)
+                        if isinstance(b, torch.Tensor):
+                            if b.data_ptr() != a.data_ptr():
+                                a.copy_(b)
+                        else:  # e.g. a harness writing progress=0.3 into a tensor field
+                            a.fill_(b)
         self._graph.replay()
         gen = state.generation + 1
         out = static.update(generation=gen)

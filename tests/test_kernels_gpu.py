@@ -285,3 +285,52 @@ def test_maf_on_gpu_matches_cpu():
         ref, _ = p.evaluate(None, X)
         out, _ = p.evaluate(None, X.cuda())
         assert torch.allclose(out.cpu(), ref, rtol=1e-4, atol=1e-4), i
+
+
+@pytest.mark.parametrize("R,d,K", [(1, 1, 1), (100, 20, 6), (3000, 257, 9), (64, 1000, 16)])
+def test_de_trial_kernel(R, d, K):
+    from evoxmi.ops.evo import de_trial
+
+    g = torch.Generator().manual_seed(R + d)
+    rows = 2 * R + 3
+    P = torch.randn(rows, d, generator=g) * 50
+    idx = torch.randint(0, rows, (R, K), generator=g)
+    coef = torch.randn(R, K, generator=g)
+    coef[coef.abs() < 0.3] = 0
+    cur = torch.randint(0, rows, (R,), generator=g)
+    mode = torch.randint(0, 3, (R,), generator=g)
+    CR = torch.rand(R, generator=g)
+    jr = torch.randint(0, d, (R,), generator=g)
+    L = torch.randint(0, d, (R,), generator=g)
+    lb, ub = torch.full((d,), -60.0), torch.full((d,), 60.0)
+    key = rnd.PRNGKey(R)
+    for rep in ("clip", "midpoint", "none"):
+        ref = de_trial(key, P, idx, coef, cur, mode, CR, jr, L, lb, ub, rep)
+        c = lambda t: t.cuda()
+        out = de_trial(c(key), c(P), c(idx), c(coef), c(cur), c(mode), c(CR), c(jr), c(L), c(lb), c(ub), rep).cpu()
+        assert torch.allclose(out, ref, rtol=1e-5, atol=1e-3), rep
+
+
+@pytest.mark.parametrize("name", ["DE", "ODE", "CoDE", "JaDE", "SaDE", "SHADE", "LSHADE", "ILSHADE", "JSO", "LSHADE_RSP", "EPSDE", "EVDE"])
+def test_de_variants_graph_matches_eager(name):
+    """A DE generation captured in a hipGraph replays to the same state as eager."""
+    from evoxmi.algorithms import de_variants as dv
+    from evoxmi.problems.numerical import CEC2022TestSuit
+    from evoxmi.workflows import StdWorkflow
+
+    D = 10
+    lb, ub = torch.full((D,), -100.0, device="cuda"), torch.full((D,), 100.0, device="cuda")
+    outs = []
+    for graph in (False, True):
+        algo = getattr(dv, name)(lb=lb, ub=ub, pop_size=100)
+        wf = StdWorkflow(algo, CEC2022TestSuit.create(1), graph=graph)
+        st = wf.init(rnd.PRNGKey(7, device="cuda"))
+        for i in range(6):
+            st = wf.step(st)
+            a = st.get_child_state("algorithm")
+            if "progress" in a.keys():
+                st = st.update_child("algorithm", a.update(progress=(i + 1) / 10))
+        outs.append(st.get_child_state("algorithm").fitness.clone())
+    fin = torch.isfinite(outs[0])
+    assert torch.equal(fin, torch.isfinite(outs[1]))
+    assert torch.allclose(outs[0][fin], outs[1][fin], rtol=1e-5, atol=1e-4)

@@ -9,6 +9,9 @@ timeout -k 10 600 python -m pytest tests -x -q -m gpu ${PYTEST_ARGS} > gpurun_ou
 rc=$?
 tail -25 gpurun_out/pytest_gpu.log
 [ $rc -ne 0 ] && [ $rc -ne 5 ] && exit $rc
+echo "== smoke"
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -30 gpurun_out/smoke.log; exit 1; }
+tail -2 gpurun_out/smoke.log
 echo "== bench"
 timeout -k 10 300 python bench.py --steps ${STEPS:-20} --warmup ${WARMUP:-3} ${BENCH_ARGS} > gpurun_out/bench.log 2>&1 || { tail -30 gpurun_out/bench.log; exit 1; }
 cat gpurun_out/bench.log | tail -3
