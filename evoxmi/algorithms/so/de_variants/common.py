@@ -145,7 +145,7 @@ def diff_choices(key, cur, P: int, population, reduced=None, archive=None, rank_
         ranks = torch.argsort(torch.argsort(fitness, stable=True), stable=True)
         w = rank_k * (N - ranks).to(torch.float32) + 1
         kth = torch.clamp(N - _t(red, dev, torch.int64), 0, N - 1)
-        nth = torch.sort(w).values[kth]
+        nth = torch.sort(w).values.gather(0, kth.reshape(1))
         w = torch.where(w < nth, torch.zeros_like(w), w)
         logp = torch.log(w / w.sum())
         g = rnd.gumbel(key, (R, N)).to(dev) + logp[None, :]

@@ -127,7 +127,7 @@ class LSHADE(Algorithm):
         mv = C.move_n_small(fit, red)
         moved_fit = torch.where(live, fit[mv], torch.full_like(fit, float("inf")))
         moved_pop = torch.where(live[:, None], pop[mv], torch.full_like(pop, float("nan")))
-        worst = pop[torch.argmax(torch.where(torch.isnan(fit), torch.full_like(fit, -float("inf")), fit))]
+        worst = pop.index_select(0, torch.argmax(torch.where(torch.isnan(fit), torch.full_like(fit, -float("inf")), fit)).reshape(1))[0]
         # success-history memories
         ok = tfit < state.fitness
         nan = torch.full_like(tfit, float("nan"))
@@ -174,9 +174,7 @@ class ILSHADE(LSHADE):
         return (lehmer + old_slot0) / 2
 
     def _pin(self, mem):
-        mem = mem.clone()
-        mem[self.H - 1] = 0.9
-        return mem
+        return torch.cat([mem[: self.H - 1], torch.full_like(mem[:1], 0.9)])
 
     def _p_next(self, progress):
         return self.p_min + (self.p_max - self.p_min) * progress

@@ -44,7 +44,7 @@ class ODE(DE):
         strat = (b, b, self.num_difference_vectors, C.BIN)
         de_trials, _ = C.generate_trials(k_tr, pop, state.fitness, state.best_index, cur, strat, self.differential_weight,
                                          self.cross_probability, 0, self.lb, self.ub, choices=ch)
-        base = pop[state.best_index].expand(cur.shape[0], -1) if self.base_vector == "best" else pop[ch[:, 0]]
+        base = pop.index_select(0, state.best_index.reshape(1)).expand(cur.shape[0], -1) if self.base_vector == "best" else pop[ch[:, 0]]
         opposite = self.ub + self.lb - base
         trials = torch.where(state.counter % 2 == 0, de_trials, opposite)
         return trials, state.update(trial_vectors=trials, key=key)
