@@ -281,8 +281,9 @@ at::Tensor dtlz(const at::Tensor& X, int64_t m, int64_t variant) {
 
 at::Tensor de_trial(const at::Tensor& P, const at::Tensor& idx, const at::Tensor& coef, const at::Tensor& cur, const at::Tensor& mode,
                     const at::Tensor& CR, const at::Tensor& jr, const at::Tensor& L, const at::Tensor& key, const at::Tensor& lb,
-                    const at::Tensor& ub, int64_t repair) {
+                    const at::Tensor& ub, int64_t repair, const at::Tensor& err) {
   CHECK_DEV(P); CHECK_F32(P); CHECK_CONTIG(P);
+  TORCH_CHECK(err.is_cuda() && err.scalar_type() == at::kInt && err.numel() >= 1, "de_trial: err must be int32[1] on the device");
   TORCH_CHECK(P.dim() == 2, "de_trial: P must be (rows, d)");
   const int64_t R = idx.size(0), K = idx.size(1), d = P.size(1);
   TORCH_CHECK(K >= 1 && K <= 16, "de_trial: 1 <= K <= 16");
@@ -301,7 +302,7 @@ at::Tensor de_trial(const at::Tensor& P, const at::Tensor& idx, const at::Tensor
   if (R > 0 && d > 0)
     evx_de_trial(P.data_ptr<float>(), i32(idx, R * K, "idx"), f32(coef, R * K, "coef"), (int)K, i32(cur, R, "cur"), i32(mode, R, "mode"),
                  f32(CR, R, "CR"), i32(jr, R, "jr"), i32(L, R, "L"), key.data_ptr<int64_t>(), f32(lb, d, "lb"), f32(ub, d, "ub"), (int)repair,
-                 out.data_ptr<float>(), (int)R, (int)d, cur_stream());
+                 out.data_ptr<float>(), (int)R, (int)d, (int)P.size(0), err.data_ptr<int>(), cur_stream());
   return out;
 }
 
@@ -318,7 +319,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("sbx(Tensor x, Tensor keys, float pro_c, float dis_c, int type) -> Tensor");
   m.def("pm(Tensor x, Tensor lb, Tensor ub, Tensor keys, float pro_m, float dis_m, int nm) -> Tensor");
   m.def("nds(Tensor f) -> Tensor");
-  m.def("de_trial(Tensor P, Tensor idx, Tensor coef, Tensor cur, Tensor mode, Tensor CR, Tensor jr, Tensor L, Tensor key, Tensor lb, Tensor ub, int repair) -> Tensor");
+  m.def("de_trial(Tensor P, Tensor idx, Tensor coef, Tensor cur, Tensor mode, Tensor CR, Tensor jr, Tensor L, Tensor key, Tensor lb, Tensor ub, int repair, Tensor err) -> Tensor");
   m.def("dtlz(Tensor X, int m, int variant) -> Tensor");
   m.def("classic_eval(Tensor X, int func, float a, float b, float c) -> Tensor");
   m.def("gemm_f32(Tensor A, int a_rc, Tensor? a_gather, Tensor? a_sub, int a_sub_on_k, Tensor? a_kscale, Tensor? a_kw, Tensor? a_sscale, int a_sscale_inv, Tensor B, int b_rc, Tensor? b_gather, Tensor? b_sub, int b_sub_on_k, Tensor? b_kscale, Tensor? b_kw, Tensor? b_sscale, int b_sscale_inv, Tensor? alpha_ptr, Tensor? bias_n, float beta, Tensor? Cin, int M, int N, int K, int splits, float alpha) -> Tensor");

@@ -43,5 +43,5 @@ void evx_pm(const float* x, float* out, int n, int d, int nm, const float* lb, c
 void evx_dtlz(const float* X, float* F, int N, int D, int M, int variant, hipStream_t s);
 void evx_de_trial(const float* P, const int32_t* idx, const float* coef, int K, const int32_t* cur, const int32_t* mode,
                   const float* CR, const int32_t* jr, const int32_t* L, const int64_t* key, const float* lb, const float* ub,
-                  int repair, float* out, int R, int d, hipStream_t s);
+                  int repair, float* out, int R, int d, int rows, int* err, hipStream_t s);
 void evx_nds(const float* f, int n, int m, uint32_t* DT, int32_t* rank, int32_t* cnt, hipStream_t s);

@@ -94,7 +94,7 @@ __global__ void __launch_bounds__(256) de_trial_kernel(const float* __restrict__
                                                        const int32_t* __restrict__ jr, const int32_t* __restrict__ L,
                                                        const int64_t* __restrict__ key, const float* __restrict__ lb,
                                                        const float* __restrict__ ub, int repair, float* __restrict__ out, int R,
-                                                       int d) {
+                                                       int d, int rows, int* __restrict__ err) {
   const uint32_t k0 = (uint32_t)key[0], k1 = (uint32_t)key[1];
   const int64_t total = (int64_t)R * d;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
@@ -102,9 +102,19 @@ __global__ void __launch_bounds__(256) de_trial_kernel(const float* __restrict__
     float m = 0.f;
     for (int k = 0; k < K; ++k) {
       const float c = coef[i * K + k];
-      if (c != 0.f) m = fmaf(c, P[(int64_t)idx[i * K + k] * d + j], m);
+      const int r = idx[i * K + k];
+      if ((unsigned)r >= (unsigned)rows) {  // never dereference a bad row: flag it and skip
+        if (j == 0) atomicOr(err, 1);
+        continue;
+      }
+      if (c != 0.f) m = fmaf(c, P[(int64_t)r * d + j], m);
     }
-    const float x = P[(int64_t)cur[i] * d + j];
+    int rc = cur[i];
+    if ((unsigned)rc >= (unsigned)rows) {
+      if (j == 0) atomicOr(err, 2);
+      rc = 0;
+    }
+    const float x = P[(int64_t)rc * d + j];
     const int md = mode[i];
     float v;
     if (md == 0) {
@@ -140,8 +150,8 @@ void evx_pm(const float* x, float* out, int n, int d, int nm, const float* lb, c
 
 void evx_de_trial(const float* P, const int32_t* idx, const float* coef, int K, const int32_t* cur, const int32_t* mode,
                   const float* CR, const int32_t* jr, const int32_t* L, const int64_t* key, const float* lb, const float* ub,
-                  int repair, float* out, int R, int d, hipStream_t s) {
+                  int repair, float* out, int R, int d, int rows, int* err, hipStream_t s) {
   const int64_t total = (int64_t)R * d;
   const int grid = (int)std::min<int64_t>((total + 255) / 256, 8192);
-  de_trial_kernel<<<grid, 256, 0, s>>>(P, idx, coef, K, cur, mode, CR, jr, L, key, lb, ub, repair, out, R, d);
+  de_trial_kernel<<<grid, 256, 0, s>>>(P, idx, coef, K, cur, mode, CR, jr, L, key, lb, ub, repair, out, R, d, rows, err);
 }

@@ -27,6 +27,8 @@ from typing import Optional, Union
 
 import torch
 
+from evoxmi.ops.sort import topk as _topk
+
 from ....core import State
 from ....ops import evo as evo_ops
 from ....ops import random as rnd
@@ -149,7 +151,7 @@ def diff_choices(key, cur, P: int, population, reduced=None, archive=None, rank_
         w = torch.where(w < nth, torch.zeros_like(w), w)
         logp = torch.log(w / w.sum())
         g = rnd.gumbel(key, (R, N)).to(dev) + logp[None, :]
-        choice = torch.topk(g, min(P, N), dim=1).indices
+        choice = _topk(g, min(P, N), dim=1)[1]
         return _remap_self(choice, cur, red), population
     if archive is None:
         choice = sample_distinct(key, R, P, N, red, dev)

@@ -14,6 +14,8 @@ import math
 
 import torch
 
+from evoxmi.ops.sort import topk as _topk
+
 from ...ops import random as rnd
 
 
@@ -131,7 +133,7 @@ def batched_de_diff_sum_rank(key, diff_padding_num: int, num_diff_vects, populat
     w = torch.where(w < nth, torch.zeros_like(w), w)
     logp = torch.log(w / w.sum())
     g = rnd.gumbel(key, (N, N)).to(population.device) + logp[None, :]
-    choice = torch.topk(g, diff_padding_num, dim=1).indices
+    choice = _topk(g, diff_padding_num, dim=1)[1]
     index = torch.arange(N, device=population.device)[:, None]
     choice = torch.where(choice == index, torch.full_like(choice, P - 1), choice)
     return _signed_sum(population[choice], num_diff_vects), choice[:, 0]

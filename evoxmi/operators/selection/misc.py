@@ -6,6 +6,8 @@ from typing import Callable
 
 import torch
 
+from evoxmi.ops.sort import topk as _topk
+
 from ...ops import random as rnd
 from ...utils.common import cos_dist
 
@@ -72,7 +74,7 @@ class Tournament:
 
 
 def topk_fit(population, fitness, topk):
-    v, i = torch.topk(fitness, topk, largest=False, sorted=True)
+    v, i = _topk(fitness, topk, largest=False)
     return population[i], v
 
 

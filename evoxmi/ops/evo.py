@@ -1,6 +1,8 @@
 """Device launchers of the fused variation operators (``evo_ops.hip``)."""
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _ext
@@ -22,6 +24,23 @@ def polynomial(key, x, lb, ub, pro_m, dis_m):
 
 
 _CROSS = {"bin": 0, "exp": 1, "arith": 2}
+_DEBUG = os.environ.get("EVOXMI_DEBUG", "0") == "1"
+_ERR = {}
+
+
+def _err_flag(dev):
+    """Sticky device flag the index-checking kernels OR their errors into (read it with
+    ``kernel_error_flags()``; with EVOXMI_DEBUG=1 every launch checks it synchronously)."""
+    if dev not in _ERR:
+        _ERR[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
+    return _ERR[dev]
+
+
+def kernel_error_flags(device="cuda") -> int:
+    v = 0
+    for f in _ERR.values():
+        v |= int(f.item())
+    return v
 _REPAIR = {"none": 0, "clip": 1, "midpoint": 2}
 
 
@@ -44,8 +63,15 @@ def de_trial(key, P, idx, coef, cur, mode, CR, jr, L, lb, ub, repair="clip"):
     if P.is_cuda:
         i32 = lambda t: t.to(device=dev, dtype=torch.int32).contiguous()
         f32 = lambda t: t.to(device=dev, dtype=torch.float32).contiguous()
-        return _ext.ops().de_trial(P.contiguous(), i32(idx), f32(coef), i32(cur), i32(mode), f32(CR), i32(jr), i32(L),
-                                   key.contiguous(), lb, ub, rep)
+        err = _err_flag(dev)
+        out = _ext.ops().de_trial(P.contiguous(), i32(idx), f32(coef), i32(cur), i32(mode), f32(CR), i32(jr), i32(L),
+                                  key.contiguous(), lb, ub, rep, err)
+        if _DEBUG and not torch.cuda.is_current_stream_capturing():
+            bad = int(err.item())
+            if bad:
+                raise RuntimeError(f"de_trial: out-of-range row index (flag {bad}); idx range "
+                                   f"[{int(idx.min())}, {int(idx.max())}], cur range [{int(cur.min())}, {int(cur.max())}], rows {P.shape[0]}")
+        return out
     m = torch.einsum("rk,rkd->rd", coef.to(P.dtype), P[idx.long()])
     x = P[cur.long()]
     j = torch.arange(d, device=dev)[None, :]

@@ -232,6 +232,12 @@ def batched_permutation(key, rows: int, n: int) -> torch.Tensor:
     return torch.argsort(uniform(key, (rows, n)), dim=1, stable=True)
 
 
+def _topk(x, k, dim=-1, largest=True):
+    from .sort import topk
+
+    return topk(x, k, dim, largest)
+
+
 def choice(key, a: Union[int, torch.Tensor], shape=(), replace: bool = True, p=None, axis: int = 0) -> torch.Tensor:
     """Sample from ``a`` (int ⇒ ``range(a)``), optionally weighted by ``p``."""
     shape = _as_shape(shape)
@@ -253,7 +259,7 @@ def choice(key, a: Union[int, torch.Tensor], shape=(), replace: bool = True, p=N
             idx = torch.searchsorted(cdf, u).clamp_max(n - 1)
         else:
             g = gumbel(key, (n,)) + torch.log(p)
-            idx = torch.topk(g, m).indices
+            idx = _topk(g, m)[1]
     idx = idx.reshape(shape)
     if isinstance(a, int):
         return idx

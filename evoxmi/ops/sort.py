@@ -25,3 +25,30 @@ def argsort_i32(keys: torch.Tensor):
         return _ext.ops().argsort_f32(keys.contiguous(), 0)
     v, i = torch.sort(keys, stable=True)
     return v, i.to(torch.int32)
+
+
+def topk(x: torch.Tensor, k: int, dim: int = -1, largest: bool = True):
+    """hipGraph-capture-safe top-k → (values, indices), sorted.
+
+    ``torch.topk`` on ROCm returns corrupted indices when replayed from a captured
+    hipGraph (observed on MI355X / torch 2.10+rocm7.0: the index buffer aliases a
+    float workspace), so every capturable code path uses this instead: k rounds of
+    arg-max with masking for small k, a stable argsort otherwise.
+    """
+    if dim != -1 and dim != x.ndim - 1:
+        v, i = topk(x.transpose(dim, -1), k, -1, largest)
+        return v.transpose(dim, -1), i.transpose(dim, -1)
+    n = x.shape[-1]
+    k = min(k, n)
+    if k <= 8:
+        work = x.clone() if largest else -x
+        fill = float("-inf") if work.is_floating_point() else torch.iinfo(work.dtype).min
+        idx = []
+        for _ in range(k):
+            j = torch.argmax(work, dim=-1, keepdim=True)
+            idx.append(j)
+            work.scatter_(-1, j, fill)
+        ind = torch.cat(idx, -1)
+    else:
+        ind = torch.argsort(x, dim=-1, descending=largest, stable=True)[..., :k]
+    return torch.gather(x, -1, ind), ind

@@ -1,0 +1,126 @@
+"""Time-budgeted DE harness on CEC2022 (parity with the reference fork's ``run/run_de.py``).
+
+For every function of the suite and every independent run, the optimiser runs until
+``--max-time`` seconds have elapsed; after each generation the elapsed fraction is
+injected into the algorithm state as ``progress`` (and the step count as ``iter``),
+which drives the L-SHADE-family schedules (reference ``run/run_de.py:74-94``).
+Results are appended to ``<out>/result_de.txt`` (best fitness of runs 2..R and the
+FE count) and ``<out>/result_de_history.txt`` (best-so-far history of the median run,
+``--samples`` points).
+
+MI355X-specific: with ``--graph`` (default on a GPU) each generation is one hipGraph
+replay; the best-so-far value is read back only every ``--sync-every`` generations so
+the host never stalls the queue for the time check.
+
+Example: ``python run/run_de.py --algo LSHADE --dim 20 --pop 100 --runs 4 --max-time 5``
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+
+def sample_history(num_samples, hist):
+    if not hist:
+        return []
+    n = len(hist)
+    idx = [int(i * (n - 1) / max(num_samples - 1, 1)) for i in range(num_samples)]
+    return [hist[i] for i in idx]
+
+
+def main(argv=None):
+    from evoxmi import random as rnd
+    from evoxmi.algorithms import de_variants
+    from evoxmi.monitors import EvalMonitor
+    from evoxmi.problems.numerical import CEC2022TestSuit
+    from evoxmi.workflows import StdWorkflow
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--algo", default="EVDE", choices=de_variants.__all__)
+    ap.add_argument("--funcs", default="1-12")
+    ap.add_argument("--dim", type=int, default=20)
+    ap.add_argument("--pop", type=int, default=100)
+    ap.add_argument("--runs", type=int, default=32)
+    ap.add_argument("--max-time", type=float, default=60.0)
+    ap.add_argument("--max-steps", type=int, default=9999999)
+    ap.add_argument("--samples", type=int, default=100)
+    ap.add_argument("--sync-every", type=int, default=10)
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--out", default="run")
+    ap.add_argument("--device", default="cuda" if torch.cuda.is_available() else "cpu")
+    ap.add_argument("--no-graph", action="store_true")
+    args = ap.parse_args(argv)
+
+    a, _, b = args.funcs.partition("-")
+    funcs = list(range(int(a), int(b or a) + 1))
+    dev = torch.device(args.device)
+    graph = dev.type == "cuda" and not args.no_graph
+    D = args.dim
+    lb, ub = torch.full((D,), -100.0, device=dev), torch.full((D,), 100.0, device=dev)
+    os.makedirs(args.out, exist_ok=True)
+    res_path, hist_path = os.path.join(args.out, "result_de.txt"), os.path.join(args.out, "result_de_history.txt")
+    header = f"Problem_Dim: {D}, Time: {args.max_time}, Optimizer: {args.algo}, Popsize: {args.pop}, Iters: {args.max_steps}\n\n"
+    for pth in (res_path, hist_path):
+        with open(pth, "w") as f:
+            f.write(header)
+    key = rnd.PRNGKey(args.seed, device=dev)
+    for fn in funcs:
+        problem = CEC2022TestSuit.create(fn)
+        name = type(problem).__name__
+        print(name, flush=True)
+        with open(res_path, "a") as f:
+            f.write(f"{name}  ")
+        with open(hist_path, "a") as f:
+            f.write(f"{name}  ")
+        best_all, hist_all = [], []
+        steps = 0
+        for run in range(args.runs):
+            algo = getattr(de_variants, args.algo)(lb=lb, ub=ub, pop_size=args.pop)
+            mon = EvalMonitor(full_fit_history=False)
+            wf = StdWorkflow(algo, problem, monitors=[mon], graph=graph)
+            key, sub = rnd.split(key)
+            state = wf.init(sub)
+            hist = []
+            t0 = time.time()
+            for i in range(args.max_steps):
+                state = wf.step(state)
+                steps = i
+                if i % args.sync_every == 0 or i == args.max_steps - 1:
+                    hist.append(float(mon.get_best_fitness()))
+                elapsed = time.time() - t0
+                alg = state.get_child_state("algorithm")
+                upd = {}
+                if "progress" in alg.keys():
+                    upd["progress"] = elapsed / args.max_time
+                if "iter" in alg.keys() and not isinstance(alg.iter, torch.Tensor):
+                    upd["iter"] = i
+                if upd:
+                    state = state.update_child("algorithm", alg.update(**upd))
+                if elapsed >= args.max_time:
+                    break
+            if dev.type == "cuda":
+                torch.cuda.synchronize()
+            best = float(mon.get_best_fitness())
+            hist.append(best)
+            print(f"min fitness: {best}\nSteps: {steps} Runs: {run}\nTime: {time.time() - t0:.3f} s\n", flush=True)
+            if run >= 1 or args.runs == 1:
+                best_all.append(best)
+                hist_all.append(sample_history(args.samples, hist))
+                with open(res_path, "a") as f:
+                    f.write(f"{best} ")
+        with open(res_path, "a") as f:
+            f.write(f"{steps * args.pop}\n")
+        order = sorted(range(len(best_all)), key=lambda k: best_all[k])
+        med = order[len(order) // 2]
+        with open(hist_path, "a") as f:
+            f.write(f"{hist_all[med]}\n")
+
+
+if __name__ == "__main__":
+    main()

@@ -334,3 +334,24 @@ def test_de_variants_graph_matches_eager(name):
     fin = torch.isfinite(outs[0])
     assert torch.equal(fin, torch.isfinite(outs[1]))
     assert torch.allclose(outs[0][fin], outs[1][fin], rtol=1e-5, atol=1e-4)
+
+
+def test_topk_safe_under_graph_capture():
+    """ops.sort.topk replayed from a hipGraph matches torch.topk on the CPU."""
+    from evoxmi.ops.sort import topk
+
+    x = torch.randn(500, 3000, device="cuda")
+    out_i = torch.empty((500, 3), dtype=torch.int64, device="cuda")
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        topk(x, 3)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        out_i.copy_(topk(x, 3)[1])
+    for seed in range(3):
+        x.copy_(torch.randn(500, 3000, generator=torch.Generator().manual_seed(seed)).cuda())
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out_i.cpu(), torch.topk(x.cpu(), 3).indices)
