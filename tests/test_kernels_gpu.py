@@ -355,3 +355,41 @@ def test_topk_safe_under_graph_capture():
         g.replay()
         torch.cuda.synchronize()
         assert torch.equal(out_i.cpu(), torch.topk(x.cpu(), 3).indices)
+
+
+ES_GRAPH = ["OpenES", "PGPE", "SNES", "DES", "ARS", "ESMC", "CR_FM_NES", "PersistentES", "NoiseReuseES", "SeparableNES",
+            "MAES", "LMMAES", "RMES", "AMaLGaM", "IndependentAMaLGaM", "SepCMAES", "LES"]
+
+
+@pytest.mark.parametrize("name", ES_GRAPH)
+def test_es_variants_graph_matches_eager(name):
+    import evoxmi.algorithms as A
+    from evoxmi.problems.numerical import Sphere
+    from evoxmi.workflows import StdWorkflow
+    import warnings
+
+    mean = torch.tensor([5.0, -10, 15, -20, 25, 1, 2, 3], device="cuda")
+    mk = {
+        "OpenES": lambda: A.OpenES(mean, 64, learning_rate=1, noise_stdev=3, optimizer="adam"),
+        "PGPE": lambda: A.PGPE(64, mean, optimizer="clipup", stdev_init=3.0),
+        "SNES": lambda: A.SNES(64, mean, sigma=3.0), "DES": lambda: A.DES(64, mean, sigma_init=3.0),
+        "ARS": lambda: A.ARS(64, mean, lr=0.5, sigma=1.0), "ESMC": lambda: A.ESMC(65, mean, lr=0.5, sigma=1.0),
+        "CR_FM_NES": lambda: A.CR_FM_NES(64, mean, sigma=3.0), "PersistentES": lambda: A.PersistentES(64, mean, lr=0.5),
+        "NoiseReuseES": lambda: A.NoiseReuseES(64, mean, lr=0.5),
+        "SeparableNES": lambda: A.SeparableNES(mean, torch.ones(8, device="cuda") * 3, pop_size=64),
+        "MAES": lambda: A.MAES(mean, init_stdev=1.0, pop_size=20), "LMMAES": lambda: A.LMMAES(mean, init_stdev=1.0, pop_size=20),
+        "RMES": lambda: A.RMES(mean, init_stdev=1.0, pop_size=20), "AMaLGaM": lambda: A.AMaLGaM(mean, init_stdev=1.0, pop_size=20),
+        "IndependentAMaLGaM": lambda: A.IndependentAMaLGaM(mean, init_stdev=1.0, pop_size=20),
+        "SepCMAES": lambda: A.SepCMAES(mean, init_stdev=1.0, pop_size=20), "LES": lambda: A.LES(64, mean, sigma_init=3.0),
+    }[name]
+    outs = []
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        for graph in (False, True):
+            wf = StdWorkflow(mk(), Sphere(), graph=graph)
+            st = wf.init(rnd.PRNGKey(3, device="cuda"))
+            for _ in range(6):
+                st = wf.step(st)
+            a = st.get_child_state("algorithm")
+            outs.append((a.center if "center" in a.keys() else a.mean).clone())
+    assert torch.allclose(outs[0], outs[1], rtol=1e-4, atol=1e-4)

@@ -125,3 +125,58 @@ def test_sade_cr_memory_parallel_matches_sequential():
     out = _cr_memory_update(mem, sid, ok, CRs)
     assert torch.equal(torch.isnan(out), torch.isnan(ref))
     assert torch.equal(out[~torch.isnan(out)], ref[~torch.isnan(ref)])
+
+
+# ---------------------------------------------------------------- ES zoo
+from evoxmi.algorithms import (  # noqa: E402
+    ARS, ASEBO, CR_FM_NES, DES, ESMC, LES, LMMAES, MAES, PGPE, RMES, SNES, XNES, AMaLGaM, GuidedES, IndependentAMaLGaM,
+    NoiseReuseES, OpenES, PersistentES, SeparableNES,
+)
+
+
+def test_xnes():
+    assert run_single_objective_algorithm(XNES(MEAN, torch.eye(5) * 2, pop_size=100)) < 0.1
+
+
+@pytest.mark.parametrize("optimizer", ["adam", "clipup"])
+def test_pgpe(optimizer):
+    algo = PGPE(100, MEAN, optimizer=optimizer, center_learning_rate=0.3, stdev_init=10, stdev_learning_rate=0.2)
+    assert run_single_objective_algorithm(algo, fitness_shaping=True) < 0.1
+
+
+@pytest.mark.parametrize("optimizer", ["adam", None])
+def test_openes(optimizer):
+    algo = OpenES(MEAN, 100, learning_rate=1, noise_stdev=3, optimizer=optimizer, mirrored_sampling=True)
+    assert run_single_objective_algorithm(algo, fitness_shaping=True, num_iter=1000) < 1
+
+
+ES_CASES = {
+    "SeparableNES": (lambda: SeparableNES(MEAN, torch.ones(5) * 3, pop_size=100), 0.1),
+    "MAES": (lambda: MAES(MEAN, init_stdev=1.0, pop_size=20), 0.1),
+    "LMMAES": (lambda: LMMAES(MEAN, init_stdev=1.0, pop_size=20), 0.1),
+    "RMES": (lambda: RMES(MEAN, init_stdev=1.0, pop_size=20), 0.1),
+    "AMaLGaM": (lambda: AMaLGaM(MEAN, init_stdev=1.0, pop_size=20), 0.1),
+    "IndependentAMaLGaM": (lambda: IndependentAMaLGaM(MEAN, init_stdev=1.0, pop_size=20), 0.1),
+    "SNES": (lambda: SNES(100, MEAN, sigma=3.0), 0.1),
+    "DES": (lambda: DES(100, MEAN, sigma_init=3.0), 0.1),
+    "ARS": (lambda: ARS(100, MEAN, lr=0.5, sigma=1.0), 1.0),
+    "ESMC": (lambda: ESMC(101, MEAN, lr=0.5, sigma=1.0), 1.0),
+    "GuidedES": (lambda: GuidedES(100, MEAN, sigma_init=1.0, lrate_init=0.05), 1.0),
+    "ASEBO": (lambda: ASEBO(100, MEAN, lr=0.5, sigma=1.0, subspace_dims=5), 1.0),
+    "CR_FM_NES": (lambda: CR_FM_NES(100, MEAN, sigma=3.0), 0.1),
+    "PersistentES": (lambda: PersistentES(100, MEAN, lr=0.5, sigma=1.0), 1.0),
+    "NoiseReuseES": (lambda: NoiseReuseES(100, MEAN, lr=0.5, sigma=1.0), 1.0),
+}
+
+
+@pytest.mark.parametrize("name", sorted(ES_CASES))
+def test_es_zoo_sphere(name):
+    mk, thr = ES_CASES[name]
+    assert run_single_objective_algorithm(mk()) < thr
+
+
+def test_les_runs_without_pretrained_params():
+    with pytest.warns(UserWarning):
+        algo = LES(100, MEAN, sigma_init=3.0)
+    f = run_single_objective_algorithm(algo, num_iter=20)
+    assert f == f  # finite / not NaN; no meta-trained weights are available (see les.py)
