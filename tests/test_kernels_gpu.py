@@ -357,7 +357,7 @@ def test_topk_safe_under_graph_capture():
         assert torch.equal(out_i.cpu(), torch.topk(x.cpu(), 3).indices)
 
 
-ES_GRAPH = ["OpenES", "PGPE", "SNES", "DES", "ARS", "ESMC", "CR_FM_NES", "PersistentES", "NoiseReuseES", "SeparableNES",
+ES_GRAPH = ["CSO", "CLPSO", "SLPSOGS", "DMSPSOEL", "FIPS", "SwmmPSO", "FSPSO", "OpenES", "PGPE", "SNES", "DES", "ARS", "ESMC", "CR_FM_NES", "PersistentES", "NoiseReuseES", "SeparableNES",
             "MAES", "LMMAES", "RMES", "AMaLGaM", "IndependentAMaLGaM", "SepCMAES", "LES"]
 
 
@@ -369,7 +369,12 @@ def test_es_variants_graph_matches_eager(name):
     import warnings
 
     mean = torch.tensor([5.0, -10, 15, -20, 25, 1, 2, 3], device="cuda")
+    lb, ub = torch.full((8,), -32.0, device="cuda"), torch.full((8,), 32.0, device="cuda")
     mk = {
+        "CSO": lambda: A.CSO(lb, ub, 64), "SLPSOGS": lambda: A.SLPSOGS(lb, ub, 64, 0.01, 0.7),
+        "CLPSO": lambda: A.CLPSO(lb, ub, 64, 0.5, 1.5, torch.full((64,), 0.05, device="cuda")),
+        "DMSPSOEL": lambda: A.DMSPSOEL(lb, ub, 3, 9, 37, 3, 5, 0.7, 1.5, 1.5, 1.5, 1.5), "FIPS": lambda: A.FIPS(lb, ub, 64),
+        "SwmmPSO": lambda: A.SwmmPSO(lb, ub, 64), "FSPSO": lambda: A.FSPSO(lb, ub, 64),
         "OpenES": lambda: A.OpenES(mean, 64, learning_rate=1, noise_stdev=3, optimizer="adam"),
         "PGPE": lambda: A.PGPE(64, mean, optimizer="clipup", stdev_init=3.0),
         "SNES": lambda: A.SNES(64, mean, sigma=3.0), "DES": lambda: A.DES(64, mean, sigma_init=3.0),
@@ -391,5 +396,6 @@ def test_es_variants_graph_matches_eager(name):
             for _ in range(6):
                 st = wf.step(st)
             a = st.get_child_state("algorithm")
-            outs.append((a.center if "center" in a.keys() else a.mean).clone())
+            k = next(k for k in ("center", "mean", "population") if k in a.keys())
+            outs.append(a[k].clone())
     assert torch.allclose(outs[0], outs[1], rtol=1e-4, atol=1e-4)

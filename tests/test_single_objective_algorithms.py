@@ -180,3 +180,39 @@ def test_les_runs_without_pretrained_params():
         algo = LES(100, MEAN, sigma_init=3.0)
     f = run_single_objective_algorithm(algo, num_iter=20)
     assert f == f  # finite / not NaN; no meta-trained weights are available (see les.py)
+
+
+# ---------------------------------------------------------------- PSO zoo
+from evoxmi.algorithms import CLPSO, CSO, DMSPSOEL, FIPS, FSPSO, SLPSOGS, SLPSOUS, SwmmPSO  # noqa: E402
+from evoxmi.algorithms.so.pso_variants import topology_utils as topo  # noqa: E402
+
+PSO_CASES = {
+    "CSO": (lambda: CSO(LB, UB, 100), 0.1),  # reference test_cso
+    "CLPSO": (lambda: CLPSO(LB, UB, 100, inertia_weight=0.5, const_coefficient=1.5, learning_probability=torch.full((100,), 0.05)), 0.1),
+    "SLPSOGS": (lambda: SLPSOGS(LB, UB, 100, social_influence_factor=0.01, demonstrator_choice_factor=0.7), 0.1),
+    "SLPSOUS": (lambda: SLPSOUS(LB, UB, 100, social_influence_factor=0.01, demonstrator_choice_factor=0.7), 0.1),
+    "DMSPSOEL": (lambda: DMSPSOEL(LB, UB, 3, 9, 73, 5, 200, 0.7, 1.5, 1.5, 1.5, 1.5), 0.1),
+    "FIPS": (lambda: FIPS(LB, UB, 100), 1.0),
+    "SwmmPSO": (lambda: SwmmPSO(LB, UB, 100), 0.1),
+    "FSPSO": (lambda: FSPSO(LB, UB, 100), 0.1),
+}
+
+
+@pytest.mark.parametrize("name", sorted(PSO_CASES))
+def test_pso_zoo_sphere(name):
+    mk, thr = PSO_CASES[name]
+    assert run_single_objective_algorithm(mk()) < thr
+
+
+def test_square_topology_is_von_neumann():
+    adj = topo.get_square_neighbour(torch.zeros(12, 2))  # 3 x 4 grid
+    assert torch.equal(adj, adj.T) and int(adj.sum(1).max()) == 4 and int(adj.sum(1).min()) == 4
+    lst, mask = topo.build_adjacancy_list_from_matrix(adj)
+    assert torch.equal(mask.sum(1), adj.sum(1))
+
+
+def test_knn_circles_topology():
+    pop = torch.randn(30, 3, generator=torch.Generator().manual_seed(0))
+    adj = topo.get_circles_neighbour(rnd.PRNGKey(0), pop, K=2, shortcut=3)
+    assert torch.equal(adj, adj.T) and bool((adj.diag() == 1).all())
+    assert int(adj.sum(1).min()) >= 2
