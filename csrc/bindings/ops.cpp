@@ -306,6 +306,53 @@ at::Tensor de_trial(const at::Tensor& P, const at::Tensor& idx, const at::Tensor
   return out;
 }
 
+std::vector<at::Tensor> moead_scan(const at::Tensor& objs, const at::Tensor& off_objs, const at::Tensor& P, const at::Tensor& W,
+                                   const at::Tensor& z, int64_t func, int64_t nr, int64_t update_z) {
+  CHECK_DEV(objs); CHECK_F32(objs); CHECK_CONTIG(objs); CHECK_DEV(off_objs); CHECK_F32(off_objs); CHECK_CONTIG(off_objs);
+  CHECK_DEV(W); CHECK_F32(W); CHECK_CONTIG(W); CHECK_DEV(z); CHECK_F32(z); CHECK_CONTIG(z);
+  TORCH_CHECK(P.is_cuda() && P.scalar_type() == at::kInt && P.is_contiguous() && P.dim() == 2, "moead_scan: P must be int32 (R, T)");
+  const int64_t N = objs.size(0), M = objs.size(1), R = off_objs.size(0), T = P.size(1);
+  TORCH_CHECK(M >= 1 && M <= 16 && off_objs.size(1) == M && W.size(0) == N && W.size(1) == M && z.numel() == M, "moead_scan: shapes");
+  TORCH_CHECK(P.size(0) == R && T >= 1 && T <= 64, "moead_scan: 1 <= T <= 64");
+  TORCH_CHECK(func >= 0 && func <= 3, "moead_scan: func in {0 tch, 1 pbi, 2 ws, 3 mtch}");
+  c10::DeviceGuard g(objs.device());
+  auto o = objs.clone();
+  auto zz = z.clone();
+  auto owner = at::empty({N}, objs.options().dtype(at::kInt));
+  if (N > 0) evx_moead_scan(o.data_ptr<float>(), off_objs.data_ptr<float>(), P.data_ptr<int>(), W.data_ptr<float>(), zz.data_ptr<float>(),
+                            owner.data_ptr<int>(), (int)N, (int)R, (int)T, (int)M, (int)func, (int)nr, (int)update_z, cur_stream());
+  return {owner, o, zz};
+}
+
+// Stochastic ranking (Runarsson & Yao; SRA reference sra.py:13-64): bubble-sort sweeps over
+// adjacent pairs comparing by indicator I1 with probability pc (fixed per-pair draws
+// `rnd`, as the reference reuses them in every sweep), else by I2; at most ceil(n/2)
+// sweeps, stopping early when a sweep makes no swap.  Inherently sequential and tiny:
+// a host loop over CPU tensors.
+at::Tensor stochastic_ranking(const at::Tensor& I1_, const at::Tensor& I2_, const at::Tensor& rnd_, double pc) {
+  auto I1 = I1_.to(at::kCPU, at::kFloat).contiguous();
+  auto I2 = I2_.to(at::kCPU, at::kFloat).contiguous();
+  auto rnd = rnd_.to(at::kCPU, at::kFloat).contiguous();
+  const int64_t n = I1.numel();
+  TORCH_CHECK(I2.numel() == n && rnd.numel() >= std::max<int64_t>(n - 1, 0), "stochastic_ranking: sizes");
+  auto rank = at::arange(n, at::TensorOptions().dtype(at::kLong));
+  int64_t* r = rank.data_ptr<int64_t>();
+  const float *a = I1.data_ptr<float>(), *b = I2.data_ptr<float>(), *u = rnd.data_ptr<float>();
+  const int64_t sweeps = (n + 1) / 2;
+  bool swapped = true;
+  for (int64_t it = 0; it < sweeps && swapped; ++it) {
+    swapped = false;
+    for (int64_t j = 0; j + 1 < n; ++j) {
+      const float* key = (u[j] < pc) ? a : b;
+      if (key[r[j]] < key[r[j + 1]]) {
+        std::swap(r[j], r[j + 1]);
+        swapped = true;
+      }
+    }
+  }
+  return rank;
+}
+
 }  // namespace
 
 TORCH_LIBRARY(evoxmi, m) {
@@ -319,6 +366,8 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("sbx(Tensor x, Tensor keys, float pro_c, float dis_c, int type) -> Tensor");
   m.def("pm(Tensor x, Tensor lb, Tensor ub, Tensor keys, float pro_m, float dis_m, int nm) -> Tensor");
   m.def("nds(Tensor f) -> Tensor");
+  m.def("stochastic_ranking(Tensor I1, Tensor I2, Tensor rnd, float pc) -> Tensor");
+  m.def("moead_scan(Tensor objs, Tensor off_objs, Tensor P, Tensor W, Tensor z, int func, int nr, int update_z) -> Tensor[]");
   m.def("de_trial(Tensor P, Tensor idx, Tensor coef, Tensor cur, Tensor mode, Tensor CR, Tensor jr, Tensor L, Tensor key, Tensor lb, Tensor ub, int repair, Tensor err) -> Tensor");
   m.def("dtlz(Tensor X, int m, int variant) -> Tensor");
   m.def("classic_eval(Tensor X, int func, float a, float b, float c) -> Tensor");
@@ -327,6 +376,7 @@ TORCH_LIBRARY(evoxmi, m) {
 }
 
 TORCH_LIBRARY_IMPL(evoxmi, CompositeExplicitAutograd, m) {
+  m.impl("stochastic_ranking", &stochastic_ranking);
   m.impl("gemm_set_config", &gemm_set_config);
 }
 
@@ -336,6 +386,7 @@ TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
   m.impl("sbx", &sbx);
   m.impl("pm", &pm);
   m.impl("nds", &nds);
+  m.impl("moead_scan", &moead_scan);
   m.impl("de_trial", &de_trial);
   m.impl("dtlz", &dtlz);
   m.impl("philox_words", &philox_words);

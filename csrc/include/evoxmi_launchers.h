@@ -44,4 +44,6 @@ void evx_dtlz(const float* X, float* F, int N, int D, int M, int variant, hipStr
 void evx_de_trial(const float* P, const int32_t* idx, const float* coef, int K, const int32_t* cur, const int32_t* mode,
                   const float* CR, const int32_t* jr, const int32_t* L, const int64_t* key, const float* lb, const float* ub,
                   int repair, float* out, int R, int d, int rows, int* err, hipStream_t s);
+void evx_moead_scan(float* objs, const float* off_objs, const int32_t* P, const float* W, float* z, int32_t* owner, int N, int R,
+                    int T, int M, int func, int nr, int update_z, hipStream_t s);
 void evx_nds(const float* f, int n, int m, uint32_t* DT, int32_t* rank, int32_t* cnt, hipStream_t s);

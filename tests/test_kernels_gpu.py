@@ -399,3 +399,36 @@ def test_es_variants_graph_matches_eager(name):
             k = next(k for k in ("center", "mean", "population") if k in a.keys())
             outs.append(a[k].clone())
     assert torch.allclose(outs[0], outs[1], rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("func", ["tchebycheff", "pbi", "weighted_sum", "modified_tchebycheff"])
+@pytest.mark.parametrize("nr,update_z", [(2, True), (64, False)])
+def test_moead_scan_kernel(func, nr, update_z):
+    from evoxmi.ops.mo import moead_scan
+
+    g = torch.Generator().manual_seed(7)
+    N, R, T, M = 300, 300, 30, 3
+    objs, off = torch.rand(N, M, generator=g), torch.rand(R, M, generator=g) * 0.9
+    P = torch.randint(0, N, (R, T), generator=g)
+    W = torch.rand(N, M, generator=g) + 0.05
+    z = torch.zeros(M) - 0.01
+    ref = moead_scan(objs, off, P, W, z, func, nr=nr, update_z=update_z)
+    out = moead_scan(objs.cuda(), off.cuda(), P.cuda(), W.cuda(), z.cuda(), func, nr=nr, update_z=update_z)
+    assert torch.equal(out[0].cpu(), ref[0])
+    assert torch.allclose(out[1].cpu(), ref[1]) and torch.allclose(out[2].cpu(), ref[2])
+
+
+@pytest.mark.parametrize("name", ["NSGA2", "NSGA3", "MOEAD", "MOEADDRA", "EAGMOEAD", "RVEA", "IBEA", "HypE", "SPEA2", "TDEA", "LMOCSO"])
+def test_moea_on_gpu(name):
+    import evoxmi.algorithms as A
+    from evoxmi.problems.numerical import DTLZ2
+    from evoxmi.workflows import StdWorkflow
+
+    lb, ub = torch.zeros(12, device="cuda"), torch.ones(12, device="cuda")
+    algo = getattr(A, name)(3, lb, ub, 100) if name == "LMOCSO" else getattr(A, name)(lb, ub, 3, 100)
+    wf = StdWorkflow(algo, DTLZ2(d=12, m=3))
+    st = wf.init(rnd.PRNGKey(1, device="cuda"))
+    for _ in range(5):
+        st = wf.step(st)
+    f = st.get_child_state("algorithm").fitness
+    assert f.is_cuda and torch.isfinite(f[~torch.isnan(f).any(1)]).all()
