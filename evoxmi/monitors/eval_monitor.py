@@ -14,6 +14,7 @@ from __future__ import annotations
 import warnings
 
 import torch
+import torch.utils._pytree as pytree
 
 from ..core import Monitor
 
@@ -65,6 +66,29 @@ class EvalMonitor(Monitor):
         else:
             self.record_fit_multi_obj(cand_sol, fitness)
 
+    # candidate solutions may be tensors or pytrees of tensors (e.g. TreeAlgorithm,
+    # neuroevolution parameter trees): every row operation is applied leaf-wise
+    @staticmethod
+    def _rows(sol):
+        leaves = [x for x in pytree.tree_leaves(sol) if isinstance(x, torch.Tensor)]
+        return leaves[0].shape[0] if leaves else None
+
+    @staticmethod
+    def _sel(sol, idx):
+        return pytree.tree_map(lambda x: x.index_select(0, idx) if isinstance(x, torch.Tensor) else x, sol)
+
+    @staticmethod
+    def _where(better, a, b):
+        return pytree.tree_map(lambda x, y: torch.where(better.reshape((-1,) + (1,) * (x.dim() - 1)), x, y), a, b)
+
+    @staticmethod
+    def _cat(a, b):
+        return pytree.tree_map(lambda x, y: torch.cat([x, y], 0), a, b)
+
+    @staticmethod
+    def _clone(a):
+        return pytree.tree_map(lambda x: x.clone() if isinstance(x, torch.Tensor) else x, a)
+
     def record_fit_single_obj(self, cand_sol, fitness):
         if self.full_sol_history:
             self.solution_history.append(self._keep(cand_sol))
@@ -72,30 +96,30 @@ class EvalMonitor(Monitor):
             self.fitness_history.append(self._keep(fitness))
         n = fitness.shape[0]
         k = min(self.topk, n)
-        if cand_sol is not None and cand_sol.shape[0] != n:
+        if cand_sol is not None and self._rows(cand_sol) != n:
             cand_sol = None  # distributed generic path: rows are sharded
         if k == 1:
             i = torch.argmin(fitness)
-            fit = fitness[i : i + 1] if False else fitness.index_select(0, i.reshape(1))
-            sol = cand_sol.index_select(0, i.reshape(1)) if cand_sol is not None else None
+            fit = fitness.index_select(0, i.reshape(1))
+            sol = self._sel(cand_sol, i.reshape(1)) if cand_sol is not None else None
             if self.topk_fitness is None:
-                self.topk_fitness, self.topk_solutions = fit.clone(), (sol.clone() if sol is not None else None)
+                self.topk_fitness, self.topk_solutions = fit.clone(), (self._clone(sol) if sol is not None else None)
             else:
                 better = fit < self.topk_fitness  # device-side select, no host sync
                 self.topk_fitness = torch.where(better, fit, self.topk_fitness)
                 if sol is not None and self.topk_solutions is not None:
-                    self.topk_solutions = torch.where(better[:, None], sol, self.topk_solutions)
+                    self.topk_solutions = self._where(better, sol, self.topk_solutions)
         else:
             vals, idx = torch.topk(fitness, k, largest=False, sorted=True)
-            sols = cand_sol.index_select(0, idx) if cand_sol is not None else None
+            sols = self._sel(cand_sol, idx) if cand_sol is not None else None
             if self.topk_fitness is not None:
                 vals = torch.cat([self.topk_fitness, vals])
                 if sols is not None and self.topk_solutions is not None:
-                    sols = torch.cat([self.topk_solutions, sols], 0)
+                    sols = self._cat(self.topk_solutions, sols)
                 v2, i2 = torch.topk(vals, k, largest=False, sorted=True)
                 vals = v2
                 if sols is not None:
-                    sols = sols.index_select(0, i2)
+                    sols = self._sel(sols, i2)
             self.topk_fitness, self.topk_solutions = vals, sols
 
     def record_fit_multi_obj(self, cand_sol, fitness):
