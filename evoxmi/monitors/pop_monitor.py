@@ -31,6 +31,12 @@ class PopMonitor(Monitor):
             self.population_history.append(self._keep(getattr(alg, self.population_name)))
         self.fitness_history.append(self._keep(getattr(alg, self.fitness_name)))
 
+    def get_latest_fitness(self):
+        return self.fitness_history[-1]
+
+    def get_latest_population(self):
+        return self.population_history[-1]
+
     def get_population_history(self):
         return self.population_history
 

@@ -53,7 +53,8 @@ class _ForwardingMonitor(Monitor):
         self.conn = conn
         self.queue = []
         for h in self._hooks:
-            setattr(self, h, self._make(h))
+            if h != "post_eval":  # post_eval is a real method: it also ships the fitness to the driver
+                setattr(self, h, self._make(h))
 
     def hooks(self):
         return list(self._hooks) + ["post_eval"]

@@ -58,3 +58,12 @@ def uniform(key, shape, minval=0.0, maxval=1.0):
     minval = np.asarray(minval, np.float32)
     maxval = np.asarray(maxval, np.float32)
     return np.maximum(minval, f * (maxval - minval) + minval).astype(np.float32)
+
+
+def normal(key, shape):
+    """jax.random.normal: √2·erfinv(U(nextafter(−1, 0), 1)) in float32."""
+    from scipy.special import erfinv
+
+    lo = np.nextafter(np.float32(-1.0), np.float32(0.0))
+    u = uniform(key, shape, lo, np.float32(1.0))
+    return (np.sqrt(np.float32(2.0)) * erfinv(u.astype(np.float64))).astype(np.float32)
