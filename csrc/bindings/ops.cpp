@@ -353,6 +353,23 @@ at::Tensor stochastic_ranking(const at::Tensor& I1_, const at::Tensor& I2_, cons
   return rank;
 }
 
+std::vector<at::Tensor> ant_rollout(const at::Tensor& W, int64_t h1, int64_t h2, const at::Tensor& init, int64_t cap) {
+  CHECK_DEV(W); CHECK_F32(W); CHECK_CONTIG(W); CHECK_DEV(init); CHECK_F32(init); CHECK_CONTIG(init);
+  TORCH_CHECK(W.dim() == 2, "ant_rollout: W must be (N, P)");
+  TORCH_CHECK(h1 >= 1 && h1 <= 512 && h2 >= 1 && h2 <= 512, "ant_rollout: hidden sizes in [1, 512]");
+  const int64_t P = 27 * h1 + h1 + h1 * h2 + h2 + h2 * 8 + 8;
+  TORCH_CHECK(W.size(1) == P, "ant_rollout: W has ", W.size(1), " columns, MLP 27-", h1, "-", h2, "-8 needs ", P);
+  TORCH_CHECK(init.numel() == 29, "ant_rollout: init state must have 29 entries");
+  TORCH_CHECK((P + 32 + h1 + h2 + 8) * 4 <= 160 * 1024, "ant_rollout: MLP too large for one wave's LDS");
+  c10::DeviceGuard g(W.device());
+  const int64_t N = W.size(0);
+  auto ret = at::empty({N}, W.options());
+  auto steps = at::empty({N}, W.options().dtype(at::kInt));
+  if (N > 0) evx_ant_rollout(W.data_ptr<float>(), P, (int)N, (int)h1, (int)h2, init.data_ptr<float>(), (int)cap, ret.data_ptr<float>(),
+                             steps.data_ptr<int>(), cur_stream());
+  return {ret, steps};
+}
+
 }  // namespace
 
 TORCH_LIBRARY(evoxmi, m) {
@@ -366,6 +383,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("sbx(Tensor x, Tensor keys, float pro_c, float dis_c, int type) -> Tensor");
   m.def("pm(Tensor x, Tensor lb, Tensor ub, Tensor keys, float pro_m, float dis_m, int nm) -> Tensor");
   m.def("nds(Tensor f) -> Tensor");
+  m.def("ant_rollout(Tensor W, int h1, int h2, Tensor init, int cap) -> Tensor[]");
   m.def("stochastic_ranking(Tensor I1, Tensor I2, Tensor rnd, float pc) -> Tensor");
   m.def("moead_scan(Tensor objs, Tensor off_objs, Tensor P, Tensor W, Tensor z, int func, int nr, int update_z) -> Tensor[]");
   m.def("de_trial(Tensor P, Tensor idx, Tensor coef, Tensor cur, Tensor mode, Tensor CR, Tensor jr, Tensor L, Tensor key, Tensor lb, Tensor ub, int repair, Tensor err) -> Tensor");
@@ -386,6 +404,7 @@ TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
   m.impl("sbx", &sbx);
   m.impl("pm", &pm);
   m.impl("nds", &nds);
+  m.impl("ant_rollout", &ant_rollout);
   m.impl("moead_scan", &moead_scan);
   m.impl("de_trial", &de_trial);
   m.impl("dtlz", &dtlz);

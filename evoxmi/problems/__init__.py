@@ -1,1 +1,3 @@
 from . import numerical
+from . import neuroevolution
+from . import evoxbench

@@ -1,0 +1,4 @@
+from .brax import Brax
+from .gym import Gym, CapEpisode
+from .env_pool import EnvPool
+from .envs import get_environment, Ant, CartPole, Pendulum, MountainCarContinuous
