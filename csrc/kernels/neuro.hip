@@ -1,15 +1,15 @@
 // Persistent neuroevolution rollout (K15): Brax-style Ant + per-individual MLP policy.
 //
-// One wave64 owns one individual for the whole episode: its MLP weights are copied
-// into LDS once and reused for every control step (no per-step weight traffic from
-// HBM), the forward pass is lane-parallel over hidden units (lane j computes units
-// j, j+64, ...; weights are stored (in, out) row-major so a row read is contiguous
-// across lanes → bank-conflict free), and the physics (5 semi-implicit 10 ms
-// sub-steps, feet by forward kinematics, penalty contacts with smooth friction) is
-// evaluated redundantly by every lane from register state, so the only
-// synchronisation inside the episode is the wave's own LDS exchange of the
-// activations.  Waves leave the loop independently when their episode ends
-// (sticky done), so there are no block barriers after the weight load.
+// One wave64 owns one individual for the whole episode and its weights stay on-chip
+// for every control step (no per-step weight traffic from HBM):
+//  * ant_rollout_reg_kernel (h1, h2 <= 64): weights in VGPRs, lane j = hidden unit j;
+//  * ant_rollout_kernel (larger layers): weights in LDS, lanes stride over units
+//    ((in, out) row-major, so a row read is contiguous across lanes).
+// The body state is lane-uniform; the four legs of each 10 ms semi-implicit
+// sub-step (5 per control step; feet by forward kinematics, penalty contacts with
+// smooth friction) are evaluated by lane quads and reduced with DPP.  Waves leave
+// the loop independently when their episode ends (sticky done), so there are no
+// block barriers after the weight load.
 //
 // Semantics mirror evoxmi/problems/neuroevolution/reinforcement_learning/envs.py:Ant
 // (the CPU reference); constants below must match ANT there.
@@ -24,6 +24,8 @@ constexpr float KC = 2000.f, CC = 60.f, MU = 1.f, EPSV = 0.05f, GRAV = 9.81f;
 constexpr int SUB = 5;
 __constant__ float LEG_ANG[4] = {0.7854f, 2.3562f, 3.9270f, 5.4978f};
 __constant__ float ANK_SGN[4] = {1.f, -1.f, -1.f, 1.f};
+__constant__ float LEG_COS[4] = {0.70710678f, -0.70710678f, -0.70710678f, 0.70710678f};
+__constant__ float LEG_SIN[4] = {0.70710678f, 0.70710678f, -0.70710678f, -0.70710678f};
 
 struct AntState {
   float p[3], q[4], v[3], w[3], jq[8], jqd[8];
@@ -44,64 +46,82 @@ __device__ __forceinline__ void qrot(const float* q, const float* v, float* o) {
   for (int k = 0; k < 3; ++k) o[k] = v[k] + q[0] * t[k] + u[k];
 }
 
-__device__ void substep(AntState& s, const float* tau) {
-  // joints
+// Lane-split sub-step for the register kernel: the four legs are evaluated in
+// parallel by lane groups (leg = lane & 3) instead of redundantly by every lane,
+// and the per-leg force/torque are summed across each quad with two DPP
+// quad-permutes.  Joint and body integration stay lane-uniform.
+__device__ __forceinline__ float quad_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));  // xor 1
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));  // xor 2
+  return v;
+}
+// tanh via one v_exp and one v_rcp (|error| ~1e-7 near 0, saturates exactly)
+__device__ __forceinline__ float fast_tanh(float x) {
+  const float e = __expf(2.f * fminf(fmaxf(x, -15.f), 15.f));
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f);
+}
+__device__ __forceinline__ float sel4(int k, float a, float b, float c, float d) {
+  return k == 0 ? a : (k == 1 ? b : (k == 2 ? c : d));
+}
+
+__device__ __forceinline__ void substep_split(AntState& s, const float* tau, int leg, float lc, float ls, float sg) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const int leg = j >> 1;
+    const int lg = j >> 1;
     const bool ankle = j & 1;
-    const float sg = ankle ? ANK_SGN[leg] : 1.f;
+    const float sj = ankle ? ANK_SGN[lg] : 1.f;
     const float lo = ankle ? ANK_LO : HIP_LO, hi = ankle ? ANK_HI : HIP_HI;
-    const float mag = s.jq[j] * sg;
+    const float mag = s.jq[j] * sj;
     const float viol = fmaxf(lo - mag, 0.f) - fmaxf(mag - hi, 0.f);
-    const float acc = (tau[j] - JD * s.jqd[j] + LIMK * viol * sg) / JI;
+    const float acc = (tau[j] - JD * s.jqd[j] + LIMK * viol * sj) * (1.f / JI);
     s.jqd[j] += DT * acc;
     s.jq[j] += DT * s.jqd[j];
   }
-  float F[3] = {0.f, 0.f, -MASS * GRAV}, T[3] = {0.f, 0.f, 0.f};
+  const float hip = sel4(leg, s.jq[0], s.jq[2], s.jq[4], s.jq[6]);
+  const float ank = sel4(leg, s.jq[1], s.jq[3], s.jq[5], s.jq[7]);
+  const float hipd = sel4(leg, s.jqd[0], s.jqd[2], s.jqd[4], s.jqd[6]);
+  const float ankd = sel4(leg, s.jqd[1], s.jqd[3], s.jqd[5], s.jqd[7]);
+  const float a = ank * sg;
+  const float ca = __cosf(a), sa = __sinf(a), ch = __cosf(hip), sh = __sinf(hip);
+  const float cphi = lc * ch - ls * sh, sphi = ls * ch + lc * sh;
+  const float reach = HIPR + L1 + L2 * ca;
+  const float loc[3] = {reach * cphi, reach * sphi, -L2 * sa};
+  const float dreach = -L2 * sa * ankd * sg;
+  const float dloc[3] = {dreach * cphi - reach * sphi * hipd, dreach * sphi + reach * cphi * hipd, -L2 * ca * ankd * sg};
+  float r[3], dr[3], wr[3];
+  qrot(s.q, loc, r);
+  qrot(s.q, dloc, dr);
+  cross(s.w, r, wr);
+  const float fz = s.p[2] + r[2];
+  const float fv[3] = {s.v[0] + wr[0] + dr[0], s.v[1] + wr[1] + dr[1], s.v[2] + wr[2] + dr[2]};
+  const float pen = fmaxf(-fz, 0.f);
+  const float fn = fmaxf(KC * pen - CC * fv[2] * (pen > 0.f ? 1.f : 0.f), 0.f);
+  const float ivn = rsqrtf(fv[0] * fv[0] + fv[1] * fv[1] + EPSV * EPSV);
+  float f[3] = {-MU * fn * fv[0] * ivn, -MU * fn * fv[1] * ivn, fn};
+  float T[3];
+  cross(r, f, T);
+  float F[3];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float sg = ANK_SGN[k];
-    const float hip = s.jq[2 * k], ank = s.jq[2 * k + 1], hipd = s.jqd[2 * k], ankd = s.jqd[2 * k + 1];
-    const float phi = LEG_ANG[k] + hip, a = ank * sg;
-    const float ca = cosf(a), sa = sinf(a), cphi = cosf(phi), sphi = sinf(phi);
-    const float reach = HIPR + L1 + L2 * ca;
-    const float loc[3] = {reach * cphi, reach * sphi, -L2 * sa};
-    const float dreach = -L2 * sa * ankd * sg;
-    const float dloc[3] = {dreach * cphi - reach * sphi * hipd, dreach * sphi + reach * cphi * hipd, -L2 * ca * ankd * sg};
-    float r[3], dr[3], wr[3];
-    qrot(s.q, loc, r);
-    qrot(s.q, dloc, dr);
-    cross(s.w, r, wr);
-    const float fz = s.p[2] + r[2];
-    const float fv[3] = {s.v[0] + wr[0] + dr[0], s.v[1] + wr[1] + dr[1], s.v[2] + wr[2] + dr[2]};
-    const float pen = fmaxf(-fz, 0.f);
-    const float fn = fmaxf(KC * pen - CC * fv[2] * (pen > 0.f ? 1.f : 0.f), 0.f);
-    const float vn = sqrtf(fv[0] * fv[0] + fv[1] * fv[1] + EPSV * EPSV);
-    const float f[3] = {-MU * fn * fv[0] / vn, -MU * fn * fv[1] / vn, fn};
-    float t[3];
-    cross(r, f, t);
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      F[c] += f[c];
-      T[c] += t[c];
-    }
+  for (int c = 0; c < 3; ++c) {
+    F[c] = quad_sum(f[c]);
+    T[c] = quad_sum(T[c]);
   }
+  F[2] -= MASS * GRAV;
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     F[c] -= LDAMP * s.v[c];
     T[c] -= ADAMP * s.w[c];
-    s.v[c] += DT * F[c] / MASS;
-    s.w[c] += DT * T[c] / INERTIA;
+    s.v[c] += DT * F[c] * (1.f / MASS);
+    s.w[c] += DT * T[c] * (1.f / INERTIA);
     s.p[c] += DT * s.v[c];
   }
   const float w = s.q[0], x = s.q[1], y = s.q[2], z = s.q[3];
   const float ox = s.w[0], oy = s.w[1], oz = s.w[2];
   float nq[4] = {w + DT * 0.5f * (-ox * x - oy * y - oz * z), x + DT * 0.5f * (ox * w + oy * z - oz * y),
                  y + DT * 0.5f * (oy * w + oz * x - ox * z), z + DT * 0.5f * (oz * w + ox * y - oy * x)};
-  const float n = sqrtf(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
+  const float in = rsqrtf(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
 #pragma unroll
-  for (int c = 0; c < 4; ++c) s.q[c] = nq[c] / n;
+  for (int c = 0; c < 4; ++c) s.q[c] = nq[c] * in;
 }
 
 // layer sizes: in = 27, hidden h1, h2 (any, ≤ 256), out = 8; tanh everywhere
@@ -134,6 +154,7 @@ __global__ void __launch_bounds__(256) ant_rollout_kernel(const float* __restric
   for (int i = 0; i < 3; ++i) s.w[i] = init[10 + i];
   for (int i = 0; i < 8; ++i) s.jq[i] = init[13 + i];
   for (int i = 0; i < 8; ++i) s.jqd[i] = init[21 + i];
+  const int leg = lane & 3;
   float total = 0.f;
   int t = 0;
   for (; t < cap; ++t) {
@@ -180,10 +201,125 @@ __global__ void __launch_bounds__(256) ant_rollout_kernel(const float* __restric
     }
     __builtin_amdgcn_wave_barrier();  // a0..a3 are rewritten next step
     const float x0 = s.p[0];
-    for (int k = 0; k < SUB; ++k) substep(s, tau);
+    for (int k = 0; k < SUB; ++k) substep_split(s, tau, leg, LEG_COS[leg], LEG_SIN[leg], ANK_SGN[leg]);
     const bool healthy = (s.p[2] >= 0.2f) && (s.p[2] <= 1.0f);
     if (!healthy) break;  // sticky done: the terminating step earns nothing
-    total += (s.p[0] - x0) / (DT * SUB) + 1.f - 0.5f * csum;
+    total += (s.p[0] - x0) * (1.f / (DT * SUB)) + 1.f - 0.5f * csum;
+  }
+  if (lane == 0) {
+    ret[ind] = total;
+    if (steps_out) steps_out[ind] = t;
+  }
+}
+
+// Register-resident variant for h1, h2 <= 64 (the north-star 27-64-64-8 policy):
+// lane j keeps column j of W1 / W2 and row j of W3 in VGPRs (≈100 registers), so
+// the control step touches neither LDS nor memory.  The observation is already
+// lane-uniform (the physics runs redundantly on every lane), layer 2 broadcasts
+// a1[i] with v_readlane, and layer 3's eight 64-lane dot products are reduced by a
+// transposing butterfly (4+2+1 exchanges that halve the live values per stage,
+// then 3 full stages: 10 lane exchanges instead of 48).  Unused units are zero
+// padded, which keeps their activations at tanh(0) = 0.
+__device__ __forceinline__ float rl(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+__global__ void __launch_bounds__(64, 2) ant_rollout_reg_kernel(const float* __restrict__ W, int64_t P, int N, int h1, int h2,
+                                                              const float* __restrict__ init, int cap, float* __restrict__ ret,
+                                                              int* __restrict__ steps_out) {
+  const int lane = threadIdx.x & 63;
+  // one wave per workgroup: a finished episode frees its slot immediately, which
+  // matters because episode lengths differ by orders of magnitude
+  const int ind = blockIdx.x;
+  if (ind >= N) return;
+  const float* W1 = W + (int64_t)ind * P;
+  const float* B1 = W1 + 27 * h1;
+  const float* W2 = B1 + h1;
+  const float* B2 = W2 + h1 * h2;
+  const float* W3 = B2 + h2;
+  const float* B3 = W3 + h2 * 8;
+  const bool u1 = lane < h1, u2 = lane < h2;
+  float w1[27], w2[64], w3[8], b3[8];
+#pragma unroll
+  for (int i = 0; i < 27; ++i) w1[i] = u1 ? W1[i * h1 + lane] : 0.f;
+  const float b1 = u1 ? B1[lane] : 0.f;
+#pragma unroll
+  for (int i = 0; i < 64; ++i) w2[i] = (u2 && i < h1) ? W2[i * h2 + lane] : 0.f;
+  const float b2 = u2 ? B2[lane] : 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    w3[k] = u2 ? W3[lane * 8 + k] : 0.f;
+    b3[k] = B3[k];
+  }
+  AntState s;
+  for (int i = 0; i < 3; ++i) s.p[i] = init[i];
+  for (int i = 0; i < 4; ++i) s.q[i] = init[3 + i];
+  for (int i = 0; i < 3; ++i) s.v[i] = init[7 + i];
+  for (int i = 0; i < 3; ++i) s.w[i] = init[10 + i];
+  for (int i = 0; i < 8; ++i) s.jq[i] = init[13 + i];
+  for (int i = 0; i < 8; ++i) s.jqd[i] = init[21 + i];
+  const bool hb5 = lane & 32, hb4 = lane & 16, hb3 = lane & 8;
+  const int leg = lane & 3;
+  const float lc = LEG_COS[leg], ls = LEG_SIN[leg], lsg = ANK_SGN[leg];
+  float total = 0.f;
+  int t = 0;
+  for (; t < cap; ++t) {
+    float o[27];
+    o[0] = s.p[2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[1 + i] = s.q[i];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[5 + i] = s.jq[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) o[13 + i] = s.v[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) o[16 + i] = s.w[i];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[19 + i] = s.jqd[i];
+    float acc = b1;
+#pragma unroll
+    for (int i = 0; i < 27; ++i) acc = fmaf(o[i], w1[i], acc);
+    const float a1 = fast_tanh(acc);
+    float c4[4] = {b2, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 64; ++i) c4[i & 3] = fmaf(rl(a1, i), w2[i], c4[i & 3]);
+    const float a2 = fast_tanh((c4[0] + c4[1]) + (c4[2] + c4[3]));
+    // 8 partial products → transposing butterfly reduction
+    float v4[4], v2[2], v1;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float keep = hb5 ? a2 * w3[j + 4] : a2 * w3[j];
+      const float send = hb5 ? a2 * w3[j] : a2 * w3[j + 4];
+      v4[j] = keep + __shfl_xor(send, 32, 64);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float keep = hb4 ? v4[j + 2] : v4[j];
+      const float send = hb4 ? v4[j] : v4[j + 2];
+      v2[j] = keep + __shfl_xor(send, 16, 64);
+    }
+    {
+      const float keep = hb3 ? v2[1] : v2[0];
+      const float send = hb3 ? v2[0] : v2[1];
+      v1 = keep + __shfl_xor(send, 8, 64);
+    }
+    v1 += __shfl_xor(v1, 4, 64);
+    v1 += __shfl_xor(v1, 2, 64);
+    v1 += __shfl_xor(v1, 1, 64);
+    float tau[8], csum = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      // output k lives in the lanes whose bits (5,4,3) spell k
+      const float a = fminf(fmaxf(fast_tanh(rl(v1, ((k >> 2) & 1) * 32 + ((k >> 1) & 1) * 16 + (k & 1) * 8) + b3[k]), -1.f), 1.f);
+      tau[k] = GEAR * a;
+      csum += a * a;
+    }
+    const float x0 = s.p[0];
+    #pragma unroll 1
+    for (int k = 0; k < SUB; ++k) substep_split(s, tau, leg, lc, ls, lsg);
+    const bool healthy = (s.p[2] >= 0.2f) && (s.p[2] <= 1.0f);
+    if (!healthy) break;
+    total += (s.p[0] - x0) * (1.f / (DT * SUB)) + 1.f - 0.5f * csum;
   }
   if (lane == 0) {
     ret[ind] = total;
@@ -196,6 +332,10 @@ __global__ void __launch_bounds__(256) ant_rollout_kernel(const float* __restric
 int64_t evx_ant_lds_bytes(int64_t P, int h1, int h2, int waves) { return (P + 32 + h1 + h2 + 8) * 4 * waves; }
 
 void evx_ant_rollout(const float* W, int64_t P, int N, int h1, int h2, const float* init, int cap, float* ret, int* steps, hipStream_t s) {
+  if (h1 <= 64 && h2 <= 64) {
+    ant_rollout_reg_kernel<<<N, 64, 0, s>>>(W, P, N, h1, h2, init, cap, ret, steps);
+    return;
+  }
   const int64_t per = (P + 32 + h1 + h2 + 8) * 4;
   int waves = 4;
   while (waves > 1 && per * waves > 160 * 1024) --waves;

@@ -55,7 +55,8 @@ class Brax(Problem):
         if self._fused_ok(weights):
             s0, _ = self.env.reset(state.key.cpu(), 1)
             h1, h2 = self.policy.sizes[1], self.policy.sizes[2]
-            ret, _steps = neuro_ops.ant_rollout(self.policy.flat(weights), h1, h2, s0[0], self.cap_episode)
+            ret, steps = neuro_ops.ant_rollout(self.policy.flat(weights), h1, h2, s0[0], self.cap_episode)
+            self.last_episode_lengths = steps  # diagnostics only (not part of the state)
             return ret, state
         leaves = [x for x in torch.utils._pytree.tree_leaves(weights) if isinstance(x, torch.Tensor)]
         n, dev = leaves[0].shape[0], leaves[0].device

@@ -21,13 +21,44 @@ from typing import Callable, List, Optional
 
 import torch
 
-from ....core import Problem, State
+from ....core import Problem, State, Stateful
 from .envs import get_environment
 
 try:  # pragma: no cover - not installed in this image
     import gymnasium as _gym
 except Exception:  # noqa: BLE001
     _gym = None
+
+
+class Normalizer(Stateful):
+    """Running observation normaliser (reference ``gym.py:21-56``, unused there).
+
+    Keeps Σx, Σx² and the count in the state; ``std = sqrt(max(E[x²] − mean², 1e-2))``.
+    The reference unpacks ``mean``/``std`` in the wrong order (``:33-34``) — here
+    both methods return ``(value, state)`` consistently."""
+
+    def setup(self, key):
+        return State(sum=torch.zeros(()), sumOfSquares=torch.zeros(()), count=torch.zeros(()))
+
+    def mean(self, state):
+        return state.sum / state.count, state
+
+    def std(self, state):
+        m = state.sum / state.count
+        return torch.sqrt(torch.clamp(state.sumOfSquares / state.count - m * m, min=1e-2)), state
+
+    def normalize(self, state, x):
+        state = state.update(count=state.count + 1, sum=state.sum + x, sumOfSquares=state.sumOfSquares + x * x)
+        mean, state = self.mean(state)
+        std, state = self.std(state)
+        return (x - mean) / std, state
+
+    def normalize_obvs(self, state, obvs):
+        state = state.update(count=state.count + obvs.shape[0], sum=state.sum + obvs.sum(0),
+                             sumOfSquares=state.sumOfSquares + (obvs * obvs).sum(0))
+        mean, state = self.mean(state)
+        std, state = self.std(state)
+        return (obvs - mean) / std, state
 
 
 class CapEpisode:

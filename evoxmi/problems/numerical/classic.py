@@ -74,9 +74,25 @@ def ellipsoid_func(X):
     return (i * X * X).sum(-1)
 
 
+# ---------------------------------------------------------------------------
+# Decision-axis sharding protocol (SURVEY §2.2 strategy P2, used by
+# evoxmi.parallel.DimShardedProblem): ``partial_terms(Xb, col0, d, own)`` maps the
+# column block ``Xb`` (its first ``own`` columns start at global column ``col0``;
+# ``dim_halo`` extra columns follow) to per-row additive terms (N, k); the terms of
+# all blocks are summed by one all-reduce and ``combine_terms(T, d)`` finishes.
+
+
 class Sphere(Problem):
+    dim_halo = 0
+
     def evaluate(self, state, X):
         return sphere_func(X), state
+
+    def partial_terms(self, Xb, col0, d, own):
+        return (Xb * Xb).sum(-1, keepdim=True)
+
+    def combine_terms(self, T, d):
+        return T[:, 0]
 
 
 class Ackley(Problem):
@@ -84,32 +100,89 @@ class Ackley(Problem):
         super().__init__()
         self.a, self.b, self.c = float(a), float(b), float(c)
 
+    dim_halo = 0
+
     def evaluate(self, state, X):
         return ackley_func(self.a, self.b, self.c, X), state
 
+    def partial_terms(self, Xb, col0, d, own):
+        return torch.stack([(Xb * Xb).sum(-1), torch.cos(self.c * Xb).sum(-1)], -1)
+
+    def combine_terms(self, T, d):
+        return -self.a * torch.exp(-self.b * torch.sqrt(T[:, 0] / d)) - torch.exp(T[:, 1] / d) + self.a + math.e
+
 
 class Rastrigin(Problem):
+    dim_halo = 0
+
     def evaluate(self, state, X):
         return rastrigin_func(X), state
 
+    def partial_terms(self, Xb, col0, d, own):
+        return (Xb * Xb - 10 * torch.cos(2 * math.pi * Xb)).sum(-1, keepdim=True)
+
+    def combine_terms(self, T, d):
+        return 10 * d + T[:, 0]
+
 
 class Rosenbrock(Problem):
+    dim_halo = 1  # the term of column i needs x_{i+1}
+
     def evaluate(self, state, X):
         return rosenbrock_func(X), state
 
+    def partial_terms(self, Xb, col0, d, own):
+        n = min(own, d - 1 - col0)  # pair terms whose left column is owned here
+        if n <= 0:
+            return Xb.new_zeros(Xb.shape[0], 1)
+        a, b = Xb[:, :n], Xb[:, 1 : n + 1]
+        return (100 * (b - a * a) ** 2 + (a - 1) ** 2).sum(-1, keepdim=True)
+
+    def combine_terms(self, T, d):
+        return T[:, 0]
+
 
 class Griewank(Problem):
+    dim_halo = 0
+
     def evaluate(self, state, X):
         return griewank_func(X), state
+
+    def partial_terms(self, Xb, col0, d, own):
+        # the product is carried as (Σ log|cos|, #negative factors) so it stays additive
+        i = torch.arange(col0 + 1, col0 + Xb.shape[1] + 1, device=Xb.device, dtype=Xb.dtype)
+        cs = torch.cos(Xb / torch.sqrt(i))
+        return torch.stack([(Xb * Xb).sum(-1), torch.log(cs.abs()).sum(-1), (cs < 0).sum(-1).to(Xb.dtype)], -1)
+
+    def combine_terms(self, T, d):
+        sign = 1 - 2 * torch.remainder(T[:, 2], 2)
+        return T[:, 0] / 4000 - sign * torch.exp(T[:, 1]) + 1
 
 
 class Schwefel(Problem):
     """Minimum at x = [420.9687462275036, ...]."""
 
+    dim_halo = 0
+
     def evaluate(self, state, X):
         return schwefel_func(X), state
 
+    def partial_terms(self, Xb, col0, d, own):
+        return (Xb * torch.sin(torch.sqrt(torch.abs(Xb)))).sum(-1, keepdim=True)
+
+    def combine_terms(self, T, d):
+        return 418.9828872724338 * d - T[:, 0]
+
 
 class Ellipsoid(Problem):
+    dim_halo = 0
+
     def evaluate(self, state, X):
         return ellipsoid_func(X), state
+
+    def partial_terms(self, Xb, col0, d, own):
+        i = torch.arange(col0 + 1, col0 + Xb.shape[1] + 1, device=Xb.device, dtype=Xb.dtype)
+        return (i * Xb * Xb).sum(-1, keepdim=True)
+
+    def combine_terms(self, T, d):
+        return T[:, 0]

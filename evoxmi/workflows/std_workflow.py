@@ -91,6 +91,7 @@ class StdWorkflow(Workflow):
         # distributed context
         self.distributed_step = False
         self._dist = None
+        self._dim_shard_group = None  # set by enable_multi_devices (decision-axis sharding)
         # graph-mode bookkeeping
         self._graph = None
         self._static = None
@@ -110,6 +111,10 @@ class StdWorkflow(Workflow):
         return fitness if od == 1 else fitness * od
 
     def _evaluate(self, state, transformed):
+        if self._dim_shard_group is not None:
+            from ..parallel.dim_sharded import dim_sharded_fitness
+
+            return dim_sharded_fitness(self.problem, transformed, self._dim_shard_group[0]), state
         if self.jit_problem:
             return use_state(self.problem.evaluate)(state, transformed)
         fitness, state = use_state(self.problem.evaluate)(state, transformed)
@@ -306,12 +311,25 @@ class StdWorkflow(Workflow):
         return state
 
     def enable_multi_devices(self, state: State, devices=None) -> State:
-        """Reference ``std_workflow.py:272-309`` shards along the decision axis with
-        GSPMD.  With one process per GPU that role is played by
-        :class:`evoxmi.parallel.DimShardedProblem`; here we keep the call for API
-        parity and fall back to population sharding when a process group exists."""
+        """Shard the evaluation along the decision axis (reference
+        ``std_workflow.py:272-309``, GSPMD over ``PositionalSharding(devices)``).
+
+        One process per GPU: if the problem implements the dim-sharding protocol
+        (:func:`evoxmi.parallel.supports_dim_sharding`), each rank evaluates its
+        column block and the per-row partial terms are all-reduced
+        (:class:`evoxmi.parallel.DimShardedProblem`); the algorithm stays replicated
+        (same key on every rank).  Other problems fall back to population sharding.
+        The state structure is unchanged, so this may be called after ``init``."""
         if not self.jit_problem:
             raise ValueError("multi-devices with non jit problem isn't currently supported")
-        if torch.distributed.is_available() and torch.distributed.is_initialized():
-            return self.enable_distributed(state)
-        return state
+        if not (torch.distributed.is_available() and torch.distributed.is_initialized()):
+            return state
+        from ..parallel.dim_sharded import supports_dim_sharding
+
+        if supports_dim_sharding(self.problem):
+            from ..parallel.context import DistContext
+
+            ctx = DistContext(group=devices if isinstance(devices, torch.distributed.ProcessGroup) else None)
+            self._dim_shard_group = (ctx.group,)
+            return ctx.broadcast_state(state)
+        return self.enable_distributed(state)

@@ -434,14 +434,14 @@ def test_moea_on_gpu(name):
     assert f.is_cuda and torch.isfinite(f[~torch.isnan(f).any(1)]).all()
 
 
-@pytest.mark.parametrize("cap", [1, 5, 20])
-def test_ant_rollout_kernel_matches_torch(cap):
+@pytest.mark.parametrize("cap,hidden", [(1, 64), (5, 64), (20, 64), (20, 40), (20, 96)])
+def test_ant_rollout_kernel_matches_torch(cap, hidden):
     """Fused LDS-resident Ant rollout vs the torch reference env + batched MLP."""
     from evoxmi.models import MLPPolicy
     from evoxmi.problems.neuroevolution import Brax
     from evoxmi.utils import TreeAndVector
 
-    policy = MLPPolicy([27, 64, 64, 8])
+    policy = MLPPolicy([27, hidden, hidden, 8])
     params = policy.init(rnd.PRNGKey(0))
     tv = TreeAndVector(params)
     pop = tv.to_vector(params) + 0.3 * torch.randn(96, tv.to_vector(params).numel(), generator=torch.Generator().manual_seed(cap))

@@ -85,3 +85,17 @@ def test_openes_ant_improves():
     for _ in range(10):
         st = wf.step(st)
     assert math.isfinite(first) and float(mon.get_best_fitness()) >= first
+
+
+def test_normalizer_running_statistics():
+    from evoxmi.problems.neuroevolution.reinforcement_learning import Normalizer
+
+    n = Normalizer()
+    st = n.init(rnd.PRNGKey(0))
+    torch.manual_seed(0)
+    a, b = torch.randn(50, 3) * 4 + 1, torch.randn(30, 3) * 4 + 1
+    _, st = n.normalize_obvs(st, a)
+    out, st = n.normalize_obvs(st, b)
+    allx = torch.cat([a, b])
+    ref = (b - allx.mean(0)) / allx.std(0, unbiased=False)
+    assert torch.allclose(out, ref, atol=1e-4)

@@ -25,25 +25,63 @@ def main():
     ap.add_argument("--cap", type=int, default=1000)
     ap.add_argument("--gens", type=int, default=5)
     ap.add_argument("--hidden", type=int, default=64)
+    ap.add_argument("--wscale", type=float, default=0.1)
+    ap.add_argument("--kernel-only", action="store_true", help="time the fused rollout alone on random policies")
     args = ap.parse_args()
+    if args.kernel_only:
+        return kernel_only(args)
     dev = torch.device("cuda")
     policy = MLPPolicy([27, args.hidden, args.hidden, 8])
     params = policy.init(rnd.PRNGKey(0), device=dev)
     tv = TreeAndVector(params)
     algo = OpenES(tv.to_vector(params), args.pop, learning_rate=0.01, noise_stdev=0.05, optimizer="adam")
-    wf = StdWorkflow(algo, Brax(policy, "ant", args.cap), sol_transforms=[tv.batched_to_tree], fit_transforms=[rank_based_fitness],
+    prob = Brax(policy, "ant", args.cap)
+    wf = StdWorkflow(algo, prob, sol_transforms=[tv.batched_to_tree], fit_transforms=[rank_based_fitness],
                      opt_direction="max")
     st = wf.init(rnd.PRNGKey(1, device=dev))
     st = wf.step(st)
     torch.cuda.synchronize()
     t = time.perf_counter()
+    env_steps = 0
     for _ in range(args.gens):
         st = wf.step(st)
+        env_steps += prob.last_episode_lengths.sum()
     torch.cuda.synchronize()
+    env_steps = int(env_steps)
     dt = (time.perf_counter() - t) / args.gens
     out = {"pop": args.pop, "cap_episode": args.cap, "params": policy.num_params, "ms_per_gen": round(dt * 1e3, 2),
-           "gens_per_sec": round(1 / dt, 3), "env_steps_per_sec": round(args.pop * args.cap / dt, 1)}
+           "gens_per_sec": round(1 / dt, 3), "env_steps_per_sec": round(env_steps / args.gens / dt, 1),
+           "mean_episode_len": round(env_steps / args.gens / args.pop, 1)}
     print(json.dumps(out))
+
+
+def kernel_only(args):
+    """Rollout throughput without the ES loop: random-init policies (+ a large
+    perturbation so some survive long), counted in env steps actually simulated."""
+    from evoxmi import random as rnd
+    from evoxmi.ops import neuro
+    from evoxmi.problems.neuroevolution.reinforcement_learning.envs import get_environment
+
+    h = args.hidden
+    P = neuro.ant_param_count(h, h)
+    g = torch.Generator(device="cuda").manual_seed(0)
+    W = args.wscale * torch.randn(args.pop, P, device="cuda", generator=g)
+    s0, _ = get_environment("ant").reset(rnd.PRNGKey(0), 1)
+    init = s0[0].cuda()
+    neuro.ant_rollout(W, h, h, init, args.cap)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    steps = 0
+    for _ in range(args.gens):
+        _, st = neuro.ant_rollout(W, h, h, init, args.cap)
+        steps += st.sum()
+    torch.cuda.synchronize()
+    max_len = int(st.max())
+    dt = (time.perf_counter() - t) / args.gens
+    steps = int(steps) / args.gens
+    print(json.dumps({"mode": "kernel_only", "pop": args.pop, "hidden": h, "cap": args.cap, "ms_per_rollout": round(dt * 1e3, 3),
+                      "mean_episode_len": round(steps / args.pop, 1), "max_episode_len": max_len,
+                      "us_per_step_of_longest": round(dt * 1e6 / max(max_len, 1), 3), "env_steps_per_sec": round(steps / dt, 1)}))
 
 
 if __name__ == "__main__":
