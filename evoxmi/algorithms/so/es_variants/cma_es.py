@@ -43,6 +43,9 @@ def _default_weights(mu: int):
 
 
 class CMAES(Algorithm):
+    # fields that differ across ranks under the sharded protocol (excluded from replica checks)
+    rank_local_fields = ("population",)
+
     def __init__(self, center_init, init_stdev, pop_size=None, recombination_weights=None, cm=1, eig_sweeps=None):
         super().__init__()
         self.center_init = center_init

@@ -1,0 +1,92 @@
+"""Runtime knobs.
+
+The reference has no flag system: every parameter is a constructor kwarg and a few
+behaviours follow environment variables (``XLA_PYTHON_CLIENT_PREALLOCATE``,
+``CUDA_VISIBLE_DEVICES``; ``docs/source/miscellaneous/*.md``).  evoxmi keeps kwargs
+as the API and gathers the process-wide *implementation* choices here, each
+readable from an ``EVOXMI_*`` environment variable and overridable in code:
+
+>>> from evoxmi import config
+>>> config.get("eigh")
+'jacobi'
+>>> with config.override(jacobi_sweeps=3):
+...     ...
+
+Device selection uses ``HIP_VISIBLE_DEVICES`` (or ``ROCR_VISIBLE_DEVICES``) as
+usual for ROCm; multi-process runs read ``RANK``/``LOCAL_RANK``/``WORLD_SIZE``.
+"""
+from __future__ import annotations
+
+import contextlib
+import os
+from dataclasses import dataclass
+from typing import Any, Callable, Dict
+
+
+@dataclass(frozen=True)
+class Knob:
+    env: str
+    default: Any
+    parse: Callable[[str], Any]
+    doc: str
+
+
+def _bool(s: str) -> bool:
+    return s.strip().lower() in ("1", "true", "yes", "on")
+
+
+KNOBS: Dict[str, Knob] = {
+    "eigh": Knob("EVOXMI_EIGH", "jacobi", str, "symmetric eigensolver for CMA-ES: 'jacobi' (warm-started HIP block Jacobi) or 'torch' (rocSOLVER)"),
+    "jacobi_sweeps": Knob("EVOXMI_JACOBI_SWEEPS", 2, int, "maximum warm-started Jacobi sweeps per decomposition (stops early once converged)"),
+    "jacobi_tol_factor": Knob("EVOXMI_JACOBI_TOL_FACTOR", 4.0, float, "convergence: ‖offdiag‖ ≤ factor·eps_f32·sqrt(n)·‖diag‖"),
+    "jacobi_inner_tol": Knob("EVOXMI_JACOBI_INNER_TOL", 1e-6, float, "per-subproblem skip threshold of the Jacobi solve kernel"),
+    "jacobi_inner": Knob("EVOXMI_JACOBI_INNER", 1, int, "inner sweeps per 32×32 Jacobi subproblem"),
+    "debug": Knob("EVOXMI_DEBUG", False, _bool, "synchronous kernel error-flag checks after fused kernels (not while capturing)"),
+    "trace": Knob("EVOXMI_TRACE", False, _bool, "emit roctx ranges around ask / evaluate / tell in eager workflow steps"),
+    "arch": Knob("EVOXMI_ARCH", "gfx950", str, "offload architecture the HIP extension is compiled for"),
+    "check_replicas_every": Knob("EVOXMI_CHECK_REPLICAS_EVERY", 0, int, "distributed: checksum the replicated state across ranks every k generations (0 = off)"),
+    "heartbeat_interval": Knob("EVOXMI_HEARTBEAT_INTERVAL", 5.0, float, "seconds between rank heartbeats written to the TCPStore"),
+    "heartbeat_timeout": Knob("EVOXMI_HEARTBEAT_TIMEOUT", 60.0, float, "a rank whose heartbeat is older than this is reported dead"),
+}
+
+_overrides: Dict[str, Any] = {}
+
+
+def get(name: str) -> Any:
+    if name in _overrides:
+        return _overrides[name]
+    k = KNOBS[name]
+    raw = os.environ.get(k.env)
+    return k.default if raw is None else k.parse(raw)
+
+
+def set(name: str, value: Any) -> None:  # noqa: A001 - mirrors get()
+    if name not in KNOBS:
+        raise KeyError(f"unknown evoxmi knob {name!r}; known: {sorted(KNOBS)}")
+    _overrides[name] = value
+
+
+def reset(name: str = None) -> None:
+    if name is None:
+        _overrides.clear()
+    else:
+        _overrides.pop(name, None)
+
+
+@contextlib.contextmanager
+def override(**kw):
+    saved = {k: _overrides[k] for k in kw if k in _overrides}
+    try:
+        for k, v in kw.items():
+            set(k, v)
+        yield
+    finally:
+        for k in kw:
+            _overrides.pop(k, None)
+        _overrides.update(saved)
+
+
+def describe() -> str:
+    """Table of every knob, its environment variable and its current value."""
+    rows = [f"{n:22s} {k.env:30s} {get(n)!r:>10}  {k.doc}" for n, k in KNOBS.items()]
+    return "\n".join(rows)

@@ -12,7 +12,6 @@ flag, so the whole solve is graph-capturable (no host round trip).
 """
 from __future__ import annotations
 
-import os
 
 import torch
 
@@ -36,8 +35,10 @@ def warm_eigh(C: torch.Tensor, B_prev: torch.Tensor, max_sweeps: int = None, tol
 
     Returns ``(w, B)`` with ``C ≈ B diag(w) Bᵀ`` (eigenvalues not sorted).
     """
-    impl = os.environ.get("EVOXMI_EIGH", "jacobi")
-    if not C.is_cuda or impl == "library":
+    from .. import config
+
+    impl = config.get("eigh")
+    if not C.is_cuda or impl in ("library", "torch"):
         return eigh_reference(C)
     from . import jacobi
 

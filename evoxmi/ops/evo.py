@@ -1,11 +1,11 @@
 """Device launchers of the fused variation operators (``evo_ops.hip``)."""
 from __future__ import annotations
 
-import os
 
 import torch
 
 from . import _ext
+from .. import config
 from . import random as rnd
 
 
@@ -24,7 +24,6 @@ def polynomial(key, x, lb, ub, pro_m, dis_m):
 
 
 _CROSS = {"bin": 0, "exp": 1, "arith": 2}
-_DEBUG = os.environ.get("EVOXMI_DEBUG", "0") == "1"
 _ERR = {}
 
 
@@ -66,7 +65,7 @@ def de_trial(key, P, idx, coef, cur, mode, CR, jr, L, lb, ub, repair="clip"):
         err = _err_flag(dev)
         out = _ext.ops().de_trial(P.contiguous(), i32(idx), f32(coef), i32(cur), i32(mode), f32(CR), i32(jr), i32(L),
                                   key.contiguous(), lb, ub, rep, err)
-        if _DEBUG and not torch.cuda.is_current_stream_capturing():
+        if config.get("debug") and not torch.cuda.is_current_stream_capturing():
             bad = int(err.item())
             if bad:
                 raise RuntimeError(f"de_trial: out-of-range row index (flag {bad}); idx range "

@@ -15,14 +15,11 @@ import torch
 from . import _ext
 from .linalg import matmul, matmul_tn
 
-import os
+from .. import config
 
-WARM_SWEEPS = int(os.environ.get("EVOXMI_JACOBI_SWEEPS", "2"))
 COLD_SWEEPS = 12
 # convergence is judged against the f32 floor of ‖offdiag‖/‖diag‖ ≈ eps·sqrt(n)
-TOL_FACTOR = float(os.environ.get("EVOXMI_JACOBI_TOL_FACTOR", "4.0"))
-INNER_TOL = float(os.environ.get("EVOXMI_JACOBI_INNER_TOL", "1e-6"))
-MAX_INNER = int(os.environ.get("EVOXMI_JACOBI_INNER", "1"))
+# (sweeps / tolerance / inner sweeps are evoxmi.config knobs: EVOXMI_JACOBI_*)
 
 
 @functools.lru_cache(maxsize=16)
@@ -74,9 +71,10 @@ def warm_eigh(C: torch.Tensor, B_prev: torch.Tensor = None, max_sweeps: int = No
         Bp[:n, :n] = B_prev
         Bp[n:, n:] = eye_pad
         A = matmul_tn(Bp, matmul(Cp, Bp)).contiguous()
-        sweeps = WARM_SWEEPS if max_sweeps is None else max_sweeps
-    tol = tol or TOL_FACTOR * 1.1920929e-07 * max(n, 16) ** 0.5
-    w, stats = _ext.ops().jacobi_sweeps(A, Bp, schedule(np_ // 16, dev), int(sweeps), float(tol), INNER_TOL, MAX_INNER)
+        sweeps = config.get("jacobi_sweeps") if max_sweeps is None else max_sweeps
+    tol = tol or config.get("jacobi_tol_factor") * 1.1920929e-07 * max(n, 16) ** 0.5
+    w, stats = _ext.ops().jacobi_sweeps(A, Bp, schedule(np_ // 16, dev), int(sweeps), float(tol),
+                                        float(config.get("jacobi_inner_tol")), int(config.get("jacobi_inner")))
     out = (w[:n].contiguous(), Bp[:n, :n].contiguous())
     return (*out, stats) if return_stats else out
 

@@ -12,3 +12,4 @@ from .common import (
     x32_func_call,
 )
 from .optim import OptaxWrapper, OptimizerWrapper, adam, clipup, get_optimizer, sgd
+from .profiling import PhaseTimer, trace_range

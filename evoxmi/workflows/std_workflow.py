@@ -31,6 +31,7 @@ MI355X-first execution model (replaces ``jax.jit`` / ``pmap``):
 """
 from __future__ import annotations
 
+import contextlib
 import warnings
 from typing import Callable, List, Optional, Union
 
@@ -39,7 +40,9 @@ import torch
 from ..core import Algorithm, Monitor, Problem, State, Workflow, use_state
 from ..core.algorithm import algorithm_has_init_ask
 from ..core.state import tree_flatten, tree_map
+from .. import config
 from ..utils.common import parse_opt_direction
+from ..utils.profiling import trace_range
 
 HOOKS = ("pre_step", "pre_ask", "post_ask", "pre_eval", "post_eval", "pre_tell", "post_tell", "post_step")
 
@@ -59,6 +62,7 @@ class StdWorkflow(Workflow):
         monitor=None,
         graph: bool = False,
         nan_policy: str = "keep",
+        phase_timer=None,
     ):
         super().__init__()
         self.algorithm = algorithm
@@ -87,6 +91,9 @@ class StdWorkflow(Workflow):
         assert nan_policy in ("keep", "inf"), "nan_policy must be 'keep' or 'inf'"
         self.nan_policy = nan_policy
         self.graph = graph
+        # optional evoxmi.utils.profiling.PhaseTimer (per-phase hipEvent timing, eager steps;
+        # in graph mode the whole replay is one "graph_replay" phase)
+        self.phase_timer = phase_timer
         self._has_init_ask = algorithm_has_init_ask(algorithm)
         # distributed context
         self.distributed_step = False
@@ -131,12 +138,13 @@ class StdWorkflow(Workflow):
             ask, tell = alg.init_ask, alg.init_tell
         else:
             ask, tell = alg.ask, alg.tell
-        if sharded:
-            d = self._dist
-            ask_s = alg.init_ask_sharded if is_init else alg.ask_sharded
-            cand_sol, state = use_state(ask_s)(state, d)
-        else:
-            cand_sol, state = use_state(ask)(state)
+        with self._phase("ask"):
+            if sharded:
+                d = self._dist
+                ask_s = alg.init_ask_sharded if is_init else alg.ask_sharded
+                cand_sol, state = use_state(ask_s)(state, d)
+            else:
+                cand_sol, state = use_state(ask)(state)
         for m in self.registered_hooks["post_ask"]:
             m.post_ask(state, cand_sol)
 
@@ -152,12 +160,14 @@ class StdWorkflow(Workflow):
         for m in self.registered_hooks["pre_eval"]:
             m.pre_eval(state, local, transformed)
 
-        fitness, state = self._evaluate(state, transformed)
+        with self._phase("evaluate"):
+            fitness, state = self._evaluate(state, transformed)
         if self.nan_policy == "inf":
             fitness = torch.nan_to_num(fitness, nan=float("inf"))
 
         if self.distributed_step:
-            fitness = self._dist.all_gather_rows(fitness, cand_sol.shape[0] if not sharded else self._dist.global_pop)
+            with self._phase("all_gather"):
+                fitness = self._dist.all_gather_rows(fitness, cand_sol.shape[0] if not sharded else self._dist.global_pop)
 
         fitness = self._opt_dir(fitness)
         for m in self.registered_hooks["post_eval"]:
@@ -167,16 +177,31 @@ class StdWorkflow(Workflow):
             tfit = t(tfit)
         for m in self.registered_hooks["pre_tell"]:
             m.pre_tell(state, local, transformed, fitness, tfit)
-        if sharded:
-            tell_s = alg.init_tell_sharded if is_init else alg.tell_sharded
-            state = use_state(tell_s)(state, tfit, self._dist)
-        else:
-            state = use_state(tell)(state, tfit)
+        with self._phase("tell"):
+            if sharded:
+                tell_s = alg.init_tell_sharded if is_init else alg.tell_sharded
+                state = use_state(tell_s)(state, tfit, self._dist)
+            else:
+                state = use_state(tell)(state, tfit)
         for m in self.registered_hooks["post_tell"]:
             m.post_tell(state)
         if record is not None:
             record.update(cand_sol=local, transformed=transformed, fitness=fitness, tfit=tfit)
         return state.update(generation=state.generation + 1)
+
+    def _phase(self, name):
+        """roctx range (EVOXMI_TRACE=1) and/or hipEvent timer around one phase;
+        inert while a hipGraph is being captured."""
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            return contextlib.nullcontext()
+        timer = self.phase_timer
+        if timer is None and not config.get("trace"):
+            return contextlib.nullcontext()
+        stack = contextlib.ExitStack()
+        stack.enter_context(trace_range(name))
+        if timer is not None:
+            stack.enter_context(timer.phase(name))
+        return stack
 
     def _step_eager(self, state):
         is_init = self._has_init_ask and state.generation == 0
@@ -249,7 +274,8 @@ class StdWorkflow(Workflow):
                                 a.copy_(b)
                         else:  # e.g. a harness writing progress=0.3 into a tensor field
                             a.fill_(b)
-        self._graph.replay()
+        with self._phase("graph_replay"):
+            self._graph.replay()
         gen = state.generation + 1
         out = static.update(generation=gen)
         self._static = out
@@ -278,6 +304,16 @@ class StdWorkflow(Workflow):
             state = self._step_eager(state)
         for m in self.registered_hooks["post_step"]:
             m.post_step(state)
+        k = config.get("check_replicas_every")
+        if self.distributed_step and k and int(state.generation) % k == 0:
+            # race/divergence detector: replicas must stay bit-identical
+            chk = state
+            local = getattr(self.algorithm, "rank_local_fields", ()) if self._dist.algorithm_sharded else ()
+            if local:
+                alg = state.get_child_state("algorithm")
+                chk = state.update_child("algorithm", alg.replace(**{f: torch.zeros(0) for f in local}))
+            if not self._dist.check_replicas(chk):
+                raise RuntimeError(f"replicated algorithm state diverged across ranks at generation {int(state.generation)}")
         return state
 
     def valid(self, state: State, metric: str = "loss"):
