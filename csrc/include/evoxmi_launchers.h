@@ -47,4 +47,5 @@ void evx_de_trial(const float* P, const int32_t* idx, const float* coef, int K, 
 void evx_moead_scan(float* objs, const float* off_objs, const int32_t* P, const float* W, float* z, int32_t* owner, int N, int R,
                     int T, int M, int func, int nr, int update_z, hipStream_t s);
 void evx_ant_rollout(const float* W, int64_t P, int N, int h1, int h2, const float* init, int cap, float* ret, int* steps, hipStream_t s);
-void evx_nds(const float* f, int n, int m, uint32_t* DT, int32_t* rank, int32_t* cnt, hipStream_t s);
+size_t evx_nds_workspace_words(int n);
+void evx_nds(const float* f, int n, int m, int limit, uint32_t* DW, int32_t* rank, uint32_t* ws, hipStream_t s);

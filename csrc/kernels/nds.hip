@@ -1,21 +1,27 @@
-// Non-dominated sorting on the GPU (K9).
+// Non-dominated sorting on the GPU (K9 of SURVEY §2.10; reference
+// operators/selection/non_dominate.py:30-113).
 //
-// 1. dominance kernel: DT[j][w] bit b set ⇔ individual i = 32w + b dominates j
-//    (minimisation: ≤ in every objective, < in at least one).  Each thread builds one
-//    32-bit word from 32 compares of m objectives; objectives of the 32 candidates are
-//    staged in LDS.  cnt[j] = popcount over the row = number of dominators of j.
-// 2. peel kernel: ONE workgroup (1024 threads) peels the fronts without returning to
-//    the host: the current front is kept as a bitmask F (n/32 words in LDS) plus the
-//    list of its non-zero words; each unranked j subtracts Σ popcount(DT[j][w] & F[w])
-//    over that list.  The loop runs until every row is ranked.
+// 1. dominance kernel: word-major bit matrix DW[w][j], bit b set ⇔ individual
+//    i = 32w + b dominates j (minimisation: ≤ in every objective, < in at least one).
+//    Word-major so a wave's 64 lanes (64 consecutive j) read 256 contiguous bytes.
+//    The 32 candidates of word w are staged in LDS.
+// 2. peel kernel: a chip-wide persistent grid (≤ 128 workgroups, all co-resident on
+//    the 256 CUs) computes one front per iteration.  j joins front k iff every
+//    dominator of j is already ranked:  DW[w][j] & ~R[w] == 0 for all w, where R is
+//    the ranked bitset (early exit at the first word with an unranked dominator, so
+//    most tests read one or two words).  R is double-buffered and only ever OR-ed
+//    (R_next |= R_cur | new-front bits), so one grid barrier per front suffices; the
+//    loop ends when the per-iteration "still unranked" counter is zero or at least
+//    `limit` rows are ranked (NSGA-II only needs fronts until N survivors are
+//    covered: the rest get rank = n).  The barrier spins with a bound: on timeout
+//    the kernel sets an error flag and every wave exits (no hang is possible).
 #include "evoxmi_common.h"
 
 namespace {
 
 template <int M>
 __global__ void __launch_bounds__(256) dominance_kernel(const float* __restrict__ f, int n, int m, int nw,
-                                                        uint32_t* __restrict__ DT) {
-  // grid.x over words w (blockDim.y = 1), each thread a row j
+                                                        uint32_t* __restrict__ DW) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   const int w = blockIdx.y;
   __shared__ float cand[32 * 8];
@@ -31,8 +37,8 @@ __global__ void __launch_bounds__(256) dominance_kernel(const float* __restrict_
 #pragma unroll
   for (int k = 0; k < 8; ++k) fj[k] = k < mm ? f[(int64_t)j * m + k] : 0.f;
   uint32_t word = 0;
-  for (int b = 0; b < 32; ++b) {
-    if (32 * w + b >= n) break;
+  const int nb = min(32, n - 32 * w);
+  for (int b = 0; b < nb; ++b) {
     bool le = true, lt = false;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -44,62 +50,110 @@ __global__ void __launch_bounds__(256) dominance_kernel(const float* __restrict_
     }
     if (le && lt) word |= (1u << b);
   }
-  DT[(int64_t)j * nw + w] = word;
+  DW[(int64_t)w * n + j] = word;
 }
 
-__global__ void __launch_bounds__(1024) peel_kernel(const uint32_t* __restrict__ DT, int n, int nw, int32_t* __restrict__ rank,
-                                                    int32_t* __restrict__ cnt_g) {
-  extern __shared__ uint32_t smem[];
-  uint32_t* F = smem;                         // nw words: current front bitmask
-  uint32_t* nzw = smem + nw;                  // list of non-zero word ids
-  __shared__ int nnz, front_size;
-  // dominator counts
-  for (int j = threadIdx.x; j < n; j += blockDim.x) {
-    int c = 0;
-    for (int w = 0; w < nw; ++w) c += __popc(DT[(int64_t)j * nw + w]);
-    cnt_g[j] = c;
-    rank[j] = -1;
+// workspace layout (uint32): [0] barrier count, [1] barrier generation, [2] error flag,
+// [3] ranked total, [4 .. 4+nw) R0, [4+nw .. 4+2nw) R1, [4+2nw .. 4+2nw+n+1) left[k]
+constexpr int kSpinLimit = 1 << 24;
+
+__device__ __forceinline__ bool grid_barrier(uint32_t* ws, uint32_t nblocks, uint32_t& gen) {
+  __syncthreads();
+  __shared__ int ok;
+  if (threadIdx.x == 0) {
+    ok = 1;
+    __threadfence();
+    const uint32_t arrived = __hip_atomic_fetch_add(&ws[0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1;
+    if (arrived == nblocks) {
+      __hip_atomic_store(&ws[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&ws[1], gen + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      int spins = 0;
+      while (__hip_atomic_load(&ws[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == gen) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > kSpinLimit) {
+          __hip_atomic_store(&ws[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok = 0;
+          break;
+        }
+      }
+    }
+    __threadfence();
   }
   __syncthreads();
-  for (int r = 0;; ++r) {
-    for (int w = threadIdx.x; w < nw; w += blockDim.x) F[w] = 0;
-    if (threadIdx.x == 0) { nnz = 0; front_size = 0; }
+  gen += 1;
+  return ok && __hip_atomic_load(&ws[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+}
+
+__global__ void __launch_bounds__(256) peel_kernel(const uint32_t* __restrict__ DW, int n, int nw, int limit,
+                                                   int32_t* __restrict__ rank, uint32_t* __restrict__ ws) {
+  uint32_t* R[2] = {ws + 4, ws + 4 + nw};
+  uint32_t* left = ws + 4 + 2 * nw;
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nthreads = gridDim.x * blockDim.x;
+  __shared__ uint32_t wg_left;
+  uint32_t gen = 0;
+  for (int j = tid; j < n; j += nthreads) rank[j] = -1;
+  for (int k = 0;; ++k) {
+    const uint32_t* Rc = R[k & 1];
+    uint32_t* Rn = R[(k + 1) & 1];
+    if (threadIdx.x == 0) wg_left = 0;
     __syncthreads();
-    for (int j = threadIdx.x; j < n; j += blockDim.x) {
-      if (rank[j] < 0 && cnt_g[j] == 0) {
-        rank[j] = r;
-        atomicOr(&F[j >> 5], 1u << (j & 31));
-        atomicAdd(&front_size, 1);
-      }
+    // carry the ranked set into the next buffer (it holds R_{k-1} ⊆ R_k)
+    for (int w = tid; w < nw; w += nthreads) {
+      const uint32_t v = __hip_atomic_load(&Rc[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (v) __hip_atomic_fetch_or(&Rn[w], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    __syncthreads();
-    if (front_size == 0) break;
-    for (int w = threadIdx.x; w < nw; w += blockDim.x)
-      if (F[w]) nzw[atomicAdd(&nnz, 1)] = w;
-    __syncthreads();
-    const int nz = nnz;
-    for (int j = threadIdx.x; j < n; j += blockDim.x) {
+    uint32_t my_left = 0;
+    for (int j = tid; j < n; j += nthreads) {
       if (rank[j] >= 0) continue;
-      int dec = 0;
-      const uint32_t* row = DT + (int64_t)j * nw;
-      for (int q = 0; q < nz; ++q) {
-        const int w = nzw[q];
-        dec += __popc(row[w] & F[w]);
+      bool free_ = true;
+      for (int w = 0; w < nw; ++w) {
+        const uint32_t d = DW[(int64_t)w * n + j];
+        if (d & ~__hip_atomic_load(&Rc[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { free_ = false; break; }
       }
-      cnt_g[j] -= dec;
+      if (free_) {
+        rank[j] = k;
+        __hip_atomic_fetch_or(&Rn[j >> 5], 1u << (j & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(&ws[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        ++my_left;
+      }
     }
+    if (my_left) atomicAdd(&wg_left, my_left);
     __syncthreads();
+    if (threadIdx.x == 0 && wg_left)
+      __hip_atomic_fetch_add(&left[k], wg_left, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!grid_barrier(ws, gridDim.x, gen)) return;
+    const uint32_t still = __hip_atomic_load(&left[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t done = __hip_atomic_load(&ws[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (still == 0) return;
+    if ((int)done >= limit || k + 1 >= n) {
+      for (int j = tid; j < n; j += nthreads)
+        if (rank[j] < 0) rank[j] = n;
+      return;
+    }
   }
+}
+
+__global__ void __launch_bounds__(256) zero_kernel(uint32_t* __restrict__ p, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = 0u;
 }
 
 }  // namespace
 
-void evx_nds(const float* f, int n, int m, uint32_t* DT, int32_t* rank, int32_t* cnt, hipStream_t s) {
+size_t evx_nds_workspace_words(int n) { return 4 + 2 * (size_t)((n + 31) / 32) + (size_t)n + 1; }
+
+void evx_nds(const float* f, int n, int m, int limit, uint32_t* DW, int32_t* rank, uint32_t* ws, hipStream_t s) {
   const int nw = (n + 31) / 32;
   dim3 grid((n + 255) / 256, nw);
-  if (m == 2) dominance_kernel<2><<<grid, 256, 0, s>>>(f, n, m, nw, DT);
-  else if (m == 3) dominance_kernel<3><<<grid, 256, 0, s>>>(f, n, m, nw, DT);
-  else dominance_kernel<0><<<grid, 256, 0, s>>>(f, n, m, nw, DT);
-  const size_t shm = 2 * (size_t)nw * sizeof(uint32_t);
-  peel_kernel<<<1, 1024, shm, s>>>(DT, n, nw, rank, cnt);
+  if (m == 2) dominance_kernel<2><<<grid, 256, 0, s>>>(f, n, m, nw, DW);
+  else if (m == 3) dominance_kernel<3><<<grid, 256, 0, s>>>(f, n, m, nw, DW);
+  else dominance_kernel<0><<<grid, 256, 0, s>>>(f, n, m, nw, DW);
+  // a kernel, not hipMemsetAsync: the workspace must be zeroed inside captured hipGraphs too
+  const int64_t nws = (int64_t)evx_nds_workspace_words(n);
+  const int zb = (int)((nws + 255) / 256 < 64 ? (nws + 255) / 256 : 64);
+  zero_kernel<<<zb, 256, 0, s>>>(ws, nws);
+  const int blocks = min((n + 255) / 256, 128);
+  peel_kernel<<<blocks, 256, 0, s>>>(DW, n, nw, limit, rank, ws);
 }

@@ -42,9 +42,8 @@ class MOAlgorithm(Algorithm):
 
 def nsga2_select(fitness, n):
     """Indices of the n survivors by (rank, −crowding) (reference ``eagmoead.py:22-30``)."""
-    rank = non_dominated_sort(fitness)
-    order = torch.argsort(rank, stable=True)
-    worst = rank[order[n - 1]]
+    rank = non_dominated_sort(fitness, until=n)
+    worst = torch.sort(rank).values[n - 1]  # 0-d view: no host sync (capturable)
     cd = crowding_distance(fitness, rank == worst)
     return lexsort([-cd, rank.to(cd.dtype)])[:n]
 

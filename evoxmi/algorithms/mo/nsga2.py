@@ -49,9 +49,9 @@ class NSGA2(Algorithm):
     def tell(self, state, fitness):
         merged_pop = torch.cat([state.population, state.next_generation], 0)
         merged_fit = torch.cat([state.fitness, fitness], 0)
-        rank = non_dominated_sort(merged_fit)
-        order = torch.argsort(rank, stable=True)
-        worst = rank[order[self.pop_size]]
+        rank = non_dominated_sort(merged_fit, until=self.pop_size + 1)
+        # the (pop_size)-th smallest rank, read as a 0-d view (no host sync: graph-capturable)
+        worst = torch.sort(rank).values[self.pop_size]
         mask = rank == worst
         cd = crowding_distance(merged_fit, mask)
         keep = lexsort([-cd, rank.to(cd.dtype)])[: self.pop_size]

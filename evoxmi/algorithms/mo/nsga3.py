@@ -42,9 +42,8 @@ class NSGA3(MOAlgorithm):
         merged_pop = torch.cat([state.population, state.next_generation], 0)
         merged_fit = torch.cat([state.fitness, fitness], 0)
         n = merged_fit.shape[0]
-        rank = non_dominated_sort(merged_fit)
-        order = torch.argsort(rank, stable=True)
-        last_rank = rank[order[N]]
+        rank = non_dominated_sort(merged_fit, until=N + 1)
+        last_rank = torch.sort(rank).values[N]  # 0-d view: no host sync (capturable)
         valid = rank <= last_rank
         inf = torch.full_like(merged_fit, float("inf"))
         ideal = torch.where(valid[:, None], merged_fit, inf).min(0).values

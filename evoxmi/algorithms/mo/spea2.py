@@ -44,6 +44,24 @@ def truncation(obj, k, mask):
     return keep & mask
 
 
+def truncation_predicated(obj, k, mask, max_k: int):
+    """``truncation`` with a device-resident removal count ``k`` (≤ ``max_k``)."""
+    n = obj.shape[0]
+    inf = float("inf")
+    dis = torch.cdist(obj, obj)
+    dis = dis.masked_fill(torch.eye(n, dtype=torch.bool, device=obj.device), inf)
+    dis = torch.where(mask[:, None] & mask[None, :], dis, torch.full_like(dis, inf))
+    keep = torch.ones(n, dtype=torch.bool, device=obj.device)
+    col = torch.arange(n, device=obj.device)
+    for step in range(max_k):
+        act = k > step
+        idx = torch.argmin(dis.min(1).values)
+        hit = (col == idx) & act
+        keep = keep & ~hit
+        dis = dis.masked_fill(hit[:, None] | hit[None, :], inf)
+    return keep & mask
+
+
 class SPEA2(MOAlgorithm):
     def __init__(self, lb, ub, n_objs, pop_size, mutation_op=None, crossover_op=None):
         super().__init__(lb, ub, n_objs, pop_size, mutation_op, crossover_op)
@@ -60,11 +78,19 @@ class SPEA2(MOAlgorithm):
         merged_fit = torch.cat([state.fitness, fitness], 0)
         sig = cal_fitness(merged_fit)
         mask = sig < 1
-        num_valid = int(mask.sum())
-        if num_valid <= self.pop_size:
-            order = torch.argsort(sig, stable=True)
+        if merged_fit.is_cuda and torch.cuda.is_current_stream_capturing():
+            # capturable form: the removal count stays on the device; a fixed N-step loop with
+            # predicated updates replaces the data-dependent one, and the branch becomes a select
+            num_valid = mask.sum()
+            keep = truncation_predicated(merged_fit, num_valid - self.pop_size, mask, self.pop_size)
+            key = torch.where(num_valid <= self.pop_size, sig, (~keep).to(sig.dtype))
+            order = torch.argsort(key, stable=True)
         else:
-            keep = truncation(merged_fit, num_valid - self.pop_size, mask)
-            order = torch.argsort((~keep).to(torch.int64), stable=True)
+            num_valid = int(mask.sum())
+            if num_valid <= self.pop_size:
+                order = torch.argsort(sig, stable=True)
+            else:
+                keep = truncation(merged_fit, num_valid - self.pop_size, mask)
+                order = torch.argsort((~keep).to(torch.int64), stable=True)
         idx = order[: self.pop_size]
         return state.update(population=merged_pop[idx], fitness=merged_fit[idx])

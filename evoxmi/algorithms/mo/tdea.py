@@ -65,8 +65,8 @@ class TDEA(MOAlgorithm):
         N, m = self.pop_size, self.n_objs
         pop = torch.cat([state.population, state.next_generation], 0)
         obj = torch.cat([state.fitness, fitness], 0)
-        rank = non_dominated_sort(obj)
-        worst = rank[torch.argsort(rank, stable=True)[N]]
+        rank = non_dominated_sort(obj, until=N + 1)
+        worst = torch.sort(rank).values[N]
         mask = rank <= worst
         z = torch.minimum(state.z, obj.min(0).values)
         w1 = torch.where(torch.eye(m, dtype=torch.bool, device=obj.device), 1.0, 1e-6)

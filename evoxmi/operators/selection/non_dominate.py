@@ -45,13 +45,17 @@ def host_rank_from_domination_matrix(dominate_mat, dominate_count):
     return rank
 
 
-def non_dominated_sort(x: torch.Tensor, method: str = "auto") -> torch.Tensor:
-    """Pareto rank of every row of ``x`` (n, m); 0 = first front (minimisation)."""
+def non_dominated_sort(x: torch.Tensor, method: str = "auto", until: int = 0) -> torch.Tensor:
+    """Pareto rank of every row of ``x`` (n, m); 0 = first front (minimisation).
+
+    ``until`` > 0 (GPU path) stops peeling once at least ``until`` rows are ranked;
+    the remaining rows get rank ``n``.  Selection that keeps the best ``k`` rows only
+    needs ``until = k`` (or ``k + 1`` to also read the rank just past the cut)."""
     assert method in ("auto", "scan", "full map-reduce", "host")
     if x.is_cuda and method in ("auto", "full map-reduce"):
         from ...ops import nds
 
-        return nds.non_dominated_sort(x)
+        return nds.non_dominated_sort(x, until)
     dom = dominate_relation(x, x)
     count = dom.sum(0).to(torch.int32)
     if method == "host":
@@ -112,9 +116,8 @@ def non_dominate(population, fitness, topk: int):
     tie-break key (``non_dominate.py:195-197``); the intent — larger crowding
     distance first — is implemented here.
     """
-    rank = non_dominated_sort(fitness)
-    order = torch.argsort(rank, stable=True)
-    worst_rank = rank[order[topk - 1]]
+    rank = non_dominated_sort(fitness, until=topk)
+    worst_rank = torch.sort(rank).values[topk - 1]
     mask = rank == worst_rank
     cd = crowding_distance(fitness, mask)
     combined = lexsort([-cd, rank.to(cd.dtype)])[:topk]

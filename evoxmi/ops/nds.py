@@ -6,10 +6,12 @@ import torch
 from . import _ext
 
 
-def non_dominated_sort(f: torch.Tensor) -> torch.Tensor:
+def non_dominated_sort(f: torch.Tensor, until: int = 0) -> torch.Tensor:
+    """Pareto ranks; with ``until`` > 0 fronts are peeled only until ≥ ``until`` rows are
+    ranked and the remaining rows get rank ``n`` (larger than every real rank)."""
     f = f.to(torch.float32).contiguous()
     if f.shape[0] <= 65536 and f.shape[1] <= 8:
-        return _ext.ops().nds(f)
+        return _ext.ops().nds(f, int(until))
     from ..operators.selection.non_dominate import _peel
     from ..utils.common import dominate_relation
 
@@ -20,7 +22,7 @@ def non_dominated_sort(f: torch.Tensor) -> torch.Tensor:
 def crowding_distance(costs: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
     """Vectorised over objectives: one batched sort of the (m, n) masked keys."""
     n, m = costs.shape
-    inf = torch.tensor(float("inf"), device=costs.device, dtype=costs.dtype)
+    inf = torch.full((), float("inf"), device=costs.device, dtype=costs.dtype)  # fill kernel, not an H2D copy (capturable)
     nvalid = mask.sum()
     key = torch.where(mask[:, None], costs, inf).T  # (m, n)
     order = torch.argsort(key, dim=1, stable=True)

@@ -70,9 +70,8 @@ class LSMOP(Problem):
             for j in range(self.nk):
                 start = len_ + self.m - 1 + j * sublen
                 acc = acc + func(x[:, start : start + sublen].contiguous())
-            gs.append(acc)
-        g = torch.stack(gs, 1)
-        return g / torch.tensor(self.sublen, dtype=x.dtype, device=x.device)[None, :] / self.nk
+            gs.append(acc / (sublen * self.nk))  # host scalar: no H2D copy (graph-capturable)
+        return torch.stack(gs, 1)
 
     def _link(self, X, cosine: bool):
         n, d = X.shape

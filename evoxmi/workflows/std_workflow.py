@@ -19,7 +19,8 @@ MI355X-first execution model (replaces ``jax.jit`` / ``pmap``):
   returned in graph mode aliases the workflow's static buffers (clone to keep a
   snapshot).  Monitor hooks that consume the step's tensors are replayed on the
   host after each graph launch with the graph's static output buffers, so
-  monitors need not be capture-safe.
+  monitors need not be capture-safe.  ``graph="auto"`` tries the capture once and
+  falls back to eager steps (with a warning) if the step is not capturable.
 * ``enable_distributed(state)`` turns the workflow into an SPMD program with one
   process per GPU (``torch.distributed``; backend ``nccl`` = RCCL over xGMI on
   MI355X, ``gloo`` on CPU).  The algorithm state is replicated; every rank
@@ -60,7 +61,7 @@ class StdWorkflow(Workflow):
         jit_problem: bool = True,
         num_objectives: Optional[int] = None,
         monitor=None,
-        graph: bool = False,
+        graph: Union[bool, str] = False,
         nan_policy: str = "keep",
         phase_timer=None,
     ):
@@ -101,6 +102,7 @@ class StdWorkflow(Workflow):
         self._dim_shard_group = None  # set by enable_multi_devices (decision-axis sharding)
         # graph-mode bookkeeping
         self._graph = None
+        self._graph_failed = False
         self._static = None
         self._static_out = None
         self._hook_args = None
@@ -298,8 +300,20 @@ class StdWorkflow(Workflow):
     def step(self, state: State) -> State:
         for m in self.registered_hooks["pre_step"]:
             m.pre_step(state)
-        if self.graph and not (self._has_init_ask and state.generation == 0):
-            state = self._step_graph(state)
+        if self.graph and not self._graph_failed and not (self._has_init_ask and state.generation == 0):
+            if self.graph == "auto" and self._graph is None:
+                try:
+                    state = self._step_graph(state)
+                except (RuntimeError, torch.AcceleratorError) as e:
+                    # capture-unsafe step (host sync / H2D copy / data-dependent shape):
+                    # the capture was invalidated, the input state is untouched — run eagerly from now on
+                    self._graph_failed = True
+                    self._graph = None
+                    torch.cuda.synchronize()
+                    warnings.warn(f"graph='auto': {type(self.algorithm).__name__} step is not capturable ({str(e).splitlines()[0]}); running eagerly")
+                    state = self._step_eager(state)
+            else:
+                state = self._step_graph(state)
         else:
             state = self._step_eager(state)
         for m in self.registered_hooks["post_step"]:

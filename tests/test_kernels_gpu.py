@@ -250,6 +250,40 @@ def test_nds_kernel_matches_cpu(n, m):
     assert torch.equal(out.to(torch.int32), ref.to(torch.int32))
 
 
+@pytest.mark.parametrize("n,m,until", [(8192, 3, 4097), (2000, 2, 700), (700, 4, 1)])
+def test_nds_kernel_until(n, m, until):
+    """Peeling stops once >= `until` rows are ranked: those ranks are exact, the rest get n."""
+    from evoxmi.operators.selection import non_dominated_sort
+
+    f = torch.rand(n, m, generator=torch.Generator().manual_seed(n + m))
+    ref = non_dominated_sort(f).to(torch.int32)
+    out = non_dominated_sort(f.cuda(), until=until).cpu()
+    cut = int(torch.sort(ref).values[until - 1])
+    exact = ref <= cut
+    assert torch.equal(out[exact], ref[exact])
+    assert (out[~exact] == n).all()
+
+
+def test_nds_under_graph_capture():
+    from evoxmi.operators.selection import non_dominated_sort
+
+    x = torch.rand(3000, 3, device="cuda")
+    out = torch.empty(3000, dtype=torch.int32, device="cuda")
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        non_dominated_sort(x)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        out.copy_(non_dominated_sort(x))
+    for seed in range(3):
+        x.copy_(torch.rand(3000, 3, generator=torch.Generator().manual_seed(seed)).cuda())
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out.cpu(), non_dominated_sort(x.cpu()).to(torch.int32))
+
+
 def test_crowding_gpu_matches_cpu():
     from evoxmi.operators.selection import crowding_distance
 
