@@ -234,7 +234,7 @@ void gemm_set_config(int64_t cfg) { evx_gemm_set_config((int)cfg); }
 at::Tensor sbx(const at::Tensor& x, const at::Tensor& keys, double pro_c, double dis_c, int64_t type) {
   CHECK_DEV(x); CHECK_F32(x); CHECK_CONTIG(x); CHECK_DEV(keys);
   TORCH_CHECK(x.dim() == 2, "x must be (n, d)");
-  TORCH_CHECK(keys.scalar_type() == at::kLong && keys.is_contiguous() && keys.numel() == 8, "keys must be int64[4,2]");
+  TORCH_CHECK(keys.scalar_type() == at::kLong && keys.is_contiguous() && keys.numel() == 4, "keys must be int64[2,2]");
   TORCH_CHECK(type == 1 || type == 2, "type must be 1 or 2");
   const int64_t n = x.size(0), d = x.size(1);
   c10::DeviceGuard g(x.device());
@@ -373,6 +373,76 @@ std::vector<at::Tensor> ant_rollout(const at::Tensor& W, int64_t h1, int64_t h2,
   return {ret, steps};
 }
 
+std::vector<at::Tensor> moead_parents(const at::Tensor& nb, const at::Tensor& key) {
+  CHECK_DEV(nb); CHECK_CONTIG(nb); check_key(key);
+  TORCH_CHECK(nb.dim() == 2 && nb.scalar_type() == at::kLong && nb.size(1) >= 1 && nb.size(1) < 65536, "neighbours must be int64 (N, T), T < 65536");
+  c10::DeviceGuard g(nb.device());
+  const int64_t N = nb.size(0);
+  auto p0 = at::empty({N}, nb.options().dtype(at::kInt)), p1 = at::empty({N}, nb.options().dtype(at::kInt));
+  if (N > 0) evx_moead_parents(nb.data_ptr<int64_t>(), (int)N, (int)nb.size(1), key.data_ptr<int64_t>(), p0.data_ptr<int>(), p1.data_ptr<int>(), cur_stream());
+  return {p0, p1};
+}
+
+at::Tensor moead_variation(const at::Tensor& pop, const at::Tensor& p0, const at::Tensor& p1, const at::Tensor& kx, const at::Tensor& km,
+                           const at::Tensor& lb, const at::Tensor& ub, double pro_c, double dis_c, double pro_m, double dis_m, int64_t nm) {
+  for (auto* t : {&pop, &lb, &ub}) { CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t); }
+  for (auto* t : {&p0, &p1}) { CHECK_DEV(*t); CHECK_CONTIG(*t); TORCH_CHECK(t->scalar_type() == at::kInt, "parents must be int32"); }
+  TORCH_CHECK(kx.scalar_type() == at::kLong && kx.numel() == 4 && kx.is_contiguous() && kx.is_cuda(), "kx must be int64[2][2] on device");
+  TORCH_CHECK(km.scalar_type() == at::kLong && km.numel() == 4 && km.is_contiguous() && km.is_cuda(), "km must be int64[2][2] on device");
+  TORCH_CHECK(pop.dim() == 2 && lb.numel() == pop.size(1) && ub.numel() == pop.size(1), "bounds must be (d,)");
+  const int64_t N = p0.numel(), d = pop.size(1);
+  TORCH_CHECK(p1.numel() == N, "p0/p1 length mismatch");
+  c10::DeviceGuard g(pop.device());
+  auto out = at::empty({N, d}, pop.options());
+  if (N > 0 && d > 0)
+    evx_moead_variation(pop.data_ptr<float>(), p0.data_ptr<int>(), p1.data_ptr<int>(), out.data_ptr<float>(), (int)N, (int)d, kx.data_ptr<int64_t>(),
+                        km.data_ptr<int64_t>(), lb.data_ptr<float>(), ub.data_ptr<float>(), (float)pro_c, (float)dis_c, (float)pro_m, (float)dis_m,
+                        (int)nm, cur_stream());
+  return out;
+}
+
+std::vector<at::Tensor> moead_replace(const at::Tensor& pop_obj, const at::Tensor& off_obj, const at::Tensor& W, const at::Tensor& z,
+                                      const at::Tensor& zmax, const at::Tensor& rowptr, const at::Tensor& owner, int64_t func) {
+  for (auto* t : {&pop_obj, &off_obj, &W, &z, &zmax}) { CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t); }
+  for (auto* t : {&rowptr, &owner}) { CHECK_DEV(*t); CHECK_CONTIG(*t); TORCH_CHECK(t->scalar_type() == at::kInt, "CSR must be int32"); }
+  const int64_t N = pop_obj.size(0), M = pop_obj.size(1);
+  TORCH_CHECK(M >= 1 && M <= 16 && W.size(0) == N && W.size(1) == M && off_obj.size(1) == M && z.numel() == M && zmax.numel() == M, "shape mismatch");
+  TORCH_CHECK(rowptr.numel() == N + 1 && func >= 0 && func <= 4, "rowptr must be (N+1,), func 0..4");
+  c10::DeviceGuard g(pop_obj.device());
+  auto win = at::empty({N}, pop_obj.options().dtype(at::kInt));
+  auto new_obj = at::empty_like(pop_obj);
+  if (N > 0)
+    evx_moead_replace(pop_obj.data_ptr<float>(), off_obj.data_ptr<float>(), W.data_ptr<float>(), z.data_ptr<float>(), zmax.data_ptr<float>(),
+                      rowptr.data_ptr<int>(), owner.data_ptr<int>(), (int)N, (int)M, (int)func, win.data_ptr<int>(), new_obj.data_ptr<float>(), cur_stream());
+  return {win, new_obj};
+}
+
+at::Tensor moead_select_rows(const at::Tensor& pop, const at::Tensor& off, const at::Tensor& win) {
+  for (auto* t : {&pop, &off}) { CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t); }
+  CHECK_DEV(win); TORCH_CHECK(win.scalar_type() == at::kInt && win.numel() == pop.size(0), "win must be int32 (N,)");
+  TORCH_CHECK(off.size(1) == pop.size(1), "row width mismatch");
+  c10::DeviceGuard g(pop.device());
+  auto out = at::empty_like(pop);
+  if (pop.numel() > 0)
+    evx_moead_select_rows(pop.data_ptr<float>(), off.data_ptr<float>(), win.data_ptr<int>(), out.data_ptr<float>(), (int)pop.size(0), (int)pop.size(1), cur_stream());
+  return out;
+}
+
+at::Tensor lsmop_g(const at::Tensor& X, std::vector<int64_t> start, std::vector<int64_t> sublen, std::vector<int64_t> func, int64_t nk, int64_t cosine) {
+  CHECK_DEV(X); CHECK_F32(X); CHECK_CONTIG(X);
+  const int64_t ng = (int64_t)start.size();
+  TORCH_CHECK(X.dim() == 2 && ng >= 1 && ng <= 16 && (int64_t)sublen.size() == ng && (int64_t)func.size() == ng && nk >= 1, "lsmop_g: bad groups");
+  std::vector<int> s32(ng), l32(ng), f32(ng);
+  for (int64_t k = 0; k < ng; ++k) {
+    TORCH_CHECK(start[k] >= 1 && sublen[k] >= 0 && start[k] + nk * sublen[k] <= X.size(1) && func[k] >= 0 && func[k] <= 5, "lsmop_g: group out of range");
+    s32[k] = (int)start[k]; l32[k] = (int)sublen[k]; f32[k] = (int)func[k];
+  }
+  c10::DeviceGuard g(X.device());
+  auto G = at::empty({X.size(0), ng}, X.options());
+  if (X.size(0) > 0) evx_lsmop_g(X.data_ptr<float>(), G.data_ptr<float>(), (int)X.size(0), (int)X.size(1), (int)ng, (int)nk, (int)cosine, s32.data(), l32.data(), f32.data(), cur_stream());
+  return G;
+}
+
 }  // namespace
 
 TORCH_LIBRARY(evoxmi, m) {
@@ -393,6 +463,11 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("dtlz(Tensor X, int m, int variant) -> Tensor");
   m.def("classic_eval(Tensor X, int func, float a, float b, float c) -> Tensor");
   m.def("gemm_f32(Tensor A, int a_rc, Tensor? a_gather, Tensor? a_sub, int a_sub_on_k, Tensor? a_kscale, Tensor? a_kw, Tensor? a_sscale, int a_sscale_inv, Tensor B, int b_rc, Tensor? b_gather, Tensor? b_sub, int b_sub_on_k, Tensor? b_kscale, Tensor? b_kw, Tensor? b_sscale, int b_sscale_inv, Tensor? alpha_ptr, Tensor? bias_n, float beta, Tensor? Cin, int M, int N, int K, int splits, float alpha) -> Tensor");
+  m.def("lsmop_g(Tensor X, int[] start, int[] sublen, int[] func, int nk, int cosine) -> Tensor");
+  m.def("moead_parents(Tensor nb, Tensor key) -> Tensor[]");
+  m.def("moead_variation(Tensor pop, Tensor p0, Tensor p1, Tensor kx, Tensor km, Tensor lb, Tensor ub, float pro_c, float dis_c, float pro_m, float dis_m, int nm) -> Tensor");
+  m.def("moead_replace(Tensor pop_obj, Tensor off_obj, Tensor W, Tensor z, Tensor zmax, Tensor rowptr, Tensor owner, int func) -> Tensor[]");
+  m.def("moead_select_rows(Tensor pop, Tensor off, Tensor win) -> Tensor");
   m.def("pso_update(Tensor pop, Tensor vel, Tensor lbl, Tensor lbf, Tensor fit, Tensor gbl, Tensor kp, Tensor kg, float w, float phip, float phig, Tensor lb, Tensor ub) -> Tensor[]");
 }
 
@@ -418,4 +493,9 @@ TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
   m.impl("argsort_f32", &argsort_f32);
   m.impl("gemm_f32", &gemm_f32);
   m.impl("pso_update", &pso_update);
+  m.impl("lsmop_g", &lsmop_g);
+  m.impl("moead_parents", &moead_parents);
+  m.impl("moead_variation", &moead_variation);
+  m.impl("moead_replace", &moead_replace);
+  m.impl("moead_select_rows", &moead_select_rows);
 }

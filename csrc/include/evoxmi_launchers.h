@@ -49,3 +49,15 @@ void evx_moead_scan(float* objs, const float* off_objs, const int32_t* P, const 
 void evx_ant_rollout(const float* W, int64_t P, int N, int h1, int h2, const float* init, int cap, float* ret, int* steps, hipStream_t s);
 size_t evx_nds_workspace_words(int n);
 void evx_nds(const float* f, int n, int m, int limit, uint32_t* DW, int32_t* rank, uint32_t* ws, hipStream_t s);
+
+// moead.hip
+void evx_moead_parents(const int64_t* nb, int N, int T, const int64_t* key, int32_t* p0, int32_t* p1, hipStream_t s);
+void evx_moead_variation(const float* pop, const int32_t* p0, const int32_t* p1, float* out, int N, int d, const int64_t* kx,
+                         const int64_t* km, const float* lb, const float* ub, float pro_c, float dis_c, float pro_m, float dis_m,
+                         int nm, hipStream_t s);
+void evx_moead_replace(const float* pop_obj, const float* off_obj, const float* W, const float* z, const float* zmax,
+                       const int32_t* rowptr, const int32_t* owner, int N, int M, int func, int32_t* win, float* new_obj,
+                       hipStream_t s);
+void evx_moead_select_rows(const float* pop, const float* off, const int32_t* win, float* out, int N, int d, hipStream_t s);
+void evx_lsmop_g(const float* X, float* G, int N, int D, int ng, int nk, int cosine, const int* start, const int* sublen, const int* func,
+                 hipStream_t s);

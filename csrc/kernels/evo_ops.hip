@@ -12,27 +12,44 @@ __device__ __forceinline__ uint32_t word_at(uint64_t i, uint32_t k0, uint32_t k1
   return ws[i & 3];
 }
 
-// keys: 4 consecutive keys (int64[4][2]) = split(key, 4) → mu, b1, b2, b3
+// keys: split(key, 2) → per-gene word (μ = top 24 bits, bit 0 = sign of β, bit 1 = skip),
+// per-pair rate uniform.  One thread per 4 consecutive genes when they share a Philox
+// block (d % 4 == 0), else one gene per thread.
+__device__ __forceinline__ float sbx_beta(uint32_t w, float e) {
+  const float mu = evx::u24(w);
+  float beta = mu <= 0.5f ? exp2f(e * __log2f(2.f * mu)) : exp2f(-e * __log2f(2.f - 2.f * mu));
+  if (w & 1u) beta = -beta;
+  if (w & 2u) beta = 1.f;
+  return beta;
+}
+
 __global__ void __launch_bounds__(256) sbx_kernel(const float* __restrict__ x, float* __restrict__ out, int n, int d,
                                                   const int64_t* __restrict__ keys, float pro_c, float dis_c, int type) {
   const int np = n / 2;
-  const int64_t total = (int64_t)np * d;
-  uint32_t km0 = (uint32_t)keys[0], km1 = (uint32_t)keys[1];
-  uint32_t ka0 = (uint32_t)keys[2], ka1 = (uint32_t)keys[3];
-  uint32_t kb0 = (uint32_t)keys[4], kb1 = (uint32_t)keys[5];
-  uint32_t kc0 = (uint32_t)keys[6], kc1 = (uint32_t)keys[7];
+  const uint32_t kg0 = (uint32_t)keys[0], kg1 = (uint32_t)keys[1];
+  const uint32_t kp0 = (uint32_t)keys[2], kp1 = (uint32_t)keys[3];
   const float e = 1.f / (dis_c + 1.f);
+  const int vec = (d & 3) == 0 ? 4 : 1;
+  const int64_t total = (int64_t)np * d / vec;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    const int i = (int)(t / d), j = (int)(t - (int64_t)i * d);
-    const float p1 = x[(int64_t)i * d + j], p2 = x[(int64_t)(np + i) * d + j];
-    const float mu = evx::u24(word_at((uint64_t)t, km0, km1));
-    float beta = mu <= 0.5f ? powf(2.f * mu, e) : powf(2.f - 2.f * mu, -e);
-    if (word_at((uint64_t)t, ka0, ka1) >> 31) beta = -beta;
-    if (evx::u24(word_at((uint64_t)t, kb0, kb1)) < 0.5f) beta = 1.f;
-    if (evx::u24(word_at((uint64_t)i, kc0, kc1)) > pro_c) beta = 1.f;
-    const float mid = 0.5f * (p1 + p2), half = 0.5f * (p1 - p2);
-    out[(int64_t)i * d + j] = mid + beta * half;
-    if (type == 1) out[(int64_t)(np + i) * d + j] = mid - beta * half;
+    const int64_t g0 = t * vec;
+    const int i = (int)(g0 / d), j0 = (int)(g0 - (int64_t)i * d);
+    const bool no_x = evx::u24(word_at((uint64_t)i, kp0, kp1)) > pro_c;
+    uint32_t ws[4];
+    if (vec == 4) {
+      const evx::u4 w = evx::philox_block((uint64_t)g0 >> 2, kg0, kg1);
+      ws[0] = w.x; ws[1] = w.y; ws[2] = w.z; ws[3] = w.w;
+    } else {
+      ws[0] = word_at((uint64_t)g0, kg0, kg1);
+    }
+    for (int v = 0; v < vec; ++v) {
+      const int j = j0 + v;
+      const float p1 = x[(int64_t)i * d + j], p2 = x[(int64_t)(np + i) * d + j];
+      const float beta = no_x ? 1.f : sbx_beta(ws[v], e);
+      const float mid = 0.5f * (p1 + p2), half = 0.5f * (p1 - p2);
+      out[(int64_t)i * d + j] = mid + beta * half;
+      if (type == 1) out[(int64_t)(np + i) * d + j] = mid - beta * half;
+    }
   }
   if (type == 1 && (n & 1)) {  // odd population: last parent passes through
     for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < d; j += gridDim.x * blockDim.x)
@@ -56,8 +73,8 @@ __global__ void __launch_bounds__(256) pm_kernel(const float* __restrict__ x, fl
       const float lo = lb[j], hi = ub[j], span = hi - lo;
       v = fmaxf(fminf(v, hi), lo);
       const bool site = evx::u24(word_at((uint64_t)t, ks0, ks1)) < pr;
-      const float mu = evx::u24(word_at((uint64_t)t, ku0, ku1));
       if (site) {
+        const float mu = evx::u24(word_at((uint64_t)t, ku0, ku1));  // drawn only at mutation sites
         if (mu <= 0.5f) {
           const float nrm = (v - lo) / span;
           v = v + span * (powf(2.f * mu + (1.f - 2.f * mu) * powf(1.f - nrm, e1), inv) - 1.f);

@@ -47,7 +47,92 @@ __global__ void __launch_bounds__(256) dtlz_kernel(const float* __restrict__ X, 
   }
 }
 
+// ---------------------------------------------------------------- LSMOP1–9 distance terms (K14)
+// One wave64 per row computes g_k for every objective group k straight from the RAW
+// decision row: the linkage x̃_c = (1 + t_c)·x_c − 10·x_0 (t_c = (c+1)/d, or
+// cos(π(c+1)/(2d)) for LSMOP5–9) is applied in-register, each of the nk subcomponent
+// segments is reduced by the wave (sum / second sum / product / max as the inner
+// function needs), and g_k = Σ_sub f(segment) / (sublen_k · nk).  The (n, d) matrix is
+// read once; the linked copy and the 15 strided segment copies of the eager path vanish.
+constexpr int LS_MAXG = 16;
+struct LsmopGroups {
+  int start[LS_MAXG], sublen[LS_MAXG], func[LS_MAXG];
+  int ng, nk, cosine;
+};
+
+__device__ __forceinline__ float wave_reduce(float v, int op) {  // op 0 sum, 1 prod, 2 max
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float u = __shfl_xor(v, o, 64);
+    v = op == 0 ? v + u : (op == 1 ? v * u : fmaxf(v, u));
+  }
+  return v;
+}
+
+// one wave64 per row (no block barriers: every reduction is a 6-step xor butterfly)
+__global__ void __launch_bounds__(256) lsmop_g_kernel(const float* __restrict__ X, float* __restrict__ G, int N, int D, LsmopGroups gr) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= N) return;
+  const float* x = X + (int64_t)row * D;
+  const float x0 = x[0];
+  const float invd = 1.f / (float)D;
+  auto link = [&](int c) {
+    const float t = gr.cosine ? cosf((float)(c + 1) * invd * (PI_F * 0.5f)) : (float)(c + 1) * invd;
+    return (1.f + t) * x[c] - 10.f * x0;
+  };
+  float gout = 0.f;
+  for (int k = 0; k < gr.ng; ++k) {
+    const int L = gr.sublen[k], fn = gr.func[k];
+    float gk = 0.f;
+    for (int sub = 0; sub < gr.nk; ++sub) {
+      const int s0 = gr.start[k] + sub * L;
+      float a = 0.f, b = (fn == 1) ? 1.f : 0.f;
+      for (int i = lane; i < L; i += 64) {
+        const float z = link(s0 + i);
+        switch (fn) {
+          case 0: a += z * z; break;                                                     // sphere
+          case 1: a += z * z; b *= cosf(z * rsqrtf((float)(i + 1))); break;              // griewank
+          case 2: if (i + 1 < L) { const float zn = link(s0 + i + 1), u = zn - z * z;    // rosenbrock
+                    a += 100.f * u * u + (z - 1.f) * (z - 1.f); } break;
+          case 3: a += z * z; b += cosf(2.f * PI_F * z); break;                          // ackley
+          case 4: a = fmaxf(a, fabsf(z)); break;                                         // schwefel (max |z|)
+          default: a += z * z - 10.f * cosf(2.f * PI_F * z) + 10.f; break;               // rastrigin
+        }
+      }
+      float v;
+      if (fn == 4) {
+        v = wave_reduce(a, 2);
+      } else if (fn == 1) {
+        v = wave_reduce(a, 0) / 4000.f - wave_reduce(b, 1) + 1.f;
+      } else if (fn == 3) {
+        const float sa = wave_reduce(a, 0), sb = wave_reduce(b, 0);
+        v = -20.f * expf(-0.2f * sqrtf(sa / (float)L)) - expf(sb / (float)L) + 20.f + 2.718281828459045f;
+      } else {
+        v = wave_reduce(a, 0);
+      }
+      gk += v;
+    }
+    if (lane == k) gout = gk / (float)(L * gr.nk);
+  }
+  if (lane < gr.ng) G[(int64_t)row * gr.ng + lane] = gout;
+}
+
 }  // namespace
+
+void evx_lsmop_g(const float* X, float* G, int N, int D, int ng, int nk, int cosine, const int* start, const int* sublen, const int* func,
+                 hipStream_t s) {
+  LsmopGroups gr;
+  gr.ng = ng;
+  gr.nk = nk;
+  gr.cosine = cosine;
+  for (int k = 0; k < ng && k < LS_MAXG; ++k) {
+    gr.start[k] = start[k];
+    gr.sublen[k] = sublen[k];
+    gr.func[k] = func[k];
+  }
+  lsmop_g_kernel<<<(N + 3) / 4, 256, 0, s>>>(X, G, N, D, gr);
+}
 
 void evx_dtlz(const float* X, float* F, int N, int D, int M, int variant, hipStream_t s) {
   const dim3 block(256), grid((N + 3) / 4);

@@ -99,6 +99,7 @@ class MOEAD(Algorithm):
         self.sample = UniformSampling(self.pop_size, self.n_objs)
         self.aggregate_func = AggregationFunction(self.func_name)
         self._rev = None
+        self._rev32 = None
 
     def setup(self, key):
         key, k1, k2 = rnd.split(key, 3)
@@ -131,8 +132,22 @@ class MOEAD(Algorithm):
         perm = torch.argsort(rnd.uniform(key, (n, T)).to(state.neighbors.device), dim=1, stable=True)[:, :2]
         return torch.gather(state.neighbors, 1, perm)
 
+    def _fused(self, x):
+        """The default SBX(type 2) + PM pipeline runs as the fused moead.hip kernels on a GPU."""
+        c, m = self.crossover, self.mutation
+        return (x.is_cuda and x.dtype == torch.float32 and self.dim > 0
+                and type(c) is crossover.SimulatedBinary and c.type == 2
+                and type(m) is mutation.Polynomial and m.boundary[0] is self.lb and m.boundary[1] is self.ub)
+
     def ask(self, state):
         key, sub, sel_key, mut_key = rnd.split(state.key, 4)
+        if self._fused(state.population):
+            from ...ops import mo as mo_ops
+
+            p0, p1 = mo_ops.moead_parents(state.neighbors, sub)
+            c, m = self.crossover, self.mutation
+            off = mo_ops.moead_variation(state.population, p0, p1, sel_key, mut_key, self.lb, self.ub, c.pro_c, c.dis_c, m.pro_m, m.dis_m)
+            return off, state.update(next_generation=off, key=key)
         parent = self._parents(state, sub)
         pop = state.population
         selected = torch.cat([pop[parent[:, 0]], pop[parent[:, 1]]], 0)
@@ -149,6 +164,15 @@ class MOEAD(Algorithm):
     def tell(self, state, fitness):
         z = torch.minimum(state.z, fitness.min(0).values)
         z_max = state.fitness.max(0).values
+        if fitness.is_cuda and state.population.dtype == torch.float32:
+            from ...ops import mo as mo_ops
+
+            rowptr, _, owner = self._reverse(state)
+            if self._rev32 is None or self._rev32[0].data_ptr() != rowptr.data_ptr():
+                self._rev32 = (rowptr, rowptr.to(torch.int32), owner.to(torch.int32))
+            win, new_obj = mo_ops.moead_replace(state.fitness, fitness, state.weight_vector, z, z_max, self._rev32[1], self._rev32[2], self.func_name)
+            new_pop = mo_ops.moead_select_rows(state.population, state.next_generation, win)
+            return state.update(population=new_pop, fitness=new_obj, z=z)
         win, new_obj = moead_replace(state.fitness, fitness, state.weight_vector, z, z_max, self.aggregate_func, self._reverse(state))
         new_pop = torch.where((win >= 0)[:, None], state.next_generation[win.clamp_min(0)], state.population)
         return state.update(population=new_pop, fitness=new_obj, z=z)

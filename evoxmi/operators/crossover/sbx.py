@@ -9,22 +9,29 @@ from ...ops import random as rnd
 
 def simulated_binary(key, x, pro_c=1.0, dis_c=20.0, type=1):
     """PlatEMO SBX: first half × second half; ``type=1`` → 2 children per pair
-    (+ the odd last row passes through), ``type=2`` → 1 child per pair."""
+    (+ the odd last row passes through), ``type=2`` → 1 child per pair.
+
+    Random streams (shared bit-for-bit with the HIP kernels): ``split(key, 2)`` →
+    a per-gene word ``w`` whose top 24 bits give μ, bit 0 the sign of β and bit 1
+    the 50 % "no crossover on this gene" coin; and a per-pair uniform compared with
+    ``pro_c``.  One Philox word per gene instead of three."""
     if x.is_cuda and x.dtype == torch.float32:
         from ...ops import evo as evo_ops
 
         return evo_ops.sbx(key, x, float(pro_c), float(dis_c), int(type))
-    mu_key, b1, b2, b3 = rnd.split(key, 4)
+    gene_key, pair_key = rnd.split(key, 2)
     n, d = x.shape
     p1 = x[: n // 2]
     p2 = x[n // 2 : n // 2 * 2]
     n_p = p1.shape[0]
     dev = x.device
-    mu = rnd.uniform(mu_key, (n_p, d)).to(dev)
+    w = rnd.bits(gene_key, (n_p, d)).to(dev)
+    mu = rnd._u24(w)
     beta = torch.where(mu <= 0.5, (2 * mu) ** (1 / (dis_c + 1)), (2 - 2 * mu) ** (-1 / (dis_c + 1)))
-    beta = beta * (1 - 2 * rnd.randint(b1, (n_p, d), 0, 2).to(dev).to(x.dtype))
-    beta = torch.where(rnd.uniform(b2, (n_p, d)).to(dev) < 0.5, torch.ones_like(beta), beta)
-    beta = torch.where((rnd.uniform(b3, (n_p, 1)).to(dev) > pro_c).expand(n_p, d), torch.ones_like(beta), beta)
+    beta = torch.where((w & 1) == 1, -beta, beta)
+    beta = torch.where(((w >> 1) & 1) == 1, torch.ones_like(beta), beta)
+    beta = torch.where((rnd.uniform(pair_key, (n_p, 1)).to(dev) > pro_c).expand(n_p, d), torch.ones_like(beta), beta)
+    beta = beta.to(x.dtype)
     mid, half = (p1 + p2) / 2, (p1 - p2) / 2
     if type == 1:
         off = torch.cat([mid + beta * half, mid - beta * half], 0)

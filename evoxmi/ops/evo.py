@@ -10,7 +10,7 @@ from . import random as rnd
 
 
 def sbx(key, x, pro_c, dis_c, type):
-    keys = rnd.split(key, 4).contiguous()
+    keys = rnd.split(key, 2).contiguous()
     return _ext.ops().sbx(x.contiguous(), keys, float(pro_c), float(dis_c), int(type))
 
 

@@ -46,3 +46,40 @@ def moead_scan(objs, off_objs, P, W, z, func="tchebycheff", nr=None, update_z=Fa
         o[sel] = fo
         owner[sel] = i
     return owner, o, zz
+
+
+# ---------------------------------------------------------------- MOEA/D generation (moead.hip)
+MOEAD_FUNCS = {"tchebycheff": 0, "pbi": 1, "weighted_sum": 2, "modified_tchebycheff": 3, "tchebycheff_norm": 4}
+
+
+def moead_parents(neighbors: torch.Tensor, key: torch.Tensor):
+    """First two columns of a per-row random permutation of ``neighbors`` (N, T):
+    the rows' two smallest ``uniform(key, (N, T))`` entries, ties by column index
+    (= ``argsort(uniform, stable=True)[:, :2]``).  Returns int32 (p0, p1)."""
+    return _ext.ops().moead_parents(neighbors.to(torch.int64).contiguous(), key.contiguous())
+
+
+def moead_variation(pop, p0, p1, key_x, key_m, lb, ub, pro_c, dis_c, pro_m, dis_m):
+    """clip(PM(SBX_type2(pop[p0], pop[p1]))) in one pass; ``key_x``/``key_m`` are the keys
+    ``SimulatedBinary`` / ``Polynomial`` would receive (bit-identical results)."""
+    from . import random as rnd
+
+    n, d = p0.numel(), pop.shape[1]
+    nm = n if n == 1 else (n // 2) * 2
+    lb = lb.to(device=pop.device, dtype=torch.float32).expand(d).contiguous()
+    ub = ub.to(device=pop.device, dtype=torch.float32).expand(d).contiguous()
+    return _ext.ops().moead_variation(pop.contiguous(), p0, p1, rnd.split(key_x, 2).contiguous(), rnd.split(key_m, 2).contiguous(),
+                                      lb, ub, float(pro_c), float(dis_c), float(pro_m), float(dis_m), int(nm))
+
+
+def moead_replace(pop_obj, off_obj, w, z, z_max, rowptr, owner, func):
+    """Winner offspring per slot (or −1) and the new objective matrix — the exact parallel
+    form of the reference's sequential replacement scan (see algorithms/mo/moead.py)."""
+    fid = MOEAD_FUNCS[func] if isinstance(func, str) else int(func)
+    f32 = lambda t: t.to(torch.float32).contiguous()
+    return _ext.ops().moead_replace(f32(pop_obj), f32(off_obj), f32(w), f32(z), f32(z_max), rowptr, owner, fid)
+
+
+def moead_select_rows(pop, off, win):
+    """pop'[s] = off[win[s]] if win[s] >= 0 else pop[s]."""
+    return _ext.ops().moead_select_rows(pop.contiguous(), off.contiguous(), win.to(torch.int32).contiguous())

@@ -34,6 +34,9 @@ def _ackley(X):
     return ackley_func(20.0, 0.2, 2 * math.pi, X)
 
 
+_FUNC_ID = {sphere_func: 0, griewank_func: 1, rosenbrock_func: 2, _ackley: 3, _schwefel: 4, _rastrigin: 5}
+
+
 class LSMOP(Problem):
     _late_d = True  # groups computed with d = 100·m when d is None, then d = m + 4
 
@@ -61,6 +64,17 @@ class LSMOP(Problem):
 
     def pf(self):
         return UniformSampling(self.ref_num * self.m, self.m)()[0] / 2
+
+    def _g(self, inner_funcs, X, cosine: bool):
+        """Distance terms g (n, m) from the RAW decisions: on a GPU one fused pass
+        (``mo_problems.hip: lsmop_g_kernel``), else link + grouped reductions."""
+        if X.is_cuda and X.dtype == torch.float32 and 2 <= self.m <= 16 and self.len[self.m] + self.m - 1 <= X.shape[1]:
+            from ...ops import _ext
+
+            funcs = [_FUNC_ID[f] for _, f in zip(range(self.m), cycle(inner_funcs))]
+            starts = [self.len[k] + self.m - 1 for k in range(self.m)]
+            return _ext.ops().lsmop_g(X.contiguous(), starts, list(self.sublen), funcs, self.nk, int(cosine))
+        return self._calc_g(inner_funcs, self._link(X, cosine))
 
     def _calc_g(self, inner_funcs, x):
         n = x.shape[0]
@@ -99,28 +113,24 @@ class LSMOP(Problem):
 
 class LSMOP1(LSMOP):
     def evaluate(self, state, X):
-        X = self._link(X, False)
-        return self._linear_front(X, self._calc_g([sphere_func], X)), state
+        return self._linear_front(X, self._g([sphere_func], X, False)), state
 
 
 class LSMOP2(LSMOP):
     def evaluate(self, state, X):
-        X = self._link(X, False)
-        return self._linear_front(X, self._calc_g([griewank_func, _schwefel], X)), state
+        return self._linear_front(X, self._g([griewank_func, _schwefel], X, False)), state
 
 
 class LSMOP3(LSMOP):
     _late_d = False
 
     def evaluate(self, state, X):
-        X = self._link(X, False)
-        return self._linear_front(X, self._calc_g([_rastrigin, rosenbrock_func], X)), state
+        return self._linear_front(X, self._g([_rastrigin, rosenbrock_func], X, False)), state
 
 
 class LSMOP4(LSMOP):
     def evaluate(self, state, X):
-        X = self._link(X, False)
-        return self._linear_front(X, self._calc_g([_ackley, griewank_func], X)), state
+        return self._linear_front(X, self._g([_ackley, griewank_func], X, False)), state
 
 
 class _SphericalPF:
@@ -131,33 +141,28 @@ class _SphericalPF:
 
 class LSMOP5(_SphericalPF, LSMOP):
     def evaluate(self, state, X):
-        X = self._link(X, True)
-        return self._spherical_front(X, self._calc_g([sphere_func], X)), state
+        return self._spherical_front(X, self._g([sphere_func], X, True)), state
 
 
 class LSMOP6(LSMOP):
     def evaluate(self, state, X):
-        X = self._link(X, True)
-        return self._spherical_front(X, self._calc_g([rosenbrock_func, _schwefel], X)), state
+        return self._spherical_front(X, self._g([rosenbrock_func, _schwefel], X, True)), state
 
 
 class LSMOP7(_SphericalPF, LSMOP):
     def evaluate(self, state, X):
-        X = self._link(X, True)
-        return self._spherical_front(X, self._calc_g([_ackley, rosenbrock_func], X)), state
+        return self._spherical_front(X, self._g([_ackley, rosenbrock_func], X, True)), state
 
 
 class LSMOP8(_SphericalPF, LSMOP):
     def evaluate(self, state, X):
-        X = self._link(X, True)
-        return self._spherical_front(X, self._calc_g([griewank_func, sphere_func], X)), state
+        return self._spherical_front(X, self._g([griewank_func, sphere_func], X, True)), state
 
 
 class LSMOP9(LSMOP):
     def evaluate(self, state, X):
         m = self.m
-        X = self._link(X, True)
-        g = 1 + self._calc_g([sphere_func, _ackley], X).sum(1, keepdim=True)
+        g = 1 + self._g([sphere_func, _ackley], X, True).sum(1, keepdim=True)
         fm = X[:, : m - 1]
         last = (1 + g) * (m - (fm / (1 + g) * (1 + torch.sin(3 * math.pi * fm))).sum(1, keepdim=True))
         return torch.cat([fm, last], 1), state

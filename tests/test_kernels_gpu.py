@@ -504,3 +504,70 @@ def test_ant_rollout_long_episode_statistics():
     # chaotic dynamics: individual returns may diverge late in the episode, the population statistics must not
     assert abs(float(out.mean()) - float(ref.mean())) < 0.05 * float(ref.abs().mean()) + 1.0
     assert torch.isfinite(out).all()
+
+
+# ---------------------------------------------------------------- MOEA/D generation kernels
+def test_moead_parents_matches_argsort():
+    from evoxmi.ops.mo import moead_parents
+
+    N, T = 300, 77
+    nb = torch.randint(0, N, (N, T), generator=torch.Generator().manual_seed(0))
+    key = rnd.PRNGKey(9)
+    perm = torch.argsort(rnd.uniform(key, (N, T)), dim=1, stable=True)[:, :2]
+    ref = torch.gather(nb, 1, perm)
+    p0, p1 = moead_parents(nb.cuda(), key.cuda())
+    assert torch.equal(p0.cpu().long(), ref[:, 0]) and torch.equal(p1.cpu().long(), ref[:, 1])
+
+
+@pytest.mark.parametrize("d", [64, 37])
+def test_moead_variation_matches_operators(d):
+    from evoxmi.operators.crossover import SimulatedBinary
+    from evoxmi.operators.mutation import Polynomial
+    from evoxmi.ops.mo import moead_variation
+
+    N = 101
+    g = torch.Generator().manual_seed(d)
+    pop = torch.rand(N, d, generator=g) * 4 - 2
+    lb, ub = torch.full((d,), -2.0), torch.full((d,), 2.0)
+    p0, p1 = torch.randint(0, N, (N,), generator=g), torch.randint(0, N, (N,), generator=g)
+    kx, km = rnd.PRNGKey(1), rnd.PRNGKey(2)
+    off = SimulatedBinary(type=2)(kx, torch.cat([pop[p0], pop[p1]], 0))
+    ref = torch.clamp(Polynomial((lb, ub))(km, off), lb, ub)
+    c = lambda t: t.cuda()
+    out = moead_variation(c(pop), c(p0).int(), c(p1).int(), c(kx), c(km), c(lb), c(ub), 1.0, 20.0, 1.0, 20.0).cpu()
+    assert torch.allclose(out, ref, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("func", ["tchebycheff", "pbi", "weighted_sum", "modified_tchebycheff", "tchebycheff_norm"])
+def test_moead_replace_matches_sequential(func):
+    from evoxmi.algorithms.mo.moead import moead_replace, moead_replace_sequential, reverse_neighbors
+    from evoxmi.ops import mo as mo_ops
+    from evoxmi.utils.common import AggregationFunction
+
+    N, T, M, d = 200, 20, 3, 5
+    g = torch.Generator().manual_seed(3)
+    w = torch.rand(N, M, generator=g) + 0.05
+    nb = torch.argsort(torch.rand(N, N, generator=g), 1)[:, :T]
+    pop_obj, off_obj = torch.rand(N, M, generator=g), torch.rand(N, M, generator=g)
+    pop, off = torch.rand(N, d, generator=g), torch.rand(N, d, generator=g)
+    z, zmax = torch.zeros(M) - 0.01, torch.ones(M) * 1.1
+    agg = AggregationFunction(func)
+    ref_pop, ref_obj = moead_replace_sequential(pop, pop_obj, off, off_obj, w, z, zmax, nb, agg)
+    rowptr, _, owner = reverse_neighbors(nb.cuda())
+    c = lambda t: t.cuda()
+    win, new_obj = mo_ops.moead_replace(c(pop_obj), c(off_obj), c(w), c(z), c(zmax), rowptr.int(), owner.int(), func)
+    new_pop = mo_ops.moead_select_rows(c(pop), c(off), win)
+    assert torch.allclose(new_obj.cpu(), ref_obj) and torch.allclose(new_pop.cpu(), ref_pop)
+
+
+@pytest.mark.parametrize("cls", ["LSMOP1", "LSMOP2", "LSMOP3", "LSMOP4", "LSMOP5", "LSMOP6", "LSMOP7", "LSMOP8", "LSMOP9"])
+def test_lsmop_fused_matches_eager(cls):
+    import evoxmi.problems.numerical as P
+
+    prob = getattr(P, cls)(d=300, m=3)
+    X = torch.rand(64, 300, generator=torch.Generator().manual_seed(4))
+    ub = torch.cat([torch.ones(2), 10 * torch.ones(298)])
+    X = X * ub
+    ref, _ = prob.evaluate(None, X)
+    out, _ = prob.evaluate(None, X.cuda())
+    assert torch.allclose(out.cpu(), ref, rtol=2e-4, atol=1e-3)
