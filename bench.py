@@ -80,9 +80,9 @@ def main():
     evals_per_s = gens_per_s * args.pop
     if rank == 0:
         out = {
-            "metric": "evaluations/sec (CMA-ES pop=10k, CEC'22 F1 d=1000; generations/sec in extra)",
+            "metric": "generations/sec + evaluations/sec, CMA-ES pop=10k on CEC'22 at 1/2/4/8 MI355X",
             "value": round(evals_per_s, 1),
-            "unit": "evals/s",
+            "unit": "evals/s (evaluations/sec; generations/sec in generations_per_sec)",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,

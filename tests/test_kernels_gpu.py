@@ -214,6 +214,25 @@ def test_jacobi_warm_start_converges_fast():
     assert ((B.T @ B - torch.eye(n, dtype=torch.float64)).norm() / math.sqrt(n)).item() < 3e-5
 
 
+def test_jacobi_warm_chain_stays_orthonormal():
+    """CMA-ES-like chain: a clustered spectrum (eigenvalues within ±5 % of 1) nudged by a
+    rank-μ term every step; the carried basis must not drift from orthonormality."""
+    from evoxmi.ops import jacobi
+
+    n = 500
+    g = torch.Generator(device="cuda").manual_seed(3)
+    C = torch.eye(n, device="cuda")
+    B = torch.eye(n, device="cuda")
+    for _ in range(40):
+        Y = torch.randn(1000, n, device="cuda", generator=g)
+        C = 0.99 * C + 0.01 * (Y.T @ Y) / 1000
+        w, B = jacobi.warm_eigh(C, B)
+    orth = (B.double().T @ B.double() - torch.eye(n, device="cuda", dtype=torch.float64)).norm().item()
+    assert orth < 1e-3
+    res = ((B.double() * w.double()) @ B.double().T - C.double()).norm() / C.double().norm()
+    assert res.item() < 2e-3
+
+
 @pytest.mark.parametrize("n,type", [(64, 1), (63, 1), (64, 2), (4096, 1)])
 def test_sbx_kernel_matches_cpu(n, type):
     from evoxmi.operators.crossover import simulated_binary
