@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--func", type=int, default=1)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--profile-phases", action="store_true")
+    ap.add_argument("--force-dist", action="store_true", help="run the distributed (sharded + RCCL) path even on one rank")
     args = ap.parse_args()
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -43,7 +44,7 @@ def main():
     from evoxmi.workflows import StdWorkflow
     import torch.distributed as dist
 
-    rank, world, device = init_distributed()
+    rank, world, device = init_distributed(force=args.force_dist)
     if device.type != "cuda":
         print("bench.py needs a HIP device", file=sys.stderr)
     torch.manual_seed(0)
@@ -54,13 +55,14 @@ def main():
     use_graph = (not args.no_graph) and device.type == "cuda"
     wf = StdWorkflow(algo, prob, graph=use_graph)
     state = wf.init(key)
-    if world > 1:
+    dist_on = world > 1 or args.force_dist
+    if dist_on:
         state = wf.enable_distributed(state)
 
     def sync():
         if device.type == "cuda":
             torch.cuda.synchronize(device)
-        if world > 1:
+        if dist_on:
             dist.barrier()
 
     for _ in range(args.warmup):
@@ -72,7 +74,7 @@ def main():
     sync()
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-    if world > 1:
+    if dist_on:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     ms = elapsed / args.steps * 1e3
@@ -105,7 +107,7 @@ def main():
             },
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

@@ -19,8 +19,10 @@ def env_world():
     return int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
 
 
-def init_distributed(backend: str = None, timeout_s: int = 600):
-    """Initialise the default process group if the env describes >1 rank.
+def init_distributed(backend: str = None, timeout_s: int = 600, force: bool = False):
+    """Initialise the default process group if the env describes >1 rank (or always,
+    with ``force=True`` — a one-rank RCCL group exercises the distributed code path,
+    including hipGraph capture of the collectives, on a single GPU).
 
     Returns ``(rank, world_size, device)``.
     """
@@ -31,7 +33,7 @@ def init_distributed(backend: str = None, timeout_s: int = 600):
         device = torch.device("cuda", local)
     else:
         device = torch.device("cpu")
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
         be = backend or ("nccl" if use_gpu else "gloo")

@@ -41,6 +41,7 @@ class Brax(Problem):
         self.cap_episode = cap_episode
         self.fused = fused
         self.check_every = check_every
+        self._s0 = None
 
     def setup(self, key):
         return State(key=key)
@@ -51,11 +52,26 @@ class Brax(Problem):
                 and self.policy.output_activation == "tanh" and isinstance(weights, dict)
                 and next(iter(weights.values()))["w"].is_cuda)
 
+    def _initial_state(self, key, device):
+        """The reset state (one row; every individual starts from it).  The problem key
+        never changes (reference ``brax.py:53-54`` resets from ``state.key`` and returns
+        ``state`` unchanged), so the reset is computed once — the key is read on the
+        host only then — and reused, including inside a captured hipGraph (whose
+        warm-up step always runs eagerly on the same state first)."""
+        c = self._s0
+        if c is not None and (c[0] is key or (key.is_cuda and torch.cuda.is_current_stream_capturing())):
+            return c[1]
+        s0, _ = self.env.reset(key.cpu(), 1)
+        s0 = s0[0].to(device)
+        self._s0 = (key, s0)
+        return s0
+
     def evaluate(self, state, weights):
         if self._fused_ok(weights):
-            s0, _ = self.env.reset(state.key.cpu(), 1)
+            w = self.policy.flat(weights)
+            s0 = self._initial_state(state.key, w.device)
             h1, h2 = self.policy.sizes[1], self.policy.sizes[2]
-            ret, steps = neuro_ops.ant_rollout(self.policy.flat(weights), h1, h2, s0[0], self.cap_episode)
+            ret, steps = neuro_ops.ant_rollout(w, h1, h2, s0, self.cap_episode)
             self.last_episode_lengths = steps  # diagnostics only (not part of the state)
             return ret, state
         leaves = [x for x in torch.utils._pytree.tree_leaves(weights) if isinstance(x, torch.Tensor)]

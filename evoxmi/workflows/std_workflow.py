@@ -358,6 +358,13 @@ class StdWorkflow(Workflow):
         if self._dist.algorithm_sharded:
             pop_size = getattr(self.algorithm, "pop_size")
             self._dist.set_global_pop(pop_size)
+            # rank-local fields (e.g. the sampled rows) hold only this rank's slice from the
+            # start, so every step keeps the same shapes (required for hipGraph capture)
+            local = getattr(self.algorithm, "rank_local_fields", ())
+            if local:
+                start, size = self._dist.slice_of(pop_size)
+                alg = state.get_child_state("algorithm")
+                state = state.update_child("algorithm", alg.update(**{f: alg[f][start : start + size].clone() for f in local}))
         return state
 
     def enable_multi_devices(self, state: State, devices=None) -> State:

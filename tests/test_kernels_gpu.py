@@ -590,3 +590,26 @@ def test_lsmop_fused_matches_eager(cls):
     ref, _ = prob.evaluate(None, X)
     out, _ = prob.evaluate(None, X.cuda())
     assert torch.allclose(out.cpu(), ref, rtol=2e-4, atol=1e-3)
+
+
+def test_openes_ant_graph_matches_eager():
+    """A whole OpenES + fused Ant-rollout generation replays from a hipGraph."""
+    from evoxmi.algorithms import OpenES
+    from evoxmi.models import MLPPolicy
+    from evoxmi.problems.neuroevolution import Brax
+    from evoxmi.utils import TreeAndVector, rank_based_fitness
+    from evoxmi.workflows import StdWorkflow
+
+    outs = []
+    for graph in (False, True):
+        policy = MLPPolicy([27, 32, 32, 8])
+        params = policy.init(rnd.PRNGKey(1), device="cuda")
+        tv = TreeAndVector(params)
+        wf = StdWorkflow(OpenES(tv.to_vector(params), 64, learning_rate=0.05, noise_stdev=0.1, optimizer="adam"), Brax(policy, "ant", 80),
+                         sol_transforms=[tv.batched_to_tree], fit_transforms=[rank_based_fitness], opt_direction="max", graph=graph)
+        st = wf.init(rnd.PRNGKey(3, device="cuda"))
+        for _ in range(4):
+            st = wf.step(st)
+        assert (wf._graph is not None) == graph
+        outs.append(st.get_child_state("algorithm").center.clone())
+    assert torch.allclose(outs[0], outs[1], rtol=1e-5, atol=1e-6)

@@ -127,6 +127,40 @@ def test_sharded_cma_es_gloo_matches_single_process():
         assert torch.allclose(sigma, ref.sigma, rtol=1e-3)
 
 
+def _sharded_openes_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from evoxmi.algorithms import OpenES
+    from evoxmi.parallel import destroy, init_distributed
+
+    init_distributed(backend="gloo")
+    wf = StdWorkflow(OpenES(torch.full((9,), 2.0), 30, learning_rate=0.05, noise_stdev=0.3, optimizer="adam"), Sphere())
+    st = wf.init(rnd.PRNGKey(5))
+    st = wf.enable_distributed(st)
+    assert st.get_child_state("algorithm").noise.shape[0] == 10  # rank-local rows only
+    for _ in range(12):
+        st = wf.step(st)
+    out[rank] = st.get_child_state("algorithm").center.clone()
+    destroy()
+
+
+def test_sharded_openes_gloo_matches_single_process():
+    """Mirrored noise rows regenerated per rank (world 3, pop 30: rank 1's slice [10, 20)
+    straddles the mirror point 15) + all-reduced partial gradients == single-process OpenES."""
+    from evoxmi.algorithms import OpenES
+
+    wf = StdWorkflow(OpenES(torch.full((9,), 2.0), 30, learning_rate=0.05, noise_stdev=0.3, optimizer="adam"), Sphere())
+    st = wf.init(rnd.PRNGKey(5))
+    for _ in range(12):
+        st = wf.step(st)
+    ref = st.get_child_state("algorithm").center
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_sharded_openes_worker, args=(3, _free_port(), out), nprocs=3, join=True)
+    assert torch.equal(out[0], out[1]) and torch.equal(out[0], out[2])  # replicas stay bit-identical
+    assert torch.allclose(out[0], ref, rtol=1e-4, atol=1e-5)
+
+
 # ------------------------------------------------------------------ monitors
 def test_std_so_monitor():
     m = StdSOMonitor(record_topk=1, record_fit_history=True)

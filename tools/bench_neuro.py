@@ -1,6 +1,8 @@
-"""OpenES + Brax-style Ant throughput (north-star config 4 shape: pop 8192, MLP 27-64-64-8).
+"""OpenES + Brax-style Ant throughput (north-star config 4: pop 8192, MLP 27-64-64-8).
 
 python tools/bench_neuro.py [--pop 8192] [--cap 1000] [--gens 5]
+torchrun --nproc-per-node N tools/bench_neuro.py ...   (population sharded over N GPUs:
+each rank rolls out its slice, OpenES all-reduces the partial gradient over RCCL)
 """
 import argparse
 import json
@@ -27,32 +29,52 @@ def main():
     ap.add_argument("--hidden", type=int, default=64)
     ap.add_argument("--wscale", type=float, default=0.1)
     ap.add_argument("--kernel-only", action="store_true", help="time the fused rollout alone on random policies")
+    ap.add_argument("--force-dist", action="store_true", help="distributed path even on one rank")
+    ap.add_argument("--graph", action="store_true", help="capture the generation in a hipGraph")
     args = ap.parse_args()
     if args.kernel_only:
         return kernel_only(args)
-    dev = torch.device("cuda")
+    from evoxmi.parallel import init_distributed
+    import torch.distributed as dist
+
+    rank, world, dev = init_distributed(force=args.force_dist)
+    dist_on = world > 1 or args.force_dist
     policy = MLPPolicy([27, args.hidden, args.hidden, 8])
     params = policy.init(rnd.PRNGKey(0), device=dev)
     tv = TreeAndVector(params)
     algo = OpenES(tv.to_vector(params), args.pop, learning_rate=0.01, noise_stdev=0.05, optimizer="adam")
     prob = Brax(policy, "ant", args.cap)
     wf = StdWorkflow(algo, prob, sol_transforms=[tv.batched_to_tree], fit_transforms=[rank_based_fitness],
-                     opt_direction="max")
+                     opt_direction="max", graph=args.graph)
     st = wf.init(rnd.PRNGKey(1, device=dev))
+    if dist_on:
+        st = wf.enable_distributed(st)
+
+    def sync():
+        torch.cuda.synchronize()
+        if dist_on:
+            dist.barrier()
+
     st = wf.step(st)
-    torch.cuda.synchronize()
+    sync()
     t = time.perf_counter()
-    env_steps = 0
+    env_steps = torch.zeros((), dtype=torch.int64, device=dev)
     for _ in range(args.gens):
         st = wf.step(st)
         env_steps += prob.last_episode_lengths.sum()
-    torch.cuda.synchronize()
-    env_steps = int(env_steps)
-    dt = (time.perf_counter() - t) / args.gens
-    out = {"pop": args.pop, "cap_episode": args.cap, "params": policy.num_params, "ms_per_gen": round(dt * 1e3, 2),
+    sync()
+    dt = torch.tensor([(time.perf_counter() - t) / args.gens], dtype=torch.float64, device=dev)
+    if dist_on:
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+        dist.all_reduce(env_steps)
+    dt, env_steps = float(dt), int(env_steps)
+    out = {"pop": args.pop, "n_gpus": world, "cap_episode": args.cap, "params": policy.num_params, "ms_per_gen": round(dt * 1e3, 2),
            "gens_per_sec": round(1 / dt, 3), "env_steps_per_sec": round(env_steps / args.gens / dt, 1),
-           "mean_episode_len": round(env_steps / args.gens / args.pop, 1)}
-    print(json.dumps(out))
+           "mean_episode_len": round(env_steps / args.gens / args.pop, 1), "graph": args.graph}
+    if rank == 0:
+        print(json.dumps(out))
+    if dist_on:
+        dist.destroy_process_group()
 
 
 def kernel_only(args):
