@@ -9,13 +9,15 @@ cμ ≈ 4.98e-3 and the eigendecomposition runs every generation.
 MI355X execution of one generation on a GPU (everything stays in HBM, no host
 synchronisation, hipGraph-capturable):
 
-* ``ask``: Philox normals (``rng.hip``) → ONE f32 MFMA GEMM
-  ``X = mean + σ · (Z ∘ D) Bᵀ`` with the ``∘D`` scaling fused into the
-  A-operand prologue and ``mean + σ·`` into the epilogue (σ read from HBM).
-* ``tell``: LDS bitonic argsort of the fitness; the weighted mean and the
-  rank-μ update ``Σ wᵢ yᵢ yᵢᵀ`` are GEMMs whose prologue *gathers* the selected
-  rows by index and applies ``(x − m)/σ · w`` on the fly (the selected
-  population is never materialised), split-K into deterministic slabs;
+* ``ask``: Philox normals (``rng.hip``) → ONE plain f32 GEMM
+  ``X = mean + Z (σ·B∘D)ᵀ`` (σ folded into the d×d factor on the device; the
+  ``mean`` bias in the epilogue) — hipBLASLt by default (``EVOXMI_PLAIN_GEMM``),
+  or the framework MFMA kernel with ``mean + σ·`` fused in its epilogue.
+* ``tell``: argsort of the fitness; the weighted mean is a gathered weighted row
+  sum (``reduce.hip``); the rank-μ update ``Σ wᵢ yᵢ yᵢᵀ`` is either a plain vendor
+  GEMM on the materialised ``Y = (x_sel − m)/σ`` (default) or the framework GEMM
+  whose prologue *gathers* the selected rows by index and applies
+  ``(x − m)/σ · w`` on the fly, split-K into deterministic slabs;
   warm-started block-Jacobi ``eigh`` (:mod:`evoxmi.ops.eigh`); ``invsqrtC`` as a
   GEMM with ``1/D`` fused in the prologue.
 * Sharded (``ask_sharded``/``tell_sharded``): each rank generates only its rows
@@ -32,7 +34,8 @@ import torch
 from ....core import Algorithm, State
 from ....ops import random as rnd
 from ....ops.eigh import symmetrize_upper, warm_eigh
-from ....ops.linalg import Operand, gemm
+from .... import config
+from ....ops.linalg import Operand, gemm, plain_nt
 from ....ops.reduce import weighted_rowsum
 from ....ops.sort import argsort, argsort_i32
 
@@ -107,8 +110,10 @@ class CMAES(Algorithm):
         d = self.dim
         z = rnd.normal(key, (rows, d), offset=row0 * d)
         if z.is_cuda:
-            # X = mean + σ (Z∘D) Bᵀ = mean + σ Z (B∘D)ᵀ : one prologue-free MFMA GEMM with
-            # mean + σ· fused in the epilogue (σ read from HBM, no host sync)
+            # X = mean + σ (Z∘D) Bᵀ = mean + Z (σ·B∘D)ᵀ : σ (a device scalar, no host sync)
+            # folds into the d×d factor, leaving one plain GEMM with a bias epilogue
+            if config.get("plain_gemm") == "blas":
+                return plain_nt(z, (state.B * (state.D * state.sigma)).contiguous(), bias_n=state.mean)
             BD = (state.B * state.D).contiguous()
             return gemm(Operand(z), Operand(BD), rows, d, d, alpha_ptr=state.sigma.reshape(1), bias_n=state.mean)
         return state.mean + state.sigma * (state.D * z) @ state.B.T
@@ -127,6 +132,12 @@ class CMAES(Algorithm):
             one_over = state.sigma.reshape(1)
             # weighted mean shift: gathered weighted row sum (reduce.hip), deterministic
             dm = weighted_rowsum(population, rows, wvec, state.mean, K)
+            if config.get("plain_gemm") == "blas":
+                # materialise Y = (x_sel − m)/σ once (K×d, 20 MB at the north-star shape) and
+                # run the rank-μ product as a plain vendor GEMM Yᵀ·(w∘Y)
+                Y = population.index_select(0, rows) if rows is not None else population
+                Y = (Y - state.mean) / state.sigma
+                return dm, torch.mm((Y * wvec[:, None]).t(), Y)
             splits = max(1, min(16, K // 256))
             S = gemm(
                 Operand(population, rc=True, gather=rows, sub=state.mean, kw=wvec, sscale=one_over, sscale_inv=True),
@@ -168,7 +179,7 @@ class CMAES(Algorithm):
         w = torch.clamp(w, min=1e-30)
         D = torch.sqrt(w)
         if B.is_cuda:
-            invsqrtC = gemm(Operand(B, kscale=1.0 / D), Operand(B), self.dim, self.dim, self.dim)
+            invsqrtC = plain_nt(B / D, B) if config.get("plain_gemm") == "blas" else gemm(Operand(B, kscale=1.0 / D), Operand(B), self.dim, self.dim, self.dim)
         else:
             invsqrtC = (B / D) @ B.T
         return B, D, invsqrtC

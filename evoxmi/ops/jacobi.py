@@ -65,6 +65,8 @@ def reorthonormalize(B: torch.Tensor) -> torch.Tensor:
 
     n = B.shape[0]
     B = B.contiguous()
+    if config.get("plain_gemm") == "blas":
+        return torch.addmm(B, B, B.t() @ B, beta=1.5, alpha=-0.5)
     X = gemm(Operand(B, rc=True), Operand(B, rc=True), n, n, n)
     return gemm(Operand(B), Operand(X), n, n, n, alpha=-0.5, beta=1.5, Cin=B)
 
@@ -85,7 +87,10 @@ def warm_eigh(C: torch.Tensor, B_prev: torch.Tensor = None, max_sweeps: int = No
     else:
         Bp[:n, :n] = reorthonormalize(B_prev) if config.get("jacobi_reortho") else B_prev
         Bp[n:, n:] = eye_pad
-        A = matmul_tn(Bp, matmul(Cp, Bp)).contiguous()
+        if config.get("plain_gemm") == "blas":
+            A = (Bp.t() @ (Cp @ Bp)).contiguous()
+        else:
+            A = matmul_tn(Bp, matmul(Cp, Bp)).contiguous()
         sweeps = config.get("jacobi_sweeps") if max_sweeps is None else max_sweeps
     tol = tol or config.get("jacobi_tol_factor") * 1.1920929e-07 * max(n, 16) ** 0.5
     w, stats = _ext.ops().jacobi_sweeps(A, Bp, schedule(np_ // 16, dev), int(sweeps), float(tol),

@@ -1,13 +1,15 @@
 """Sorting primitives (K19).  Device path: LDS bitonic argsort in one workgroup for
-n ≤ 16384 (the population sizes of every north-star config); larger inputs use
-the ROCm library sort.  Ties are broken by index (== stable sort)."""
+n ≤ 2048 (one launch, no workspace); larger inputs use the ROCm library radix sort,
+which spreads over the CUs (MI355X, n = 10 000: 37 µs vs 127 µs for the
+single-workgroup bitonic network — profiles/r1_kernel_microbench.json).  Ties are
+broken by index (== stable sort)."""
 from __future__ import annotations
 
 import torch
 
 from . import _ext
 
-MAX_LDS_SORT = 16384
+MAX_LDS_SORT = 2048
 
 
 def argsort(keys: torch.Tensor, descending: bool = False):

@@ -208,7 +208,7 @@ class _CEC2022(Problem):
     def _ssr(self, X, o, M, s):
         N, D = X.shape
         if X.is_cuda:
-            return linalg.gemm(linalg.Operand((X - o).contiguous()), linalg.Operand(M), N, D, D, alpha=float(s))
+            return linalg.plain_nt((X - o).contiguous(), M, alpha=float(s))
         return ((X - o) * s) @ M.T
 
     def _basic(self, Z, fid, perm=None, start=0, length=None, sub=None, scale=1.0, ysrc=None, ystart=0):

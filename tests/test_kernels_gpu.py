@@ -88,6 +88,16 @@ def test_argsort(n):
     assert torch.allclose(k.cpu()[~torch.isnan(rk)], rk[~torch.isnan(rk)])
 
 
+@pytest.mark.parametrize("n", [2048, 10000, 16384])
+def test_lds_bitonic_argsort_kernel(n):
+    """The single-workgroup LDS kernel itself (argsort() routes n > 2048 to the library sort)."""
+    x = torch.randn(n)
+    x[3] = x[5]
+    k, i = _ext.ops().argsort_f32(x.cuda(), 0)
+    rk, ri = torch.sort(x, stable=True)
+    assert torch.equal(i.cpu().long(), ri) and torch.equal(k.cpu(), rk)
+
+
 @pytest.mark.parametrize("name", ["sphere", "ackley", "rastrigin", "rosenbrock", "griewank", "schwefel", "ellipsoid"])
 @pytest.mark.parametrize("d", [2, 30, 1000])
 def test_classic_kernels(name, d):
