@@ -25,7 +25,12 @@ namespace {
 
 constexpr int BS = 16;   // block size
 constexpr int PS = 32;   // pair size
-constexpr int LDP = 33;  // padded LDS row
+constexpr int LDP = 33;  // padded LDS row (apply kernel tiles)
+// solve kernel pitches: S rows at 49 floats (odd ⇒ transposed reads conflict-free; the
+// 2×2-block reads of lanes (k, l), (k+1, l) land 17 banks apart), V rows at 40 floats
+// (rows 2k and 2k+2 land 16 banks apart)
+constexpr int LDS_S = 49;
+constexpr int LDS_V = 40;
 
 __device__ __forceinline__ int pair_index(const int* __restrict__ sched, int P, int i) {
   // i in [0, 32): first 16 from block I, next 16 from block J
@@ -60,8 +65,8 @@ __global__ void __launch_bounds__(256) jacobi_solve_kernel(const float* __restri
                                                            float* __restrict__ Vout, const int* __restrict__ flag,
                                                            float tol, int max_inner) {
   if (flag && *flag) return;
-  __shared__ float S[PS * LDP];
-  __shared__ float V[PS * LDP];
+  __shared__ float S[PS * LDS_S];
+  __shared__ float V[PS * LDS_V];
   __shared__ float red[8];
   const int t = threadIdx.x;
   const int P = blockIdx.x;
@@ -70,16 +75,16 @@ __global__ void __launch_bounds__(256) jacobi_solve_kernel(const float* __restri
     int i = e >> 5, j = e & 31;
     int gi = (i < 16 ? blkI : blkJ) * BS + (i & 15);
     int gj = (j < 16 ? blkI : blkJ) * BS + (j & 15);
-    S[i * LDP + j] = A[(int64_t)gi * np + gj];
-    V[i * LDP + j] = (i == j) ? 1.f : 0.f;
+    S[i * LDS_S + j] = A[(int64_t)gi * np + gj];
+    V[i * LDS_V + j] = (i == j) ? 1.f : 0.f;
   }
   __syncthreads();
   for (int e = t; e < PS * PS; e += 256) {
     int i = e >> 5, j = e & 31;
     if (i < j) {
-      float v = 0.5f * (S[i * LDP + j] + S[j * LDP + i]);
-      S[i * LDP + j] = v;
-      S[j * LDP + i] = v;
+      float v = 0.5f * (S[i * LDS_S + j] + S[j * LDS_S + i]);
+      S[i * LDS_S + j] = v;
+      S[j * LDS_S + i] = v;
     }
   }
   __syncthreads();
@@ -90,7 +95,7 @@ __global__ void __launch_bounds__(256) jacobi_solve_kernel(const float* __restri
     float off = 0.f, dia = 0.f;
     for (int e = t; e < PS * PS; e += 256) {
       int i = e >> 5, j = e & 31;
-      float v = S[i * LDP + j];
+      float v = S[i * LDS_S + j];
       if (i == j) dia += v * v; else off += v * v;
     }
     off = evx::wave_sum(off);
@@ -115,10 +120,10 @@ __global__ void __launch_bounds__(256) jacobi_solve_kernel(const float* __restri
         ql = lb + ((14 - ll + r) % 15) + 1;
       }
       // ---- read phase
-      float alp = S[pl * LDP + pl], alq = S[ql * LDP + ql], alo = S[pl * LDP + ql];
-      float x00 = S[pk * LDP + pl], x01 = S[pk * LDP + ql], x10 = S[qk * LDP + pl], x11 = S[qk * LDP + ql];
-      float v0a = V[vr0 * LDP + pl], v0b = V[vr0 * LDP + ql];
-      float v1a = V[vr1 * LDP + pl], v1b = V[vr1 * LDP + ql];
+      float alp = S[pl * LDS_S + pl], alq = S[ql * LDS_S + ql], alo = S[pl * LDS_S + ql];
+      float x00 = S[pk * LDS_S + pl], x01 = S[pk * LDS_S + ql], x10 = S[qk * LDS_S + pl], x11 = S[qk * LDS_S + ql];
+      float v0a = V[vr0 * LDS_V + pl], v0b = V[vr0 * LDS_V + ql];
+      float v1a = V[vr1 * LDS_V + pl], v1b = V[vr1 * LDS_V + ql];
       float cl = 1.f, sl = 0.f;
       if (alo != 0.f) {
         float tau = (alq - alp) * __builtin_amdgcn_rcpf(2.f * alo);
@@ -134,19 +139,19 @@ __global__ void __launch_bounds__(256) jacobi_solve_kernel(const float* __restri
       if (k == l) { o01 = 0.f; o10 = 0.f; }
       __syncthreads();
       // ---- write phase
-      S[pk * LDP + pl] = o00;
-      S[pk * LDP + ql] = o01;
-      S[qk * LDP + pl] = o10;
-      S[qk * LDP + ql] = o11;
-      V[vr0 * LDP + pl] = v0a * cl - v0b * sl;
-      V[vr0 * LDP + ql] = v0a * sl + v0b * cl;
-      V[vr1 * LDP + pl] = v1a * cl - v1b * sl;
-      V[vr1 * LDP + ql] = v1a * sl + v1b * cl;
+      S[pk * LDS_S + pl] = o00;
+      S[pk * LDS_S + ql] = o01;
+      S[qk * LDS_S + pl] = o10;
+      S[qk * LDS_S + ql] = o11;
+      V[vr0 * LDS_V + pl] = v0a * cl - v0b * sl;
+      V[vr0 * LDS_V + ql] = v0a * sl + v0b * cl;
+      V[vr1 * LDS_V + pl] = v1a * cl - v1b * sl;
+      V[vr1 * LDS_V + ql] = v1a * sl + v1b * cl;
       __syncthreads();
     }
   }
   float* Vo = Vout + (int64_t)P * PS * PS;
-  for (int e = t; e < PS * PS; e += 256) Vo[e] = V[(e >> 5) * LDP + (e & 31)];
+  for (int e = t; e < PS * PS; e += 256) Vo[e] = V[(e >> 5) * LDS_V + (e & 31)];
 }
 
 // ---------------------------------------------------------------------------------- apply
