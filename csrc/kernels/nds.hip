@@ -5,17 +5,18 @@
 //    i = 32w + b dominates j (minimisation: ≤ in every objective, < in at least one).
 //    Word-major so a wave's 64 lanes (64 consecutive j) read 256 contiguous bytes.
 //    The 32 candidates of word w are staged in LDS.
-// 2. peel kernel: a chip-wide persistent grid (≤ 128 workgroups, all co-resident on
-//    the 256 CUs) computes one front per iteration.  j joins front k iff every
+// 2. peel kernel: a chip-wide persistent grid (≤ 256 workgroups of 64 rows × 4 word
+//    quarters, all co-resident on the 256 CUs) computes one front per iteration.  j joins front k iff every
 //    dominator of j is already ranked:  DW[w][j] & ~R[w] == 0 for all w, where R is
-//    the ranked bitset (early exit at the first word with an unranked dominator, so
-//    most tests read one or two words).  R is double-buffered and only ever OR-ed
+//    the ranked bitset (early exit at the first word with an unranked dominator; the
+//    next front's test of the same row resumes at that word).  R is double-buffered and only ever OR-ed
 //    (R_next |= R_cur | new-front bits), so one grid barrier per front suffices; the
 //    loop ends when the per-iteration "still unranked" counter is zero or at least
 //    `limit` rows are ranked (NSGA-II only needs fronts until N survivors are
 //    covered: the rest get rank = n).  The barrier spins with a bound: on timeout
 //    the kernel sets an error flag and every wave exits (no hang is possible).
 #include "evoxmi_common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -54,7 +55,9 @@ __global__ void __launch_bounds__(256) dominance_kernel(const float* __restrict_
 }
 
 // workspace layout (uint32): [0] barrier count, [1] barrier generation, [2] error flag,
-// [3] ranked total, [4 .. 4+nw) R0, [4+nw .. 4+2nw) R1, [4+2nw .. 4+2nw+n+1) left[k]
+// [3] ranked total, [4 .. 4+nw) R0, [4+nw .. 4+2nw) R1, [4+2nw .. 4+2nw+n+1) left[k],
+// then 4n words: per-(row, word-quarter) resume word (words before it hold only ranked
+// dominators, and R only grows, so each scan continues where the previous front's stopped)
 constexpr int kSpinLimit = 1 << 24;
 
 __device__ __forceinline__ bool grid_barrier(uint32_t* ws, uint32_t nblocks, uint32_t& gen) {
@@ -85,52 +88,98 @@ __device__ __forceinline__ bool grid_barrier(uint32_t* ws, uint32_t nblocks, uin
   return ok && __hip_atomic_load(&ws[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
 }
 
-__global__ void __launch_bounds__(256) peel_kernel(const uint32_t* __restrict__ DW, int n, int nw, int limit,
+// Peel layout: a workgroup owns 64 rows j (one per lane) and its four waves split each
+// row's dominance words into quarters, so the sequential early-exit scan of a row is a
+// quarter as long; words are loaded CHUNK at a time (independent loads in flight), the
+// ranked bitset of the front is copied to LDS once per front, and every (row, quarter)
+// keeps a resume pointer (words before it hold only ranked dominators; R only grows).
+constexpr int PEEL_CHUNK = 16;
+constexpr int PEEL_PARTS = 8;  // waves per workgroup = word parts per row
+constexpr int PEEL_MAXW = 2048;  // n <= 65536
+
+__global__ void __launch_bounds__(64 * PEEL_PARTS) peel_kernel(const uint32_t* __restrict__ DW, int n, int nw, int limit,
                                                    int32_t* __restrict__ rank, uint32_t* __restrict__ ws) {
   uint32_t* R[2] = {ws + 4, ws + 4 + nw};
   uint32_t* left = ws + 4 + 2 * nw;
-  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
-  const int nthreads = gridDim.x * blockDim.x;
+  uint32_t* wptr = left + n + 1;  // 4 per row
+  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int qlen = (nw + PEEL_PARTS - 1) / PEEL_PARTS, w0q = q * qlen, w1q = min(nw, w0q + qlen);
+  __shared__ uint32_t Rs[PEEL_MAXW];
+  __shared__ uint8_t fail_q[PEEL_PARTS][64];
+  __shared__ uint8_t done_s[4][64];  // ranked flags of this workgroup's rows (≤ 4 passes: n ≤ 65536)
   __shared__ uint32_t wg_left;
   uint32_t gen = 0;
-  for (int j = tid; j < n; j += nthreads) rank[j] = -1;
+  const int rows_per_pass = gridDim.x * 64;
+  for (int j = blockIdx.x * 64 + lane; j < n; j += rows_per_pass)
+    if (q == 0) rank[j] = -1;
+  if (q < 4) done_s[q][lane] = 0;
+  for (int j = blockIdx.x * 64 + lane; j < n; j += rows_per_pass) wptr[PEEL_PARTS * (int64_t)j + q] = (uint32_t)w0q;
   for (int k = 0;; ++k) {
     const uint32_t* Rc = R[k & 1];
     uint32_t* Rn = R[(k + 1) & 1];
     if (threadIdx.x == 0) wg_left = 0;
-    __syncthreads();
+    for (int w = threadIdx.x; w < nw; w += blockDim.x) Rs[w] = __hip_atomic_load(&Rc[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // carry the ranked set into the next buffer (it holds R_{k-1} ⊆ R_k)
-    for (int w = tid; w < nw; w += nthreads) {
+    for (int w = blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += gridDim.x * blockDim.x) {
       const uint32_t v = __hip_atomic_load(&Rc[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (v) __hip_atomic_fetch_or(&Rn[w], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    uint32_t my_left = 0;
-    for (int j = tid; j < n; j += nthreads) {
-      if (rank[j] >= 0) continue;
-      bool free_ = true;
-      for (int w = 0; w < nw; ++w) {
-        const uint32_t d = DW[(int64_t)w * n + j];
-        if (d & ~__hip_atomic_load(&Rc[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { free_ = false; break; }
+    __syncthreads();
+    uint32_t my_left = 0, my_ranked = 0;  // my_ranked: lane-uniform in wave 0
+    for (int jb = blockIdx.x * 64, pass = 0; jb < n; jb += rows_per_pass, ++pass) {
+      const int j = jb + lane;
+      const bool active = j < n && !done_s[pass][lane];
+      bool fail = false;
+      if (active) {
+        int w = (int)wptr[PEEL_PARTS * (int64_t)j + q];
+        while (w < w1q && !fail) {
+          uint32_t d[PEEL_CHUNK];
+#pragma unroll
+          for (int u = 0; u < PEEL_CHUNK; ++u) d[u] = (w + u < w1q) ? DW[(int64_t)(w + u) * n + j] : 0u;
+          int f = PEEL_CHUNK;
+#pragma unroll
+          for (int u = PEEL_CHUNK - 1; u >= 0; --u)
+            if (w + u < w1q && (d[u] & ~Rs[w + u])) f = u;
+          if (f < PEEL_CHUNK) { w += f; fail = true; }
+          else w += PEEL_CHUNK;
+        }
+        wptr[PEEL_PARTS * (int64_t)j + q] = (uint32_t)min(w, w1q);
       }
-      if (free_) {
-        rank[j] = k;
-        __hip_atomic_fetch_or(&Rn[j >> 5], 1u << (j & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(&ws[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        ++my_left;
+      fail_q[q][lane] = fail;
+      __syncthreads();
+      if (q == 0) {
+        // wave 0 owns the 64 rows: ballot the new front members, one atomic OR per 32-row
+        // word (jb is a multiple of 64) and one ranked-count add per workgroup per front
+        bool any_fail = false;
+#pragma unroll
+        for (int p2 = 0; p2 < PEEL_PARTS; ++p2) any_fail |= fail_q[p2][lane];
+        const bool free_ = active && !any_fail;
+        const uint64_t m = __ballot(free_);
+        if (free_) {
+          rank[j] = k;
+          done_s[pass][lane] = 1;
+        } else if (active) {
+          ++my_left;
+        }
+        if (lane == 0 && (uint32_t)m) __hip_atomic_fetch_or(&Rn[jb >> 5], (uint32_t)m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 32 && (uint32_t)(m >> 32)) __hip_atomic_fetch_or(&Rn[(jb >> 5) + 1], (uint32_t)(m >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        my_ranked += __popcll(m);
       }
+      __syncthreads();
     }
     if (my_left) atomicAdd(&wg_left, my_left);
     __syncthreads();
     if (threadIdx.x == 0 && wg_left)
       __hip_atomic_fetch_add(&left[k], wg_left, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0 && my_ranked)
+      __hip_atomic_fetch_add(&ws[3], my_ranked, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (!grid_barrier(ws, gridDim.x, gen)) return;
     const uint32_t still = __hip_atomic_load(&left[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t done = __hip_atomic_load(&ws[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (still == 0) return;
     if ((int)done >= limit || k + 1 >= n) {
-      for (int j = tid; j < n; j += nthreads)
-        if (rank[j] < 0) rank[j] = n;
+      for (int jb = blockIdx.x * 64, pass = 0; jb < n; jb += rows_per_pass, ++pass)
+        if (q == 0 && jb + lane < n && !done_s[pass][lane]) rank[jb + lane] = n;
       return;
     }
   }
@@ -142,7 +191,7 @@ __global__ void __launch_bounds__(256) zero_kernel(uint32_t* __restrict__ p, int
 
 }  // namespace
 
-size_t evx_nds_workspace_words(int n) { return 4 + 2 * (size_t)((n + 31) / 32) + (size_t)n + 1; }
+size_t evx_nds_workspace_words(int n) { return 4 + 2 * (size_t)((n + 31) / 32) + (PEEL_PARTS + 1) * (size_t)n + 1; }
 
 void evx_nds(const float* f, int n, int m, int limit, uint32_t* DW, int32_t* rank, uint32_t* ws, hipStream_t s) {
   const int nw = (n + 31) / 32;
@@ -154,6 +203,10 @@ void evx_nds(const float* f, int n, int m, int limit, uint32_t* DW, int32_t* ran
   const int64_t nws = (int64_t)evx_nds_workspace_words(n);
   const int zb = (int)((nws + 255) / 256 < 64 ? (nws + 255) / 256 : 64);
   zero_kernel<<<zb, 256, 0, s>>>(ws, nws);
-  const int blocks = min((n + 255) / 256, 128);
-  peel_kernel<<<blocks, 256, 0, s>>>(DW, n, nw, limit, rank, ws);
+  // workgroups of the persistent peel: 64 rows each (EVOXMI_NDS_BLOCKS caps it; ≤ 256,
+  // one per CU at most, so every workgroup is co-resident for the grid barrier)
+  static const int cap = [] { const char* e = getenv("EVOXMI_NDS_BLOCKS"); const int v = e ? atoi(e) : 256; return v < 1 ? 1 : (v > 256 ? 256 : v); }();
+  int blocks = min((n + 63) / 64, cap);
+  blocks = max(blocks, (n + 255) / 256);  // the kernel keeps ≤ 4 row passes per workgroup in LDS
+  peel_kernel<<<blocks, 64 * PEEL_PARTS, 0, s>>>(DW, n, nw, limit, rank, ws);
 }
