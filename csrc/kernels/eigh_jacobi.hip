@@ -65,9 +65,13 @@ __global__ void __launch_bounds__(256) jacobi_solve_kernel(const float* __restri
                                                            float* __restrict__ Vout, const int* __restrict__ flag,
                                                            float tol, int max_inner) {
   if (flag && *flag) return;
-  __shared__ float S[PS * LDS_S];
+  // S is double-buffered: a round reads Sc and writes every element of Sn (the 2×2 blocks
+  // of the 256 threads tile the 32×32 matrix), so the read and write phases need no
+  // barrier in between; V has one owner per element within a round (single buffer).
+  __shared__ float Sbuf[2][PS * LDS_S];
   __shared__ float V[PS * LDS_V];
   __shared__ float red[8];
+  float* S = Sbuf[0];
   const int t = threadIdx.x;
   const int P = blockIdx.x;
   const int blkI = sched[2 * P], blkJ = sched[2 * P + 1];
@@ -119,7 +123,8 @@ __global__ void __launch_bounds__(256) jacobi_solve_kernel(const float* __restri
         pl = lb + (ll == 0 ? 0 : ((ll - 1 + r) % 15) + 1);
         ql = lb + ((14 - ll + r) % 15) + 1;
       }
-      // ---- read phase
+      // ---- read phase (current buffer)
+      float* Sn = (S == Sbuf[0]) ? Sbuf[1] : Sbuf[0];
       float alp = S[pl * LDS_S + pl], alq = S[ql * LDS_S + ql], alo = S[pl * LDS_S + ql];
       float x00 = S[pk * LDS_S + pl], x01 = S[pk * LDS_S + ql], x10 = S[qk * LDS_S + pl], x11 = S[qk * LDS_S + ql];
       float v0a = V[vr0 * LDS_V + pl], v0b = V[vr0 * LDS_V + ql];
@@ -137,16 +142,16 @@ __global__ void __launch_bounds__(256) jacobi_solve_kernel(const float* __restri
       float o00 = y00 * cl - y01 * sl, o01 = y00 * sl + y01 * cl;
       float o10 = y10 * cl - y11 * sl, o11 = y10 * sl + y11 * cl;
       if (k == l) { o01 = 0.f; o10 = 0.f; }
-      __syncthreads();
-      // ---- write phase
-      S[pk * LDS_S + pl] = o00;
-      S[pk * LDS_S + ql] = o01;
-      S[qk * LDS_S + pl] = o10;
-      S[qk * LDS_S + ql] = o11;
+      // ---- write phase (next buffer)
+      Sn[pk * LDS_S + pl] = o00;
+      Sn[pk * LDS_S + ql] = o01;
+      Sn[qk * LDS_S + pl] = o10;
+      Sn[qk * LDS_S + ql] = o11;
       V[vr0 * LDS_V + pl] = v0a * cl - v0b * sl;
       V[vr0 * LDS_V + ql] = v0a * sl + v0b * cl;
       V[vr1 * LDS_V + pl] = v1a * cl - v1b * sl;
       V[vr1 * LDS_V + ql] = v1a * sl + v1b * cl;
+      S = Sn;
       __syncthreads();
     }
   }
