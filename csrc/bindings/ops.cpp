@@ -443,6 +443,62 @@ at::Tensor lsmop_g(const at::Tensor& X, std::vector<int64_t> start, std::vector<
   return G;
 }
 
+// ---------------------------------------------------------------- CMA-ES tell epilogue (cmaes.hip)
+std::vector<at::Tensor> cma_delta_gemv(const at::Tensor& M, const at::Tensor& mean, const at::Tensor& dm, double cm) {
+  for (auto* t : {&M, &mean, &dm}) { CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t); }
+  const int64_t d = mean.numel();
+  TORCH_CHECK(M.dim() == 2 && M.size(0) == d && M.size(1) == d && dm.numel() == d, "cma_delta_gemv: shapes");
+  c10::DeviceGuard g(M.device());
+  auto mo = at::empty_like(mean), de = at::empty_like(mean), y = at::empty_like(mean);
+  if (d > 0) evx_cma_delta_gemv(M.data_ptr<float>(), mean.data_ptr<float>(), dm.data_ptr<float>(), (float)cm, (int)d, mo.data_ptr<float>(),
+                                de.data_ptr<float>(), y.data_ptr<float>(), cur_stream());
+  return {mo, de, y};
+}
+
+std::vector<at::Tensor> cma_paths(const at::Tensor& ps, const at::Tensor& pc, const at::Tensor& y, const at::Tensor& delta,
+                                  const at::Tensor& sigma, const at::Tensor& count_iter, std::vector<double> consts) {
+  for (auto* t : {&ps, &pc, &y, &delta, &sigma}) { CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t); }
+  CHECK_DEV(count_iter);
+  TORCH_CHECK(count_iter.scalar_type() == at::kLong && count_iter.numel() == 1 && sigma.numel() == 1, "cma_paths: scalars");
+  TORCH_CHECK(consts.size() == 9, "cma_paths: 9 constants");
+  const int64_t d = ps.numel();
+  TORCH_CHECK(pc.numel() == d && y.numel() == d && delta.numel() == d, "cma_paths: shapes");
+  c10::DeviceGuard g(ps.device());
+  float k[9];
+  for (int i = 0; i < 9; ++i) k[i] = (float)consts[i];
+  auto pso = at::empty_like(ps), pco = at::empty_like(pc);
+  auto so = at::empty_like(sigma), ao = at::empty_like(sigma), ho = at::empty_like(sigma);
+  evx_cma_paths(ps.data_ptr<float>(), pc.data_ptr<float>(), y.data_ptr<float>(), delta.data_ptr<float>(), sigma.data_ptr<float>(),
+                count_iter.data_ptr<int64_t>(), (int)d, k, pso.data_ptr<float>(), pco.data_ptr<float>(), so.data_ptr<float>(),
+                ao.data_ptr<float>(), ho.data_ptr<float>(), cur_stream());
+  return {pso, pco, so, ao, ho};
+}
+
+std::vector<at::Tensor> cma_cov_pad(const at::Tensor& C, const at::Tensor& S, const at::Tensor& pc, const at::Tensor& a, double c1,
+                                    double cmu, const at::Tensor& Bprev, int64_t np) {
+  for (auto* t : {&C, &S, &pc, &a, &Bprev}) { CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t); }
+  const int64_t d = pc.numel();
+  TORCH_CHECK(C.dim() == 2 && C.size(0) == d && C.size(1) == d && S.sizes() == C.sizes() && Bprev.sizes() == C.sizes(), "cma_cov_pad: shapes");
+  TORCH_CHECK(np >= d && np % 32 == 0 && a.numel() == 1, "cma_cov_pad: np must be a multiple of 32 and >= d");
+  c10::DeviceGuard g(C.device());
+  auto Cn = at::empty_like(C);
+  auto Cp = at::empty({np, np}, C.options()), Bp = at::empty({np, np}, C.options());
+  evx_cma_cov_pad(C.data_ptr<float>(), S.data_ptr<float>(), pc.data_ptr<float>(), a.data_ptr<float>(), (float)c1, (float)cmu,
+                  Bprev.data_ptr<float>(), (int)d, (int)np, Cn.data_ptr<float>(), Cp.data_ptr<float>(), Bp.data_ptr<float>(), cur_stream());
+  return {Cn, Cp, Bp};
+}
+
+std::vector<at::Tensor> cma_eig_out(const at::Tensor& Bp, const at::Tensor& w, int64_t d) {
+  for (auto* t : {&Bp, &w}) { CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t); }
+  const int64_t np = Bp.size(0);
+  TORCH_CHECK(Bp.dim() == 2 && Bp.size(1) == np && w.numel() >= d && d <= np, "cma_eig_out: shapes");
+  c10::DeviceGuard g(Bp.device());
+  auto B = at::empty({d, d}, Bp.options()), BD = at::empty({d, d}, Bp.options()), D = at::empty({d}, Bp.options());
+  if (d > 0) evx_cma_eig_out(Bp.data_ptr<float>(), w.data_ptr<float>(), (int)d, (int)np, B.data_ptr<float>(), D.data_ptr<float>(),
+                             BD.data_ptr<float>(), cur_stream());
+  return {B, D, BD};
+}
+
 }  // namespace
 
 TORCH_LIBRARY(evoxmi, m) {
@@ -464,6 +520,10 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("classic_eval(Tensor X, int func, float a, float b, float c) -> Tensor");
   m.def("gemm_f32(Tensor A, int a_rc, Tensor? a_gather, Tensor? a_sub, int a_sub_on_k, Tensor? a_kscale, Tensor? a_kw, Tensor? a_sscale, int a_sscale_inv, Tensor B, int b_rc, Tensor? b_gather, Tensor? b_sub, int b_sub_on_k, Tensor? b_kscale, Tensor? b_kw, Tensor? b_sscale, int b_sscale_inv, Tensor? alpha_ptr, Tensor? bias_n, float beta, Tensor? Cin, int M, int N, int K, int splits, float alpha) -> Tensor");
   m.def("lsmop_g(Tensor X, int[] start, int[] sublen, int[] func, int nk, int cosine) -> Tensor");
+  m.def("cma_delta_gemv(Tensor M, Tensor mean, Tensor dm, float cm) -> Tensor[]");
+  m.def("cma_paths(Tensor ps, Tensor pc, Tensor y, Tensor delta, Tensor sigma, Tensor count_iter, float[] consts) -> Tensor[]");
+  m.def("cma_cov_pad(Tensor C, Tensor S, Tensor pc, Tensor a, float c1, float cmu, Tensor Bprev, int np) -> Tensor[]");
+  m.def("cma_eig_out(Tensor Bp, Tensor w, int d) -> Tensor[]");
   m.def("moead_parents(Tensor nb, Tensor key) -> Tensor[]");
   m.def("moead_variation(Tensor pop, Tensor p0, Tensor p1, Tensor kx, Tensor km, Tensor lb, Tensor ub, float pro_c, float dis_c, float pro_m, float dis_m, int nm) -> Tensor");
   m.def("moead_replace(Tensor pop_obj, Tensor off_obj, Tensor W, Tensor z, Tensor zmax, Tensor rowptr, Tensor owner, int func) -> Tensor[]");
@@ -494,6 +554,10 @@ TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
   m.impl("gemm_f32", &gemm_f32);
   m.impl("pso_update", &pso_update);
   m.impl("lsmop_g", &lsmop_g);
+  m.impl("cma_delta_gemv", &cma_delta_gemv);
+  m.impl("cma_paths", &cma_paths);
+  m.impl("cma_cov_pad", &cma_cov_pad);
+  m.impl("cma_eig_out", &cma_eig_out);
   m.impl("moead_parents", &moead_parents);
   m.impl("moead_variation", &moead_variation);
   m.impl("moead_replace", &moead_replace);

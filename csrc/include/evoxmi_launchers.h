@@ -61,3 +61,13 @@ void evx_moead_replace(const float* pop_obj, const float* off_obj, const float* 
 void evx_moead_select_rows(const float* pop, const float* off, const int32_t* win, float* out, int N, int d, hipStream_t s);
 void evx_lsmop_g(const float* X, float* G, int N, int D, int ng, int nk, int cosine, const int* start, const int* sublen, const int* func,
                  hipStream_t s);
+
+// cmaes.hip
+void evx_cma_delta_gemv(const float* M, const float* mean, const float* dm, float cm, int d, float* mean_out, float* delta, float* y,
+                        hipStream_t s);
+void evx_cma_paths(const float* ps, const float* pc, const float* y, const float* delta, const float* sigma, const int64_t* count_iter,
+                   int d, const float* consts, float* ps_out, float* pc_out, float* sigma_out, float* a_out, float* hsig_out,
+                   hipStream_t s);
+void evx_cma_cov_pad(const float* C, const float* S, const float* pc, const float* a, float c1, float cmu, const float* Bprev, int d,
+                     int np, float* Cn, float* Cp, float* Bp, hipStream_t s);
+void evx_cma_eig_out(const float* Bp, const float* w, int d, int np, float* B, float* D, float* BdivD, hipStream_t s);

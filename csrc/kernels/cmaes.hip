@@ -1,0 +1,169 @@
+// CMA-ES tell epilogue (K3 of SURVEY §2.10; reference es_variants/cma_es.py:162-198).
+//
+// After the rank-μ product S and the weighted mean shift dm are formed, the reference
+// performs ~40 small vector/matrix ops per generation (mean, evolution paths, hσ, σ,
+// covariance blend, symmetrisation, identity padding for the eigensolver, eigenbasis
+// extraction).  On MI355X each of those is a ~2–5 µs launch, so they are fused into four
+// kernels:
+//   1. delta_gemv : δ = (m + c_m·dm) − m,  y = invsqrtC·δ   (one wave per row, float4)
+//   2. paths      : p_σ, ‖p_σ‖, hσ, p_c, σ and the covariance blend factor a — one
+//                   workgroup, every scalar stays on the device (graph-capturable)
+//   3. cov_pad    : C' = a·C + c1·p_c p_cᵀ + cμ·S (written as the new state), the padded
+//                   symmetric eigensolver input Cp = sym_upper(C') ⊕ I and the padded
+//                   warm start Bp = B_prev ⊕ I, by 32×32 tiles (LDS transpose for the
+//                   lower tiles, coalesced reads and writes everywhere)
+//   4. eig_out    : B = Bp[:d, :d], D = sqrt(max(w, 1e-30)), B∘D⁻¹ (for invsqrtC = (B/D)Bᵀ)
+#include "evoxmi_common.h"
+
+namespace {
+using namespace evx;
+
+__global__ void __launch_bounds__(256) delta_gemv_kernel(const float* __restrict__ M, const float* __restrict__ mean,
+                                                         const float* __restrict__ dm, float cm, int d, float* __restrict__ mean_out,
+                                                         float* __restrict__ delta, float* __restrict__ y) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= d) return;
+  const float* row = M + (int64_t)r * d;
+  float acc = 0.f;
+  if ((d & 3) == 0) {
+    for (int c = lane * 4; c < d; c += 256) {
+      const float4 m4 = *reinterpret_cast<const float4*>(row + c);
+      const float4 mu = *reinterpret_cast<const float4*>(mean + c);
+      const float4 g = *reinterpret_cast<const float4*>(dm + c);
+      acc += m4.x * ((mu.x + cm * g.x) - mu.x) + m4.y * ((mu.y + cm * g.y) - mu.y) + m4.z * ((mu.z + cm * g.z) - mu.z) +
+             m4.w * ((mu.w + cm * g.w) - mu.w);
+    }
+  } else {
+    for (int c = lane; c < d; c += 64) acc += row[c] * ((mean[c] + cm * dm[c]) - mean[c]);
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) {
+    y[r] = acc;
+    const float mn = mean[r] + cm * dm[r];
+    mean_out[r] = mn;
+    delta[r] = mn - mean[r];
+  }
+}
+
+struct PathConsts {
+  float cs, c_ps, cc, c_pc, chiN, damps, c1, cmu, hs_thresh;
+};
+
+// scal: [0] sigma (in), outputs: sigma_out, a_out, hsig_out (device scalars)
+__global__ void __launch_bounds__(1024) paths_kernel(const float* __restrict__ ps, const float* __restrict__ pc,
+                                                     const float* __restrict__ y, const float* __restrict__ delta,
+                                                     const float* __restrict__ sigma, const int64_t* __restrict__ count_iter, int d,
+                                                     PathConsts k, float* __restrict__ ps_out, float* __restrict__ pc_out,
+                                                     float* __restrict__ sigma_out, float* __restrict__ a_out, float* __restrict__ hsig_out) {
+  __shared__ float scratch[16];
+  const float s = sigma[0];
+  const float inv_s = 1.f / s;
+  float nrm2 = 0.f;
+  for (int i = threadIdx.x; i < d; i += blockDim.x) {
+    const float v = (1.f - k.cs) * ps[i] + k.c_ps * y[i] * inv_s;
+    ps_out[i] = v;
+    nrm2 += v * v;
+  }
+  const float nrm = sqrtf(block_sum(nrm2, scratch));
+  const float count = (float)count_iter[0];
+  const float hs = (nrm / sqrtf(1.f - powf(1.f - k.cs, 2.f * count)) < k.hs_thresh) ? 1.f : 0.f;
+  for (int i = threadIdx.x; i < d; i += blockDim.x) pc_out[i] = (1.f - k.cc) * pc[i] + hs * k.c_pc * delta[i] * inv_s;
+  if (threadIdx.x == 0) {
+    sigma_out[0] = s * expf((k.cs / k.damps) * (nrm / k.chiN - 1.f));
+    a_out[0] = (1.f - k.c1 - k.cmu) + k.c1 * (1.f - hs) * k.cc * (2.f - k.cc);
+    hsig_out[0] = hs;
+  }
+}
+
+constexpr int TS = 32;
+
+// grid (np/32, np/32), 256 threads: tile (ti, tj); each thread handles 4 rows of the tile
+__global__ void __launch_bounds__(256) cov_pad_kernel(const float* __restrict__ C, const float* __restrict__ S,
+                                                      const float* __restrict__ pc, const float* __restrict__ a_ptr, float c1, float cmu,
+                                                      const float* __restrict__ Bprev, int d, int np, float* __restrict__ Cn,
+                                                      float* __restrict__ Cp, float* __restrict__ Bp) {
+  __shared__ float T[TS][TS + 1];
+  const int ti = blockIdx.y, tj = blockIdx.x;
+  const int c = threadIdx.x & 31, r0 = threadIdx.x >> 5;  // 8 row groups
+  const float a = a_ptr[0];
+  // own tile: C' (state) and Bp
+#pragma unroll
+  for (int rr = 0; rr < TS; rr += 8) {
+    const int i = ti * TS + r0 + rr, j = tj * TS + c;
+    float v = (i == j) ? 1.f : 0.f, b = v;
+    if (i < d && j < d) {
+      v = a * C[(int64_t)i * d + j] + c1 * pc[i] * pc[j] + cmu * S[(int64_t)i * d + j];
+      Cn[(int64_t)i * d + j] = v;
+      b = Bprev[(int64_t)i * d + j];
+    }
+    Bp[(int64_t)i * np + j] = b;
+    if (ti < tj) Cp[(int64_t)i * np + j] = v;     // strictly upper tile: as is
+    else if (ti == tj) T[r0 + rr][c] = v;         // diagonal tile: symmetrise from its upper half
+  }
+  if (ti == tj) {
+    __syncthreads();
+#pragma unroll
+    for (int rr = 0; rr < TS; rr += 8) {
+      const int li = r0 + rr, lj = c;
+      const float v = li <= lj ? T[li][lj] : T[lj][li];
+      Cp[(int64_t)(ti * TS + li) * np + tj * TS + lj] = v;
+    }
+    return;
+  }
+  if (ti < tj) return;
+  // strictly lower tile of Cp = transpose of the upper tile C'(tj, ti)
+#pragma unroll
+  for (int rr = 0; rr < TS; rr += 8) {
+    const int i = tj * TS + r0 + rr, j = ti * TS + c;  // element (i, j) of the upper tile
+    float v = (i == j) ? 1.f : 0.f;
+    if (i < d && j < d) v = a * C[(int64_t)i * d + j] + c1 * pc[i] * pc[j] + cmu * S[(int64_t)i * d + j];
+    T[r0 + rr][c] = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int rr = 0; rr < TS; rr += 8) {
+    const int li = r0 + rr, lj = c;
+    Cp[(int64_t)(ti * TS + li) * np + tj * TS + lj] = T[lj][li];
+  }
+}
+
+__global__ void __launch_bounds__(256) eig_out_kernel(const float* __restrict__ Bp, const float* __restrict__ w, int d, int np,
+                                                      float* __restrict__ B, float* __restrict__ D, float* __restrict__ BdivD) {
+  const int64_t total = (int64_t)d * d;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int i = (int)(e / d), j = (int)(e - (int64_t)i * d);
+    const float dj = sqrtf(fmaxf(w[j], 1e-30f));
+    const float b = Bp[(int64_t)i * np + j];
+    B[e] = b;
+    BdivD[e] = b / dj;
+    if (i == 0) D[j] = dj;
+  }
+}
+
+}  // namespace
+
+void evx_cma_delta_gemv(const float* M, const float* mean, const float* dm, float cm, int d, float* mean_out, float* delta, float* y,
+                        hipStream_t s) {
+  delta_gemv_kernel<<<(d + 3) / 4, 256, 0, s>>>(M, mean, dm, cm, d, mean_out, delta, y);
+}
+
+void evx_cma_paths(const float* ps, const float* pc, const float* y, const float* delta, const float* sigma, const int64_t* count_iter,
+                   int d, const float* consts, float* ps_out, float* pc_out, float* sigma_out, float* a_out, float* hsig_out,
+                   hipStream_t s) {
+  PathConsts k{consts[0], consts[1], consts[2], consts[3], consts[4], consts[5], consts[6], consts[7], consts[8]};
+  paths_kernel<<<1, 1024, 0, s>>>(ps, pc, y, delta, sigma, count_iter, d, k, ps_out, pc_out, sigma_out, a_out, hsig_out);
+}
+
+void evx_cma_cov_pad(const float* C, const float* S, const float* pc, const float* a, float c1, float cmu, const float* Bprev, int d,
+                     int np, float* Cn, float* Cp, float* Bp, hipStream_t s) {
+  dim3 grid(np / TS, np / TS);
+  cov_pad_kernel<<<grid, 256, 0, s>>>(C, S, pc, a, c1, cmu, Bprev, d, np, Cn, Cp, Bp);
+}
+
+void evx_cma_eig_out(const float* Bp, const float* w, int d, int np, float* B, float* D, float* BdivD, hipStream_t s) {
+  const int64_t total = (int64_t)d * d;
+  int g = (int)((total + 255) / 256);
+  if (g > 4096) g = 4096;
+  eig_out_kernel<<<g, 256, 0, s>>>(Bp, w, d, np, B, D, BdivD);
+}

@@ -153,7 +153,34 @@ class CMAES(Algorithm):
         S = (y.T * wvec) @ y
         return dm, S
 
+    def _fused_epilogue_ok(self, state):
+        return (state.C.is_cuda and self.decomp_per_iter == 1 and config.get("cma_fused")
+                and config.get("eigh") == "jacobi" and state.count_iter.dtype == torch.int64)
+
+    def _finish_tell_fused(self, state, dm, S):
+        """Same update as ``_finish_tell`` in four fused kernels around the eigensolver
+        (``cmaes.hip``): δ/invsqrtC·δ, the evolution paths and σ, the covariance blend
+        with the padded eigensolver operands, and the eigenbasis extraction."""
+        from ....ops import _ext, jacobi
+
+        ops = _ext.ops()
+        d = self.dim
+        mean, delta, y = ops.cma_delta_gemv(state.invsqrtC.contiguous(), state.mean.contiguous(), dm.contiguous(), float(self.cm))
+        consts = [self.cs, math.sqrt(self.cs * (2 - self.cs) * self.mueff), self.cc, math.sqrt(self.cc * (2 - self.cc) * self.mueff),
+                  self.chiN, self.damps, self.c1, self.cmu, (1.4 + 2 / (d + 1)) * self.chiN]
+        ps, pc, sigma, a, _hsig = ops.cma_paths(state.ps.contiguous(), state.pc.contiguous(), y, delta, state.sigma.reshape(1).contiguous(),
+                                                state.count_iter.reshape(1).contiguous(), consts)
+        np_ = jacobi.padded_size(d)
+        C, Cp, Bp = ops.cma_cov_pad(state.C.contiguous(), S.contiguous(), pc, a, float(self.c1), float(self.cmu), state.B.contiguous(), np_)
+        w, Bp = jacobi.warm_eigh_padded(Cp, Bp, d, max_sweeps=self.eig_sweeps)
+        B, D, BdivD = ops.cma_eig_out(Bp, w, d)
+        invsqrtC = plain_nt(BdivD, B) if config.get("plain_gemm") == "blas" else gemm(Operand(BdivD), Operand(B), d, d, d)
+        return state.update(mean=mean, ps=ps, pc=pc, C=C, sigma=sigma.reshape(state.sigma.shape), B=B, D=D, invsqrtC=invsqrtC,
+                            count_eigen=state.count_eigen + 1)
+
     def _finish_tell(self, state, dm, S):
+        if self._fused_epilogue_ok(state):
+            return self._finish_tell_fused(state, dm, S)
         d = self.dim
         mean = state.mean + self.cm * dm
         delta_mean = mean - state.mean

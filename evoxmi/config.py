@@ -37,6 +37,7 @@ def _bool(s: str) -> bool:
 
 KNOBS: Dict[str, Knob] = {
     "eigh": Knob("EVOXMI_EIGH", "jacobi", str, "symmetric eigensolver for CMA-ES: 'jacobi' (warm-started HIP block Jacobi) or 'torch' (rocSOLVER)"),
+    "cma_fused": Knob("EVOXMI_CMA_FUSED", 1, int, "CMA-ES tell epilogue as the fused cmaes.hip kernels (0: reference-shaped torch ops)"),
     "plain_gemm": Knob("EVOXMI_PLAIN_GEMM", "blas", str, "GEMMs without fused prologues: 'blas' (hipBLASLt) or 'evoxmi' (framework MFMA kernel)"),
     "jacobi_sweeps": Knob("EVOXMI_JACOBI_SWEEPS", 2, int, "maximum warm-started Jacobi sweeps per decomposition (stops early once converged)"),
     "jacobi_tol_factor": Knob("EVOXMI_JACOBI_TOL_FACTOR", 4.0, float, "convergence: ‖offdiag‖ ≤ factor·eps_f32·sqrt(n)·‖diag‖"),

@@ -99,6 +99,28 @@ def warm_eigh(C: torch.Tensor, B_prev: torch.Tensor = None, max_sweeps: int = No
     return (*out, stats) if return_stats else out
 
 
+def warm_eigh_padded(Cp: torch.Tensor, Bp: torch.Tensor, n: int, max_sweeps: int = None, tol: float = None):
+    """``warm_eigh`` on operands that are already padded to ``padded_size(n)`` with an
+    identity block (``Cp`` symmetric; ``Bp`` the previous basis, e.g. from the fused
+    CMA-ES epilogue).  Returns ``(w_padded, Bp_rotated)``; the first ``n`` entries /
+    the leading n×n block are the decomposition of the unpadded matrix."""
+    np_ = Cp.shape[0]
+    assert np_ == padded_size(n) and Bp.shape == Cp.shape
+    if config.get("jacobi_reortho"):
+        # Newton–Schulz on the padded basis: the identity block is a fixed point
+        Bp = torch.addmm(Bp, Bp, Bp.t() @ Bp, beta=1.5, alpha=-0.5) if config.get("plain_gemm") == "blas" else reorthonormalize(Bp)
+    if config.get("plain_gemm") == "blas":
+        A = (Bp.t() @ (Cp @ Bp)).contiguous()
+    else:
+        A = matmul_tn(Bp, matmul(Cp, Bp)).contiguous()
+    Bp = Bp.contiguous()
+    sweeps = config.get("jacobi_sweeps") if max_sweeps is None else max_sweeps
+    tol = tol or config.get("jacobi_tol_factor") * 1.1920929e-07 * max(n, 16) ** 0.5
+    w, _ = _ext.ops().jacobi_sweeps(A, Bp, schedule(np_ // 16, Cp.device), int(sweeps), float(tol),
+                                    float(config.get("jacobi_inner_tol")), int(config.get("jacobi_inner")))
+    return w, Bp
+
+
 def eigh(C: torch.Tensor, max_sweeps: int = None):
     """Cold-start symmetric eigendecomposition on the GPU (eigenvalues ascending)."""
     w, V = warm_eigh(C, None, max_sweeps=max_sweeps)
