@@ -54,10 +54,28 @@ class MLPPolicy:
     __call__ = apply
 
     def flat(self, params):
-        """[W1, b1, W2, b2, …] rows (N, P) — the fused-kernel layout."""
+        """[W1, b1, W2, b2, …] rows (N, P) — the fused-kernel layout.  When the leaves are
+        consecutive column slices of one row-major (N, P) buffer (what
+        ``TreeAndVector.batched_to_tree`` produces from the population), that buffer is
+        returned as a view instead of being copied (212 MB per generation at the
+        north-star shape)."""
         parts = []
         for i in range(len(self.sizes) - 1):
             p = params[f"layer{i}"]
             n = p["w"].shape[0]
             parts += [p["w"].reshape(n, -1), p["b"].reshape(n, -1)]
-        return torch.cat(parts, 1)
+        base = _contiguous_columns(parts)
+        return base if base is not None else torch.cat(parts, 1)
+
+
+def _contiguous_columns(parts):
+    """The (N, ΣP) view covering ``parts`` if they are adjacent column blocks of one buffer."""
+    p0 = parts[0]
+    P = sum(t.shape[1] for t in parts)
+    ptr = p0.untyped_storage().data_ptr()
+    off = p0.storage_offset()
+    for t in parts:
+        if t.untyped_storage().data_ptr() != ptr or t.storage_offset() != off or (t.shape[0] > 1 and t.stride(0) != P) or t.stride(1) != 1:
+            return None
+        off += t.shape[1]
+    return p0.as_strided((p0.shape[0], P), (P, 1), p0.storage_offset())
