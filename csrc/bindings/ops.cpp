@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include "evoxmi_launchers.h"
+#include "../host/stochastic_ranking.h"
 
 namespace {
 
@@ -338,21 +339,8 @@ at::Tensor stochastic_ranking(const at::Tensor& I1_, const at::Tensor& I2_, cons
   auto rnd = rnd_.to(at::kCPU, at::kFloat).contiguous();
   const int64_t n = I1.numel();
   TORCH_CHECK(I2.numel() == n && rnd.numel() >= std::max<int64_t>(n - 1, 0), "stochastic_ranking: sizes");
-  auto rank = at::arange(n, at::TensorOptions().dtype(at::kLong));
-  int64_t* r = rank.data_ptr<int64_t>();
-  const float *a = I1.data_ptr<float>(), *b = I2.data_ptr<float>(), *u = rnd.data_ptr<float>();
-  const int64_t sweeps = (n + 1) / 2;
-  bool swapped = true;
-  for (int64_t it = 0; it < sweeps && swapped; ++it) {
-    swapped = false;
-    for (int64_t j = 0; j + 1 < n; ++j) {
-      const float* key = (u[j] < pc) ? a : b;
-      if (key[r[j]] < key[r[j + 1]]) {
-        std::swap(r[j], r[j + 1]);
-        swapped = true;
-      }
-    }
-  }
+  auto rank = at::empty({n}, at::TensorOptions().dtype(at::kLong));
+  evx_host::stochastic_ranking(I1.data_ptr<float>(), I2.data_ptr<float>(), rnd.data_ptr<float>(), (float)pc, n, rank.data_ptr<int64_t>());
   return rank;
 }
 

@@ -35,7 +35,7 @@ def _torch_dir():
 
 
 def _headers():
-    hs = glob.glob(os.path.join(CSRC, "include", "*.h"))
+    hs = glob.glob(os.path.join(CSRC, "include", "*.h")) + glob.glob(os.path.join(CSRC, "host", "*.h"))
     return max((os.path.getmtime(h) for h in hs), default=0.0)
 
 
