@@ -8,7 +8,10 @@ agg = defaultdict(lambda: defaultdict(list))
 meta = {}
 for r in rows:
     name = r["Kernel_Name"]
-    short = name.split("(")[0][-70:] if not name.startswith("void (anon") else name[:110]
+    if "(anonymous namespace)::" in name[:40]:
+        short = name[:110]
+    else:
+        short = name.split("(")[0][-70:] or name[:110]
     key = short + f" [vgpr={r['VGPR_Count']} agpr={r['Accum_VGPR_Count']} lds={r['LDS_Block_Size']}]"
     agg[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
     meta[key] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
