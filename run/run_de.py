@@ -10,7 +10,10 @@ FE count) and ``<out>/result_de_history.txt`` (best-so-far history of the median
 
 MI355X-specific: with ``--graph`` (default on a GPU) each generation is one hipGraph
 replay; the best-so-far value is read back only every ``--sync-every`` generations so
-the host never stalls the queue for the time check.
+the host never stalls the queue for the time check.  ``--concurrent K`` runs K
+independent runs at once, each on its own HIP stream (a pop-100, d-20 generation
+occupies a handful of CUs, so K graphs replayed on K streams overlap on the 256 CUs);
+every run still gets its own ``--max-time`` wall-clock budget.
 
 Example: ``python run/run_de.py --algo LSHADE --dim 20 --pop 100 --runs 4 --max-time 5``
 """
@@ -24,6 +27,14 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch  # noqa: E402
+
+
+class _nullcontext:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *a):
+        return False
 
 
 def sample_history(num_samples, hist):
@@ -55,6 +66,7 @@ def main(argv=None):
     ap.add_argument("--out", default="run")
     ap.add_argument("--device", default="cuda" if torch.cuda.is_available() else "cpu")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--concurrent", type=int, default=1, help="independent runs executed at once on separate HIP streams")
     args = ap.parse_args(argv)
 
     a, _, b = args.funcs.partition("-")
@@ -80,40 +92,52 @@ def main(argv=None):
             f.write(f"{name}  ")
         best_all, hist_all = [], []
         steps = 0
-        for run in range(args.runs):
-            algo = getattr(de_variants, args.algo)(lb=lb, ub=ub, pop_size=args.pop)
-            mon = EvalMonitor(full_fit_history=False)
-            wf = StdWorkflow(algo, problem, monitors=[mon], graph=graph)
-            key, sub = rnd.split(key)
-            state = wf.init(sub)
-            hist = []
+        K = max(1, args.concurrent)
+        for run0 in range(0, args.runs, K):
+            batch = list(range(run0, min(args.runs, run0 + K)))
+            jobs = []
+            for run in batch:
+                algo = getattr(de_variants, args.algo)(lb=lb, ub=ub, pop_size=args.pop)
+                mon = EvalMonitor(full_fit_history=False)
+                wf = StdWorkflow(algo, problem, monitors=[mon], graph=graph)
+                key, sub = rnd.split(key)
+                stream = torch.cuda.Stream(device=dev) if dev.type == "cuda" and K > 1 else None
+                jobs.append({"run": run, "wf": wf, "mon": mon, "state": wf.init(sub), "hist": [], "stream": stream, "steps": 0, "done": False})
             t0 = time.time()
             for i in range(args.max_steps):
-                state = wf.step(state)
-                steps = i
-                if i % args.sync_every == 0 or i == args.max_steps - 1:
-                    hist.append(float(mon.get_best_fitness()))
-                elapsed = time.time() - t0
-                alg = state.get_child_state("algorithm")
-                upd = {}
-                if "progress" in alg.keys():
-                    upd["progress"] = elapsed / args.max_time
-                if "iter" in alg.keys() and not isinstance(alg.iter, torch.Tensor):
-                    upd["iter"] = i
-                if upd:
-                    state = state.update_child("algorithm", alg.update(**upd))
-                if elapsed >= args.max_time:
+                active = [j for j in jobs if not j["done"]]
+                if not active:
                     break
+                for j in active:
+                    with torch.cuda.stream(j["stream"]) if j["stream"] is not None else _nullcontext():
+                        state = j["wf"].step(j["state"])
+                        j["steps"] = i
+                        if i % args.sync_every == 0 or i == args.max_steps - 1:
+                            j["hist"].append(float(j["mon"].get_best_fitness()))
+                        elapsed = time.time() - t0
+                        alg = state.get_child_state("algorithm")
+                        upd = {}
+                        if "progress" in alg.keys():
+                            upd["progress"] = elapsed / args.max_time
+                        if "iter" in alg.keys() and not isinstance(alg.iter, torch.Tensor):
+                            upd["iter"] = i
+                        if upd:
+                            state = state.update_child("algorithm", alg.update(**upd))
+                        j["state"] = state
+                        if elapsed >= args.max_time:
+                            j["done"] = True
             if dev.type == "cuda":
                 torch.cuda.synchronize()
-            best = float(mon.get_best_fitness())
-            hist.append(best)
-            print(f"min fitness: {best}\nSteps: {steps} Runs: {run}\nTime: {time.time() - t0:.3f} s\n", flush=True)
-            if run >= 1 or args.runs == 1:
-                best_all.append(best)
-                hist_all.append(sample_history(args.samples, hist))
-                with open(res_path, "a") as f:
-                    f.write(f"{best} ")
+            for j in jobs:
+                run, steps = j["run"], j["steps"]
+                best = float(j["mon"].get_best_fitness())
+                j["hist"].append(best)
+                print(f"min fitness: {best}\nSteps: {steps} Runs: {run}\nTime: {time.time() - t0:.3f} s\n", flush=True)
+                if run >= 1 or args.runs == 1:
+                    best_all.append(best)
+                    hist_all.append(sample_history(args.samples, j["hist"]))
+                    with open(res_path, "a") as f:
+                        f.write(f"{best} ")
         with open(res_path, "a") as f:
             f.write(f"{steps * args.pop}\n")
         order = sorted(range(len(best_all)), key=lambda k: best_all[k])
