@@ -8,6 +8,7 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault("EVOXMI_CMA_FUSED", "0")  # the probe hooks warm_eigh (the unfused epilogue's entry point)
 import torch  # noqa: E402
 
 from evoxmi import random as rnd  # noqa: E402
