@@ -487,6 +487,18 @@ std::vector<at::Tensor> cma_eig_out(const at::Tensor& Bp, const at::Tensor& w, i
   return {B, D, BD};
 }
 
+at::Tensor nsga_select(const at::Tensor& rank, const at::Tensor& f, int64_t N, int64_t mask_pos) {
+  CHECK_DEV(rank); CHECK_CONTIG(rank); CHECK_DEV(f); CHECK_F32(f); CHECK_CONTIG(f);
+  TORCH_CHECK(rank.scalar_type() == at::kInt && f.dim() == 2 && rank.numel() == f.size(0), "nsga_select: rank int32 (n,), f (n, m)");
+  const int64_t n = f.size(0);
+  TORCH_CHECK(n >= 1 && n <= 8192, "nsga_select: 1 <= n <= 8192");
+  TORCH_CHECK(N >= 1 && N <= n && mask_pos >= N - 1 && mask_pos < n, "nsga_select: need N <= n and N-1 <= mask_pos < n");
+  c10::DeviceGuard g(f.device());
+  auto keep = at::empty({N}, f.options().dtype(at::kLong));
+  evx_nsga_select(rank.data_ptr<int>(), f.data_ptr<float>(), (int)n, (int)f.size(1), (int)N, (int)mask_pos, keep.data_ptr<int64_t>(), cur_stream());
+  return keep;
+}
+
 }  // namespace
 
 TORCH_LIBRARY(evoxmi, m) {
@@ -512,6 +524,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("cma_paths(Tensor ps, Tensor pc, Tensor y, Tensor delta, Tensor sigma, Tensor count_iter, float[] consts) -> Tensor[]");
   m.def("cma_cov_pad(Tensor C, Tensor S, Tensor pc, Tensor a, float c1, float cmu, Tensor Bprev, int np) -> Tensor[]");
   m.def("cma_eig_out(Tensor Bp, Tensor w, int d) -> Tensor[]");
+  m.def("nsga_select(Tensor rank, Tensor f, int N, int mask_pos) -> Tensor");
   m.def("moead_parents(Tensor nb, Tensor key) -> Tensor[]");
   m.def("moead_variation(Tensor pop, Tensor p0, Tensor p1, Tensor kx, Tensor km, Tensor lb, Tensor ub, float pro_c, float dis_c, float pro_m, float dis_m, int nm) -> Tensor");
   m.def("moead_replace(Tensor pop_obj, Tensor off_obj, Tensor W, Tensor z, Tensor zmax, Tensor rowptr, Tensor owner, int func) -> Tensor[]");
@@ -546,6 +559,7 @@ TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
   m.impl("cma_paths", &cma_paths);
   m.impl("cma_cov_pad", &cma_cov_pad);
   m.impl("cma_eig_out", &cma_eig_out);
+  m.impl("nsga_select", &nsga_select);
   m.impl("moead_parents", &moead_parents);
   m.impl("moead_variation", &moead_variation);
   m.impl("moead_replace", &moead_replace);

@@ -42,6 +42,10 @@ class MOAlgorithm(Algorithm):
 
 def nsga2_select(fitness, n):
     """Indices of the n survivors by (rank, −crowding) (reference ``eagmoead.py:22-30``)."""
+    if fitness.is_cuda and fitness.shape[0] <= 8192:
+        from ...ops import nds
+
+        return nds.nsga2_survivors(fitness, n, n - 1, until=n)
     rank = non_dominated_sort(fitness, until=n)
     worst = torch.sort(rank).values[n - 1]  # 0-d view: no host sync (capturable)
     cd = crowding_distance(fitness, rank == worst)

@@ -49,6 +49,12 @@ class NSGA2(Algorithm):
     def tell(self, state, fitness):
         merged_pop = torch.cat([state.population, state.next_generation], 0)
         merged_fit = torch.cat([state.fitness, fitness], 0)
+        if merged_fit.is_cuda and merged_fit.shape[0] <= 8192:
+            # fused selection kernel: same ranks/crowding/lexsort semantics as below
+            from ...ops import nds
+
+            keep = nds.nsga2_survivors(merged_fit, self.pop_size, self.pop_size, until=self.pop_size + 1)
+            return state.update(population=merged_pop[keep], fitness=merged_fit[keep])
         rank = non_dominated_sort(merged_fit, until=self.pop_size + 1)
         # the (pop_size)-th smallest rank, read as a 0-d view (no host sync: graph-capturable)
         worst = torch.sort(rank).values[self.pop_size]

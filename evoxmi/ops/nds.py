@@ -36,3 +36,12 @@ def crowding_distance(costs: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
     d.scatter_(1, order.gather(1, last.expand(m, 1)), inf.expand(m, 1))
     dist = d.sum(0)
     return torch.where(mask, dist, -inf)
+
+
+def nsga2_survivors(f: torch.Tensor, N: int, mask_pos: int, until: int = 0) -> torch.Tensor:
+    """Indices of the N survivors of NSGA-II environmental selection (rank, then crowding
+    distance on the front ``rank == sorted(rank)[mask_pos]``, lexsort order) — the fused
+    ``nsga_select.hip`` kernel after the device non-dominated sort (n ≤ 8192)."""
+    f = f.to(torch.float32).contiguous()
+    rank = non_dominated_sort(f, until)
+    return _ext.ops().nsga_select(rank, f, int(N), int(mask_pos))

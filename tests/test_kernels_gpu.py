@@ -665,3 +665,29 @@ def test_cmaes_fused_epilogue_matches_torch_ops(d):
     (rf, wf_), (rr, wr) = quality(f), quality(r)
     assert rf <= 1.5 * rr + 1e-4 and wf_ <= 1.5 * wr + 1e-4, (rf, rr, wf_, wr)
     assert torch.allclose(torch.sort(f.D).values, torch.sort(r.D).values, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("n,m,N,shift,front", [(8192, 3, 4096, 0, "rand"), (8192, 3, 4096, -1, "rand"), (300, 2, 150, 0, "rand"),
+                                                (200, 4, 100, -1, "rand"), (64, 3, 63, 0, "rand"), (8192, 3, 4096, 0, "pareto"),
+                                                (3000, 3, 1500, -1, "pareto"), (1500, 2, 750, 0, "pareto")])
+def test_nsga_select_kernel_matches_torch(n, m, N, shift, front):
+    """Fused NSGA-II selection == non_dominated_sort → crowding on the front of
+    sorted(rank)[mask_pos] → lexsort((−cd, rank))[:N] (CPU reference ops).  "pareto"
+    puts most rows on one front (the 2/4/8-items-per-thread crowding sorts)."""
+    from evoxmi.operators.selection.non_dominate import crowding_distance, lexsort, non_dominated_sort
+    from evoxmi.ops.nds import nsga2_survivors
+
+    g = torch.Generator().manual_seed(n + m)
+    f = torch.rand(n, m, generator=g)
+    if front == "pareto":
+        f[n // 8:] = f[n // 8:] / f[n // 8:].sum(1, keepdim=True)  # simplex: mutually non-dominated
+    f[: n // 10] = torch.round(f[: n // 10] * 8) / 8  # ties in objective values
+    f[5] = f[7]  # duplicate rows
+    f[9:12, 0] = torch.tensor([-0.0, 0.0, -0.0])  # signed zeros compare equal (radix keys canonicalised)
+    mask_pos = N + shift
+    rank = non_dominated_sort(f)
+    worst = torch.sort(rank).values[mask_pos]
+    cd = crowding_distance(f, rank == worst)
+    ref = lexsort([-cd, rank.to(cd.dtype)])[:N]
+    out = nsga2_survivors(f.cuda(), N, mask_pos, until=mask_pos + 1).cpu()
+    assert torch.equal(out, ref)
