@@ -64,23 +64,18 @@ __device__ __forceinline__ float sel4(int k, float a, float b, float c, float d)
   return k == 0 ? a : (k == 1 ? b : (k == 2 ? c : d));
 }
 
-__device__ __forceinline__ void substep_split(AntState& s, const float* tau, int leg, float lc, float ls, float sg) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int lg = j >> 1;
-    const bool ankle = j & 1;
-    const float sj = ankle ? ANK_SGN[lg] : 1.f;
-    const float lo = ankle ? ANK_LO : HIP_LO, hi = ankle ? ANK_HI : HIP_HI;
-    const float mag = s.jq[j] * sj;
-    const float viol = fmaxf(lo - mag, 0.f) - fmaxf(mag - hi, 0.f);
-    const float acc = (tau[j] - JD * s.jqd[j] + LIMK * viol * sj) * (1.f / JI);
-    s.jqd[j] += DT * acc;
-    s.jq[j] += DT * s.jqd[j];
-  }
-  const float hip = sel4(leg, s.jq[0], s.jq[2], s.jq[4], s.jq[6]);
-  const float ank = sel4(leg, s.jq[1], s.jq[3], s.jq[5], s.jq[7]);
-  const float hipd = sel4(leg, s.jqd[0], s.jqd[2], s.jqd[4], s.jqd[6]);
-  const float ankd = sel4(leg, s.jqd[1], s.jqd[3], s.jqd[5], s.jqd[7]);
+__device__ __forceinline__ void joint_step(float& q, float& qd, float tau, float sj, float lo, float hi) {
+  const float mag = q * sj;
+  const float viol = fmaxf(lo - mag, 0.f) - fmaxf(mag - hi, 0.f);
+  const float acc = (tau - JD * qd + LIMK * viol * sj) * (1.f / JI);
+  qd += DT * acc;
+  q += DT * qd;
+}
+
+// Body part of a sub-step: this lane's leg (foot by forward kinematics, penalty contact),
+// quad-summed force/torque, then the lane-uniform body integration.
+template <class S>
+__device__ __forceinline__ void body_step(S& s, float hip, float ank, float hipd, float ankd, float lc, float ls, float sg) {
   const float a = ank * sg;
   const float ca = __cosf(a), sa = __sinf(a), ch = __cosf(hip), sh = __sinf(hip);
   const float cphi = lc * ch - ls * sh, sphi = ls * ch + lc * sh;
@@ -122,6 +117,34 @@ __device__ __forceinline__ void substep_split(AntState& s, const float* tau, int
   const float in = rsqrtf(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
 #pragma unroll
   for (int c = 0; c < 4; ++c) s.q[c] = nq[c] * in;
+}
+
+// LDS kernel: all eight joints lane-uniform, then this lane's leg
+__device__ __forceinline__ void substep_split(AntState& s, const float* tau, int leg, float lc, float ls, float sg) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const bool ankle = j & 1;
+    joint_step(s.jq[j], s.jqd[j], tau[j], ankle ? ANK_SGN[j >> 1] : 1.f, ankle ? ANK_LO : HIP_LO, ankle ? ANK_HI : HIP_HI);
+  }
+  const float hip = sel4(leg, s.jq[0], s.jq[2], s.jq[4], s.jq[6]);
+  const float ank = sel4(leg, s.jq[1], s.jq[3], s.jq[5], s.jq[7]);
+  const float hipd = sel4(leg, s.jqd[0], s.jqd[2], s.jqd[4], s.jqd[6]);
+  const float ankd = sel4(leg, s.jqd[1], s.jqd[3], s.jqd[5], s.jqd[7]);
+  body_step(s, hip, ank, hipd, ankd, lc, ls, sg);
+}
+
+// Register kernel: lane quad position `leg` owns that leg's two joints (the same
+// operations as substep_split, so bit-identical), which removes ~70 lane-uniform
+// instructions per sub-step; the observation gathers the joints with v_readlane.
+struct AntBody {
+  float p[3], q[4], v[3], w[3];
+};
+
+__device__ __forceinline__ void substep_leg(AntBody& s, float& hip, float& ank, float& hipd, float& ankd, float th, float ta,
+                                            float lc, float ls, float sg) {
+  joint_step(hip, hipd, th, 1.f, HIP_LO, HIP_HI);
+  joint_step(ank, ankd, ta, sg, ANK_LO, ANK_HI);
+  body_step(s, hip, ank, hipd, ankd, lc, ls, sg);
 }
 
 // layer sizes: in = 27, hidden h1, h2 (any, ≤ 256), out = 8; tanh everywhere
@@ -214,19 +237,35 @@ __global__ void __launch_bounds__(256) ant_rollout_kernel(const float* __restric
 
 // Register-resident variant for h1, h2 <= 64 (the north-star 27-64-64-8 policy):
 // lane j keeps column j of W1 / W2 and row j of W3 in VGPRs (≈100 registers), so
-// the control step touches neither LDS nor memory.  The observation is already
-// lane-uniform (the physics runs redundantly on every lane), layer 2 broadcasts
-// a1[i] with v_readlane, and layer 3's eight 64-lane dot products are reduced by a
-// transposing butterfly (4+2+1 exchanges that halve the live values per stage,
-// then 3 full stages: 10 lane exchanges instead of 48).  Unused units are zero
-// padded, which keeps their activations at tanh(0) = 0.
+// the control step touches no memory.  The body part of the observation is lane-uniform
+// (the body integration runs redundantly on every lane), the joints come from the
+// leg-owning lanes by v_readlane, layer 2 broadcasts a1 through 256 B of LDS, and
+// layer 3's eight 64-lane dot products are reduced by a transposing butterfly (4+2+1
+// exchanges that halve the live values per stage, then 3 full stages: 10 lane
+// exchanges instead of 48, all permlane-swap / DPP, none through the LDS permute
+// unit).  Unused units are zero padded, which keeps their activations at tanh(0) = 0.
 __device__ __forceinline__ float rl(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+// cross-lane partners without the LDS permute unit (ds_bpermute costs an LDS round trip
+// per exchange on the step's critical path): gfx950 permlane swaps for lane ^ 32 and
+// lane ^ 16, DPP row rotate for lane ^ 8
+__device__ __forceinline__ float xor32(float x, bool hi) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(hi ? r[0] : r[1]);
+}
+__device__ __forceinline__ float xor16(float x, bool hi) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(hi ? r[0] : r[1]);
+}
+__device__ __forceinline__ float xor8(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x128, 0xF, 0xF, false));  // row_ror:8
 }
 
 __global__ void __launch_bounds__(64, 2) ant_rollout_reg_kernel(const float* __restrict__ W, int64_t P, int N, int h1, int h2,
                                                               const float* __restrict__ init, int cap, float* __restrict__ ret,
                                                               int* __restrict__ steps_out) {
+  __shared__ float a1s[64];
   const int lane = threadIdx.x & 63;
   // one wave per workgroup: a finished episode frees its slot immediately, which
   // matters because episode lengths differ by orders of magnitude
@@ -251,13 +290,13 @@ __global__ void __launch_bounds__(64, 2) ant_rollout_reg_kernel(const float* __r
     w3[k] = u2 ? W3[lane * 8 + k] : 0.f;
     b3[k] = B3[k];
   }
-  AntState s;
+  AntBody s;
   for (int i = 0; i < 3; ++i) s.p[i] = init[i];
   for (int i = 0; i < 4; ++i) s.q[i] = init[3 + i];
   for (int i = 0; i < 3; ++i) s.v[i] = init[7 + i];
   for (int i = 0; i < 3; ++i) s.w[i] = init[10 + i];
-  for (int i = 0; i < 8; ++i) s.jq[i] = init[13 + i];
-  for (int i = 0; i < 8; ++i) s.jqd[i] = init[21 + i];
+  const int lg = lane & 3;
+  float hq = init[13 + 2 * lg], aq = init[14 + 2 * lg], hqd = init[21 + 2 * lg], aqd = init[22 + 2 * lg];
   const bool hb5 = lane & 32, hb4 = lane & 16, hb3 = lane & 8;
   const int leg = lane & 3;
   const float lc = LEG_COS[leg], ls = LEG_SIN[leg], lsg = ANK_SGN[leg];
@@ -269,20 +308,34 @@ __global__ void __launch_bounds__(64, 2) ant_rollout_reg_kernel(const float* __r
 #pragma unroll
     for (int i = 0; i < 4; ++i) o[1 + i] = s.q[i];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) o[5 + i] = s.jq[i];
+    for (int l = 0; l < 4; ++l) {
+      o[5 + 2 * l] = rl(hq, l);
+      o[6 + 2 * l] = rl(aq, l);
+      o[19 + 2 * l] = rl(hqd, l);
+      o[20 + 2 * l] = rl(aqd, l);
+    }
 #pragma unroll
     for (int i = 0; i < 3; ++i) o[13 + i] = s.v[i];
 #pragma unroll
     for (int i = 0; i < 3; ++i) o[16 + i] = s.w[i];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) o[19 + i] = s.jqd[i];
     float acc = b1;
 #pragma unroll
     for (int i = 0; i < 27; ++i) acc = fmaf(o[i], w1[i], acc);
-    const float a1 = fast_tanh(acc);
+    // layer 2: a1 is broadcast through 256 B of LDS (16 ds_read_b128 instead of 64
+    // v_readlane + SGPR hazard nops)
+    a1s[lane] = fast_tanh(acc);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     float c4[4] = {b2, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < 64; ++i) c4[i & 3] = fmaf(rl(a1, i), w2[i], c4[i & 3]);
+    for (int i = 0; i < 16; ++i) {
+      const float4 a = reinterpret_cast<const float4*>(a1s)[i];
+      c4[0] = fmaf(a.x, w2[4 * i], c4[0]);
+      c4[1] = fmaf(a.y, w2[4 * i + 1], c4[1]);
+      c4[2] = fmaf(a.z, w2[4 * i + 2], c4[2]);
+      c4[3] = fmaf(a.w, w2[4 * i + 3], c4[3]);
+    }
     const float a2 = fast_tanh((c4[0] + c4[1]) + (c4[2] + c4[3]));
     // 8 partial products → transposing butterfly reduction
     float v4[4], v2[2], v1;
@@ -290,22 +343,21 @@ __global__ void __launch_bounds__(64, 2) ant_rollout_reg_kernel(const float* __r
     for (int j = 0; j < 4; ++j) {
       const float keep = hb5 ? a2 * w3[j + 4] : a2 * w3[j];
       const float send = hb5 ? a2 * w3[j] : a2 * w3[j + 4];
-      v4[j] = keep + __shfl_xor(send, 32, 64);
+      v4[j] = keep + xor32(send, hb5);
     }
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const float keep = hb4 ? v4[j + 2] : v4[j];
       const float send = hb4 ? v4[j] : v4[j + 2];
-      v2[j] = keep + __shfl_xor(send, 16, 64);
+      v2[j] = keep + xor16(send, hb4);
     }
     {
       const float keep = hb3 ? v2[1] : v2[0];
       const float send = hb3 ? v2[0] : v2[1];
-      v1 = keep + __shfl_xor(send, 8, 64);
+      v1 = keep + xor8(send);
     }
-    v1 += __shfl_xor(v1, 4, 64);
-    v1 += __shfl_xor(v1, 2, 64);
-    v1 += __shfl_xor(v1, 1, 64);
+    v1 = quad_sum(v1);  // lanes ^1, ^2
+    v1 += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v1), 0x141, 0xF, 0xF, false));  // row_half_mirror: the other quad
     float tau[8], csum = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -315,8 +367,9 @@ __global__ void __launch_bounds__(64, 2) ant_rollout_reg_kernel(const float* __r
       csum += a * a;
     }
     const float x0 = s.p[0];
+    const float th = sel4(leg, tau[0], tau[2], tau[4], tau[6]), ta = sel4(leg, tau[1], tau[3], tau[5], tau[7]);
     #pragma unroll 1
-    for (int k = 0; k < SUB; ++k) substep_split(s, tau, leg, lc, ls, lsg);
+    for (int k = 0; k < SUB; ++k) substep_leg(s, hq, aq, hqd, aqd, th, ta, lc, ls, lsg);
     const bool healthy = (s.p[2] >= 0.2f) && (s.p[2] <= 1.0f);
     if (!healthy) break;
     total += (s.p[0] - x0) * (1.f / (DT * SUB)) + 1.f - 0.5f * csum;
