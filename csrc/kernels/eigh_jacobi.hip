@@ -52,10 +52,17 @@ __device__ __forceinline__ void rot_params(float app, float aqq, float apq, floa
   }
 }
 
+__device__ __forceinline__ float rl(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ float row_pick(int row, float a, float b, float c, float d) {
+  return row < 2 ? (row == 0 ? a : b) : (row == 2 ? c : d);
+}
+
 // 256 threads per 32×32 subproblem: thread t owns the 2×2 block (row pair k = t>>4,
 // col pair l = t&15) of S and the V items (rows 2k, 2k+1 × col pair l).  Each thread
 // computes ONE rotation (its column pair l) from S; the row-pair rotation k is taken
-// from lane (k, k) of the same wave with a cross-lane shuffle.  Per inner round: one
+// from lane (k, k) of the same wave with one v_readlane per 16-lane row.  Per inner round: one
 // LDS read phase, barrier, one LDS write phase, barrier.
 // MODE 0 ("cross"): 16 inner rounds pairing I[x] with J[(x + r) mod 16] — only the
 //   coupling block A_IJ is annihilated; within-block pairs are handled by MODE 1.
@@ -93,7 +100,8 @@ __global__ void __launch_bounds__(256) jacobi_solve_kernel(const float* __restri
   }
   __syncthreads();
   const int k = t >> 4, l = t & 15;
-  const int src_lane = ((k & 3) << 4) | k;  // lane (k, k) inside this wave
+  const int row = k & 3;                                     // 16-lane row of this thread
+  const int w4 = __builtin_amdgcn_readfirstlane((t >> 6) << 2);  // first k of this wave
   const int vr0 = 2 * k, vr1 = 2 * k + 1;
   for (int sweep = 0; sweep < max_inner; ++sweep) {
     float off = 0.f, dia = 0.f;
@@ -136,7 +144,10 @@ __global__ void __launch_bounds__(256) jacobi_solve_kernel(const float* __restri
         cl = __builtin_amdgcn_rsqf(fmaf(tt, tt, 1.f));
         sl = tt * cl;
       }
-      const float ck = __shfl(cl, src_lane, 64), sk = __shfl(sl, src_lane, 64);
+      // row-pair rotation from lane (k, k): one v_readlane per 16-lane row (k = 4·wave + row)
+      // instead of a ds_bpermute round trip on the round's critical path
+      const float ck = row_pick(row, rl(cl, w4), rl(cl, 17 + w4), rl(cl, 34 + w4), rl(cl, 51 + w4));
+      const float sk = row_pick(row, rl(sl, w4), rl(sl, 17 + w4), rl(sl, 34 + w4), rl(sl, 51 + w4));
       float y00 = ck * x00 - sk * x10, y01 = ck * x01 - sk * x11;
       float y10 = sk * x00 + ck * x10, y11 = sk * x01 + ck * x11;
       float o00 = y00 * cl - y01 * sl, o01 = y00 * sl + y01 * cl;
