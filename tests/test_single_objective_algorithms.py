@@ -216,3 +216,25 @@ def test_knn_circles_topology():
     adj = topo.get_circles_neighbour(rnd.PRNGKey(0), pop, K=2, shortcut=3)
     assert torch.equal(adj, adj.T) and bool((adj.diag() == 1).all())
     assert int(adj.sum(1).min()) >= 2
+
+
+@pytest.mark.parametrize("name", ["IPOPCMAES", "BIPOPCMAES"])
+def test_restart_cmaes_changes_sample_count(name):
+    """IPOP/BIPOP restarts really resize the population (the reference's static shapes
+    never change the sample count) and keep optimising afterwards."""
+    import evoxmi.algorithms as A
+    from evoxmi.problems.numerical import Sphere
+    from evoxmi.workflows import StdWorkflow
+
+    algo = getattr(A, name)(torch.full((5,), 3.0), init_stdev=1.0, pop_size=8, stagnation_threshold=3)
+    wf = StdWorkflow(algo, Sphere())
+    st = wf.init(rnd.PRNGKey(2))
+    sizes = set()
+    for _ in range(60):
+        st = wf.step(st)
+        a = st.get_child_state("algorithm")
+        sizes.add(int(a.pop_size))
+        assert a.population.shape[0] == int(a.pop_size) or a.restarts > 0
+    a = st.get_child_state("algorithm")
+    assert a.restarts >= 1 and len(sizes) >= 2 and min(sizes) == 8
+    assert torch.isfinite(a.mean).all()

@@ -225,3 +225,27 @@ def test_pop_monitor(fitness_only):
     assert (m.get_latest_fitness() == st.get_child_state("algorithm").fitness).all()
     if not fitness_only:
         assert (m.get_latest_population() == st.get_child_state("algorithm").population).all()
+
+
+def test_evoxvis_monitor_arrow_round_trip(tmp_path):
+    """EvoXVisMonitor registers as a workflow monitor (the reference's cannot)
+    and its Arrow IPC file reads back generation-by-generation."""
+    import numpy as np
+
+    from evoxmi.algorithms import PSO
+    from evoxmi.monitors.evoxvis_monitor import EvoXVisMonitor, read_evoxvis
+    from evoxmi.problems.numerical import Sphere
+    from evoxmi.workflows import StdWorkflow
+
+    mon = EvoXVisMonitor("run", out_dir=str(tmp_path), batch_size=3)
+    wf = StdWorkflow(PSO(torch.full((4,), -5.0), torch.full((4,), 5.0), 10), Sphere(), monitors=[mon])
+    st = wf.init(rnd.PRNGKey(0))
+    for _ in range(7):
+        st = wf.step(st)
+    mon.close()
+    out = read_evoxvis(mon.path)
+    assert out["generation"] == list(range(7))
+    assert all(f.shape == (10,) for f in out["fitness"]) and all(p.shape == (10, 4) for p in out["population"])
+    for f, p in zip(out["fitness"], out["population"]):
+        assert np.allclose(f, (p.astype(np.float64) ** 2).sum(1), rtol=1e-5)  # Sphere of the recorded population
+    assert out["duration"] == sorted(out["duration"])
