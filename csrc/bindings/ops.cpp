@@ -173,7 +173,7 @@ at::Tensor cec_basic(const at::Tensor& Z, int64_t fid, const c10::optional<at::T
 // are enqueued on the current stream; convergence is a device flag, so the call is
 // graph-capturable.  Returns [w(np) diag of A, stats(2) = (off², diag²) at the last check].
 std::vector<at::Tensor> jacobi_sweeps(at::Tensor A, at::Tensor B, const at::Tensor& sched, int64_t sweeps, double tol,
-                                      double inner_tol, int64_t max_inner) {
+                                      double inner_tol, int64_t max_inner, int64_t fused) {
   CHECK_DEV(A); CHECK_F32(A); CHECK_CONTIG(A); CHECK_DEV(B); CHECK_F32(B); CHECK_CONTIG(B);
   const int64_t np = A.size(0);
   TORCH_CHECK(A.dim() == 2 && A.size(1) == np && B.sizes() == A.sizes(), "A, B must be np×np");
@@ -187,14 +187,37 @@ std::vector<at::Tensor> jacobi_sweeps(at::Tensor A, at::Tensor B, const at::Tens
   auto flag = at::zeros({1}, opts.dtype(at::kInt));
   auto part = at::empty({2 * evx_jacobi_parts()}, opts.dtype(at::kDouble));
   auto stats = at::zeros({2}, opts.dtype(at::kDouble));
-  auto Vbuf = at::empty({(np / 32) * 32 * 32}, opts);
+  const int64_t npairs = np / 32;
   hipStream_t st = cur_stream();
   const double tol2 = tol * tol;
   evx_jacobi_check(A.data_ptr<float>(), (int)np, part.data_ptr<double>(), flag.data_ptr<int>(), tol2, stats.data_ptr<double>(), st);
+  const int* sp = sched.data_ptr<int>();
+  if (!fused) {
+    auto Vbuf = at::empty({npairs * 32 * 32}, opts);
+    for (int64_t sw = 0; sw < sweeps; ++sw) {
+      for (int64_t t = 0; t < nb; ++t)
+        evx_jacobi_round(A.data_ptr<float>(), B.data_ptr<float>(), (int)np, sp + t * nb, Vbuf.data_ptr<float>(),
+                         flag.data_ptr<int>(), (float)inner_tol, (int)max_inner, t == 0 ? 1 : 0, st);
+      evx_jacobi_check(A.data_ptr<float>(), (int)np, part.data_ptr<double>(), flag.data_ptr<int>(), tol2, stats.data_ptr<double>(), st);
+    }
+    return {A.diagonal().clone(), stats};
+  }
+  // fused: every apply launch also solves the next round's subproblems (V double-buffered)
+  TORCH_CHECK(nb <= 256, "fused Jacobi: np <= 4096");
+  auto Vbuf = at::empty({2, npairs * 32 * 32}, opts);
+  auto counters = at::zeros({std::max<int64_t>(sweeps, 1) * nb * npairs}, opts.dtype(at::kInt));
+  float* V[2] = {Vbuf[0].data_ptr<float>(), Vbuf[1].data_ptr<float>()};
+  if (sweeps > 0)
+    evx_jacobi_solve(A.data_ptr<float>(), (int)np, sp, V[0], flag.data_ptr<int>(), (float)inner_tol, (int)max_inner, 1, st);
   for (int64_t sw = 0; sw < sweeps; ++sw) {
-    for (int64_t t = 0; t < nb; ++t)
-      evx_jacobi_round(A.data_ptr<float>(), B.data_ptr<float>(), (int)np, sched.data_ptr<int>() + t * nb, Vbuf.data_ptr<float>(),
-                       flag.data_ptr<int>(), (float)inner_tol, (int)max_inner, t == 0 ? 1 : 0, st);
+    for (int64_t t = 0; t < nb; ++t) {
+      const int64_t r = sw * nb + t;
+      const bool last = sw == sweeps - 1 && t == nb - 1;
+      const int64_t tn = (t + 1) % nb;
+      evx_jacobi_apply_solve(A.data_ptr<float>(), B.data_ptr<float>(), (int)np, sp + t * nb, V[r & 1], flag.data_ptr<int>(),
+                             last ? nullptr : sp + tn * nb, tn == 0 ? 1 : 0, V[(r + 1) & 1], counters.data_ptr<int>() + r * npairs,
+                             (float)inner_tol, (int)max_inner, st);
+    }
     evx_jacobi_check(A.data_ptr<float>(), (int)np, part.data_ptr<double>(), flag.data_ptr<int>(), tol2, stats.data_ptr<double>(), st);
   }
   return {A.diagonal().clone(), stats};
@@ -505,7 +528,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("philox_fill(Tensor key, int n, int dist, int offset) -> Tensor");
   m.def("argsort_f32(Tensor keys, int descending) -> Tensor[]");
   m.def("cec_basic(Tensor Z, int fid, Tensor? perm, int start, int L, Tensor? sub, float scale, Tensor? Y, int ystart, int yperm) -> Tensor");
-  m.def("jacobi_sweeps(Tensor A, Tensor B, Tensor sched, int sweeps, float tol, float inner_tol, int max_inner) -> Tensor[]");
+  m.def("jacobi_sweeps(Tensor A, Tensor B, Tensor sched, int sweeps, float tol, float inner_tol, int max_inner, int fused=0) -> Tensor[]");
   m.def("philox_words(Tensor key, int nblocks, int domain, int offset) -> Tensor");
   m.def("weighted_rowsum(Tensor X, Tensor? idx, Tensor w, Tensor? sub, int K) -> Tensor");
   m.def("gemm_set_config(int cfg) -> ()");

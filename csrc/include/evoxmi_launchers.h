@@ -31,6 +31,13 @@ void evx_cec_basic(const float* Z, int64_t ld, int N, int fid, const int32_t* pe
                    float scale, const float* Y, int64_t ldy, int ystart, int yperm, float* out, hipStream_t s);
 void evx_jacobi_round(float* A, float* B, int np, const int* sched_t, float* Vbuf, const int* flag, float inner_tol,
                       int max_inner, int mode, hipStream_t s);
+void evx_jacobi_solve(const float* A, int np, const int* sched_t, float* Vbuf, const int* flag, float inner_tol, int max_inner,
+                      int mode, hipStream_t s);
+// round t's apply; with sched_next != nullptr the same launch also solves round t+1's
+// subproblems into Vnext (counters: npairs ints, zeroed, private to this round)
+void evx_jacobi_apply_solve(float* A, float* B, int np, const int* sched_t, const float* Vcur, const int* flag,
+                            const int* sched_next, int mode_next, float* Vnext, int* counters, float inner_tol, int max_inner,
+                            hipStream_t s);
 void evx_jacobi_check(const float* A, int np, double* part, int* flag, double tol2, double* last_off, hipStream_t s);
 int evx_jacobi_parts();
 void evx_philox_words(const int64_t* key, int64_t nblocks, uint32_t domain, int64_t offset, int64_t* out, hipStream_t s);

@@ -67,20 +67,23 @@ __device__ __forceinline__ float row_pick(int row, float a, float b, float c, fl
 // MODE 0 ("cross"): 16 inner rounds pairing I[x] with J[(x + r) mod 16] — only the
 //   coupling block A_IJ is annihilated; within-block pairs are handled by MODE 1.
 // MODE 1 ("within"): 15 circle-method rounds inside I and inside J simultaneously.
+// S is double-buffered: a round reads Sc and writes every element of Sn (the 2×2 blocks
+// of the 256 threads tile the 32×32 matrix), so the read and write phases need no
+// barrier in between; V has one owner per element within a round (single buffer).
+struct SolveSmem {
+  float Sbuf[2][PS * LDS_S];
+  float V[PS * LDS_V];
+  float red[8];
+};
+
 template <int MODE>
-__global__ void __launch_bounds__(256) jacobi_solve_kernel(const float* __restrict__ A, int np, const int* __restrict__ sched,
-                                                           float* __restrict__ Vout, const int* __restrict__ flag,
-                                                           float tol, int max_inner) {
-  if (flag && *flag) return;
-  // S is double-buffered: a round reads Sc and writes every element of Sn (the 2×2 blocks
-  // of the 256 threads tile the 32×32 matrix), so the read and write phases need no
-  // barrier in between; V has one owner per element within a round (single buffer).
-  __shared__ float Sbuf[2][PS * LDS_S];
-  __shared__ float V[PS * LDS_V];
-  __shared__ float red[8];
+__device__ void solve_pair(const float* __restrict__ A, int np, const int* __restrict__ sched, int P, float* __restrict__ Vout,
+                           float tol, int max_inner, SolveSmem& sm) {
+  float (*Sbuf)[PS * LDS_S] = sm.Sbuf;
+  float* V = sm.V;
+  float* red = sm.red;
   float* S = Sbuf[0];
   const int t = threadIdx.x;
-  const int P = blockIdx.x;
   const int blkI = sched[2 * P], blkJ = sched[2 * P + 1];
   for (int e = t; e < PS * PS; e += 256) {
     int i = e >> 5, j = e & 31;
@@ -168,22 +171,31 @@ __global__ void __launch_bounds__(256) jacobi_solve_kernel(const float* __restri
   }
   float* Vo = Vout + (int64_t)P * PS * PS;
   for (int e = t; e < PS * PS; e += 256) Vo[e] = V[(e >> 5) * LDS_V + (e & 31)];
+  __syncthreads();  // LDS reuse by the caller
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(256) jacobi_solve_kernel(const float* __restrict__ A, int np, const int* __restrict__ sched,
+                                                           float* __restrict__ Vout, const int* __restrict__ flag,
+                                                           float tol, int max_inner) {
+  if (flag && *flag) return;
+  __shared__ SolveSmem sm;
+  solve_pair<MODE>(A, np, sched, blockIdx.x, Vout, tol, max_inner, sm);
 }
 
 // ---------------------------------------------------------------------------------- apply
 // One wave per 32×32 tile; all global loads of the tile and of V_Q / V_P are issued up
 // front (independent registers) so one memory latency covers the whole tile.
-__global__ void __launch_bounds__(256) jacobi_apply_kernel(float* __restrict__ A, float* __restrict__ B, int np,
-                                                           const int* __restrict__ sched, const float* __restrict__ Vp,
-                                                           const int* __restrict__ flag) {
-  if (flag && *flag) return;
-  __shared__ float T0s[4][PS * LDP];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  float* T0 = T0s[wv];
+typedef __attribute__((address_space(1))) float gf32;
+
+// PUBLISH: the A tile is stored write-through (sc1, agent-scope relaxed atomic stores) so
+// a workgroup on another XCD can read it in the same launch after an acquire
+template <bool PUBLISH>
+__device__ __forceinline__ void apply_tile(float* __restrict__ A, float* __restrict__ B, int np, const int* __restrict__ sched,
+                                           const float* __restrict__ Vp, int tile, float* T0) {
+  const int lane = threadIdx.x & 63;
   const int npairs = np / PS;
-  const int tile = blockIdx.x * 4 + wv;
   const int nA = npairs * npairs;
-  if (tile >= 2 * nA) return;
   const bool isA = tile < nA;
   int P = 0, Q, row0 = 0;
   if (isA) { P = tile / npairs; Q = tile % npairs; }
@@ -231,7 +243,92 @@ __global__ void __launch_bounds__(256) jacobi_apply_kernel(float* __restrict__ A
   for (int r = 0; r < 16; ++r) {
     const int i = (r & 3) + 8 * (r >> 2) + 4 * h;
     const int gi = isA ? ((i < 16 ? pI : pJ) * BS + (i & 15)) : row0 + i;
-    M[(int64_t)gi * np + gj] = out[r];
+    if (PUBLISH && isA) __hip_atomic_store((gf32*)(M + (int64_t)gi * np + gj), out[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else M[(int64_t)gi * np + gj] = out[r];
+  }
+}
+
+__global__ void __launch_bounds__(256) jacobi_apply_kernel(float* __restrict__ A, float* __restrict__ B, int np,
+                                                           const int* __restrict__ sched, const float* __restrict__ Vp,
+                                                           const int* __restrict__ flag) {
+  if (flag && *flag) return;
+  __shared__ float T0s[4][PS * LDP];
+  const int wv = threadIdx.x >> 6;
+  const int npairs = np / PS;
+  const int tile = blockIdx.x * 4 + wv;
+  if (tile >= 2 * npairs * npairs) return;
+  apply_tile<false>(A, B, np, sched, Vp, tile, T0s[wv]);
+}
+
+// ------------------------------------------------------------------------- fused apply + next solve
+// Round t's apply, and the subproblem solves of round t+1 in the same launch: the next
+// pair P' = (X, Y) reads the blocks (X,X), (X,Y), (Y,X), (Y,Y) of the updated A, which
+// live in 1 (X, Y from one current pair) or 4 current tiles.  A tiles are stored
+// write-through (sc1: the XCDs' L2s are not coherent with each other, and a per-workgroup
+// buffer_wbl2 release made the first version 5x slower), each wave drains its stores,
+// and after the workgroup barrier one lane per tile counts the tile's contributions on a
+// per-(round, pair) counter (relaxed agent-scope atomic); the workgroup that completes a
+// pair's count acquires (L1 invalidate) and solves it while other tiles are still being
+// applied.  This removes the separate solve launch and overlaps the
+// latency-bound 32×32 solves with the tail of the apply.
+constexpr int MAXNB = 256;  // np ≤ 4096
+
+__global__ void __launch_bounds__(256) jacobi_apply_solve_kernel(float* __restrict__ A, float* __restrict__ B, int np,
+                                                                 const int* __restrict__ sched, const float* __restrict__ Vp,
+                                                                 const int* __restrict__ flag, const int* __restrict__ sched_next,
+                                                                 int mode_next, float* __restrict__ Vnext, int* __restrict__ counters,
+                                                                 float tol, int max_inner) {
+  if (flag && *flag) return;
+  __shared__ float T0s[4][PS * LDP];
+  __shared__ SolveSmem sm;
+  __shared__ int pair_cur[MAXNB], pair_next[MAXNB];
+  __shared__ int todo[8], ntodo;
+  const int wv = threadIdx.x >> 6;
+  const int npairs = np / PS, nb = np / BS;
+  const int nA = npairs * npairs;
+  const int tile = blockIdx.x * 4 + wv;
+  if (tile < 2 * nA) apply_tile<true>(A, B, np, sched, Vp, tile, T0s[wv]);
+  // block → pair maps of this round and the next
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) {
+    pair_cur[sched[i]] = i >> 1;
+    pair_next[sched_next[i]] = i >> 1;
+  }
+  if (threadIdx.x == 0) ntodo = 0;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    const int tl = blockIdx.x * 4 + threadIdx.x;
+    if (tl < nA) {
+      const int P = tl / npairs, Q = tl % npairs;
+      const int rb[2] = {sched[2 * P], sched[2 * P + 1]}, cb[2] = {sched[2 * Q], sched[2 * Q + 1]};
+      int seen[4], ns = 0;
+      for (int x = 0; x < 2; ++x)
+        for (int y = 0; y < 2; ++y) {
+          const int pn = pair_next[rb[x]];
+          if (pn != pair_next[cb[y]]) continue;
+          bool dup = false;
+          for (int u = 0; u < ns; ++u) dup |= seen[u] == pn;
+          if (dup) continue;
+          seen[ns++] = pn;
+          const int X = sched_next[2 * pn], Y = sched_next[2 * pn + 1];
+          const int target = pair_cur[X] == pair_cur[Y] ? 1 : 4;
+          if (atomicAdd(&counters[pn], 1) + 1 == target) todo[atomicAdd(&ntodo, 1)] = pn;
+        }
+    }
+  }
+  __syncthreads();
+  const int nt = ntodo;
+  if (nt == 0) return;  // uniform
+  // acquire: one lane invalidates this CU's L1, waits for it, and the barrier releases
+  // the other waves' loads behind it
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  for (int i = 0; i < nt; ++i) {
+    if (mode_next) solve_pair<1>(A, np, sched_next, todo[i], Vnext, tol, max_inner, sm);
+    else solve_pair<0>(A, np, sched_next, todo[i], Vnext, tol, max_inner, sm);
   }
 }
 
@@ -288,6 +385,28 @@ void evx_jacobi_round(float* A, float* B, int np, const int* sched_t, float* Vbu
     jacobi_solve_kernel<1><<<npairs, 256, 0, s>>>(A, np, sched_t, Vbuf, flag, inner_tol, max_inner);
   const int tiles = 2 * npairs * npairs;
   jacobi_apply_kernel<<<(tiles + 3) / 4, 256, 0, s>>>(A, B, np, sched_t, Vbuf, flag);
+}
+
+void evx_jacobi_solve(const float* A, int np, const int* sched_t, float* Vbuf, const int* flag, float inner_tol, int max_inner,
+                      int mode, hipStream_t s) {
+  const int npairs = np / PS;
+  if (mode == 0)
+    jacobi_solve_kernel<0><<<npairs, 256, 0, s>>>(A, np, sched_t, Vbuf, flag, inner_tol, max_inner);
+  else
+    jacobi_solve_kernel<1><<<npairs, 256, 0, s>>>(A, np, sched_t, Vbuf, flag, inner_tol, max_inner);
+}
+
+void evx_jacobi_apply_solve(float* A, float* B, int np, const int* sched_t, const float* Vcur, const int* flag,
+                            const int* sched_next, int mode_next, float* Vnext, int* counters, float inner_tol, int max_inner,
+                            hipStream_t s) {
+  const int npairs = np / PS;
+  const int tiles = 2 * npairs * npairs;
+  if (sched_next == nullptr) {
+    jacobi_apply_kernel<<<(tiles + 3) / 4, 256, 0, s>>>(A, B, np, sched_t, Vcur, flag);
+    return;
+  }
+  jacobi_apply_solve_kernel<<<(tiles + 3) / 4, 256, 0, s>>>(A, B, np, sched_t, Vcur, flag, sched_next, mode_next, Vnext, counters,
+                                                            inner_tol, max_inner);
 }
 
 void evx_jacobi_check(const float* A, int np, double* part, int* flag, double tol2, double* last_off, hipStream_t s) {

@@ -94,7 +94,7 @@ def warm_eigh(C: torch.Tensor, B_prev: torch.Tensor = None, max_sweeps: int = No
         sweeps = config.get("jacobi_sweeps") if max_sweeps is None else max_sweeps
     tol = tol or config.get("jacobi_tol_factor") * 1.1920929e-07 * max(n, 16) ** 0.5
     w, stats = _ext.ops().jacobi_sweeps(A, Bp, schedule(np_ // 16, dev), int(sweeps), float(tol),
-                                        float(config.get("jacobi_inner_tol")), int(config.get("jacobi_inner")))
+                                        float(config.get("jacobi_inner_tol")), int(config.get("jacobi_inner")), int(config.get("jacobi_fused")))
     out = (w[:n].contiguous(), Bp[:n, :n].contiguous())
     return (*out, stats) if return_stats else out
 
@@ -117,7 +117,7 @@ def warm_eigh_padded(Cp: torch.Tensor, Bp: torch.Tensor, n: int, max_sweeps: int
     sweeps = config.get("jacobi_sweeps") if max_sweeps is None else max_sweeps
     tol = tol or config.get("jacobi_tol_factor") * 1.1920929e-07 * max(n, 16) ** 0.5
     w, _ = _ext.ops().jacobi_sweeps(A, Bp, schedule(np_ // 16, Cp.device), int(sweeps), float(tol),
-                                    float(config.get("jacobi_inner_tol")), int(config.get("jacobi_inner")))
+                                    float(config.get("jacobi_inner_tol")), int(config.get("jacobi_inner")), int(config.get("jacobi_fused")))
     return w, Bp
 
 

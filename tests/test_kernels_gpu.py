@@ -207,6 +207,25 @@ def test_jacobi_cold_eigh(n):
     assert torch.allclose(w, wr, rtol=1e-4, atol=1e-4 * wr.abs().max().item())
 
 
+@pytest.mark.parametrize("n,sweeps", [(100, 3), (1000, 2), (300, 1)])
+def test_jacobi_fused_apply_solve_is_bit_identical(n, sweeps):
+    """The fused launch (round t's apply + round t+1's solves, cross-workgroup counters)
+    computes exactly the same rotations as separate solve/apply launches."""
+    from evoxmi import config
+    from evoxmi.ops import jacobi
+
+    g = torch.Generator().manual_seed(n)
+    Q, _ = torch.linalg.qr(torch.randn(n, n, generator=g, dtype=torch.float64))
+    lam = 1 + 0.05 * torch.rand(n, generator=g, dtype=torch.float64)
+    X = torch.randn(n, n, generator=g, dtype=torch.float64) * 1e-2
+    C = ((Q * lam) @ Q.T + (X + X.T)).float().cuda()
+    outs = []
+    for fused in (0, 1):
+        with config.override(jacobi_fused=fused):
+            outs.append(jacobi.warm_eigh(C, Q.float().cuda(), max_sweeps=sweeps))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
 def test_jacobi_warm_start_converges_fast():
     from evoxmi.ops import jacobi
 
