@@ -196,8 +196,8 @@ std::vector<at::Tensor> jacobi_sweeps(at::Tensor A, at::Tensor B, const at::Tens
     auto Vbuf = at::empty({npairs * 32 * 32}, opts);
     for (int64_t sw = 0; sw < sweeps; ++sw) {
       for (int64_t t = 0; t < nb; ++t)
-        evx_jacobi_round(A.data_ptr<float>(), B.data_ptr<float>(), (int)np, sp + t * nb, Vbuf.data_ptr<float>(),
-                         flag.data_ptr<int>(), (float)inner_tol, (int)max_inner, t == 0 ? 1 : 0, st);
+        evx_jacobi_round(A.data_ptr<float>(), B.data_ptr<float>(), (int)np, (int)t, Vbuf.data_ptr<float>(),
+                         flag.data_ptr<int>(), (float)inner_tol, (int)max_inner, st);
       evx_jacobi_check(A.data_ptr<float>(), (int)np, part.data_ptr<double>(), flag.data_ptr<int>(), tol2, stats.data_ptr<double>(), st);
     }
     return {A.diagonal().clone(), stats};

@@ -32,10 +32,22 @@ constexpr int LDP = 33;  // padded LDS row (apply kernel tiles)
 constexpr int LDS_S = 49;
 constexpr int LDS_V = 40;
 
-__device__ __forceinline__ int pair_index(const int* __restrict__ sched, int P, int i) {
-  // i in [0, 32): first 16 from block I, next 16 from block J
-  const int blk = sched[2 * P + (i >> 4)];
-  return blk * BS + (i & 15);
+// Block pairing of one outer round.  tab != nullptr: a row of the host schedule table
+// (jacobi.py:_schedule_cpu).  Otherwise the same pairing computed in registers — round 0
+// pairs (2P, 2P+1), round t ≥ 1 is circle-method rotation r = t−1 with block 0 fixed —
+// so the subproblem / tile gathers do not wait behind a dependent schedule load.
+struct RoundMap {
+  const int* tab;
+  int t, nb;
+};
+template <bool TAB>
+__device__ __forceinline__ int round_blk(const RoundMap m, int P, int side) {
+  if (TAB) return m.tab[2 * P + side];
+  if (m.t == 0) return 2 * P + side;
+  const int i = side ? m.nb - 1 - P : P;
+  int x = i + m.t - 2;  // < 2(nb−1) for i, t in [1, nb)
+  if (x >= m.nb - 1) x -= m.nb - 1;
+  return i == 0 ? 0 : x + 1;
 }
 
 // inner circle-method schedule on 32 items: position i in round r
@@ -77,24 +89,34 @@ struct SolveSmem {
 };
 
 template <int MODE>
-__device__ void solve_pair(const float* __restrict__ A, int np, const int* __restrict__ sched, int P, float* __restrict__ Vout,
-                           float tol, int max_inner, SolveSmem& sm) {
+__device__ void solve_pair(const float* __restrict__ A, int np, int blkI, int blkJ, int P, float* __restrict__ Vout,
+                           float tol, int max_inner, SolveSmem& sm, int stop) {
   float (*Sbuf)[PS * LDS_S] = sm.Sbuf;
   float* V = sm.V;
   float* red = sm.red;
   float* S = Sbuf[0];
   const int t = threadIdx.x;
-  const int blkI = sched[2 * P], blkJ = sched[2 * P + 1];
-  for (int e = t; e < PS * PS; e += 256) {
-    int i = e >> 5, j = e & 31;
-    int gi = (i < 16 ? blkI : blkJ) * BS + (i & 15);
-    int gj = (j < 16 ? blkI : blkJ) * BS + (j & 15);
-    S[i * LDS_S + j] = A[(int64_t)gi * np + gj];
+  // fixed trip count (blockDim = 256): the four gathers are issued back to back and share
+  // one memory latency instead of four serial load → wait → ds_write iterations
+  float g[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = t + 256 * u, i = e >> 5, j = e & 31;
+    const int gi = (i < 16 ? blkI : blkJ) * BS + (i & 15);
+    const int gj = (j < 16 ? blkI : blkJ) * BS + (j & 15);
+    g[u] = A[(int64_t)gi * np + gj];
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = t + 256 * u, i = e >> 5, j = e & 31;
+    S[i * LDS_S + j] = g[u];
     V[i * LDS_V + j] = (i == j) ? 1.f : 0.f;
   }
   __syncthreads();
-  for (int e = t; e < PS * PS; e += 256) {
-    int i = e >> 5, j = e & 31;
+  if (stop) return;  // uniform
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = t + 256 * u, i = e >> 5, j = e & 31;
     if (i < j) {
       float v = 0.5f * (S[i * LDS_S + j] + S[j * LDS_S + i]);
       S[i * LDS_S + j] = v;
@@ -108,8 +130,9 @@ __device__ void solve_pair(const float* __restrict__ A, int np, const int* __res
   const int vr0 = 2 * k, vr1 = 2 * k + 1;
   for (int sweep = 0; sweep < max_inner; ++sweep) {
     float off = 0.f, dia = 0.f;
-    for (int e = t; e < PS * PS; e += 256) {
-      int i = e >> 5, j = e & 31;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = t + 256 * u, i = e >> 5, j = e & 31;
       float v = S[i * LDS_S + j];
       if (i == j) dia += v * v; else off += v * v;
     }
@@ -170,17 +193,23 @@ __device__ void solve_pair(const float* __restrict__ A, int np, const int* __res
     }
   }
   float* Vo = Vout + (int64_t)P * PS * PS;
-  for (int e = t; e < PS * PS; e += 256) Vo[e] = V[(e >> 5) * LDS_V + (e & 31)];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = t + 256 * u;
+    Vo[e] = V[(e >> 5) * LDS_V + (e & 31)];
+  }
   __syncthreads();  // LDS reuse by the caller
 }
 
-template <int MODE>
-__global__ void __launch_bounds__(256) jacobi_solve_kernel(const float* __restrict__ A, int np, const int* __restrict__ sched,
+// flag must be non-null; its load overlaps the subproblem gather and the exit is taken after it
+template <int MODE, bool TAB>
+__global__ void __launch_bounds__(256) jacobi_solve_kernel(const float* __restrict__ A, int np, const RoundMap rm,
                                                            float* __restrict__ Vout, const int* __restrict__ flag,
                                                            float tol, int max_inner) {
-  if (flag && *flag) return;
+  const int stop = *flag;
   __shared__ SolveSmem sm;
-  solve_pair<MODE>(A, np, sched, blockIdx.x, Vout, tol, max_inner, sm);
+  const int P = blockIdx.x;
+  solve_pair<MODE>(A, np, round_blk<TAB>(rm, P, 0), round_blk<TAB>(rm, P, 1), P, Vout, tol, max_inner, sm, stop);
 }
 
 // ---------------------------------------------------------------------------------- apply
@@ -190,9 +219,9 @@ typedef __attribute__((address_space(1))) float gf32;
 
 // PUBLISH: the A tile is stored write-through (sc1, agent-scope relaxed atomic stores) so
 // a workgroup on another XCD can read it in the same launch after an acquire
-template <bool PUBLISH>
-__device__ __forceinline__ void apply_tile(float* __restrict__ A, float* __restrict__ B, int np, const int* __restrict__ sched,
-                                           const float* __restrict__ Vp, int tile, float* T0) {
+template <bool PUBLISH, bool TAB>
+__device__ __forceinline__ void apply_tile(float* __restrict__ A, float* __restrict__ B, int np, const RoundMap rm,
+                                           const float* __restrict__ Vp, int tile, float* T0, int stop = 0) {
   const int lane = threadIdx.x & 63;
   const int npairs = np / PS;
   const int nA = npairs * npairs;
@@ -202,10 +231,10 @@ __device__ __forceinline__ void apply_tile(float* __restrict__ A, float* __restr
   else { int tt = tile - nA; row0 = (tt / npairs) * PS; Q = tt % npairs; }
   float* M = isA ? A : B;
   const int h = lane >> 5, c = lane & 31;
-  const int qI = sched[2 * Q], qJ = sched[2 * Q + 1];
+  const int qI = round_blk<TAB>(rm, Q, 0), qJ = round_blk<TAB>(rm, Q, 1);
   const int gj = (c < 16 ? qI : qJ) * BS + (c & 15);
   int pI = 0, pJ = 0;
-  if (isA) { pI = sched[2 * P]; pJ = sched[2 * P + 1]; }
+  if (isA) { pI = round_blk<TAB>(rm, P, 0); pJ = round_blk<TAB>(rm, P, 1); }
   // tile gather: iteration it covers rows 2it, 2it+1 (one per half-wave), 32 columns
   float tv[16];
 #pragma unroll
@@ -223,6 +252,7 @@ __device__ __forceinline__ void apply_tile(float* __restrict__ A, float* __restr
 #pragma unroll
     for (int r = 0; r < 16; ++r) ap[r] = VP[((r & 3) + 8 * (r >> 2) + 4 * h) * PS + c];
   }
+  if (stop) return;  // converged: the flag load overlapped the gathers above
 #pragma unroll
   for (int it = 0; it < 16; ++it) T0[(2 * it + h) * LDP + c] = tv[it];
   __builtin_amdgcn_s_waitcnt(0);
@@ -248,16 +278,17 @@ __device__ __forceinline__ void apply_tile(float* __restrict__ A, float* __restr
   }
 }
 
+template <bool TAB>
 __global__ void __launch_bounds__(256) jacobi_apply_kernel(float* __restrict__ A, float* __restrict__ B, int np,
-                                                           const int* __restrict__ sched, const float* __restrict__ Vp,
+                                                           const RoundMap rm, const float* __restrict__ Vp,
                                                            const int* __restrict__ flag) {
-  if (flag && *flag) return;
+  const int stop = *flag;  // non-null; waited on only after the tile gathers are issued
   __shared__ float T0s[4][PS * LDP];
   const int wv = threadIdx.x >> 6;
   const int npairs = np / PS;
-  const int tile = blockIdx.x * 4 + wv;
+  const int tile = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wv);  // wave-uniform: scalar index math
   if (tile >= 2 * npairs * npairs) return;
-  apply_tile<false>(A, B, np, sched, Vp, tile, T0s[wv]);
+  apply_tile<false, TAB>(A, B, np, rm, Vp, tile, T0s[wv], stop);
 }
 
 // ------------------------------------------------------------------------- fused apply + next solve
@@ -287,7 +318,7 @@ __global__ void __launch_bounds__(256) jacobi_apply_solve_kernel(float* __restri
   const int npairs = np / PS, nb = np / BS;
   const int nA = npairs * npairs;
   const int tile = blockIdx.x * 4 + wv;
-  if (tile < 2 * nA) apply_tile<true>(A, B, np, sched, Vp, tile, T0s[wv]);
+  if (tile < 2 * nA) apply_tile<true, true>(A, B, np, RoundMap{sched, 0, nb}, Vp, tile, T0s[wv]);
   // block → pair maps of this round and the next
   for (int i = threadIdx.x; i < nb; i += blockDim.x) {
     pair_cur[sched[i]] = i >> 1;
@@ -327,8 +358,9 @@ __global__ void __launch_bounds__(256) jacobi_apply_solve_kernel(float* __restri
   }
   __syncthreads();
   for (int i = 0; i < nt; ++i) {
-    if (mode_next) solve_pair<1>(A, np, sched_next, todo[i], Vnext, tol, max_inner, sm);
-    else solve_pair<0>(A, np, sched_next, todo[i], Vnext, tol, max_inner, sm);
+    const int pn = todo[i];
+    if (mode_next) solve_pair<1>(A, np, sched_next[2 * pn], sched_next[2 * pn + 1], pn, Vnext, tol, max_inner, sm, 0);
+    else solve_pair<0>(A, np, sched_next[2 * pn], sched_next[2 * pn + 1], pn, Vnext, tol, max_inner, sm, 0);
   }
 }
 
@@ -338,11 +370,18 @@ __global__ void __launch_bounds__(256) jacobi_offnorm_kernel(const float* __rest
   if (flag && *flag) return;
   __shared__ float scratch[8];
   double off = 0.0, dia = 0.0;
-  const int64_t total = (int64_t)np * np;
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    int i = (int)(e / np), j = (int)(e - (int64_t)i * np);
-    float v = A[e];
-    if (i == j) dia += (double)v * v; else off += (double)v * v;
+  // row-strided (no 64-bit division per element); np % 4 == 0, rows are float4-aligned
+  for (int i = blockIdx.x; i < np; i += gridDim.x) {
+    const float4* row = reinterpret_cast<const float4*>(A + (int64_t)i * np);
+    for (int j4 = threadIdx.x; j4 < (np >> 2); j4 += blockDim.x) {
+      const float4 v = row[j4];
+      const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const double d = (double)e[q] * e[q];
+        if (4 * j4 + q == i) dia += d; else off += d;
+      }
+    }
   }
   off = evx::wave_sum_d(off);
   dia = evx::wave_sum_d(dia);
@@ -376,24 +415,26 @@ __global__ void jacobi_flag_kernel(const double* __restrict__ part, int nparts, 
 
 constexpr int kOffParts = 128;
 
-void evx_jacobi_round(float* A, float* B, int np, const int* sched_t, float* Vbuf, const int* flag, float inner_tol,
-                      int max_inner, int mode, hipStream_t s) {
+void evx_jacobi_round(float* A, float* B, int np, int round, float* Vbuf, const int* flag, float inner_tol, int max_inner,
+                      hipStream_t s) {
   const int npairs = np / PS;
-  if (mode == 0)
-    jacobi_solve_kernel<0><<<npairs, 256, 0, s>>>(A, np, sched_t, Vbuf, flag, inner_tol, max_inner);
+  const RoundMap rm{nullptr, round, np / BS};
+  if (round != 0)
+    jacobi_solve_kernel<0, false><<<npairs, 256, 0, s>>>(A, np, rm, Vbuf, flag, inner_tol, max_inner);
   else
-    jacobi_solve_kernel<1><<<npairs, 256, 0, s>>>(A, np, sched_t, Vbuf, flag, inner_tol, max_inner);
+    jacobi_solve_kernel<1, false><<<npairs, 256, 0, s>>>(A, np, rm, Vbuf, flag, inner_tol, max_inner);
   const int tiles = 2 * npairs * npairs;
-  jacobi_apply_kernel<<<(tiles + 3) / 4, 256, 0, s>>>(A, B, np, sched_t, Vbuf, flag);
+  jacobi_apply_kernel<false><<<(tiles + 3) / 4, 256, 0, s>>>(A, B, np, rm, Vbuf, flag);
 }
 
 void evx_jacobi_solve(const float* A, int np, const int* sched_t, float* Vbuf, const int* flag, float inner_tol, int max_inner,
                       int mode, hipStream_t s) {
   const int npairs = np / PS;
+  const RoundMap rm{sched_t, 0, np / BS};
   if (mode == 0)
-    jacobi_solve_kernel<0><<<npairs, 256, 0, s>>>(A, np, sched_t, Vbuf, flag, inner_tol, max_inner);
+    jacobi_solve_kernel<0, true><<<npairs, 256, 0, s>>>(A, np, rm, Vbuf, flag, inner_tol, max_inner);
   else
-    jacobi_solve_kernel<1><<<npairs, 256, 0, s>>>(A, np, sched_t, Vbuf, flag, inner_tol, max_inner);
+    jacobi_solve_kernel<1, true><<<npairs, 256, 0, s>>>(A, np, rm, Vbuf, flag, inner_tol, max_inner);
 }
 
 void evx_jacobi_apply_solve(float* A, float* B, int np, const int* sched_t, const float* Vcur, const int* flag,
@@ -402,7 +443,7 @@ void evx_jacobi_apply_solve(float* A, float* B, int np, const int* sched_t, cons
   const int npairs = np / PS;
   const int tiles = 2 * npairs * npairs;
   if (sched_next == nullptr) {
-    jacobi_apply_kernel<<<(tiles + 3) / 4, 256, 0, s>>>(A, B, np, sched_t, Vcur, flag);
+    jacobi_apply_kernel<true><<<(tiles + 3) / 4, 256, 0, s>>>(A, B, np, RoundMap{sched_t, 0, np / BS}, Vcur, flag);
     return;
   }
   jacobi_apply_solve_kernel<<<(tiles + 3) / 4, 256, 0, s>>>(A, B, np, sched_t, Vcur, flag, sched_next, mode_next, Vnext, counters,
