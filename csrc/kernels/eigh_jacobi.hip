@@ -96,16 +96,20 @@ __device__ void solve_pair(const float* __restrict__ A, int np, int blkI, int bl
   float* red = sm.red;
   float* S = Sbuf[0];
   const int t = threadIdx.x;
-  // fixed trip count (blockDim = 256): the four gathers are issued back to back and share
-  // one memory latency instead of four serial load → wait → ds_write iterations
-  float g[4];
+  // fixed trip count (blockDim = 256): the eight gathers (S[i][j] and its mirror, symmetrised
+  // in registers — a + b is commutative, so both halves get the same value) are issued back
+  // to back and share one memory latency; no separate LDS symmetrisation pass
+  float g[4], gt[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int e = t + 256 * u, i = e >> 5, j = e & 31;
     const int gi = (i < 16 ? blkI : blkJ) * BS + (i & 15);
     const int gj = (j < 16 ? blkI : blkJ) * BS + (j & 15);
     g[u] = A[(int64_t)gi * np + gj];
+    gt[u] = A[(int64_t)gj * np + gi];
   }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) g[u] = 0.5f * (g[u] + gt[u]);
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int e = t + 256 * u, i = e >> 5, j = e & 31;
@@ -114,36 +118,31 @@ __device__ void solve_pair(const float* __restrict__ A, int np, int blkI, int bl
   }
   __syncthreads();
   if (stop) return;  // uniform
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int e = t + 256 * u, i = e >> 5, j = e & 31;
-    if (i < j) {
-      float v = 0.5f * (S[i * LDS_S + j] + S[j * LDS_S + i]);
-      S[i * LDS_S + j] = v;
-      S[j * LDS_S + i] = v;
-    }
-  }
-  __syncthreads();
   const int k = t >> 4, l = t & 15;
   const int row = k & 3;                                     // 16-lane row of this thread
   const int w4 = __builtin_amdgcn_readfirstlane((t >> 6) << 2);  // first k of this wave
   const int vr0 = 2 * k, vr1 = 2 * k + 1;
   for (int sweep = 0; sweep < max_inner; ++sweep) {
-    float off = 0.f, dia = 0.f;
+    // the first inner sweep always runs (on a converged subproblem its rotations are
+    // ≈ identity); the convergence test (a block reduction + two barriers) only gates
+    // the further sweeps
+    if (sweep > 0) {
+      float off = 0.f, dia = 0.f;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = t + 256 * u, i = e >> 5, j = e & 31;
-      float v = S[i * LDS_S + j];
-      if (i == j) dia += v * v; else off += v * v;
+      for (int u = 0; u < 4; ++u) {
+        const int e = t + 256 * u, i = e >> 5, j = e & 31;
+        float v = S[i * LDS_S + j];
+        if (i == j) dia += v * v; else off += v * v;
+      }
+      off = evx::wave_sum(off);
+      dia = evx::wave_sum(dia);
+      if ((t & 63) == 0) { red[t >> 6] = off; red[4 + (t >> 6)] = dia; }
+      __syncthreads();
+      off = red[0] + red[1] + red[2] + red[3];
+      dia = red[4] + red[5] + red[6] + red[7];
+      __syncthreads();
+      if (off <= tol * tol * dia || off == 0.f) break;
     }
-    off = evx::wave_sum(off);
-    dia = evx::wave_sum(dia);
-    if ((t & 63) == 0) { red[t >> 6] = off; red[4 + (t >> 6)] = dia; }
-    __syncthreads();
-    off = red[0] + red[1] + red[2] + red[3];
-    dia = red[4] + red[5] + red[6] + red[7];
-    __syncthreads();
-    if (off <= tol * tol * dia || off == 0.f) break;
     constexpr int ROUNDS = MODE == 0 ? 16 : 15;
     for (int r = 0; r < ROUNDS; ++r) {
       int pk, qk, pl, ql;
