@@ -64,17 +64,15 @@ __device__ __forceinline__ void rot_params(float app, float aqq, float apq, floa
   }
 }
 
-__device__ __forceinline__ float rl(float v, int l) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-}
-__device__ __forceinline__ float row_pick(int row, float a, float b, float c, float d) {
-  return row < 2 ? (row == 0 ? a : b) : (row == 2 ? c : d);
+// DPP row_newbcast:0 — lane 0 of each 16-lane row to the whole row (one VALU op)
+__device__ __forceinline__ float row_bcast0(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150, 0xf, 0xf, false));
 }
 
 // 256 threads per 32×32 subproblem: thread t owns the 2×2 block (row pair k = t>>4,
-// col pair l = t&15) of S and the V items (rows 2k, 2k+1 × col pair l).  Each thread
-// computes ONE rotation (its column pair l) from S; the row-pair rotation k is taken
-// from lane (k, k) of the same wave with one v_readlane per 16-lane row.  Per inner round: one
+// col pair l = (t + k) & 15) of S and the V items (rows 2k, 2k+1 × col pair l).  Each thread
+// computes ONE rotation (its column pair l) from S; the row-pair rotation k is computed by
+// lane 0 of the thread's 16-lane row (l = k there) and broadcast with DPP.  Per inner round: one
 // LDS read phase, barrier, one LDS write phase, barrier.
 // MODE 0 ("cross"): 16 inner rounds pairing I[x] with J[(x + r) mod 16] — only the
 //   coupling block A_IJ is annihilated; within-block pairs are handled by MODE 1.
@@ -118,9 +116,10 @@ __device__ void solve_pair(const float* __restrict__ A, int np, int blkI, int bl
   }
   __syncthreads();
   if (stop) return;  // uniform
-  const int k = t >> 4, l = t & 15;
-  const int row = k & 3;                                     // 16-lane row of this thread
-  const int w4 = __builtin_amdgcn_readfirstlane((t >> 6) << 2);  // first k of this wave
+  // column pairs are skewed by the row pair, l = (lane-in-row + k) mod 16, so lane 0 of
+  // every 16-lane row owns l = k: the row-pair rotation it computes is broadcast to its
+  // row with one DPP op (was: 4 v_readlane + select per value)
+  const int k = t >> 4, l = (t + k) & 15;
   const int vr0 = 2 * k, vr1 = 2 * k + 1;
   for (int sweep = 0; sweep < max_inner; ++sweep) {
     // the first inner sweep always runs (on a converged subproblem its rotations are
@@ -162,17 +161,18 @@ __device__ void solve_pair(const float* __restrict__ A, int np, int blkI, int bl
       float x00 = S[pk * LDS_S + pl], x01 = S[pk * LDS_S + ql], x10 = S[qk * LDS_S + pl], x11 = S[qk * LDS_S + ql];
       float v0a = V[vr0 * LDS_V + pl], v0b = V[vr0 * LDS_V + ql];
       float v1a = V[vr1 * LDS_V + pl], v1b = V[vr1 * LDS_V + ql];
-      float cl = 1.f, sl = 0.f;
-      if (alo != 0.f) {
-        float tau = (alq - alp) * __builtin_amdgcn_rcpf(2.f * alo);
-        float tt = copysignf(1.f, tau) * __builtin_amdgcn_rcpf(fabsf(tau) + __builtin_sqrtf(fmaf(tau, tau, 1.f)));
-        cl = __builtin_amdgcn_rsqf(fmaf(tt, tt, 1.f));
-        sl = tt * cl;
-      }
-      // row-pair rotation from lane (k, k): one v_readlane per 16-lane row (k = 4·wave + row)
-      // instead of a ds_bpermute round trip on the round's critical path
-      const float ck = row_pick(row, rl(cl, w4), rl(cl, 17 + w4), rl(cl, 34 + w4), rl(cl, 51 + w4));
-      const float sk = row_pick(row, rl(sl, w4), rl(sl, 17 + w4), rl(sl, 34 + w4), rl(sl, 51 + w4));
+      // branch-free (a divergent `if (alo != 0)` let the compiler sink the alp/alq reads
+      // into the branch: a second LDS round trip on every inner round's critical path) and
+      // with the hardware v_sqrt_f32 (1 ulp; the IEEE sqrtf expands to ≈20 dependent
+      // instructions).  alo = 0 gives inf/NaN in tau, replaced by the identity below.
+      const float tau = (alq - alp) * __builtin_amdgcn_rcpf(2.f * alo);
+      const float tt = copysignf(1.f, tau) * __builtin_amdgcn_rcpf(fabsf(tau) + __builtin_amdgcn_sqrtf(fmaf(tau, tau, 1.f)));
+      const float cr = __builtin_amdgcn_rsqf(fmaf(tt, tt, 1.f));
+      const bool rot = alo != 0.f;
+      const float cl = rot ? cr : 1.f, sl = rot ? tt * cr : 0.f;
+      // row-pair rotation from lane (k, l = k) = lane 0 of this 16-lane row
+      const float ck = row_bcast0(cl);
+      const float sk = row_bcast0(sl);
       float y00 = ck * x00 - sk * x10, y01 = ck * x01 - sk * x11;
       float y10 = sk * x00 + ck * x10, y11 = sk * x01 + ck * x11;
       float o00 = y00 * cl - y01 * sl, o01 = y00 * sl + y01 * cl;
