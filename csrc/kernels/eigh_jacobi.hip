@@ -87,7 +87,7 @@ struct SolveSmem {
 };
 
 template <int MODE>
-__device__ void solve_pair(const float* __restrict__ A, int np, int blkI, int blkJ, int P, float* __restrict__ Vout,
+__device__ __forceinline__ void solve_pair(const float* __restrict__ A, int np, int blkI, int blkJ, int P, float* __restrict__ Vout,
                            float tol, int max_inner, SolveSmem& sm, int stop) {
   float (*Sbuf)[PS * LDS_S] = sm.Sbuf;
   float* V = sm.V;
@@ -143,6 +143,7 @@ __device__ void solve_pair(const float* __restrict__ A, int np, int blkI, int bl
       if (off <= tol * tol * dia || off == 0.f) break;
     }
     constexpr int ROUNDS = MODE == 0 ? 16 : 15;
+#pragma unroll
     for (int r = 0; r < ROUNDS; ++r) {
       int pk, qk, pl, ql;
       if (MODE == 0) {
