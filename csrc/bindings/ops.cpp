@@ -192,6 +192,15 @@ std::vector<at::Tensor> jacobi_sweeps(at::Tensor A, at::Tensor B, const at::Tens
   const double tol2 = tol * tol;
   evx_jacobi_check(A.data_ptr<float>(), (int)np, part.data_ptr<double>(), flag.data_ptr<int>(), tol2, stats.data_ptr<double>(), st);
   const int* sp = sched.data_ptr<int>();
+  if (fused == 2) {  // default: B update overlapped with the next round's solves
+    auto Vbuf = at::empty({2, npairs * 32 * 32}, opts);
+    for (int64_t sw = 0; sw < sweeps; ++sw) {
+      evx_jacobi_sweep_overlapB(A.data_ptr<float>(), B.data_ptr<float>(), (int)np, Vbuf[0].data_ptr<float>(),
+                                Vbuf[1].data_ptr<float>(), flag.data_ptr<int>(), (float)inner_tol, (int)max_inner, st);
+      evx_jacobi_check(A.data_ptr<float>(), (int)np, part.data_ptr<double>(), flag.data_ptr<int>(), tol2, stats.data_ptr<double>(), st);
+    }
+    return {A.diagonal().clone(), stats};
+  }
   if (!fused) {
     auto Vbuf = at::empty({npairs * 32 * 32}, opts);
     for (int64_t sw = 0; sw < sweeps; ++sw) {
@@ -528,7 +537,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("philox_fill(Tensor key, int n, int dist, int offset) -> Tensor");
   m.def("argsort_f32(Tensor keys, int descending) -> Tensor[]");
   m.def("cec_basic(Tensor Z, int fid, Tensor? perm, int start, int L, Tensor? sub, float scale, Tensor? Y, int ystart, int yperm) -> Tensor");
-  m.def("jacobi_sweeps(Tensor A, Tensor B, Tensor sched, int sweeps, float tol, float inner_tol, int max_inner, int fused=0) -> Tensor[]");
+  m.def("jacobi_sweeps(Tensor A, Tensor B, Tensor sched, int sweeps, float tol, float inner_tol, int max_inner, int fused=2) -> Tensor[]");
   m.def("philox_words(Tensor key, int nblocks, int domain, int offset) -> Tensor");
   m.def("weighted_rowsum(Tensor X, Tensor? idx, Tensor w, Tensor? sub, int K) -> Tensor");
   m.def("gemm_set_config(int cfg) -> ()");

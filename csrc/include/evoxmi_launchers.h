@@ -33,6 +33,10 @@ void evx_cec_basic(const float* Z, int64_t ld, int N, int fid, const int32_t* pe
 // pairing is computed in-kernel and equals jacobi.py:_schedule_cpu row `round`)
 void evx_jacobi_round(float* A, float* B, int np, int round, float* Vbuf, const int* flag, float inner_tol, int max_inner,
                       hipStream_t s);
+// one sweep (nb rounds) with round t−1's B update inside round t's solve launch (V0/V1:
+// npairs·32·32 floats each, alternated by round parity); all of B is updated on return
+void evx_jacobi_sweep_overlapB(float* A, float* B, int np, float* V0, float* V1, const int* flag, float inner_tol,
+                               int max_inner, hipStream_t s);
 void evx_jacobi_solve(const float* A, int np, const int* sched_t, float* Vbuf, const int* flag, float inner_tol, int max_inner,
                       int mode, hipStream_t s);
 // round t's apply; with sched_next != nullptr the same launch also solves round t+1's

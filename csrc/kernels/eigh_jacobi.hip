@@ -281,14 +281,45 @@ __device__ __forceinline__ void apply_tile(float* __restrict__ A, float* __restr
 template <bool TAB>
 __global__ void __launch_bounds__(256) jacobi_apply_kernel(float* __restrict__ A, float* __restrict__ B, int np,
                                                            const RoundMap rm, const float* __restrict__ Vp,
-                                                           const int* __restrict__ flag) {
+                                                           const int* __restrict__ flag, int tile0, int tile_end) {
   const int stop = *flag;  // non-null; waited on only after the tile gathers are issued
   __shared__ float T0s[4][PS * LDP];
   const int wv = threadIdx.x >> 6;
-  const int npairs = np / PS;
-  const int tile = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wv);  // wave-uniform: scalar index math
-  if (tile >= 2 * npairs * npairs) return;
+  const int tile = __builtin_amdgcn_readfirstlane(tile0 + blockIdx.x * 4 + wv);  // wave-uniform: scalar index math
+  if (tile >= tile_end) return;
   apply_tile<false, TAB>(A, B, np, rm, Vp, tile, T0s[wv], stop);
+}
+
+// ------------------------------------------------------------------------- solve ‖ B update
+// Round t's subproblem solves on workgroups [0, npairs) and, in the same launch, the
+// eigenbasis update B ← B·J_{t−1} of the previous round on the workgroups behind them.
+// The solve occupies only npairs CUs and is the critical path (latency-bound); B is
+// read by nothing but these updates, so its 32-row tiles fill the otherwise idle CUs
+// and leave the separate apply launch with the A tiles only.  V is double-buffered
+// by round parity.  Workgroups dispatch in blockIdx order, so the solves start first.
+union SolveApplySmem {
+  SolveSmem s;
+  float T0s[4][PS * LDP];
+};
+
+template <int MODE>
+__global__ void __launch_bounds__(256) jacobi_solve_applyB_kernel(float* __restrict__ A, float* __restrict__ B, int np,
+                                                                  const RoundMap rm, float* __restrict__ Vout,
+                                                                  const RoundMap rm_prev, const float* __restrict__ Vprev,
+                                                                  const int* __restrict__ flag, float tol, int max_inner) {
+  const int stop = *flag;
+  __shared__ SolveApplySmem sm;
+  const int npairs = np / PS;
+  if ((int)blockIdx.x < npairs) {
+    const int P = blockIdx.x;
+    solve_pair<MODE>(A, np, round_blk<false>(rm, P, 0), round_blk<false>(rm, P, 1), P, Vout, tol, max_inner, sm.s, stop);
+    return;
+  }
+  const int wv = threadIdx.x >> 6;
+  const int nA = npairs * npairs;
+  const int tile = __builtin_amdgcn_readfirstlane(nA + ((int)blockIdx.x - npairs) * 4 + wv);
+  if (tile >= 2 * nA) return;
+  apply_tile<false, false>(A, B, np, rm_prev, Vprev, tile, sm.T0s[wv], stop);
 }
 
 // ------------------------------------------------------------------------- fused apply + next solve
@@ -424,7 +455,27 @@ void evx_jacobi_round(float* A, float* B, int np, int round, float* Vbuf, const 
   else
     jacobi_solve_kernel<1, false><<<npairs, 256, 0, s>>>(A, np, rm, Vbuf, flag, inner_tol, max_inner);
   const int tiles = 2 * npairs * npairs;
-  jacobi_apply_kernel<false><<<(tiles + 3) / 4, 256, 0, s>>>(A, B, np, rm, Vbuf, flag);
+  jacobi_apply_kernel<false><<<(tiles + 3) / 4, 256, 0, s>>>(A, B, np, rm, Vbuf, flag, 0, tiles);
+}
+
+void evx_jacobi_sweep_overlapB(float* A, float* B, int np, float* V0, float* V1, const int* flag, float inner_tol,
+                               int max_inner, hipStream_t s) {
+  const int npairs = np / PS, nb = np / BS, nA = npairs * npairs;
+  float* V[2] = {V0, V1};
+  const int gridB = (nA + 3) / 4;
+  for (int t = 0; t < nb; ++t) {
+    const RoundMap rm{nullptr, t, nb};
+    if (t == 0) {
+      jacobi_solve_kernel<1, false><<<npairs, 256, 0, s>>>(A, np, rm, V[0], flag, inner_tol, max_inner);
+    } else {
+      const RoundMap rp{nullptr, t - 1, nb};
+      jacobi_solve_applyB_kernel<0><<<npairs + gridB, 256, 0, s>>>(A, B, np, rm, V[t & 1], rp, V[(t - 1) & 1], flag,
+                                                                   inner_tol, max_inner);
+    }
+    jacobi_apply_kernel<false><<<gridB, 256, 0, s>>>(A, B, np, rm, V[t & 1], flag, 0, nA);
+  }
+  // the last round's B update, before the convergence check can set the flag
+  jacobi_apply_kernel<false><<<gridB, 256, 0, s>>>(A, B, np, RoundMap{nullptr, nb - 1, nb}, V[(nb - 1) & 1], flag, nA, 2 * nA);
 }
 
 void evx_jacobi_solve(const float* A, int np, const int* sched_t, float* Vbuf, const int* flag, float inner_tol, int max_inner,
@@ -443,7 +494,7 @@ void evx_jacobi_apply_solve(float* A, float* B, int np, const int* sched_t, cons
   const int npairs = np / PS;
   const int tiles = 2 * npairs * npairs;
   if (sched_next == nullptr) {
-    jacobi_apply_kernel<true><<<(tiles + 3) / 4, 256, 0, s>>>(A, B, np, RoundMap{sched_t, 0, np / BS}, Vcur, flag);
+    jacobi_apply_kernel<true><<<(tiles + 3) / 4, 256, 0, s>>>(A, B, np, RoundMap{sched_t, 0, np / BS}, Vcur, flag, 0, tiles);
     return;
   }
   jacobi_apply_solve_kernel<<<(tiles + 3) / 4, 256, 0, s>>>(A, B, np, sched_t, Vcur, flag, sched_next, mode_next, Vnext, counters,

@@ -43,7 +43,7 @@ KNOBS: Dict[str, Knob] = {
     "jacobi_tol_factor": Knob("EVOXMI_JACOBI_TOL_FACTOR", 4.0, float, "convergence: ‖offdiag‖ ≤ factor·eps_f32·sqrt(n)·‖diag‖"),
     "jacobi_inner_tol": Knob("EVOXMI_JACOBI_INNER_TOL", 1e-6, float, "per-subproblem skip threshold of the Jacobi solve kernel"),
     "jacobi_reortho": Knob("EVOXMI_JACOBI_REORTHO", 1, int, "Newton–Schulz re-orthonormalisation of the warm-start basis before each decomposition"),
-    "jacobi_fused": Knob("EVOXMI_JACOBI_FUSED", 0, int, "experimental: solve round t+1's Jacobi subproblems inside round t's apply launch (slower, see profiles/NOTES.md)"),
+    "jacobi_fused": Knob("EVOXMI_JACOBI_FUSED", 2, int, "Jacobi round pipeline: 2 = B update of round t-1 inside round t's solve launch; 0 = split solve/apply launches; 1 = experimental fused apply + next solve (slower, see profiles/NOTES.md)"),
     "jacobi_inner": Knob("EVOXMI_JACOBI_INNER", 1, int, "inner sweeps per 32×32 Jacobi subproblem"),
     "debug": Knob("EVOXMI_DEBUG", False, _bool, "synchronous kernel error-flag checks after fused kernels (not while capturing)"),
     "trace": Knob("EVOXMI_TRACE", False, _bool, "emit roctx ranges around ask / evaluate / tell in eager workflow steps"),

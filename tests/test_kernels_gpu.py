@@ -220,10 +220,11 @@ def test_jacobi_fused_apply_solve_is_bit_identical(n, sweeps):
     X = torch.randn(n, n, generator=g, dtype=torch.float64) * 1e-2
     C = ((Q * lam) @ Q.T + (X + X.T)).float().cuda()
     outs = []
-    for fused in (0, 1):
+    for fused in (0, 1, 2):  # split launches / fused apply+solve / B update inside the next solve launch
         with config.override(jacobi_fused=fused):
             outs.append(jacobi.warm_eigh(C, Q.float().cuda(), max_sweeps=sweeps))
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    for o in outs[1:]:
+        assert torch.equal(outs[0][0], o[0]) and torch.equal(outs[0][1], o[1])
 
 
 def test_jacobi_warm_start_converges_fast():
