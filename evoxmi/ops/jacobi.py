@@ -38,6 +38,20 @@ def _schedule_cpu(nb: int) -> torch.Tensor:
     return torch.tensor(rounds, dtype=torch.int32)
 
 
+def round_pairing(t: int, nb: int) -> list:
+    """Row ``t`` of :func:`_schedule_cpu` in closed form — the formula the HIP kernels
+    evaluate in registers (``round_blk`` in csrc/kernels/eigh_jacobi.hip) instead of
+    loading the table: round 0 pairs (2P, 2P+1); round t ≥ 1 pairs (L[P], L[nb−1−P]) with
+    L[0] = 0 and L[i] = ((i − 2 + t) mod (nb − 1)) + 1."""
+    def blk(P, side):
+        if t == 0:
+            return 2 * P + side
+        i = nb - 1 - P if side else P
+        return 0 if i == 0 else (i - 2 + t) % (nb - 1) + 1
+
+    return [blk(P, side) for P in range(nb // 2) for side in (0, 1)]
+
+
 _DEV_SCHED = {}
 
 
