@@ -37,6 +37,7 @@ def main():
     args = ap.parse_args()
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from evoxmi import config
     from evoxmi import random as rnd
     from evoxmi.algorithms import CMAES
     from evoxmi.parallel import init_distributed
@@ -65,9 +66,12 @@ def main():
         if dist_on:
             dist.barrier()
 
+    from evoxmi.ops import eigh as eigh_mod
+
     for _ in range(args.warmup):
         state = wf.step(state)
     sync()
+    eigh_mod.HISTORY.clear()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         state = wf.step(state)
@@ -103,9 +107,20 @@ def main():
                 "pop_size": args.pop,
                 "dim": args.dim,
                 "hipgraph": use_graph,
-                "eigh": os.environ.get("EVOXMI_EIGH", "jacobi"),
+                "eigh": config.get("eigh"),
             },
         }
+        hist = list(eigh_mod.HISTORY)
+        if hist:
+            # every timed generation's decomposition: relative off-norm ‖offdiag(BᵀCB)‖/‖diag‖
+            out["eigh_stats"] = {
+                "generations": len(hist),
+                "max_off_rel": max(h.off_rel for h in hist),
+                "tol": config.get("eigh_tol"),
+                "mean_jacobi_sweeps": sum(h.jacobi_sweeps for h in hist) / len(hist),
+                "mean_refine_iters": sum(h.refine_iters for h in hist) / len(hist),
+                "fallbacks": sum(h.fallback for h in hist),
+            }
         print(json.dumps(out), flush=True)
     if dist_on:
         dist.destroy_process_group()

@@ -232,6 +232,94 @@ std::vector<at::Tensor> jacobi_sweeps(at::Tensor A, at::Tensor B, const at::Tens
   return {A.diagonal().clone(), stats};
 }
 
+
+// ---------------------------------------------------------------- sorted-block refinement (eigh_sbr.hip)
+// A / B may be row-major views with a leading dimension (e.g. the n×n corner of a padded operand).
+void check_rowmajor(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.dim() == 2 && t.stride(1) == 1 && t.stride(0) >= t.size(1),
+              name, " must be a row-major float32 device matrix");
+}
+
+at::Tensor sbr_stats(const at::Tensor& A) {
+  check_rowmajor(A, "A");
+  TORCH_CHECK(A.size(0) == A.size(1), "A must be square");
+  c10::DeviceGuard g(A.device());
+  auto o = A.options().dtype(at::kDouble);
+  auto part = at::empty({4 * evx_sbr_stat_parts()}, o);
+  auto out = at::empty({4}, o);
+  evx_sbr_stats(A.data_ptr<float>(), (int)A.size(0), A.stride(0), part.data_ptr<double>(), out.data_ptr<double>(), cur_stream());
+  return out;
+}
+
+std::vector<at::Tensor> sbr_block(const at::Tensor& A, int64_t off, int64_t sweeps, const c10::optional<at::Tensor>& dbg) {
+  check_rowmajor(A, "A");
+  const int64_t n = A.size(0);
+  TORCH_CHECK(A.size(1) == n && n >= 2 && n <= 2048, "sbr_block: square A with 2 <= n <= 2048");
+  TORCH_CHECK(off == 0 || off == 32, "sbr_block: block offset must be 0 or 32");
+  c10::DeviceGuard g(A.device());
+  const int nb = evx_sbr_nblocks((int)n, (int)off);
+  auto perm = at::empty({n}, A.options().dtype(at::kInt));
+  auto Q = at::empty({nb, 64, 64}, A.options());
+  auto dq = at::empty({n}, A.options());
+  evx_sbr_block(A.data_ptr<float>(), (int)n, A.stride(0), (int)off, (int)sweeps, perm.data_ptr<int>(), Q.data_ptr<float>(),
+                dq.data_ptr<float>(), cur_stream(), dbg ? (long long*)dbg->data_ptr<int64_t>() : nullptr);
+  return {perm, Q, dq};
+}
+
+at::Tensor sbr_far(const at::Tensor& A, int64_t off, const at::Tensor& perm, const at::Tensor& Q, const at::Tensor& dq,
+                   const at::Tensor& stats, double thr_fac) {
+  check_rowmajor(A, "A");
+  const int64_t n = A.size(0);
+  const int nb = evx_sbr_nblocks((int)n, (int)off);
+  TORCH_CHECK(perm.is_cuda() && perm.scalar_type() == at::kInt && perm.numel() == n && perm.is_contiguous(), "perm int32[n]");
+  TORCH_CHECK(Q.is_cuda() && Q.scalar_type() == at::kFloat && Q.is_contiguous() && Q.numel() == (int64_t)nb * 4096, "Q [nb,64,64]");
+  TORCH_CHECK(dq.is_cuda() && dq.scalar_type() == at::kFloat && dq.numel() == n && dq.is_contiguous(), "dq float[n]");
+  TORCH_CHECK(stats.is_cuda() && stats.scalar_type() == at::kDouble && stats.numel() == 4, "stats double[4]");
+  c10::DeviceGuard g(A.device());
+  auto X = at::empty({n, n}, A.options());
+  evx_sbr_far(A.data_ptr<float>(), (int)n, A.stride(0), (int)off, perm.data_ptr<int>(), Q.data_ptr<float>(), dq.data_ptr<float>(),
+              stats.data_ptr<double>(), (float)thr_fac, X.data_ptr<float>(), n, cur_stream());
+  return X;
+}
+
+at::Tensor sbr_bq(const at::Tensor& B, int64_t off, const at::Tensor& perm, const at::Tensor& Q) {
+  check_rowmajor(B, "B");
+  const int64_t rows = B.size(0), n = B.size(1);
+  const int nb = evx_sbr_nblocks((int)n, (int)off);
+  TORCH_CHECK(perm.is_cuda() && perm.scalar_type() == at::kInt && perm.numel() == n && perm.is_contiguous(), "perm int32[n]");
+  TORCH_CHECK(Q.is_cuda() && Q.scalar_type() == at::kFloat && Q.is_contiguous() && Q.numel() == (int64_t)nb * 4096, "Q [nb,64,64]");
+  c10::DeviceGuard g(B.device());
+  auto Bq = at::empty({rows, n}, B.options());
+  evx_sbr_bq(B.data_ptr<float>(), (int)rows, (int)n, B.stride(0), (int)off, perm.data_ptr<int>(), Q.data_ptr<float>(),
+             Bq.data_ptr<float>(), n, cur_stream());
+  return Bq;
+}
+
+
+// A = (T + Tᵀ)/2 plus [off², diag², dmin, dmax] of A
+std::vector<at::Tensor> sbr_symstats(const at::Tensor& T) {
+  check_rowmajor(T, "T");
+  const int64_t n = T.size(0);
+  TORCH_CHECK(T.size(1) == n, "T must be square");
+  c10::DeviceGuard g(T.device());
+  auto A = at::empty({n, n}, T.options());
+  auto o = T.options().dtype(at::kDouble);
+  auto part = at::empty({4 * (int64_t)evx_sbr_symstats_parts((int)n)}, o);
+  auto out = at::empty({4}, o);
+  evx_sbr_symstats(T.data_ptr<float>(), (int)n, T.stride(0), A.data_ptr<float>(), n, part.data_ptr<double>(), out.data_ptr<double>(), cur_stream());
+  return {A, out};
+}
+
+std::vector<at::Tensor> sbr_taylor_prep(const at::Tensor& X, const at::Tensor& X2, const at::Tensor& X3) {
+  for (auto* t : {&X, &X2, &X3}) { CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t); }
+  const int64_t n = X.size(0);
+  TORCH_CHECK(X.dim() == 2 && X.size(1) == n && X2.sizes() == X.sizes() && X3.sizes() == X.sizes(), "sbr_taylor_prep: n×n");
+  c10::DeviceGuard g(X.device());
+  auto P = at::empty_like(X), M = at::empty_like(X);
+  evx_sbr_taylor_prep(X.data_ptr<float>(), X2.data_ptr<float>(), X3.data_ptr<float>(), (int)n, P.data_ptr<float>(), M.data_ptr<float>(), cur_stream());
+  return {P, M};
+}
+
 at::Tensor philox_words(const at::Tensor& key, int64_t nblocks, int64_t domain, int64_t offset) {
   check_key(key);
   c10::DeviceGuard g(key.device());
@@ -561,6 +649,12 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("moead_variation(Tensor pop, Tensor p0, Tensor p1, Tensor kx, Tensor km, Tensor lb, Tensor ub, float pro_c, float dis_c, float pro_m, float dis_m, int nm) -> Tensor");
   m.def("moead_replace(Tensor pop_obj, Tensor off_obj, Tensor W, Tensor z, Tensor zmax, Tensor rowptr, Tensor owner, int func) -> Tensor[]");
   m.def("moead_select_rows(Tensor pop, Tensor off, Tensor win) -> Tensor");
+  m.def("sbr_stats(Tensor A) -> Tensor");
+  m.def("sbr_block(Tensor A, int off, int sweeps, Tensor? dbg=None) -> Tensor[]");
+  m.def("sbr_far(Tensor A, int off, Tensor perm, Tensor Q, Tensor dq, Tensor stats, float thr_fac) -> Tensor");
+  m.def("sbr_bq(Tensor B, int off, Tensor perm, Tensor Q) -> Tensor");
+  m.def("sbr_symstats(Tensor T) -> Tensor[]");
+  m.def("sbr_taylor_prep(Tensor X, Tensor X2, Tensor X3) -> Tensor[]");
   m.def("pso_update(Tensor pop, Tensor vel, Tensor lbl, Tensor lbf, Tensor fit, Tensor gbl, Tensor kp, Tensor kg, float w, float phip, float phig, Tensor lb, Tensor ub) -> Tensor[]");
 }
 
@@ -596,4 +690,10 @@ TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
   m.impl("moead_variation", &moead_variation);
   m.impl("moead_replace", &moead_replace);
   m.impl("moead_select_rows", &moead_select_rows);
+  m.impl("sbr_stats", &sbr_stats);
+  m.impl("sbr_block", &sbr_block);
+  m.impl("sbr_far", &sbr_far);
+  m.impl("sbr_bq", &sbr_bq);
+  m.impl("sbr_symstats", &sbr_symstats);
+  m.impl("sbr_taylor_prep", &sbr_taylor_prep);
 }

@@ -87,3 +87,16 @@ void evx_cma_eig_out(const float* Bp, const float* w, int d, int np, float* B, f
 
 // nsga_select.hip
 void evx_nsga_select(const int32_t* rank, const float* f, int n, int m, int N, int mask_pos, int64_t* keep, hipStream_t s);
+// sorted-block refinement of a warm-started eigendecomposition (eigh_sbr.hip, evoxmi/ops/sbr.py)
+int evx_sbr_nblocks(int n, int off);
+int evx_sbr_stat_parts();
+void evx_sbr_stats(const float* A, int n, int64_t lda, double* part, double* out, hipStream_t s);
+void evx_sbr_block(const float* A, int n, int64_t lda, int off, int sweeps, int* perm, float* Q, float* dq, hipStream_t s,
+                   long long* dbg = nullptr);
+void evx_sbr_far(const float* A, int n, int64_t lda, int off, const int* perm, const float* Q, const float* dq,
+                 const double* stats, float thr_fac, float* X, int64_t ldx, hipStream_t s);
+void evx_sbr_bq(const float* B, int rows, int n, int64_t ldb, int off, const int* perm, const float* Q, float* Bq, int64_t ldq,
+                hipStream_t s);
+int evx_sbr_symstats_parts(int n);
+void evx_sbr_symstats(const float* T, int n, int64_t ldt, float* A, int64_t lda, double* part, double* out, hipStream_t s);
+void evx_sbr_taylor_prep(const float* X, const float* X2, const float* X3, int n, float* P, float* M, hipStream_t s);

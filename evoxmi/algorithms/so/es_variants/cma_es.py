@@ -33,7 +33,8 @@ import torch
 
 from ....core import Algorithm, State
 from ....ops import random as rnd
-from ....ops.eigh import symmetrize_upper, warm_eigh
+from ....ops.eigh import sbr_phase, symmetrize_upper, warm_eigh
+from ....runtime import host_phase
 from .... import config
 from ....ops.linalg import Operand, gemm, plain_nt
 from ....ops.reduce import weighted_rowsum
@@ -103,6 +104,8 @@ class CMAES(Algorithm):
             sigma=torch.tensor(self.init_stdev, dtype=torch.float32, device=dev),
             key=key.to(dev),
             population=torch.zeros((self.pop_size, d), device=dev),
+            # last decomposition: [relative off-norm, Jacobi sweeps, refinement iterations, fallback]
+            eig_stats=torch.zeros(4, dtype=torch.float64, device=dev),
         )
 
     # ------------------------------------------------------------------ sampling
@@ -155,7 +158,7 @@ class CMAES(Algorithm):
 
     def _fused_epilogue_ok(self, state):
         return (state.C.is_cuda and self.decomp_per_iter == 1 and config.get("cma_fused")
-                and config.get("eigh") == "jacobi" and state.count_iter.dtype == torch.int64)
+                and config.get("eigh") in ("jacobi", "sbr") and state.count_iter.dtype == torch.int64)
 
     def _finish_tell_fused(self, state, dm, S):
         """Same update as ``_finish_tell`` in four fused kernels around the eigensolver
@@ -170,13 +173,23 @@ class CMAES(Algorithm):
                   self.chiN, self.damps, self.c1, self.cmu, (1.4 + 2 / (d + 1)) * self.chiN]
         ps, pc, sigma, a, _hsig = ops.cma_paths(state.ps.contiguous(), state.pc.contiguous(), y, delta, state.sigma.reshape(1).contiguous(),
                                                 state.count_iter.reshape(1).contiguous(), consts)
-        np_ = jacobi.padded_size(d)
-        C, Cp, Bp = ops.cma_cov_pad(state.C.contiguous(), S.contiguous(), pc, a, float(self.c1), float(self.cmu), state.B.contiguous(), np_)
-        w, Bp = jacobi.warm_eigh_padded(Cp, Bp, d, max_sweeps=self.eig_sweeps)
-        B, D, BdivD = ops.cma_eig_out(Bp, w, d)
+        eig_stats = state.eig_stats
+        if config.get("eigh") == "sbr":
+            # converged solve (Jacobi hand-off + sorted-block refinement), host-orchestrated:
+            # a host phase between hipGraph segments under StdWorkflow(graph=True)
+            np_ = jacobi.padded_size(d)
+            C, Cp, _ = ops.cma_cov_pad(state.C.contiguous(), S.contiguous(), pc, a, float(self.c1), float(self.cmu), state.B.contiguous(), np_)
+            # Cp[:d, :d] = triu(C) + triu(C, 1)ᵀ, the reference's symmetrisation (cma_es.py:193-195)
+            w, Bn, eig_stats = host_phase(sbr_phase, Cp[:d, :d], state.B, out_like=(state.D, state.B, state.eig_stats))
+            B, D, BdivD = ops.cma_eig_out(Bn.contiguous(), w.contiguous(), d)
+        else:
+            np_ = jacobi.padded_size(d)
+            C, Cp, Bp = ops.cma_cov_pad(state.C.contiguous(), S.contiguous(), pc, a, float(self.c1), float(self.cmu), state.B.contiguous(), np_)
+            w, Bp = jacobi.warm_eigh_padded(Cp, Bp, d, max_sweeps=self.eig_sweeps)
+            B, D, BdivD = ops.cma_eig_out(Bp, w, d)
         invsqrtC = plain_nt(BdivD, B) if config.get("plain_gemm") == "blas" else gemm(Operand(BdivD), Operand(B), d, d, d)
         return state.update(mean=mean, ps=ps, pc=pc, C=C, sigma=sigma.reshape(state.sigma.shape), B=B, D=D, invsqrtC=invsqrtC,
-                            count_eigen=state.count_eigen + 1)
+                            count_eigen=state.count_eigen + 1, eig_stats=eig_stats)
 
     def _finish_tell(self, state, dm, S):
         if self._fused_epilogue_ok(state):
@@ -258,6 +271,8 @@ class SepCMAES(CMAES):
             sigma=torch.tensor(self.init_stdev, dtype=torch.float32, device=dev),
             key=key.to(dev),
             population=torch.zeros((self.pop_size, d), device=dev),
+            # last decomposition: [relative off-norm, Jacobi sweeps, refinement iterations, fallback]
+            eig_stats=torch.zeros(4, dtype=torch.float64, device=dev),
         )
 
     def ask(self, state):

@@ -21,6 +21,10 @@ MI355X-first execution model (replaces ``jax.jit`` / ``pmap``):
   host after each graph launch with the graph's static output buffers, so
   monitors need not be capture-safe.  ``graph="auto"`` tries the capture once and
   falls back to eager steps (with a warning) if the step is not capturable.
+  Steps that need host decisions mid-generation call
+  :func:`evoxmi.runtime.host_phase`; the capture is then split into graph segments
+  with that host phase replayed eagerly between them
+  (:class:`evoxmi.runtime.SegmentedGraph`).
 * ``enable_distributed(state)`` turns the workflow into an SPMD program with one
   process per GPU (``torch.distributed``; backend ``nccl`` = RCCL over xGMI on
   MI355X, ``gloo`` on CPU).  The algorithm state is replicated; every rank
@@ -44,6 +48,7 @@ from ..core.state import tree_flatten, tree_map
 from .. import config
 from ..utils.common import parse_opt_direction
 from ..utils.profiling import trace_range
+from ..runtime.graph import SegmentedGraph
 
 HOOKS = ("pre_step", "pre_ask", "post_ask", "pre_eval", "post_eval", "pre_tell", "post_tell", "post_step")
 
@@ -233,9 +238,12 @@ class StdWorkflow(Workflow):
                 self._proto_step(False, tree_map(lambda x: x.clone() if isinstance(x, torch.Tensor) else x, static))
             torch.cuda.current_stream(dev).wait_stream(s)
             torch.cuda.synchronize(dev)
-            g = torch.cuda.CUDAGraph()
+            # segmented capture: steps that need host decisions mid-generation (e.g. the
+            # CMA-ES eigensolver's convergence checks) split the graph at host phases
+            g = SegmentedGraph()
             record = {}
-            with torch.cuda.graph(g, stream=s):
+
+            def body():
                 out = self._proto_step(False, static, record=record)
                 in_leaves, in_spec = tree_flatten(static)
                 out_leaves, out_spec = tree_flatten(out)
@@ -247,6 +255,9 @@ class StdWorkflow(Workflow):
                             raise RuntimeError("graph=True: a state tensor changed shape/dtype across a step")
                         if a.data_ptr() != b.data_ptr():
                             a.copy_(b)
+                return in_leaves, out_leaves
+
+            in_leaves, out_leaves = g.capture(body, s)
         finally:
             self.registered_hooks = saved_hooks
         # python (non-tensor) leaves must be step-invariant, except the generation counter
