@@ -377,7 +377,7 @@ at::Tensor pm(const at::Tensor& x, const at::Tensor& lb, const at::Tensor& ub, c
   return out;
 }
 
-at::Tensor nds(const at::Tensor& f, int64_t limit) {
+at::Tensor nds(const at::Tensor& f, int64_t limit, const c10::optional<at::Tensor>& err) {
   CHECK_DEV(f); CHECK_F32(f); CHECK_CONTIG(f);
   TORCH_CHECK(f.dim() == 2 && f.size(1) >= 1 && f.size(1) <= 8, "fitness must be (n, m) with m <= 8");
   const int64_t n = f.size(0), nw = (n + 31) / 32;
@@ -387,9 +387,13 @@ at::Tensor nds(const at::Tensor& f, int64_t limit) {
   auto rank = at::empty({n}, f.options().dtype(at::kInt));
   auto ws = at::empty({(int64_t)evx_nds_workspace_words((int)n)}, f.options().dtype(at::kInt));
   if (limit <= 0 || limit > n) limit = n;
-  if (n > 0)
+  if (err) TORCH_CHECK(err->is_cuda() && err->scalar_type() == at::kInt && err->numel() >= 1, "err must be a device int32 flag");
+  if (n > 0) {
+    const int blocks = evx_nds_peel_blocks((int)n);
+    TORCH_CHECK(blocks > 0, "nds: the persistent peel cannot be co-resident on this device at n = ", n);
     evx_nds(f.data_ptr<float>(), (int)n, (int)f.size(1), (int)limit, reinterpret_cast<uint32_t*>(DW.data_ptr<int>()), rank.data_ptr<int>(),
-            reinterpret_cast<uint32_t*>(ws.data_ptr<int>()), cur_stream());
+            reinterpret_cast<uint32_t*>(ws.data_ptr<int>()), err ? err->data_ptr<int>() : nullptr, blocks, cur_stream());
+  }
   return rank;
 }
 
@@ -631,7 +635,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("gemm_set_config(int cfg) -> ()");
   m.def("sbx(Tensor x, Tensor keys, float pro_c, float dis_c, int type) -> Tensor");
   m.def("pm(Tensor x, Tensor lb, Tensor ub, Tensor keys, float pro_m, float dis_m, int nm) -> Tensor");
-  m.def("nds(Tensor f, int limit=0) -> Tensor");
+  m.def("nds(Tensor f, int limit=0, Tensor? err=None) -> Tensor");
   m.def("ant_rollout(Tensor W, int h1, int h2, Tensor init, int cap) -> Tensor[]");
   m.def("stochastic_ranking(Tensor I1, Tensor I2, Tensor rnd, float pc) -> Tensor");
   m.def("moead_scan(Tensor objs, Tensor off_objs, Tensor P, Tensor W, Tensor z, int func, int nr, int update_z) -> Tensor[]");

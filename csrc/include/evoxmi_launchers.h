@@ -61,7 +61,9 @@ void evx_moead_scan(float* objs, const float* off_objs, const int32_t* P, const 
                     int T, int M, int func, int nr, int update_z, hipStream_t s);
 void evx_ant_rollout(const float* W, int64_t P, int N, int h1, int h2, const float* init, int cap, float* ret, int* steps, hipStream_t s);
 size_t evx_nds_workspace_words(int n);
-void evx_nds(const float* f, int n, int m, int limit, uint32_t* DW, int32_t* rank, uint32_t* ws, hipStream_t s);
+int evx_nds_peel_blocks(int n);
+void evx_nds(const float* f, int n, int m, int limit, uint32_t* DW, int32_t* rank, uint32_t* ws, int32_t* err, int blocks,
+             hipStream_t s);
 
 // moead.hip
 void evx_moead_parents(const int64_t* nb, int N, int T, const int64_t* key, int32_t* p0, int32_t* p1, hipStream_t s);

@@ -169,7 +169,9 @@ __device__ __forceinline__ void solve_pair(const float* __restrict__ A, int np, 
       const float tau = (alq - alp) * __builtin_amdgcn_rcpf(2.f * alo);
       const float tt = copysignf(1.f, tau) * __builtin_amdgcn_rcpf(fabsf(tau) + __builtin_amdgcn_sqrtf(fmaf(tau, tau, 1.f)));
       const float cr = __builtin_amdgcn_rsqf(fmaf(tt, tt, 1.f));
-      const bool rot = alo != 0.f;
+      // normal-range couplings only: a denormal alo makes rcp(2·alo) overflow to inf and, with
+      // alq == alp, tau = 0·inf = NaN (IEEE denormals under -O3)
+      const bool rot = fabsf(alo) >= 1.17549435e-38f;
       const float cl = rot ? cr : 1.f, sl = rot ? tt * cr : 0.f;
       // row-pair rotation from lane (k, l = k) = lane 0 of this 16-lane row
       const float ck = row_bcast0(cl);

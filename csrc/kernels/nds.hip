@@ -98,7 +98,8 @@ constexpr int PEEL_PARTS = 8;  // waves per workgroup = word parts per row
 constexpr int PEEL_MAXW = 2048;  // n <= 65536
 
 __global__ void __launch_bounds__(64 * PEEL_PARTS) peel_kernel(const uint32_t* __restrict__ DW, int n, int nw, int limit,
-                                                   int32_t* __restrict__ rank, uint32_t* __restrict__ ws) {
+                                                   int32_t* __restrict__ rank, uint32_t* __restrict__ ws, int32_t* __restrict__ err,
+                                                   int barrier_extra) {
   uint32_t* R[2] = {ws + 4, ws + 4 + nw};
   uint32_t* left = ws + 4 + 2 * nw;
   uint32_t* wptr = left + n + 1;  // 4 per row
@@ -173,7 +174,14 @@ __global__ void __launch_bounds__(64 * PEEL_PARTS) peel_kernel(const uint32_t* _
       __hip_atomic_fetch_add(&left[k], wg_left, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (threadIdx.x == 0 && my_ranked)
       __hip_atomic_fetch_add(&ws[3], my_ranked, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!grid_barrier(ws, gridDim.x, gen)) return;
+    if (!grid_barrier(ws, gridDim.x + barrier_extra, gen)) {
+      // a workgroup never arrived (not co-resident): rows not ranked yet go last (rank n,
+      // never the best front) and the sticky device error word tells the host
+      for (int jb = blockIdx.x * 64, pass = 0; jb < n; jb += rows_per_pass, ++pass)
+        if (q == 0 && jb + lane < n && !done_s[pass][lane]) rank[jb + lane] = n;
+      if (threadIdx.x == 0 && err) __hip_atomic_fetch_or(err, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
     const uint32_t still = __hip_atomic_load(&left[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t done = __hip_atomic_load(&ws[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (still == 0) return;
@@ -193,7 +201,28 @@ __global__ void __launch_bounds__(256) zero_kernel(uint32_t* __restrict__ p, int
 
 size_t evx_nds_workspace_words(int n) { return 4 + 2 * (size_t)((n + 31) / 32) + (PEEL_PARTS + 1) * (size_t)n + 1; }
 
-void evx_nds(const float* f, int n, int m, int limit, uint32_t* DW, int32_t* rank, uint32_t* ws, hipStream_t s) {
+// Workgroups the persistent peel may use: every one must be co-resident for the grid
+// barrier, so the grid is capped by the device's CU count × the kernel's occupancy
+// (hipOccupancy… on this kernel), not by a hard-coded 256.  Returns 0 if the peel cannot
+// run co-resident at this n (the caller falls back to the host-orchestrated peel).
+int evx_nds_peel_blocks(int n) {
+  static int capacity = -1;
+  if (capacity < 0) {
+    int dev = 0, cus = 0, per_cu = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, peel_kernel, 64 * PEEL_PARTS, 0) != hipSuccess) per_cu = 0;
+    capacity = cus * per_cu;
+  }
+  static const int cap = [] { const char* e = getenv("EVOXMI_NDS_BLOCKS"); const int v = e ? atoi(e) : (1 << 30); return v < 1 ? 1 : v; }();
+  int blocks = min(min((n + 63) / 64, cap), capacity);
+  const int need = (n + 255) / 256;  // the kernel keeps ≤ 4 row passes per workgroup in LDS
+  if (blocks < need) return 0;
+  return blocks;
+}
+
+void evx_nds(const float* f, int n, int m, int limit, uint32_t* DW, int32_t* rank, uint32_t* ws, int32_t* err, int blocks,
+             hipStream_t s) {
   const int nw = (n + 31) / 32;
   dim3 grid((n + 255) / 256, nw);
   if (m == 2) dominance_kernel<2><<<grid, 256, 0, s>>>(f, n, m, nw, DW);
@@ -203,10 +232,8 @@ void evx_nds(const float* f, int n, int m, int limit, uint32_t* DW, int32_t* ran
   const int64_t nws = (int64_t)evx_nds_workspace_words(n);
   const int zb = (int)((nws + 255) / 256 < 64 ? (nws + 255) / 256 : 64);
   zero_kernel<<<zb, 256, 0, s>>>(ws, nws);
-  // workgroups of the persistent peel: 64 rows each (EVOXMI_NDS_BLOCKS caps it; ≤ 256,
-  // one per CU at most, so every workgroup is co-resident for the grid barrier)
-  static const int cap = [] { const char* e = getenv("EVOXMI_NDS_BLOCKS"); const int v = e ? atoi(e) : 256; return v < 1 ? 1 : (v > 256 ? 256 : v); }();
-  int blocks = min((n + 63) / 64, cap);
-  blocks = max(blocks, (n + 255) / 256);  // the kernel keeps ≤ 4 row passes per workgroup in LDS
-  peel_kernel<<<blocks, 64 * PEEL_PARTS, 0, s>>>(DW, n, nw, limit, rank, ws);
+  // fault-injection hook for the error-path test: the barrier then waits for a workgroup
+  // that is never launched, times out, and the sticky error word must report it
+  static const int extra = getenv("EVOXMI_NDS_FAULT_TEST") ? 1 : 0;
+  peel_kernel<<<blocks, 64 * PEEL_PARTS, 0, s>>>(DW, n, nw, limit, rank, ws, err, extra);
 }

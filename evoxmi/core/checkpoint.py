@@ -3,8 +3,9 @@
 The reference pickles the whole tree (``src/evox/core/state.py:228-234``).  Pickle
 executes code on load, so evoxmi writes a single **safetensors** file instead:
 
-* every tensor leaf is a safetensors entry keyed by its tree path
-  (``algorithm/C``, ``algorithm/optimizer/opt_state.0`` ...);
+* every tensor leaf is a safetensors entry keyed by a running index (``t0``, ``t1``, ...;
+  version 1 keyed by the tree path, which let a dict key containing ``.`` or ``/``
+  collide with another leaf); the manifest keeps the tree path of each tensor;
 * the tree itself — node ids, field names, child names, Python scalars and
   dataclass type names — is a JSON manifest stored in the safetensors metadata
   under ``evoxmi_manifest`` with a ``format``/``version`` tag.
@@ -22,7 +23,7 @@ from typing import Any, Dict
 import torch
 
 FORMAT = "evoxmi-state"
-VERSION = 1
+VERSION = 2
 
 _DATACLASS_REGISTRY: Dict[str, type] = {}
 
@@ -38,9 +39,10 @@ def _encode_value(v: Any, path: str, tensors: dict):
     if isinstance(v, State):
         return {"t": "state", "node": _encode_node(v, path, tensors)}
     if isinstance(v, torch.Tensor):
-        key = path
+        key = f"t{len(tensors)}"
+        assert key not in tensors
         tensors[key] = v.detach().to("cpu").contiguous().clone()
-        return {"t": "tensor", "key": key}
+        return {"t": "tensor", "key": key, "path": path}
     if v is None:
         return {"t": "none"}
     if isinstance(v, bool):
@@ -57,7 +59,17 @@ def _encode_value(v: Any, path: str, tensors: dict):
             "items": [_encode_value(x, f"{path}.{i}", tensors) for i, x in enumerate(v)],
         }
     if isinstance(v, dict):
-        return {"t": "dict", "items": {str(k): _encode_value(x, f"{path}.{k}", tensors) for k, x in v.items()}}
+        for k in v:
+            if not isinstance(k, (str, int, float, bool)):
+                raise TypeError(f"cannot checkpoint dict key of type {type(k)} at {path}")
+        if len({str(k) for k in v}) != len(v):
+            raise ValueError(f"dict keys at {path} collide once stringified: {list(v)}")
+        return {
+            "t": "dict",
+            "items": {str(k): _encode_value(x, f"{path}.{k}", tensors) for k, x in v.items()},
+            # JSON object keys are strings: record the original key types to restore them
+            "ktypes": {str(k): type(k).__name__ for k in v},
+        }
     if dataclasses.is_dataclass(v):
         name = f"{type(v).__module__}.{type(v).__qualname__}"
         return {
@@ -85,7 +97,9 @@ def _decode_value(d: dict, tensors: dict, device):
         items = [_decode_value(x, tensors, device) for x in d["items"]]
         return tuple(items) if t == "tuple" else items
     if t == "dict":
-        return {k: _decode_value(x, tensors, device) for k, x in d["items"].items()}
+        conv = {"int": int, "float": float, "bool": lambda s: s == "True", "str": str}
+        kt = d.get("ktypes", {})
+        return {conv[kt.get(k, "str")](k): _decode_value(x, tensors, device) for k, x in d["items"].items()}
     if t == "dataclass":
         cls = _DATACLASS_REGISTRY.get(d["cls"])
         if cls is None:

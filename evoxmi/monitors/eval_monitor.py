@@ -25,6 +25,13 @@ def _apply_dir(x, od):
     return x if od == 1 else x * od
 
 
+def _check_kernels():
+    from ..ops import _ext
+
+    if _ext._ERR:
+        _ext.check_kernel_errors()
+
+
 class EvalMonitor(Monitor):
     def __init__(self, full_fit_history=True, full_sol_history=False, topk=1, calc_pf=False, history_to_host=False):
         super().__init__()
@@ -140,19 +147,24 @@ class EvalMonitor(Monitor):
         self.latest_solution = cand_sol.detach().clone() if cand_sol is not None else None
 
     # ---------------------------------------------------------------- getters
+    # Getters are host sync points: a kernel failure recorded in the sticky device error
+    # word (e.g. the NDS grid barrier timing out) raises here instead of going unnoticed.
     def get_latest_fitness(self):
+        _check_kernels()
         return _apply_dir(self.latest_fitness, self.opt_direction)
 
     def get_latest_solution(self):
         return self.latest_solution
 
     def get_pf_fitness(self):
+        _check_kernels()
         return _apply_dir(self.pf_fitness, self.opt_direction)
 
     def get_pf_solutions(self):
         return self.pf_solutions
 
     def get_topk_fitness(self):
+        _check_kernels()
         return _apply_dir(self.topk_fitness, self.opt_direction)
 
     def get_topk_solutions(self):
@@ -162,6 +174,7 @@ class EvalMonitor(Monitor):
         return None if self.topk_solutions is None else self.topk_solutions[0]
 
     def get_best_fitness(self):
+        _check_kernels()
         if self.topk_fitness is None:
             warnings.warn("trying to get info from a monitor with no recorded data")
             return None
@@ -190,6 +203,7 @@ class EvalMonitor(Monitor):
     def flush(self):
         if torch.cuda.is_available() and torch.cuda.is_initialized():
             torch.cuda.synchronize()
+        _check_kernels()
 
     def close(self):
         self.flush()

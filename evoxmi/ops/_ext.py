@@ -53,3 +53,38 @@ def ops():
 
 def philox_fill(key: torch.Tensor, n: int, dist: int, offset: int = 0) -> torch.Tensor:
     return ops().philox_fill(key, int(n), int(dist), int(offset))
+
+
+# ---------------------------------------------------------------- sticky kernel error word
+# Kernels that can detect a failure they cannot report synchronously (out-of-range
+# indices, a persistent kernel's grid barrier timing out) OR a bit into one int32 word per
+# device.  It is read at host sync points: monitor getters, ``check_kernel_errors()``,
+# and after every launch when EVOXMI_DEBUG=1.
+KERNEL_ERROR_BITS = {1: "de_trial: out-of-range row index", 2: "de_trial: out-of-range target row",
+                     4: "nds: persistent peel grid barrier timed out (workgroups not co-resident)"}
+_ERR = {}
+
+
+def error_flag(dev) -> torch.Tensor:
+    dev = torch.device(dev)
+    if dev not in _ERR:
+        _ERR[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
+    return _ERR[dev]
+
+
+def kernel_error_flags() -> int:
+    v = 0
+    for f in _ERR.values():
+        v |= int(f.item())
+    return v
+
+
+def check_kernel_errors(reset: bool = True) -> None:
+    """Raise if any kernel has set the sticky error word (one host sync per device)."""
+    v = kernel_error_flags()
+    if v:
+        if reset:
+            for f in _ERR.values():
+                f.zero_()
+        msgs = [m for b, m in KERNEL_ERROR_BITS.items() if v & b] or [f"flag {v}"]
+        raise RuntimeError("evoxmi kernel error: " + "; ".join(msgs))

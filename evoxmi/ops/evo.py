@@ -24,22 +24,15 @@ def polynomial(key, x, lb, ub, pro_m, dis_m):
 
 
 _CROSS = {"bin": 0, "exp": 1, "arith": 2}
-_ERR = {}
-
-
 def _err_flag(dev):
-    """Sticky device flag the index-checking kernels OR their errors into (read it with
-    ``kernel_error_flags()``; with EVOXMI_DEBUG=1 every launch checks it synchronously)."""
-    if dev not in _ERR:
-        _ERR[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
-    return _ERR[dev]
+    """Sticky device error word (``_ext.error_flag``); read with ``kernel_error_flags()``."""
+    return _ext.error_flag(dev)
 
 
 def kernel_error_flags(device="cuda") -> int:
-    v = 0
-    for f in _ERR.values():
-        v |= int(f.item())
-    return v
+    return _ext.kernel_error_flags()
+
+
 _REPAIR = {"none": 0, "clip": 1, "midpoint": 2}
 
 

@@ -4,6 +4,7 @@ from __future__ import annotations
 import torch
 
 from . import _ext
+from .. import config
 
 
 def non_dominated_sort(f: torch.Tensor, until: int = 0) -> torch.Tensor:
@@ -11,7 +12,15 @@ def non_dominated_sort(f: torch.Tensor, until: int = 0) -> torch.Tensor:
     ranked and the remaining rows get rank ``n`` (larger than every real rank)."""
     f = f.to(torch.float32).contiguous()
     if f.shape[0] <= 65536 and f.shape[1] <= 8:
-        return _ext.ops().nds(f, int(until))
+        try:
+            rank = _ext.ops().nds(f, int(until), _ext.error_flag(f.device))
+        except RuntimeError as e:
+            if "co-resident" not in str(e):
+                raise
+        else:
+            if config.get("debug") and not torch.cuda.is_current_stream_capturing():
+                _ext.check_kernel_errors()
+            return rank
     from ..operators.selection.non_dominate import _peel
     from ..utils.common import dominate_relation
 

@@ -46,10 +46,21 @@ def test_moea_runs(name):
     assert run_moea(ALGOS[name]()) < float("inf")
 
 
-@pytest.mark.parametrize("name", ["NSGA2", "NSGA3", "MOEAD", "RVEA", "SPEA2", "TDEA", "IBEA"])
+# IGD on DTLZ2 (m = 3, d = 12, N = 100) after 100 generations, seed 42 (measured:
+# BCEIBEA .055, BiGE .071, EAGMOEAD .239, GDE3 .083, HypE .104, IBEA .079, IMMOEA .109,
+# KnEA .061, LMOCSO .067, MOEAD .055, MOEADDRA .083, MOEADM2M .135, NSGA2 .075, NSGA3 .054,
+# RVEA .055, RVEAa .065, SPEA2 .058, SRA .088, TDEA .054).  Bounds are 0.1 except where the
+# algorithm's design limits it on this front: EAG-MOEA/D decomposes with a *weighted sum*
+# (reference eagmoead.py:79), which cannot reach the concave parts of the DTLZ2 front;
+# M2M splits N = 100 over regional subpopulations; HypE's Monte-Carlo HV and IM-MOEA's
+# inverse models converge more slowly in 100 generations.
+IGD_BOUND = {"EAGMOEAD": 0.3, "MOEADM2M": 0.2, "HypE": 0.15, "IMMOEA": 0.15}
+
+
+@pytest.mark.parametrize("name", sorted(ALGOS))
 def test_moea_converges_dtlz2(name):
     algo = ALGOS[name]()
-    assert run_moea(algo, DTLZ2(d=N, m=M), iters=100) < 0.1
+    assert run_moea(algo, DTLZ2(d=N, m=M), iters=100) < IGD_BOUND.get(name, 0.1)
 
 
 def test_moead_scan_gpu_semantics_cpu_oracle():

@@ -52,7 +52,8 @@ def test_basic_tree_and_node_ids():
     assert top.mid.a_leaf._node_id == 3
     assert top.mid.b_leaf._node_id == 4
     assert st.get_child_state("mid").get_child_state("b_leaf").c == 2
-    assert st.mid is None if False else True
+    assert set(st._child_states) == {"leaf", "mid"}
+    assert set(st.get_child_state("mid")._child_states) == {"a_leaf", "b_leaf"}
 
 
 def test_use_state_scoping():
@@ -115,3 +116,21 @@ def test_find_and_update_path():
     assert sub.c == 1
     st2 = st.update_path(path, sub.update(c=10))
     assert st2.get_child_state("mid").get_child_state("a_leaf").c == 10
+
+
+def test_checkpoint_dict_keys_do_not_collide(tmp_path):
+    """A dict key containing '.' must not overwrite another leaf's tensor, and non-str
+    dict keys come back with their type (advisor finding on checkpoint.py)."""
+    import torch
+
+    from evoxmi.core import State
+    from evoxmi.core.checkpoint import load_state, save_state
+
+    st = State(tab={"a.b": torch.ones(2), "a": {"b": torch.zeros(3)}, 7: torch.full((1,), 7.0)})
+    p = str(tmp_path / "ck.safetensors")
+    save_state(st, p)
+    back = load_state(p)
+    tab = back.tab
+    assert torch.equal(tab["a.b"], torch.ones(2))
+    assert torch.equal(tab["a"]["b"], torch.zeros(3))
+    assert 7 in tab and torch.equal(tab[7], torch.full((1,), 7.0))
