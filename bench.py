@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--profile-phases", action="store_true")
     ap.add_argument("--force-dist", action="store_true", help="run the distributed (sharded + RCCL) path even on one rank")
+    ap.add_argument("--phase-steps", type=int, default=3, help="eager generations timed per phase after the timed loop (0: off)")
     args = ap.parse_args()
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -77,6 +78,21 @@ def main():
         state = wf.step(state)
     sync()
     elapsed = time.perf_counter() - t0
+    # per-phase breakdown (outside the timed region): a few eager generations with
+    # stream-ordered hipEvent timers; "tell" includes "eigh" (and "all_reduce" when sharded)
+    hist = list(eigh_mod.HISTORY)  # decompositions of the timed generations only
+    phases = None
+    if args.phase_steps > 0:
+        from evoxmi.utils.profiling import PhaseTimer
+
+        timer = PhaseTimer(device)
+        wf.phase_timer = timer
+        graph_on, wf.graph = wf.graph, False
+        for _ in range(args.phase_steps):
+            state = wf.step(state)
+        sync()
+        wf.graph, wf.phase_timer = graph_on, None
+        phases = {k: round(v["mean_ms"], 4) for k, v in timer.summary().items()}
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if dist_on:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -110,7 +126,8 @@ def main():
                 "eigh": config.get("eigh"),
             },
         }
-        hist = list(eigh_mod.HISTORY)
+        if phases:
+            out["phases_ms_eager"] = phases
         if hist:
             # every timed generation's decomposition: relative off-norm ‖offdiag(BᵀCB)‖/‖diag‖
             out["eigh_stats"] = {

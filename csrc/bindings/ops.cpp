@@ -495,21 +495,34 @@ std::vector<at::Tensor> moead_parents(const at::Tensor& nb, const at::Tensor& ke
   return {p0, p1};
 }
 
+// rows = 0: every offspring (N = p0.numel()); rows > 0: offspring row0 .. row0+rows−1 only;
+// win given: output row s = offspring win[s] (regenerated) or pop[s] when win[s] < 0
 at::Tensor moead_variation(const at::Tensor& pop, const at::Tensor& p0, const at::Tensor& p1, const at::Tensor& kx, const at::Tensor& km,
-                           const at::Tensor& lb, const at::Tensor& ub, double pro_c, double dis_c, double pro_m, double dis_m, int64_t nm) {
+                           const at::Tensor& lb, const at::Tensor& ub, double pro_c, double dis_c, double pro_m, double dis_m, int64_t nm,
+                           int64_t row0, int64_t rows, const c10::optional<at::Tensor>& win) {
   for (auto* t : {&pop, &lb, &ub}) { CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t); }
   for (auto* t : {&p0, &p1}) { CHECK_DEV(*t); CHECK_CONTIG(*t); TORCH_CHECK(t->scalar_type() == at::kInt, "parents must be int32"); }
   TORCH_CHECK(kx.scalar_type() == at::kLong && kx.numel() == 4 && kx.is_contiguous() && kx.is_cuda(), "kx must be int64[2][2] on device");
   TORCH_CHECK(km.scalar_type() == at::kLong && km.numel() == 4 && km.is_contiguous() && km.is_cuda(), "km must be int64[2][2] on device");
   TORCH_CHECK(pop.dim() == 2 && lb.numel() == pop.size(1) && ub.numel() == pop.size(1), "bounds must be (d,)");
-  const int64_t N = p0.numel(), d = pop.size(1);
-  TORCH_CHECK(p1.numel() == N, "p0/p1 length mismatch");
+  const int64_t Np = p0.numel(), d = pop.size(1);
+  TORCH_CHECK(p1.numel() == Np, "p0/p1 length mismatch");
+  int64_t R = rows > 0 ? rows : Np;
+  const int32_t* wp = nullptr;
+  if (win) {
+    TORCH_CHECK(win->is_cuda() && win->scalar_type() == at::kInt && win->is_contiguous() && win->numel() == pop.size(0),
+                "win must be int32 (N,) with one entry per population row");
+    R = pop.size(0);
+    wp = win->data_ptr<int>();
+    row0 = 0;
+  }
+  TORCH_CHECK(row0 >= 0 && (win || row0 + R <= Np), "moead_variation: offspring rows out of range");
   c10::DeviceGuard g(pop.device());
-  auto out = at::empty({N, d}, pop.options());
-  if (N > 0 && d > 0)
-    evx_moead_variation(pop.data_ptr<float>(), p0.data_ptr<int>(), p1.data_ptr<int>(), out.data_ptr<float>(), (int)N, (int)d, kx.data_ptr<int64_t>(),
+  auto out = at::empty({R, d}, pop.options());
+  if (R > 0 && d > 0)
+    evx_moead_variation(pop.data_ptr<float>(), p0.data_ptr<int>(), p1.data_ptr<int>(), out.data_ptr<float>(), (int)R, (int)d, kx.data_ptr<int64_t>(),
                         km.data_ptr<int64_t>(), lb.data_ptr<float>(), ub.data_ptr<float>(), (float)pro_c, (float)dis_c, (float)pro_m, (float)dis_m,
-                        (int)nm, cur_stream());
+                        (int)nm, cur_stream(), (int)row0, wp);
   return out;
 }
 
@@ -650,7 +663,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("cma_eig_out(Tensor Bp, Tensor w, int d) -> Tensor[]");
   m.def("nsga_select(Tensor rank, Tensor f, int N, int mask_pos) -> Tensor");
   m.def("moead_parents(Tensor nb, Tensor key) -> Tensor[]");
-  m.def("moead_variation(Tensor pop, Tensor p0, Tensor p1, Tensor kx, Tensor km, Tensor lb, Tensor ub, float pro_c, float dis_c, float pro_m, float dis_m, int nm) -> Tensor");
+  m.def("moead_variation(Tensor pop, Tensor p0, Tensor p1, Tensor kx, Tensor km, Tensor lb, Tensor ub, float pro_c, float dis_c, float pro_m, float dis_m, int nm, int row0=0, int rows=0, Tensor? win=None) -> Tensor");
   m.def("moead_replace(Tensor pop_obj, Tensor off_obj, Tensor W, Tensor z, Tensor zmax, Tensor rowptr, Tensor owner, int func) -> Tensor[]");
   m.def("moead_select_rows(Tensor pop, Tensor off, Tensor win) -> Tensor");
   m.def("sbr_stats(Tensor A) -> Tensor");

@@ -69,7 +69,7 @@ void evx_nds(const float* f, int n, int m, int limit, uint32_t* DW, int32_t* ran
 void evx_moead_parents(const int64_t* nb, int N, int T, const int64_t* key, int32_t* p0, int32_t* p1, hipStream_t s);
 void evx_moead_variation(const float* pop, const int32_t* p0, const int32_t* p1, float* out, int N, int d, const int64_t* kx,
                          const int64_t* km, const float* lb, const float* ub, float pro_c, float dis_c, float pro_m, float dis_m,
-                         int nm, hipStream_t s);
+                         int nm, hipStream_t s, int row0 = 0, const int32_t* win = nullptr);
 void evx_moead_replace(const float* pop_obj, const float* off_obj, const float* W, const float* z, const float* zmax,
                        const int32_t* rowptr, const int32_t* owner, int N, int M, int func, int32_t* win, float* new_obj,
                        hipStream_t s);

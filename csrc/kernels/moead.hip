@@ -139,18 +139,32 @@ __device__ __forceinline__ float pm_gene(float v, float lo, float hi, uint32_t w
 
 // one thread = 4 consecutive genes (d % 4 == 0 ⇒ they share one Philox block per stream):
 // 2 Philox blocks per 4 genes (SBX word + PM site) plus one per row for the pair rate
+// Output row r holds offspring i = row0 + r, or (SELECT) i = win[r] with a copy of pop[r]
+// where win[r] < 0: the population-sharded MOEA/D regenerates the winning offspring rows
+// from the replicated population instead of shipping them between GPUs.  Counters use
+// the global offspring index i, so every row is bit-identical to the full launch.
+template <bool SELECT>
 __global__ void __launch_bounds__(256) variation4_kernel(const float* __restrict__ pop, const int32_t* __restrict__ p0,
                                                          const int32_t* __restrict__ p1, float* __restrict__ out, int N, int d,
                                                          const int64_t* __restrict__ kx, const int64_t* __restrict__ km,
                                                          const float* __restrict__ lb, const float* __restrict__ ub,
-                                                         float pro_c, float dis_c, float pro_m, float dis_m, int nm) {
+                                                         float pro_c, float dis_c, float pro_m, float dis_m, int nm, int row0,
+                                                         const int32_t* __restrict__ win) {
   const VarKeys K = load_keys(kx, km);
   const int q = d >> 2;
   const int64_t total = (int64_t)N * q;
   const float e = 1.f / (dis_c + 1.f), e1 = dis_m + 1.f, inv = 1.f / (dis_m + 1.f), pr = pro_m / d;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    const int i = (int)(t / q), c = (int)(t - (int64_t)i * q);
+    const int r = (int)(t / q), c = (int)(t - (int64_t)r * q);
     const int j = c << 2;
+    int i = row0 + r;
+    if (SELECT) {
+      i = win[r];
+      if (i < 0) {
+        *reinterpret_cast<float4*>(out + (int64_t)r * d + j) = *reinterpret_cast<const float4*>(pop + (int64_t)r * d + j);
+        continue;
+      }
+    }
     const uint64_t g0 = (uint64_t)i * d + j;
     const float4 a = *reinterpret_cast<const float4*>(pop + (int64_t)p0[i] * d + j);
     const float4 b = *reinterpret_cast<const float4*>(pop + (int64_t)p1[i] * d + j);
@@ -174,27 +188,38 @@ __global__ void __launch_bounds__(256) variation4_kernel(const float* __restrict
     y.y = fmaxf(fminf(y.y, hi.y), lo.y);
     y.z = fmaxf(fminf(y.z, hi.z), lo.z);
     y.w = fmaxf(fminf(y.w, hi.w), lo.w);
-    *reinterpret_cast<float4*>(out + (int64_t)i * d + j) = y;
+    *reinterpret_cast<float4*>(out + (int64_t)r * d + j) = y;
   }
 }
 
 // generic d: one thread per gene
+template <bool SELECT>
 __global__ void __launch_bounds__(256) variation1_kernel(const float* __restrict__ pop, const int32_t* __restrict__ p0,
                                                          const int32_t* __restrict__ p1, float* __restrict__ out, int N, int d,
                                                          const int64_t* __restrict__ kx, const int64_t* __restrict__ km,
                                                          const float* __restrict__ lb, const float* __restrict__ ub,
-                                                         float pro_c, float dis_c, float pro_m, float dis_m, int nm) {
+                                                         float pro_c, float dis_c, float pro_m, float dis_m, int nm, int row0,
+                                                         const int32_t* __restrict__ win) {
   const VarKeys K = load_keys(kx, km);
   const int64_t total = (int64_t)N * d;
   const float e = 1.f / (dis_c + 1.f), e1 = dis_m + 1.f, inv = 1.f / (dis_m + 1.f), pr = pro_m / d;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    const int i = (int)(t / d), j = (int)(t - (int64_t)i * d);
+  for (int64_t tt = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; tt < total; tt += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(tt / d), j = (int)(tt - (int64_t)r * d);
+    int i = row0 + r;
+    if (SELECT) {
+      i = win[r];
+      if (i < 0) {
+        out[tt] = pop[tt];
+        continue;
+      }
+    }
+    const int64_t t = (int64_t)i * d + j;  // global gene counter
     const float a = pop[(int64_t)p0[i] * d + j], b = pop[(int64_t)p1[i] * d + j];
     const bool no_x = u24(word_at((uint64_t)i, K.pr0, K.pr1)) > pro_c;
     float y = sbx_child(a, b, word_at(t, K.g0, K.g1), no_x, e);
     const float lo = lb[j], hi = ub[j];
     if (i < nm) y = pm_gene(y, lo, hi, word_at(t, K.st0, K.st1), (uint64_t)t, K, pr, e1, inv);
-    out[t] = fmaxf(fminf(y, hi), lo);
+    out[tt] = fmaxf(fminf(y, hi), lo);
   }
 }
 
@@ -262,11 +287,16 @@ void evx_moead_parents(const int64_t* nb, int N, int T, const int64_t* key, int3
 
 void evx_moead_variation(const float* pop, const int32_t* p0, const int32_t* p1, float* out, int N, int d, const int64_t* kx,
                          const int64_t* km, const float* lb, const float* ub, float pro_c, float dis_c, float pro_m, float dis_m,
-                         int nm, hipStream_t s) {
-  if ((d & 3) == 0)
-    variation4_kernel<<<grid1((int64_t)N * (d >> 2)), 256, 0, s>>>(pop, p0, p1, out, N, d, kx, km, lb, ub, pro_c, dis_c, pro_m, dis_m, nm);
-  else
-    variation1_kernel<<<grid1((int64_t)N * d), 256, 0, s>>>(pop, p0, p1, out, N, d, kx, km, lb, ub, pro_c, dis_c, pro_m, dis_m, nm);
+                         int nm, hipStream_t s, int row0, const int32_t* win) {
+  if ((d & 3) == 0) {
+    const int g = grid1((int64_t)N * (d >> 2));
+    if (win) variation4_kernel<true><<<g, 256, 0, s>>>(pop, p0, p1, out, N, d, kx, km, lb, ub, pro_c, dis_c, pro_m, dis_m, nm, row0, win);
+    else variation4_kernel<false><<<g, 256, 0, s>>>(pop, p0, p1, out, N, d, kx, km, lb, ub, pro_c, dis_c, pro_m, dis_m, nm, row0, win);
+  } else {
+    const int g = grid1((int64_t)N * d);
+    if (win) variation1_kernel<true><<<g, 256, 0, s>>>(pop, p0, p1, out, N, d, kx, km, lb, ub, pro_c, dis_c, pro_m, dis_m, nm, row0, win);
+    else variation1_kernel<false><<<g, 256, 0, s>>>(pop, p0, p1, out, N, d, kx, km, lb, ub, pro_c, dis_c, pro_m, dis_m, nm, row0, win);
+  }
 }
 
 void evx_moead_replace(const float* pop_obj, const float* off_obj, const float* W, const float* z, const float* zmax,

@@ -118,6 +118,12 @@ class MOEAD(Algorithm):
             neighbors=neighbors,
             z=torch.zeros(self.n_objs, device=dev),
             key=key,
+            # parents (p0, p1) and variation keys of the current offspring, and the last
+            # replacement's winner per slot (−1: kept): what the population-sharded tell needs
+            # to regenerate winning rows locally instead of moving them between GPUs
+            parents=torch.zeros((2, self.pop_size), dtype=torch.int32, device=dev),
+            var_keys=torch.zeros((2, 2), dtype=torch.int64, device=dev),
+            win=torch.full((self.pop_size,), -1, dtype=torch.int32, device=dev),
         )
 
     def init_ask(self, state):
@@ -139,29 +145,45 @@ class MOEAD(Algorithm):
                 and type(c) is crossover.SimulatedBinary and c.type == 2
                 and type(m) is mutation.Polynomial and m.boundary[0] is self.lb and m.boundary[1] is self.ub)
 
-    def ask(self, state):
-        key, sub, sel_key, mut_key = rnd.split(state.key, 4)
+    def _parent_pairs(self, state, key):
+        """(2, N) int32: the two parents of every offspring (first two entries of a random
+        permutation of its neighbour row)."""
         if self._fused(state.population):
             from ...ops import mo as mo_ops
 
-            p0, p1 = mo_ops.moead_parents(state.neighbors, sub)
-            c, m = self.crossover, self.mutation
-            off = mo_ops.moead_variation(state.population, p0, p1, sel_key, mut_key, self.lb, self.ub, c.pro_c, c.dis_c, m.pro_m, m.dis_m)
-            return off, state.update(next_generation=off, key=key)
-        parent = self._parents(state, sub)
+            p0, p1 = mo_ops.moead_parents(state.neighbors, key)
+            return torch.stack([p0, p1])
+        return self._parents(state, key).T.to(torch.int32).contiguous()
+
+    def _offspring_rows(self, state, parents, sel_key, mut_key, row0=0, rows=0, win=None):
+        """Offspring of ``parents`` (all, a row slice, or — with ``win`` — the winner of every
+        slot with ``population`` where there is none).  Counters are global offspring
+        indices, so every variant is bit-identical to the full generation."""
         pop = state.population
-        selected = torch.cat([pop[parent[:, 0]], pop[parent[:, 1]]], 0)
-        off = self.crossover(sel_key, selected)
-        off = self.mutation(mut_key, off)
-        off = torch.clamp(off, self.lb, self.ub)
-        return off, state.update(next_generation=off, key=key)
+        c, m = self.crossover, self.mutation
+        if self._fused(pop):
+            from ...ops import mo as mo_ops
+
+            return mo_ops.moead_variation(pop, parents[0].contiguous(), parents[1].contiguous(), sel_key, mut_key, self.lb, self.ub,
+                                          c.pro_c, c.dis_c, m.pro_m, m.dis_m, row0=row0, rows=rows, win=win)
+        p = parents.long()
+        off = torch.clamp(self.mutation(mut_key, self.crossover(sel_key, torch.cat([pop[p[0]], pop[p[1]]], 0))), self.lb, self.ub)
+        if win is not None:
+            return torch.where((win >= 0)[:, None], off[win.long().clamp_min(0)], pop)
+        return off[row0 : row0 + rows] if rows else off
+
+    def ask(self, state):
+        key, sub, sel_key, mut_key = rnd.split(state.key, 4)
+        parents = self._parent_pairs(state, sub)
+        off = self._offspring_rows(state, parents, sel_key, mut_key)
+        return off, state.update(next_generation=off, key=key, parents=parents, var_keys=torch.stack([sel_key, mut_key]))
 
     def _reverse(self, state):
         if self._rev is None or self._rev[0].device != state.neighbors.device or self._rev[1].shape[0] != state.neighbors.numel():
             self._rev = reverse_neighbors(state.neighbors)
         return self._rev
 
-    def tell(self, state, fitness):
+    def _replace(self, state, fitness):
         z = torch.minimum(state.z, fitness.min(0).values)
         z_max = state.fitness.max(0).values
         if fitness.is_cuda and state.population.dtype == torch.float32:
@@ -171,11 +193,64 @@ class MOEAD(Algorithm):
             if self._rev32 is None or self._rev32[0].data_ptr() != rowptr.data_ptr():
                 self._rev32 = (rowptr, rowptr.to(torch.int32), owner.to(torch.int32))
             win, new_obj = mo_ops.moead_replace(state.fitness, fitness, state.weight_vector, z, z_max, self._rev32[1], self._rev32[2], self.func_name)
+        else:
+            win, new_obj = moead_replace(state.fitness, fitness, state.weight_vector, z, z_max, self.aggregate_func, self._reverse(state))
+        return win.to(torch.int32), new_obj, z
+
+    def tell(self, state, fitness):
+        win, new_obj, z = self._replace(state, fitness)
+        if state.population.is_cuda and state.population.dtype == torch.float32:
+            from ...ops import mo as mo_ops
+
             new_pop = mo_ops.moead_select_rows(state.population, state.next_generation, win)
-            return state.update(population=new_pop, fitness=new_obj, z=z)
-        win, new_obj = moead_replace(state.fitness, fitness, state.weight_vector, z, z_max, self.aggregate_func, self._reverse(state))
-        new_pop = torch.where((win >= 0)[:, None], state.next_generation[win.clamp_min(0)], state.population)
-        return state.update(population=new_pop, fitness=new_obj, z=z)
+        else:
+            new_pop = torch.where((win >= 0)[:, None], state.next_generation[win.long().clamp_min(0)], state.population)
+        return state.update(population=new_pop, fitness=new_obj, z=z, win=win)
+
+    # ------------------------------------------------------------------ population-sharded SPMD
+    # Slots (weight vectors, Das–Dennis order = contiguous regions of the simplex) are split in
+    # balanced contiguous ranges; the population stays replicated.  A rank generates and
+    # evaluates only its own slots' offspring; the (N, m) objectives are all-gathered (196 KB
+    # at N = 16 290); the exact parallel replacement runs redundantly on every rank; each rank
+    # then REGENERATES the winning offspring rows from its replica (same parents, keys and
+    # counters) instead of receiving them — no d-length row crosses xGMI.
+    rank_local_fields = ("next_generation",)
+
+    def init_ask_sharded(self, state, dist):
+        start, size = dist.slice_of(self.pop_size)
+        return state.population[start : start + size], state
+
+    def init_tell_sharded(self, state, fitness, dist):
+        return self.init_tell(state, fitness)
+
+    def ask_sharded(self, state, dist):
+        key, sub, sel_key, mut_key = rnd.split(state.key, 4)
+        start, size = dist.slice_of(self.pop_size)
+        parents = self._parent_pairs(state, sub)
+        off = self._offspring_rows(state, parents, sel_key, mut_key, row0=start, rows=size)
+        return off, state.update(next_generation=off, key=key, parents=parents, var_keys=torch.stack([sel_key, mut_key]))
+
+    def tell_sharded(self, state, fitness, dist):
+        win, new_obj, z = self._replace(state, fitness)
+        new_pop = self._offspring_rows(state, state.parents, state.var_keys[0], state.var_keys[1], win=win)
+        return state.update(population=new_pop, fitness=new_obj, z=z, win=win)
+
+
+def cross_shard_winner_fraction(win: torch.Tensor, world: int):
+    """(winners / N, fraction of winners generated on another rank than the slot's owner):
+    the share of d-length rows a row-shipping design would move every generation."""
+    from ...parallel.context import balanced_slices
+
+    n = win.shape[0]
+    owner = torch.empty(n, dtype=torch.int64)
+    for r, (s, z) in enumerate(balanced_slices(n, world)):
+        owner[s : s + z] = r
+    w = win.cpu().long()
+    has = w >= 0
+    if not bool(has.any()):
+        return 0.0, 0.0
+    cross = owner[has] != owner[w[has]]
+    return float(has.float().mean()), float(cross.float().mean())
 
 
 def moead_replace_sequential(pop, pop_obj, off, off_obj, w, z, z_max, neighbors, agg):

@@ -35,6 +35,7 @@ from ....core import Algorithm, State
 from ....ops import random as rnd
 from ....ops.eigh import sbr_phase, symmetrize_upper, warm_eigh
 from ....runtime import host_phase
+from ....utils import profiling
 from .... import config
 from ....ops.linalg import Operand, gemm, plain_nt
 from ....ops.reduce import weighted_rowsum
@@ -180,12 +181,14 @@ class CMAES(Algorithm):
             np_ = jacobi.padded_size(d)
             C, Cp, _ = ops.cma_cov_pad(state.C.contiguous(), S.contiguous(), pc, a, float(self.c1), float(self.cmu), state.B.contiguous(), np_)
             # Cp[:d, :d] = triu(C) + triu(C, 1)ᵀ, the reference's symmetrisation (cma_es.py:193-195)
-            w, Bn, eig_stats = host_phase(sbr_phase, Cp[:d, :d], state.B, out_like=(state.D, state.B, state.eig_stats))
+            with profiling.phase("eigh"):
+                w, Bn, eig_stats = host_phase(sbr_phase, Cp[:d, :d], state.B, out_like=(state.D, state.B, state.eig_stats))
             B, D, BdivD = ops.cma_eig_out(Bn.contiguous(), w.contiguous(), d)
         else:
             np_ = jacobi.padded_size(d)
             C, Cp, Bp = ops.cma_cov_pad(state.C.contiguous(), S.contiguous(), pc, a, float(self.c1), float(self.cmu), state.B.contiguous(), np_)
-            w, Bp = jacobi.warm_eigh_padded(Cp, Bp, d, max_sweeps=self.eig_sweeps)
+            with profiling.phase("eigh"):
+                w, Bp = jacobi.warm_eigh_padded(Cp, Bp, d, max_sweeps=self.eig_sweeps)
             B, D, BdivD = ops.cma_eig_out(Bp, w, d)
         invsqrtC = plain_nt(BdivD, B) if config.get("plain_gemm") == "blas" else gemm(Operand(BdivD), Operand(B), d, d, d)
         return state.update(mean=mean, ps=ps, pc=pc, C=C, sigma=sigma.reshape(state.sigma.shape), B=B, D=D, invsqrtC=invsqrtC,
@@ -244,14 +247,20 @@ class CMAES(Algorithm):
     def tell_sharded(self, state, fitness, dist):
         """``fitness`` is the all-gathered (λ,) vector; ``state.population`` the local rows."""
         start, size = dist.slice_of(self.pop_size)
-        _, order = argsort(fitness)
-        # weight of every global row (0 outside the top μ), restricted to the local slice
+        if fitness.is_cuda:
+            _, order = argsort_i32(fitness.contiguous())
+            order = order.long()
+        else:
+            _, order = argsort(fitness)
+        # weight of every global row (0 outside the top μ), restricted to the local slice: the
+        # rank-μ partial sum runs over this rank's λ/N rows only (shapes fixed for hipGraphs)
         wfull = torch.zeros(self.pop_size, dtype=torch.float32, device=fitness.device)
         wfull.index_copy_(0, order[: self.mu], self.weights.to(fitness.device))
         wloc = wfull[start : start + size].contiguous()
         dm, S = self._weighted_stats(state, state.population, None, size, wloc, gather=False)
         buf = torch.cat([dm.reshape(-1), S.reshape(-1)])
-        dist.all_reduce_(buf)
+        with profiling.phase("all_reduce"):
+            dist.all_reduce_(buf)
         d = self.dim
         return self._finish_tell(state, buf[:d], buf[d:].reshape(d, d))
 

@@ -59,17 +59,22 @@ def moead_parents(neighbors: torch.Tensor, key: torch.Tensor):
     return _ext.ops().moead_parents(neighbors.to(torch.int64).contiguous(), key.contiguous())
 
 
-def moead_variation(pop, p0, p1, key_x, key_m, lb, ub, pro_c, dis_c, pro_m, dis_m):
+def moead_variation(pop, p0, p1, key_x, key_m, lb, ub, pro_c, dis_c, pro_m, dis_m, row0=0, rows=0, win=None):
     """clip(PM(SBX_type2(pop[p0], pop[p1]))) in one pass; ``key_x``/``key_m`` are the keys
-    ``SimulatedBinary`` / ``Polynomial`` would receive (bit-identical results)."""
+    ``SimulatedBinary`` / ``Polynomial`` would receive (bit-identical results).
+
+    ``rows > 0``: only offspring ``row0 .. row0+rows−1`` (a rank's slice); ``win``: output
+    row s is offspring ``win[s]`` regenerated from ``pop`` (``pop[s]`` where ``win[s] < 0``)
+    — the population-sharded MOEA/D's row update without moving offspring rows."""
     from . import random as rnd
 
     n, d = p0.numel(), pop.shape[1]
     nm = n if n == 1 else (n // 2) * 2
     lb = lb.to(device=pop.device, dtype=torch.float32).expand(d).contiguous()
     ub = ub.to(device=pop.device, dtype=torch.float32).expand(d).contiguous()
+    w = win.to(torch.int32).contiguous() if win is not None else None
     return _ext.ops().moead_variation(pop.contiguous(), p0, p1, rnd.split(key_x, 2).contiguous(), rnd.split(key_m, 2).contiguous(),
-                                      lb, ub, float(pro_c), float(dis_c), float(pro_m), float(dis_m), int(nm))
+                                      lb, ub, float(pro_c), float(dis_c), float(pro_m), float(dis_m), int(nm), int(row0), int(rows), w)
 
 
 def moead_replace(pop_obj, off_obj, w, z, z_max, rowptr, owner, func):

@@ -52,6 +52,19 @@ def trace_range(name: str, enabled: Optional[bool] = None):
             torch.cuda.nvtx.range_pop()
 
 
+_ACTIVE_TIMER = None
+
+
+def phase(name: str):
+    """Time ``name`` on the workflow's active :class:`PhaseTimer` (eager steps with a
+    ``phase_timer``); a no-op otherwise.  Lets algorithms expose inner phases (e.g. the
+    CMA-ES eigensolve inside ``tell``) in the same per-phase breakdown."""
+    t = _ACTIVE_TIMER
+    if t is None:
+        return contextlib.nullcontext()
+    return t.phase(name)
+
+
 class PhaseTimer:
     """Accumulate per-phase wall time without host synchronisation.
 

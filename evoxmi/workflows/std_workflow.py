@@ -211,8 +211,15 @@ class StdWorkflow(Workflow):
         return stack
 
     def _step_eager(self, state):
+        from ..utils import profiling
+
         is_init = self._has_init_ask and state.generation == 0
-        return self._proto_step(bool(is_init), state)
+        prev = profiling._ACTIVE_TIMER
+        profiling._ACTIVE_TIMER = self.phase_timer
+        try:
+            return self._proto_step(bool(is_init), state)
+        finally:
+            profiling._ACTIVE_TIMER = prev
 
     # ------------------------------------------------------------------ hipGraph path
     def _hooks_inside_step(self):

@@ -4,9 +4,15 @@
   moead : MOEA/D pop=16384 on LSMOP1 (m=3, d=10000), Tchebycheff aggregation
 
 python tools/bench_mo.py --algo nsga2|moead [--gens 20] [--warmup 3] [--no-graph]
+torchrun --nproc-per-node 8 --master-addr 127.0.0.1 tools/bench_mo.py --algo moead
 
-Prints one JSON line: generations/s and evaluations/s of full generations
-(ask → evaluate → tell), random-init populations, fp32.
+Prints one JSON line (rank 0): generations/s and evaluations/s of full generations
+(ask → evaluate → tell), random-init populations, fp32.  Under torchrun (or with
+--force-dist) the workflow is population-sharded: MOEA/D ranks own contiguous slot
+ranges, generate/evaluate only their offspring, all-gather the (N, m) objectives and
+regenerate winning rows locally; the line then also reports the cross-shard winner
+fraction (winning offspring generated on another rank than the slot's owner — the rows
+a row-shipping design would move over xGMI every generation).
 """
 import argparse
 import json
@@ -45,16 +51,27 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--force-dist", action="store_true", help="sharded protocol even on one rank")
     args = ap.parse_args()
-    dev = torch.device("cpu" if args.cpu else "cuda")
+    import torch.distributed as dist
+    from evoxmi.parallel import init_distributed
+
+    rank, world, dev = init_distributed(force=args.force_dist, backend="gloo" if args.cpu else None)
+    if args.cpu:
+        dev = torch.device("cpu")
     algo, prob = build(args, dev)
+    dist_on = world > 1 or args.force_dist
 
     def sync():
         if dev.type == "cuda":
             torch.cuda.synchronize()
+        if dist_on:
+            dist.barrier()
 
     wf = StdWorkflow(algo, prob, graph=not (args.no_graph or args.cpu))
     st = wf.init(rnd.PRNGKey(7, device=dev))
+    if dist_on:
+        st = wf.enable_distributed(st)
     for _ in range(1 + args.warmup):
         st = wf.step(st)
     sync()
@@ -62,14 +79,30 @@ def main():
     for _ in range(args.gens):
         st = wf.step(st)
     sync()
-    dt = (time.perf_counter() - t) / args.gens
-    fit = st.get_child_state("algorithm").fitness
+    dt = torch.tensor([(time.perf_counter() - t) / args.gens], dtype=torch.float64, device=dev)
+    if dist_on:
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    dt = float(dt)
+    a = st.get_child_state("algorithm")
+    fit = a.fitness
     pop = algo.pop_size
-    print(json.dumps({
-        "config": args.algo, "pop": pop, "dim": algo.dim, "n_objs": 3, "graph": not (args.no_graph or args.cpu),
+    out = {
+        "config": args.algo, "pop": pop, "dim": algo.dim, "n_objs": 3, "graph": not (args.no_graph or args.cpu), "n_gpus": world,
+        "parallelism": f"pop-shard{world}" if dist_on else "single",
         "ms_per_gen": round(dt * 1e3, 3), "gens_per_sec": round(1 / dt, 2), "evals_per_sec": round(pop / dt, 1),
         "fitness_finite": bool(torch.isfinite(fit).all()), "mean_obj": [round(float(v), 4) for v in fit.mean(0)],
-    }))
+    }
+    if args.algo == "moead":
+        from evoxmi.algorithms.mo.moead import cross_shard_winner_fraction
+
+        frac, cross = cross_shard_winner_fraction(a.win, max(world, 2) if not dist_on else world)
+        out["winner_fraction"] = round(frac, 4)
+        out["cross_shard_winner_fraction"] = round(cross, 4)
+        out["cross_shard_fraction_world"] = world if dist_on else 2
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist_on:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":
