@@ -25,12 +25,25 @@ void check_key(const at::Tensor& key) {
   TORCH_CHECK(key.scalar_type() == at::kLong && key.numel() == 2 && key.is_contiguous(), "key must be int64[2]");
 }
 
+// A key (2,) or a stack of per-run keys (B, 2) (BatchedRuns: evoxmi/ops/batching.py);
+// returns B (0 for a single key).
+int64_t key_batch(const at::Tensor& key, const char* op) {
+  CHECK_DEV(key);
+  TORCH_CHECK(key.scalar_type() == at::kLong && key.is_contiguous(), op, ": key must be contiguous int64");
+  if (key.dim() == 1) {
+    TORCH_CHECK(key.numel() == 2, op, ": key must be int64[2]");
+    return 0;
+  }
+  TORCH_CHECK(key.dim() == 2 && key.size(1) == 2 && key.size(0) >= 1 && key.size(0) <= 65535, op, ": keys must be (B, 2), B ≤ 65535");
+  return key.size(0);
+}
+
 at::Tensor philox_fill(const at::Tensor& key, int64_t n, int64_t dist, int64_t offset) {
-  check_key(key);
+  const int64_t B = key_batch(key, "philox_fill");
   TORCH_CHECK(offset % 4 == 0, "offset must be a multiple of 4");
   c10::DeviceGuard g(key.device());
-  auto out = at::empty({n}, key.options().dtype(at::kFloat));
-  if (n > 0) evx_philox_fill(out.data_ptr<float>(), n, key.data_ptr<int64_t>(), (int)dist, offset, cur_stream());
+  auto out = B ? at::empty({B, n}, key.options().dtype(at::kFloat)) : at::empty({n}, key.options().dtype(at::kFloat));
+  if (n > 0) evx_philox_fill(out.data_ptr<float>(), n, key.data_ptr<int64_t>(), (int)dist, offset, cur_stream(), B ? (int)B : 1);
   return out;
 }
 
@@ -130,13 +143,18 @@ at::Tensor gemm_f32(const at::Tensor& A, int64_t a_rc, const c10::optional<at::T
 }
 
 std::vector<at::Tensor> argsort_f32(const at::Tensor& keys, int64_t descending) {
+  // 1-D keys, or (B, n): B independent rows sorted by B workgroups of one launch
   CHECK_DEV(keys); CHECK_F32(keys); CHECK_CONTIG(keys);
-  const int64_t n = keys.numel();
+  TORCH_CHECK(keys.dim() <= 2, "argsort_f32: keys must be (n,) or (B, n)");
+  const int64_t B = keys.dim() == 2 ? keys.size(0) : 1;
+  const int64_t n = keys.dim() == 0 ? 1 : keys.size(-1);
   TORCH_CHECK(n <= evx_argsort_max_n(), "argsort_f32: n > ", evx_argsort_max_n());
+  TORCH_CHECK(B <= 65535, "argsort_f32: B > 65535");
   c10::DeviceGuard g(keys.device());
-  auto ok = at::empty({n}, keys.options());
-  auto oi = at::empty({n}, keys.options().dtype(at::kInt));
-  if (n > 0) evx_argsort(keys.data_ptr<float>(), (int)n, (int)descending, ok.data_ptr<float>(), oi.data_ptr<int32_t>(), cur_stream());
+  auto ok = at::empty_like(keys);
+  auto oi = at::empty(keys.sizes(), keys.options().dtype(at::kInt));
+  if (n > 0 && B > 0)
+    evx_argsort(keys.data_ptr<float>(), (int)n, (int)descending, ok.data_ptr<float>(), oi.data_ptr<int32_t>(), cur_stream(), (int)B);
   return {ok, oi};
 }
 
@@ -321,10 +339,11 @@ std::vector<at::Tensor> sbr_taylor_prep(const at::Tensor& X, const at::Tensor& X
 }
 
 at::Tensor philox_words(const at::Tensor& key, int64_t nblocks, int64_t domain, int64_t offset) {
-  check_key(key);
+  const int64_t B = key_batch(key, "philox_words");
   c10::DeviceGuard g(key.device());
-  auto out = at::empty({nblocks, 4}, key.options());
-  if (nblocks > 0) evx_philox_words(key.data_ptr<int64_t>(), nblocks, (uint32_t)domain, offset, out.data_ptr<int64_t>(), cur_stream());
+  auto out = B ? at::empty({B, nblocks, 4}, key.options()) : at::empty({nblocks, 4}, key.options());
+  if (nblocks > 0)
+    evx_philox_words(key.data_ptr<int64_t>(), nblocks, (uint32_t)domain, offset, out.data_ptr<int64_t>(), cur_stream(), B ? (int)B : 1);
   return out;
 }
 
@@ -412,8 +431,13 @@ at::Tensor de_trial(const at::Tensor& P, const at::Tensor& idx, const at::Tensor
                     const at::Tensor& ub, int64_t repair, const at::Tensor& err) {
   CHECK_DEV(P); CHECK_F32(P); CHECK_CONTIG(P);
   TORCH_CHECK(err.is_cuda() && err.scalar_type() == at::kInt && err.numel() >= 1, "de_trial: err must be int32[1] on the device");
-  TORCH_CHECK(P.dim() == 2, "de_trial: P must be (rows, d)");
-  const int64_t R = idx.size(0), K = idx.size(1), d = P.size(1);
+  // single run: P (rows, d), idx (R, K), key (2,); B batched runs: P (B, rows, d), idx (B, R, K),
+  // per-row tensors (B, R), keys (B, 2) — one launch, grid.y = run
+  const int64_t B = key_batch(key, "de_trial");
+  const int64_t Bn = B ? B : 1;
+  TORCH_CHECK(P.dim() == (B ? 3 : 2) && idx.dim() == P.dim() && (!B || (P.size(0) == B && idx.size(0) == B)),
+              "de_trial: P must be (rows, d) with idx (R, K), or (B, rows, d) with idx (B, R, K) and keys (B, 2)");
+  const int64_t R = idx.size(-2), K = idx.size(-1), d = P.size(-1), rows = P.size(-2);
   TORCH_CHECK(K >= 1 && K <= 16, "de_trial: 1 <= K <= 16");
   auto i32 = [&](const at::Tensor& t, int64_t n, const char* nm) {
     TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kInt && t.is_contiguous() && t.numel() == n, "de_trial: ", nm, " must be contiguous int32[", n, "]");
@@ -423,14 +447,14 @@ at::Tensor de_trial(const at::Tensor& P, const at::Tensor& idx, const at::Tensor
     TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == n, "de_trial: ", nm, " must be contiguous f32[", n, "]");
     return t.data_ptr<float>();
   };
-  TORCH_CHECK(key.scalar_type() == at::kLong && key.is_contiguous() && key.numel() == 2, "de_trial: key must be int64[2]");
   TORCH_CHECK(repair >= 0 && repair <= 2, "de_trial: repair in {0,1,2}");
   c10::DeviceGuard g(P.device());
-  auto out = at::empty({R, d}, P.options());
+  auto out = B ? at::empty({B, R, d}, P.options()) : at::empty({R, d}, P.options());
   if (R > 0 && d > 0)
-    evx_de_trial(P.data_ptr<float>(), i32(idx, R * K, "idx"), f32(coef, R * K, "coef"), (int)K, i32(cur, R, "cur"), i32(mode, R, "mode"),
-                 f32(CR, R, "CR"), i32(jr, R, "jr"), i32(L, R, "L"), key.data_ptr<int64_t>(), f32(lb, d, "lb"), f32(ub, d, "ub"), (int)repair,
-                 out.data_ptr<float>(), (int)R, (int)d, (int)P.size(0), err.data_ptr<int>(), cur_stream());
+    evx_de_trial(P.data_ptr<float>(), i32(idx, Bn * R * K, "idx"), f32(coef, Bn * R * K, "coef"), (int)K, i32(cur, Bn * R, "cur"),
+                 i32(mode, Bn * R, "mode"), f32(CR, Bn * R, "CR"), i32(jr, Bn * R, "jr"), i32(L, Bn * R, "L"), key.data_ptr<int64_t>(),
+                 f32(lb, d, "lb"), f32(ub, d, "ub"), (int)repair, out.data_ptr<float>(), (int)R, (int)d, (int)rows, err.data_ptr<int>(),
+                 cur_stream(), (int)Bn);
   return out;
 }
 

@@ -3,7 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-void evx_philox_fill(float* out, int64_t n, const int64_t* key, int dist, int64_t elem_offset, hipStream_t s);
+void evx_philox_fill(float* out, int64_t n, const int64_t* key, int dist, int64_t elem_offset, hipStream_t s, int batch = 1);
 void evx_classic_eval(const float* X, float* out, int N, int D, int func, float a, float b, float c, hipStream_t s);
 void evx_pso_update(const float* pop, const float* vel, const float* lbl, const float* lbf, const float* fit,
                     const float* gbl, const int64_t* kp, const int64_t* kg, float w, float phip, float phig,
@@ -26,7 +26,7 @@ void evx_gemm_f32(EvxOperand a, EvxOperand b, float* C, int64_t ldc, int M, int 
                   const float* alpha_ptr, const float* bias_n, float beta, const float* Cin, int64_t ldcin, hipStream_t s);
 int evx_gemm_splits_used(int K, int splits);
 int evx_argsort_max_n();
-void evx_argsort(const float* keys, int n, int descending, float* out_keys, int32_t* out_idx, hipStream_t s);
+void evx_argsort(const float* keys, int n, int descending, float* out_keys, int32_t* out_idx, hipStream_t s, int batch = 1);
 void evx_cec_basic(const float* Z, int64_t ld, int N, int fid, const int32_t* perm, int start, int L, const float* sub,
                    float scale, const float* Y, int64_t ldy, int ystart, int yperm, float* out, hipStream_t s);
 // outer round `round` of a sweep (0: within-block pairing, ≥1: circle-method rounds; the
@@ -46,7 +46,8 @@ void evx_jacobi_apply_solve(float* A, float* B, int np, const int* sched_t, cons
                             hipStream_t s);
 void evx_jacobi_check(const float* A, int np, double* part, int* flag, double tol2, double* last_off, hipStream_t s);
 int evx_jacobi_parts();
-void evx_philox_words(const int64_t* key, int64_t nblocks, uint32_t domain, int64_t offset, int64_t* out, hipStream_t s);
+void evx_philox_words(const int64_t* key, int64_t nblocks, uint32_t domain, int64_t offset, int64_t* out, hipStream_t s,
+                      int batch = 1);
 void evx_weighted_rowsum(const float* X, int64_t ldx, const int32_t* idx, const float* w, const float* sub, int K, int D,
                          float* partial, int chunks, hipStream_t s);
 void evx_gemm_set_config(int cfg);
@@ -56,7 +57,7 @@ void evx_pm(const float* x, float* out, int n, int d, int nm, const float* lb, c
 void evx_dtlz(const float* X, float* F, int N, int D, int M, int variant, hipStream_t s);
 void evx_de_trial(const float* P, const int32_t* idx, const float* coef, int K, const int32_t* cur, const int32_t* mode,
                   const float* CR, const int32_t* jr, const int32_t* L, const int64_t* key, const float* lb, const float* ub,
-                  int repair, float* out, int R, int d, int rows, int* err, hipStream_t s);
+                  int repair, float* out, int R, int d, int rows, int* err, hipStream_t s, int batch = 1);
 void evx_moead_scan(float* objs, const float* off_objs, const int32_t* P, const float* W, float* z, int32_t* owner, int N, int R,
                     int T, int M, int func, int nr, int update_z, hipStream_t s);
 void evx_ant_rollout(const float* W, int64_t P, int N, int h1, int h2, const float* init, int cap, float* ret, int* steps, hipStream_t s);

@@ -112,6 +112,14 @@ __global__ void __launch_bounds__(256) de_trial_kernel(const float* __restrict__
                                                        const int64_t* __restrict__ key, const float* __restrict__ lb,
                                                        const float* __restrict__ ub, int repair, float* __restrict__ out, int R,
                                                        int d, int rows, int* __restrict__ err) {
+  // batched runs: grid.y = run b; its R trial rows, P rows and key are run-local
+  const int64_t b = blockIdx.y;
+  P += b * rows * (int64_t)d;
+  idx += b * R * (int64_t)K;
+  coef += b * R * (int64_t)K;
+  cur += b * R; mode += b * R; CR += b * R; jr += b * R; L += b * R;
+  key += 2 * b;
+  out += b * R * (int64_t)d;
   const uint32_t k0 = (uint32_t)key[0], k1 = (uint32_t)key[1];
   const int64_t total = (int64_t)R * d;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
@@ -167,8 +175,8 @@ void evx_pm(const float* x, float* out, int n, int d, int nm, const float* lb, c
 
 void evx_de_trial(const float* P, const int32_t* idx, const float* coef, int K, const int32_t* cur, const int32_t* mode,
                   const float* CR, const int32_t* jr, const int32_t* L, const int64_t* key, const float* lb, const float* ub,
-                  int repair, float* out, int R, int d, int rows, int* err, hipStream_t s) {
+                  int repair, float* out, int R, int d, int rows, int* err, hipStream_t s, int batch) {
   const int64_t total = (int64_t)R * d;
-  const int grid = (int)std::min<int64_t>((total + 255) / 256, 8192);
+  const dim3 grid((int)std::min<int64_t>((total + 255) / 256, 8192), batch);
   de_trial_kernel<<<grid, 256, 0, s>>>(P, idx, coef, K, cur, mode, CR, jr, L, key, lb, ub, repair, out, R, d, rows, err);
 }

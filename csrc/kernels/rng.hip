@@ -9,6 +9,9 @@ namespace {
 template <int DIST>
 __global__ void __launch_bounds__(256) philox_fill_kernel(float* __restrict__ out, int64_t n,
                                                           const int64_t* __restrict__ key, int64_t block_offset) {
+  // batched runs (BatchedRuns): grid.y indexes the key / output row
+  key += 2 * (int64_t)blockIdx.y;
+  out += n * (int64_t)blockIdx.y;
   uint32_t k0, k1;
   evx::load_key(key, k0, k1);
   const int64_t nb = (n + 3) >> 2;
@@ -32,11 +35,12 @@ __global__ void __launch_bounds__(256) philox_fill_kernel(float* __restrict__ ou
 
 }  // namespace
 
-void evx_philox_fill(float* out, int64_t n, const int64_t* key, int dist, int64_t elem_offset, hipStream_t s) {
+void evx_philox_fill(float* out, int64_t n, const int64_t* key, int dist, int64_t elem_offset, hipStream_t s, int batch) {
   const int64_t nb = (n + 3) >> 2;
-  int grid = (int)((nb + 255) / 256);
-  if (grid > 4096) grid = 4096;
-  if (grid < 1) grid = 1;
+  int gx = (int)((nb + 255) / 256);
+  if (gx > 4096) gx = 4096;
+  if (gx < 1) gx = 1;
+  const dim3 grid(gx, batch);
   if (dist == 0)
     philox_fill_kernel<0><<<grid, 256, 0, s>>>(out, n, key, elem_offset >> 2);
   else
@@ -49,6 +53,8 @@ void evx_philox_fill(float* out, int64_t n, const int64_t* key, int dist, int64_
 namespace {
 __global__ void philox_words_kernel(const int64_t* __restrict__ key, int64_t nblocks, uint32_t domain, int64_t offset,
                                     int64_t* __restrict__ out) {
+  key += 2 * (int64_t)blockIdx.y;
+  out += 4 * nblocks * (int64_t)blockIdx.y;
   uint32_t k0, k1;
   evx::load_key(key, k0, k1);
   for (int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; b < nblocks; b += (int64_t)gridDim.x * blockDim.x) {
@@ -62,9 +68,11 @@ __global__ void philox_words_kernel(const int64_t* __restrict__ key, int64_t nbl
 }
 }  // namespace
 
-void evx_philox_words(const int64_t* key, int64_t nblocks, uint32_t domain, int64_t offset, int64_t* out, hipStream_t s) {
-  int grid = (int)((nblocks + 255) / 256);
-  if (grid > 1024) grid = 1024;
-  if (grid < 1) grid = 1;
+void evx_philox_words(const int64_t* key, int64_t nblocks, uint32_t domain, int64_t offset, int64_t* out, hipStream_t s,
+                      int batch) {
+  int gx = (int)((nblocks + 255) / 256);
+  if (gx > 1024) gx = 1024;
+  if (gx < 1) gx = 1;
+  const dim3 grid(gx, batch);
   philox_words_kernel<<<grid, 256, 0, s>>>(key, nblocks, domain, offset, out);
 }

@@ -47,6 +47,10 @@ __device__ __forceinline__ void reg_stages(Run<E>& R, int k, int e0) {
 template <int LOGN>
 __global__ void __launch_bounds__(1024) bitonic_argsort_kernel(const float* __restrict__ keys, int n, int descending,
                                                                float* __restrict__ out_keys, int32_t* __restrict__ out_idx) {
+  // one workgroup per row (batched runs sort their rows in one launch)
+  keys += (int64_t)blockIdx.x * n;
+  out_idx += (int64_t)blockIdx.x * n;
+  if (out_keys) out_keys += (int64_t)blockIdx.x * n;
   constexpr int NP = 1 << LOGN;
   constexpr int T = 1024;
   constexpr int E = NP / T;  // 1..16
@@ -120,14 +124,14 @@ __global__ void __launch_bounds__(1024) bitonic_argsort_kernel(const float* __re
 
 int evx_argsort_max_n() { return 16384; }
 
-void evx_argsort(const float* keys, int n, int descending, float* out_keys, int32_t* out_idx, hipStream_t s) {
+void evx_argsort(const float* keys, int n, int descending, float* out_keys, int32_t* out_idx, hipStream_t s, int batch) {
   int logn = 10;
   while ((1 << logn) < n) ++logn;
   switch (logn) {
-    case 10: bitonic_argsort_kernel<10><<<1, 1024, 0, s>>>(keys, n, descending, out_keys, out_idx); break;
-    case 11: bitonic_argsort_kernel<11><<<1, 1024, 0, s>>>(keys, n, descending, out_keys, out_idx); break;
-    case 12: bitonic_argsort_kernel<12><<<1, 1024, 0, s>>>(keys, n, descending, out_keys, out_idx); break;
-    case 13: bitonic_argsort_kernel<13><<<1, 1024, 0, s>>>(keys, n, descending, out_keys, out_idx); break;
-    default: bitonic_argsort_kernel<14><<<1, 1024, 0, s>>>(keys, n, descending, out_keys, out_idx); break;
+    case 10: bitonic_argsort_kernel<10><<<batch, 1024, 0, s>>>(keys, n, descending, out_keys, out_idx); break;
+    case 11: bitonic_argsort_kernel<11><<<batch, 1024, 0, s>>>(keys, n, descending, out_keys, out_idx); break;
+    case 12: bitonic_argsort_kernel<12><<<batch, 1024, 0, s>>>(keys, n, descending, out_keys, out_idx); break;
+    case 13: bitonic_argsort_kernel<13><<<batch, 1024, 0, s>>>(keys, n, descending, out_keys, out_idx); break;
+    default: bitonic_argsort_kernel<14><<<batch, 1024, 0, s>>>(keys, n, descending, out_keys, out_idx); break;
   }
 }

@@ -202,15 +202,16 @@ def generate_trials(key, population, fitness, best_index, cur, strategy, F, CR, 
     # archive path indexes the moved P ∪ A matrix, reference differential_evolution.py:139-141)
     base_idx = torch.stack([choices[:, 0], best + off, pb + off, cur + off], 1)
     idx = torch.cat([base_idx, choices[:, 1:]], 1)
-    coef = torch.zeros((R, idx.shape[1]), dtype=torch.float32, device=dev)
     prim, sec, nd, cross = strat[:, 0], strat[:, 1], strat[:, 2], strat[:, 3]
     Fs = F if Fw is None else F * _t(Fw, dev)
-    coef.scatter_add_(1, prim[:, None], (1 - Fs)[:, None])
-    coef.scatter_add_(1, sec[:, None], Fs[:, None])
+    # out-of-place (one-hot sums, concatenation) so the same code runs under torch.func.vmap
+    # (BatchedRuns: independent runs as one launch sequence)
+    c4 = torch.arange(4, device=dev)[None, :]
+    base_coef = (c4 == prim[:, None]).to(torch.float32) * (1 - Fs)[:, None] + (c4 == sec[:, None]).to(torch.float32) * Fs[:, None]
     j = torch.arange(1, P, device=dev)[None, :]
     keep = (j < 2 * nd[:, None] + 1).to(torch.float32)
     sign = torch.where(j % 2 == 1, 1.0, -1.0)
-    coef[:, 4:] = F[:, None] * keep * sign
+    coef = torch.cat([base_coef, F[:, None] * keep * sign], 1)
     jr = rnd.randint(k_jr, (R,), 0, d).to(dev)
     # exponential crossover: window length min(Geometric(CR), d) − 1 from a random start
     u = rnd.uniform(k_exp, (R,)).to(dev)
@@ -227,10 +228,8 @@ def greedy_replace(population, fitness, trials, trial_fitness, cur=None, strict=
         return torch.where(better[:, None], trials, population), torch.where(better, trial_fitness, fitness), better
     old_f = fitness[cur]
     better = trial_fitness < old_f if strict else trial_fitness <= old_f
-    pop = population.clone()
-    fit = fitness.clone()
-    pop[cur] = torch.where(better[:, None], trials, population[cur])
-    fit[cur] = torch.where(better, trial_fitness, old_f)
+    pop = population.index_copy(0, cur, torch.where(better[:, None], trials, population[cur]))
+    fit = fitness.index_copy(0, cur, torch.where(better, trial_fitness, old_f))
     return pop, fit, better
 
 
@@ -269,8 +268,7 @@ def move_n_small(a: torch.Tensor, n: IntLike):
     a stable partition putting the ``n`` smallest entries (first in stable sort order)
     in front, keeping the original relative order on both sides.  Returns the indices."""
     N = a.shape[0]
-    rank = torch.empty(N, dtype=torch.int64, device=a.device)
-    rank[torch.argsort(a, stable=True)] = torch.arange(N, device=a.device)
+    rank = torch.argsort(torch.argsort(a, stable=True), stable=True)  # inverse permutation, out of place
     small = rank < _t(n, a.device, torch.int64)
     key = (~small).to(torch.int64) * N + torch.arange(N, device=a.device)
     return torch.argsort(key)

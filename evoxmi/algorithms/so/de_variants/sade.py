@@ -69,8 +69,8 @@ class SaDE(Algorithm):
     def tell(self, state, trial_fitness):
         pop, fit, ok = C.greedy_replace(state.population, state.fitness, state.trial_vectors, trial_fitness, strict=False)
         sid = state.strategy_ids
-        succ = torch.zeros(4, dtype=torch.int64, device=sid.device).scatter_add_(0, sid, ok.to(torch.int64))
-        fail = torch.zeros(4, dtype=torch.int64, device=sid.device).scatter_add_(0, sid, (~ok).to(torch.int64))
+        succ = torch.zeros(4, dtype=torch.int64, device=sid.device).scatter_add(0, sid, ok.to(torch.int64))
+        fail = torch.zeros(4, dtype=torch.int64, device=sid.device).scatter_add(0, sid, (~ok).to(torch.int64))
         sm = torch.cat([succ[None], state.success_memory[:-1]], 0)
         fm = torch.cat([fail[None], state.failure_memory[:-1]], 0)
         return state.update(population=pop, fitness=fit, best_index=torch.argmin(fit), success_memory=sm, failure_memory=fm,

@@ -36,4 +36,7 @@ def algorithm_has_init_ask(algorithm: Algorithm, state: State = None) -> bool:
     the class hierarchy instead, which gives the same answer for every algorithm
     that follows the base-class contract (``init_ask`` returning ``None`` = absent).
     """
+    wraps = getattr(algorithm, "wraps_init_ask", None)  # containers answer for the wrapped algorithm
+    if wraps is not None:
+        return bool(wraps())
     return type(algorithm).init_ask is not Algorithm.init_ask

@@ -49,7 +49,7 @@ def topk(x: torch.Tensor, k: int, dim: int = -1, largest: bool = True):
         for _ in range(k):
             j = torch.argmax(work, dim=-1, keepdim=True)
             idx.append(j)
-            work.scatter_(-1, j, fill)
+            work = work.scatter(-1, j, fill)  # out of place: also runs under vmap
         ind = torch.cat(idx, -1)
     else:
         ind = torch.argsort(x, dim=-1, descending=largest, stable=True)[..., :k]

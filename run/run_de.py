@@ -15,6 +15,13 @@ independent runs at once, each on its own HIP stream (a pop-100, d-20 generation
 occupies a handful of CUs, so K graphs replayed on K streams overlap on the 256 CUs);
 every run still gets its own ``--max-time`` wall-clock budget.
 
+``--batched`` runs ALL ``--runs`` independent runs as one vmapped computation
+(:class:`evoxmi.algorithms.BatchedRuns`): one (runs·pop, d) evaluation and one launch
+sequence (one hipGraph replay) per generation advance every run, sharing the wall-clock
+budget.  Run ``r`` uses the same per-run key in both modes (``split(fold_in(key_f, 1),
+runs)[r]``), so with ``--progress steps`` (progress = step / --max-steps, no clock)
+the batched and sequential harnesses compute the same runs.
+
 Example: ``python run/run_de.py --algo LSHADE --dim 20 --pop 100 --runs 4 --max-time 5``
 """
 from __future__ import annotations
@@ -67,6 +74,10 @@ def main(argv=None):
     ap.add_argument("--device", default="cuda" if torch.cuda.is_available() else "cpu")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--concurrent", type=int, default=1, help="independent runs executed at once on separate HIP streams")
+    ap.add_argument("--batched", action="store_true", help="all runs as one vmapped computation (BatchedRuns)")
+    ap.add_argument("--progress", choices=("time", "steps"), default="time",
+                    help="progress injected into the state: elapsed/--max-time (reference) or step/--max-steps")
+    ap.add_argument("--json", default=None, help="write a per-function summary (aggregate gens/s, best values)")
     args = ap.parse_args(argv)
 
     a, _, b = args.funcs.partition("-")
@@ -82,6 +93,7 @@ def main(argv=None):
         with open(pth, "w") as f:
             f.write(header)
     key = rnd.PRNGKey(args.seed, device=dev)
+    summary = {}
     for fn in funcs:
         problem = CEC2022TestSuit.create(fn)
         name = type(problem).__name__
@@ -93,6 +105,19 @@ def main(argv=None):
         best_all, hist_all = [], []
         steps = 0
         K = max(1, args.concurrent)
+        fkey = rnd.fold_in(key, fn)
+        run_keys = rnd.split(rnd.fold_in(fkey, 1), args.runs)
+        if args.batched:
+            best_all, hist_all, steps, gps = _run_batched(args, problem, lb, ub, fkey, graph, dev)
+            summary[name] = {"gens_per_s_aggregate": gps, "steps": steps, "best": best_all}
+            with open(res_path, "a") as f:
+                f.write(" ".join(str(b) for b in best_all) + f" {steps * args.pop}\n")
+            order = sorted(range(len(best_all)), key=lambda k: best_all[k])
+            with open(hist_path, "a") as f:
+                f.write(f"{hist_all[order[len(order) // 2]]}\n")
+            continue
+        t_fn = time.time()
+        gens_total = 0
         for run0 in range(0, args.runs, K):
             batch = list(range(run0, min(args.runs, run0 + K)))
             jobs = []
@@ -100,9 +125,9 @@ def main(argv=None):
                 algo = getattr(de_variants, args.algo)(lb=lb, ub=ub, pop_size=args.pop)
                 mon = EvalMonitor(full_fit_history=False)
                 wf = StdWorkflow(algo, problem, monitors=[mon], graph=graph)
-                key, sub = rnd.split(key)
+                st0 = _with_algorithm_key(wf.init(fkey), algo, run_keys[run])
                 stream = torch.cuda.Stream(device=dev) if dev.type == "cuda" and K > 1 else None
-                jobs.append({"run": run, "wf": wf, "mon": mon, "state": wf.init(sub), "hist": [], "stream": stream, "steps": 0, "done": False})
+                jobs.append({"run": run, "wf": wf, "mon": mon, "state": st0, "hist": [], "stream": stream, "steps": 0, "done": False})
             t0 = time.time()
             for i in range(args.max_steps):
                 active = [j for j in jobs if not j["done"]]
@@ -118,18 +143,19 @@ def main(argv=None):
                         alg = state.get_child_state("algorithm")
                         upd = {}
                         if "progress" in alg.keys():
-                            upd["progress"] = elapsed / args.max_time
+                            upd["progress"] = elapsed / args.max_time if args.progress == "time" else (i + 1) / args.max_steps
                         if "iter" in alg.keys() and not isinstance(alg.iter, torch.Tensor):
                             upd["iter"] = i
                         if upd:
                             state = state.update_child("algorithm", alg.update(**upd))
                         j["state"] = state
-                        if elapsed >= args.max_time:
+                        if elapsed >= args.max_time or (args.progress == "steps" and i + 1 >= args.max_steps):
                             j["done"] = True
             if dev.type == "cuda":
                 torch.cuda.synchronize()
             for j in jobs:
                 run, steps = j["run"], j["steps"]
+                gens_total += steps + 1
                 best = float(j["mon"].get_best_fitness())
                 j["hist"].append(best)
                 print(f"min fitness: {best}\nSteps: {steps} Runs: {run}\nTime: {time.time() - t0:.3f} s\n", flush=True)
@@ -140,10 +166,67 @@ def main(argv=None):
                         f.write(f"{best} ")
         with open(res_path, "a") as f:
             f.write(f"{steps * args.pop}\n")
+        summary[name] = {"gens_per_s_aggregate": gens_total / (time.time() - t_fn), "steps": steps, "best": best_all}
         order = sorted(range(len(best_all)), key=lambda k: best_all[k])
         med = order[len(order) // 2]
         with open(hist_path, "a") as f:
             f.write(f"{hist_all[med]}\n")
+    if args.json:
+        import json
+
+        with open(args.json, "w") as f:
+            json.dump({"algo": args.algo, "dim": D, "pop": args.pop, "runs": args.runs, "batched": args.batched,
+                       "functions": summary}, f)
+    return summary
+
+
+def _with_algorithm_key(state, algo, key):
+    """Re-initialise the algorithm's sub-state from ``key`` (keeping its node id)."""
+    st, _ = algo._recursive_init(key, algo._node_id, algo._module_name, False)
+    return state.update_child("algorithm", st)
+
+
+def _run_batched(args, problem, lb, ub, fkey, graph, dev):
+    """All runs of one function as one vmapped computation; returns (best of runs
+    2..R (all if R == 1), sampled median history, steps, aggregate generations/s)."""
+    from evoxmi import random as rnd
+    from evoxmi.algorithms import de_variants
+    from evoxmi.algorithms.containers.batched import BatchedRuns
+    from evoxmi.workflows import StdWorkflow
+
+    algo = BatchedRuns(getattr(de_variants, args.algo)(lb=lb, ub=ub, pop_size=args.pop), args.runs)
+    wf = StdWorkflow(algo, problem, graph=graph)
+    # the runs' keys are split(fold_in(fkey, 1), R) exactly as in the sequential harness
+    state = _with_algorithm_key(wf.init(fkey), algo, rnd.fold_in(fkey, 1))
+    has_progress = "progress" in state.get_child_state("algorithm").runs.keys()
+    hist = []
+    t0 = time.time()
+    i = 0
+    while i < args.max_steps:
+        state = wf.step(state)
+        elapsed = time.time() - t0
+        alg = state.get_child_state("algorithm")
+        if i % args.sync_every == 0:
+            hist.append(algo.best_fitness(alg).tolist())
+        if has_progress:
+            prog = elapsed / args.max_time if args.progress == "time" else (i + 1) / args.max_steps
+            state = state.update_child("algorithm", algo.set_field(alg, progress=prog))
+        i += 1
+        if elapsed >= args.max_time:
+            break
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    dt = time.time() - t0
+    best = algo.best_fitness(state.get_child_state("algorithm")).tolist()
+    hist.append(best)
+    keep = list(range(1, args.runs)) if args.runs > 1 else [0]
+    steps = i - 1
+    print(f"batched {args.runs} runs: {i} generations in {dt:.3f} s "
+          f"({i * args.runs / dt:.0f} aggregate gens/s); best {min(best)}", flush=True)
+    bests = [best[r] for r in keep]
+    order = sorted(keep, key=lambda r: best[r])
+    med = order[len(order) // 2]
+    return bests, sample_history(args.samples, [h[med] for h in hist]), steps, i * args.runs / dt
 
 
 if __name__ == "__main__":
