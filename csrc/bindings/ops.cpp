@@ -328,13 +328,34 @@ std::vector<at::Tensor> sbr_symstats(const at::Tensor& T) {
   return {A, out};
 }
 
-std::vector<at::Tensor> sbr_taylor_prep(const at::Tensor& X, const at::Tensor& X2, const at::Tensor& X3) {
+// in-place variant for the solver's static workspace (no copies inside its captured graphs)
+void sbr_symstats_out(const at::Tensor& T, at::Tensor& A, at::Tensor& st) {
+  check_rowmajor(T, "T");
+  const int64_t n = T.size(0);
+  TORCH_CHECK(T.size(1) == n, "T must be square");
+  CHECK_DEV(A); CHECK_F32(A); CHECK_CONTIG(A);
+  TORCH_CHECK(A.size(0) == n && A.size(1) == n && A.data_ptr() != T.data_ptr(), "sbr_symstats_out: A must be a separate n×n buffer");
+  TORCH_CHECK(st.is_cuda() && st.scalar_type() == at::kDouble && st.is_contiguous() && st.numel() == 4, "sbr_symstats_out: st must be float64[4]");
+  c10::DeviceGuard g(T.device());
+  auto part = at::empty({4 * (int64_t)evx_sbr_symstats_parts((int)n)}, T.options().dtype(at::kDouble));
+  evx_sbr_symstats(T.data_ptr<float>(), (int)n, T.stride(0), A.data_ptr<float>(), n, part.data_ptr<double>(), st.data_ptr<double>(), cur_stream());
+}
+
+std::vector<at::Tensor> sbr_taylor_prep(const at::Tensor& X, const at::Tensor& X2, const at::Tensor& X3,
+                                        const c10::optional<at::Tensor>& alpha) {
   for (auto* t : {&X, &X2, &X3}) { CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t); }
   const int64_t n = X.size(0);
   TORCH_CHECK(X.dim() == 2 && X.size(1) == n && X2.sizes() == X.sizes() && X3.sizes() == X.sizes(), "sbr_taylor_prep: n×n");
+  const float* ap = nullptr;
+  if (alpha.has_value() && alpha->defined()) {
+    CHECK_DEV(*alpha); CHECK_F32(*alpha);
+    TORCH_CHECK(alpha->numel() == 1, "sbr_taylor_prep: alpha must be a 1-element device tensor");
+    ap = alpha->data_ptr<float>();
+  }
   c10::DeviceGuard g(X.device());
   auto P = at::empty_like(X), M = at::empty_like(X);
-  evx_sbr_taylor_prep(X.data_ptr<float>(), X2.data_ptr<float>(), X3.data_ptr<float>(), (int)n, P.data_ptr<float>(), M.data_ptr<float>(), cur_stream());
+  evx_sbr_taylor_prep(X.data_ptr<float>(), X2.data_ptr<float>(), X3.data_ptr<float>(), (int)n, ap, P.data_ptr<float>(), M.data_ptr<float>(),
+                      cur_stream());
   return {P, M};
 }
 
@@ -695,7 +716,8 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("sbr_far(Tensor A, int off, Tensor perm, Tensor Q, Tensor dq, Tensor stats, float thr_fac) -> Tensor");
   m.def("sbr_bq(Tensor B, int off, Tensor perm, Tensor Q) -> Tensor");
   m.def("sbr_symstats(Tensor T) -> Tensor[]");
-  m.def("sbr_taylor_prep(Tensor X, Tensor X2, Tensor X3) -> Tensor[]");
+  m.def("sbr_symstats_out(Tensor T, Tensor(a!) A, Tensor(b!) st) -> ()");
+  m.def("sbr_taylor_prep(Tensor X, Tensor X2, Tensor X3, Tensor? alpha=None) -> Tensor[]");
   m.def("pso_update(Tensor pop, Tensor vel, Tensor lbl, Tensor lbf, Tensor fit, Tensor gbl, Tensor kp, Tensor kg, float w, float phip, float phig, Tensor lb, Tensor ub) -> Tensor[]");
 }
 
@@ -735,6 +757,7 @@ TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
   m.impl("sbr_block", &sbr_block);
   m.impl("sbr_far", &sbr_far);
   m.impl("sbr_bq", &sbr_bq);
+  m.impl("sbr_symstats_out", &sbr_symstats_out);
   m.impl("sbr_symstats", &sbr_symstats);
   m.impl("sbr_taylor_prep", &sbr_taylor_prep);
 }

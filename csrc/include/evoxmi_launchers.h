@@ -102,4 +102,5 @@ void evx_sbr_bq(const float* B, int rows, int n, int64_t ldb, int off, const int
                 hipStream_t s);
 int evx_sbr_symstats_parts(int n);
 void evx_sbr_symstats(const float* T, int n, int64_t ldt, float* A, int64_t lda, double* part, double* out, hipStream_t s);
-void evx_sbr_taylor_prep(const float* X, const float* X2, const float* X3, int n, float* P, float* M, hipStream_t s);
+void evx_sbr_taylor_prep(const float* X, const float* X2, const float* X3, int n, const float* alpha, float* P, float* M,
+                         hipStream_t s);

@@ -158,14 +158,17 @@ __global__ void __launch_bounds__(256) sbr_symstats_kernel(const float* __restri
   }
 }
 
-// Taylor terms of exp(X): P = X/24 + X²/120 + X³/720, M = I + X + X²/2 + X³/6 (one pass)
+// Taylor terms of exp(αX) (α: damping factor on the device, 1 if null):
+// P = α³(Y/24 + Y²/120 + Y³/720), M = I + Y + Y²/2 + Y³/6 with Y = αX, so that
+// exp(αX) ≈ M + X³·P (one pass; X³·P carries the α³ of Y³)
 __global__ void __launch_bounds__(256) sbr_taylor_prep_kernel(const float* __restrict__ X, const float* __restrict__ X2,
-                                                              const float* __restrict__ X3, int n, float* __restrict__ P,
-                                                              float* __restrict__ M) {
+                                                              const float* __restrict__ X3, int n, const float* __restrict__ alpha,
+                                                              float* __restrict__ P, float* __restrict__ M) {
+  const float a = alpha ? alpha[0] : 1.f, a2 = a * a, a3 = a2 * a;
   const int64_t total = (int64_t)n * n;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    const float x = X[e], x2 = X2[e], x3 = X3[e];
-    P[e] = x * (1.f / 24.f) + x2 * (1.f / 120.f) + x3 * (1.f / 720.f);
+    const float x = a * X[e], x2 = a2 * X2[e], x3 = a3 * X3[e];
+    P[e] = a3 * (x * (1.f / 24.f) + x2 * (1.f / 120.f) + x3 * (1.f / 720.f));
     const int64_t i = e / n, j = e - i * n;
     M[e] = (i == j ? 1.f : 0.f) + x + 0.5f * x2 + x3 * (1.f / 6.f);
   }
@@ -371,6 +374,173 @@ __global__ void __launch_bounds__(1024) sbr_block_kernel(const float* __restrict
   if (tid < m) dq_out[s + tid] = Sc[tid * LP + tid];
 }
 
+// Jacobi rotation (c, s, t) annihilating the (p, q) entry of [[app, apq], [apq, aqq]]
+__device__ __forceinline__ float3 jacobi_rot(float app, float aqq, float apq) {
+  // rotate only on a normal-range coupling: a denormal apq would make the reciprocal overflow.
+  // Branch-free: for |θ| ≳ 1e19, θ² = inf gives t = 0 (the exact t ≈ 1/(2θ) < 1e-19).
+  const bool rot_on = fabsf(apq) >= FLT_MIN;
+  const float theta = (aqq - app) * (0.5f * __builtin_amdgcn_rcpf(rot_on ? apq : 1.f));
+  const float at = fabsf(theta);
+  float t = copysignf(__builtin_amdgcn_rcpf(at + __builtin_amdgcn_sqrtf(fmaf(theta, theta, 1.f))), theta);
+  t = rot_on ? t : 0.f;
+  const float c = __builtin_amdgcn_rsqf(fmaf(t, t, 1.f));
+  return make_float3(c, t * c, t);
+}
+
+// Version 2 of the block solve: double-buffered S, one barrier per round, Q in registers.
+//
+// 528 "S threads" (9 waves): thread {u ≤ v} owns the 2×2 blocks {p_u, q_u}×{p_v, q_v} of
+// S' = Jᵀ S J and their transposes (written as the exact transpose: S stays symmetric).  It
+// recomputes the rotations of pairs u and v itself from the round's input buffer (pure
+// functions of S: every thread gets bit-identical values) — no separate parameter phase,
+// no second barrier.  The pair-u diagonal block is set exactly.
+//
+// One "Q wave" accumulates Q' = Q J with lane k = row k of Q in 64 registers: column
+// pairs of a circle-method round sit at fixed register slots when the 63 rotating slots
+// shift by one per round (slot s holds column (s + r) mod 63, slot 63 column 63), so
+// every index is static.  The S threads publish (c, σ·s) per pair (σ: orientation of the
+// pair in slot order) and the Q wave applies round g after the barrier that ends it,
+// concurrently with the S threads' round g + 1.  63·sweeps rounds return the slots to
+// the identity mapping; the wave shifts its register file once per 7 rounds (static
+// indices in between).
+constexpr int kPairItems = (BK / 2) * (BK / 2 + 1) / 2;  // 528 unordered pairs {u ≤ v}
+constexpr int kSThreads = 576;                             // 9 waves
+// PROBE (tools/probe_sbr_block.py): bit 1 skips the Q work, bit 2 the S block updates, bit 4
+// reuses pair u's rotation for pair v (cost of the per-thread rotation recomputation)
+template <int PROBE>
+__global__ void __launch_bounds__(kSThreads + 64) sbr_block2_kernel(const float* __restrict__ A, int n, int64_t lda, int off,
+                                                                   int sweeps, int* __restrict__ perm_out, float* __restrict__ Q_out,
+                                                                   float* __restrict__ dq_out) {
+  __shared__ float Sb[2][BK * LP];
+  __shared__ __attribute__((aligned(16))) float2 rq[2][BK / 2];
+  __shared__ float key[kMaxN];
+  __shared__ int idx[kMaxN];
+  __shared__ int members[BK];
+  int P = 1;
+  while (P < n) P <<= 1;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < P; i += blockDim.x) {
+    key[i] = i < n ? A[(int64_t)i * lda + i] : FLT_MAX;
+    idx[i] = i;
+  }
+  __syncthreads();
+  lds_bitonic(key, idx, P);
+  int s0, e0;
+  block_range(blockIdx.x, off, n, s0, e0);
+  const int m = e0 - s0;
+  if (tid < BK) {
+    members[tid] = tid < m ? idx[s0 + tid] : -1;
+    if (tid < m) perm_out[s0 + tid] = idx[s0 + tid];
+  }
+  __syncthreads();
+  for (int i = tid; i < BK * BK; i += blockDim.x) {
+    const int a = i >> 6, c = i & 63;
+    const int ra = members[a], rc = members[c];
+    Sb[0][a * LP + c] = (ra >= 0 && rc >= 0) ? A[(int64_t)ra * lda + rc] : 0.f;
+  }
+  __syncthreads();
+  const int G = (BK - 1) * sweeps;
+  if (tid < kSThreads) {
+    // thread ↔ unordered pair-of-pairs {u ≤ v} (528 of them): it owns the 2×2 blocks
+    // (u, v) and (v, u) = (u, v)ᵀ, so it needs only the two rotations u and v
+    const bool active = tid < kPairItems;
+    int u = 0, rem = active ? tid : 0;  // inactive threads (528…575) map to item 0, never store
+    while (u < BK / 2 - 1 && rem >= BK / 2 - u) {
+      rem -= BK / 2 - u;
+      ++u;
+    }
+    const int v = u + rem;
+    const bool dg = u == v;
+    for (int g = 0; g < G; ++g) {
+      const int r = g % (BK - 1);
+      const float* Si = Sb[g & 1];
+      float* So = Sb[(g + 1) & 1];
+      if (active) {
+        const int2 pu = rr_pair(r, u), pv = rr_pair(r, v);
+        const int ux = pu.x * LP, uy = pu.y * LP, vx = pv.x * LP, vy = pv.y * LP;
+        const float u_pp = Si[ux + pu.x], u_qq = Si[uy + pu.y], u_pq = Si[ux + pu.y];
+        const float v_pp = Si[vx + pv.x], v_qq = Si[vy + pv.y], v_pq = Si[vx + pv.y];
+        const float a = Si[ux + pv.x], b = Si[ux + pv.y], c = Si[uy + pv.x], d = Si[uy + pv.y];
+        const float3 ru = (PROBE & 4) ? make_float3(1.f, 0.f, 0.f) : jacobi_rot(u_pp, u_qq, u_pq);
+        const float3 rv = jacobi_rot(v_pp, v_qq, v_pq);
+        if (dg) {
+          // publish in slot orientation for the Q wave: the first slot of pair 0 is slot 63
+          // (column 63 = q), of pair v ≥ 1 slot v (column (r + v) mod 63)
+          const int f = v == 0 ? BK - 1 : (r + v) % (BK - 1);
+          rq[g & 1][v] = make_float2(rv.x, f == pv.x ? rv.y : -rv.y);
+        }
+        if (!(PROBE & 2)) {
+          // O = J_uᵀ S[u rows, v cols] J_v: right (col p' = c·p − s·q, col q' = s·p + c·q), then left
+          const float a1 = rv.x * a - rv.y * b, b1 = rv.y * a + rv.x * b;
+          const float c1 = rv.x * c - rv.y * d, d1 = rv.y * c + rv.x * d;
+          float o00 = ru.x * a1 - ru.y * c1, o01 = ru.x * b1 - ru.y * d1;
+          float o10 = ru.y * a1 + ru.x * c1, o11 = ru.y * b1 + ru.x * d1;
+          o00 = dg ? a - ru.z * b : o00;  // pair u's own block: set exactly
+          o11 = dg ? d + ru.z * b : o11;
+          o01 = dg ? 0.f : o01;
+          o10 = dg ? 0.f : o10;
+          So[ux + pv.x] = o00;
+          So[ux + pv.y] = o01;
+          So[uy + pv.x] = o10;
+          So[uy + pv.y] = o11;
+          So[vx + pu.x] = o00;
+          So[vy + pu.x] = o01;
+          So[vx + pu.y] = o10;
+          So[vy + pu.y] = o11;
+        } else if (dg) {
+          So[ux + pu.x] = ru.x;
+        }
+      }
+      __syncthreads();
+    }
+  } else {
+    const int k = tid - kSThreads;  // row of Q
+    float q[BK];
+#pragma unroll
+    for (int j = 0; j < BK; ++j) q[j] = j == k ? 1.f : 0.f;
+    // 7 rounds with statically shifted slot indices, then one 7-slot shift of the register
+    // file (63 = 9·7, so the shift never straddles a sweep)
+    for (int g0 = 0; g0 < G; g0 += 7) {
+#pragma unroll
+      for (int t = 0; t < 7; ++t) {
+        __syncthreads();
+        if (PROBE & 1) continue;
+        const float2* R = rq[(g0 + t) & 1];
+        // rotations in 4 groups of 8 (one LDS wait per group; keeps the VGPR budget of
+        // 3 waves per SIMD without spilling the 64-entry row)
+#pragma unroll
+        for (int i0 = 0; i0 < BK / 2; i0 += 8) {
+          float2 cs[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) cs[i] = R[i0 + i];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int pi = i0 + i;
+            // pair 0: (slot 63, slot t); pair i ≥ 1: (slot i, slot 63 − i), shifted by t
+            const int si = pi == 0 ? BK - 1 : (pi + t) % (BK - 1);
+            const int sj = pi == 0 ? t : (BK - 1 - pi + t) % (BK - 1);
+            const float x = q[si], y = q[sj];
+            q[si] = cs[i].x * x - cs[i].y * y;
+            q[sj] = cs[i].y * x + cs[i].x * y;
+          }
+        }
+      }
+      float tmp[7];
+#pragma unroll
+      for (int j = 0; j < 7; ++j) tmp[j] = q[j];
+#pragma unroll
+      for (int j = 0; j < BK - 1 - 7; ++j) q[j] = q[j + 7];
+#pragma unroll
+      for (int j = 0; j < 7; ++j) q[BK - 1 - 7 + j] = tmp[j];
+    }
+    float* Qo = Q_out + (int64_t)blockIdx.x * BK * BK + (int64_t)k * BK;
+#pragma unroll
+    for (int j = 0; j < BK; j += 4) *reinterpret_cast<float4*>(Qo + j) = make_float4(q[j], q[j + 1], q[j + 2], q[j + 3]);
+  }
+  __syncthreads();
+  if (tid < m) dq_out[s0 + tid] = Sb[G & 1][tid * LP + tid];
+}
+
 // 64×64×64 product in LDS: Out[c][e] (+)= Σ_a L[a][c]·R[a][e] (TA: L read transposed) or
 // Σ_a L[c][a]·R[a][e]; every thread owns a 4×4 micro-tile.
 template <bool TA>
@@ -468,7 +638,9 @@ __global__ void __launch_bounds__(256) sbr_far_kernel(const float* __restrict__ 
       const int e = c0 + j;
       if (e >= ml) continue;
       const float den = dl[e] - dk[c];
-      X[(int64_t)(sk + c) * ldx + sl + e] = fabsf(den) > thr ? acc[i][j] / den : 0.f;
+      // the 2×2 Jacobi angle ½·atan(2a/den): a/den to first order for well-separated
+      // pairs, saturating at π/4 for strongly coupled ones (no blow-up near the threshold)
+      X[(int64_t)(sk + c) * ldx + sl + e] = fabsf(den) > thr ? 0.5f * atanf(2.f * acc[i][j] / den) : 0.f;
     }
   }
 }
@@ -530,18 +702,36 @@ void evx_sbr_symstats(const float* T, int n, int64_t ldt, float* A, int64_t lda,
   sbr_stats_final_kernel<<<1, 256, 0, s>>>(part, nt * nt, out);
 }
 
-void evx_sbr_taylor_prep(const float* X, const float* X2, const float* X3, int n, float* P, float* M, hipStream_t s) {
+void evx_sbr_taylor_prep(const float* X, const float* X2, const float* X3, int n, const float* alpha, float* P, float* M,
+                         hipStream_t s) {
   const int64_t total = (int64_t)n * n;
   int g = (int)((total + 255) / 256);
   if (g > 2048) g = 2048;
-  sbr_taylor_prep_kernel<<<g, 256, 0, s>>>(X, X2, X3, n, P, M);
+  sbr_taylor_prep_kernel<<<g, 256, 0, s>>>(X, X2, X3, n, alpha, P, M);
 }
 
 void evx_sbr_block(const float* A, int n, int64_t lda, int off, int sweeps, int* perm, float* Q, float* dq, hipStream_t s,
                    long long* dbg) {
-  const int probe = sweeps >> 8;  // diagnostic variants (tools/probe_sbr_block.py): 1 no S update, 2 no Q update
+  int probe = sweeps >> 8;  // diagnostic variants (tools/probe_sbr_block.py): 1 no S update, 2 no Q update
   sweeps &= 255;
   const dim3 g(evx_sbr_nblocks(n, off)), b(64 * kWaves);
+  if (probe == 0 && !dbg) {
+    sbr_block2_kernel<0><<<g, kSThreads + 64, 0, s>>>(A, n, lda, off, sweeps, perm, Q, dq);
+    return;
+  }
+  if (probe >= 8) {  // version-2 probes
+    switch (probe - 8) {
+      case 1: sbr_block2_kernel<1><<<g, kSThreads + 64, 0, s>>>(A, n, lda, off, sweeps, perm, Q, dq); break;
+      case 2: sbr_block2_kernel<2><<<g, kSThreads + 64, 0, s>>>(A, n, lda, off, sweeps, perm, Q, dq); break;
+      case 3: sbr_block2_kernel<3><<<g, kSThreads + 64, 0, s>>>(A, n, lda, off, sweeps, perm, Q, dq); break;
+      case 4: sbr_block2_kernel<4><<<g, kSThreads + 64, 0, s>>>(A, n, lda, off, sweeps, perm, Q, dq); break;
+      case 5: sbr_block2_kernel<5><<<g, kSThreads + 64, 0, s>>>(A, n, lda, off, sweeps, perm, Q, dq); break;
+      case 7: sbr_block2_kernel<7><<<g, kSThreads + 64, 0, s>>>(A, n, lda, off, sweeps, perm, Q, dq); break;
+      default: sbr_block2_kernel<0><<<g, kSThreads + 64, 0, s>>>(A, n, lda, off, sweeps, perm, Q, dq); break;
+    }
+    return;
+  }
+  if (probe == 4) probe = 0;  // version 1 (probe tool: sweeps | 4 << 8)
   if (probe == 1) sbr_block_kernel<1><<<g, b, 0, s>>>(A, n, lda, off, sweeps, perm, Q, dq, dbg);
   else if (probe == 2) sbr_block_kernel<2><<<g, b, 0, s>>>(A, n, lda, off, sweeps, perm, Q, dq, dbg);
   else if (probe == 3) sbr_block_kernel<3><<<g, b, 0, s>>>(A, n, lda, off, sweeps, perm, Q, dq, dbg);

@@ -252,12 +252,21 @@ class CMAES(Algorithm):
             order = order.long()
         else:
             _, order = argsort(fitness)
-        # weight of every global row (0 outside the top μ), restricted to the local slice: the
-        # rank-μ partial sum runs over this rank's λ/N rows only (shapes fixed for hipGraphs)
+        # weight of every global row (0 outside the top μ).  A rank holds at most
+        # K = min(μ, λ/N) selected rows — its K best local rows — so the rank-μ partial sum
+        # gathers exactly those K rows (weight 0 for any that missed the global top μ):
+        # the same K = μ GEMM as the unsharded tell on one rank, fixed shapes for hipGraphs
         wfull = torch.zeros(self.pop_size, dtype=torch.float32, device=fitness.device)
         wfull.index_copy_(0, order[: self.mu], self.weights.to(fitness.device))
-        wloc = wfull[start : start + size].contiguous()
-        dm, S = self._weighted_stats(state, state.population, None, size, wloc, gather=False)
+        K = min(self.mu, size)
+        floc = fitness[start : start + size].contiguous()
+        if floc.is_cuda:
+            _, lorder = argsort_i32(floc)
+        else:
+            _, lorder = argsort(floc)
+        lsel = lorder[:K].contiguous()
+        wsel = wfull[start : start + size].index_select(0, lsel.long()).contiguous()
+        dm, S = self._weighted_stats(state, state.population, lsel, K, wsel, gather=True)
         buf = torch.cat([dm.reshape(-1), S.reshape(-1)])
         with profiling.phase("all_reduce"):
             dist.all_reduce_(buf)

@@ -53,6 +53,11 @@ def _run(cmd):
     return r.stdout
 
 
+# per-file device flags: the SBR block kernel's register-resident Q rows are updated with
+# scalar FMAs; SLP vectorisation packs them into v_pk ops that need ~3 v_mov shuffles each
+FILE_FLAGS = {"eigh_sbr.hip": ["-fno-slp-vectorize"]}
+
+
 def build(verbose: bool = True, jobs: int = None) -> str:
     os.makedirs(BUILD, exist_ok=True)
     td = _torch_dir()
@@ -86,7 +91,7 @@ def build(verbose: bool = True, jobs: int = None) -> str:
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
         objs.append(obj)
         if _stale(src, obj, hdr):
-            tasks.append([hipcc] + dev_flags + ["-c", src, "-o", obj])
+            tasks.append([hipcc] + dev_flags + FILE_FLAGS.get(os.path.basename(src), []) + ["-c", src, "-o", obj])
     for src in sorted(glob.glob(os.path.join(CSRC, "bindings", "*.cpp"))):
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
         objs.append(obj)
