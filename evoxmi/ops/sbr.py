@@ -264,6 +264,7 @@ class SBRConfig:
     max_iters: int = 16
     damp_tau: float = 1.0      # cap on ‖αX‖₂ (0: undamped)
     damp_kappa: float = 0.5    # estimate ‖X‖₂ only while κ exceeds this
+    near_only: float = 3.0     # near-only (no far step) iteration once off_rel ≤ near_only·tol
     max_jacobi: int = 16
     block_sweeps: int = 2
     thr_fac: float = 0.3
@@ -282,22 +283,31 @@ def _read(st: torch.Tensor):
     return (off_rel, kappa) if len(v) == 4 else (off_rel, kappa, v[4])
 
 
-def _refine_core(C, A, B, st, off: int, ns: bool, damp: bool, cfg: SBRConfig, out=None):
+def _refine_core(C, A, B, st, off: int, ns: bool, damp: bool, cfg: SBRConfig, out=None, far_on: bool = True):
     """One iteration; returns (A, B, stats, α).  ``out = (A, B, st)`` static buffers to
     write the results into (the workspace graphs: no copies).  ``damp``: estimate ‖X‖₂
-    and cap the step (the host enables it while κ is large)."""
+    and cap the step (the host enables it while κ is large).  ``far_on = False``: a
+    near-only iteration (block solves, B ← B[:, perm]·Qblk, A ← BᵀCB) for the last step,
+    when the residual is almost entirely near pairs (4 GEMMs fewer)."""
     perm, Q, dq = block_solve(A, off, cfg.block_sweeps)
-    X = far(A, off, perm, Q, dq, st, cfg.thr_fac)
-    X2 = X @ X
-    alpha = damping(X2, cfg.damp_tau) if damp and cfg.damp_tau > 0 else None
-    Bq = bq(B, off, perm, Q)
-    V = expm_taylor6(X, X2, alpha)
-    if ns:
-        Bn = Bq @ V
-        BtB = Bn.t() @ Bn
-        Bn = torch.addmm(Bn, Bn, BtB, beta=1.5, alpha=-0.5, out=out[1]) if out else newton_schulz(Bn)
+    alpha = None
+    if not far_on:
+        Bn = bq(B, off, perm, Q)
+        if out:
+            out[1].copy_(Bn)
+            Bn = out[1]
     else:
-        Bn = torch.mm(Bq, V, out=out[1]) if out else Bq @ V
+        X = far(A, off, perm, Q, dq, st, cfg.thr_fac)
+        X2 = X @ X
+        alpha = damping(X2, cfg.damp_tau) if damp and cfg.damp_tau > 0 else None
+        Bq = bq(B, off, perm, Q)
+        V = expm_taylor6(X, X2, alpha)
+        if ns:
+            Bn = Bq @ V
+            BtB = Bn.t() @ Bn
+            Bn = torch.addmm(Bn, Bn, BtB, beta=1.5, alpha=-0.5, out=out[1]) if out else newton_schulz(Bn)
+        else:
+            Bn = torch.mm(Bq, V, out=out[1]) if out else Bq @ V
     if out and Bn.is_cuda:
         T = Bn.t() @ (C @ Bn)
         _ext.ops().sbr_symstats_out(T, out[0], out[2])
@@ -309,9 +319,9 @@ def _refine_core(C, A, B, st, off: int, ns: bool, damp: bool, cfg: SBRConfig, ou
     return A, Bn, st, alpha
 
 
-def refine_step(C, A, B, st, it: int, cfg: SBRConfig, ns: bool = None, damp: bool = True):
+def refine_step(C, A, B, st, it: int, cfg: SBRConfig, ns: bool = None, damp: bool = True, far_on: bool = True):
     ns = it < cfg.ns_iters if ns is None else ns
-    return _refine_core(C, A, B, st, (it % 2) * (BK // 2), ns, damp, cfg)
+    return _refine_core(C, A, B, st, (it % 2) * (BK // 2), ns, damp, cfg, far_on=far_on)
 
 
 class _Workspace:
@@ -350,17 +360,17 @@ class _Workspace:
 
         self._capture(("init",), body).replay()
 
-    def iterate(self, it: int, ns: bool, damp: bool):
+    def iterate(self, it: int, ns: bool, damp: bool, far_on: bool = True):
         off = (it % 2) * (BK // 2)
 
         def body():
             # A, B, stats are written in place (A and B are fully read before the last
             # GEMM/kernel of the iteration overwrites them)
             _, _, _, alpha = _refine_core(self.C, self.A, self.B, self.st, off, ns, damp, self.cfg,
-                                          out=(self.A, self.B, self.st))
+                                          out=(self.A, self.B, self.st), far_on=far_on)
             self.info[4:].copy_(alpha)
 
-        self._capture(("it", off, ns, damp), body).replay()
+        self._capture(("it", off, ns, damp, far_on), body).replay()
 
 
 _WS = {}
@@ -447,12 +457,14 @@ def eigh_warm(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None):
         # (κ > damp_kappa: converging iterations have ‖X‖₂ ≪ 1 and are never capped)
         ns = it < cfg.ns_iters or alpha < 1.0
         damp = kappa > cfg.damp_kappa
+        # close to the tolerance the residual is near pairs only: skip the far step
+        far_on = not (it > 0 and off_rel <= cfg.near_only * cfg.tol)
         if ws is not None:
-            ws.iterate(it, ns, damp)
+            ws.iterate(it, ns, damp, far_on)
             A, B, st = ws.A, ws.B, ws.st
             off_rel, kappa, alpha = _read(ws.info)
         else:
-            A, B, st, a = refine_step(C, A, B, st, it, cfg, ns, damp)
+            A, B, st, a = refine_step(C, A, B, st, it, cfg, ns, damp, far_on)
             off_rel, kappa, alpha = _read(torch.cat([st.double(), a.double().reshape(1)]))
         it += 1
         info.damped += alpha < 1.0

@@ -151,35 +151,45 @@ def test_sbr_eigh_converges_at_north_star_size(gens):
 
 @gpu
 def test_cmaes_trajectories_sbr_vs_library_eigh():
-    """CMA-ES λ = 10⁴, d = 1000 on CEC'22 F1 for 100 generations: the converged SBR solver
-    and rocSOLVER eigh give the same best-fitness trajectory (median ratio within 5 %), and
-    every SBR decomposition meets the tolerance."""
+    """CMA-ES λ = 10⁴, d = 1000 for 100 generations with the converged SBR solver and with
+    rocSOLVER eigh: every SBR decomposition meets the tolerance and the runs make the same
+    progress.  Progress is the objective at the distribution mean on the (axis-scaled)
+    Ellipsoid, which CMA-ES must learn through its eigenbasis; best-so-far on CEC'22 F1 is
+    no measure here — it freezes at the luckiest early sample while σ adapts, and on F1
+    even the mean's value swings by orders of magnitude (tools/traj_probe.py).  Two
+    decompositions that agree to 1e-5 still make the runs drift apart chaotically (≈10 %
+    per seed after 60 generations), so the comparison uses the median over three seeds."""
+    import statistics
+
     from evoxmi import config as cfg
     from evoxmi import random as rnd
     from evoxmi.algorithms import CMAES
-    from evoxmi.problems.numerical import CEC2022TestSuit
+    from evoxmi.problems.numerical import Ellipsoid
     from evoxmi.workflows import StdWorkflow
 
-    from evoxmi.monitors import EvalMonitor
-
-    def traj(impl):
+    def traj(impl, seed):
         with cfg.override(eigh=impl):
-            center = (torch.rand(1000, generator=torch.Generator().manual_seed(1)) * 160 - 80).cuda()
-            algo = CMAES(center_init=center, init_stdev=20.0, pop_size=10000)
-            mon = EvalMonitor()
+            center = (torch.rand(1000, generator=torch.Generator().manual_seed(1)) * 10 - 5).cuda()
+            algo = CMAES(center_init=center, init_stdev=1.0, pop_size=10000)
+            prob = Ellipsoid()
             # rocSOLVER syevd is not hipGraph-capturable: the library run steps eagerly
-            wf = StdWorkflow(algo, CEC2022TestSuit.create(1), monitors=[mon], graph=(impl == "sbr"))
-            st = wf.init(rnd.PRNGKey(7, device=torch.device("cuda")))
-            best, offs = [], []
+            wf = StdWorkflow(algo, prob, graph=(impl == "sbr"))
+            st = wf.init(rnd.PRNGKey(seed, device=torch.device("cuda")))
+            pst = st.get_child_state("problem")
+            f, offs = [], []
             for _ in range(100):
                 st = wf.step(st)
-                best.append(float(mon.get_best_fitness()))
+                a = st.get_child_state("algorithm")
+                f.append(float(prob.evaluate(pst, a.mean.reshape(1, -1))[0][0]))
                 if impl == "sbr":
-                    offs.append(float(st.get_child_state("algorithm").eig_stats[0]))
-            return torch.tensor(best, dtype=torch.float64), offs
+                    offs.append(float(a.eig_stats[0]))
+            return f, offs
 
-    f_sbr, offs = traj("sbr")
-    f_lib, _ = traj("torch")
+    runs = {impl: [traj(impl, s) for s in (7, 8, 9)] for impl in ("sbr", "torch")}
+    offs = [o for f, oo in runs["sbr"] for o in oo]
     assert max(offs) <= 1e-5, max(offs)
-    ratio = (f_sbr[10:] / f_lib[10:]).median().item()
-    assert abs(ratio - 1) < 0.05, (ratio, f_sbr[::10].tolist(), f_lib[::10].tolist())
+    med = {impl: [statistics.median(r[0][g] for r in runs[impl]) for g in range(100)] for impl in runs}
+    logr = [abs(math.log(med["sbr"][g] / med["torch"][g])) for g in range(10, 100)]
+    assert statistics.median(logr) < math.log(1.05), (statistics.median(logr), med["sbr"][::10], med["torch"][::10])
+    prog = {impl: math.log(med[impl][10] / med[impl][99]) for impl in med}
+    assert prog["torch"] > 1.0 and abs(prog["sbr"] / prog["torch"] - 1) < 0.05, prog

@@ -16,23 +16,36 @@ from evoxmi.problems.numerical import CEC2022TestSuit  # noqa: E402
 from evoxmi.workflows import StdWorkflow  # noqa: E402
 
 
-def traj(impl, seed, gens=100):
+def traj(impl, seed, gens=100, problem="f1"):
+    from evoxmi.problems.numerical import Ellipsoid
+
     with cfg.override(eigh=impl):
-        center = (torch.rand(1000, generator=torch.Generator().manual_seed(1)) * 160 - 80).cuda()
-        algo = CMAES(center_init=center, init_stdev=20.0, pop_size=10000)
+        if problem == "f1":
+            center = (torch.rand(1000, generator=torch.Generator().manual_seed(1)) * 160 - 80).cuda()
+            algo = CMAES(center_init=center, init_stdev=20.0, pop_size=10000)
+            prob = CEC2022TestSuit.create(1)
+        else:
+            center = (torch.rand(1000, generator=torch.Generator().manual_seed(1)) * 10 - 5).cuda()
+            algo = CMAES(center_init=center, init_stdev=1.0, pop_size=10000)
+            prob = Ellipsoid()
         mon = EvalMonitor()
-        wf = StdWorkflow(algo, CEC2022TestSuit.create(1), monitors=[mon], graph=(impl == "sbr"))
+        wf = StdWorkflow(algo, prob, monitors=[mon], graph=(impl == "sbr"))
         st = wf.init(rnd.PRNGKey(seed, device=torch.device("cuda")))
         out = []
+        pst = st.get_child_state("problem")
         for _ in range(gens):
             st = wf.step(st)
-            out.append(float(mon.get_best_fitness()))
+            # fitness at the distribution mean: the algorithm's progress (best-so-far is
+            # dominated by lucky early samples while σ adapts)
+            m = st.get_child_state("algorithm").mean.reshape(1, -1)
+            out.append(float(prob.evaluate(pst, m)[0][0]))
         return out
 
 
 if __name__ == "__main__":
     seeds = [int(s) for s in (sys.argv[1] if len(sys.argv) > 1 else "7,8,9").split(",")]
-    res = {impl: {s: traj(impl, s) for s in seeds} for impl in ("sbr", "torch")}
+    problem = sys.argv[2] if len(sys.argv) > 2 else "f1"
+    res = {impl: {s: traj(impl, s, problem=problem) for s in seeds} for impl in ("sbr", "torch")}
     for impl in res:
         for s in seeds:
             t = res[impl][s]
