@@ -683,7 +683,48 @@ at::Tensor nsga_select(const at::Tensor& rank, const at::Tensor& f, int64_t N, i
 
 }  // namespace
 
+// ---- K17 / K18 (mo_geom.hip)
+std::vector<at::Tensor> knn(const at::Tensor& X, const at::Tensor& Y, int64_t T) {
+  for (auto* t : {&X, &Y}) { CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t); }
+  TORCH_CHECK(X.dim() == 2 && Y.dim() == 2 && X.size(1) == Y.size(1), "knn: X (N, m), Y (M, m)");
+  const int64_t N = X.size(0), M = Y.size(0), m = X.size(1);
+  TORCH_CHECK(m >= 1 && m <= evx_knn_max_m(), "knn: 1 <= m <= ", evx_knn_max_m());
+  TORCH_CHECK(T >= 1 && T <= evx_knn_max_t() && T <= M, "knn: 1 <= T <= min(", evx_knn_max_t(), ", M)");
+  c10::DeviceGuard g(X.device());
+  auto d = at::empty({N, T}, X.options());
+  auto i = at::empty({N, T}, X.options().dtype(at::kInt));
+  if (N > 0) evx_knn(X.data_ptr<float>(), Y.data_ptr<float>(), (int)N, (int)M, (int)m, (int)T, d.data_ptr<float>(), i.data_ptr<int32_t>(), cur_stream());
+  return {d, i};
+}
+
+at::Tensor hv_count(const at::Tensor& S, const at::Tensor& P, int64_t strict) {
+  for (auto* t : {&S, &P}) { CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t); }
+  TORCH_CHECK(S.dim() == 2 && P.dim() == 2 && S.size(1) == P.size(1), "hv_count: samples (S, m), points (n, m)");
+  const int64_t m = S.size(1);
+  TORCH_CHECK(m >= 1 && m <= evx_hv_max_m(), "hv_count: 1 <= m <= ", evx_hv_max_m());
+  c10::DeviceGuard g(S.device());
+  auto c = at::empty({S.size(0)}, S.options().dtype(at::kInt));
+  if (S.size(0) > 0) evx_hv_count(S.data_ptr<float>(), P.data_ptr<float>(), (int)S.size(0), (int)P.size(0), (int)m, (int)strict, c.data_ptr<int32_t>(), cur_stream());
+  return c;
+}
+
+at::Tensor hv_contrib(const at::Tensor& S, const at::Tensor& P, const at::Tensor& count, const at::Tensor& alpha) {
+  for (auto* t : {&S, &P, &alpha}) { CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t); }
+  TORCH_CHECK(count.is_cuda() && count.scalar_type() == at::kInt && count.is_contiguous() && count.numel() == S.size(0), "hv_contrib: count int32[S]");
+  TORCH_CHECK(S.dim() == 2 && P.dim() == 2 && S.size(1) == P.size(1) && S.size(1) <= evx_hv_max_m(), "hv_contrib: samples (S, m), points (n, m)");
+  TORCH_CHECK(alpha.numel() >= P.size(0), "hv_contrib: alpha needs n entries");
+  c10::DeviceGuard g(S.device());
+  auto f = at::zeros({P.size(0)}, S.options());
+  if (P.size(0) > 0)
+    evx_hv_contrib(S.data_ptr<float>(), P.data_ptr<float>(), count.data_ptr<int32_t>(), alpha.data_ptr<float>(), (int)S.size(0), (int)P.size(0),
+                   (int)S.size(1), f.data_ptr<float>(), cur_stream());
+  return f;
+}
+
 TORCH_LIBRARY(evoxmi, m) {
+  m.def("knn(Tensor X, Tensor Y, int T) -> Tensor[]");
+  m.def("hv_count(Tensor S, Tensor P, int strict) -> Tensor");
+  m.def("hv_contrib(Tensor S, Tensor P, Tensor count, Tensor alpha) -> Tensor");
   m.def("philox_fill(Tensor key, int n, int dist, int offset) -> Tensor");
   m.def("argsort_f32(Tensor keys, int descending) -> Tensor[]");
   m.def("cec_basic(Tensor Z, int fid, Tensor? perm, int start, int L, Tensor? sub, float scale, Tensor? Y, int ystart, int yperm) -> Tensor");
@@ -757,6 +798,9 @@ TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
   m.impl("sbr_block", &sbr_block);
   m.impl("sbr_far", &sbr_far);
   m.impl("sbr_bq", &sbr_bq);
+  m.impl("knn", &knn);
+  m.impl("hv_count", &hv_count);
+  m.impl("hv_contrib", &hv_contrib);
   m.impl("sbr_symstats_out", &sbr_symstats_out);
   m.impl("sbr_symstats", &sbr_symstats);
   m.impl("sbr_taylor_prep", &sbr_taylor_prep);

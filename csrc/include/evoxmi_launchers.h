@@ -104,3 +104,12 @@ int evx_sbr_symstats_parts(int n);
 void evx_sbr_symstats(const float* T, int n, int64_t ldt, float* A, int64_t lda, double* part, double* out, hipStream_t s);
 void evx_sbr_taylor_prep(const float* X, const float* X2, const float* X3, int n, const float* alpha, float* P, float* M,
                          hipStream_t s);
+
+// mo_geom.hip (K17 k-nearest rows, K18 Monte-Carlo hypervolume)
+int evx_knn_max_t();
+int evx_knn_max_m();
+void evx_knn(const float* X, const float* Y, int N, int M, int m, int T, float* out_d, int32_t* out_i, hipStream_t s);
+int evx_hv_max_m();
+void evx_hv_count(const float* S, const float* P, int ns, int np, int m, int strict, int32_t* count, hipStream_t s);
+void evx_hv_contrib(const float* S, const float* P, const int32_t* count, const float* alpha, int ns, int np, int m, float* f,
+                    hipStream_t s);

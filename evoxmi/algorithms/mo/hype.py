@@ -12,23 +12,20 @@ import torch
 from ...core import State
 from ...operators import selection
 from ...operators.selection.non_dominate import lexsort, non_dominated_sort
+from ...ops import geom
 from ...ops import random as rnd
 from .common import MOAlgorithm
 
 
-def cal_hv(points, ref, k, n_sample, key, chunk=2048):
+def cal_hv(points, ref, k, n_sample, key):
     n, m = points.shape
     j = torch.arange(1, n, dtype=torch.float32, device=points.device)
     alpha = torch.cumprod(torch.cat([torch.ones(1, device=points.device), (k - j) / (n - j)]), 0) / torch.arange(1, n + 1, device=points.device)
     f_min = points.min(0).values
     samples = rnd.uniform(key, (n_sample, m)).to(points.device) * (ref - f_min) + f_min
-    f = torch.zeros(n, device=points.device)
-    for s0 in range(0, n_sample, chunk):
-        s = samples[s0 : s0 + chunk]
-        pds = (points[:, None, :] <= s[None, :, :]).all(-1)  # (n, S): point dominates sample
-        ds = pds.sum(0)
-        ds = torch.where(ds == 0, ds, ds - 1)
-        f = f + torch.where(pds, alpha[ds][None, :], torch.zeros((), device=points.device)).sum(1)
+    # K18: per-sample dominator counts, then per-point Σ α[count − 1] (two kernels on the GPU)
+    cnt = geom.hv_count(samples, points, strict=False)
+    f = geom.hv_contrib(samples, points, cnt, alpha)
     return f * torch.prod(ref - f_min) / n_sample
 
 

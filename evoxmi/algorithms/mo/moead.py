@@ -26,21 +26,16 @@ import torch
 from ...core import Algorithm, State
 from ...operators import crossover, mutation
 from ...operators.sampling import UniformSampling
+from ...ops import geom
 from ...ops import random as rnd
 from ...utils.common import AggregationFunction
 
 
-def nearest_neighbors(w: torch.Tensor, T: int, chunk: int = 4096) -> torch.Tensor:
-    """T nearest weight vectors of every weight (ties by index, like a stable argsort)."""
-    n = w.shape[0]
-    out = []
-    ww = (w * w).sum(1)
-    for s in range(0, n, chunk):
-        blk = w[s : s + chunk]
-        d2 = (ww[s : s + chunk, None] + ww[None, :] - 2 * blk @ w.T).clamp_min(0)
-        d = torch.sqrt(d2)
-        out.append(torch.argsort(d, dim=1, stable=True)[:, :T])
-    return torch.cat(out, 0)
+def nearest_neighbors(w: torch.Tensor, T: int) -> torch.Tensor:
+    """T nearest weight vectors of every weight (ties by index, like the reference's stable
+    argsort of the distance matrix, moead.py:65-67).  On the GPU one fused kernel keeps
+    each row's top-T in registers (``ops.geom.knn``, K17): no N×N matrix at N = 16384."""
+    return geom.knn(w, w, T)[1]
 
 
 def reverse_neighbors(neighbors: torch.Tensor):

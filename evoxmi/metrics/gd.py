@@ -1,12 +1,14 @@
 """Generational distance GD and GD+ (reference ``metrics/gd.py:7-41``).
 
-``GD_p = (Σ_i min_j d(x_i, z_j)^p / |X|)^{1/p}``; the distances are one
-``torch.cdist`` (GEMM form on the matrix cores); GD+ uses the modified distance
+``GD_p = (Σ_i min_j d(x_i, z_j)^p / |X|)^{1/p}``; the nearest distances come from the
+fused nearest-row kernel (``ops.geom.min_dist``, K17); GD+ uses the modified distance
 ‖max(x − z, 0)‖ (Ishibuchi et al. 2015).
 """
 from __future__ import annotations
 
 import torch
+
+from ..ops import geom
 
 
 def _plus_dist(a, b):
@@ -16,7 +18,7 @@ def _plus_dist(a, b):
 
 def gd(objs, pf, p=1):
     objs, pf = objs.to(torch.float32), pf.to(torch.float32).to(objs.device)
-    m = torch.cdist(objs, pf).min(1).values
+    m = geom.min_dist(objs, pf)
     return ((m**p).sum() / objs.shape[0]) ** (1 / p)
 
 

@@ -7,8 +7,8 @@
 * ``exact_hv`` — exact value by slicing (HSO) for any m, O(n^{m−1} log n), meant for
   fronts of moderate size / validation of the estimators.
 
-Both estimators are vectorised as (samples × points × m) comparisons, chunked so the
-working set stays bounded.  Like the reference, points are measured as |objs − ref|
+Both estimators reduce to per-sample dominator counts (samples × points × m comparisons):
+one tiled HIP kernel on the GPU (``ops.geom.hv_count``), chunked torch on the CPU.  Like the reference, points are measured as |objs − ref|
 so either optimisation direction works.
 """
 from __future__ import annotations
@@ -16,20 +16,13 @@ from __future__ import annotations
 import numpy as np
 import torch
 
+from ..ops import geom
 from ..ops import random as rnd
 
-_CHUNK = 1 << 22  # samples × points per chunk
-
-
 def _dominated_counts(samples, points):
-    """For each sample, how many points strictly dominate it (sample < point in all m)."""
-    S, n = samples.shape[0], points.shape[0]
-    step = max(1, _CHUNK // max(n, 1))
-    out = []
-    for s0 in range(0, S, step):
-        s = samples[s0 : s0 + step]
-        out.append((s[:, None, :] < points[None, :, :]).all(-1).sum(1))
-    return torch.cat(out)
+    """For each sample, how many points strictly dominate it (sample < point in all m);
+    one tiled kernel on the GPU (``ops.geom.hv_count``, K18)."""
+    return geom.hv_count(samples, points, strict=True)
 
 
 def bounding_cube_monte_carlo_hv(key, objs, ref, num_sample):

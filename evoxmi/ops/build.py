@@ -55,7 +55,9 @@ def _run(cmd):
 
 # per-file device flags: the SBR block kernel's register-resident Q rows are updated with
 # scalar FMAs; SLP vectorisation packs them into v_pk ops that need ~3 v_mov shuffles each
-FILE_FLAGS = {"eigh_sbr.hip": ["-fno-slp-vectorize"]}
+# mo_geom.hip: its distance loop must stay unfused (bit-identical ties with the CPU
+# oracle); plain "fast" contraction ignores the in-source pragma
+FILE_FLAGS = {"eigh_sbr.hip": ["-fno-slp-vectorize"], "mo_geom.hip": ["-ffp-contract=fast-honor-pragmas"]}
 
 
 def build(verbose: bool = True, jobs: int = None) -> str:

@@ -742,3 +742,84 @@ def test_nds_barrier_timeout_is_reported():
     out = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, timeout=110)
     assert out.returncode == 0, out.stderr[-2000:]
     assert "RAISED" in out.stdout
+
+
+# ---------------------------------------------------------------- K17 / K18 (mo_geom.hip)
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,M,m,T", [(1000, 1000, 3, 20), (300, 5000, 10, 1), (257, 64, 64, 32), (50, 40, 2, 7)])
+def test_knn_kernel_matches_direct_form(N, M, m, T):
+    from evoxmi.ops import geom
+
+    g = torch.Generator().manual_seed(N + M)
+    X, Y = torch.rand(N, m, generator=g), torch.rand(M, m, generator=g)
+    d_ref, i_ref = geom.knn(X, Y, T)
+    d, i = geom.knn(X.cuda(), Y.cuda(), T)
+    assert torch.allclose(d.cpu(), d_ref, rtol=1e-5, atol=1e-6)
+    agree = (i.cpu() == i_ref).float().mean().item()
+    assert agree > 0.999, agree  # index order may differ only at rounding-level ties
+    # the returned indices are the claimed distances
+    dd = torch.sqrt(((X[:, None, :] - Y[i.cpu()]) ** 2).sum(-1))
+    assert torch.allclose(dd, d.cpu(), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_knn_kernel_ties_by_index():
+    from evoxmi.ops import geom
+
+    # uniform weights on a simplex lattice: many exactly equal distances
+    from evoxmi.operators.sampling import UniformSampling
+
+    w = UniformSampling(300, 3)()[0].float()
+    d_ref, i_ref = geom.knn(w, w, 20)
+    d, i = geom.knn(w.cuda(), w.cuda(), 20)
+    assert torch.equal(i.cpu(), i_ref)
+    assert torch.allclose(d.cpu(), d_ref, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("strict", [True, False])
+def test_hv_count_kernel(strict):
+    from evoxmi.ops import geom
+
+    g = torch.Generator().manual_seed(3)
+    S, P = torch.rand(20000, 3, generator=g), torch.rand(150, 3, generator=g)
+    P[5] = S[7]  # exact equality exercises < vs <=
+    ref = geom.hv_count(S, P, strict)
+    out = geom.hv_count(S.cuda(), P.cuda(), strict).cpu()
+    assert torch.equal(out, ref)
+
+
+@pytest.mark.gpu
+def test_hv_contrib_kernel_and_hype_cal_hv():
+    from evoxmi import random as rnd
+    from evoxmi.algorithms.mo.hype import cal_hv
+    from evoxmi.ops import geom
+
+    g = torch.Generator().manual_seed(4)
+    S, P = torch.rand(10000, 3, generator=g), torch.rand(100, 3, generator=g) * 0.8
+    cnt = geom.hv_count(S, P, False)
+    alpha = torch.rand(100, generator=g)
+    ref = geom.hv_contrib(S, P, cnt, alpha)
+    out = geom.hv_contrib(S.cuda(), P.cuda(), cnt.cuda(), alpha.cuda()).cpu()
+    assert torch.allclose(out, ref, rtol=1e-5, atol=1e-5)
+    # HypE's estimator on the device equals the CPU oracle for the same samples
+    key = rnd.PRNGKey(5)
+    ref_pt = torch.full((3,), 1.2)
+    f_cpu = cal_hv(P, ref_pt, 50, 10000, key)
+    f_gpu = cal_hv(P.cuda(), ref_pt.cuda(), 50, 10000, key.cuda()).cpu()
+    assert torch.allclose(f_gpu, f_cpu, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_igd_and_moead_neighbors_use_knn_kernel():
+    from evoxmi.algorithms.mo.moead import nearest_neighbors
+    from evoxmi.metrics.igd import igd
+    from evoxmi.problems.numerical import DTLZ2
+
+    pf = DTLZ2(m=3).pf()
+    objs = pf[::7] + 0.01 * torch.rand(pf[::7].shape, generator=torch.Generator().manual_seed(0))
+    assert abs(float(igd(objs.cuda(), pf.cuda())) - float(igd(objs, pf))) < 1e-6
+    from evoxmi.operators.sampling import UniformSampling
+
+    w = UniformSampling(1000, 3)()[0].float()
+    assert torch.equal(nearest_neighbors(w.cuda(), 20).cpu(), nearest_neighbors(w, 20))
