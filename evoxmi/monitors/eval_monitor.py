@@ -50,12 +50,33 @@ class EvalMonitor(Monitor):
         self.latest_fitness = None
         self.eval_count = 0
         self.opt_direction = 1
+        self._dist = None
 
     def hooks(self):
         return ["post_eval"]
 
     def set_opt_direction(self, opt_direction):
         self.opt_direction = opt_direction
+
+    def set_dist(self, ctx):
+        """Population-sharded runs: candidate rows are rank-local (the workflow's
+        ``enable_distributed``).  The best solution is then found with ONE MINLOC
+        all-reduce over the ranks' local minima (packed ordered-f32 | global index,
+        ``DistContext.all_reduce_min_loc``) and its row assembled by a SUM all-reduce
+        to which only the owner contributes (graph-safe: no host-side owner lookup)."""
+        self._dist = ctx
+
+    def _sharded_best(self, local_sol, fitness):
+        d = self._dist
+        n = fitness.shape[0]
+        start, size = d.slice_of(n)
+        f_loc = fitness[start : start + size]
+        i_loc = torch.argmin(f_loc)
+        val, gidx = d.all_reduce_min_loc(f_loc[i_loc], i_loc + start)
+        mine = (gidx == i_loc + start).to(local_sol.dtype)
+        row = local_sol.index_select(0, i_loc.reshape(1)) * mine
+        d.all_reduce_(row)
+        return val.reshape(1), row
 
     def _keep(self, x):
         if x is None:
@@ -104,7 +125,16 @@ class EvalMonitor(Monitor):
         n = fitness.shape[0]
         k = min(self.topk, n)
         if cand_sol is not None and self._rows(cand_sol) != n:
-            cand_sol = None  # distributed generic path: rows are sharded
+            if k == 1 and self._dist is not None and isinstance(cand_sol, torch.Tensor):
+                fit, sol = self._sharded_best(cand_sol, fitness)
+                if self.topk_fitness is None:
+                    self.topk_fitness, self.topk_solutions = fit.clone(), sol.clone()
+                else:
+                    better = fit < self.topk_fitness
+                    self.topk_fitness = torch.where(better, fit, self.topk_fitness)
+                    self.topk_solutions = torch.where(better[:, None], sol, self.topk_solutions)
+                return
+            cand_sol = None  # rows are sharded and there is no context: fitness only
         if k == 1:
             i = torch.argmin(fitness)
             fit = fitness.index_select(0, i.reshape(1))

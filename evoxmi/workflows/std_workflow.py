@@ -372,6 +372,9 @@ class StdWorkflow(Workflow):
 
         self._dist = DistContext(group=group, algorithm=self.algorithm)
         self.distributed_step = True
+        for m in self.monitors:  # monitors that track sharded rows (EvalMonitor best solution)
+            if hasattr(m, "set_dist"):
+                m.set_dist(self._dist)
         state = self._dist.broadcast_state(state)
         if self._dist.algorithm_sharded:
             pop_size = getattr(self.algorithm, "pop_size")

@@ -249,3 +249,45 @@ def test_evoxvis_monitor_arrow_round_trip(tmp_path):
     for f, p in zip(out["fitness"], out["population"]):
         assert np.allclose(f, (p.astype(np.float64) ** 2).sum(1), rtol=1e-5)  # Sphere of the recorded population
     assert out["duration"] == sorted(out["duration"])
+
+
+def _sharded_monitor_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from evoxmi.monitors import EvalMonitor
+    from evoxmi.parallel import destroy, init_distributed
+
+    init_distributed(backend="gloo")
+    mon = EvalMonitor(full_fit_history=False)
+    wf = StdWorkflow(CMAES(torch.full((10,), 3.0), init_stdev=1.0, pop_size=24), Sphere(), monitors=[mon])
+    st = wf.init(rnd.PRNGKey(7))
+    st = wf.enable_distributed(st)
+    for _ in range(6):
+        st = wf.step(st)
+    out[rank] = (mon.get_best_fitness().clone(), mon.get_best_solution().clone())
+    destroy()
+
+
+def test_sharded_monitor_best_solution_via_minloc():
+    """Population-sharded CMA-ES (rows rank-local): the monitor's best solution is found by
+    one MINLOC all-reduce + an owner-only SUM all-reduce of the row, identical on every
+    rank and consistent with the best fitness."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_sharded_monitor_worker, args=(3, _free_port(), out), nprocs=3, join=True)
+    f0, x0 = out[0]
+    for r in (1, 2):
+        assert torch.equal(out[r][0], f0) and torch.equal(out[r][1], x0)
+    assert x0.shape == (10,)
+    assert torch.allclose((x0 * x0).sum(), f0, rtol=1e-6)
+
+
+def test_min_loc_packing_roundtrip_single_process():
+    from evoxmi.parallel.context import DistContext
+
+    ctx = DistContext.__new__(DistContext)
+    ctx.world_size, ctx.group = 1, None
+    for v in (-3.5, -0.0, 0.0, 1e-30, 2.5, 7e30):
+        t = torch.tensor(v, dtype=torch.float32)
+        val, idx = ctx.all_reduce_min_loc(t, torch.tensor(12345))
+        assert torch.equal(val.view(torch.int32), t.view(torch.int32)) and int(idx) == 12345
