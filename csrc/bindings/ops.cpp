@@ -683,6 +683,20 @@ at::Tensor nsga_select(const at::Tensor& rank, const at::Tensor& f, int64_t N, i
 
 }  // namespace
 
+// OpenES gradient with Philox-regenerated noise: g[j] = Σ_i w[i] ε(row0 + i, j)
+at::Tensor es_noise_grad(const at::Tensor& key, const at::Tensor& w, int64_t d, int64_t row0) {
+  check_key(key);
+  CHECK_DEV(w); CHECK_F32(w); CHECK_CONTIG(w);
+  TORCH_CHECK(w.dim() == 1 && d >= 1 && row0 >= 0, "es_noise_grad: w (rows,), d >= 1");
+  const int64_t rows = w.size(0);
+  const int chunks = (int)std::max<int64_t>(1, std::min<int64_t>(64, rows / 64));
+  c10::DeviceGuard g(w.device());
+  auto partial = at::empty({chunks, d}, w.options());
+  if (rows > 0) evx_es_noise_grad(key.data_ptr<int64_t>(), w.data_ptr<float>(), rows, d, row0, chunks, partial.data_ptr<float>(), cur_stream());
+  else partial.zero_();
+  return partial.sum(0);
+}
+
 // ---- K17 / K18 (mo_geom.hip)
 std::vector<at::Tensor> knn(const at::Tensor& X, const at::Tensor& Y, int64_t T) {
   for (auto* t : {&X, &Y}) { CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t); }
@@ -722,6 +736,7 @@ at::Tensor hv_contrib(const at::Tensor& S, const at::Tensor& P, const at::Tensor
 }
 
 TORCH_LIBRARY(evoxmi, m) {
+  m.def("es_noise_grad(Tensor key, Tensor w, int d, int row0) -> Tensor");
   m.def("knn(Tensor X, Tensor Y, int T) -> Tensor[]");
   m.def("hv_count(Tensor S, Tensor P, int strict) -> Tensor");
   m.def("hv_contrib(Tensor S, Tensor P, Tensor count, Tensor alpha) -> Tensor");
@@ -798,6 +813,7 @@ TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
   m.impl("sbr_block", &sbr_block);
   m.impl("sbr_far", &sbr_far);
   m.impl("sbr_bq", &sbr_bq);
+  m.impl("es_noise_grad", &es_noise_grad);
   m.impl("knn", &knn);
   m.impl("hv_count", &hv_count);
   m.impl("hv_contrib", &hv_contrib);

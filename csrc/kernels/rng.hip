@@ -76,3 +76,40 @@ void evx_philox_words(const int64_t* key, int64_t nblocks, uint32_t domain, int6
   const dim3 grid(gx, batch);
   philox_words_kernel<<<grid, 256, 0, s>>>(key, nblocks, domain, offset, out);
 }
+
+// ---------------------------------------------------------------------------------------
+// OpenES gradient with regenerated noise: partial[c][j] = Σ_{i in chunk c}
+// w[i] · ε(i, j), with ε(i, j) = normal(key, element (row0 + i)·d + j) — exactly the value
+// `normal(key, (rows, d), offset=row0·d)[i, j]` that `ask` drew — so `tell` never stores
+// the N×P noise matrix.  One column per thread, chunks of rows per grid.y (partials summed
+// in a fixed order on the host side: deterministic).
+namespace {
+__global__ void __launch_bounds__(256) es_noise_grad_kernel(const int64_t* __restrict__ key, const float* __restrict__ w, int64_t rows,
+                                                            int64_t d, int64_t row0, int64_t per, float* __restrict__ partial) {
+  uint32_t k0, k1;
+  evx::load_key(key, k0, k1);
+  const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t c = blockIdx.y;
+  if (j >= d) return;
+  const int64_t i0 = c * per, i1 = min(rows, i0 + per);
+  float acc = 0.f;
+  for (int64_t i = i0; i < i1; ++i) {
+    const uint64_t e = (uint64_t)((row0 + i) * d + j);
+    const evx::u4 b = evx::philox_block(e >> 2, k0, k1);
+    // the Box–Muller pair of element e only (same operations as evx::normal4)
+    const int q = (int)(e & 3);
+    const float r = sqrtf(-2.0f * logf(evx::u24(q < 2 ? b.x : b.z)));
+    float sn, cs;
+    sincosf(6.283185307179586f * evx::u24(q < 2 ? b.y : b.w), &sn, &cs);
+    acc = fmaf(w[i], r * ((q & 1) ? sn : cs), acc);
+  }
+  partial[c * d + j] = acc;
+}
+}  // namespace
+
+void evx_es_noise_grad(const int64_t* key, const float* w, int64_t rows, int64_t d, int64_t row0, int chunks, float* partial,
+                       hipStream_t s) {
+  const int64_t per = (rows + chunks - 1) / chunks;
+  const dim3 grid((unsigned)((d + 255) / 256), (unsigned)chunks);
+  es_noise_grad_kernel<<<grid, 256, 0, s>>>(key, w, rows, d, row0, per, partial);
+}

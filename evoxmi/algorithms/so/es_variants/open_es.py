@@ -1,13 +1,16 @@
 """OpenES (Salimans et al. 2017; reference ``es_variants/open_es.py:19-82``).
 
-Mirrored sampling ``ε, −ε``, gradient ``εᵀ f / (N σ)`` (one GEMV on the matrix
-cores via hipBLAS), plain SGD step or an optimiser sub-module (``optimizer='adam'``).
+Mirrored sampling ``ε, −ε``, gradient ``εᵀ f / (N σ)``, plain SGD step or an optimiser
+sub-module (``optimizer='adam'``).  The noise matrix is never stored: ``ask``
+keeps only its Philox key, and ``tell`` regenerates ε(i, j) inside the gradient kernel
+(``rng.hip: es_noise_grad_kernel``, one fused pass; mirrored pairs folded into the
+weights ``f_i − f_{i+N/2}``).  At pop 8192 × 6 k parameters that drops a 200 MB buffer.
 
 SPMD protocol (north-star config 4, population sharded over the GPUs of a node):
-``ask_sharded`` regenerates only this rank's rows of the (virtual, mirrored) noise
-matrix from the Philox counters — row ``g`` is ``half[g]`` or ``−half[g − N/2]``
-exactly as in ``ask`` — and ``tell_sharded`` all-reduces the rank's partial
-gradient ``ε_localᵀ f_local`` (P floats) over RCCL; the centre/optimiser state
+``ask_sharded`` generates only this rank's rows of the (virtual, mirrored) noise matrix
+from the Philox counters — row ``g`` is ``half[g]`` or ``−half[g − N/2]`` exactly as in
+``ask`` — and ``tell_sharded`` regenerates the same rows inside the gradient kernel and
+all-reduces the rank's partial gradient (P floats) over RCCL; the centre/optimiser state
 stays replicated and bit-identical on every rank.
 """
 from __future__ import annotations
@@ -15,12 +18,34 @@ from __future__ import annotations
 import torch
 
 from ....core import Algorithm, State, use_state
+from ....ops import _ext
 from ....ops import random as rnd
 from ._common import make_optimizer
 
 
+def _normal_rows(key, rows: int, d: int, row0: int, dev):
+    """Rows [row0, row0 + rows) of the virtual normal matrix normal(key, (·, d)).  On the
+    device always through the Philox fill kernel (the same Box–Muller arithmetic as the
+    gradient kernel's regeneration, bit for bit)."""
+    if dev.type == "cuda":
+        off = row0 * d
+        lead = off & 3
+        flat = _ext.philox_fill(key.to(dev).contiguous(), rows * d + lead, 1, off - lead)
+        return flat[lead:].reshape(rows, d)
+    return rnd.normal(key, (rows, d), offset=row0 * d).to(dev)
+
+
+def _noise_grad(key, w, d: int, row0: int, dev):
+    """Σ_i w[i] · normal(key)[row0 + i, :] without materialising the rows on the device."""
+    if w.numel() == 0:
+        return torch.zeros(d, device=dev)
+    if dev.type == "cuda":
+        return _ext.ops().es_noise_grad(key.to(dev).contiguous(), w.to(torch.float32).contiguous(), int(d), int(row0))
+    return _normal_rows(key, w.shape[0], d, row0, dev).T @ w.to(torch.float32)
+
+
 class OpenES(Algorithm):
-    rank_local_fields = ("population", "noise")
+    rank_local_fields = ("population",)
 
     def __init__(self, center_init, pop_size, learning_rate, noise_stdev, optimizer=None, mirrored_sampling=True):
         super().__init__()
@@ -37,21 +62,35 @@ class OpenES(Algorithm):
 
     def setup(self, key):
         pop = self.center_init.expand(self.pop_size, -1).clone()
-        return State(population=pop, center=self.center_init.clone(), noise=pop.clone(), key=key)
+        return State(population=pop, center=self.center_init.clone(), noise_key=key.clone(), key=key)
 
     def ask(self, state):
         key, noise_key = rnd.split(state.key)
         dev = state.center.device
-        if self.mirrored_sampling:
-            half = rnd.normal(noise_key, (self.pop_size // 2, self.dim)).to(dev)
-            noise = torch.cat([half, -half], 0)
-        else:
-            noise = rnd.normal(noise_key, (self.pop_size, self.dim)).to(dev)
-        population = state.center[None, :] + self.noise_stdev * noise
-        return population, state.update(population=population, key=key, noise=noise)
+        population = state.center[None, :] + self.noise_stdev * self._noise_rows(noise_key, 0, self.pop_size, dev)
+        return population, state.update(population=population, key=key, noise_key=noise_key.to(state.noise_key.device))
+
+    def _grad_rows(self, noise_key, fitness, start: int, size: int, dev):
+        """Σ over global rows [start, start + size) of f_g ε_g (f indexed by global row)."""
+        d = self.dim
+        f = fitness.to(torch.float32)
+        if not self.mirrored_sampling:
+            return _noise_grad(noise_key, f[start : start + size], d, start, dev)
+        h = self.pop_size // 2
+        g = torch.zeros(d, device=dev)
+        a0, a1 = start, min(start + size, h)
+        b0, b1 = max(start, h), start + size
+        if a1 > a0 and b0 == h and b1 - h == a1 - a0 and a0 == 0:
+            # whole population on one rank: mirrored pairs folded into one pass
+            return _noise_grad(noise_key, f[:h] - f[h:], d, 0, dev)
+        if a1 > a0:
+            g = g + _noise_grad(noise_key, f[a0:a1], d, a0, dev)
+        if b1 > b0:
+            g = g - _noise_grad(noise_key, f[b0:b1], d, b0 - h, dev)
+        return g
 
     def tell(self, state, fitness):
-        grad = (state.noise.T @ fitness) / self.pop_size / self.noise_stdev
+        grad = self._grad_rows(state.noise_key, fitness, 0, self.pop_size, state.center.device) / self.pop_size / self.noise_stdev
         if self.optimizer is None:
             center = state.center - self.learning_rate * grad
         else:
@@ -61,29 +100,29 @@ class OpenES(Algorithm):
 
     # ------------------------------------------------------------------ SPMD protocol
     def _noise_rows(self, key, start: int, size: int, dev):
+        """Global rows [start, start + size) of the (mirrored) noise matrix."""
         d = self.dim
         if not self.mirrored_sampling:
-            return rnd.normal(key, (size, d), offset=start * d).to(dev)
+            return _normal_rows(key, size, d, start, dev)
         h = self.pop_size // 2
         parts = []
         a0, a1 = start, min(start + size, h)
         if a1 > a0:
-            parts.append(rnd.normal(key, (a1 - a0, d), offset=a0 * d).to(dev))
+            parts.append(_normal_rows(key, a1 - a0, d, a0, dev))
         b0, b1 = max(start, h) - h, start + size - h
         if b1 > b0:
-            parts.append(-rnd.normal(key, (b1 - b0, d), offset=b0 * d).to(dev))
+            parts.append(-_normal_rows(key, b1 - b0, d, b0, dev))
         return parts[0] if len(parts) == 1 else torch.cat(parts, 0)
 
     def ask_sharded(self, state, dist):
         start, size = dist.slice_of(self.pop_size)
         key, noise_key = rnd.split(state.key)
-        noise = self._noise_rows(noise_key, start, size, state.center.device)
-        population = state.center[None, :] + self.noise_stdev * noise
-        return population, state.update(population=population, key=key, noise=noise)
+        population = state.center[None, :] + self.noise_stdev * self._noise_rows(noise_key, start, size, state.center.device)
+        return population, state.update(population=population, key=key, noise_key=noise_key.to(state.noise_key.device))
 
     def tell_sharded(self, state, fitness, dist):
         start, size = dist.slice_of(self.pop_size)
-        g = state.noise.T @ fitness[start : start + size].to(state.noise.dtype)
+        g = self._grad_rows(state.noise_key, fitness, start, size, state.center.device)
         dist.all_reduce_(g)
         grad = g / self.pop_size / self.noise_stdev
         if self.optimizer is None:

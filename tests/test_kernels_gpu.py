@@ -823,3 +823,36 @@ def test_igd_and_moead_neighbors_use_knn_kernel():
 
     w = UniformSampling(1000, 3)()[0].float()
     assert torch.equal(nearest_neighbors(w.cuda(), 20).cpu(), nearest_neighbors(w, 20))
+
+
+# ---------------------------------------------------------------- K16: OpenES noise regeneration
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows,d,row0", [(4096, 1000, 0), (1000, 6211, 37), (7, 3, 5)])
+def test_es_noise_grad_regenerates_ask_noise(rows, d, row0):
+    from evoxmi.algorithms.so.es_variants.open_es import _noise_grad, _normal_rows
+    from evoxmi.ops import random as rnd
+
+    key = rnd.PRNGKey(rows + d, device=torch.device("cuda"))
+    w = torch.randn(rows, generator=torch.Generator().manual_seed(1)).cuda()
+    eps = _normal_rows(key, rows, d, row0, torch.device("cuda"))  # what ask() samples
+    ref = (eps.double().T @ w.double()).float()
+    g = _noise_grad(key, w, d, row0, torch.device("cuda"))
+    assert torch.allclose(g, ref, rtol=1e-4, atol=1e-4 * float(ref.abs().max()))
+
+
+@pytest.mark.gpu
+def test_open_es_gpu_matches_stored_noise_update():
+    """One OpenES generation on the GPU with regenerated noise equals the update computed
+    from the explicitly stored mirrored noise."""
+    from evoxmi import random as rnd
+    from evoxmi.algorithms import OpenES
+
+    dev = torch.device("cuda")
+    algo = OpenES(torch.zeros(300, device=dev), 64, learning_rate=0.1, noise_stdev=0.5)
+    st = algo.init(rnd.PRNGKey(3, device=dev))
+    pop, st = algo.ask(st)
+    f = (pop * pop).sum(1)
+    st2 = algo.tell(st, f)
+    eps = (pop - st.center) / 0.5
+    grad = (eps.T @ f) / 64 / 0.5
+    assert torch.allclose(st2.center, st.center - 0.1 * grad, rtol=1e-4, atol=1e-4)

@@ -137,7 +137,7 @@ def _sharded_openes_worker(rank, world, port, out):
     wf = StdWorkflow(OpenES(torch.full((9,), 2.0), 30, learning_rate=0.05, noise_stdev=0.3, optimizer="adam"), Sphere())
     st = wf.init(rnd.PRNGKey(5))
     st = wf.enable_distributed(st)
-    assert st.get_child_state("algorithm").noise.shape[0] == 10  # rank-local rows only
+    assert st.get_child_state("algorithm").population.shape[0] == 10  # rank-local rows only
     for _ in range(12):
         st = wf.step(st)
     out[rank] = st.get_child_state("algorithm").center.clone()
