@@ -1,0 +1,357 @@
+// Sorted-block refinement with 16-wide blocks in a cyclically shifted sorted order (K4, v3).
+//
+// The block step of SBR (eigh_sbr.hip) diagonalises the near (clustered) pairs of the
+// sorted diagonal exactly.  With 64-wide blocks that is 126 dependent Jacobi rounds per
+// iteration in 16 workgroups (≈134 µs, a third of the converged solve): the chip idles
+// on a latency chain.  Measured on CMA-ES matrices at d = 1000 (CPU reference, five
+// generation depths), 16-wide blocks with a far-pair threshold of thr_fac = 0.5 converge in
+// the same number of refinement iterations once past the first generations (4 at gens 25 /
+// 40; 26 vs 24 iterations summed over gens 4-40), because the far step's atan generator
+// already handles every pair whose gap exceeds 8·thr_fac·spread/n.  A 16×16 block is 30
+// rounds of one wave, ~60 workgroups instead of 16.
+//
+// Layout: position j of the shifted sorted order is index perm[j] = argsort(diag)[(j + shift)
+// mod n]; blocks are always [16k, 16k + 16) of that order (shift = 0 / 8 on alternate
+// iterations so that rank-adjacent pairs share a block in one of two iterations).  Because
+// the blocks are aligned, the generator / Bq kernels work on 64×64 tiles that contain
+// exactly four blocks and contract only over 16-wide block-diagonal factors (4× fewer
+// FMAs than a dense 64-wide product).
+//
+//   sbr16_rank_kernel   perm by rank counting (strict total order on (diag, index))
+//   sbr16_block_kernel  one wave per 16-block: 2 cyclic Jacobi sweeps in LDS → Q, dq
+//   sbr16_far_kernel    X = ½·atan(2·A1/(d_e − d_c)) on far cross-block pairs,
+//                       A1 = blockdiag(Q)ᵀ A[perm, perm] blockdiag(Q)
+//   sbr16_bq_kernel     Bq = B[:, perm] · blockdiag(Q)
+// evoxmi/ops/sbr.py holds the torch reference of each step and the host driver.
+#include "evoxmi_common.h"
+#include <float.h>
+#include <math.h>
+
+namespace {
+
+constexpr int SB = 16;            // block size
+constexpr int SP = 17;            // LDS pitch of a block (odd: conflict-free columns)
+constexpr int TL = 64;            // tile of the generator / Bq kernels (four blocks)
+constexpr int TP = 68;            // LDS pitch of a 64-wide tile (float4 aligned)
+constexpr int kRankMax = 8192;    // largest n of the rank kernel (32 KB of keys in LDS)
+
+__device__ __forceinline__ float sort_key(float v) { return isnan(v) ? INFINITY : v; }
+
+// ------------------------------------------------------------------ 1. ranks → shifted perm
+// 64 indices per workgroup, the 4 waves each count over a quarter of the keys
+__global__ void __launch_bounds__(256) sbr16_rank_kernel(const float* __restrict__ A, int n, int64_t lda, int shift,
+                                                         int* __restrict__ perm) {
+  __shared__ float key[kRankMax];
+  __shared__ int part[4][64];
+  for (int i = threadIdx.x; i < n; i += blockDim.x) key[i] = sort_key(A[(int64_t)i * lda + i]);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + lane;
+  const float ki = i < n ? key[i] : 0.f;
+  const int q = (n + 3) >> 2, j0 = w * q, j1 = min(n, j0 + q);
+  int cnt = 0;
+  for (int j = j0; j < j1; ++j) {
+    const float kj = key[j];  // same address across the wave: LDS broadcast
+    cnt += (kj < ki) | ((kj == ki) & (j < i));
+  }
+  part[w][lane] = cnt;
+  __syncthreads();
+  if (w == 0 && i < n) {
+    const int r = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
+    int pos = r - shift;
+    if (pos < 0) pos += n;
+    perm[pos] = i;
+  }
+}
+
+// circle-method round robin on 16 slots: round r pairs (15, r) and ((r+i) mod 15, (r−i) mod 15)
+__device__ __forceinline__ int2 rr16(int r, int i) {
+  int a = SB - 1, b = r;
+  if (i) {
+    a = r + i;
+    if (a >= SB - 1) a -= SB - 1;
+    b = r - i;
+    if (b < 0) b += SB - 1;
+  }
+  return make_int2(min(a, b), max(a, b));
+}
+
+// (c, s, t) of the Jacobi rotation annihilating [[app, apq], [apq, aqq]]; only on a
+// normal-range coupling (a denormal apq would overflow the reciprocal)
+__device__ __forceinline__ float3 rot16(float app, float aqq, float apq) {
+  const bool on = fabsf(apq) >= FLT_MIN;
+  const float theta = (aqq - app) * (0.5f * __builtin_amdgcn_rcpf(on ? apq : 1.f));
+  float t = copysignf(__builtin_amdgcn_rcpf(fabsf(theta) + __builtin_amdgcn_sqrtf(fmaf(theta, theta, 1.f))), theta);
+  t = on ? t : 0.f;
+  const float c = __builtin_amdgcn_rsqf(fmaf(t, t, 1.f));
+  return make_float3(c, t * c, t);
+}
+
+// ------------------------------------------------------------------ 2. block solve
+// One wave per block.  Per round: lanes 0-7 compute the 8 rotations (→ LDS), then lane
+// {u ≤ v} (36 items) forms the 2×2 blocks (u, v) and (v, u) of S' = Jᵀ S J (written as exact
+// transposes: S stays symmetric; pair u's own block set exactly), and every lane rotates a
+// 2×2 block of Q' = Q J (rows 2(L/8)+{0,1}, column pair L mod 8).  All updates are in place:
+// the 2×2 blocks of one round partition S and Q.
+__global__ void __launch_bounds__(64) sbr16_block_kernel(const float* __restrict__ A, int n, int64_t lda,
+                                                         const int* __restrict__ perm, int sweeps, float* __restrict__ Q_out,
+                                                         float* __restrict__ dq_out) {
+  __shared__ float S[SB * SP];
+  __shared__ float Qm[SB * SP];
+  __shared__ float4 rot[SB / 2];
+  __shared__ int members[SB];
+  const int lane = threadIdx.x;
+  const int s0 = blockIdx.x * SB, m = min(SB, n - s0);
+  if (lane < SB) members[lane] = lane < m ? perm[s0 + lane] : -1;
+  __syncthreads();
+#pragma unroll
+  for (int e = lane; e < SB * SB; e += 64) {
+    const int a = e >> 4, c = e & 15;
+    const int ra = members[a], rc = members[c];
+    S[a * SP + c] = (ra >= 0 && rc >= 0) ? A[(int64_t)ra * lda + rc] : 0.f;
+    Qm[a * SP + c] = a == c ? 1.f : 0.f;
+  }
+  __syncthreads();
+  // item {u ≤ v} of the lane (36 of them; lanes 36..63 only rotate Q)
+  int u = 0, rem = lane;
+  while (u < SB / 2 - 1 && rem >= SB / 2 - u) {
+    rem -= SB / 2 - u;
+    ++u;
+  }
+  const int v = u + rem;
+  const bool item = lane < (SB / 2) * (SB / 2 + 1) / 2;
+  const bool dg = u == v;
+  const int qr = (lane >> 3) * 2, qv = lane & 7;  // Q rows qr, qr+1; column pair qv
+  const int G = (SB - 1) * sweeps;
+  for (int g = 0; g < G; ++g) {
+    const int r = g % (SB - 1);
+    if (lane < SB / 2) {
+      const int2 p = rr16(r, lane);
+      const float3 cs = rot16(S[p.x * SP + p.x], S[p.y * SP + p.y], S[p.x * SP + p.y]);
+      rot[lane] = make_float4(cs.x, cs.y, cs.z, 0.f);
+    }
+    __syncthreads();
+    {
+      const int2 pq = rr16(r, qv);
+      const float4 rq = rot[qv];
+      const float x0 = Qm[qr * SP + pq.x], y0 = Qm[qr * SP + pq.y];
+      const float x1 = Qm[(qr + 1) * SP + pq.x], y1 = Qm[(qr + 1) * SP + pq.y];
+      Qm[qr * SP + pq.x] = rq.x * x0 - rq.y * y0;
+      Qm[qr * SP + pq.y] = rq.y * x0 + rq.x * y0;
+      Qm[(qr + 1) * SP + pq.x] = rq.x * x1 - rq.y * y1;
+      Qm[(qr + 1) * SP + pq.y] = rq.y * x1 + rq.x * y1;
+    }
+    if (item) {
+      const int2 pu = rr16(r, u), pv = rr16(r, v);
+      const float4 ru = rot[u], rv = rot[v];
+      const int ux = pu.x * SP, uy = pu.y * SP, vx = pv.x * SP, vy = pv.y * SP;
+      const float a = S[ux + pv.x], b = S[ux + pv.y], c = S[uy + pv.x], d = S[uy + pv.y];
+      // O = J_uᵀ S[u rows, v cols] J_v: columns first (p' = c·p − s·q, q' = s·p + c·q), then rows
+      const float a1 = rv.x * a - rv.y * b, b1 = rv.y * a + rv.x * b;
+      const float c1 = rv.x * c - rv.y * d, d1 = rv.y * c + rv.x * d;
+      float o00 = ru.x * a1 - ru.y * c1, o01 = ru.x * b1 - ru.y * d1;
+      float o10 = ru.y * a1 + ru.x * c1, o11 = ru.y * b1 + ru.x * d1;
+      o00 = dg ? a - ru.z * b : o00;
+      o11 = dg ? d + ru.z * b : o11;
+      o01 = dg ? 0.f : o01;
+      o10 = dg ? 0.f : o10;
+      S[ux + pv.x] = o00;
+      S[ux + pv.y] = o01;
+      S[uy + pv.x] = o10;
+      S[uy + pv.y] = o11;
+      if (!dg) {
+        S[vx + pu.x] = o00;
+        S[vy + pu.x] = o01;
+        S[vx + pu.y] = o10;
+        S[vy + pu.y] = o11;
+      }
+    }
+    __syncthreads();
+  }
+  float* Qo = Q_out + (int64_t)blockIdx.x * SB * SB;
+#pragma unroll
+  for (int e = lane; e < SB * SB; e += 64) Qo[e] = Qm[(e >> 4) * SP + (e & 15)];
+  if (lane < m) dq_out[s0 + lane] = S[lane * SP + lane];
+}
+
+// ------------------------------------------------------------------ block-diagonal tile helpers
+// Qt[a][c] (64×64 in LDS, pitch TP) = blockdiag of the four 16×16 Q blocks of tile t (0 elsewhere
+// is never read: the contractions below stay inside a block)
+__device__ __forceinline__ void load_qtile(const float* __restrict__ Q, int nb, int t, float* Qt) {
+  for (int e = threadIdx.x; e < 4 * SB * SB; e += blockDim.x) {
+    const int blk = e >> 8, a = (e >> 4) & 15, c = e & 15;
+    const int gb = 4 * t + blk;
+    Qt[(blk * SB + a) * TP + blk * SB + c] = gb < nb ? Q[(int64_t)gb * SB * SB + a * SB + c] : (a == c ? 1.f : 0.f);
+  }
+}
+
+// ------------------------------------------------------------------ 3. far-pair generator
+__global__ void __launch_bounds__(256) sbr16_far_kernel(const float* __restrict__ A, int n, int64_t lda,
+                                                        const int* __restrict__ perm, const float* __restrict__ Q,
+                                                        const float* __restrict__ dq, const double* __restrict__ stats,
+                                                        float thr_fac, float theta, float* __restrict__ X, int64_t ldx) {
+  __shared__ __attribute__((aligned(16))) float G[TL * TP];
+  __shared__ __attribute__((aligned(16))) float Qk[TL * TP];
+  __shared__ __attribute__((aligned(16))) float Ql[TL * TP];
+  __shared__ int pk[TL], pl[TL];
+  __shared__ float dk[TL], dl[TL], tk[TL], tl[TL];
+  const int K = blockIdx.y, L = blockIdx.x;
+  const int nb = (n + SB - 1) / SB;
+  const int sk = K * TL, sl = L * TL;
+  const int mk = min(TL, n - sk), ml = min(TL, n - sl);
+  const float gthr = thr_fac * (0.5f * SB) * (float)(stats[3] - stats[2]) / (float)n;
+  if (threadIdx.x < 2 * TL) {
+    // per position: global threshold capped by the local one (local_threshold in sbr.py)
+    const int t = threadIdx.x & (TL - 1), side = threadIdx.x >> 6;
+    const int s0 = side ? sl : sk, mm = side ? ml : mk, j = s0 + t;
+    float d = 0.f, th = gthr;
+    if (t < mm) {
+      d = dq[j];
+      if (theta > 0.f) {
+        const float up = j + SB / 2 < n ? fabsf(dq[j + SB / 2] - d) : INFINITY;
+        const float dn = j >= SB / 2 ? fabsf(d - dq[j - SB / 2]) : INFINITY;
+        th = fminf(th, theta * fminf(up, dn));
+      }
+    }
+    if (side) {
+      pl[t] = t < mm ? perm[j] : -1;
+      dl[t] = d;
+      tl[t] = th;
+    } else {
+      pk[t] = t < mm ? perm[j] : -1;
+      dk[t] = d;
+      tk[t] = th;
+    }
+  }
+  load_qtile(Q, nb, K, Qk);
+  load_qtile(Q, nb, L, Ql);
+  __syncthreads();
+  for (int e = threadIdx.x; e < TL * TL; e += blockDim.x) {
+    const int a = e >> 6, f = e & 63;
+    const int ra = pk[a], rf = pl[f];
+    G[a * TP + f] = (ra >= 0 && rf >= 0) ? A[(int64_t)ra * lda + rf] : 0.f;
+  }
+  __syncthreads();
+  const int r0 = (threadIdx.x >> 4) << 2, c0 = (threadIdx.x & 15) << 2;
+  // T[c][f] = Σ_{a in block(c)} Qk[a][c] G[a][f]: rows r0..r0+3 share one block
+  float acc[4][4] = {};
+  const int ab = r0 & ~15;
+#pragma unroll
+  for (int a = 0; a < SB; ++a) {
+    const float4 lq = *(const float4*)(Qk + (ab + a) * TP + r0);
+    const float4 g = *(const float4*)(G + (ab + a) * TP + c0);
+    const float l[4] = {lq.x, lq.y, lq.z, lq.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      acc[i][0] = fmaf(l[i], g.x, acc[i][0]);
+      acc[i][1] = fmaf(l[i], g.y, acc[i][1]);
+      acc[i][2] = fmaf(l[i], g.z, acc[i][2]);
+      acc[i][3] = fmaf(l[i], g.w, acc[i][3]);
+    }
+  }
+  __syncthreads();  // all reads of G done: T overwrites it
+#pragma unroll
+  for (int i = 0; i < 4; ++i) *(float4*)(G + (r0 + i) * TP + c0) = make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
+  __syncthreads();
+  // A1[c][e] = Σ_{f in block(e)} T[c][f] Ql[f][e]
+  float out[4][4] = {};
+  const int fb = c0 & ~15;
+#pragma unroll
+  for (int f = 0; f < SB; ++f) {
+    const float4 q = *(const float4*)(Ql + (fb + f) * TP + c0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float t = G[(r0 + i) * TP + fb + f];
+      out[i][0] = fmaf(t, q.x, out[i][0]);
+      out[i][1] = fmaf(t, q.y, out[i][1]);
+      out[i][2] = fmaf(t, q.z, out[i][2]);
+      out[i][3] = fmaf(t, q.w, out[i][3]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = r0 + i;
+    if (c >= mk) continue;
+    const int bc = (sk + c) >> 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int e = c0 + j;
+      if (e >= ml) continue;
+      const float den = dl[e] - dk[c];
+      // the 2×2 Jacobi angle ½·atan(2a/den): a/den to first order for well-separated pairs,
+      // saturating at π/4 for strongly coupled ones
+      const bool far = ((sl + e) >> 4) != bc && fabsf(den) > fminf(tk[c], tl[e]);
+      X[(int64_t)(sk + c) * ldx + sl + e] = far ? 0.5f * atanf(2.f * out[i][j] / den) : 0.f;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ 4. Bq = B[:, perm]·blockdiag(Q)
+__global__ void __launch_bounds__(256) sbr16_bq_kernel(const float* __restrict__ B, int rows, int n, int64_t ldb,
+                                                       const int* __restrict__ perm, const float* __restrict__ Q,
+                                                       float* __restrict__ Bq, int64_t ldq) {
+  __shared__ __attribute__((aligned(16))) float G[TL * TP];
+  __shared__ __attribute__((aligned(16))) float Ql[TL * TP];
+  __shared__ int pl[TL];
+  const int rt = blockIdx.y, L = blockIdx.x;
+  const int nb = (n + SB - 1) / SB;
+  const int sl = L * TL, ml = min(TL, n - sl);
+  if (threadIdx.x < TL) pl[threadIdx.x] = threadIdx.x < ml ? perm[sl + threadIdx.x] : -1;
+  load_qtile(Q, nb, L, Ql);
+  __syncthreads();
+  for (int e = threadIdx.x; e < TL * TL; e += blockDim.x) {
+    const int r = e >> 6, f = e & 63;
+    const int row = rt * TL + r, col = pl[f];
+    G[r * TP + f] = (row < rows && col >= 0) ? B[(int64_t)row * ldb + col] : 0.f;
+  }
+  __syncthreads();
+  const int r0 = (threadIdx.x >> 4) << 2, c0 = (threadIdx.x & 15) << 2;
+  const int fb = c0 & ~15;
+  float out[4][4] = {};
+#pragma unroll
+  for (int f = 0; f < SB; ++f) {
+    const float4 q = *(const float4*)(Ql + (fb + f) * TP + c0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float g = G[(r0 + i) * TP + fb + f];
+      out[i][0] = fmaf(g, q.x, out[i][0]);
+      out[i][1] = fmaf(g, q.y, out[i][1]);
+      out[i][2] = fmaf(g, q.z, out[i][2]);
+      out[i][3] = fmaf(g, q.w, out[i][3]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = rt * TL + r0 + i;
+    if (row >= rows) continue;
+    if (c0 + 3 < ml) {
+      *(float4*)(Bq + (int64_t)row * ldq + sl + c0) = make_float4(out[i][0], out[i][1], out[i][2], out[i][3]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (c0 + j < ml) Bq[(int64_t)row * ldq + sl + c0 + j] = out[i][j];
+    }
+  }
+}
+
+}  // namespace
+
+int evx_sbr16_nblocks(int n) { return (n + SB - 1) / SB; }
+int evx_sbr16_max_n() { return kRankMax; }
+
+void evx_sbr16_block(const float* A, int n, int64_t lda, int shift, int sweeps, int* perm, float* Q, float* dq, hipStream_t s) {
+  sbr16_rank_kernel<<<(n + 63) / 64, 256, 0, s>>>(A, n, lda, shift, perm);
+  sbr16_block_kernel<<<(n + SB - 1) / SB, 64, 0, s>>>(A, n, lda, perm, sweeps, Q, dq);
+}
+
+void evx_sbr16_far(const float* A, int n, int64_t lda, const int* perm, const float* Q, const float* dq, const double* stats,
+                   float thr_fac, float theta, float* X, int64_t ldx, hipStream_t s) {
+  const int nt = (n + TL - 1) / TL;
+  sbr16_far_kernel<<<dim3(nt, nt), 256, 0, s>>>(A, n, lda, perm, Q, dq, stats, thr_fac, theta, X, ldx);
+}
+
+void evx_sbr16_bq(const float* B, int rows, int n, int64_t ldb, const int* perm, const float* Q, float* Bq, int64_t ldq,
+                  hipStream_t s) {
+  const int nt = (n + TL - 1) / TL;
+  sbr16_bq_kernel<<<dim3(nt, (rows + TL - 1) / TL), 256, 0, s>>>(B, rows, n, ldb, perm, Q, Bq, ldq);
+}

@@ -44,7 +44,7 @@ def sbr_phase(C: torch.Tensor, B_prev: torch.Tensor):
     from .. import config
     from . import sbr
 
-    w, B, info = sbr.eigh_warm(C, B_prev, sbr.SBRConfig(tol=config.get("eigh_tol")))
+    w, B, info = sbr.eigh_warm(C, B_prev, sbr.SBRConfig(tol=config.get("eigh_tol"), block=config.get("sbr_block")))
     HISTORY.append(info)
     st = torch.tensor([info.off_rel, info.jacobi_sweeps, info.refine_iters, float(info.fallback)], dtype=torch.float64)
     return w, B, st.to(C.device, non_blocking=True)

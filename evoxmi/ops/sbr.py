@@ -152,6 +152,73 @@ def bq_ref(B, off, perm, Q):
     return B[:, perm.long()] @ _blockdiag(Q, B.shape[1], off)
 
 
+# ------------------------------------------------- 16-wide blocks, shifted sorted order
+# (csrc/kernels/eigh_sbr16.hip): position j of the order is index argsort(diag)[(j + shift)
+# mod n] and blocks are always [16k, 16k + 16) — shift 0 / 8 on alternate iterations.
+SB = 16
+
+
+def perm_shift_ref(A: torch.Tensor, shift: int) -> torch.Tensor:
+    d = torch.diagonal(A)
+    d = torch.where(torch.isnan(d), torch.full_like(d, float("inf")), d)
+    perm = torch.argsort(d, stable=True).to(torch.int32)
+    return torch.roll(perm, -(shift % A.shape[0]))
+
+
+def block_solve16_ref(A: torch.Tensor, shift: int, sweeps: int):
+    n = A.shape[0]
+    perm = perm_shift_ref(A, shift)
+    nb = (n + SB - 1) // SB
+    S = torch.zeros(nb, SB, SB, dtype=A.dtype, device=A.device)
+    for k in range(nb):
+        idx = perm[k * SB : (k + 1) * SB].long()
+        m = idx.numel()
+        S[k, :m, :m] = A[idx][:, idx]
+    S, Q = _block_jacobi_ref(S, sweeps)
+    dq = torch.diagonal(S, dim1=1, dim2=2).reshape(-1)[:n]
+    return perm, Q.contiguous(), dq.contiguous()
+
+
+def _blockdiag16(Q: torch.Tensor, n: int) -> torch.Tensor:
+    return torch.block_diag(*Q.unbind(0))[:n, :n]
+
+
+LOCAL_THETA = 0.5
+
+
+def local_threshold(dq: torch.Tensor, theta: float = None) -> torch.Tensor:
+    """θ·min(|d[j+8] − d[j]|, |d[j] − d[j−8]|) at every position j of the order.  A pair whose
+    gap is below both ends' local thresholds is less than half a block apart, so one of
+    the two shifts puts it in a common block: every pair is either rotated by a block solve
+    or by the far step, even inside clusters denser than the global threshold assumes."""
+    theta = LOCAL_THETA if theta is None else theta
+    n = dq.shape[0]
+    h = SB // 2
+    inf = torch.full((h,), float("inf"), dtype=dq.dtype, device=dq.device)
+    up = torch.cat([(dq[h:] - dq[:-h]).abs(), inf]) if n > h else torch.full_like(dq, float("inf"))
+    dn = torch.cat([inf, (dq[h:] - dq[:-h]).abs()]) if n > h else torch.full_like(dq, float("inf"))
+    return theta * torch.minimum(up, dn)
+
+
+def far16_ref(A, perm, Q, dq, stats, thr_fac):
+    n = A.shape[0]
+    p = perm.long()
+    Qf = _blockdiag16(Q, n)
+    A1 = Qf.T @ A[p][:, p] @ Qf
+    blk = torch.arange(n, device=A.device) // SB
+    den = dq[None, :] - dq[:, None]
+    thr = thr_fac * (0.5 * SB) * float(stats[3] - stats[2]) / n
+    thr = torch.full_like(dq, thr)
+    if LOCAL_THETA > 0:
+        thr = torch.minimum(thr, local_threshold(dq))
+    mask = (blk[None, :] != blk[:, None]) & (den.abs() > torch.minimum(thr[:, None], thr[None, :]))
+    return torch.where(mask, 0.5 * torch.atan(2 * A1 / torch.where(mask, den, torch.ones_like(den))), torch.zeros_like(A1))
+
+
+def bq16_ref(B, perm, Q):
+    return B[:, perm.long()] @ _blockdiag16(Q, B.shape[1])
+
+
 # ---------------------------------------------------------------------------- dispatch
 def _dev(t):
     return t.is_cuda
@@ -165,20 +232,30 @@ def stats(A):
     return _ext.ops().sbr_stats(_rowmajor(A)) if _dev(A) else stats_ref(A)
 
 
-def block_solve(A, off, sweeps):
+def block_solve(A, off, sweeps, bk: int = BK):
+    if bk == SB:
+        if _dev(A):
+            return tuple(_ext.ops().sbr16_block(_rowmajor(A), int(off) % A.shape[0], int(sweeps)))
+        return block_solve16_ref(A, off, sweeps)
     if _dev(A):
         perm, Q, dq = _ext.ops().sbr_block(_rowmajor(A), int(off), int(sweeps))
         return perm, Q, dq
     return block_solve_ref(A, off, sweeps)
 
 
-def far(A, off, perm, Q, dq, st, thr_fac):
+def far(A, off, perm, Q, dq, st, thr_fac, bk: int = BK):
+    if bk == SB:
+        if _dev(A):
+            return _ext.ops().sbr16_far(_rowmajor(A), perm, Q, dq, st, float(thr_fac), float(LOCAL_THETA))
+        return far16_ref(A, perm, Q, dq, st, thr_fac)
     if _dev(A):
         return _ext.ops().sbr_far(_rowmajor(A), int(off), perm, Q, dq, st, float(thr_fac))
     return far_ref(A, off, perm, Q, dq, st, thr_fac)
 
 
-def bq(B, off, perm, Q):
+def bq(B, off, perm, Q, bk: int = BK):
+    if bk == SB:
+        return _ext.ops().sbr16_bq(_rowmajor(B), perm, Q) if _dev(B) else bq16_ref(B, perm, Q)
     return _ext.ops().sbr_bq(_rowmajor(B), int(off), perm, Q) if _dev(B) else bq_ref(B, off, perm, Q)
 
 
@@ -267,11 +344,19 @@ class SBRConfig:
     near_only: float = 3.0     # near-only (no far step) iteration once off_rel ≤ near_only·tol
     max_jacobi: int = 16
     block_sweeps: int = 2
-    thr_fac: float = 0.3
+    block: int = SB            # 16: one-wave blocks in a shifted sorted order (eigh_sbr16.hip);
+                               # 64: the 64-wide offset layout (eigh_sbr.hip)
+    thr_fac: float = None      # far-pair threshold factor (default 0.5 for block 16, 0.3 for 64)
     ns_iters: int = 2          # Newton–Schulz re-orthonormalisation in the first iterations and
                                # after every damped one (undamped later ones have ‖X‖₂ ≲ 0.5:
                                # Taylor-6 is orthogonal to ~1e-6 there)
     graphs: bool = True        # replay each device iteration as a captured hipGraph
+
+    def __post_init__(self):
+        if self.thr_fac is None:
+            self.thr_fac = 0.5 if self.block == SB else 0.3
+        if self.block not in (SB, BK):
+            raise ValueError(f"SBR block size must be {SB} or {BK}, got {self.block}")
 
 
 def _read(st: torch.Tensor):
@@ -289,18 +374,18 @@ def _refine_core(C, A, B, st, off: int, ns: bool, damp: bool, cfg: SBRConfig, ou
     and cap the step (the host enables it while κ is large).  ``far_on = False``: a
     near-only iteration (block solves, B ← B[:, perm]·Qblk, A ← BᵀCB) for the last step,
     when the residual is almost entirely near pairs (4 GEMMs fewer)."""
-    perm, Q, dq = block_solve(A, off, cfg.block_sweeps)
+    perm, Q, dq = block_solve(A, off, cfg.block_sweeps, cfg.block)
     alpha = None
     if not far_on:
-        Bn = bq(B, off, perm, Q)
+        Bn = bq(B, off, perm, Q, cfg.block)
         if out:
             out[1].copy_(Bn)
             Bn = out[1]
     else:
-        X = far(A, off, perm, Q, dq, st, cfg.thr_fac)
+        X = far(A, off, perm, Q, dq, st, cfg.thr_fac, cfg.block)
         X2 = X @ X
         alpha = damping(X2, cfg.damp_tau) if damp and cfg.damp_tau > 0 else None
-        Bq = bq(B, off, perm, Q)
+        Bq = bq(B, off, perm, Q, cfg.block)
         V = expm_taylor6(X, X2, alpha)
         if ns:
             Bn = Bq @ V
@@ -321,7 +406,7 @@ def _refine_core(C, A, B, st, off: int, ns: bool, damp: bool, cfg: SBRConfig, ou
 
 def refine_step(C, A, B, st, it: int, cfg: SBRConfig, ns: bool = None, damp: bool = True, far_on: bool = True):
     ns = it < cfg.ns_iters if ns is None else ns
-    return _refine_core(C, A, B, st, (it % 2) * (BK // 2), ns, damp, cfg, far_on=far_on)
+    return _refine_core(C, A, B, st, (it % 2) * (cfg.block // 2), ns, damp, cfg, far_on=far_on)
 
 
 class _Workspace:
@@ -361,7 +446,7 @@ class _Workspace:
         self._capture(("init",), body).replay()
 
     def iterate(self, it: int, ns: bool, damp: bool, far_on: bool = True):
-        off = (it % 2) * (BK // 2)
+        off = (it % 2) * (self.cfg.block // 2)
 
         def body():
             # A, B, stats are written in place (A and B are fully read before the last
@@ -377,7 +462,7 @@ _WS = {}
 
 
 def _workspace(n, dev, cfg) -> _Workspace:
-    k = (n, str(dev), cfg.block_sweeps, cfg.thr_fac, cfg.ns_iters, cfg.damp_tau)
+    k = (n, str(dev), cfg.block, cfg.block_sweeps, cfg.thr_fac, cfg.ns_iters, cfg.damp_tau)
     if k not in _WS:
         _WS[k] = _Workspace(n, dev, cfg)
     return _WS[k]
@@ -451,14 +536,16 @@ def eigh_warm(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None):
     prev = off_rel
     diverged = False
     alpha = 1.0
+    last_far = True
     while off_rel > cfg.tol and it < cfg.max_iters:
         # re-orthonormalise in the first iterations and after a damped (large) step; the
         # ‖X‖₂ estimate runs only while the off-diagonal mass is large against the spread
         # (κ > damp_kappa: converging iterations have ‖X‖₂ ≪ 1 and are never capped)
         ns = it < cfg.ns_iters or alpha < 1.0
         damp = kappa > cfg.damp_kappa
-        # close to the tolerance the residual is near pairs only: skip the far step
-        far_on = not (it > 0 and off_rel <= cfg.near_only * cfg.tol)
+        # close to the tolerance the residual is near pairs only: skip the far step (once:
+        # if a near-only iteration did not reach the tolerance, far pairs are left)
+        far_on = not (it > 0 and off_rel <= cfg.near_only * cfg.tol and last_far)
         if ws is not None:
             ws.iterate(it, ns, damp, far_on)
             A, B, st = ws.A, ws.B, ws.st
@@ -467,6 +554,7 @@ def eigh_warm(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None):
             A, B, st, a = refine_step(C, A, B, st, it, cfg, ns, damp, far_on)
             off_rel, kappa, alpha = _read(torch.cat([st.double(), a.double().reshape(1)]))
         it += 1
+        last_far = far_on
         info.damped += alpha < 1.0
         info.history.append(("refine", off_rel, kappa))
         if not math.isfinite(off_rel) or off_rel > 1.5 * prev:

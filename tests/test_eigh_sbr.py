@@ -78,6 +78,45 @@ def test_refinement_converges_on_cma_like_matrix_cpu():
     assert torch.allclose(torch.sort(w).values, torch.linalg.eigvalsh(C.double()).float(), atol=1e-5)
 
 
+
+@pytest.mark.parametrize("n,shift", [(200, 0), (200, 8), (37, 8), (1000, 8)])
+def test_shifted_layout_reference(n, shift):
+    """16-block layout: perm is the stable argsort rolled by the shift, every block is
+    diagonalised by the reference sweeps and Bq = B[:, perm]·blockdiag(Q)."""
+    C, B = _cma_like(n, 3, seed=n) if n <= 200 else (None, None)
+    if C is None:
+        torch.manual_seed(0)
+        M = torch.randn(n, n)
+        C = M @ M.T / n
+        B = torch.linalg.qr(torch.randn(n, n))[0]
+    A = sbr.sym_product(C, B)
+    perm, Q, dq = sbr.block_solve16_ref(A, shift, 6)
+    ref = torch.roll(torch.argsort(torch.diagonal(A), stable=True), -shift)
+    assert torch.equal(perm.long(), ref)
+    Qf = sbr._blockdiag16(Q, n)
+    A1 = Qf.T @ A[perm.long()][:, perm.long()] @ Qf
+    blk = torch.arange(n) // 16
+    inblock = (blk[:, None] == blk[None, :]) & ~torch.eye(n, dtype=torch.bool)
+    assert float(A1[inblock].abs().max()) < 1e-5 * float(A.abs().max())
+    assert torch.allclose(torch.diagonal(A1), dq, atol=1e-5)
+    assert torch.allclose(sbr.bq16_ref(B, perm, Q), B[:, perm.long()] @ Qf)
+
+
+def test_refinement_block16_converges_cpu():
+    C, B = _cma_like(256, 30)
+    w, Bn, info = sbr.eigh_warm(C, B, sbr.SBRConfig(block=16))
+    assert info.off_rel <= 1e-5, info
+    assert _offrel(Bn.T @ C @ Bn) <= 2e-5
+
+
+def test_near_only_iteration_is_not_repeated():
+    """A near-only iteration (no far step) that misses the tolerance is followed by a
+    full one: the driver must not stall on far-pair residue."""
+    C, B = _cma_like(256, 8, seed=3)
+    w, Bn, info = sbr.eigh_warm(C, B, sbr.SBRConfig(block=16, near_only=1e6))
+    assert info.off_rel <= 1e-5 and info.refine_iters < 16, info
+
+
 # ------------------------------------------------------------------ GPU
 gpu = pytest.mark.gpu
 
@@ -131,6 +170,38 @@ def test_sbr_kernels_match_reference(n, off):
     assert _rel(X, X_r) < 1e-4
     Bq = sbr.bq(B.cuda(), off, perm_r.cuda(), Q_r.cuda()).cpu()
     assert _rel(Bq, sbr.bq_ref(B, off, perm_r, Q_r)) < 1e-5
+
+
+
+@gpu
+@pytest.mark.parametrize("n,shift", [(1000, 0), (1000, 8), (200, 8), (37, 8), (17, 0)])
+def test_sbr16_kernels_match_reference(n, shift):
+    C, B = _cma_like(n, 8, seed=n)
+    A = sbr.sym_product(C, B)
+    st = sbr.stats_ref(A)
+    perm_r, Q_r, dq_r = sbr.block_solve16_ref(A, shift, 2)
+    Ad = A.cuda()
+    perm, Q, dq = sbr.block_solve(Ad, shift, 2, bk=16)
+    assert torch.equal(perm.cpu(), perm_r)
+    Q, dq = Q.cpu(), dq.cpu()
+    assert float((Q.transpose(1, 2) @ Q - torch.eye(16)).abs().max()) < 2e-6
+    p = perm_r.long()
+    for k in range(Q.shape[0]):
+        idx = p[16 * k : 16 * (k + 1)]
+        m = idx.numel()
+        S = A[idx][:, idx]
+        T = Q[k, :m, :m].T @ S @ Q[k, :m, :m]
+        T_r = Q_r[k, :m, :m].T @ S @ Q_r[k, :m, :m]
+        off_k = torch.linalg.matrix_norm(T - torch.diag(torch.diagonal(T)))
+        off_r = torch.linalg.matrix_norm(T_r - torch.diag(torch.diagonal(T_r)))
+        assert off_k <= 1.5 * off_r + 1e-6 * torch.linalg.matrix_norm(S)
+        assert torch.allclose(torch.diagonal(T), dq[16 * k : 16 * k + m], atol=2e-5)
+    X = sbr.far(Ad, shift, perm_r.cuda(), Q_r.cuda(), dq_r.cuda(), st.cuda(), 0.5, bk=16).cpu()
+    X_r = sbr.far16_ref(A, perm_r, Q_r, dq_r, st, 0.5)
+    assert (X.abs() > 0).sum() == (X_r.abs() > 0).sum()
+    assert _rel(X, X_r) < 1e-4
+    Bq = sbr.bq(B.cuda(), shift, perm_r.cuda(), Q_r.cuda(), bk=16).cpu()
+    assert _rel(Bq, sbr.bq16_ref(B, perm_r, Q_r)) < 1e-5
 
 
 @gpu

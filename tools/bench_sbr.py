@@ -48,30 +48,31 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=1000)
     ap.add_argument("--gens", type=int, nargs="*", default=[4, 15, 40])
+    ap.add_argument("--block", type=int, default=16)
     a = ap.parse_args()
     dev = torch.device("cuda")
     C, B = cma_like(a.n, 20, 0, dev)
     A = sbr.sym_product(C, B)
     st = sbr.stats(A)
-    perm, Q, dq = sbr.block_solve(A, 0, 2)
-    X = sbr.far(A, 0, perm, Q, dq, st, 0.3)
-    res = {
-        "stats_us": timeit(lambda: sbr.stats(A)),
-        "block_us": timeit(lambda: sbr.block_solve(A, 0, 2)),
-        "far_us": timeit(lambda: sbr.far(A, 0, perm, Q, dq, st, 0.3)),
-        "bq_us": timeit(lambda: sbr.bq(B, 0, perm, Q)),
-        "gemm_us": timeit(lambda: X @ X),
-        "expm_us": timeit(lambda: sbr.expm_taylor6(X)),
-        "refine_step_us": timeit(lambda: sbr.refine_step(C, A, B, st, 0, sbr.SBRConfig()), reps=10),
-    }
+    res = {"stats_us": timeit(lambda: sbr.stats(A))}
+    for bk in (16, 64):
+        perm, Q, dq = sbr.block_solve(A, 0, 2, bk)
+        X = sbr.far(A, 0, perm, Q, dq, st, 0.3, bk)
+        res.update({
+            f"block{bk}_us": timeit(lambda: sbr.block_solve(A, 0, 2, bk)),
+            f"far{bk}_us": timeit(lambda: sbr.far(A, 0, perm, Q, dq, st, 0.3, bk)),
+            f"bq{bk}_us": timeit(lambda: sbr.bq(B, 0, perm, Q, bk)),
+            f"refine_step{bk}_us": timeit(lambda: sbr.refine_step(C, A, B, st, 0, sbr.SBRConfig(block=bk)), reps=10),
+        })
+    res.update({"gemm_us": timeit(lambda: X @ X), "expm_us": timeit(lambda: sbr.expm_taylor6(X))})
     print(json.dumps(res), flush=True)
     for g in a.gens:
         C, B = cma_like(a.n, g, g, dev)
-        sbr.eigh_warm(C, B)
+        sbr.eigh_warm(C, B, sbr.SBRConfig(block=a.block))
         torch.cuda.synchronize()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
-        w, Bn, info = sbr.eigh_warm(C, B)
+        w, Bn, info = sbr.eigh_warm(C, B, sbr.SBRConfig(block=a.block))
         e.record()
         torch.cuda.synchronize()
         print(json.dumps({"gen": g, "ms": s.elapsed_time(e), "off_rel": info.off_rel, "jacobi": info.jacobi_sweeps,
