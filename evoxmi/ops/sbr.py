@@ -183,7 +183,10 @@ def _blockdiag16(Q: torch.Tensor, n: int) -> torch.Tensor:
     return torch.block_diag(*Q.unbind(0))[:n, :n]
 
 
-LOCAL_THETA = 0.5
+# local threshold factor of the far mask: 0 (global threshold only) by default; the driver
+# switches it on for the rest of a solve when a far iteration stalls (pairs in clusters
+# denser than the global threshold assumes are then neither in a block nor far)
+LOCAL_THETA = 0.0
 
 
 def local_threshold(dq: torch.Tensor, theta: float = None) -> torch.Tensor:
@@ -200,7 +203,8 @@ def local_threshold(dq: torch.Tensor, theta: float = None) -> torch.Tensor:
     return theta * torch.minimum(up, dn)
 
 
-def far16_ref(A, perm, Q, dq, stats, thr_fac):
+def far16_ref(A, perm, Q, dq, stats, thr_fac, theta: float = None):
+    theta = LOCAL_THETA if theta is None else theta
     n = A.shape[0]
     p = perm.long()
     Qf = _blockdiag16(Q, n)
@@ -209,8 +213,8 @@ def far16_ref(A, perm, Q, dq, stats, thr_fac):
     den = dq[None, :] - dq[:, None]
     thr = thr_fac * (0.5 * SB) * float(stats[3] - stats[2]) / n
     thr = torch.full_like(dq, thr)
-    if LOCAL_THETA > 0:
-        thr = torch.minimum(thr, local_threshold(dq))
+    if theta > 0:
+        thr = torch.minimum(thr, local_threshold(dq, theta))
     mask = (blk[None, :] != blk[:, None]) & (den.abs() > torch.minimum(thr[:, None], thr[None, :]))
     return torch.where(mask, 0.5 * torch.atan(2 * A1 / torch.where(mask, den, torch.ones_like(den))), torch.zeros_like(A1))
 
@@ -243,11 +247,12 @@ def block_solve(A, off, sweeps, bk: int = BK):
     return block_solve_ref(A, off, sweeps)
 
 
-def far(A, off, perm, Q, dq, st, thr_fac, bk: int = BK):
+def far(A, off, perm, Q, dq, st, thr_fac, bk: int = BK, theta: float = None):
+    theta = LOCAL_THETA if theta is None else theta
     if bk == SB:
         if _dev(A):
-            return _ext.ops().sbr16_far(_rowmajor(A), perm, Q, dq, st, float(thr_fac), float(LOCAL_THETA))
-        return far16_ref(A, perm, Q, dq, st, thr_fac)
+            return _ext.ops().sbr16_far(_rowmajor(A), perm, Q, dq, st, float(thr_fac), float(theta))
+        return far16_ref(A, perm, Q, dq, st, thr_fac, theta)
     if _dev(A):
         return _ext.ops().sbr_far(_rowmajor(A), int(off), perm, Q, dq, st, float(thr_fac))
     return far_ref(A, off, perm, Q, dq, st, thr_fac)
@@ -346,15 +351,16 @@ class SBRConfig:
     block_sweeps: int = 2
     block: int = SB            # 16: one-wave blocks in a shifted sorted order (eigh_sbr16.hip);
                                # 64: the 64-wide offset layout (eigh_sbr.hip)
-    thr_fac: float = None      # far-pair threshold factor (default 0.5 for block 16, 0.3 for 64)
+    thr_fac: float = None      # far-pair threshold factor (default 0.3)
     ns_iters: int = 2          # Newton–Schulz re-orthonormalisation in the first iterations and
                                # after every damped one (undamped later ones have ‖X‖₂ ≲ 0.5:
                                # Taylor-6 is orthogonal to ~1e-6 there)
     graphs: bool = True        # replay each device iteration as a captured hipGraph
+    plan: bool = True          # graphs: replay the previous solve's iteration sequence, one stats read
 
     def __post_init__(self):
         if self.thr_fac is None:
-            self.thr_fac = 0.5 if self.block == SB else 0.3
+            self.thr_fac = 0.3
         if self.block not in (SB, BK):
             raise ValueError(f"SBR block size must be {SB} or {BK}, got {self.block}")
 
@@ -368,7 +374,8 @@ def _read(st: torch.Tensor):
     return (off_rel, kappa) if len(v) == 4 else (off_rel, kappa, v[4])
 
 
-def _refine_core(C, A, B, st, off: int, ns: bool, damp: bool, cfg: SBRConfig, out=None, far_on: bool = True):
+def _refine_core(C, A, B, st, off: int, ns: bool, damp: bool, cfg: SBRConfig, out=None, far_on: bool = True,
+                 theta: float = None):
     """One iteration; returns (A, B, stats, α).  ``out = (A, B, st)`` static buffers to
     write the results into (the workspace graphs: no copies).  ``damp``: estimate ‖X‖₂
     and cap the step (the host enables it while κ is large).  ``far_on = False``: a
@@ -382,7 +389,7 @@ def _refine_core(C, A, B, st, off: int, ns: bool, damp: bool, cfg: SBRConfig, ou
             out[1].copy_(Bn)
             Bn = out[1]
     else:
-        X = far(A, off, perm, Q, dq, st, cfg.thr_fac, cfg.block)
+        X = far(A, off, perm, Q, dq, st, cfg.thr_fac, cfg.block, theta)
         X2 = X @ X
         alpha = damping(X2, cfg.damp_tau) if damp and cfg.damp_tau > 0 else None
         Bq = bq(B, off, perm, Q, cfg.block)
@@ -404,9 +411,10 @@ def _refine_core(C, A, B, st, off: int, ns: bool, damp: bool, cfg: SBRConfig, ou
     return A, Bn, st, alpha
 
 
-def refine_step(C, A, B, st, it: int, cfg: SBRConfig, ns: bool = None, damp: bool = True, far_on: bool = True):
+def refine_step(C, A, B, st, it: int, cfg: SBRConfig, ns: bool = None, damp: bool = True, far_on: bool = True,
+                theta: float = None):
     ns = it < cfg.ns_iters if ns is None else ns
-    return _refine_core(C, A, B, st, (it % 2) * (cfg.block // 2), ns, damp, cfg, far_on=far_on)
+    return _refine_core(C, A, B, st, (it % 2) * (cfg.block // 2), ns, damp, cfg, far_on=far_on, theta=theta)
 
 
 class _Workspace:
@@ -420,6 +428,9 @@ class _Workspace:
         self.C, self.A, self.B = z(), z(), z()
         self.info = torch.zeros(5, dtype=torch.float64, device=dev)  # stats + the step's α
         self.st = self.info[:4]
+        # per-iteration copies of `info` (row 0: the initial Bᵀ C B) for planned solves,
+        # read back with one device→host copy
+        self.hist = torch.zeros(cfg.max_iters + 1, 5, dtype=torch.float64, device=dev)
         self.graphs = {}
 
     def _capture(self, key, body):
@@ -442,20 +453,24 @@ class _Workspace:
             self.B.copy_(B)
             self.A.copy_(A)
             self.st.copy_(st)
+            self.info[4:].fill_(1.0)
+            self.hist[0].copy_(self.info)
 
         self._capture(("init",), body).replay()
 
-    def iterate(self, it: int, ns: bool, damp: bool, far_on: bool = True):
+    def iterate(self, it: int, ns: bool, damp: bool, far_on: bool = True, theta: float = 0.0):
         off = (it % 2) * (self.cfg.block // 2)
+        row = min(it + 1, self.cfg.max_iters)
 
         def body():
             # A, B, stats are written in place (A and B are fully read before the last
             # GEMM/kernel of the iteration overwrites them)
             _, _, _, alpha = _refine_core(self.C, self.A, self.B, self.st, off, ns, damp, self.cfg,
-                                          out=(self.A, self.B, self.st), far_on=far_on)
+                                          out=(self.A, self.B, self.st), far_on=far_on, theta=theta)
             self.info[4:].copy_(alpha)
 
-        self._capture(("it", off, ns, damp, far_on), body).replay()
+        self._capture(("it", off, ns, damp, far_on, theta), body).replay()
+        self.hist[row].copy_(self.info)
 
 
 _WS = {}
@@ -489,17 +504,38 @@ def _jacobi_sweep(A, B, tol):
     return Ap[:n, :n].contiguous(), Bp[:n, :n].contiguous()
 
 
+_PLANS = {}
+
+
+def _decode(row) -> tuple:
+    """(off_rel, κ, α) of a history row [off², diag², dmin, dmax, α]."""
+    off, dg, mn, mx, a = (float(x) for x in row)
+    off_rel = math.sqrt(max(off, 0.0) / dg) if dg > 0 else float("nan")
+    kappa = math.sqrt(max(off, 0.0)) / (mx - mn) if mx > mn else float("inf")
+    return off_rel, kappa, a
+
+
 def eigh_warm(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None):
     """Converged eigendecomposition of symmetric ``C`` warm-started from ``B_prev``.
 
     Returns ``(w, B, info)`` with ``C ≈ B diag(w) Bᵀ`` to ``info.off_rel ≤ cfg.tol``
-    (eigenvalues in no particular order)."""
+    (eigenvalues in no particular order).
+
+    Planned solves: with device graphs the iteration sequence of the previous solve of
+    the same workspace ((Newton–Schulz, damping, far step, local threshold) per
+    iteration) is replayed without reading anything back, then the per-iteration stats
+    history is read once; a sequence that fell short continues adaptively (one stats read
+    per iteration), one that converged early is shortened for the next solve.  Consecutive
+    CMA-ES covariances differ by one rank-μ update, so the sequence is stable and a
+    generation costs one host synchronisation instead of one per iteration."""
     cfg = cfg or SBRConfig()
     info = EigInfo()
     use_graphs = cfg.graphs and C.is_cuda and not torch.cuda.is_current_stream_capturing()
-    ws = None
+    ws = wkey = None
     if use_graphs:
         ws = _workspace(C.shape[0], C.device, cfg)
+        wkey = (C.shape[0], str(C.device), cfg.block, cfg.block_sweeps, cfg.thr_fac, cfg.ns_iters, cfg.damp_tau,
+                cfg.tol, cfg.damp_kappa, cfg.near_only)
         ws.C.copy_(C)
         ws.B.copy_(B_prev)
         ws.init()
@@ -507,10 +543,46 @@ def eigh_warm(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None):
     else:
         B = newton_schulz(B_prev.contiguous())
         A, st = sym_product_stats(C, B)
-    off_rel, kappa = _read(st)
-    info.kappa0 = kappa
-    info.history.append(("init", off_rel, kappa))
     use_jacobi = C.is_cuda  # the CPU path has no Jacobi kernels: refinement only
+    steps = []                 # executed (ns, damp, far_on, θ) per iteration
+    plan = _PLANS.get(wkey) if (ws is not None and cfg.plan) else None
+    A0 = B0 = None
+    it = 0
+    diverged = False
+    if plan:
+        A0, B0 = A.clone(), B.clone()
+        for j, stp in enumerate(plan):
+            ws.iterate(j, *stp)
+        rows = [_decode(r) for r in ws.hist[: len(plan) + 1].cpu()]  # the one host sync
+        r0, k0 = rows[0][0], rows[0][1]
+        info.kappa0 = k0
+        info.history.append(("init", r0, k0))
+        prev = r0
+        for j, (r, k, a) in enumerate(rows[1:]):
+            info.history.append(("refine", r, k))
+            info.damped += a < 1.0
+            if not math.isfinite(r) or r > 1.5 * prev:
+                diverged = True
+                break
+            prev = r
+        it = len(plan)
+        steps = list(plan)
+        off_rel, kappa, alpha = rows[-1]
+        conv = next((j for j, rw in enumerate(rows[1:]) if rw[0] <= cfg.tol), None)
+        if not diverged and conv is not None and conv + 1 < len(plan):
+            steps = plan[: conv + 1]  # converged early: a shorter plan next time
+        last_far = plan[-1][2]
+        theta = plan[-1][3]
+    else:
+        off_rel, kappa = _read(st)
+        info.kappa0 = kappa
+        info.history.append(("init", off_rel, kappa))
+        r0, k0 = off_rel, kappa
+        A0, B0 = A.clone(), B.clone()
+        prev = off_rel
+        alpha = 1.0
+        last_far = True
+        theta = 0.0
 
     def jacobi_until(A, B, off_rel, kappa, kappa_target):
         st = None
@@ -522,22 +594,7 @@ def eigh_warm(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None):
             info.history.append(("jacobi", off_rel, kappa))
         return A, B, st, off_rel, kappa
 
-    if use_jacobi and kappa > cfg.kappa_max and off_rel > cfg.tol:
-        A, B, st_j, off_rel, kappa = jacobi_until(A, B, off_rel, kappa, cfg.kappa_max)
-        if st_j is not None:
-            st = st_j
-            if ws is not None:
-                ws.A.copy_(A)
-                ws.B.copy_(B)
-                ws.st.copy_(st)
-                A, B, st = ws.A, ws.B, ws.st
-    A0, B0, r0, k0 = A.clone(), B.clone(), off_rel, kappa
-    it = 0
-    prev = off_rel
-    diverged = False
-    alpha = 1.0
-    last_far = True
-    while off_rel > cfg.tol and it < cfg.max_iters:
+    while not diverged and off_rel > cfg.tol and it < cfg.max_iters:
         # re-orthonormalise in the first iterations and after a damped (large) step; the
         # ‖X‖₂ estimate runs only while the off-diagonal mass is large against the spread
         # (κ > damp_kappa: converging iterations have ‖X‖₂ ≪ 1 and are never capped)
@@ -546,25 +603,37 @@ def eigh_warm(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None):
         # close to the tolerance the residual is near pairs only: skip the far step (once:
         # if a near-only iteration did not reach the tolerance, far pairs are left)
         far_on = not (it > 0 and off_rel <= cfg.near_only * cfg.tol and last_far)
+        stp = (ns, damp, far_on, theta)
         if ws is not None:
-            ws.iterate(it, ns, damp, far_on)
+            ws.iterate(it, *stp)
             A, B, st = ws.A, ws.B, ws.st
             off_rel, kappa, alpha = _read(ws.info)
         else:
-            A, B, st, a = refine_step(C, A, B, st, it, cfg, ns, damp, far_on)
+            A, B, st, a = refine_step(C, A, B, st, it, cfg, ns, damp, far_on, theta)
             off_rel, kappa, alpha = _read(torch.cat([st.double(), a.double().reshape(1)]))
+        steps.append(stp)
         it += 1
-        last_far = far_on
         info.damped += alpha < 1.0
         info.history.append(("refine", off_rel, kappa))
         if not math.isfinite(off_rel) or off_rel > 1.5 * prev:
             diverged = True
             break
+        # an undamped far iteration close to the tolerance that barely helps: pairs inside a
+        # cluster denser than the global threshold assumes are neither far nor in a block —
+        # the local threshold takes them into the far step for the rest of the solve
+        if far_on and alpha >= 1.0 and off_rel < 100 * cfg.tol and off_rel > 0.6 * prev and cfg.block == SB:
+            theta = 1.0
+        last_far = far_on
         prev = off_rel
     info.refine_iters = it
     if (diverged or off_rel > cfg.tol) and use_jacobi:
         # safety net: back to the pre-refinement basis, finish with Jacobi sweeps
         info.fallback = True
         A, B, _, off_rel, kappa = jacobi_until(A0, B0, r0, k0, 0.0)
+    if wkey is not None:
+        if info.fallback:
+            _PLANS.pop(wkey, None)
+        else:
+            _PLANS[wkey] = steps
     info.off_rel = off_rel
     return torch.diagonal(A).clone(), B.clone() if ws is not None and B is ws.B else B, info
