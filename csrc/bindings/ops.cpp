@@ -331,6 +331,21 @@ std::vector<at::Tensor> sbr16_block(const at::Tensor& A, int64_t shift, int64_t 
   return {perm, Q, dq};
 }
 
+// α = min(1, τ/‖X‖₂) from three power steps on −X² with the n×8 probe block V
+at::Tensor sbr_damping(const at::Tensor& X2, const at::Tensor& V, double tau) {
+  check_rowmajor(X2, "X2");
+  const int64_t n = X2.size(0);
+  TORCH_CHECK(X2.size(1) == n, "X2 must be square");
+  TORCH_CHECK(V.is_cuda() && V.scalar_type() == at::kFloat && V.is_contiguous() && V.dim() == 2 && V.size(0) == n && V.size(1) == 8,
+              "V must be a contiguous float32 n×8 device matrix");
+  c10::DeviceGuard g(X2.device());
+  auto work = at::empty({3, n, 8}, X2.options());
+  auto alpha = at::empty({1}, X2.options());
+  evx_sbr_damping(X2.data_ptr<float>(), (int)n, X2.stride(0), V.data_ptr<float>(), work.data_ptr<float>(), (float)tau,
+                  alpha.data_ptr<float>(), cur_stream());
+  return alpha;
+}
+
 void check_sbr16_operands(int64_t n, const at::Tensor& perm, const at::Tensor& Q) {
   TORCH_CHECK(perm.is_cuda() && perm.scalar_type() == at::kInt && perm.numel() == n && perm.is_contiguous(), "perm int32[n]");
   TORCH_CHECK(Q.is_cuda() && Q.scalar_type() == at::kFloat && Q.is_contiguous() && Q.numel() == (int64_t)evx_sbr16_nblocks((int)n) * 256,
@@ -825,6 +840,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("sbr16_block(Tensor A, int shift, int sweeps) -> Tensor[]");
   m.def("sbr16_far(Tensor A, Tensor perm, Tensor Q, Tensor dq, Tensor stats, float thr_fac, float theta) -> Tensor");
   m.def("sbr16_bq(Tensor B, Tensor perm, Tensor Q) -> Tensor");
+  m.def("sbr_damping(Tensor X2, Tensor V, float tau) -> Tensor");
   m.def("sbr_symstats_out(Tensor T, Tensor(a!) A, Tensor(b!) st) -> ()");
   m.def("sbr_taylor_prep(Tensor X, Tensor X2, Tensor X3, Tensor? alpha=None) -> Tensor[]");
   m.def("pso_update(Tensor pop, Tensor vel, Tensor lbl, Tensor lbf, Tensor fit, Tensor gbl, Tensor kp, Tensor kg, float w, float phip, float phig, Tensor lb, Tensor ub) -> Tensor[]");
@@ -875,5 +891,6 @@ TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
   m.impl("sbr16_block", &sbr16_block);
   m.impl("sbr16_far", &sbr16_far);
   m.impl("sbr16_bq", &sbr16_bq);
+  m.impl("sbr_damping", &sbr_damping);
   m.impl("sbr_taylor_prep", &sbr_taylor_prep);
 }

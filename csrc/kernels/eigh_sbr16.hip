@@ -334,6 +334,71 @@ __global__ void __launch_bounds__(256) sbr16_bq_kernel(const float* __restrict__
   }
 }
 
+
+// ------------------------------------------------------------------ 5. step-size cap (damping)
+// ‖X‖₂ of the skew generator from three power steps on −X² (8 probe vectors): one wave per
+// row of Vout = −X²·Vin (n×8, row-major), then one workgroup forms
+// α = min(1, τ / sqrt(max_j ‖V3_j‖ / ‖V2_j‖)).  Replaces ~15 small library launches.
+__global__ void __launch_bounds__(256) sbr_power_step_kernel(const float* __restrict__ X2, int n, int64_t ldx,
+                                                             const float* __restrict__ Vin, float* __restrict__ Vout) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= n) return;
+  const float* x = X2 + (int64_t)row * ldx;
+  float acc[8] = {};
+  for (int j = lane; j < n; j += 64) {
+    const float a = x[j];
+    const float4 v0 = *(const float4*)(Vin + (int64_t)j * 8), v1 = *(const float4*)(Vin + (int64_t)j * 8 + 4);
+    acc[0] = fmaf(a, v0.x, acc[0]);
+    acc[1] = fmaf(a, v0.y, acc[1]);
+    acc[2] = fmaf(a, v0.z, acc[2]);
+    acc[3] = fmaf(a, v0.w, acc[3]);
+    acc[4] = fmaf(a, v1.x, acc[4]);
+    acc[5] = fmaf(a, v1.y, acc[5]);
+    acc[6] = fmaf(a, v1.z, acc[6]);
+    acc[7] = fmaf(a, v1.w, acc[7]);
+  }
+#pragma unroll
+  for (int c = 0; c < 8; ++c) acc[c] = evx::wave_sum(acc[c]);
+  if (lane == 0) {
+    *(float4*)(Vout + (int64_t)row * 8) = make_float4(-acc[0], -acc[1], -acc[2], -acc[3]);
+    *(float4*)(Vout + (int64_t)row * 8 + 4) = make_float4(-acc[4], -acc[5], -acc[6], -acc[7]);
+  }
+}
+
+__global__ void __launch_bounds__(256) sbr_damping_final_kernel(const float* __restrict__ V2, const float* __restrict__ V3, int n,
+                                                                float tau, float* __restrict__ alpha) {
+  __shared__ float red[2][8][4];
+  float s2[8] = {}, s3[8] = {};
+  for (int j = threadIdx.x; j < n; j += blockDim.x) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const float a = V2[(int64_t)j * 8 + c], b = V3[(int64_t)j * 8 + c];
+      s2[c] = fmaf(a, a, s2[c]);
+      s3[c] = fmaf(b, b, s3[c]);
+    }
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    s2[c] = evx::wave_sum(s2[c]);
+    s3[c] = evx::wave_sum(s3[c]);
+    if (lane == 0) {
+      red[0][c][w] = s2[c];
+      red[1][c][w] = s3[c];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float lam = 0.f;
+    for (int c = 0; c < 8; ++c) {
+      const float a = red[0][c][0] + red[0][c][1] + red[0][c][2] + red[0][c][3];
+      const float b = red[1][c][0] + red[1][c][1] + red[1][c][2] + red[1][c][3];
+      lam = fmaxf(lam, sqrtf(b) / fmaxf(sqrtf(a), 1e-30f));
+    }
+    alpha[0] = fminf(1.f, tau / sqrtf(fmaxf(lam, 1e-30f)));
+  }
+}
+
 }  // namespace
 
 int evx_sbr16_nblocks(int n) { return (n + SB - 1) / SB; }
@@ -354,4 +419,15 @@ void evx_sbr16_bq(const float* B, int rows, int n, int64_t ldb, const int* perm,
                   hipStream_t s) {
   const int nt = (n + TL - 1) / TL;
   sbr16_bq_kernel<<<dim3(nt, (rows + TL - 1) / TL), 256, 0, s>>>(B, rows, n, ldb, perm, Q, Bq, ldq);
+}
+
+void evx_sbr_damping(const float* X2, int n, int64_t ldx, const float* V, float* work, float tau, float* alpha, hipStream_t s) {
+  float* V1 = work;
+  float* V2 = work + (int64_t)n * 8;
+  float* V3 = work + (int64_t)n * 16;
+  const int g = (n + 3) / 4;
+  sbr_power_step_kernel<<<g, 256, 0, s>>>(X2, n, ldx, V, V1);
+  sbr_power_step_kernel<<<g, 256, 0, s>>>(X2, n, ldx, V1, V2);
+  sbr_power_step_kernel<<<g, 256, 0, s>>>(X2, n, ldx, V2, V3);
+  sbr_damping_final_kernel<<<1, 256, 0, s>>>(V2, V3, n, tau, alpha);
 }

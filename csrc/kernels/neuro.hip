@@ -1,13 +1,15 @@
-// Persistent neuroevolution rollout (K15): Brax-style Ant + per-individual MLP policy.
+// Persistent neuroevolution rollout (K15): articulated Brax-style Ant + per-individual MLP policy.
 //
 // One wave64 owns one individual for the whole episode and its weights stay on-chip
 // for every control step (no per-step weight traffic from HBM):
 //  * ant_rollout_reg_kernel (h1, h2 <= 64): weights in VGPRs, lane j = hidden unit j;
 //  * ant_rollout_kernel (larger layers): weights in LDS, lanes stride over units
 //    ((in, out) row-major, so a row read is contiguous across lanes).
-// The body state is lane-uniform; the four legs of each 10 ms semi-implicit
-// sub-step (5 per control step; feet by forward kinematics, penalty contacts with
-// smooth friction) are evaluated by lane quads and reduced with DPP.  Waves leave
+// The torso state is lane-uniform; lane quad position k owns leg k (its two joints and
+// the leg's relative momentum).  Per 10 ms semi-implicit sub-step (5 per control step) a
+// leg lane evaluates the knee/foot capsule-cap contacts, its joint-space dynamics (mass
+// matrix, Coriolis, gravity and contact generalized forces), and the change of the leg's
+// relative linear/angular momentum; the quad sums (DPP) drive the composite torso.  Waves leave
 // the loop independently when their episode ends (sticky done), so there are no
 // block barriers after the weight load.
 //
@@ -17,18 +19,21 @@
 
 namespace {
 
-constexpr float DT = 0.01f, GEAR = 150.f, JI = 30.f, JD = 1.f, LIMK = 500.f;
+constexpr float DT = 0.01f, GEAR = 150.f, ARM = 30.f, JD = 1.f, LIMK = 500.f;
 constexpr float HIP_LO = -0.5236f, HIP_HI = 0.5236f, ANK_LO = 0.5236f, ANK_HI = 1.2217f;
-constexpr float L1 = 0.2828f, L2 = 0.5657f, HIPR = 0.2828f, MASS = 10.f, INERTIA = 1.f, ADAMP = 0.5f, LDAMP = 0.05f;
-constexpr float KC = 2000.f, CC = 60.f, MU = 1.f, EPSV = 0.05f, GRAV = 9.81f;
+constexpr float L1 = 0.2828f, L2 = 0.5657f, HIPR = 0.2828f, ADAMP = 0.5f, LDAMP = 0.05f;
+constexpr float M1 = 0.8f, M2 = 1.2f;                     // thigh, shin
+constexpr float I1 = M1 * L1 * L1 / 12.f, I2 = M2 * L2 * L2 / 12.f;
+constexpr float MTOT = 10.f + 4.f * (M1 + M2);
+constexpr float IC = 4.474515846961317f;                  // ant_derived()["i_c"] in envs.py
+constexpr float RAD = 0.08f, KC = 2000.f, CC = 60.f, MU = 1.f, EPSV = 0.05f, GRAV = 9.81f;
+constexpr float RK = HIPR + L1, R1 = HIPR + 0.5f * L1;
 constexpr int SUB = 5;
 __constant__ float LEG_ANG[4] = {0.7854f, 2.3562f, 3.9270f, 5.4978f};
 __constant__ float ANK_SGN[4] = {1.f, -1.f, -1.f, 1.f};
-__constant__ float LEG_COS[4] = {0.70710678f, -0.70710678f, -0.70710678f, 0.70710678f};
-__constant__ float LEG_SIN[4] = {0.70710678f, 0.70710678f, -0.70710678f, -0.70710678f};
 
-struct AntState {
-  float p[3], q[4], v[3], w[3], jq[8], jqd[8];
+struct AntBody {
+  float p[3], q[4], v[3], w[3];
 };
 
 __device__ __forceinline__ void cross(const float* a, const float* b, float* o) {
@@ -60,55 +65,142 @@ __device__ __forceinline__ float fast_tanh(float x) {
   const float e = __expf(2.f * fminf(fmaxf(x, -15.f), 15.f));
   return 1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f);
 }
+__device__ __forceinline__ float rl(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
 __device__ __forceinline__ float sel4(int k, float a, float b, float c, float d) {
   return k == 0 ? a : (k == 1 ? b : (k == 2 ? c : d));
 }
 
-__device__ __forceinline__ void joint_step(float& q, float& qd, float tau, float sj, float lo, float hi) {
-  const float mag = q * sj;
-  const float viol = fmaxf(lo - mag, 0.f) - fmaxf(mag - hi, 0.f);
-  const float acc = (tau - JD * qd + LIMK * viol * sj) * (1.f / JI);
-  qd += DT * acc;
-  q += DT * qd;
+__device__ __forceinline__ void qrot_inv(const float* q, const float* v, float* o) {
+  const float qc[4] = {q[0], -q[1], -q[2], -q[3]};
+  qrot(qc, v, o);
 }
 
-// Body part of a sub-step: this lane's leg (foot by forward kinematics, penalty contact),
-// quad-summed force/torque, then the lane-uniform body integration.
-template <class S>
-__device__ __forceinline__ void body_step(S& s, float hip, float ank, float hipd, float ankd, float lc, float ls, float sg) {
-  const float a = ank * sg;
-  const float ca = __cosf(a), sa = __sinf(a), ch = __cosf(hip), sh = __sinf(hip);
-  const float cphi = lc * ch - ls * sh, sphi = ls * ch + lc * sh;
-  const float reach = HIPR + L1 + L2 * ca;
-  const float loc[3] = {reach * cphi, reach * sphi, -L2 * sa};
-  const float dreach = -L2 * sa * ankd * sg;
-  const float dloc[3] = {dreach * cphi - reach * sphi * hipd, dreach * sphi + reach * cphi * hipd, -L2 * ca * ankd * sg};
-  float r[3], dr[3], wr[3];
-  qrot(s.q, loc, r);
-  qrot(s.q, dloc, dr);
-  cross(s.w, r, wr);
-  const float fz = s.p[2] + r[2];
-  const float fv[3] = {s.v[0] + wr[0] + dr[0], s.v[1] + wr[1] + dr[1], s.v[2] + wr[2] + dr[2]};
-  const float pen = fmaxf(-fz, 0.f);
-  const float fn = fmaxf(KC * pen - CC * fv[2] * (pen > 0.f ? 1.f : 0.f), 0.f);
-  const float ivn = rsqrtf(fv[0] * fv[0] + fv[1] * fv[1] + EPSV * EPSV);
-  float f[3] = {-MU * fn * fv[0] * ivn, -MU * fn * fv[1] * ivn, fn};
-  float T[3];
-  cross(r, f, T);
-  float F[3];
+// leg's linear / angular momentum relative to the torso frame (angular about the torso
+// origin); mirrors Ant._rel_momentum in envs.py
+__device__ __forceinline__ void leg_momentum(float cphi, float sphi, float ca, float sa, float phid, float ad, float* p, float* L) {
+  const float er[3] = {cphi, sphi, 0.f}, ep[3] = {-sphi, cphi, 0.f};
+  const float r2 = RK + 0.5f * L2 * ca;
+  const float c1[3] = {R1 * cphi, R1 * sphi, 0.f};
+  const float c2[3] = {r2 * cphi, r2 * sphi, -0.5f * L2 * sa};
+  float v1[3], v2[3], t1[3], t2[3];
 #pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    F[c] = quad_sum(f[c]);
-    T[c] = quad_sum(T[c]);
+  for (int k = 0; k < 3; ++k) {
+    v1[k] = R1 * phid * ep[k];
+    v2[k] = r2 * phid * ep[k] - 0.5f * L2 * sa * ad * er[k];
   }
-  F[2] -= MASS * GRAV;
+  v2[2] -= 0.5f * L2 * ca * ad;
+  cross(c1, v1, t1);
+  cross(c2, v2, t2);
 #pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    F[c] -= LDAMP * s.v[c];
-    T[c] -= ADAMP * s.w[c];
-    s.v[c] += DT * F[c] * (1.f / MASS);
-    s.w[c] += DT * T[c] * (1.f / INERTIA);
-    s.p[c] += DT * s.v[c];
+  for (int k = 0; k < 3; ++k) {
+    p[k] = M1 * v1[k] + M2 * v2[k];
+    L[k] = M1 * t1[k] + M2 * t2[k] + I2 * ad * ep[k];
+  }
+  L[2] += (I1 + I2 * ca * ca) * phid;
+}
+
+// penalty contact of a capsule end-cap sphere at torso-frame point x (joint-driven velocity
+// xd): world force f, its torque about the torso origin, and the torso-frame force
+__device__ __forceinline__ void cap_contact(const AntBody& s, const float* x, const float* xd, float* F, float* T, float* ft) {
+  float r[3], dr[3], wr[3];
+  qrot(s.q, x, r);
+  qrot(s.q, xd, dr);
+  cross(s.w, r, wr);
+  const float pz = s.p[2] + r[2];
+  const float pv[3] = {s.v[0] + wr[0] + dr[0], s.v[1] + wr[1] + dr[1], s.v[2] + wr[2] + dr[2]};
+  const float pen = fmaxf(RAD - pz, 0.f);
+  const float fn = fmaxf(KC * pen - CC * pv[2] * (pen > 0.f ? 1.f : 0.f), 0.f);
+  const float ivn = rsqrtf(pv[0] * pv[0] + pv[1] * pv[1] + EPSV * EPSV);
+  const float f[3] = {-MU * fn * pv[0] * ivn, -MU * fn * pv[1] * ivn, fn};
+  float tq[3];
+  cross(r, f, tq);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    F[k] += f[k];
+    T[k] += tq[k];
+  }
+  qrot_inv(s.q, f, ft);
+}
+
+// One sub-step of the articulated Ant for this lane's leg (hip yaw q_h, ankle q_a with
+// sign sg, base yaw angle base); pm / Lm: the leg's relative momentum after the previous
+// sub-step (a function of the joint state, carried to avoid recomputing it).  Mirrors
+// Ant._substep in envs.py.
+__device__ __forceinline__ void art_substep(AntBody& s, float& hq, float& aq, float& hqd, float& aqd, float th, float ta,
+                                            float base, float sg, float* pm, float* Lm) {
+  const float phi = base + hq, a = aq * sg, phid = hqd, ad = aqd * sg;
+  const float cphi = __cosf(phi), sphi = __sinf(phi), ca = __cosf(a), sa = __sinf(a);
+  const float er[3] = {cphi, sphi, 0.f}, ep[3] = {-sphi, cphi, 0.f};
+  const float rf = RK + L2 * ca;
+  float F[3] = {0.f, 0.f, 0.f}, T[3] = {0.f, 0.f, 0.f}, fk[3], ff[3];
+  {
+    const float xk[3] = {RK * cphi, RK * sphi, 0.f};
+    const float vk[3] = {RK * phid * ep[0], RK * phid * ep[1], 0.f};
+    cap_contact(s, xk, vk, F, T, fk);
+    const float xf[3] = {rf * cphi, rf * sphi, -L2 * sa};
+    const float vf[3] = {rf * phid * ep[0] - L2 * sa * ad * er[0], rf * phid * ep[1] - L2 * sa * ad * er[1], -L2 * ca * ad};
+    cap_contact(s, xf, vf, F, T, ff);
+  }
+  float gt[3];
+  {
+    const float gw[3] = {0.f, 0.f, -GRAV};
+    qrot_inv(s.q, gw, gt);
+  }
+  const float r2 = RK + 0.5f * L2 * ca;
+  const float gp = gt[0] * ep[0] + gt[1] * ep[1], gr = gt[0] * er[0] + gt[1] * er[1];
+  const float Qphi = (M1 * R1 + M2 * r2) * gp + RK * (fk[0] * ep[0] + fk[1] * ep[1]) + rf * (ff[0] * ep[0] + ff[1] * ep[1]);
+  const float Qa = M2 * (-0.5f * L2) * (sa * gr + ca * gt[2]) + L2 * (-sa * (ff[0] * er[0] + ff[1] * er[1]) - ca * ff[2]);
+  const float mag = aq * sg;
+  const float vh = fmaxf(HIP_LO - hq, 0.f) - fmaxf(hq - HIP_HI, 0.f);
+  const float va = fmaxf(ANK_LO - mag, 0.f) - fmaxf(mag - ANK_HI, 0.f);
+  const float Qh = th - JD * hqd + LIMK * vh + Qphi;
+  const float Qq = ta - JD * aqd + LIMK * va * sg + sg * Qa;
+  const float H11 = ARM + M1 * R1 * R1 + I1 + M2 * r2 * r2 + I2 * ca * ca;
+  const float H22 = ARM + M2 * (0.25f * L2 * L2) + I2;
+  const float dH = -M2 * L2 * r2 * sa - 2.f * I2 * ca * sa;
+  const float hdd = (Qh - dH * hqd * ad) * __builtin_amdgcn_rcpf(H11);
+  const float add = (Qq + sg * 0.5f * dH * hqd * hqd) * __builtin_amdgcn_rcpf(H22);
+  hqd += DT * hdd;
+  aqd += DT * add;
+  hq += DT * hqd;
+  aq += DT * aqd;
+  float p1[3], L1m[3];
+  {
+    const float phi1 = base + hq, a1 = aq * sg;
+    leg_momentum(__cosf(phi1), __sinf(phi1), __cosf(a1), __sinf(a1), hqd, aqd * sg, p1, L1m);
+  }
+  // per leg, torso frame: momentum change, first moment of the link masses
+  float X[15];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    X[k] = F[k];
+    X[3 + k] = T[k];
+    X[6 + k] = p1[k] - pm[k];
+    X[9 + k] = L1m[k] - Lm[k];
+    pm[k] = p1[k];
+    Lm[k] = L1m[k];
+  }
+  X[12] = (M1 * R1 + M2 * r2) * cphi;
+  X[13] = (M1 * R1 + M2 * r2) * sphi;
+  X[14] = -M2 * 0.5f * L2 * sa;
+#pragma unroll
+  for (int k = 0; k < 15; ++k) X[k] = quad_sum(X[k]);
+  float dp[3], dL[3], cg[3];
+  qrot(s.q, X + 6, dp);
+  qrot(s.q, X + 9, dL);
+  qrot(s.q, X + 12, cg);
+  const float gw[3] = {0.f, 0.f, -GRAV};
+  float tg[3];
+  cross(cg, gw, tg);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float force = X[k] + MTOT * gw[k] - dp[k] * (1.f / DT) - LDAMP * s.v[k];
+    const float torque = X[3 + k] + tg[k] - dL[k] * (1.f / DT) - ADAMP * s.w[k];
+    s.v[k] += DT * force * (1.f / MTOT);
+    s.w[k] += DT * torque * (1.f / IC);
+    s.p[k] += DT * s.v[k];
   }
   const float w = s.q[0], x = s.q[1], y = s.q[2], z = s.q[3];
   const float ox = s.w[0], oy = s.w[1], oz = s.w[2];
@@ -119,32 +211,9 @@ __device__ __forceinline__ void body_step(S& s, float hip, float ank, float hipd
   for (int c = 0; c < 4; ++c) s.q[c] = nq[c] * in;
 }
 
-// LDS kernel: all eight joints lane-uniform, then this lane's leg
-__device__ __forceinline__ void substep_split(AntState& s, const float* tau, int leg, float lc, float ls, float sg) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const bool ankle = j & 1;
-    joint_step(s.jq[j], s.jqd[j], tau[j], ankle ? ANK_SGN[j >> 1] : 1.f, ankle ? ANK_LO : HIP_LO, ankle ? ANK_HI : HIP_HI);
-  }
-  const float hip = sel4(leg, s.jq[0], s.jq[2], s.jq[4], s.jq[6]);
-  const float ank = sel4(leg, s.jq[1], s.jq[3], s.jq[5], s.jq[7]);
-  const float hipd = sel4(leg, s.jqd[0], s.jqd[2], s.jqd[4], s.jqd[6]);
-  const float ankd = sel4(leg, s.jqd[1], s.jqd[3], s.jqd[5], s.jqd[7]);
-  body_step(s, hip, ank, hipd, ankd, lc, ls, sg);
-}
-
-// Register kernel: lane quad position `leg` owns that leg's two joints (the same
-// operations as substep_split, so bit-identical), which removes ~70 lane-uniform
-// instructions per sub-step; the observation gathers the joints with v_readlane.
-struct AntBody {
-  float p[3], q[4], v[3], w[3];
-};
-
-__device__ __forceinline__ void substep_leg(AntBody& s, float& hip, float& ank, float& hipd, float& ankd, float th, float ta,
-                                            float lc, float ls, float sg) {
-  joint_step(hip, hipd, th, 1.f, HIP_LO, HIP_HI);
-  joint_step(ank, ankd, ta, sg, ANK_LO, ANK_HI);
-  body_step(s, hip, ank, hipd, ankd, lc, ls, sg);
+__device__ __forceinline__ void init_leg_momentum(float hq, float aq, float hqd, float aqd, float base, float sg, float* pm, float* Lm) {
+  const float phi = base + hq, a = aq * sg;
+  leg_momentum(__cosf(phi), __sinf(phi), __cosf(a), __sinf(a), hqd, aqd * sg, pm, Lm);
 }
 
 // layer sizes: in = 27, hidden h1, h2 (any, ≤ 256), out = 8; tanh everywhere
@@ -170,30 +239,39 @@ __global__ void __launch_bounds__(256) ant_rollout_kernel(const float* __restric
   const float* B2 = W2 + h1 * h2;
   const float* W3 = B2 + h2;
   const float* B3 = W3 + h2 * 8;
-  AntState s;
+  AntBody s;
   for (int i = 0; i < 3; ++i) s.p[i] = init[i];
   for (int i = 0; i < 4; ++i) s.q[i] = init[3 + i];
   for (int i = 0; i < 3; ++i) s.v[i] = init[7 + i];
   for (int i = 0; i < 3; ++i) s.w[i] = init[10 + i];
-  for (int i = 0; i < 8; ++i) s.jq[i] = init[13 + i];
-  for (int i = 0; i < 8; ++i) s.jqd[i] = init[21 + i];
   const int leg = lane & 3;
+  float hq = init[13 + 2 * leg], aq = init[14 + 2 * leg], hqd = init[21 + 2 * leg], aqd = init[22 + 2 * leg];
+  float pm[3], Lm[3];
+  init_leg_momentum(hq, aq, hqd, aqd, LEG_ANG[leg], ANK_SGN[leg], pm, Lm);
   float total = 0.f;
   int t = 0;
   for (; t < cap; ++t) {
-    // observation → LDS (static register indices: one lane writes all 27 values)
+    // observation → LDS (the joints come from the leg-owning lanes 0-3)
+    float jq[8], jqd[8];
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+      jq[2 * l] = rl(hq, l);
+      jq[2 * l + 1] = rl(aq, l);
+      jqd[2 * l] = rl(hqd, l);
+      jqd[2 * l + 1] = rl(aqd, l);
+    }
     if (lane == 0) {
       a0[0] = s.p[2];
 #pragma unroll
       for (int i = 0; i < 4; ++i) a0[1 + i] = s.q[i];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) a0[5 + i] = s.jq[i];
+      for (int i = 0; i < 8; ++i) a0[5 + i] = jq[i];
 #pragma unroll
       for (int i = 0; i < 3; ++i) a0[13 + i] = s.v[i];
 #pragma unroll
       for (int i = 0; i < 3; ++i) a0[16 + i] = s.w[i];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) a0[19 + i] = s.jqd[i];
+      for (int i = 0; i < 8; ++i) a0[19 + i] = jqd[i];
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -224,7 +302,8 @@ __global__ void __launch_bounds__(256) ant_rollout_kernel(const float* __restric
     }
     __builtin_amdgcn_wave_barrier();  // a0..a3 are rewritten next step
     const float x0 = s.p[0];
-    for (int k = 0; k < SUB; ++k) substep_split(s, tau, leg, LEG_COS[leg], LEG_SIN[leg], ANK_SGN[leg]);
+    const float th = sel4(leg, tau[0], tau[2], tau[4], tau[6]), ta = sel4(leg, tau[1], tau[3], tau[5], tau[7]);
+    for (int k = 0; k < SUB; ++k) art_substep(s, hq, aq, hqd, aqd, th, ta, LEG_ANG[leg], ANK_SGN[leg], pm, Lm);
     const bool healthy = (s.p[2] >= 0.2f) && (s.p[2] <= 1.0f);
     if (!healthy) break;  // sticky done: the terminating step earns nothing
     total += (s.p[0] - x0) * (1.f / (DT * SUB)) + 1.f - 0.5f * csum;
@@ -244,9 +323,6 @@ __global__ void __launch_bounds__(256) ant_rollout_kernel(const float* __restric
 // exchanges that halve the live values per stage, then 3 full stages: 10 lane
 // exchanges instead of 48, all permlane-swap / DPP, none through the LDS permute
 // unit).  Unused units are zero padded, which keeps their activations at tanh(0) = 0.
-__device__ __forceinline__ float rl(float v, int l) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-}
 // cross-lane partners without the LDS permute unit (ds_bpermute costs an LDS round trip
 // per exchange on the step's critical path): gfx950 permlane swaps for lane ^ 32 and
 // lane ^ 16, DPP row rotate for lane ^ 8
@@ -299,7 +375,9 @@ __global__ void __launch_bounds__(64, 2) ant_rollout_reg_kernel(const float* __r
   float hq = init[13 + 2 * lg], aq = init[14 + 2 * lg], hqd = init[21 + 2 * lg], aqd = init[22 + 2 * lg];
   const bool hb5 = lane & 32, hb4 = lane & 16, hb3 = lane & 8;
   const int leg = lane & 3;
-  const float lc = LEG_COS[leg], ls = LEG_SIN[leg], lsg = ANK_SGN[leg];
+  const float lbase = LEG_ANG[leg], lsg = ANK_SGN[leg];
+  float pm[3], Lm[3];
+  init_leg_momentum(hq, aq, hqd, aqd, lbase, lsg, pm, Lm);
   float total = 0.f;
   int t = 0;
   for (; t < cap; ++t) {
@@ -369,7 +447,7 @@ __global__ void __launch_bounds__(64, 2) ant_rollout_reg_kernel(const float* __r
     const float x0 = s.p[0];
     const float th = sel4(leg, tau[0], tau[2], tau[4], tau[6]), ta = sel4(leg, tau[1], tau[3], tau[5], tau[7]);
     #pragma unroll 1
-    for (int k = 0; k < SUB; ++k) substep_leg(s, hq, aq, hqd, aqd, th, ta, lc, ls, lsg);
+    for (int k = 0; k < SUB; ++k) art_substep(s, hq, aq, hqd, aqd, th, ta, lbase, lsg, pm, Lm);
     const bool healthy = (s.p[2] >= 0.2f) && (s.p[2] <= 1.0f);
     if (!healthy) break;
     total += (s.p[0] - x0) * (1.f / (DT * SUB)) + 1.f - 0.5f * csum;
@@ -393,6 +471,6 @@ void evx_ant_rollout(const float* W, int64_t P, int N, int h1, int h2, const flo
   int waves = 4;
   while (waves > 1 && per * waves > 160 * 1024) --waves;
   const int blocks = (N + waves - 1) / waves;
-  hipFuncSetAttribute((const void*)ant_rollout_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(per * waves));
+  (void)hipFuncSetAttribute((const void*)ant_rollout_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(per * waves));
   ant_rollout_kernel<<<blocks, 64 * waves, per * waves, s>>>(W, P, N, h1, h2, init, cap, ret, steps, waves);
 }

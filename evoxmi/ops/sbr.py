@@ -272,7 +272,7 @@ def expm_taylor6(X: torch.Tensor, X2: torch.Tensor = None, alpha: torch.Tensor =
     X3 = X2 @ X
     if X.is_cuda:
         P, M = _ext.ops().sbr_taylor_prep(X.contiguous(), X2, X3, alpha)
-        return torch.addmm(M, X3, P)
+        return torch.addmm(M, X3, P, out=M)  # in place: no copy of M into a fresh output
     a = 1.0 if alpha is None else alpha.reshape(())
     Y, Y2, Y3 = a * X, (a * a) * X2, (a * a * a) * X3
     P = Y / 24 + Y2 / 120 + Y3 / 720
@@ -298,6 +298,8 @@ def damping(X2: torch.Tensor, tau: float) -> torch.Tensor:
     capping ‖αX‖₂ at τ = 1 turns it into a contraction (measured: generation 1 converges
     in 10 iterations instead of needing block-Jacobi sweeps first)."""
     V = _probe_vectors(X2.shape[0], str(X2.device))
+    if X2.is_cuda:
+        return _ext.ops().sbr_damping(_rowmajor(X2), V, float(tau))
     V1 = -(X2 @ V)
     V2 = -(X2 @ V1)
     V3 = -(X2 @ V2)
@@ -566,11 +568,20 @@ def eigh_warm(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None):
                 break
             prev = r
         it = len(plan)
-        steps = list(plan)
         off_rel, kappa, alpha = rows[-1]
-        conv = next((j for j, rw in enumerate(rows[1:]) if rw[0] <= cfg.tol), None)
-        if not diverged and conv is not None and conv + 1 < len(plan):
-            steps = plan[: conv + 1]  # converged early: a shorter plan next time
+        # next plan: the decisions the adaptive loop would take on these stats (the replayed
+        # flags came from an earlier generation), cut at the first converged iteration
+        steps = []
+        last_far, theta = True, plan[0][3]
+        for j in range(len(plan)):
+            r, k, _ = rows[j]
+            a_prev = rows[j][2]
+            stp = (j < cfg.ns_iters or a_prev < 1.0, k > cfg.damp_kappa,
+                   not (j > 0 and r <= cfg.near_only * cfg.tol and last_far), max(theta, plan[j][3]))
+            steps.append(stp)
+            last_far = stp[2]
+            if rows[j + 1][0] <= cfg.tol:
+                break
         last_far = plan[-1][2]
         theta = plan[-1][3]
     else:

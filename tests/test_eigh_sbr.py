@@ -264,3 +264,21 @@ def test_cmaes_trajectories_sbr_vs_library_eigh():
     assert statistics.median(logr) < math.log(1.05), (statistics.median(logr), med["sbr"][::10], med["torch"][::10])
     prog = {impl: math.log(med[impl][10] / med[impl][99]) for impl in med}
     assert prog["torch"] > 1.0 and abs(prog["sbr"] / prog["torch"] - 1) < 0.05, prog
+
+
+@gpu
+def test_damping_kernel_matches_torch_power_iteration():
+    torch.manual_seed(5)
+    n = 1000
+    M = torch.randn(n, n) * 1e-3
+    X = M - M.T
+    X2 = (X @ X).cuda()
+    V = sbr._probe_vectors(n, "cuda")
+    a = float(sbr.damping(X2, 0.05))
+    X2c, Vc = X2.cpu().double(), V.cpu().double()
+    V1 = -(X2c @ Vc)
+    V2 = -(X2c @ V1)
+    V3 = -(X2c @ V2)
+    lam = float((V3.norm(dim=0) / V2.norm(dim=0)).max())
+    ref = min(1.0, 0.05 / math.sqrt(lam))
+    assert abs(a - ref) <= 1e-4 * ref

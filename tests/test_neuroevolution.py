@@ -71,6 +71,33 @@ def test_ant_env_invariants():
     assert torch.allclose(s[:, 3:7].norm(dim=1), torch.ones(3), atol=1e-5)
 
 
+def test_ant_joint_torques_react_on_the_torso():
+    """Articulated legs: in free fall without gravity or damping, driving all hip joints
+    one way spins the torso the other way, and the composite angular momentum
+    I_c·ω + Σ L_rel (legs' momentum relative to the torso) is conserved."""
+    from evoxmi.problems.neuroevolution.reinforcement_learning import envs
+
+    env = envs.Ant()
+    env.P = dict(envs.ANT, gravity=0.0, ang_damp=0.0, lin_damp=0.0, joint_damping=0.0, z0=5.0)
+    s, _ = env.reset(rnd.PRNGKey(0), 1)
+    s[:, 7:] = 0.0  # at rest
+    s[:, 13:21] = torch.tensor([0.0, 1.0, 0.0, -1.0, 0.0, -1.0, 0.0, 1.0])
+    a = torch.tensor([[0.2, 0.0] * 4])
+    D = envs.ant_derived(env.P)
+
+    def lz(s):
+        phi, aa, phid, ad, _ = env._leg_geometry(s)
+        _, L = env._rel_momentum(phi, aa, phid, ad)
+        return D["i_c"] * float(s[0, 12]) + float(L[0, :, 2].sum()), float(L[0, :, 2].sum())
+
+    for _ in range(6):
+        s, _, _, _ = env.step(s, a)
+    total, legs = lz(s)
+    assert float(s[0, 21]) > 0 and legs > 0  # hips turned the commanded way
+    assert float(s[0, 12]) < 0  # the torso reacts
+    assert abs(total) < 0.02 * abs(legs)
+
+
 def test_openes_ant_improves():
     """The centre policy's episode return (not the monotone best-so-far) must improve
     after OpenES generations on the native Ant."""
