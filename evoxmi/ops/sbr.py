@@ -289,7 +289,7 @@ def _probe_vectors(n: int, dev: str) -> torch.Tensor:
     return torch.cos(0.7 * i * (j + 1) + j).to(device=dev, dtype=torch.float32).contiguous()
 
 
-def damping(X2: torch.Tensor, tau: float) -> torch.Tensor:
+def damping(X2: torch.Tensor, tau: float, out: torch.Tensor = None) -> torch.Tensor:
     """α = min(1, τ / ‖X‖₂) for the skew generator X, with ‖X‖₂² = λmax(−X²) estimated
     by three block power steps on 8 fixed probe vectors (device-only, graph-capturable).
 
@@ -299,7 +299,7 @@ def damping(X2: torch.Tensor, tau: float) -> torch.Tensor:
     in 10 iterations instead of needing block-Jacobi sweeps first)."""
     V = _probe_vectors(X2.shape[0], str(X2.device))
     if X2.is_cuda:
-        return _ext.ops().sbr_damping(_rowmajor(X2), V, float(tau))
+        return _ext.ops().sbr_damping(_rowmajor(X2), V, float(tau), out)
     V1 = -(X2 @ V)
     V2 = -(X2 @ V1)
     V3 = -(X2 @ V2)
@@ -347,7 +347,8 @@ class SBRConfig:
                                  # damped generator converges from any warm start)
     max_iters: int = 16
     damp_tau: float = 1.0      # cap on ‖αX‖₂ (0: undamped)
-    damp_kappa: float = 0.5    # estimate ‖X‖₂ only while κ exceeds this
+    damp_kappa: float = 1.0    # estimate ‖X‖₂ in the first iteration and while κ exceeds this
+                               # (steady-state CMA-ES: κ ≈ 1.3 → 0.45 → 0.1: only iteration 0)
     near_only: float = 3.0     # near-only (no far step) iteration once off_rel ≤ near_only·tol
     max_jacobi: int = 16
     block_sweeps: int = 2
@@ -378,11 +379,12 @@ def _read(st: torch.Tensor):
 
 def _refine_core(C, A, B, st, off: int, ns: bool, damp: bool, cfg: SBRConfig, out=None, far_on: bool = True,
                  theta: float = None):
-    """One iteration; returns (A, B, stats, α).  ``out = (A, B, st)`` static buffers to
-    write the results into (the workspace graphs: no copies).  ``damp``: estimate ‖X‖₂
-    and cap the step (the host enables it while κ is large).  ``far_on = False``: a
-    near-only iteration (block solves, B ← B[:, perm]·Qblk, A ← BᵀCB) for the last step,
-    when the residual is almost entirely near pairs (4 GEMMs fewer)."""
+    """One iteration; returns (A, B, stats, α).  ``out = (A, B, st, α)`` static buffers to
+    write the results into (the workspace graphs: no copies; ``st`` may be a row of the
+    stats history).  ``damp``: estimate ‖X‖₂ and cap the step (the host enables it while κ
+    is large).  ``far_on = False``: a near-only iteration (block solves, B ← B[:, perm]·Qblk,
+    A ← BᵀCB) for the last step, when the residual is almost entirely near pairs (4 GEMMs
+    fewer)."""
     perm, Q, dq = block_solve(A, off, cfg.block_sweeps, cfg.block)
     alpha = None
     if not far_on:
@@ -393,7 +395,8 @@ def _refine_core(C, A, B, st, off: int, ns: bool, damp: bool, cfg: SBRConfig, ou
     else:
         X = far(A, off, perm, Q, dq, st, cfg.thr_fac, cfg.block, theta)
         X2 = X @ X
-        alpha = damping(X2, cfg.damp_tau) if damp and cfg.damp_tau > 0 else None
+        if damp and cfg.damp_tau > 0:
+            alpha = damping(X2, cfg.damp_tau, out=out[3] if out else None)
         Bq = bq(B, off, perm, Q, cfg.block)
         V = expm_taylor6(X, X2, alpha)
         if ns:
@@ -409,7 +412,7 @@ def _refine_core(C, A, B, st, off: int, ns: bool, damp: bool, cfg: SBRConfig, ou
     else:
         A, st = sym_product_stats(C, Bn)
     if alpha is None:
-        alpha = torch.ones(1, device=Bn.device)
+        alpha = out[3] if out else torch.ones(1, device=Bn.device)
     return A, Bn, st, alpha
 
 
@@ -421,19 +424,35 @@ def refine_step(C, A, B, st, it: int, cfg: SBRConfig, ns: bool = None, damp: boo
 
 class _Workspace:
     """Static device buffers + captured hipGraphs of the refinement iteration (one per
-    (block offset, Newton–Schulz) variant) and of the initial Bᵀ C B, so a generation's
-    solve costs one graph launch + one 32-byte stats read per iteration."""
+    (iteration index, block offset, flags) variant) and of the initial Bᵀ C B.  Iteration
+    j reads its stats from row j of ``hist`` and writes row j + 1 (and its step size to
+    ``alpha[j + 1]``), so a planned solve is a chain of graph launches with no copies and
+    a single device→host read at the end."""
 
     def __init__(self, n: int, dev, cfg: SBRConfig):
         self.n, self.cfg = n, cfg
         z = lambda: torch.zeros(n, n, device=dev)  # noqa: E731
         self.C, self.A, self.B = z(), z(), z()
-        self.info = torch.zeros(5, dtype=torch.float64, device=dev)  # stats + the step's α
-        self.st = self.info[:4]
-        # per-iteration copies of `info` (row 0: the initial Bᵀ C B) for planned solves,
-        # read back with one device→host copy
-        self.hist = torch.zeros(cfg.max_iters + 1, 5, dtype=torch.float64, device=dev)
+        self.hist = torch.zeros(cfg.max_iters + 1, 4, dtype=torch.float64, device=dev)
+        self.alpha = torch.ones(cfg.max_iters + 1, dtype=torch.float32, device=dev)
         self.graphs = {}
+        self.pool = torch.cuda.graph_pool_handle()  # graphs replay one at a time: one memory pool
+        self.warm = False
+
+    def precapture(self, n_iters: int = 7):
+        """Capture the steady-state variants up front (iteration j: Newton–Schulz for j < 2,
+        damping for j = 0, with and without the far step) so plan changes in later
+        generations replay existing graphs instead of capturing new ones mid-run.  The
+        captures run on copies of the current buffers and leave them unchanged."""
+        saved = (self.A.clone(), self.B.clone(), self.hist.clone(), self.alpha.clone())
+        for j in range(min(n_iters, self.cfg.max_iters)):
+            for far_on in ((True, False) if j > 0 else (True,)):
+                self.iterate(j, j < self.cfg.ns_iters, j == 0, far_on, 0.0, replay=False)
+        self.A.copy_(saved[0])
+        self.B.copy_(saved[1])
+        self.hist.copy_(saved[2])
+        self.alpha.copy_(saved[3])
+        self.warm = True
 
     def _capture(self, key, body):
         if key not in self.graphs:
@@ -443,36 +462,41 @@ class _Workspace:
                 body()
             torch.cuda.current_stream(self.C.device).wait_stream(s)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=s):
+            with torch.cuda.graph(g, stream=s, pool=self.pool):
                 body()
             self.graphs[key] = g
         return self.graphs[key]
 
     def init(self):
+        # no re-orthonormalisation here: iteration 0 always applies Newton–Schulz to its result
         def body():
-            B = newton_schulz(self.B)
-            A, st = sym_product_stats(self.C, B)
-            self.B.copy_(B)
-            self.A.copy_(A)
-            self.st.copy_(st)
-            self.info[4:].fill_(1.0)
-            self.hist[0].copy_(self.info)
+            T = self.B.t() @ (self.C @ self.B)
+            _ext.ops().sbr_symstats_out(T, self.A, self.hist[0])
+            self.alpha.fill_(1.0)
 
         self._capture(("init",), body).replay()
 
-    def iterate(self, it: int, ns: bool, damp: bool, far_on: bool = True, theta: float = 0.0):
+    def iterate(self, it: int, ns: bool, damp: bool, far_on: bool = True, theta: float = 0.0, replay: bool = True):
         off = (it % 2) * (self.cfg.block // 2)
-        row = min(it + 1, self.cfg.max_iters)
+        j = min(it, self.cfg.max_iters - 1)
 
         def body():
-            # A, B, stats are written in place (A and B are fully read before the last
-            # GEMM/kernel of the iteration overwrites them)
-            _, _, _, alpha = _refine_core(self.C, self.A, self.B, self.st, off, ns, damp, self.cfg,
-                                          out=(self.A, self.B, self.st), far_on=far_on, theta=theta)
-            self.info[4:].copy_(alpha)
+            # A, B are written in place (fully read before the last GEMM/kernel of the
+            # iteration overwrites them); stats row j → row j + 1
+            _refine_core(self.C, self.A, self.B, self.hist[j], off, ns, damp, self.cfg,
+                         out=(self.A, self.B, self.hist[j + 1], self.alpha[j + 1 : j + 2]), far_on=far_on, theta=theta)
 
-        self._capture(("it", off, ns, damp, far_on, theta), body).replay()
-        self.hist[row].copy_(self.info)
+        g = self._capture(("it", j, off, ns, damp, far_on, theta), body)
+        if replay:
+            g.replay()
+
+    def read(self, it: int):
+        """(off_rel, κ, α) after iteration ``it`` (−1: the initial product)."""
+        return _decode(list(self.hist[it + 1].cpu()) + [float(self.alpha[it + 1])])
+
+    def read_all(self, k: int):
+        h = torch.cat([self.hist[: k + 1], self.alpha[: k + 1, None].double()], 1).cpu()
+        return [_decode(r) for r in h]
 
 
 _WS = {}
@@ -540,22 +564,22 @@ def eigh_warm(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None):
                 cfg.tol, cfg.damp_kappa, cfg.near_only)
         ws.C.copy_(C)
         ws.B.copy_(B_prev)
+        if not ws.warm and cfg.plan:
+            ws.precapture()
         ws.init()
-        A, B, st = ws.A, ws.B, ws.st
+        A, B, st = ws.A, ws.B, ws.hist[0]
     else:
         B = newton_schulz(B_prev.contiguous())
         A, st = sym_product_stats(C, B)
     use_jacobi = C.is_cuda  # the CPU path has no Jacobi kernels: refinement only
     steps = []                 # executed (ns, damp, far_on, θ) per iteration
     plan = _PLANS.get(wkey) if (ws is not None and cfg.plan) else None
-    A0 = B0 = None
     it = 0
     diverged = False
     if plan:
-        A0, B0 = A.clone(), B.clone()
         for j, stp in enumerate(plan):
             ws.iterate(j, *stp)
-        rows = [_decode(r) for r in ws.hist[: len(plan) + 1].cpu()]  # the one host sync
+        rows = ws.read_all(len(plan))  # the one host sync
         r0, k0 = rows[0][0], rows[0][1]
         info.kappa0 = k0
         info.history.append(("init", r0, k0))
@@ -576,7 +600,7 @@ def eigh_warm(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None):
         for j in range(len(plan)):
             r, k, _ = rows[j]
             a_prev = rows[j][2]
-            stp = (j < cfg.ns_iters or a_prev < 1.0, k > cfg.damp_kappa,
+            stp = (j < cfg.ns_iters or a_prev < 1.0, j == 0 or k > cfg.damp_kappa,
                    not (j > 0 and r <= cfg.near_only * cfg.tol and last_far), max(theta, plan[j][3]))
             steps.append(stp)
             last_far = stp[2]
@@ -589,7 +613,6 @@ def eigh_warm(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None):
         info.kappa0 = kappa
         info.history.append(("init", off_rel, kappa))
         r0, k0 = off_rel, kappa
-        A0, B0 = A.clone(), B.clone()
         prev = off_rel
         alpha = 1.0
         last_far = True
@@ -610,15 +633,15 @@ def eigh_warm(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None):
         # ‖X‖₂ estimate runs only while the off-diagonal mass is large against the spread
         # (κ > damp_kappa: converging iterations have ‖X‖₂ ≪ 1 and are never capped)
         ns = it < cfg.ns_iters or alpha < 1.0
-        damp = kappa > cfg.damp_kappa
+        damp = it == 0 or kappa > cfg.damp_kappa
         # close to the tolerance the residual is near pairs only: skip the far step (once:
         # if a near-only iteration did not reach the tolerance, far pairs are left)
         far_on = not (it > 0 and off_rel <= cfg.near_only * cfg.tol and last_far)
         stp = (ns, damp, far_on, theta)
         if ws is not None:
             ws.iterate(it, *stp)
-            A, B, st = ws.A, ws.B, ws.st
-            off_rel, kappa, alpha = _read(ws.info)
+            A, B, st = ws.A, ws.B, ws.hist[min(it + 1, cfg.max_iters)]
+            off_rel, kappa, alpha = ws.read(it)
         else:
             A, B, st, a = refine_step(C, A, B, st, it, cfg, ns, damp, far_on, theta)
             off_rel, kappa, alpha = _read(torch.cat([st.double(), a.double().reshape(1)]))
@@ -640,6 +663,8 @@ def eigh_warm(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None):
     if (diverged or off_rel > cfg.tol) and use_jacobi:
         # safety net: back to the pre-refinement basis, finish with Jacobi sweeps
         info.fallback = True
+        B0 = newton_schulz(B_prev.contiguous())
+        A0, _ = sym_product_stats(C, B0)
         A, B, _, off_rel, kappa = jacobi_until(A0, B0, r0, k0, 0.0)
     if wkey is not None:
         if info.fallback:
