@@ -158,6 +158,22 @@ std::vector<at::Tensor> argsort_f32(const at::Tensor& keys, int64_t descending) 
   return {ok, oi};
 }
 
+// same contract as argsort_f32, rocPRIM block radix sort in one workgroup per row (sort.hip)
+std::vector<at::Tensor> radix_argsort_f32(const at::Tensor& keys, int64_t descending) {
+  CHECK_DEV(keys); CHECK_F32(keys); CHECK_CONTIG(keys);
+  TORCH_CHECK(keys.dim() <= 2, "radix_argsort_f32: keys must be (n,) or (B, n)");
+  const int64_t B = keys.dim() == 2 ? keys.size(0) : 1;
+  const int64_t n = keys.dim() == 0 ? 1 : keys.size(-1);
+  TORCH_CHECK(n <= evx_argsort_max_n(), "radix_argsort_f32: n > ", evx_argsort_max_n());
+  TORCH_CHECK(B <= 65535, "radix_argsort_f32: B > 65535");
+  c10::DeviceGuard g(keys.device());
+  auto ok = at::empty_like(keys);
+  auto oi = at::empty(keys.sizes(), keys.options().dtype(at::kInt));
+  if (n > 0 && B > 0)
+    evx_radix_argsort(keys.data_ptr<float>(), (int)n, (int)descending, ok.data_ptr<float>(), oi.data_ptr<int32_t>(), cur_stream(), (int)B);
+  return {ok, oi};
+}
+
 at::Tensor cec_basic(const at::Tensor& Z, int64_t fid, const c10::optional<at::Tensor>& perm, int64_t start, int64_t L,
                      const c10::optional<at::Tensor>& sub, double scale, const c10::optional<at::Tensor>& Y, int64_t ystart,
                      int64_t yperm) {
@@ -332,7 +348,7 @@ std::vector<at::Tensor> sbr16_block(const at::Tensor& A, int64_t shift, int64_t 
 }
 
 // α = min(1, τ/‖X‖₂) from three power steps on −X² with the n×8 probe block V
-at::Tensor sbr_damping(const at::Tensor& X2, const at::Tensor& V, double tau) {
+at::Tensor sbr_damping(const at::Tensor& X2, const at::Tensor& V, double tau, const c10::optional<at::Tensor>& out) {
   check_rowmajor(X2, "X2");
   const int64_t n = X2.size(0);
   TORCH_CHECK(X2.size(1) == n, "X2 must be square");
@@ -340,7 +356,8 @@ at::Tensor sbr_damping(const at::Tensor& X2, const at::Tensor& V, double tau) {
               "V must be a contiguous float32 n×8 device matrix");
   c10::DeviceGuard g(X2.device());
   auto work = at::empty({3, n, 8}, X2.options());
-  auto alpha = at::empty({1}, X2.options());
+  at::Tensor alpha = out ? *out : at::empty({1}, X2.options());
+  TORCH_CHECK(alpha.is_cuda() && alpha.scalar_type() == at::kFloat && alpha.numel() == 1 && alpha.is_contiguous(), "out: float32[1]");
   evx_sbr_damping(X2.data_ptr<float>(), (int)n, X2.stride(0), V.data_ptr<float>(), work.data_ptr<float>(), (float)tau,
                   alpha.data_ptr<float>(), cur_stream());
   return alpha;
@@ -679,6 +696,27 @@ at::Tensor lsmop_g(const at::Tensor& X, std::vector<int64_t> start, std::vector<
 }
 
 // ---------------------------------------------------------------- CMA-ES tell epilogue (cmaes.hip)
+// Yw = (pop[rows] − mean)·sqrt(w)/σ (K×d), rows int32 (or none: the first K rows)
+at::Tensor cma_center_rows(const at::Tensor& pop, const c10::optional<at::Tensor>& rows, const at::Tensor& mean, const at::Tensor& sigma,
+                           const at::Tensor& w) {
+  CHECK_DEV(pop); CHECK_F32(pop);
+  TORCH_CHECK(pop.dim() == 2 && pop.stride(1) == 1, "cma_center_rows: pop must be row-major 2-D");
+  const int64_t d = pop.size(1), K = w.numel();
+  TORCH_CHECK(mean.is_contiguous() && mean.numel() == d && sigma.numel() == 1 && w.is_contiguous(), "cma_center_rows: mean (d,), sigma (1,), w (K,)");
+  const int32_t* rp = nullptr;
+  if (rows) {
+    TORCH_CHECK(rows->scalar_type() == at::kInt && rows->is_contiguous() && rows->numel() == K, "cma_center_rows: rows int32[K]");
+    rp = rows->data_ptr<int32_t>();
+  } else {
+    TORCH_CHECK(K <= pop.size(0), "cma_center_rows: K > rows of pop");
+  }
+  c10::DeviceGuard g(pop.device());
+  auto Y = at::empty({K, d}, pop.options());
+  evx_cma_center_rows(pop.data_ptr<float>(), pop.stride(0), rp, mean.data_ptr<float>(), sigma.contiguous().data_ptr<float>(),
+                      w.data_ptr<float>(), (int)K, (int)d, Y.data_ptr<float>(), cur_stream());
+  return Y;
+}
+
 std::vector<at::Tensor> cma_delta_gemv(const at::Tensor& M, const at::Tensor& mean, const at::Tensor& dm, double cm) {
   for (auto* t : {&M, &mean, &dm}) { CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t); }
   const int64_t d = mean.numel();
@@ -807,6 +845,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("hv_contrib(Tensor S, Tensor P, Tensor count, Tensor alpha) -> Tensor");
   m.def("philox_fill(Tensor key, int n, int dist, int offset) -> Tensor");
   m.def("argsort_f32(Tensor keys, int descending) -> Tensor[]");
+  m.def("radix_argsort_f32(Tensor keys, int descending) -> Tensor[]");
   m.def("cec_basic(Tensor Z, int fid, Tensor? perm, int start, int L, Tensor? sub, float scale, Tensor? Y, int ystart, int yperm) -> Tensor");
   m.def("jacobi_sweeps(Tensor A, Tensor B, Tensor sched, int sweeps, float tol, float inner_tol, int max_inner, int fused=2) -> Tensor[]");
   m.def("philox_words(Tensor key, int nblocks, int domain, int offset) -> Tensor");
@@ -824,6 +863,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("gemm_f32(Tensor A, int a_rc, Tensor? a_gather, Tensor? a_sub, int a_sub_on_k, Tensor? a_kscale, Tensor? a_kw, Tensor? a_sscale, int a_sscale_inv, Tensor B, int b_rc, Tensor? b_gather, Tensor? b_sub, int b_sub_on_k, Tensor? b_kscale, Tensor? b_kw, Tensor? b_sscale, int b_sscale_inv, Tensor? alpha_ptr, Tensor? bias_n, float beta, Tensor? Cin, int M, int N, int K, int splits, float alpha) -> Tensor");
   m.def("lsmop_g(Tensor X, int[] start, int[] sublen, int[] func, int nk, int cosine) -> Tensor");
   m.def("cma_delta_gemv(Tensor M, Tensor mean, Tensor dm, float cm) -> Tensor[]");
+  m.def("cma_center_rows(Tensor pop, Tensor? rows, Tensor mean, Tensor sigma, Tensor w) -> Tensor");
   m.def("cma_paths(Tensor ps, Tensor pc, Tensor y, Tensor delta, Tensor sigma, Tensor count_iter, float[] consts) -> Tensor[]");
   m.def("cma_cov_pad(Tensor C, Tensor S, Tensor pc, Tensor a, float c1, float cmu, Tensor Bprev, int np) -> Tensor[]");
   m.def("cma_eig_out(Tensor Bp, Tensor w, int d) -> Tensor[]");
@@ -840,7 +880,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("sbr16_block(Tensor A, int shift, int sweeps) -> Tensor[]");
   m.def("sbr16_far(Tensor A, Tensor perm, Tensor Q, Tensor dq, Tensor stats, float thr_fac, float theta) -> Tensor");
   m.def("sbr16_bq(Tensor B, Tensor perm, Tensor Q) -> Tensor");
-  m.def("sbr_damping(Tensor X2, Tensor V, float tau) -> Tensor");
+  m.def("sbr_damping(Tensor X2, Tensor V, float tau, Tensor(a!)? out=None) -> Tensor");
   m.def("sbr_symstats_out(Tensor T, Tensor(a!) A, Tensor(b!) st) -> ()");
   m.def("sbr_taylor_prep(Tensor X, Tensor X2, Tensor X3, Tensor? alpha=None) -> Tensor[]");
   m.def("pso_update(Tensor pop, Tensor vel, Tensor lbl, Tensor lbf, Tensor fit, Tensor gbl, Tensor kp, Tensor kg, float w, float phip, float phig, Tensor lb, Tensor ub) -> Tensor[]");
@@ -866,10 +906,12 @@ TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
   m.impl("jacobi_sweeps", &jacobi_sweeps);
   m.impl("cec_basic", &cec_basic);
   m.impl("argsort_f32", &argsort_f32);
+  m.impl("radix_argsort_f32", &radix_argsort_f32);
   m.impl("gemm_f32", &gemm_f32);
   m.impl("pso_update", &pso_update);
   m.impl("lsmop_g", &lsmop_g);
   m.impl("cma_delta_gemv", &cma_delta_gemv);
+  m.impl("cma_center_rows", &cma_center_rows);
   m.impl("cma_paths", &cma_paths);
   m.impl("cma_cov_pad", &cma_cov_pad);
   m.impl("cma_eig_out", &cma_eig_out);

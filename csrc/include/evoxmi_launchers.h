@@ -25,6 +25,9 @@ struct EvxOperand {
 void evx_gemm_f32(EvxOperand a, EvxOperand b, float* C, int64_t ldc, int M, int N, int K, int splits, float alpha,
                   const float* alpha_ptr, const float* bias_n, float beta, const float* Cin, int64_t ldcin, hipStream_t s);
 int evx_gemm_splits_used(int K, int splits);
+void evx_cma_center_rows(const float* pop, int64_t ldp, const int32_t* rows, const float* mean, const float* sigma, const float* w, int K,
+                         int d, float* Y, hipStream_t s);
+void evx_radix_argsort(const float* keys, int n, int descending, float* out_keys, int32_t* out_idx, hipStream_t s, int batch);
 int evx_argsort_max_n();
 void evx_argsort(const float* keys, int n, int descending, float* out_keys, int32_t* out_idx, hipStream_t s, int batch = 1);
 void evx_cec_basic(const float* Z, int64_t ld, int N, int fid, const int32_t* perm, int start, int L, const float* sub,

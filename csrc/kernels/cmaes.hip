@@ -141,6 +141,28 @@ __global__ void __launch_bounds__(256) eig_out_kernel(const float* __restrict__ 
   }
 }
 
+
+// Rank-μ operand: Yw[i, :] = (pop[rows[i], :] − mean) · sqrt(w_i) / σ, so Σ wᵢ yᵢ yᵢᵀ = Ywᵀ Yw
+// is one plain GEMM (gather, centring, scaling in one pass instead of 4 library kernels).
+// One workgroup per selected row, float4 along d.
+__global__ void __launch_bounds__(256) center_rows_kernel(const float* __restrict__ pop, int64_t ldp, const int32_t* __restrict__ rows,
+                                                          const float* __restrict__ mean, const float* __restrict__ sigma,
+                                                          const float* __restrict__ w, int d, float* __restrict__ Y) {
+  const int i = blockIdx.x;
+  const int64_t src = rows ? rows[i] : i;
+  const float sc = sqrtf(w[i]) / sigma[0];
+  const float* x = pop + src * ldp;
+  float* y = Y + (int64_t)i * d;
+  if ((d & 3) == 0 && (ldp & 3) == 0) {
+    for (int c = threadIdx.x * 4; c < d; c += blockDim.x * 4) {
+      const float4 a = *(const float4*)(x + c), m = *(const float4*)(mean + c);
+      *(float4*)(y + c) = make_float4((a.x - m.x) * sc, (a.y - m.y) * sc, (a.z - m.z) * sc, (a.w - m.w) * sc);
+    }
+  } else {
+    for (int c = threadIdx.x; c < d; c += blockDim.x) y[c] = (x[c] - mean[c]) * sc;
+  }
+}
+
 }  // namespace
 
 void evx_cma_delta_gemv(const float* M, const float* mean, const float* dm, float cm, int d, float* mean_out, float* delta, float* y,
@@ -166,4 +188,9 @@ void evx_cma_eig_out(const float* Bp, const float* w, int d, int np, float* B, f
   int g = (int)((total + 255) / 256);
   if (g > 4096) g = 4096;
   eig_out_kernel<<<g, 256, 0, s>>>(Bp, w, d, np, B, D, BdivD);
+}
+
+void evx_cma_center_rows(const float* pop, int64_t ldp, const int32_t* rows, const float* mean, const float* sigma, const float* w, int K,
+                         int d, float* Y, hipStream_t s) {
+  if (K > 0) center_rows_kernel<<<K, 256, 0, s>>>(pop, ldp, rows, mean, sigma, w, d, Y);
 }

@@ -12,6 +12,8 @@
 //     groups hit distinct banks.
 // At NP = 16384: 55 LDS stages instead of the 105 of an all-LDS bitonic network.
 #include "evoxmi_common.h"
+#include <float.h>
+#include <rocprim/block/block_radix_sort.hpp>
 
 namespace {
 
@@ -120,7 +122,53 @@ __global__ void __launch_bounds__(1024) bitonic_argsort_kernel(const float* __re
   }
 }
 
+// Single-workgroup LDS radix argsort (rocPRIM block radix sort, 1024 threads × IT keys
+// held in registers, 8-bit digits): 4 scatter passes through LDS instead of the bitonic
+// network's 55 LDS stages.  Stable: keys are loaded in blocked order with index payloads,
+// padding (the extreme NaN bit pattern, index ≥ n) sorts behind every real key, so ties
+// break by index as in torch.sort(stable=True).
+template <int IT>
+__global__ void __launch_bounds__(1024) radix_argsort_kernel(const float* __restrict__ keys, int n, int descending,
+                                                             float* __restrict__ out_keys, int32_t* __restrict__ out_idx) {
+  using sort_t = rocprim::block_radix_sort<float, 1024, IT, int32_t>;
+  __shared__ typename sort_t::storage_type storage;
+  const float* kb = keys + (int64_t)blockIdx.x * n;
+  float k[IT];
+  int32_t v[IT];
+  // padding sorts behind every real key, NaNs included (largest / smallest NaN bit patterns)
+  const float pad = __uint_as_float(descending ? 0xffffffffu : 0x7fffffffu);
+#pragma unroll
+  for (int r = 0; r < IT; ++r) {
+    const int i = threadIdx.x * IT + r;
+    k[r] = i < n ? kb[i] : pad;
+    v[r] = i;
+  }
+  if (descending)
+    sort_t().sort_desc(k, v, storage);
+  else
+    sort_t().sort(k, v, storage);
+  float* ok = out_keys ? out_keys + (int64_t)blockIdx.x * n : nullptr;
+  int32_t* oi = out_idx + (int64_t)blockIdx.x * n;
+#pragma unroll
+  for (int r = 0; r < IT; ++r) {
+    const int i = threadIdx.x * IT + r;
+    if (i < n) {
+      if (ok) ok[i] = k[r];
+      oi[i] = v[r];
+    }
+  }
+}
+
 }  // namespace
+
+void evx_radix_argsort(const float* keys, int n, int descending, float* out_keys, int32_t* out_idx, hipStream_t s, int batch) {
+  if (n <= 2048) radix_argsort_kernel<2><<<batch, 1024, 0, s>>>(keys, n, descending, out_keys, out_idx);
+  else if (n <= 4096) radix_argsort_kernel<4><<<batch, 1024, 0, s>>>(keys, n, descending, out_keys, out_idx);
+  else if (n <= 8192) radix_argsort_kernel<8><<<batch, 1024, 0, s>>>(keys, n, descending, out_keys, out_idx);
+  else if (n <= 10240) radix_argsort_kernel<10><<<batch, 1024, 0, s>>>(keys, n, descending, out_keys, out_idx);
+  else if (n <= 12288) radix_argsort_kernel<12><<<batch, 1024, 0, s>>>(keys, n, descending, out_keys, out_idx);
+  else radix_argsort_kernel<16><<<batch, 1024, 0, s>>>(keys, n, descending, out_keys, out_idx);
+}
 
 int evx_argsort_max_n() { return 16384; }
 

@@ -73,6 +73,9 @@ class CMAES(Algorithm):
             self.weights = rw
         self.weights = self.weights.to(center_init.device)
         self._set_rates()
+        # iteration plans of the converged eigensolver, private to this optimiser run
+        # (evoxmi.ops.sbr.eigh_warm): results depend only on the run's own history
+        self._eig_plans = {}
 
     def _set_rates(self):
         w = self.weights.double()
@@ -139,9 +142,13 @@ class CMAES(Algorithm):
             if config.get("plain_gemm") == "blas":
                 # materialise Y = (x_sel − m)/σ once (K×d, 20 MB at the north-star shape) and
                 # run the rank-μ product as a plain vendor GEMM Yᵀ·(w∘Y)
-                Y = population.index_select(0, rows) if rows is not None else population
-                Y = (Y - state.mean) / state.sigma
-                return dm, torch.mm((Y * wvec[:, None]).t(), Y)
+                # (weights are positive: Σ wᵢ yᵢ yᵢᵀ = Ywᵀ Yw with Yw = y·sqrt(w), one fused
+                # gather/centre/scale pass, cmaes.hip)
+                from ....ops import _ext
+
+                Yw = _ext.ops().cma_center_rows(population, rows, state.mean.contiguous(), state.sigma.reshape(1),
+                                                wvec.contiguous())
+                return dm, torch.mm(Yw.t(), Yw)
             splits = max(1, min(16, K // 256))
             S = gemm(
                 Operand(population, rc=True, gather=rows, sub=state.mean, kw=wvec, sscale=one_over, sscale_inv=True),
@@ -182,7 +189,7 @@ class CMAES(Algorithm):
             C, Cp, _ = ops.cma_cov_pad(state.C.contiguous(), S.contiguous(), pc, a, float(self.c1), float(self.cmu), state.B.contiguous(), np_)
             # Cp[:d, :d] = triu(C) + triu(C, 1)ᵀ, the reference's symmetrisation (cma_es.py:193-195)
             with profiling.phase("eigh"):
-                w, Bn, eig_stats = host_phase(sbr_phase, Cp[:d, :d], state.B, out_like=(state.D, state.B, state.eig_stats))
+                w, Bn, eig_stats = host_phase(sbr_phase, Cp[:d, :d], state.B, self.__dict__.setdefault("_eig_plans", {}), out_like=(state.D, state.B, state.eig_stats))
             B, D, BdivD = ops.cma_eig_out(Bn.contiguous(), w.contiguous(), d)
         else:
             np_ = jacobi.padded_size(d)
@@ -217,7 +224,7 @@ class CMAES(Algorithm):
 
     def _decomposition_C(self, C, B_prev):
         Cs = symmetrize_upper(C)
-        w, B = warm_eigh(Cs, B_prev, max_sweeps=self.eig_sweeps)
+        w, B = warm_eigh(Cs, B_prev, max_sweeps=self.eig_sweeps, plans=self.__dict__.setdefault("_eig_plans", {}))
         B = B.contiguous()
         w = torch.clamp(w, min=1e-30)
         D = torch.sqrt(w)

@@ -38,19 +38,19 @@ def symmetrize_upper(C: torch.Tensor) -> torch.Tensor:
 HISTORY = collections.deque(maxlen=4096)
 
 
-def sbr_phase(C: torch.Tensor, B_prev: torch.Tensor):
+def sbr_phase(C: torch.Tensor, B_prev: torch.Tensor, plans: dict = None):
     """Host phase of the converged solver: ``(w, B, stats)`` with stats =
     float64[off_rel, jacobi_sweeps, refine_iters, fallback] (evoxmi.ops.sbr)."""
     from .. import config
     from . import sbr
 
-    w, B, info = sbr.eigh_warm(C, B_prev, sbr.SBRConfig(tol=config.get("eigh_tol"), block=config.get("sbr_block")))
+    w, B, info = sbr.eigh_warm(C, B_prev, sbr.SBRConfig(tol=config.get("eigh_tol"), block=config.get("sbr_block")), plans)
     HISTORY.append(info)
     st = torch.tensor([info.off_rel, info.jacobi_sweeps, info.refine_iters, float(info.fallback)], dtype=torch.float64)
     return w, B, st.to(C.device, non_blocking=True)
 
 
-def warm_eigh(C: torch.Tensor, B_prev: torch.Tensor, max_sweeps: int = None, tol: float = None):
+def warm_eigh(C: torch.Tensor, B_prev: torch.Tensor, max_sweeps: int = None, tol: float = None, plans: dict = None):
     """Eigen-decomposition of symmetric ``C`` warm-started from basis ``B_prev``.
 
     Returns ``(w, B)`` with ``C ≈ B diag(w) Bᵀ`` (eigenvalues not sorted).
@@ -63,7 +63,7 @@ def warm_eigh(C: torch.Tensor, B_prev: torch.Tensor, max_sweeps: int = None, tol
     if impl == "sbr":
         from ..runtime import host_phase
 
-        w, B, _ = host_phase(sbr_phase, C, B_prev, out_like=(C.new_empty(C.shape[0]), C, C.new_empty(4, dtype=torch.float64)))
+        w, B, _ = host_phase(sbr_phase, C, B_prev, plans, out_like=(C.new_empty(C.shape[0]), C, C.new_empty(4, dtype=torch.float64)))
         return w, B
     from . import jacobi
 

@@ -444,22 +444,22 @@ class _Workspace:
         damping for j = 0, with and without the far step) so plan changes in later
         generations replay existing graphs instead of capturing new ones mid-run.  The
         captures run on copies of the current buffers and leave them unchanged."""
-        saved = (self.A.clone(), self.B.clone(), self.hist.clone(), self.alpha.clone())
         for j in range(min(n_iters, self.cfg.max_iters)):
             for far_on in ((True, False) if j > 0 else (True,)):
                 self.iterate(j, j < self.cfg.ns_iters, j == 0, far_on, 0.0, replay=False)
-        self.A.copy_(saved[0])
-        self.B.copy_(saved[1])
-        self.hist.copy_(saved[2])
-        self.alpha.copy_(saved[3])
         self.warm = True
 
     def _capture(self, key, body):
         if key not in self.graphs:
+            # the bodies update A / B / hist / alpha in place: the warm-up run must not
+            # count as an iteration, so the buffers are restored before capturing
+            saved = [t.clone() for t in (self.A, self.B, self.hist, self.alpha)]
             s = torch.cuda.Stream(device=self.C.device)
             s.wait_stream(torch.cuda.current_stream(self.C.device))
             with torch.cuda.stream(s):  # warm-up (allocator, lazy init) outside the capture
                 body()
+                for t, v in zip((self.A, self.B, self.hist, self.alpha), saved):
+                    t.copy_(v)
             torch.cuda.current_stream(self.C.device).wait_stream(s)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=s, pool=self.pool):
@@ -541,7 +541,7 @@ def _decode(row) -> tuple:
     return off_rel, kappa, a
 
 
-def eigh_warm(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None):
+def eigh_warm(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None, plans: dict = None):
     """Converged eigendecomposition of symmetric ``C`` warm-started from ``B_prev``.
 
     Returns ``(w, B, info)`` with ``C ≈ B diag(w) Bᵀ`` to ``info.off_rel ≤ cfg.tol``
@@ -549,7 +549,9 @@ def eigh_warm(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None):
 
     Planned solves: with device graphs the iteration sequence of the previous solve of
     the same workspace ((Newton–Schulz, damping, far step, local threshold) per
-    iteration) is replayed without reading anything back, then the per-iteration stats
+    iteration) is replayed without reading anything back (``plans``: the dict that holds
+    the sequence — one per optimiser run, so the decomposition of a run depends only on
+    that run's own history; the module-level default is shared), then the per-iteration stats
     history is read once; a sequence that fell short continues adaptively (one stats read
     per iteration), one that converged early is shortened for the next solve.  Consecutive
     CMA-ES covariances differ by one rank-μ update, so the sequence is stable and a
@@ -573,7 +575,8 @@ def eigh_warm(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None):
         A, st = sym_product_stats(C, B)
     use_jacobi = C.is_cuda  # the CPU path has no Jacobi kernels: refinement only
     steps = []                 # executed (ns, damp, far_on, θ) per iteration
-    plan = _PLANS.get(wkey) if (ws is not None and cfg.plan) else None
+    plans = _PLANS if plans is None else plans
+    plan = plans.get(wkey) if (ws is not None and cfg.plan) else None
     it = 0
     diverged = False
     if plan:
@@ -668,8 +671,8 @@ def eigh_warm(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None):
         A, B, _, off_rel, kappa = jacobi_until(A0, B0, r0, k0, 0.0)
     if wkey is not None:
         if info.fallback:
-            _PLANS.pop(wkey, None)
+            plans.pop(wkey, None)
         else:
-            _PLANS[wkey] = steps
+            plans[wkey] = steps
     info.off_rel = off_rel
     return torch.diagonal(A).clone(), B.clone() if ws is not None and B is ws.B else B, info

@@ -1,21 +1,22 @@
-"""Sorting primitives (K19).  Device path: LDS bitonic argsort in one workgroup for
-n ≤ 2048 (one launch, no workspace); larger inputs use the ROCm library radix sort,
-which spreads over the CUs (MI355X, n = 10 000: 37 µs vs 127 µs for the
-single-workgroup bitonic network — profiles/r1_kernel_microbench.json).  Ties are
-broken by index (== stable sort)."""
+"""Sorting primitives (K19).  Device path: one-workgroup LDS radix argsort (rocPRIM block
+radix sort, ``sort.hip``) for n ≤ 4096 — one launch, no workspace; larger inputs use the
+ROCm library radix sort, which spreads over the CUs.  Measured on MI355X
+(profiles/r2_sort_microbench.log, µs per call): n = 1000: radix 10.7 / bitonic 11.2 /
+library 21.0; n = 4096: 21.3 / 31.5 / 31.7; n = 10 000: 43.9 / 119.8 / 32.5 — one
+workgroup stops paying off above ≈4k keys.  Ties are broken by index (== stable sort)."""
 from __future__ import annotations
 
 import torch
 
 from . import _ext
 
-MAX_LDS_SORT = 2048
+MAX_LDS_SORT = 4096
 
 
 def argsort(keys: torch.Tensor, descending: bool = False):
     """Return ``(sorted_keys, indices[int64])`` of a 1-D float tensor."""
     if keys.is_cuda and keys.dtype == torch.float32 and keys.numel() <= MAX_LDS_SORT:
-        k, i = _ext.ops().argsort_f32(keys.contiguous(), int(descending))
+        k, i = _ext.ops().radix_argsort_f32(keys.contiguous(), int(descending))
         return k, i.long()
     v, i = torch.sort(keys, descending=descending, stable=True)
     return v, i
@@ -24,7 +25,7 @@ def argsort(keys: torch.Tensor, descending: bool = False):
 def argsort_i32(keys: torch.Tensor):
     """Ascending argsort returning int32 indices (feeds gather prologues directly)."""
     if keys.is_cuda and keys.dtype == torch.float32 and keys.numel() <= MAX_LDS_SORT:
-        return _ext.ops().argsort_f32(keys.contiguous(), 0)
+        return _ext.ops().radix_argsort_f32(keys.contiguous(), 0)
     v, i = torch.sort(keys, stable=True)
     return v, i.to(torch.int32)
 

@@ -282,3 +282,13 @@ def test_damping_kernel_matches_torch_power_iteration():
     lam = float((V3.norm(dim=0) / V2.norm(dim=0)).max())
     ref = min(1.0, 0.05 / math.sqrt(lam))
     assert abs(a - ref) <= 1e-4 * ref
+
+
+@gpu
+def test_sbr_eigh_is_deterministic():
+    """Same inputs, fresh plans ⇒ bitwise identical decompositions (graph captures on first
+    use of an iteration variant must not apply the iteration twice)."""
+    C, B = _cma_like(1000, 6, seed=3, dev="cuda")
+    outs = [sbr.eigh_warm(C, B, sbr.SBRConfig(), plans={}) for _ in range(3)]
+    for w, Bn, info in outs[1:]:
+        assert torch.equal(Bn, outs[0][1]) and info.refine_iters == outs[0][2].refine_iters
