@@ -347,6 +347,8 @@ class SBRConfig:
                                  # damped generator converges from any warm start)
     max_iters: int = 16
     damp_tau: float = 1.0      # cap on ‖αX‖₂ (0: undamped)
+    ns_kappa: float = 0.3      # Newton–Schulz also while κ exceeds this (large undamped steps
+                               # early in a cold start: Taylor-6 loses orthogonality at ‖X‖₂ ≈ 1)
     damp_kappa: float = 1.0    # estimate ‖X‖₂ in the first iteration and while κ exceeds this
                                # (steady-state CMA-ES: κ ≈ 1.3 → 0.45 → 0.1: only iteration 0)
     near_only: float = 3.0     # near-only (no far step) iteration once off_rel ≤ near_only·tol
@@ -603,7 +605,7 @@ def eigh_warm(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None, plan
         for j in range(len(plan)):
             r, k, _ = rows[j]
             a_prev = rows[j][2]
-            stp = (j < cfg.ns_iters or a_prev < 1.0, j == 0 or k > cfg.damp_kappa,
+            stp = (j < cfg.ns_iters or a_prev < 1.0 or k > cfg.ns_kappa, j == 0 or k > cfg.damp_kappa,
                    not (j > 0 and r <= cfg.near_only * cfg.tol and last_far), max(theta, plan[j][3]))
             steps.append(stp)
             last_far = stp[2]
@@ -635,7 +637,7 @@ def eigh_warm(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None, plan
         # re-orthonormalise in the first iterations and after a damped (large) step; the
         # ‖X‖₂ estimate runs only while the off-diagonal mass is large against the spread
         # (κ > damp_kappa: converging iterations have ‖X‖₂ ≪ 1 and are never capped)
-        ns = it < cfg.ns_iters or alpha < 1.0
+        ns = it < cfg.ns_iters or alpha < 1.0 or kappa > cfg.ns_kappa
         damp = it == 0 or kappa > cfg.damp_kappa
         # close to the tolerance the residual is near pairs only: skip the far step (once:
         # if a near-only iteration did not reach the tolerance, far pairs are left)
