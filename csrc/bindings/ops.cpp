@@ -363,6 +363,21 @@ at::Tensor sbr_damping(const at::Tensor& X2, const at::Tensor& V, double tau, co
   return alpha;
 }
 
+std::vector<at::Tensor> sbr_taylor4_prep(const at::Tensor& X, const at::Tensor& X2, const c10::optional<at::Tensor>& alpha) {
+  CHECK_DEV(X); CHECK_F32(X); CHECK_CONTIG(X); CHECK_CONTIG(X2);
+  const int64_t n = X.size(0);
+  TORCH_CHECK(X.dim() == 2 && X.size(1) == n && X2.sizes() == X.sizes(), "sbr_taylor4_prep: n×n");
+  const float* ap = nullptr;
+  if (alpha) {
+    TORCH_CHECK(alpha->numel() == 1 && alpha->scalar_type() == at::kFloat, "sbr_taylor4_prep: alpha float32[1]");
+    ap = alpha->data_ptr<float>();
+  }
+  c10::DeviceGuard g(X.device());
+  auto P = at::empty_like(X), M = at::empty_like(X);
+  evx_sbr_taylor4_prep(X.data_ptr<float>(), X2.data_ptr<float>(), (int)n, ap, P.data_ptr<float>(), M.data_ptr<float>(), cur_stream());
+  return {P, M};
+}
+
 void check_sbr16_operands(int64_t n, const at::Tensor& perm, const at::Tensor& Q) {
   TORCH_CHECK(perm.is_cuda() && perm.scalar_type() == at::kInt && perm.numel() == n && perm.is_contiguous(), "perm int32[n]");
   TORCH_CHECK(Q.is_cuda() && Q.scalar_type() == at::kFloat && Q.is_contiguous() && Q.numel() == (int64_t)evx_sbr16_nblocks((int)n) * 256,
@@ -880,6 +895,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("sbr16_block(Tensor A, int shift, int sweeps) -> Tensor[]");
   m.def("sbr16_far(Tensor A, Tensor perm, Tensor Q, Tensor dq, Tensor stats, float thr_fac, float theta) -> Tensor");
   m.def("sbr16_bq(Tensor B, Tensor perm, Tensor Q) -> Tensor");
+  m.def("sbr_taylor4_prep(Tensor X, Tensor X2, Tensor? alpha=None) -> Tensor[]");
   m.def("sbr_damping(Tensor X2, Tensor V, float tau, Tensor(a!)? out=None) -> Tensor");
   m.def("sbr_symstats_out(Tensor T, Tensor(a!) A, Tensor(b!) st) -> ()");
   m.def("sbr_taylor_prep(Tensor X, Tensor X2, Tensor X3, Tensor? alpha=None) -> Tensor[]");
@@ -934,5 +950,6 @@ TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
   m.impl("sbr16_far", &sbr16_far);
   m.impl("sbr16_bq", &sbr16_bq);
   m.impl("sbr_damping", &sbr_damping);
+  m.impl("sbr_taylor4_prep", &sbr_taylor4_prep);
   m.impl("sbr_taylor_prep", &sbr_taylor_prep);
 }

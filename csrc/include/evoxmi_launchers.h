@@ -109,6 +109,7 @@ int evx_sbr_symstats_parts(int n);
 // 16-wide blocks in a shifted sorted order (eigh_sbr16.hip)
 int evx_sbr16_nblocks(int n);
 int evx_sbr16_max_n();
+void evx_sbr_taylor4_prep(const float* X, const float* X2, int n, const float* alpha, float* P, float* M, hipStream_t s);
 void evx_sbr_damping(const float* X2, int n, int64_t ldx, const float* V, float* work, float tau, float* alpha, hipStream_t s);
 void evx_sbr16_block(const float* A, int n, int64_t lda, int shift, int sweeps, int* perm, float* Q, float* dq, hipStream_t s);
 void evx_sbr16_far(const float* A, int n, int64_t lda, const int* perm, const float* Q, const float* dq, const double* stats,

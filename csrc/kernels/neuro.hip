@@ -77,6 +77,22 @@ __device__ __forceinline__ void qrot_inv(const float* q, const float* v, float* 
   qrot(qc, v, o);
 }
 
+// rotation matrix of a unit quaternion (row-major): R v and Rᵀ v then cost 9 FMAs each
+__device__ __forceinline__ void quat_mat(const float* q, float* R) {
+  const float w = q[0], x = q[1], y = q[2], z = q[3];
+  R[0] = 1.f - 2.f * (y * y + z * z); R[1] = 2.f * (x * y - w * z); R[2] = 2.f * (x * z + w * y);
+  R[3] = 2.f * (x * y + w * z); R[4] = 1.f - 2.f * (x * x + z * z); R[5] = 2.f * (y * z - w * x);
+  R[6] = 2.f * (x * z - w * y); R[7] = 2.f * (y * z + w * x); R[8] = 1.f - 2.f * (x * x + y * y);
+}
+__device__ __forceinline__ void mrot(const float* R, const float* v, float* o) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) o[i] = R[3 * i] * v[0] + R[3 * i + 1] * v[1] + R[3 * i + 2] * v[2];
+}
+__device__ __forceinline__ void mrot_t(const float* R, const float* v, float* o) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) o[i] = R[i] * v[0] + R[3 + i] * v[1] + R[6 + i] * v[2];
+}
+
 // leg's linear / angular momentum relative to the torso frame (angular about the torso
 // origin); mirrors Ant._rel_momentum in envs.py
 __device__ __forceinline__ void leg_momentum(float cphi, float sphi, float ca, float sa, float phid, float ad, float* p, float* L) {
@@ -103,10 +119,11 @@ __device__ __forceinline__ void leg_momentum(float cphi, float sphi, float ca, f
 
 // penalty contact of a capsule end-cap sphere at torso-frame point x (joint-driven velocity
 // xd): world force f, its torque about the torso origin, and the torso-frame force
-__device__ __forceinline__ void cap_contact(const AntBody& s, const float* x, const float* xd, float* F, float* T, float* ft) {
+__device__ __forceinline__ void cap_contact(const AntBody& s, const float* R, const float* x, const float* xd, float* F, float* T,
+                                            float* ft) {
   float r[3], dr[3], wr[3];
-  qrot(s.q, x, r);
-  qrot(s.q, xd, dr);
+  mrot(R, x, r);
+  mrot(R, xd, dr);
   cross(s.w, r, wr);
   const float pz = s.p[2] + r[2];
   const float pv[3] = {s.v[0] + wr[0] + dr[0], s.v[1] + wr[1] + dr[1], s.v[2] + wr[2] + dr[2]};
@@ -121,7 +138,7 @@ __device__ __forceinline__ void cap_contact(const AntBody& s, const float* x, co
     F[k] += f[k];
     T[k] += tq[k];
   }
-  qrot_inv(s.q, f, ft);
+  mrot_t(R, f, ft);
 }
 
 // One sub-step of the articulated Ant for this lane's leg (hip yaw q_h, ankle q_a with
@@ -129,25 +146,23 @@ __device__ __forceinline__ void cap_contact(const AntBody& s, const float* x, co
 // sub-step (a function of the joint state, carried to avoid recomputing it).  Mirrors
 // Ant._substep in envs.py.
 __device__ __forceinline__ void art_substep(AntBody& s, float& hq, float& aq, float& hqd, float& aqd, float th, float ta,
-                                            float base, float sg, float* pm, float* Lm) {
-  const float phi = base + hq, a = aq * sg, phid = hqd, ad = aqd * sg;
-  const float cphi = __cosf(phi), sphi = __sinf(phi), ca = __cosf(a), sa = __sinf(a);
+                                            float base, float sg, float* pm, float* Lm, float* tc) {
+  const float phid = hqd, ad = aqd * sg;
+  const float cphi = tc[0], sphi = tc[1], ca = tc[2], sa = tc[3];  // of the current joint state
+  float R[9];
+  quat_mat(s.q, R);
   const float er[3] = {cphi, sphi, 0.f}, ep[3] = {-sphi, cphi, 0.f};
   const float rf = RK + L2 * ca;
   float F[3] = {0.f, 0.f, 0.f}, T[3] = {0.f, 0.f, 0.f}, fk[3], ff[3];
   {
     const float xk[3] = {RK * cphi, RK * sphi, 0.f};
     const float vk[3] = {RK * phid * ep[0], RK * phid * ep[1], 0.f};
-    cap_contact(s, xk, vk, F, T, fk);
+    cap_contact(s, R, xk, vk, F, T, fk);
     const float xf[3] = {rf * cphi, rf * sphi, -L2 * sa};
     const float vf[3] = {rf * phid * ep[0] - L2 * sa * ad * er[0], rf * phid * ep[1] - L2 * sa * ad * er[1], -L2 * ca * ad};
-    cap_contact(s, xf, vf, F, T, ff);
+    cap_contact(s, R, xf, vf, F, T, ff);
   }
-  float gt[3];
-  {
-    const float gw[3] = {0.f, 0.f, -GRAV};
-    qrot_inv(s.q, gw, gt);
-  }
+  const float gt[3] = {-GRAV * R[6], -GRAV * R[7], -GRAV * R[8]};  // Rᵀ (0, 0, −g)
   const float r2 = RK + 0.5f * L2 * ca;
   const float gp = gt[0] * ep[0] + gt[1] * ep[1], gr = gt[0] * er[0] + gt[1] * er[1];
   const float Qphi = (M1 * R1 + M2 * r2) * gp + RK * (fk[0] * ep[0] + fk[1] * ep[1]) + rf * (ff[0] * ep[0] + ff[1] * ep[1]);
@@ -169,7 +184,11 @@ __device__ __forceinline__ void art_substep(AntBody& s, float& hq, float& aq, fl
   float p1[3], L1m[3];
   {
     const float phi1 = base + hq, a1 = aq * sg;
-    leg_momentum(__cosf(phi1), __sinf(phi1), __cosf(a1), __sinf(a1), hqd, aqd * sg, p1, L1m);
+    tc[0] = __cosf(phi1);
+    tc[1] = __sinf(phi1);
+    tc[2] = __cosf(a1);
+    tc[3] = __sinf(a1);
+    leg_momentum(tc[0], tc[1], tc[2], tc[3], hqd, aqd * sg, p1, L1m);
   }
   // per leg, torso frame: momentum change, first moment of the link masses
   float X[15];
@@ -188,9 +207,9 @@ __device__ __forceinline__ void art_substep(AntBody& s, float& hq, float& aq, fl
 #pragma unroll
   for (int k = 0; k < 15; ++k) X[k] = quad_sum(X[k]);
   float dp[3], dL[3], cg[3];
-  qrot(s.q, X + 6, dp);
-  qrot(s.q, X + 9, dL);
-  qrot(s.q, X + 12, cg);
+  mrot(R, X + 6, dp);
+  mrot(R, X + 9, dL);
+  mrot(R, X + 12, cg);
   const float gw[3] = {0.f, 0.f, -GRAV};
   float tg[3];
   cross(cg, gw, tg);
@@ -211,9 +230,14 @@ __device__ __forceinline__ void art_substep(AntBody& s, float& hq, float& aq, fl
   for (int c = 0; c < 4; ++c) s.q[c] = nq[c] * in;
 }
 
-__device__ __forceinline__ void init_leg_momentum(float hq, float aq, float hqd, float aqd, float base, float sg, float* pm, float* Lm) {
+__device__ __forceinline__ void init_leg_momentum(float hq, float aq, float hqd, float aqd, float base, float sg, float* pm, float* Lm,
+                                                  float* tc) {
   const float phi = base + hq, a = aq * sg;
-  leg_momentum(__cosf(phi), __sinf(phi), __cosf(a), __sinf(a), hqd, aqd * sg, pm, Lm);
+  tc[0] = __cosf(phi);
+  tc[1] = __sinf(phi);
+  tc[2] = __cosf(a);
+  tc[3] = __sinf(a);
+  leg_momentum(tc[0], tc[1], tc[2], tc[3], hqd, aqd * sg, pm, Lm);
 }
 
 // layer sizes: in = 27, hidden h1, h2 (any, ≤ 256), out = 8; tanh everywhere
@@ -246,8 +270,8 @@ __global__ void __launch_bounds__(256) ant_rollout_kernel(const float* __restric
   for (int i = 0; i < 3; ++i) s.w[i] = init[10 + i];
   const int leg = lane & 3;
   float hq = init[13 + 2 * leg], aq = init[14 + 2 * leg], hqd = init[21 + 2 * leg], aqd = init[22 + 2 * leg];
-  float pm[3], Lm[3];
-  init_leg_momentum(hq, aq, hqd, aqd, LEG_ANG[leg], ANK_SGN[leg], pm, Lm);
+  float pm[3], Lm[3], tc[4];
+  init_leg_momentum(hq, aq, hqd, aqd, LEG_ANG[leg], ANK_SGN[leg], pm, Lm, tc);
   float total = 0.f;
   int t = 0;
   for (; t < cap; ++t) {
@@ -303,7 +327,7 @@ __global__ void __launch_bounds__(256) ant_rollout_kernel(const float* __restric
     __builtin_amdgcn_wave_barrier();  // a0..a3 are rewritten next step
     const float x0 = s.p[0];
     const float th = sel4(leg, tau[0], tau[2], tau[4], tau[6]), ta = sel4(leg, tau[1], tau[3], tau[5], tau[7]);
-    for (int k = 0; k < SUB; ++k) art_substep(s, hq, aq, hqd, aqd, th, ta, LEG_ANG[leg], ANK_SGN[leg], pm, Lm);
+    for (int k = 0; k < SUB; ++k) art_substep(s, hq, aq, hqd, aqd, th, ta, LEG_ANG[leg], ANK_SGN[leg], pm, Lm, tc);
     const bool healthy = (s.p[2] >= 0.2f) && (s.p[2] <= 1.0f);
     if (!healthy) break;  // sticky done: the terminating step earns nothing
     total += (s.p[0] - x0) * (1.f / (DT * SUB)) + 1.f - 0.5f * csum;
@@ -376,8 +400,8 @@ __global__ void __launch_bounds__(64, 2) ant_rollout_reg_kernel(const float* __r
   const bool hb5 = lane & 32, hb4 = lane & 16, hb3 = lane & 8;
   const int leg = lane & 3;
   const float lbase = LEG_ANG[leg], lsg = ANK_SGN[leg];
-  float pm[3], Lm[3];
-  init_leg_momentum(hq, aq, hqd, aqd, lbase, lsg, pm, Lm);
+  float pm[3], Lm[3], tc[4];
+  init_leg_momentum(hq, aq, hqd, aqd, lbase, lsg, pm, Lm, tc);
   float total = 0.f;
   int t = 0;
   for (; t < cap; ++t) {
@@ -447,7 +471,7 @@ __global__ void __launch_bounds__(64, 2) ant_rollout_reg_kernel(const float* __r
     const float x0 = s.p[0];
     const float th = sel4(leg, tau[0], tau[2], tau[4], tau[6]), ta = sel4(leg, tau[1], tau[3], tau[5], tau[7]);
     #pragma unroll 1
-    for (int k = 0; k < SUB; ++k) art_substep(s, hq, aq, hqd, aqd, th, ta, lbase, lsg, pm, Lm);
+    for (int k = 0; k < SUB; ++k) art_substep(s, hq, aq, hqd, aqd, th, ta, lbase, lsg, pm, Lm, tc);
     const bool healthy = (s.p[2] >= 0.2f) && (s.p[2] <= 1.0f);
     if (!healthy) break;
     total += (s.p[0] - x0) * (1.f / (DT * SUB)) + 1.f - 0.5f * csum;

@@ -282,6 +282,21 @@ def expm_taylor6(X: torch.Tensor, X2: torch.Tensor = None, alpha: torch.Tensor =
     return V
 
 
+def expm_taylor4(X: torch.Tensor, X2: torch.Tensor, alpha: torch.Tensor = None) -> torch.Tensor:
+    """exp(αX) to 4th order with one GEMM on top of X² (Paterson–Stockmeyer), Y = αX:
+    I + Y + Y²/2 + Y²(Y/6 + Y²/24).  Orthogonal to ‖Y‖⁵/120: used where
+    ‖Y‖ is small (κ below ``SBRConfig.t4_kappa``)."""
+    if X.is_cuda:
+        P, M = _ext.ops().sbr_taylor4_prep(X.contiguous(), X2, alpha)
+        return torch.addmm(M, X2, P, out=M)
+    a = 1.0 if alpha is None else alpha.reshape(())
+    Y, Y2 = a * X, (a * a) * X2
+    V = Y2 @ (Y / 6 + Y2 / 24)
+    V += Y + Y2 / 2
+    V.diagonal().add_(1.0)
+    return V
+
+
 @functools.lru_cache(maxsize=8)
 def _probe_vectors(n: int, dev: str) -> torch.Tensor:
     i = torch.arange(n, dtype=torch.float64)[:, None]
@@ -349,6 +364,7 @@ class SBRConfig:
     damp_tau: float = 1.0      # cap on ‖αX‖₂ (0: undamped)
     ns_kappa: float = 0.3      # Newton–Schulz also while κ exceeds this (large undamped steps
                                # early in a cold start: Taylor-6 loses orthogonality at ‖X‖₂ ≈ 1)
+    t4_kappa: float = 0.05     # Taylor-4 exponential once κ is below this (‖X‖₂ small)
     damp_kappa: float = 1.0    # estimate ‖X‖₂ in the first iteration and while κ exceeds this
                                # (steady-state CMA-ES: κ ≈ 1.3 → 0.45 → 0.1: only iteration 0)
     near_only: float = 3.0     # near-only (no far step) iteration once off_rel ≤ near_only·tol
@@ -380,7 +396,7 @@ def _read(st: torch.Tensor):
 
 
 def _refine_core(C, A, B, st, off: int, ns: bool, damp: bool, cfg: SBRConfig, out=None, far_on: bool = True,
-                 theta: float = None):
+                 theta: float = None, order: int = 6):
     """One iteration; returns (A, B, stats, α).  ``out = (A, B, st, α)`` static buffers to
     write the results into (the workspace graphs: no copies; ``st`` may be a row of the
     stats history).  ``damp``: estimate ‖X‖₂ and cap the step (the host enables it while κ
@@ -400,7 +416,7 @@ def _refine_core(C, A, B, st, off: int, ns: bool, damp: bool, cfg: SBRConfig, ou
         if damp and cfg.damp_tau > 0:
             alpha = damping(X2, cfg.damp_tau, out=out[3] if out else None)
         Bq = bq(B, off, perm, Q, cfg.block)
-        V = expm_taylor6(X, X2, alpha)
+        V = expm_taylor6(X, X2, alpha) if order == 6 else expm_taylor4(X, X2, alpha)
         if ns:
             Bn = Bq @ V
             BtB = Bn.t() @ Bn
@@ -419,9 +435,25 @@ def _refine_core(C, A, B, st, off: int, ns: bool, damp: bool, cfg: SBRConfig, ou
 
 
 def refine_step(C, A, B, st, it: int, cfg: SBRConfig, ns: bool = None, damp: bool = True, far_on: bool = True,
-                theta: float = None):
+                theta: float = None, order: int = 6):
     ns = it < cfg.ns_iters if ns is None else ns
-    return _refine_core(C, A, B, st, (it % 2) * (cfg.block // 2), ns, damp, cfg, far_on=far_on, theta=theta)
+    return _refine_core(C, A, B, st, (it % 2) * (cfg.block // 2), ns, damp, cfg, far_on=far_on, theta=theta, order=order)
+
+
+def decide(cfg: SBRConfig, it: int, off_rel: float, kappa: float, alpha_prev: float, last_far: bool, theta: float) -> tuple:
+    """Flags of refinement iteration ``it`` from the stats before it: (Newton–Schulz, damping,
+    far step, local-threshold θ, Taylor order)."""
+    # re-orthonormalise in the first iterations, after a damped (large) step and while κ is
+    # large; the ‖X‖₂ estimate runs in iteration 0 and while κ is very large
+    ns = it < cfg.ns_iters or alpha_prev < 1.0 or kappa > cfg.ns_kappa
+    damp = it == 0 or kappa > cfg.damp_kappa
+    # close to the tolerance the residual is near pairs only: skip the far step (once: if a
+    # near-only iteration did not reach the tolerance, far pairs are left)
+    far_on = not (it > 0 and off_rel <= cfg.near_only * cfg.tol and last_far)
+    # Taylor-4 (one GEMM fewer) only for small steps: a damped ‖αX‖₂ ≈ 1 step loses ~1e-2 of
+    # orthogonality at 4th order, more than one Newton–Schulz step repairs
+    order = 4 if kappa < cfg.t4_kappa else 6
+    return (ns, damp, far_on, theta, order)
 
 
 class _Workspace:
@@ -441,14 +473,17 @@ class _Workspace:
         self.pool = torch.cuda.graph_pool_handle()  # graphs replay one at a time: one memory pool
         self.warm = False
 
-    def precapture(self, n_iters: int = 7):
-        """Capture the steady-state variants up front (iteration j: Newton–Schulz for j < 2,
-        damping for j = 0, with and without the far step) so plan changes in later
-        generations replay existing graphs instead of capturing new ones mid-run.  The
-        captures run on copies of the current buffers and leave them unchanged."""
+    def precapture(self, n_iters: int = 9):
+        """Capture the iteration variants of the first tens of generations up front
+        (iteration j: Newton–Schulz always for j < 2 and optionally later, damping at j = 0,
+        with and without the far step, Taylor order 6 for j < 2 and 4 / 6 later) so plan
+        changes replay existing graphs instead of capturing new ones mid-run.  Capture
+        warm-ups leave the buffers unchanged (``_capture``)."""
         for j in range(min(n_iters, self.cfg.max_iters)):
-            for far_on in ((True, False) if j > 0 else (True,)):
-                self.iterate(j, j < self.cfg.ns_iters, j == 0, far_on, 0.0, replay=False)
+            for ns in ((True,) if j < self.cfg.ns_iters else (True, False)):
+                for far_on in ((True, False) if j > 0 else (True,)):
+                    for order in ((6,) if j < 2 else (4, 6)):
+                        self.iterate(j, ns, j == 0, far_on, 0.0, order, replay=False)
         self.warm = True
 
     def _capture(self, key, body):
@@ -478,7 +513,7 @@ class _Workspace:
 
         self._capture(("init",), body).replay()
 
-    def iterate(self, it: int, ns: bool, damp: bool, far_on: bool = True, theta: float = 0.0, replay: bool = True):
+    def _body(self, it: int, ns: bool, damp: bool, far_on: bool, theta: float, order: int):
         off = (it % 2) * (self.cfg.block // 2)
         j = min(it, self.cfg.max_iters - 1)
 
@@ -486,11 +521,26 @@ class _Workspace:
             # A, B are written in place (fully read before the last GEMM/kernel of the
             # iteration overwrites them); stats row j → row j + 1
             _refine_core(self.C, self.A, self.B, self.hist[j], off, ns, damp, self.cfg,
-                         out=(self.A, self.B, self.hist[j + 1], self.alpha[j + 1 : j + 2]), far_on=far_on, theta=theta)
+                         out=(self.A, self.B, self.hist[j + 1], self.alpha[j + 1 : j + 2]), far_on=far_on, theta=theta,
+                         order=order)
 
-        g = self._capture(("it", j, off, ns, damp, far_on, theta), body)
+        return ("it", j, off, ns, damp, far_on, theta, order), body
+
+    def iterate(self, it: int, ns: bool, damp: bool, far_on: bool = True, theta: float = 0.0, order: int = 6,
+                replay: bool = True):
+        key, body = self._body(it, ns, damp, far_on, theta, order)
+        g = self._capture(key, body)
         if replay:
             g.replay()
+
+    def run_plan(self, plan):
+        """The iterations of a plan, one graph launch each.  (One graph per plan would save
+        ≈8 µs of launch gap per iteration, but plans keep changing in the first tens of
+        generations and a capture costs ≈2.7 ms: measured as a net loss over 50
+        generations, profiles/NOTES.md.)"""
+        for j, stp in enumerate(plan):
+            k, b = self._body(j, *stp)
+            self._capture(k, b).replay()
 
     def read(self, it: int):
         """(off_rel, κ, α) after iteration ``it`` (−1: the initial product)."""
@@ -582,8 +632,7 @@ def eigh_warm(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None, plan
     it = 0
     diverged = False
     if plan:
-        for j, stp in enumerate(plan):
-            ws.iterate(j, *stp)
+        ws.run_plan(plan)
         rows = ws.read_all(len(plan))  # the one host sync
         r0, k0 = rows[0][0], rows[0][1]
         info.kappa0 = k0
@@ -603,10 +652,8 @@ def eigh_warm(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None, plan
         steps = []
         last_far, theta = True, plan[0][3]
         for j in range(len(plan)):
-            r, k, _ = rows[j]
-            a_prev = rows[j][2]
-            stp = (j < cfg.ns_iters or a_prev < 1.0 or k > cfg.ns_kappa, j == 0 or k > cfg.damp_kappa,
-                   not (j > 0 and r <= cfg.near_only * cfg.tol and last_far), max(theta, plan[j][3]))
+            r, k, a_prev = rows[j]
+            stp = decide(cfg, j, r, k, a_prev, last_far, max(theta, plan[j][3]))
             steps.append(stp)
             last_far = stp[2]
             if rows[j + 1][0] <= cfg.tol:
@@ -637,18 +684,14 @@ def eigh_warm(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None, plan
         # re-orthonormalise in the first iterations and after a damped (large) step; the
         # ‖X‖₂ estimate runs only while the off-diagonal mass is large against the spread
         # (κ > damp_kappa: converging iterations have ‖X‖₂ ≪ 1 and are never capped)
-        ns = it < cfg.ns_iters or alpha < 1.0 or kappa > cfg.ns_kappa
-        damp = it == 0 or kappa > cfg.damp_kappa
-        # close to the tolerance the residual is near pairs only: skip the far step (once:
-        # if a near-only iteration did not reach the tolerance, far pairs are left)
-        far_on = not (it > 0 and off_rel <= cfg.near_only * cfg.tol and last_far)
-        stp = (ns, damp, far_on, theta)
+        stp = decide(cfg, it, off_rel, kappa, alpha, last_far, theta)
+        far_on = stp[2]
         if ws is not None:
             ws.iterate(it, *stp)
             A, B, st = ws.A, ws.B, ws.hist[min(it + 1, cfg.max_iters)]
             off_rel, kappa, alpha = ws.read(it)
         else:
-            A, B, st, a = refine_step(C, A, B, st, it, cfg, ns, damp, far_on, theta)
+            A, B, st, a = refine_step(C, A, B, st, it, cfg, *stp)
             off_rel, kappa, alpha = _read(torch.cat([st.double(), a.double().reshape(1)]))
         steps.append(stp)
         it += 1

@@ -292,3 +292,19 @@ def test_sbr_eigh_is_deterministic():
     outs = [sbr.eigh_warm(C, B, sbr.SBRConfig(), plans={}) for _ in range(3)]
     for w, Bn, info in outs[1:]:
         assert torch.equal(Bn, outs[0][1]) and info.refine_iters == outs[0][2].refine_iters
+
+
+@gpu
+@pytest.mark.parametrize("order", [4, 6])
+def test_taylor_exponential_kernels(order):
+    torch.manual_seed(order)
+    n = 300
+    M = torch.randn(n, n) * 0.003  # ‖X‖₂ ≈ 0.15: Taylor-4 is orthogonal to ~1e-6 there
+    X = M - M.T
+    X2 = X @ X
+    alpha = torch.tensor([0.7])
+    f = sbr.expm_taylor4 if order == 4 else sbr.expm_taylor6
+    ref = f(X, X2, alpha)
+    out = f(X.cuda(), X2.cuda(), alpha.cuda()).cpu()
+    assert _rel(out, ref) < 1e-5
+    assert float((ref.T @ ref - torch.eye(n)).abs().max()) < 1e-5  # orthogonal to the order's truncation
