@@ -378,6 +378,20 @@ std::vector<at::Tensor> sbr_taylor4_prep(const at::Tensor& X, const at::Tensor& 
   return {P, M};
 }
 
+// (v, s²) of linear-kernel GP regressions from (Σf², Σf·x, Σx², n), all float64 of one shape
+std::vector<at::Tensor> linear_gp_fit(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, const at::Tensor& n, int64_t steps,
+                                      double lr) {
+  for (const at::Tensor* t : {&a, &b, &c, &n}) {
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kDouble && t->is_contiguous() && t->sizes() == a.sizes(),
+                "linear_gp_fit: contiguous float64 device tensors of one shape");
+  }
+  c10::DeviceGuard g(a.device());
+  auto v = at::empty(a.sizes(), a.options().dtype(at::kFloat)), s2 = at::empty(a.sizes(), a.options().dtype(at::kFloat));
+  evx_linear_gp_fit(a.data_ptr<double>(), b.data_ptr<double>(), c.data_ptr<double>(), n.data_ptr<double>(), a.numel(), (int)steps, lr,
+                    v.data_ptr<float>(), s2.data_ptr<float>(), cur_stream());
+  return {v, s2};
+}
+
 void check_sbr16_operands(int64_t n, const at::Tensor& perm, const at::Tensor& Q) {
   TORCH_CHECK(perm.is_cuda() && perm.scalar_type() == at::kInt && perm.numel() == n && perm.is_contiguous(), "perm int32[n]");
   TORCH_CHECK(Q.is_cuda() && Q.scalar_type() == at::kFloat && Q.is_contiguous() && Q.numel() == (int64_t)evx_sbr16_nblocks((int)n) * 256,
@@ -896,6 +910,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("sbr16_far(Tensor A, Tensor perm, Tensor Q, Tensor dq, Tensor stats, float thr_fac, float theta) -> Tensor");
   m.def("sbr16_bq(Tensor B, Tensor perm, Tensor Q) -> Tensor");
   m.def("sbr_taylor4_prep(Tensor X, Tensor X2, Tensor? alpha=None) -> Tensor[]");
+  m.def("linear_gp_fit(Tensor a, Tensor b, Tensor c, Tensor n, int steps, float lr) -> Tensor[]");
   m.def("sbr_damping(Tensor X2, Tensor V, float tau, Tensor(a!)? out=None) -> Tensor");
   m.def("sbr_symstats_out(Tensor T, Tensor(a!) A, Tensor(b!) st) -> ()");
   m.def("sbr_taylor_prep(Tensor X, Tensor X2, Tensor X3, Tensor? alpha=None) -> Tensor[]");
@@ -950,6 +965,7 @@ TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
   m.impl("sbr16_far", &sbr16_far);
   m.impl("sbr16_bq", &sbr16_bq);
   m.impl("sbr_damping", &sbr_damping);
+  m.impl("linear_gp_fit", &linear_gp_fit);
   m.impl("sbr_taylor4_prep", &sbr_taylor4_prep);
   m.impl("sbr_taylor_prep", &sbr_taylor_prep);
 }

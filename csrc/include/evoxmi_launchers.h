@@ -128,3 +128,7 @@ int evx_hv_max_m();
 void evx_hv_count(const float* S, const float* P, int ns, int np, int m, int strict, int32_t* count, hipStream_t s);
 void evx_hv_contrib(const float* S, const float* P, const int32_t* count, const float* alpha, int ns, int np, int m, float* f,
                     hipStream_t s);
+
+// batched linear-kernel GP hyper-parameter fits (gp_fit.hip, IM-MOEA)
+void evx_linear_gp_fit(const double* a, const double* b, const double* c, const double* n, int64_t models, int steps, double lr,
+                       float* v, float* s2, hipStream_t s);

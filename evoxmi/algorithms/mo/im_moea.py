@@ -7,12 +7,14 @@ offspring are sampled from the predictive distribution at evenly spaced objectiv
 values over the extended range [1.5·min − 0.5·max, 1.5·max − 0.5·min], and NSGA-II
 selection keeps N.
 
-MI355X form: a GP with the linear kernel k(f, f') = v·f·f' and Gaussian noise σ² is
-Bayesian linear regression, whose predictive mean and variance are closed-form
-rank-one expressions — so all K·M·l inverse models of a generation are one batched
-tensor computation on the device instead of K·M·l separate 250-step optimiser runs
-(the reference's Adam at lr 1e-3 for 250 steps moves gpjax's initial v = σ = 1 by
-well under 25 %; they are kept at those values here).
+MI355X form: a GP with the linear kernel k(f, f') = v·f·f' and Gaussian noise s² is
+Bayesian linear regression: its marginal likelihood and predictive mean / variance are
+closed-form in the sufficient statistics (Σf², Σf·x, Σx², n).  The hyper-parameters are
+fitted as in the reference (250 Adam steps at lr 1e-3 on the softplus-unconstrained
+(v, s) from v = s = 1, ``im_moea.py:310-314``) for every partition × objective × variable
+at once: one thread per model runs the whole optimisation in registers
+(``csrc/kernels/gp_fit.hip``; :func:`linear_gp_fit` is the torch reference), then all
+inverse models are sampled in one batched tensor computation.
 Partitions use the largest cosine (the reference's ``ask`` takes the *smallest*
 cosine similarity, ``im_moea.py:120``, i.e. the farthest vector).
 """
@@ -27,6 +29,38 @@ from ...operators.sampling import UniformSampling
 from ...ops import random as rnd
 from ...utils.common import cos_dist
 from .common import MOAlgorithm, nsga2_select
+
+
+_U0 = 0.5413248546129181  # softplus⁻¹(1)
+
+
+def linear_gp_fit(a, b, c, n, steps: int = 250, lr: float = 1e-3):
+    """(v, s²) of linear-kernel GP regressions x = GP(f) from the sufficient statistics
+    a = Σf², b = Σf·x, c = Σx², n (tensors of one shape): Adam on the negative marginal
+    likelihood nll = ½(c − v b²/D)/s² + ½(n − 1) log s² + ½ log D, D = s² + v a, in softplus
+    coordinates (the reference's gpjax ``Linear`` kernel + ``Gaussian`` likelihood fit)."""
+    a, b, c, n = (t.to(torch.float64).contiguous() for t in (a, b, c, n))
+    if a.is_cuda:
+        from ...ops import _ext
+
+        return tuple(_ext.ops().linear_gp_fit(a, b, c, n, int(steps), float(lr)))
+    sp = torch.nn.functional.softplus
+    uv = torch.full_like(a, _U0)
+    us = torch.full_like(a, _U0)
+    mv, ms, vv, vs = (torch.zeros_like(a) for _ in range(4))
+    for t in range(1, steps + 1):
+        v, s = sp(uv), sp(us)
+        s2 = s * s
+        D = s2 + v * a
+        gv = -0.5 * b * b / (D * D) + 0.5 * a / D
+        gs2 = -0.5 * c / (s2 * s2) + 0.5 * v * b * b * (s2 + D) / (D * D * s2 * s2) + 0.5 * (n - 1) / s2 + 0.5 / D
+        g_uv, g_us = gv * torch.sigmoid(uv), gs2 * 2 * s * torch.sigmoid(us)
+        mv, ms = 0.9 * mv + 0.1 * g_uv, 0.9 * ms + 0.1 * g_us
+        vv, vs = 0.999 * vv + 0.001 * g_uv * g_uv, 0.999 * vs + 0.001 * g_us * g_us
+        uv = uv - lr * (mv / (1 - 0.9**t)) / (torch.sqrt(vv / (1 - 0.999**t)) + 1e-8)
+        us = us - lr * (ms / (1 - 0.9**t)) / (torch.sqrt(vs / (1 - 0.999**t)) + 1e-8)
+    s = sp(us)
+    return sp(uv).float(), (s * s).float()
 
 
 class IMMOEA(MOAlgorithm):
@@ -69,16 +103,20 @@ class IMMOEA(MOAlgorithm):
         lo = torch.where(ok[:, None], 1.5 * fmin - 0.5 * fmax, fit.min(0).values)
         hi = torch.where(ok[:, None], 1.5 * fmax - 0.5 * fmin, fit.max(0).values)
         dims = torch.argsort(rnd.uniform(k_dims, (K, M, D)).to(dev), dim=-1)[..., :l]  # (K, M, l)
-        v, s2 = 1.0, 1.0
         f2 = (mask[:, :, None] * fit[None] ** 2).sum(1)  # (K, M)  Σ f²
         fx = torch.einsum("cn,nm,nd->cmd", mask, fit, pop)  # (K, M, D)  Σ f·x
+        xx = mask @ (pop * pop)  # (K, D)  Σ x²
+        # fitted hyper-parameters of every (partition, objective, variable) inverse model
+        v, s2 = linear_gp_fit(f2[:, :, None].expand(K, M, D), fx, xx[:, None, :].expand(K, M, D),
+                              counts.to(torch.float64)[:, None, None].expand(K, M, D))
+        v, s2 = v.to(pop.dtype), s2.to(pop.dtype)
         t = torch.linspace(0, 1, n_off, device=dev)
         fstar = lo[:, :, None] + (hi - lo)[:, :, None] * t  # (K, M, n_off)
-        denom = s2 + v * f2  # (K, M)
-        coef = v * fx / denom[:, :, None]  # (K, M, D)
+        denom = s2 + v * f2[:, :, None]  # (K, M, D)
+        coef = v * fx / denom  # (K, M, D)
         mean = fstar[..., None] * coef[:, :, None, :]  # (K, M, n_off, D)
-        var = v * fstar**2 * s2 / denom[:, :, None] + s2  # (K, M, n_off)
-        sample = mean + torch.sqrt(var)[..., None] * rnd.normal(k_noise, (K, M, n_off, D)).to(dev)
+        var = (v * s2 / denom)[:, :, None, :] * (fstar**2)[..., None] + s2[:, :, None, :]  # (K, M, n_off, D)
+        sample = mean + torch.sqrt(var) * rnd.normal(k_noise, (K, M, n_off, D)).to(dev)
         sel = torch.zeros((K, M, D), dtype=torch.bool, device=dev).scatter_(2, dims, True) & ok[:, None, None]
         # objective m writes its own variable group into the offspring block of that objective
         m_of = torch.arange(n_off, device=dev) % M  # spread the M inverse models over the offspring

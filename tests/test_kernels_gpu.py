@@ -872,3 +872,16 @@ def test_radix_argsort_matches_stable_torch_sort(n, descending):
     ok, oi = _ext.ops().radix_argsort_f32(kd, descending)
     rv, ri = torch.sort(k, dim=1, descending=bool(descending), stable=True)
     assert torch.equal(oi.cpu().long(), ri) and torch.allclose(ok.cpu(), rv, equal_nan=True)
+
+
+def test_linear_gp_fit_kernel_matches_torch():
+    from evoxmi.algorithms.mo.im_moea import linear_gp_fit
+
+    g = torch.Generator().manual_seed(1)
+    n = torch.randint(2, 60, (500,), generator=g).double()
+    a = torch.rand(500, generator=g, dtype=torch.float64) * n * 4
+    b = (torch.rand(500, generator=g, dtype=torch.float64) - 0.5) * a
+    c = torch.rand(500, generator=g, dtype=torch.float64) * n * 3 + b * b / a
+    v_r, s2_r = linear_gp_fit(a, b, c, n)
+    v, s2 = linear_gp_fit(a.cuda(), b.cuda(), c.cuda(), n.cuda())
+    assert torch.allclose(v.cpu(), v_r, rtol=1e-5) and torch.allclose(s2.cpu(), s2_r, rtol=1e-5)

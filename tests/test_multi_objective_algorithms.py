@@ -72,3 +72,26 @@ def test_moead_scan_gpu_semantics_cpu_oracle():
     W = torch.rand(20, 3, generator=g) + 0.1
     owner, o, z = moead_scan(objs, off, P, W, torch.zeros(3), "tchebycheff", nr=2, update_z=True)
     assert (owner >= -1).all() and torch.equal(o[owner >= 0], off[owner[owner >= 0]])
+
+
+def test_immoea_gp_fit_matches_gp_regression():
+    """IM-MOEA's batched closed-form fit reproduces GPRegression(Linear) + Adam(1e-3) × 250
+    (the reference's inverse-model fit, im_moea.py:310-314)."""
+    from evoxmi.algorithms.mo.im_moea import linear_gp_fit
+    from evoxmi.operators.gaussian_process import GPRegression
+    from evoxmi.operators.gaussian_process.kernels import Linear
+    from evoxmi.utils import optim
+
+    sp = torch.nn.functional.softplus
+    g = torch.Generator().manual_seed(0)
+    stats, ref = [], []
+    for slope, noise, n in ((0.7, 0.3, 40), (-1.5, 0.05, 12), (0.0, 2.0, 25)):
+        f = torch.rand(n, generator=g, dtype=torch.float64) * 3
+        x = slope * f + noise * torch.randn(n, generator=g, dtype=torch.float64)
+        m = GPRegression(kernel=Linear()).fit(f[:, None], x, optimzer=optim.adam(1e-3))
+        ref.append((float(sp(m._u["k_variance"])), float(sp(m._u["obs_stddev"])) ** 2))
+        stats.append(((f * f).sum(), (f * x).sum(), (x * x).sum(), float(n)))
+    a, b, c, n = (torch.tensor([s[i] for s in stats], dtype=torch.float64) for i in range(4))
+    v, s2 = linear_gp_fit(a, b, c, n)
+    for i, (rv, rs2) in enumerate(ref):
+        assert abs(float(v[i]) - rv) < 1e-4 and abs(float(s2[i]) - rs2) < 1e-4
