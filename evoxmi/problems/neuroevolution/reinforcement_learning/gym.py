@@ -3,9 +3,10 @@
 The reference runs CPU gymnasium environments in Ray worker actors and evaluates
 the policy in a controller actor.  Here:
 
-* when ``gymnasium`` is importable and ``env_name``/``env_creator`` is given, the
-  environments are stepped on the host in ``num_workers`` batches (sequential
-  vectorised loop; policies run batched on the policy device);
+* with an ``env_creator`` (or ``env_name`` when ``gymnasium`` is importable) the host
+  environments are stepped in ``num_workers`` parallel worker processes
+  (:class:`.host_envs.EnvWorkers`, the reference's Ray worker actors), the policy runs
+  batched on the policy device (the controller);
 * otherwise (this image) the native batched re-implementations of
   :mod:`.envs` are used (CartPole-v1 / Pendulum-v1 / MountainCarContinuous-v0 have
   the gymnasium dynamics), on whatever device the weights live on.
@@ -124,26 +125,37 @@ class Gym(Problem):
             return total, state
         return self._host_rollout(state, weights, n, dev)  # pragma: no cover
 
-    def _host_rollout(self, state, weights, n, dev):  # pragma: no cover - requires gymnasium
-        envs = [self.env_creator() if self.env_creator else _gym.make(self.env_name, **self.env_options) for _ in range(n)]
-        seed = int(state.key[1])
-        obs = torch.stack([torch.as_tensor(e.reset(seed=seed)[0], dtype=torch.float32) for e in envs]).to(dev)
-        total = torch.zeros(n, len(self.mo_keys) or 1)
-        alive = [True] * n
-        for _ in range(self.cap_episode):
-            act = self._act(weights, obs, n).cpu()
-            new_obs = []
-            for i, e in enumerate(envs):
-                if alive[i]:
-                    o, r, term, trunc, info = e.step(act[i].argmax().item() if act[i].numel() > 1 and hasattr(e.action_space, "n") else act[i].numpy())
-                    vals = [info[k] for k in self.mo_keys] if self.mo_keys else [r]
-                    total[i] += torch.tensor(vals, dtype=torch.float32)
-                    alive[i] = not (term or trunc)
-                    new_obs.append(torch.as_tensor(o, dtype=torch.float32))
-                else:
-                    new_obs.append(obs[i].cpu())
-            obs = torch.stack(new_obs).to(dev)
-            if not any(alive):
-                break
+    def _host_rollout(self, state, weights, n, dev):
+        from .host_envs import EnvWorkers
+
+        creator = self.env_creator
+        if creator is None:  # pragma: no cover - requires gymnasium
+            name, opts = self.env_name, self.env_options
+            creator = _GymCreator(name, opts)
+        discrete = bool(getattr(creator, "discrete", True))
+        workers = EnvWorkers(creator, n, self.num_workers, self.mo_keys, discrete=discrete)
+        try:
+            seed = int(state.key[1])
+            obs = torch.as_tensor(workers.reset(seed)).to(dev)
+            total = torch.zeros(n, len(self.mo_keys) or 1)
+            alive = torch.ones(n, dtype=torch.bool)
+            for _ in range(self.cap_episode):
+                act = self._act(weights, obs, n).detach().cpu().numpy()
+                o, r, done = workers.step(act)
+                total += alive[:, None].to(total.dtype) * torch.as_tensor(r)
+                alive &= ~torch.as_tensor(done)
+                obs = torch.as_tensor(o).to(dev)
+                if not bool(alive.any()):
+                    break
+        finally:
+            workers.close()
         out = total.to(dev)
         return (out[:, 0] if not self.mo_keys else out), state
+
+
+class _GymCreator:  # pragma: no cover - requires gymnasium
+    def __init__(self, name, opts):
+        self.name, self.opts = name, opts
+
+    def __call__(self):
+        return _gym.make(self.name, **self.opts)

@@ -60,7 +60,7 @@ def test_envpool_cartpole_runs_on_native_batched_env():
     tv = TreeAndVector(params)
     results = []
     for _ in range(2):
-        prob = EnvPool(policy, "CartPole-v1", cap_episode=200)
+        prob = EnvPool(policy, "CartPole-v1", num_envs=16, cap_episode_length=200)
         wf = StdWorkflow(PGPE(16, tv.to_vector(params), optimizer="adam"), prob, sol_transforms=[tv.batched_to_tree],
                          opt_direction="max")
         st = wf.init(rnd.PRNGKey(2))
@@ -68,3 +68,36 @@ def test_envpool_cartpole_runs_on_native_batched_env():
             st = wf.step(st)
         results.append(st.get_child_state("algorithm").center.clone())
     assert torch.isfinite(results[0]).all() and torch.equal(results[0], results[1])
+
+
+def test_envpool_loop_matches_manual_rollout():
+    """The reference's EnvPool loop (seed, reset, vmapped policy, masked reward sum until all
+    done) over the envpool-style batched API."""
+    from evoxmi.models import MLPPolicy
+    from evoxmi.problems.neuroevolution import EnvPool
+    from evoxmi.problems.neuroevolution.reinforcement_learning.env_pool import make
+    from evoxmi.utils import TreeAndVector
+
+    policy = MLPPolicy([4, 8, 2])
+    params = policy.init(rnd.PRNGKey(1))
+    tv = TreeAndVector(params)
+    pop = tv.to_vector(params) + 0.5 * torch.randn(8, tv.to_vector(params).numel(), generator=torch.Generator().manual_seed(0))
+    tree = tv.batched_to_tree(pop)
+    prob = EnvPool(policy, "CartPole-v1", num_envs=8, cap_episode_length=150)
+    st = prob.init(rnd.PRNGKey(3))
+    ret, _ = prob.evaluate(st, tree)
+    # manual replay with the same seed
+    _, sub = rnd.split(st.key)
+    env = make("CartPole-v1", 8)
+    env.seed(rnd.randint(sub, (1,), 0, 2**31 - 1))
+    obs, _ = env.reset()
+    done = torch.zeros(8, dtype=torch.bool)
+    tot = torch.zeros(8)
+    for _ in range(150):
+        a = torch.stack([policy(torch.utils._pytree.tree_map(lambda x: x[i], tree), obs[i]) for i in range(8)])
+        obs, r, term, trunc, _ = env.step(a)
+        tot += (~done).float() * r
+        done |= term | trunc
+        if done.all():
+            break
+    assert torch.allclose(ret, tot) and float(ret.max()) >= 9

@@ -133,3 +133,24 @@ def test_normalizer_running_statistics():
     allx = torch.cat([a, b])
     ref = (b - allx.mean(0)) / allx.std(0, unbiased=False)
     assert torch.allclose(out, ref, atol=1e-4)
+
+
+def test_gym_host_env_workers_match_sequential():
+    """Host environments stepped by 3 worker processes (the reference's Ray actors) give the
+    same returns as one worker; the policy runs batched in the controller."""
+    from evoxmi.problems.neuroevolution.reinforcement_learning import Gym
+    from evoxmi.problems.neuroevolution.reinforcement_learning.host_envs import PyCartPole
+
+    torch.manual_seed(0)
+    W = torch.randn(7, 4, 2)
+
+    def policy(w, obs):
+        return torch.einsum("no,noa->na", obs, w)
+
+    out = []
+    for nw in (1, 3):
+        prob = Gym(policy, num_workers=nw, env_creator=PyCartPole, batch_policy=True, cap_episode=200)
+        st = prob.init(rnd.PRNGKey(4))
+        r, _ = prob.evaluate(st, W)
+        out.append(r)
+    assert torch.equal(out[0], out[1]) and float(out[0].max()) > 9
