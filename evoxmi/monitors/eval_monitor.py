@@ -17,6 +17,7 @@ import torch
 import torch.utils._pytree as pytree
 
 from ..core import Monitor
+from .async_d2h import D2HCopier, HostList
 
 
 def _apply_dir(x, od):
@@ -40,8 +41,11 @@ class EvalMonitor(Monitor):
         self.topk = topk
         self.calc_pf = calc_pf
         self.history_to_host = history_to_host
-        self.fitness_history = []
-        self.solution_history = []
+        # history_to_host: entries are copied to pinned host memory on a side stream
+        # (async_d2h.D2HCopier) and resolved when read
+        self.fitness_history = HostList()
+        self.solution_history = HostList()
+        self._d2h = D2HCopier() if history_to_host else None
         self.topk_fitness = None
         self.topk_solutions = None
         self.pf_solutions = None
@@ -81,11 +85,9 @@ class EvalMonitor(Monitor):
     def _keep(self, x):
         if x is None:
             return None
-        if self.history_to_host and x.is_cuda:
-            h = torch.empty(x.shape, dtype=x.dtype, pin_memory=True)
-            h.copy_(x, non_blocking=True)
-            return h
-        return x.detach().clone()
+        if self._d2h is not None and isinstance(x, torch.Tensor):
+            return self._d2h.submit(x)
+        return pytree.tree_map(lambda t: t.detach().clone() if isinstance(t, torch.Tensor) else t, x)
 
     def post_eval(self, _state, cand_sol, _transformed, fitness):
         self.eval_count += int(fitness.shape[0])

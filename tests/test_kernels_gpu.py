@@ -885,3 +885,22 @@ def test_linear_gp_fit_kernel_matches_torch():
     v_r, s2_r = linear_gp_fit(a, b, c, n)
     v, s2 = linear_gp_fit(a.cuda(), b.cuda(), c.cuda(), n.cuda())
     assert torch.allclose(v.cpu(), v_r, rtol=1e-5) and torch.allclose(s2.cpu(), s2_r, rtol=1e-5)
+
+
+def test_eval_monitor_async_host_history_matches_device_history():
+    """history_to_host copies on a side stream (async_d2h) while the hipGraph-replayed
+    generations continue; the host history equals the device-kept one."""
+    from evoxmi.algorithms import CMAES
+    from evoxmi.monitors import EvalMonitor
+    from evoxmi.problems.numerical import Sphere
+    from evoxmi.workflows import StdWorkflow
+
+    m_host, m_dev = EvalMonitor(history_to_host=True), EvalMonitor()
+    wf = StdWorkflow(CMAES(torch.zeros(32, device="cuda") + 3, 1.0, pop_size=64), Sphere(), monitors=[m_host, m_dev], graph=True)
+    st = wf.init(rnd.PRNGKey(0, device="cuda"))
+    for _ in range(6):
+        st = wf.step(st)
+    hh, hd = m_host.get_history(), m_dev.get_history()
+    assert len(hh) == len(hd) == 7
+    for a, b in zip(hh, hd):
+        assert not a.is_cuda and torch.equal(a, b.cpu())
