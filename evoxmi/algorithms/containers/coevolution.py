@@ -25,7 +25,7 @@ def _as_stack(algos):
     return algos if isinstance(algos, StackedModules) else StackedModules(list(algos))
 
 
-class VectorizedCoevolution(Algorithm):
+class _CoevolutionBase(Algorithm):
     def __init__(self, base_algorithms, dim, num_subpops, random_subpop=False, dtype=torch.float32):
         super().__init__()
         self.base_algorithms = _as_stack(base_algorithms)
@@ -97,7 +97,70 @@ class VectorizedCoevolution(Algorithm):
         return state.update(best_dec=best_dec, best_fit=torch.minimum(bf, mins), coop_pops=None)
 
 
-class Coevolution(VectorizedCoevolution):
+class VectorizedCoevolution(_CoevolutionBase):
+    """Every sub-population advances each generation.  Multi-GPU (the
+    reference's vmap over sub-algorithms mapped onto devices): under
+    ``StdWorkflow.enable_distributed`` rank r owns sub-populations
+    [r·K/W, (r+1)·K/W) — it runs only their ask/tell and evaluates only their cooperative
+    rows; the objectives are all-gathered by the workflow and the K best blocks by one
+    all-gather of K × dim/K floats, so the context vector stays replicated.  Sub-states of
+    the other ranks' sub-populations are not advanced locally (rank-owned state)."""
+
+    pop_size = None  # rows per generation depend on the sub-algorithms (CSO asks P/2): dynamic all-gather
+
+    def _owned(self, dist):
+        K, W = self.num_subpops, dist.world_size
+        if K % W:
+            raise ValueError(f"VectorizedCoevolution on {W} ranks needs num_subpops divisible by the world size (got {K})")
+        per = K // W
+        return list(range(dist.rank * per, (dist.rank + 1) * per))
+
+    def init_ask_sharded(self, state, dist):
+        # every rank initialises every sub-algorithm (replicated, as the states are at this
+        # point); each owned sub-population scores the shared initial rows, so the global
+        # batch keeps the K·P shape of the later generations
+        init, state = self.init_ask(state)
+        local = init.repeat(len(self._owned(dist)), 1)
+        return local, state.update(coop_pops=init)
+
+    def init_tell_sharded(self, state, fitness, dist):
+        P = fitness.shape[0] // self.num_subpops
+        return self.init_tell(state, fitness[:P])  # the K copies are identical
+
+    def ask_sharded(self, state, dist):
+        ks = self._owned(dist)
+        subs = []
+        for k in ks:
+            sub, state = use_state(self.base_algorithms[k].ask, k)(state)
+            subs.append(sub)
+        P = subs[0].shape[0]
+        coop = state.best_dec.to(subs[0].device).expand(len(ks), P, self.dim).clone()
+        for i, k in enumerate(ks):
+            coop[i, :, k * self.sub_dim : (k + 1) * self.sub_dim] = subs[i]
+        coop = self._scatter_perm(coop.reshape(len(ks) * P, self.dim), state)
+        return coop, state.update(coop_pops=coop)
+
+    def tell_sharded(self, state, fitness, dist):
+        K = self.num_subpops
+        ks = self._owned(dist)
+        fit = fitness.reshape(K, -1)  # ranks own equal numbers of equal-size sub-populations
+        for k in ks:
+            state = use_state(self.base_algorithms[k].tell, k)(state, fit[k])
+        mins, arg = fit.min(1)
+        P = fit.shape[1]
+        loc = torch.arange(len(ks), device=fit.device)
+        kt = torch.tensor(ks, device=fit.device)
+        coop = state.coop_pops.reshape(len(ks), P, self.dim)
+        best_loc = self._gather_perm(coop[loc, arg[kt]], state)  # (|ks|, dim)
+        blocks = best_loc.reshape(len(ks), K, self.sub_dim)[loc, kt]  # block k of owned sub-population k's best
+        blocks = dist.all_gather_rows(blocks.contiguous(), K)  # (K, sub_dim), sub-population order
+        old = state.best_dec.to(blocks.device).reshape(K, self.sub_dim)
+        bf = state.best_fit.to(mins.device)
+        best_dec = torch.where((bf > mins)[:, None], blocks, old).reshape(self.dim)
+        return state.update(best_dec=best_dec, best_fit=torch.minimum(bf, mins), coop_pops=None)
+
+
+class Coevolution(_CoevolutionBase):
     def setup(self, key):
         return super().setup(key).update(iter_counter=0)
 

@@ -377,12 +377,14 @@ class StdWorkflow(Workflow):
                 m.set_dist(self._dist)
         state = self._dist.broadcast_state(state)
         if self._dist.algorithm_sharded:
-            pop_size = getattr(self.algorithm, "pop_size")
+            # None: the algorithm's per-step row count varies (e.g. co-evolution containers
+            # of CSO sub-swarms) — the fitness all-gather then exchanges the sizes
+            pop_size = getattr(self.algorithm, "pop_size", None)
             self._dist.set_global_pop(pop_size)
             # rank-local fields (e.g. the sampled rows) hold only this rank's slice from the
             # start, so every step keeps the same shapes (required for hipGraph capture)
             local = getattr(self.algorithm, "rank_local_fields", ())
-            if local:
+            if local and pop_size is not None:
                 start, size = self._dist.slice_of(pop_size)
                 alg = state.get_child_state("algorithm")
                 state = state.update_child("algorithm", alg.update(**{f: alg[f][start : start + size].clone() for f in local}))
