@@ -37,7 +37,9 @@ def dim_sharded_fitness(problem, X: torch.Tensor, group=None) -> torch.Tensor:
     d = X.shape[1]
     col0, own = balanced_slices(d, world)[rank]
     hi = min(col0 + own + problem.dim_halo, d)
-    T = problem.partial_terms(X[:, col0:hi], col0, d, own).contiguous()
+    # shifted-rotated problems shard the rotated coordinates: they take the full rows
+    Xb = X if getattr(problem, "dim_shard_full_rows", False) else X[:, col0:hi]
+    T = problem.partial_terms(Xb, col0, d, own).contiguous()
     if world > 1:
         dist.all_reduce(T, op=dist.ReduceOp.SUM, group=group)
     return problem.combine_terms(T, d)

@@ -255,7 +255,25 @@ class _CEC2022(Problem):
         return self._evaluate(X, c), state
 
 
-class F1_CEC2022(_CEC2022):
+class _RowSharded:
+    """Decision-axis sharding (strategy P2, ``evoxmi.parallel.dim_sharded``) of a shifted-
+    rotated function: the rotation mixes every column, so a rank does not take a column
+    block of x but a block of z = M(x − o)·s — its rows of M against the replicated
+    population (1/W of the rotation GEMM) — and returns per-row additive terms over its
+    z indices (``dim_shard_full_rows``: ``partial_terms`` receives the full rows)."""
+
+    dim_shard_full_rows = True
+    dim_halo = 0
+    ssr_scale = 1.0
+
+    def _zblock(self, X, col0, d, own, halo=0):
+        X = X.to(torch.float32).contiguous()
+        c = self._consts(d, X.device)
+        hi = min(col0 + own + halo, d)
+        return self._ssr(X, c["Os"][:d], c["M"][col0:hi].contiguous(), self.ssr_scale)
+
+
+class F1_CEC2022(_RowSharded, _CEC2022):
     """Shifted & rotated Zakharov."""
     func_num = 1
 
@@ -264,40 +282,95 @@ class F1_CEC2022(_CEC2022):
         Z = self._ssr(X, c["Os"][:D], c["M"], 1.0)
         return self._clamp(self._basic(Z, ZAKHAROV))
 
+    def partial_terms(self, X, col0, d, own):
+        z = self._zblock(X, col0, d, own)
+        i = torch.arange(col0 + 1, col0 + own + 1, device=z.device, dtype=z.dtype)
+        return torch.stack([(z * z).sum(1), (0.5 * i * z).sum(1)], 1)
 
-class F2_CEC2022(_CEC2022):
+    def combine_terms(self, T, d):
+        return self._clamp(T[:, 0] + T[:, 1] ** 2 + T[:, 1] ** 4)
+
+
+class F2_CEC2022(_RowSharded, _CEC2022):
     func_num = 2
+    ssr_scale = 2.048 / 100.0
 
     def _evaluate(self, X, c):
         D = X.shape[1]
         Z = self._ssr(X, c["Os"][:D], c["M"], 2.048 / 100.0)
         return self._clamp(self._basic(Z, ROSENBROCK))
 
+    def partial_terms(self, X, col0, d, own):
+        z = self._zblock(X, col0, d, own, halo=1) + 1  # pair terms whose left index is owned
+        n = min(own, d - 1 - col0)
+        if n <= 0:
+            return z.new_zeros(z.shape[0], 1)
+        a, b = z[:, :n], z[:, 1 : n + 1]
+        return (100 * (a * a - b) ** 2 + (1 - a) ** 2).sum(1, keepdim=True)
+
+    def combine_terms(self, T, d):
+        return self._clamp(T[:, 0])
+
 
 class F3_CEC2022(_CEC2022):
     """Schaffer F7 on y = x − o (the reference discards the rotation, kept for fidelity)."""
     func_num = 3
+    dim_halo = 1  # pair terms (y_j, y_{j+1}): plain column blocks suffice (no rotation)
 
     def _evaluate(self, X, c):
         D = X.shape[1]
         o = c["Os"][:D]
         return self._clamp(self._basic(X, SCHAFFERF7, sub=o))
 
+    def partial_terms(self, Xb, col0, d, own):
+        y = Xb.to(torch.float32) - self._consts(d, Xb.device)["Os"][col0 : col0 + Xb.shape[1]]
+        n = min(own, d - 1 - col0)
+        if n <= 0:
+            return y.new_zeros(y.shape[0], 1)
+        sq = torch.sqrt(y[:, :n] ** 2 + y[:, 1 : n + 1] ** 2)
+        t = torch.sin(50.0 * sq**0.2)
+        return (sq**0.5 + sq**0.5 * t * t).sum(1, keepdim=True)
 
-class F4_CEC2022(_CEC2022):
+    def combine_terms(self, T, d):
+        f = T[:, 0]
+        return self._clamp(f * f / (d - 1) / (d - 1))
+
+
+class F4_CEC2022(_RowSharded, _CEC2022):
     func_num = 4
 
     def _evaluate(self, X, c):
         D = X.shape[1]
         return self._clamp(self._basic(self._ssr(X, c["Os"][:D], c["M"], 1.0), RASTRIGIN))
 
+    def partial_terms(self, X, col0, d, own):
+        z = self._zblock(X, col0, d, own) * 0.0512
+        return (z * z - 10 * torch.cos(2 * math.pi * z) + 10).sum(1, keepdim=True)
 
-class F5_CEC2022(_CEC2022):
+    def combine_terms(self, T, d):
+        return self._clamp(T[:, 0])
+
+
+class F5_CEC2022(_RowSharded, _CEC2022):
     func_num = 5
 
     def _evaluate(self, X, c):
         D = X.shape[1]
         return self._clamp(self._basic(self._ssr(X, c["Os"][:D], c["M"], 1.0), LEVY))
+
+    def partial_terms(self, X, col0, d, own):
+        w = 1 + self._zblock(X, col0, d, own) / 4
+        j = torch.arange(col0, col0 + own, device=w.device)
+        first = (j == 0).to(w.dtype)
+        last = (j == d - 1).to(w.dtype)
+        mid = 1 - last
+        t1 = (first * torch.sin(math.pi * w) ** 2).sum(1)
+        t2 = (mid * (w - 1) ** 2 * (1 + 10 * torch.sin(math.pi * w + 1) ** 2)).sum(1)
+        t3 = (last * (w - 1) ** 2 * (1 + torch.sin(2 * math.pi * w) ** 2)).sum(1)
+        return (t1 + t2 + t3)[:, None]
+
+    def combine_terms(self, T, d):
+        return self._clamp(T[:, 0])
 
 
 class _Hybrid(_CEC2022):

@@ -78,3 +78,23 @@ def test_enable_multi_devices_gloo_matches_single_process():
     assert torch.equal(p0, p1)  # replicas stay identical: every rank combines the same all-reduced terms
     assert torch.allclose(g0, ref.global_best_fitness, rtol=1e-4, atol=1e-4)
     assert torch.allclose(p0, ref.population, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("fn", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_cec2022_partial_terms_reproduce_full_evaluation(fn, world):
+    """Shifted-rotated CEC'22 functions shard the rotated coordinates (their rows of M);
+    F3 (no rotation) takes plain column blocks with a halo of one."""
+    from evoxmi.problems.numerical import CEC2022TestSuit
+
+    p = CEC2022TestSuit.create(fn)
+    assert supports_dim_sharding(p)
+    d = 20
+    X = (torch.rand(13, d, generator=torch.Generator().manual_seed(fn)) * 20 - 10)
+    full, _ = p.evaluate(None, X)
+    T = 0
+    for col0, own in balanced_slices(d, world):
+        hi = min(col0 + own + p.dim_halo, d)
+        Xb = X if getattr(p, "dim_shard_full_rows", False) else X[:, col0:hi]
+        T = T + p.partial_terms(Xb, col0, d, own)
+    assert torch.allclose(p.combine_terms(T, d), full, rtol=2e-5, atol=1e-4)
