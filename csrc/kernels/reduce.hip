@@ -15,12 +15,28 @@ __global__ void __launch_bounds__(256) weighted_rowsum_kernel(const float* __res
   const int k0 = c * per, k1 = min(K, k0 + per);
   if (j >= D) return;
   const float m = sub ? sub[j] : 0.f;
-  float acc = 0.f;
-  for (int k = k0; k < k1; ++k) {
-    const int64_t r = idx ? (int64_t)idx[k] : (int64_t)k;
-    acc = fmaf(w[k], X[r * ldx + j] - m, acc);
+  // 4 rows in flight per iteration (independent gathers), fixed summation order
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int k = k0;
+  for (; k + 3 < k1; k += 4) {
+    int64_t r0 = k, r1 = k + 1, r2 = k + 2, r3 = k + 3;
+    if (idx) {
+      r0 = idx[k];
+      r1 = idx[k + 1];
+      r2 = idx[k + 2];
+      r3 = idx[k + 3];
+    }
+    const float x0 = X[r0 * ldx + j], x1 = X[r1 * ldx + j], x2 = X[r2 * ldx + j], x3 = X[r3 * ldx + j];
+    a0 = fmaf(w[k], x0 - m, a0);
+    a1 = fmaf(w[k + 1], x1 - m, a1);
+    a2 = fmaf(w[k + 2], x2 - m, a2);
+    a3 = fmaf(w[k + 3], x3 - m, a3);
   }
-  partial[(int64_t)c * D + j] = acc;
+  for (; k < k1; ++k) {
+    const int64_t r = idx ? (int64_t)idx[k] : (int64_t)k;
+    a0 = fmaf(w[k], X[r * ldx + j] - m, a0);
+  }
+  partial[(int64_t)c * D + j] = (a0 + a1) + (a2 + a3);
 }
 }  // namespace
 

@@ -904,3 +904,17 @@ def test_eval_monitor_async_host_history_matches_device_history():
     assert len(hh) == len(hd) >= 6
     for a, b in zip(hh, hd):
         assert not a.is_cuda and torch.equal(a, b.cpu())
+
+
+@pytest.mark.parametrize("K,D", [(5000, 1000), (7, 33), (130, 257)])
+def test_weighted_rowsum_kernel(K, D):
+    from evoxmi.ops.reduce import weighted_rowsum
+
+    g = torch.Generator().manual_seed(K)
+    X = torch.randn(K + 50, D, generator=g)
+    idx = torch.randperm(K + 50, generator=g)[:K].to(torch.int32)
+    w = torch.rand(K, generator=g)
+    sub = torch.randn(D, generator=g)
+    ref = (w.double()[:, None] * (X[idx.long()].double() - sub.double())).sum(0)
+    out = weighted_rowsum(X.cuda(), idx.cuda(), w.cuda(), sub.cuda(), K).cpu()
+    assert torch.allclose(out.double(), ref, rtol=1e-4, atol=1e-3)
