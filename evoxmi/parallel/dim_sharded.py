@@ -39,7 +39,14 @@ def dim_sharded_fitness(problem, X: torch.Tensor, group=None) -> torch.Tensor:
     hi = min(col0 + own + problem.dim_halo, d)
     # shifted-rotated problems shard the rotated coordinates: they take the full rows
     Xb = X if getattr(problem, "dim_shard_full_rows", False) else X[:, col0:hi]
-    T = problem.partial_terms(Xb, col0, d, own).contiguous()
+    T = problem.partial_terms(Xb, col0, d, own)
+    if isinstance(T, tuple):  # (sum terms, max terms), e.g. LSMOP's Schwefel groups
+        Ts, Tm = T[0].contiguous(), T[1].contiguous()
+        if world > 1:
+            dist.all_reduce(Ts, op=dist.ReduceOp.SUM, group=group)
+            dist.all_reduce(Tm, op=dist.ReduceOp.MAX, group=group)
+        return problem.combine_terms((Ts, Tm), d)
+    T = T.contiguous()
     if world > 1:
         dist.all_reduce(T, op=dist.ReduceOp.SUM, group=group)
     return problem.combine_terms(T, d)

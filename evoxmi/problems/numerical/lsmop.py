@@ -59,11 +59,86 @@ class LSMOP(Problem):
         self.len = tuple(lens)
         self.d = self.m + 4 if d is None else d
 
+    _funcs = (sphere_func,)
+    _cosine = False
+    # decision-axis sharding (evoxmi.parallel.dim_sharded): full rows (the linkage needs
+    # x₁), each rank reduces the parts of the m·nk variable groups inside its column block
+    dim_shard_full_rows = True
+    dim_halo = 0
+    dim_shard_max_terms = True  # the Schwefel groups reduce with max
+
     def setup(self, key):
         return State(key=key)
 
     def pf(self):
         return UniformSampling(self.ref_num * self.m, self.m)()[0] / 2
+
+    def _groups(self):
+        """(objective k, column start, length, inner function) of every subcomponent."""
+        out = []
+        for k, (len_, sublen, func) in enumerate(zip(self.len, self.sublen, cycle(self._funcs))):
+            if k >= self.m:
+                break
+            for j in range(self.nk):
+                out.append((k, len_ + self.m - 1 + j * sublen, sublen, func))
+        return out
+
+    def partial_terms(self, X, col0, d, own):
+        n, m = X.shape[0], self.m
+        c1 = col0 + own
+        x = self._link(X, self._cosine)
+        groups = self._groups()
+        T = X.new_zeros(n, 3 * len(groups) + m - 1)
+        Tm = X.new_zeros(n, len(groups))
+        for gi, (k, s, L, func) in enumerate(groups):
+            a, b = max(s, col0), min(s + L, c1)
+            if a >= b:
+                continue
+            z = x[:, a:b]
+            if func is sphere_func:
+                T[:, 3 * gi] = (z * z).sum(1)
+            elif func is _rastrigin:
+                T[:, 3 * gi] = (z * z - 10 * torch.cos(2 * math.pi * z) + 10).sum(1)
+            elif func is rosenbrock_func:
+                hi = min(b, s + L - 1)  # pairs (i, i + 1) inside the group whose left index is owned
+                if hi > a:
+                    u, v = x[:, a:hi], x[:, a + 1 : hi + 1]
+                    T[:, 3 * gi] = (100 * (v - u * u) ** 2 + (u - 1) ** 2).sum(1)
+            elif func is griewank_func:
+                i = torch.arange(a - s + 1, b - s + 1, device=X.device, dtype=X.dtype)
+                cz = torch.cos(z / torch.sqrt(i))
+                T[:, 3 * gi] = (z * z).sum(1) / 4000
+                T[:, 3 * gi + 1] = torch.log(torch.abs(cz)).sum(1)
+                T[:, 3 * gi + 2] = (cz < 0).to(X.dtype).sum(1)
+            elif func is _ackley:
+                T[:, 3 * gi] = (z * z).sum(1)
+                T[:, 3 * gi + 1] = torch.cos(2 * math.pi * z).sum(1)
+            elif func is _schwefel:
+                Tm[:, gi] = torch.abs(z).amax(1)
+        lo, hi = col0, min(c1, m - 1)
+        if hi > lo:  # the position variables x₁…x_{m−1} for the front
+            T[:, 3 * len(groups) + lo : 3 * len(groups) + hi] = X[:, lo:hi]
+        return T, Tm
+
+    def combine_terms(self, T, d):
+        T, Tm = T
+        n, m = T.shape[0], self.m
+        groups = self._groups()
+        g = T.new_zeros(n, m)
+        for gi, (k, s, L, func) in enumerate(groups):
+            t0, t1, t2 = T[:, 3 * gi], T[:, 3 * gi + 1], T[:, 3 * gi + 2]
+            if func is griewank_func:
+                sign = 1 - 2 * torch.remainder(torch.round(t2), 2)
+                v = t0 - sign * torch.exp(t1) + 1
+            elif func is _ackley:
+                v = -20 * torch.exp(-0.2 * torch.sqrt(t0 / L)) - torch.exp(t1 / L) + 20 + math.e
+            elif func is _schwefel:
+                v = Tm[:, gi]
+            else:
+                v = t0
+            g[:, k] = g[:, k] + v / (L * self.nk)
+        Xf = T[:, 3 * len(groups) :]
+        return self._finish(Xf, g)
 
     def _g(self, inner_funcs, X, cosine: bool):
         """Distance terms g (n, m) from the RAW decisions: on a GPU one fused pass
@@ -111,26 +186,29 @@ class LSMOP(Problem):
         return g2 * a * b
 
 
-class LSMOP1(LSMOP):
+class _Linear(LSMOP):
     def evaluate(self, state, X):
-        return self._linear_front(X, self._g([sphere_func], X, False)), state
+        return self._finish(X, self._g(self._funcs, X, self._cosine)), state
+
+    def _finish(self, X, g):
+        return self._linear_front(X, g)
 
 
-class LSMOP2(LSMOP):
-    def evaluate(self, state, X):
-        return self._linear_front(X, self._g([griewank_func, _schwefel], X, False)), state
+class LSMOP1(_Linear):
+    _funcs = (sphere_func,)
 
 
-class LSMOP3(LSMOP):
+class LSMOP2(_Linear):
+    _funcs = (griewank_func, _schwefel)
+
+
+class LSMOP3(_Linear):
     _late_d = False
-
-    def evaluate(self, state, X):
-        return self._linear_front(X, self._g([_rastrigin, rosenbrock_func], X, False)), state
+    _funcs = (_rastrigin, rosenbrock_func)
 
 
-class LSMOP4(LSMOP):
-    def evaluate(self, state, X):
-        return self._linear_front(X, self._g([_ackley, griewank_func], X, False)), state
+class LSMOP4(_Linear):
+    _funcs = (_ackley, griewank_func)
 
 
 class _SphericalPF:
@@ -139,33 +217,45 @@ class _SphericalPF:
         return f / torch.sqrt((f * f).sum(1, keepdim=True))
 
 
-class LSMOP5(_SphericalPF, LSMOP):
+class _Spherical(LSMOP):
+    _cosine = True
+
     def evaluate(self, state, X):
-        return self._spherical_front(X, self._g([sphere_func], X, True)), state
+        return self._finish(X, self._g(self._funcs, X, self._cosine)), state
+
+    def _finish(self, X, g):
+        return self._spherical_front(X, g)
 
 
-class LSMOP6(LSMOP):
-    def evaluate(self, state, X):
-        return self._spherical_front(X, self._g([rosenbrock_func, _schwefel], X, True)), state
+class LSMOP5(_SphericalPF, _Spherical):
+    _funcs = (sphere_func,)
 
 
-class LSMOP7(_SphericalPF, LSMOP):
-    def evaluate(self, state, X):
-        return self._spherical_front(X, self._g([_ackley, rosenbrock_func], X, True)), state
+class LSMOP6(_Spherical):
+    _funcs = (rosenbrock_func, _schwefel)
 
 
-class LSMOP8(_SphericalPF, LSMOP):
-    def evaluate(self, state, X):
-        return self._spherical_front(X, self._g([griewank_func, sphere_func], X, True)), state
+class LSMOP7(_SphericalPF, _Spherical):
+    _funcs = (_ackley, rosenbrock_func)
+
+
+class LSMOP8(_SphericalPF, _Spherical):
+    _funcs = (griewank_func, sphere_func)
 
 
 class LSMOP9(LSMOP):
+    _funcs = (sphere_func, _ackley)
+    _cosine = True
+
     def evaluate(self, state, X):
+        return self._finish(X, self._g(self._funcs, X, self._cosine)), state
+
+    def _finish(self, X, g):
         m = self.m
-        g = 1 + self._g([sphere_func, _ackley], X, True).sum(1, keepdim=True)
+        g = 1 + g.sum(1, keepdim=True)
         fm = X[:, : m - 1]
         last = (1 + g) * (m - (fm / (1 + g) * (1 + torch.sin(3 * math.pi * fm))).sum(1, keepdim=True))
-        return torch.cat([fm, last], 1), state
+        return torch.cat([fm, last], 1)
 
     def pf(self):
         interval = [0, 0.251412, 0.631627, 0.859401]

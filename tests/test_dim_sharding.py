@@ -98,3 +98,24 @@ def test_cec2022_partial_terms_reproduce_full_evaluation(fn, world):
         Xb = X if getattr(p, "dim_shard_full_rows", False) else X[:, col0:hi]
         T = T + p.partial_terms(Xb, col0, d, own)
     assert torch.allclose(p.combine_terms(T, d), full, rtol=2e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("fn", range(1, 10))
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_lsmop_partial_terms_reproduce_full_evaluation(fn, world):
+    """LSMOP (config 5's problem, the d ≥ 10⁴ use case): every rank reduces the parts of the
+    m·nk variable groups inside its column block (sum terms; the Schwefel groups by max,
+    the Griewank products through log|cos| + sign counts)."""
+    import evoxmi.problems.numerical as P
+
+    p = getattr(P, f"LSMOP{fn}")(d=120, m=3)
+    assert supports_dim_sharding(p)
+    X = torch.rand(9, 120, generator=torch.Generator().manual_seed(fn), dtype=torch.float64)
+    X[:, 2:] = X[:, 2:] * 10
+    full, _ = p.evaluate(None, X)
+    Ts = Tm = 0
+    for col0, own in balanced_slices(120, world):
+        ts, tm = p.partial_terms(X, col0, 120, own)
+        Ts = Ts + ts
+        Tm = torch.maximum(Tm, tm) if torch.is_tensor(Tm) else tm
+    assert torch.allclose(p.combine_terms((Ts, Tm), 120), full, rtol=1e-9, atol=1e-9)
