@@ -331,19 +331,20 @@ at::Tensor sbr_bq(const at::Tensor& B, int64_t off, const at::Tensor& perm, cons
 
 
 // 16-wide blocks in a shifted sorted order (eigh_sbr16.hip)
-std::vector<at::Tensor> sbr16_block(const at::Tensor& A, int64_t shift, int64_t sweeps) {
+std::vector<at::Tensor> sbr16_block(const at::Tensor& A, int64_t shift, int64_t sweeps, int64_t sb) {
   check_rowmajor(A, "A");
   const int64_t n = A.size(0);
   TORCH_CHECK(A.size(1) == n && n >= 2 && n <= evx_sbr16_max_n(), "sbr16_block: square A with 2 <= n <= ", evx_sbr16_max_n());
   TORCH_CHECK(shift >= 0 && shift < n, "sbr16_block: shift in [0, n)");
   TORCH_CHECK(sweeps >= 0 && sweeps <= 64, "sbr16_block: sweeps in [0, 64]");
+  TORCH_CHECK(sb == 16 || sb == 32, "sbr16_block: block size 16 or 32");
   c10::DeviceGuard g(A.device());
-  const int nb = evx_sbr16_nblocks((int)n);
+  const int nb = evx_sbr16_nblocks((int)n, (int)sb);
   auto perm = at::empty({n}, A.options().dtype(at::kInt));
-  auto Q = at::empty({nb, 16, 16}, A.options());
+  auto Q = at::empty({nb, sb, sb}, A.options());
   auto dq = at::empty({n}, A.options());
   evx_sbr16_block(A.data_ptr<float>(), (int)n, A.stride(0), (int)shift, (int)sweeps, perm.data_ptr<int>(), Q.data_ptr<float>(),
-                  dq.data_ptr<float>(), cur_stream());
+                  dq.data_ptr<float>(), (int)sb, cur_stream());
   return {perm, Q, dq};
 }
 
@@ -392,10 +393,13 @@ std::vector<at::Tensor> linear_gp_fit(const at::Tensor& a, const at::Tensor& b, 
   return {v, s2};
 }
 
-void check_sbr16_operands(int64_t n, const at::Tensor& perm, const at::Tensor& Q) {
+int64_t check_sbr16_operands(int64_t n, const at::Tensor& perm, const at::Tensor& Q) {
   TORCH_CHECK(perm.is_cuda() && perm.scalar_type() == at::kInt && perm.numel() == n && perm.is_contiguous(), "perm int32[n]");
-  TORCH_CHECK(Q.is_cuda() && Q.scalar_type() == at::kFloat && Q.is_contiguous() && Q.numel() == (int64_t)evx_sbr16_nblocks((int)n) * 256,
-              "Q [ceil(n/16),16,16]");
+  TORCH_CHECK(Q.dim() == 3 && (Q.size(1) == 16 || Q.size(1) == 32) && Q.size(2) == Q.size(1), "Q [nb, sb, sb], sb 16 or 32");
+  const int64_t sb = Q.size(1);
+  TORCH_CHECK(Q.is_cuda() && Q.scalar_type() == at::kFloat && Q.is_contiguous() && Q.size(0) == evx_sbr16_nblocks((int)n, (int)sb),
+              "Q [ceil(n/sb), sb, sb]");
+  return sb;
 }
 
 at::Tensor sbr16_far(const at::Tensor& A, const at::Tensor& perm, const at::Tensor& Q, const at::Tensor& dq, const at::Tensor& stats,
@@ -403,24 +407,24 @@ at::Tensor sbr16_far(const at::Tensor& A, const at::Tensor& perm, const at::Tens
   check_rowmajor(A, "A");
   const int64_t n = A.size(0);
   TORCH_CHECK(A.size(1) == n, "A must be square");
-  check_sbr16_operands(n, perm, Q);
+  const int64_t sb = check_sbr16_operands(n, perm, Q);
   TORCH_CHECK(dq.is_cuda() && dq.scalar_type() == at::kFloat && dq.numel() == n && dq.is_contiguous(), "dq float[n]");
   TORCH_CHECK(stats.is_cuda() && stats.scalar_type() == at::kDouble && stats.numel() >= 4 && stats.is_contiguous(), "stats double[4]");
   c10::DeviceGuard g(A.device());
   auto X = at::empty({n, n}, A.options());
   evx_sbr16_far(A.data_ptr<float>(), (int)n, A.stride(0), perm.data_ptr<int>(), Q.data_ptr<float>(), dq.data_ptr<float>(),
-                stats.data_ptr<double>(), (float)thr_fac, (float)theta, X.data_ptr<float>(), n, cur_stream());
+                stats.data_ptr<double>(), (float)thr_fac, (float)theta, X.data_ptr<float>(), n, (int)sb, cur_stream());
   return X;
 }
 
 at::Tensor sbr16_bq(const at::Tensor& B, const at::Tensor& perm, const at::Tensor& Q) {
   check_rowmajor(B, "B");
   const int64_t rows = B.size(0), n = B.size(1);
-  check_sbr16_operands(n, perm, Q);
+  const int64_t sb = check_sbr16_operands(n, perm, Q);
   c10::DeviceGuard g(B.device());
   auto Bq = at::empty({rows, n}, B.options());
   evx_sbr16_bq(B.data_ptr<float>(), (int)rows, (int)n, B.stride(0), perm.data_ptr<int>(), Q.data_ptr<float>(), Bq.data_ptr<float>(), n,
-               cur_stream());
+               (int)sb, cur_stream());
   return Bq;
 }
 
@@ -906,7 +910,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("sbr_far(Tensor A, int off, Tensor perm, Tensor Q, Tensor dq, Tensor stats, float thr_fac) -> Tensor");
   m.def("sbr_bq(Tensor B, int off, Tensor perm, Tensor Q) -> Tensor");
   m.def("sbr_symstats(Tensor T) -> Tensor[]");
-  m.def("sbr16_block(Tensor A, int shift, int sweeps) -> Tensor[]");
+  m.def("sbr16_block(Tensor A, int shift, int sweeps, int sb=16) -> Tensor[]");
   m.def("sbr16_far(Tensor A, Tensor perm, Tensor Q, Tensor dq, Tensor stats, float thr_fac, float theta) -> Tensor");
   m.def("sbr16_bq(Tensor B, Tensor perm, Tensor Q) -> Tensor");
   m.def("sbr_taylor4_prep(Tensor X, Tensor X2, Tensor? alpha=None) -> Tensor[]");

@@ -107,14 +107,14 @@ void evx_sbr_bq(const float* B, int rows, int n, int64_t ldb, int off, const int
                 hipStream_t s);
 int evx_sbr_symstats_parts(int n);
 // 16-wide blocks in a shifted sorted order (eigh_sbr16.hip)
-int evx_sbr16_nblocks(int n);
+int evx_sbr16_nblocks(int n, int sb);
 int evx_sbr16_max_n();
 void evx_sbr_taylor4_prep(const float* X, const float* X2, int n, const float* alpha, float* P, float* M, hipStream_t s);
 void evx_sbr_damping(const float* X2, int n, int64_t ldx, const float* V, float* work, float tau, float* alpha, hipStream_t s);
-void evx_sbr16_block(const float* A, int n, int64_t lda, int shift, int sweeps, int* perm, float* Q, float* dq, hipStream_t s);
+void evx_sbr16_block(const float* A, int n, int64_t lda, int shift, int sweeps, int* perm, float* Q, float* dq, int sb, hipStream_t s);
 void evx_sbr16_far(const float* A, int n, int64_t lda, const int* perm, const float* Q, const float* dq, const double* stats,
-                   float thr_fac, float theta, float* X, int64_t ldx, hipStream_t s);
-void evx_sbr16_bq(const float* B, int rows, int n, int64_t ldb, const int* perm, const float* Q, float* Bq, int64_t ldq,
+                   float thr_fac, float theta, float* X, int64_t ldx, int sb, hipStream_t s);
+void evx_sbr16_bq(const float* B, int rows, int n, int64_t ldb, const int* perm, const float* Q, float* Bq, int64_t ldq, int sb,
                   hipStream_t s);
 void evx_sbr_symstats(const float* T, int n, int64_t ldt, float* A, int64_t lda, double* part, double* out, hipStream_t s);
 void evx_sbr_taylor_prep(const float* X, const float* X2, const float* X3, int n, const float* alpha, float* P, float* M,

@@ -29,8 +29,7 @@
 
 namespace {
 
-constexpr int SB = 16;            // block size
-constexpr int SP = 17;            // LDS pitch of a block (odd: conflict-free columns)
+// block size SB ∈ {16, 32} is a template parameter; LDS pitch SB + 1 (odd: conflict-free columns)
 constexpr int TL = 64;            // tile of the generator / Bq kernels (four blocks)
 constexpr int TP = 68;            // LDS pitch of a 64-wide tile (float4 aligned)
 constexpr int kRankMax = 8192;    // largest n of the rank kernel (32 KB of keys in LDS)
@@ -64,7 +63,8 @@ __global__ void __launch_bounds__(256) sbr16_rank_kernel(const float* __restrict
   }
 }
 
-// circle-method round robin on 16 slots: round r pairs (15, r) and ((r+i) mod 15, (r−i) mod 15)
+// circle-method round robin on SB slots: round r pairs (SB−1, r) and ((r+i) mod (SB−1), (r−i) mod (SB−1))
+template <int SB>
 __device__ __forceinline__ int2 rr16(int r, int i) {
   int a = SB - 1, b = r;
   if (i) {
@@ -93,9 +93,11 @@ __device__ __forceinline__ float3 rot16(float app, float aqq, float apq) {
 // transposes: S stays symmetric; pair u's own block set exactly), and every lane rotates a
 // 2×2 block of Q' = Q J (rows 2(L/8)+{0,1}, column pair L mod 8).  All updates are in place:
 // the 2×2 blocks of one round partition S and Q.
-__global__ void __launch_bounds__(64) sbr16_block_kernel(const float* __restrict__ A, int n, int64_t lda,
-                                                         const int* __restrict__ perm, int sweeps, float* __restrict__ Q_out,
-                                                         float* __restrict__ dq_out) {
+template <int SB>
+__global__ void __launch_bounds__(SB * SB / 4) sbr16_block_kernel(const float* __restrict__ A, int n, int64_t lda,
+                                                                  const int* __restrict__ perm, int sweeps, float* __restrict__ Q_out,
+                                                                  float* __restrict__ dq_out) {
+  constexpr int SP = SB + 1, NT = SB * SB / 4;
   __shared__ float S[SB * SP];
   __shared__ float Qm[SB * SP];
   __shared__ float4 rot[SB / 2];
@@ -105,8 +107,8 @@ __global__ void __launch_bounds__(64) sbr16_block_kernel(const float* __restrict
   if (lane < SB) members[lane] = lane < m ? perm[s0 + lane] : -1;
   __syncthreads();
 #pragma unroll
-  for (int e = lane; e < SB * SB; e += 64) {
-    const int a = e >> 4, c = e & 15;
+  for (int e = lane; e < SB * SB; e += NT) {
+    const int a = e / SB, c = e % SB;
     const int ra = members[a], rc = members[c];
     S[a * SP + c] = (ra >= 0 && rc >= 0) ? A[(int64_t)ra * lda + rc] : 0.f;
     Qm[a * SP + c] = a == c ? 1.f : 0.f;
@@ -121,18 +123,18 @@ __global__ void __launch_bounds__(64) sbr16_block_kernel(const float* __restrict
   const int v = u + rem;
   const bool item = lane < (SB / 2) * (SB / 2 + 1) / 2;
   const bool dg = u == v;
-  const int qr = (lane >> 3) * 2, qv = lane & 7;  // Q rows qr, qr+1; column pair qv
+  const int qr = (lane / (SB / 2)) * 2, qv = lane % (SB / 2);  // Q rows qr, qr+1; column pair qv
   const int G = (SB - 1) * sweeps;
   for (int g = 0; g < G; ++g) {
     const int r = g % (SB - 1);
     if (lane < SB / 2) {
-      const int2 p = rr16(r, lane);
+      const int2 p = rr16<SB>(r, lane);
       const float3 cs = rot16(S[p.x * SP + p.x], S[p.y * SP + p.y], S[p.x * SP + p.y]);
       rot[lane] = make_float4(cs.x, cs.y, cs.z, 0.f);
     }
     __syncthreads();
     {
-      const int2 pq = rr16(r, qv);
+      const int2 pq = rr16<SB>(r, qv);
       const float4 rq = rot[qv];
       const float x0 = Qm[qr * SP + pq.x], y0 = Qm[qr * SP + pq.y];
       const float x1 = Qm[(qr + 1) * SP + pq.x], y1 = Qm[(qr + 1) * SP + pq.y];
@@ -142,7 +144,7 @@ __global__ void __launch_bounds__(64) sbr16_block_kernel(const float* __restrict
       Qm[(qr + 1) * SP + pq.y] = rq.y * x1 + rq.x * y1;
     }
     if (item) {
-      const int2 pu = rr16(r, u), pv = rr16(r, v);
+      const int2 pu = rr16<SB>(r, u), pv = rr16<SB>(r, v);
       const float4 ru = rot[u], rv = rot[v];
       const int ux = pu.x * SP, uy = pu.y * SP, vx = pv.x * SP, vy = pv.y * SP;
       const float a = S[ux + pv.x], b = S[ux + pv.y], c = S[uy + pv.x], d = S[uy + pv.y];
@@ -170,22 +172,24 @@ __global__ void __launch_bounds__(64) sbr16_block_kernel(const float* __restrict
   }
   float* Qo = Q_out + (int64_t)blockIdx.x * SB * SB;
 #pragma unroll
-  for (int e = lane; e < SB * SB; e += 64) Qo[e] = Qm[(e >> 4) * SP + (e & 15)];
+  for (int e = lane; e < SB * SB; e += NT) Qo[e] = Qm[(e / SB) * SP + (e % SB)];
   if (lane < m) dq_out[s0 + lane] = S[lane * SP + lane];
 }
 
 // ------------------------------------------------------------------ block-diagonal tile helpers
 // Qt[a][c] (64×64 in LDS, pitch TP) = blockdiag of the four 16×16 Q blocks of tile t (0 elsewhere
 // is never read: the contractions below stay inside a block)
+template <int SB>
 __device__ __forceinline__ void load_qtile(const float* __restrict__ Q, int nb, int t, float* Qt) {
-  for (int e = threadIdx.x; e < 4 * SB * SB; e += blockDim.x) {
-    const int blk = e >> 8, a = (e >> 4) & 15, c = e & 15;
-    const int gb = 4 * t + blk;
+  for (int e = threadIdx.x; e < TL * SB; e += blockDim.x) {
+    const int blk = e / (SB * SB), a = (e / SB) % SB, c = e % SB;
+    const int gb = (TL / SB) * t + blk;
     Qt[(blk * SB + a) * TP + blk * SB + c] = gb < nb ? Q[(int64_t)gb * SB * SB + a * SB + c] : (a == c ? 1.f : 0.f);
   }
 }
 
 // ------------------------------------------------------------------ 3. far-pair generator
+template <int SB>
 __global__ void __launch_bounds__(256) sbr16_far_kernel(const float* __restrict__ A, int n, int64_t lda,
                                                         const int* __restrict__ perm, const float* __restrict__ Q,
                                                         const float* __restrict__ dq, const double* __restrict__ stats,
@@ -223,8 +227,8 @@ __global__ void __launch_bounds__(256) sbr16_far_kernel(const float* __restrict_
       tk[t] = th;
     }
   }
-  load_qtile(Q, nb, K, Qk);
-  load_qtile(Q, nb, L, Ql);
+  load_qtile<SB>(Q, nb, K, Qk);
+  load_qtile<SB>(Q, nb, L, Ql);
   __syncthreads();
   for (int e = threadIdx.x; e < TL * TL; e += blockDim.x) {
     const int a = e >> 6, f = e & 63;
@@ -235,7 +239,7 @@ __global__ void __launch_bounds__(256) sbr16_far_kernel(const float* __restrict_
   const int r0 = (threadIdx.x >> 4) << 2, c0 = (threadIdx.x & 15) << 2;
   // T[c][f] = Σ_{a in block(c)} Qk[a][c] G[a][f]: rows r0..r0+3 share one block
   float acc[4][4] = {};
-  const int ab = r0 & ~15;
+  const int ab = r0 & ~(SB - 1);
 #pragma unroll
   for (int a = 0; a < SB; ++a) {
     const float4 lq = *(const float4*)(Qk + (ab + a) * TP + r0);
@@ -255,7 +259,7 @@ __global__ void __launch_bounds__(256) sbr16_far_kernel(const float* __restrict_
   __syncthreads();
   // A1[c][e] = Σ_{f in block(e)} T[c][f] Ql[f][e]
   float out[4][4] = {};
-  const int fb = c0 & ~15;
+  const int fb = c0 & ~(SB - 1);
 #pragma unroll
   for (int f = 0; f < SB; ++f) {
     const float4 q = *(const float4*)(Ql + (fb + f) * TP + c0);
@@ -272,7 +276,7 @@ __global__ void __launch_bounds__(256) sbr16_far_kernel(const float* __restrict_
   for (int i = 0; i < 4; ++i) {
     const int c = r0 + i;
     if (c >= mk) continue;
-    const int bc = (sk + c) >> 4;
+    const int bc = (sk + c) / SB;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int e = c0 + j;
@@ -280,13 +284,14 @@ __global__ void __launch_bounds__(256) sbr16_far_kernel(const float* __restrict_
       const float den = dl[e] - dk[c];
       // the 2×2 Jacobi angle ½·atan(2a/den): a/den to first order for well-separated pairs,
       // saturating at π/4 for strongly coupled ones
-      const bool far = ((sl + e) >> 4) != bc && fabsf(den) > fminf(tk[c], tl[e]);
+      const bool far = ((sl + e) / SB) != bc && fabsf(den) > fminf(tk[c], tl[e]);
       X[(int64_t)(sk + c) * ldx + sl + e] = far ? 0.5f * atanf(2.f * out[i][j] / den) : 0.f;
     }
   }
 }
 
 // ------------------------------------------------------------------ 4. Bq = B[:, perm]·blockdiag(Q)
+template <int SB>
 __global__ void __launch_bounds__(256) sbr16_bq_kernel(const float* __restrict__ B, int rows, int n, int64_t ldb,
                                                        const int* __restrict__ perm, const float* __restrict__ Q,
                                                        float* __restrict__ Bq, int64_t ldq) {
@@ -297,7 +302,7 @@ __global__ void __launch_bounds__(256) sbr16_bq_kernel(const float* __restrict__
   const int nb = (n + SB - 1) / SB;
   const int sl = L * TL, ml = min(TL, n - sl);
   if (threadIdx.x < TL) pl[threadIdx.x] = threadIdx.x < ml ? perm[sl + threadIdx.x] : -1;
-  load_qtile(Q, nb, L, Ql);
+  load_qtile<SB>(Q, nb, L, Ql);
   __syncthreads();
   for (int e = threadIdx.x; e < TL * TL; e += blockDim.x) {
     const int r = e >> 6, f = e & 63;
@@ -306,7 +311,7 @@ __global__ void __launch_bounds__(256) sbr16_bq_kernel(const float* __restrict__
   }
   __syncthreads();
   const int r0 = (threadIdx.x >> 4) << 2, c0 = (threadIdx.x & 15) << 2;
-  const int fb = c0 & ~15;
+  const int fb = c0 & ~(SB - 1);
   float out[4][4] = {};
 #pragma unroll
   for (int f = 0; f < SB; ++f) {
@@ -416,24 +421,33 @@ __global__ void __launch_bounds__(256) sbr_taylor4_prep_kernel(const float* __re
 
 }  // namespace
 
-int evx_sbr16_nblocks(int n) { return (n + SB - 1) / SB; }
+int evx_sbr16_nblocks(int n, int sb) { return (n + sb - 1) / sb; }
 int evx_sbr16_max_n() { return kRankMax; }
 
-void evx_sbr16_block(const float* A, int n, int64_t lda, int shift, int sweeps, int* perm, float* Q, float* dq, hipStream_t s) {
+void evx_sbr16_block(const float* A, int n, int64_t lda, int shift, int sweeps, int* perm, float* Q, float* dq, int sb, hipStream_t s) {
   sbr16_rank_kernel<<<(n + 63) / 64, 256, 0, s>>>(A, n, lda, shift, perm);
-  sbr16_block_kernel<<<(n + SB - 1) / SB, 64, 0, s>>>(A, n, lda, perm, sweeps, Q, dq);
+  if (sb == 32)
+    sbr16_block_kernel<32><<<(n + 31) / 32, 256, 0, s>>>(A, n, lda, perm, sweeps, Q, dq);
+  else
+    sbr16_block_kernel<16><<<(n + 15) / 16, 64, 0, s>>>(A, n, lda, perm, sweeps, Q, dq);
 }
 
 void evx_sbr16_far(const float* A, int n, int64_t lda, const int* perm, const float* Q, const float* dq, const double* stats,
-                   float thr_fac, float theta, float* X, int64_t ldx, hipStream_t s) {
+                   float thr_fac, float theta, float* X, int64_t ldx, int sb, hipStream_t s) {
   const int nt = (n + TL - 1) / TL;
-  sbr16_far_kernel<<<dim3(nt, nt), 256, 0, s>>>(A, n, lda, perm, Q, dq, stats, thr_fac, theta, X, ldx);
+  if (sb == 32)
+    sbr16_far_kernel<32><<<dim3(nt, nt), 256, 0, s>>>(A, n, lda, perm, Q, dq, stats, thr_fac, theta, X, ldx);
+  else
+    sbr16_far_kernel<16><<<dim3(nt, nt), 256, 0, s>>>(A, n, lda, perm, Q, dq, stats, thr_fac, theta, X, ldx);
 }
 
-void evx_sbr16_bq(const float* B, int rows, int n, int64_t ldb, const int* perm, const float* Q, float* Bq, int64_t ldq,
+void evx_sbr16_bq(const float* B, int rows, int n, int64_t ldb, const int* perm, const float* Q, float* Bq, int64_t ldq, int sb,
                   hipStream_t s) {
   const int nt = (n + TL - 1) / TL;
-  sbr16_bq_kernel<<<dim3(nt, (rows + TL - 1) / TL), 256, 0, s>>>(B, rows, n, ldb, perm, Q, Bq, ldq);
+  if (sb == 32)
+    sbr16_bq_kernel<32><<<dim3(nt, (rows + TL - 1) / TL), 256, 0, s>>>(B, rows, n, ldb, perm, Q, Bq, ldq);
+  else
+    sbr16_bq_kernel<16><<<dim3(nt, (rows + TL - 1) / TL), 256, 0, s>>>(B, rows, n, ldb, perm, Q, Bq, ldq);
 }
 
 void evx_sbr_damping(const float* X2, int n, int64_t ldx, const float* V, float* work, float tau, float* alpha, hipStream_t s) {

@@ -165,13 +165,16 @@ def perm_shift_ref(A: torch.Tensor, shift: int) -> torch.Tensor:
     return torch.roll(perm, -(shift % A.shape[0]))
 
 
-def block_solve16_ref(A: torch.Tensor, shift: int, sweeps: int):
+SHIFT_BLOCKS = (16, 32)  # block sizes of the shifted layout (eigh_sbr16.hip templates)
+
+
+def block_solve16_ref(A: torch.Tensor, shift: int, sweeps: int, sb: int = SB):
     n = A.shape[0]
     perm = perm_shift_ref(A, shift)
-    nb = (n + SB - 1) // SB
-    S = torch.zeros(nb, SB, SB, dtype=A.dtype, device=A.device)
+    nb = (n + sb - 1) // sb
+    S = torch.zeros(nb, sb, sb, dtype=A.dtype, device=A.device)
     for k in range(nb):
-        idx = perm[k * SB : (k + 1) * SB].long()
+        idx = perm[k * sb : (k + 1) * sb].long()
         m = idx.numel()
         S[k, :m, :m] = A[idx][:, idx]
     S, Q = _block_jacobi_ref(S, sweeps)
@@ -189,14 +192,14 @@ def _blockdiag16(Q: torch.Tensor, n: int) -> torch.Tensor:
 LOCAL_THETA = 0.0
 
 
-def local_threshold(dq: torch.Tensor, theta: float = None) -> torch.Tensor:
+def local_threshold(dq: torch.Tensor, theta: float = None, sb: int = SB) -> torch.Tensor:
     """θ·min(|d[j+8] − d[j]|, |d[j] − d[j−8]|) at every position j of the order.  A pair whose
     gap is below both ends' local thresholds is less than half a block apart, so one of
     the two shifts puts it in a common block: every pair is either rotated by a block solve
     or by the far step, even inside clusters denser than the global threshold assumes."""
     theta = LOCAL_THETA if theta is None else theta
     n = dq.shape[0]
-    h = SB // 2
+    h = sb // 2
     inf = torch.full((h,), float("inf"), dtype=dq.dtype, device=dq.device)
     up = torch.cat([(dq[h:] - dq[:-h]).abs(), inf]) if n > h else torch.full_like(dq, float("inf"))
     dn = torch.cat([inf, (dq[h:] - dq[:-h]).abs()]) if n > h else torch.full_like(dq, float("inf"))
@@ -205,16 +208,17 @@ def local_threshold(dq: torch.Tensor, theta: float = None) -> torch.Tensor:
 
 def far16_ref(A, perm, Q, dq, stats, thr_fac, theta: float = None):
     theta = LOCAL_THETA if theta is None else theta
+    sb = Q.shape[1]
     n = A.shape[0]
     p = perm.long()
     Qf = _blockdiag16(Q, n)
     A1 = Qf.T @ A[p][:, p] @ Qf
-    blk = torch.arange(n, device=A.device) // SB
+    blk = torch.arange(n, device=A.device) // sb
     den = dq[None, :] - dq[:, None]
-    thr = thr_fac * (0.5 * SB) * float(stats[3] - stats[2]) / n
+    thr = thr_fac * (0.5 * sb) * float(stats[3] - stats[2]) / n
     thr = torch.full_like(dq, thr)
     if theta > 0:
-        thr = torch.minimum(thr, local_threshold(dq, theta))
+        thr = torch.minimum(thr, local_threshold(dq, theta, sb))
     mask = (blk[None, :] != blk[:, None]) & (den.abs() > torch.minimum(thr[:, None], thr[None, :]))
     return torch.where(mask, 0.5 * torch.atan(2 * A1 / torch.where(mask, den, torch.ones_like(den))), torch.zeros_like(A1))
 
@@ -237,10 +241,10 @@ def stats(A):
 
 
 def block_solve(A, off, sweeps, bk: int = BK):
-    if bk == SB:
+    if bk in SHIFT_BLOCKS:
         if _dev(A):
-            return tuple(_ext.ops().sbr16_block(_rowmajor(A), int(off) % A.shape[0], int(sweeps)))
-        return block_solve16_ref(A, off, sweeps)
+            return tuple(_ext.ops().sbr16_block(_rowmajor(A), int(off) % A.shape[0], int(sweeps), int(bk)))
+        return block_solve16_ref(A, off, sweeps, bk)
     if _dev(A):
         perm, Q, dq = _ext.ops().sbr_block(_rowmajor(A), int(off), int(sweeps))
         return perm, Q, dq
@@ -249,7 +253,7 @@ def block_solve(A, off, sweeps, bk: int = BK):
 
 def far(A, off, perm, Q, dq, st, thr_fac, bk: int = BK, theta: float = None):
     theta = LOCAL_THETA if theta is None else theta
-    if bk == SB:
+    if bk in SHIFT_BLOCKS:
         if _dev(A):
             return _ext.ops().sbr16_far(_rowmajor(A), perm, Q, dq, st, float(thr_fac), float(theta))
         return far16_ref(A, perm, Q, dq, st, thr_fac, theta)
@@ -259,7 +263,7 @@ def far(A, off, perm, Q, dq, st, thr_fac, bk: int = BK, theta: float = None):
 
 
 def bq(B, off, perm, Q, bk: int = BK):
-    if bk == SB:
+    if bk in SHIFT_BLOCKS:
         return _ext.ops().sbr16_bq(_rowmajor(B), perm, Q) if _dev(B) else bq16_ref(B, perm, Q)
     return _ext.ops().sbr_bq(_rowmajor(B), int(off), perm, Q) if _dev(B) else bq_ref(B, off, perm, Q)
 
@@ -382,8 +386,8 @@ class SBRConfig:
     def __post_init__(self):
         if self.thr_fac is None:
             self.thr_fac = 0.3
-        if self.block not in (SB, BK):
-            raise ValueError(f"SBR block size must be {SB} or {BK}, got {self.block}")
+        if self.block not in SHIFT_BLOCKS + (BK,):
+            raise ValueError(f"SBR block size must be one of {SHIFT_BLOCKS + (BK,)}, got {self.block}")
 
 
 def _read(st: torch.Tensor):
@@ -703,7 +707,7 @@ def eigh_warm(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None, plan
         # an undamped far iteration close to the tolerance that barely helps: pairs inside a
         # cluster denser than the global threshold assumes are neither far nor in a block —
         # the local threshold takes them into the far step for the rest of the solve
-        if far_on and alpha >= 1.0 and off_rel < 100 * cfg.tol and off_rel > 0.6 * prev and cfg.block == SB:
+        if far_on and alpha >= 1.0 and off_rel < 100 * cfg.tol and off_rel > 0.6 * prev and cfg.block in SHIFT_BLOCKS:
             theta = 1.0
         last_far = far_on
         prev = off_rel

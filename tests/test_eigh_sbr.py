@@ -174,20 +174,21 @@ def test_sbr_kernels_match_reference(n, off):
 
 
 @gpu
+@pytest.mark.parametrize("sb", [16, 32])
 @pytest.mark.parametrize("n,shift", [(1000, 0), (1000, 8), (200, 8), (37, 8), (17, 0)])
-def test_sbr16_kernels_match_reference(n, shift):
+def test_sbr16_kernels_match_reference(n, shift, sb):
     C, B = _cma_like(n, 8, seed=n)
     A = sbr.sym_product(C, B)
     st = sbr.stats_ref(A)
-    perm_r, Q_r, dq_r = sbr.block_solve16_ref(A, shift, 2)
+    perm_r, Q_r, dq_r = sbr.block_solve16_ref(A, shift, 2, sb)
     Ad = A.cuda()
-    perm, Q, dq = sbr.block_solve(Ad, shift, 2, bk=16)
+    perm, Q, dq = sbr.block_solve(Ad, shift, 2, bk=sb)
     assert torch.equal(perm.cpu(), perm_r)
     Q, dq = Q.cpu(), dq.cpu()
-    assert float((Q.transpose(1, 2) @ Q - torch.eye(16)).abs().max()) < 2e-6
+    assert float((Q.transpose(1, 2) @ Q - torch.eye(sb)).abs().max()) < 4e-6
     p = perm_r.long()
     for k in range(Q.shape[0]):
-        idx = p[16 * k : 16 * (k + 1)]
+        idx = p[sb * k : sb * (k + 1)]
         m = idx.numel()
         S = A[idx][:, idx]
         T = Q[k, :m, :m].T @ S @ Q[k, :m, :m]
@@ -195,12 +196,12 @@ def test_sbr16_kernels_match_reference(n, shift):
         off_k = torch.linalg.matrix_norm(T - torch.diag(torch.diagonal(T)))
         off_r = torch.linalg.matrix_norm(T_r - torch.diag(torch.diagonal(T_r)))
         assert off_k <= 1.5 * off_r + 1e-6 * torch.linalg.matrix_norm(S)
-        assert torch.allclose(torch.diagonal(T), dq[16 * k : 16 * k + m], atol=2e-5)
-    X = sbr.far(Ad, shift, perm_r.cuda(), Q_r.cuda(), dq_r.cuda(), st.cuda(), 0.5, bk=16).cpu()
+        assert torch.allclose(torch.diagonal(T), dq[sb * k : sb * k + m], atol=2e-5)
+    X = sbr.far(Ad, shift, perm_r.cuda(), Q_r.cuda(), dq_r.cuda(), st.cuda(), 0.5, bk=sb).cpu()
     X_r = sbr.far16_ref(A, perm_r, Q_r, dq_r, st, 0.5)
     assert (X.abs() > 0).sum() == (X_r.abs() > 0).sum()
     assert _rel(X, X_r) < 1e-4
-    Bq = sbr.bq(B.cuda(), shift, perm_r.cuda(), Q_r.cuda(), bk=16).cpu()
+    Bq = sbr.bq(B.cuda(), shift, perm_r.cuda(), Q_r.cuda(), bk=sb).cpu()
     assert _rel(Bq, sbr.bq16_ref(B, perm_r, Q_r)) < 1e-5
 
 
