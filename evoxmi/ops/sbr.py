@@ -374,8 +374,8 @@ class SBRConfig:
     near_only: float = 3.0     # near-only (no far step) iteration once off_rel ≤ near_only·tol
     max_jacobi: int = 16
     block_sweeps: int = 2
-    block: int = SB            # 16: one-wave blocks in a shifted sorted order (eigh_sbr16.hip);
-                               # 64: the 64-wide offset layout (eigh_sbr.hip)
+    block: int = 32            # 16 / 32: blocks in a shifted sorted order (eigh_sbr16.hip; 16 = one
+                               # wave per block, 32 = four); 64: the 64-wide offset layout (eigh_sbr.hip)
     thr_fac: float = None      # far-pair threshold factor (default 0.3)
     ns_iters: int = 2          # Newton–Schulz re-orthonormalisation in the first iterations and
                                # after every damped one (undamped later ones have ‖X‖₂ ≲ 0.5:

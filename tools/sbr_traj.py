@@ -28,7 +28,7 @@ rec = []
 orig = sbr.eigh_warm
 
 
-def hook(C, B_prev, cfg=None):
+def hook(C, B_prev, cfg=None, plans=None):
     rec.append((C.detach().clone(), B_prev.detach().clone()))
     return orig(C, B_prev, sbr.SBRConfig(tol=cfg.tol if cfg else 1e-5, block=64))
 
