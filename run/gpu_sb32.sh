@@ -4,7 +4,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out/sb32
 timeout -k 10 400 python -u -m pytest -q --timeout 200 --timeout-method thread tests/test_eigh_sbr.py -m gpu > gpurun_out/sb32/tests.log 2>&1
 rc=$?; tail -2 gpurun_out/sb32/tests.log; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 400 python -u tools/sbr_traj.py --gens 35 --variants 16:0.3:0:3,32:0.3:0:3,32:0.45:0:3,64:0.3:0:3 > gpurun_out/sb32/traj.log 2>&1 || exit $?
+timeout -k 10 400 python -u tools/sbr_traj.py --gens 35 --variants 16:0.3:0:3,32:0.3:0:3 > gpurun_out/sb32/traj.log 2>&1 || exit $?
 tail -1 gpurun_out/sb32/traj.log
 for i in 1 2; do
   for b in 16 32; do

@@ -55,7 +55,7 @@ def main():
     A = sbr.sym_product(C, B)
     st = sbr.stats(A)
     res = {"stats_us": timeit(lambda: sbr.stats(A))}
-    for bk in (16, 64):
+    for bk in (16, 32, 64):
         perm, Q, dq = sbr.block_solve(A, 0, 2, bk)
         X = sbr.far(A, 0, perm, Q, dq, st, 0.3, bk)
         res.update({
