@@ -40,18 +40,24 @@ __device__ __forceinline__ float sort_key(float v) { return isnan(v) ? INFINITY 
 // 64 indices per workgroup, the 4 waves each count over a quarter of the keys
 __global__ void __launch_bounds__(256) sbr16_rank_kernel(const float* __restrict__ A, int n, int64_t lda, int shift,
                                                          int* __restrict__ perm) {
-  __shared__ float key[kRankMax];
+  __shared__ __attribute__((aligned(16))) float key[kRankMax + 16];
   __shared__ int part[4][64];
-  for (int i = threadIdx.x; i < n; i += blockDim.x) key[i] = sort_key(A[(int64_t)i * lda + i]);
+  const int np = (n + 15) & ~15;  // padded with +inf: never below a real key (NaN keys are +inf too, ties by index)
+  for (int i = threadIdx.x; i < np; i += blockDim.x) key[i] = i < n ? sort_key(A[(int64_t)i * lda + i]) : INFINITY;
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int i = blockIdx.x * 64 + lane;
   const float ki = i < n ? key[i] : 0.f;
-  const int q = (n + 3) >> 2, j0 = w * q, j1 = min(n, j0 + q);
+  // each wave counts over a quarter of the keys, 4 keys per LDS broadcast read (ds_read_b128)
+  const int q = ((np >> 2) + 3) & ~3, j0 = min(np, w * q), j1 = min(np, j0 + q);
   int cnt = 0;
-  for (int j = j0; j < j1; ++j) {
-    const float kj = key[j];  // same address across the wave: LDS broadcast
-    cnt += (kj < ki) | ((kj == ki) & (j < i));
+#pragma unroll 4
+  for (int j = j0; j < j1; j += 4) {
+    const float4 k4 = *(const float4*)(key + j);  // same address across the wave: broadcast
+    cnt += (k4.x < ki) | ((k4.x == ki) & (j < i));
+    cnt += (k4.y < ki) | ((k4.y == ki) & (j + 1 < i));
+    cnt += (k4.z < ki) | ((k4.z == ki) & (j + 2 < i));
+    cnt += (k4.w < ki) | ((k4.w == ki) & (j + 3 < i));
   }
   part[w][lane] = cnt;
   __syncthreads();
