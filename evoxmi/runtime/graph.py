@@ -30,6 +30,21 @@ def capturing() -> bool:
     return _ACTIVE is not None and torch.cuda.is_current_stream_capturing()
 
 
+def copy_into(dst: Sequence[torch.Tensor], src: Sequence[torch.Tensor]):
+    """dst[i].copy_(src[i]) for all i as one multi-tensor launch when the tensors share a
+    dtype and device (``torch._foreach_copy_``), else tensor by tensor."""
+    dst, src = list(dst), list(src)
+    if not dst:
+        return
+    same = all(d.dtype == dst[0].dtype and d.device == dst[0].device and s.dtype == d.dtype and s.device == d.device
+               for d, s in zip(dst, src))
+    if same and len(dst) > 1 and hasattr(torch, "_foreach_copy_"):
+        torch._foreach_copy_(dst, src)
+    else:
+        for d, s in zip(dst, src):
+            d.copy_(s)
+
+
 def host_phase(fn: Callable, *args, out_like: Sequence[torch.Tensor]):
     """Run ``fn(*args)`` (returning tensors shaped like ``out_like``) as a host phase."""
     sess = _ACTIVE
@@ -99,5 +114,10 @@ class SegmentedGraph:
             else:
                 _, fn, args, outs = it
                 res = fn(*args)
+                groups = {}
                 for o, r in zip(outs, res):
-                    o.copy_(r)
+                    g = groups.setdefault((o.dtype, o.device), ([], []))
+                    g[0].append(o)
+                    g[1].append(r.to(o.device) if r.device != o.device else r)
+                for dst, src in groups.values():
+                    copy_into(dst, src)

@@ -48,7 +48,7 @@ from ..core.state import tree_flatten, tree_map
 from .. import config
 from ..utils.common import parse_opt_direction
 from ..utils.profiling import trace_range
-from ..runtime.graph import SegmentedGraph
+from ..runtime.graph import SegmentedGraph, copy_into
 
 HOOKS = ("pre_step", "pre_ask", "post_ask", "pre_eval", "post_eval", "pre_tell", "post_tell", "post_step")
 
@@ -256,12 +256,19 @@ class StdWorkflow(Workflow):
                 out_leaves, out_spec = tree_flatten(out)
                 if in_spec != out_spec:
                     raise RuntimeError("graph=True: the step changed the state structure; this algorithm is not graph-safe")
+                groups = {}
                 for a, b in zip(in_leaves, out_leaves):
                     if isinstance(a, torch.Tensor):
                         if a.shape != b.shape or a.dtype != b.dtype:
                             raise RuntimeError("graph=True: a state tensor changed shape/dtype across a step")
                         if a.data_ptr() != b.data_ptr():
-                            a.copy_(b)
+                            groups.setdefault((a.dtype, a.device), ([], []))
+                            groups[(a.dtype, a.device)][0].append(a)
+                            groups[(a.dtype, a.device)][1].append(b)
+                # write the new state into the static buffers with one multi-tensor copy per
+                # dtype (a dozen small leaves would otherwise be a dozen copy launches per replay)
+                for dst, src in groups.values():
+                    copy_into(dst, src)
                 return in_leaves, out_leaves
 
             in_leaves, out_leaves = g.capture(body, s)
