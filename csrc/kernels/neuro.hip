@@ -191,32 +191,39 @@ __device__ __forceinline__ void art_substep(AntBody& s, float& hq, float& aq, fl
     leg_momentum(tc[0], tc[1], tc[2], tc[3], hqd, aqd * sg, p1, L1m);
   }
   // per leg, torso frame: momentum change, first moment of the link masses
-  float X[15];
+  // this leg's wrench on the torso (world frame): contact forces / torques, minus the rate
+  // of the leg's relative momentum, plus the gravity torque of its links — rotated per lane
+  // so that only 6 values need the quad sum
+  float dpl[3], dLl[3], cgl[3];
+  {
+    float t0[3], t1[3];
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    X[k] = F[k];
-    X[3 + k] = T[k];
-    X[6 + k] = p1[k] - pm[k];
-    X[9 + k] = L1m[k] - Lm[k];
-    pm[k] = p1[k];
-    Lm[k] = L1m[k];
+    for (int k = 0; k < 3; ++k) {
+      t0[k] = p1[k] - pm[k];
+      t1[k] = L1m[k] - Lm[k];
+      pm[k] = p1[k];
+      Lm[k] = L1m[k];
+    }
+    const float cg[3] = {(M1 * R1 + M2 * r2) * cphi, (M1 * R1 + M2 * r2) * sphi, -M2 * 0.5f * L2 * sa};
+    mrot(R, t0, dpl);
+    mrot(R, t1, dLl);
+    mrot(R, cg, cgl);
   }
-  X[12] = (M1 * R1 + M2 * r2) * cphi;
-  X[13] = (M1 * R1 + M2 * r2) * sphi;
-  X[14] = -M2 * 0.5f * L2 * sa;
+  float X[6];
+  // cross(R·cg, (0, 0, −g)) = (−g·cg_y, g·cg_x, 0)
+  X[0] = F[0] - dpl[0] * (1.f / DT);
+  X[1] = F[1] - dpl[1] * (1.f / DT);
+  X[2] = F[2] - dpl[2] * (1.f / DT);
+  X[3] = T[0] - dLl[0] * (1.f / DT) - GRAV * cgl[1];
+  X[4] = T[1] - dLl[1] * (1.f / DT) + GRAV * cgl[0];
+  X[5] = T[2] - dLl[2] * (1.f / DT);
 #pragma unroll
-  for (int k = 0; k < 15; ++k) X[k] = quad_sum(X[k]);
-  float dp[3], dL[3], cg[3];
-  mrot(R, X + 6, dp);
-  mrot(R, X + 9, dL);
-  mrot(R, X + 12, cg);
+  for (int k = 0; k < 6; ++k) X[k] = quad_sum(X[k]);
   const float gw[3] = {0.f, 0.f, -GRAV};
-  float tg[3];
-  cross(cg, gw, tg);
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    const float force = X[k] + MTOT * gw[k] - dp[k] * (1.f / DT) - LDAMP * s.v[k];
-    const float torque = X[3 + k] + tg[k] - dL[k] * (1.f / DT) - ADAMP * s.w[k];
+    const float force = X[k] + MTOT * gw[k] - LDAMP * s.v[k];
+    const float torque = X[3 + k] - ADAMP * s.w[k];
     s.v[k] += DT * force * (1.f / MTOT);
     s.w[k] += DT * torque * (1.f / IC);
     s.p[k] += DT * s.v[k];
