@@ -502,7 +502,9 @@ at::Tensor weighted_rowsum(const at::Tensor& X, const c10::optional<at::Tensor>&
   auto part = at::empty({chunks, D}, X.options());
   evx_weighted_rowsum(X.data_ptr<float>(), X.stride(0), ip, w.data_ptr<float>(), optf(sub), (int)K, (int)D, part.data_ptr<float>(),
                       chunks, cur_stream());
-  return part.sum(0);
+  auto out = at::empty({D}, X.options());
+  evx_colsum(part.data_ptr<float>(), chunks, (int)D, out.data_ptr<float>(), cur_stream());
+  return out;
 }
 
 void gemm_set_config(int64_t cfg) { evx_gemm_set_config((int)cfg); }

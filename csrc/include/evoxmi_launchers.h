@@ -53,6 +53,7 @@ void evx_es_noise_grad(const int64_t* key, const float* w, int64_t rows, int64_t
                        hipStream_t s);
 void evx_philox_words(const int64_t* key, int64_t nblocks, uint32_t domain, int64_t offset, int64_t* out, hipStream_t s,
                       int batch = 1);
+void evx_colsum(const float* partial, int chunks, int D, float* out, hipStream_t s);
 void evx_weighted_rowsum(const float* X, int64_t ldx, const int32_t* idx, const float* w, const float* sub, int K, int D,
                          float* partial, int chunks, hipStream_t s);
 void evx_gemm_set_config(int cfg);

@@ -38,7 +38,25 @@ __global__ void __launch_bounds__(256) weighted_rowsum_kernel(const float* __res
   }
   partial[(int64_t)c * D + j] = (a0 + a1) + (a2 + a3);
 }
+// out[j] = Σ_c partial[c][j] in chunk order (deterministic); one thread per column,
+// consecutive threads read consecutive columns of each chunk row
+__global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ partial, int chunks, int D, float* __restrict__ out) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= D) return;
+  float a0 = 0.f, a1 = 0.f;
+  int c = 0;
+  for (; c + 1 < chunks; c += 2) {
+    a0 += partial[(int64_t)c * D + j];
+    a1 += partial[(int64_t)(c + 1) * D + j];
+  }
+  if (c < chunks) a0 += partial[(int64_t)c * D + j];
+  out[j] = a0 + a1;
+}
 }  // namespace
+
+void evx_colsum(const float* partial, int chunks, int D, float* out, hipStream_t s) {
+  colsum_kernel<<<(D + 255) / 256, 256, 0, s>>>(partial, chunks, D, out);
+}
 
 void evx_weighted_rowsum(const float* X, int64_t ldx, const int32_t* idx, const float* w, const float* sub, int K, int D,
                          float* partial, int chunks, hipStream_t s) {
