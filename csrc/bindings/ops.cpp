@@ -498,7 +498,7 @@ at::Tensor weighted_rowsum(const at::Tensor& X, const c10::optional<at::Tensor>&
   }
   const int64_t D = X.size(1);
   c10::DeviceGuard g(X.device());
-  const int chunks = (int)std::max<int64_t>(1, std::min<int64_t>(256, (K + 15) / 16));  // ≈1000 workgroups at K = 5000
+  const int chunks = (int)std::max<int64_t>(1, std::min<int64_t>(128, (K + 31) / 32));  // 512 workgroups at K = 5000, d = 1000
   auto part = at::empty({chunks, D}, X.options());
   evx_weighted_rowsum(X.data_ptr<float>(), X.stride(0), ip, w.data_ptr<float>(), optf(sub), (int)K, (int)D, part.data_ptr<float>(),
                       chunks, cur_stream());

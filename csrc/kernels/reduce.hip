@@ -38,24 +38,32 @@ __global__ void __launch_bounds__(256) weighted_rowsum_kernel(const float* __res
   }
   partial[(int64_t)c * D + j] = (a0 + a1) + (a2 + a3);
 }
-// out[j] = Σ_c partial[c][j] in chunk order (deterministic); one thread per column,
-// consecutive threads read consecutive columns of each chunk row
+// out[j] = Σ_c partial[c][j] in a fixed order (deterministic): 64 columns per workgroup, its
+// 4 waves sum the chunks c ≡ wave (mod 4) with 4 loads in flight, then wave 0 adds the 4
+// partials in wave order
 __global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ partial, int chunks, int D, float* __restrict__ out) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= D) return;
-  float a0 = 0.f, a1 = 0.f;
-  int c = 0;
-  for (; c + 1 < chunks; c += 2) {
-    a0 += partial[(int64_t)c * D + j];
-    a1 += partial[(int64_t)(c + 1) * D + j];
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + lane;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (j < D) {
+    int c = w;
+    for (; c + 12 < chunks; c += 16) {
+      a0 += partial[(int64_t)c * D + j];
+      a1 += partial[(int64_t)(c + 4) * D + j];
+      a2 += partial[(int64_t)(c + 8) * D + j];
+      a3 += partial[(int64_t)(c + 12) * D + j];
+    }
+    for (; c < chunks; c += 4) a0 += partial[(int64_t)c * D + j];
   }
-  if (c < chunks) a0 += partial[(int64_t)c * D + j];
-  out[j] = a0 + a1;
+  red[w][lane] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (w == 0 && j < D) out[j] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 }  // namespace
 
 void evx_colsum(const float* partial, int chunks, int D, float* out, hipStream_t s) {
-  colsum_kernel<<<(D + 255) / 256, 256, 0, s>>>(partial, chunks, D, out);
+  colsum_kernel<<<(D + 63) / 64, 256, 0, s>>>(partial, chunks, D, out);
 }
 
 void evx_weighted_rowsum(const float* X, int64_t ldx, const int32_t* idx, const float* w, const float* sub, int K, int D,
