@@ -50,8 +50,8 @@ __global__ void __launch_bounds__(kKnnThreads) knn_kernel(const float* __restric
   float bd[T];
   int bi[T];
 #pragma unroll
-  for (int t = 0; t < T; ++t) {
-    bd[t] = FLT_MAX;
+  for (int t = 0; t < T; ++t) {  // empty slots: (+inf, INT_MAX) — any candidate beats them
+    bd[t] = INFINITY;
     bi[t] = 0x7fffffff;
   }
   const int rows_per_tile = kKnnTile / m;
@@ -63,17 +63,21 @@ __global__ void __launch_bounds__(kKnnThreads) knn_kernel(const float* __restric
     if (!live) continue;
     for (int jj = 0; jj < nr; ++jj) {
       const float* y = ys + jj * m;  // same address in every lane: LDS broadcast
-      const float d2 = sqdist(x, y, m);
-      if (d2 < bd[T - 1]) {  // strict: an equal distance never displaces an earlier index
-        const int j = j0 + jj;
+      // a NaN distance ranks first (key −inf, reported as NaN: torch.cdist(..).min() and the
+      // reference propagate it); (key, index) order, so an inf distance still fills an
+      // empty slot and an equal key never displaces an earlier index
+      float d2 = sqdist(x, y, m);
+      d2 = (d2 != d2) ? -INFINITY : d2;
+      const int j = j0 + jj;
+      if (d2 < bd[T - 1] || (d2 == bd[T - 1] && j < bi[T - 1])) {
 #pragma unroll
         for (int t = T - 1; t > 0; --t) {
-          const bool shift = d2 < bd[t - 1];
-          const bool here = !shift && d2 < bd[t];
+          const bool shift = d2 < bd[t - 1] || (d2 == bd[t - 1] && j < bi[t - 1]);
+          const bool here = !shift && (d2 < bd[t] || (d2 == bd[t] && j < bi[t]));
           bd[t] = shift ? bd[t - 1] : (here ? d2 : bd[t]);
           bi[t] = shift ? bi[t - 1] : (here ? j : bi[t]);
         }
-        if (d2 < bd[0]) {
+        if (d2 < bd[0] || (d2 == bd[0] && j < bi[0])) {
           bd[0] = d2;
           bi[0] = j;
         }
@@ -84,7 +88,7 @@ __global__ void __launch_bounds__(kKnnThreads) knn_kernel(const float* __restric
 #pragma unroll
   for (int t = 0; t < T; ++t) {
     if (t < t_out) {
-      out_d[(int64_t)row * t_out + t] = sqrtf(bd[t]);
+      out_d[(int64_t)row * t_out + t] = bd[t] == -INFINITY ? NAN : sqrtf(bd[t]);
       out_i[(int64_t)row * t_out + t] = bi[t];
     }
   }

@@ -77,8 +77,10 @@ class EvalMonitor(Monitor):
         f_loc = fitness[start : start + size]
         i_loc = torch.argmin(f_loc)
         val, gidx = d.all_reduce_min_loc(f_loc[i_loc], i_loc + start)
-        mine = (gidx == i_loc + start).to(local_sol.dtype)
-        row = local_sol.index_select(0, i_loc.reshape(1)) * mine
+        mine = gidx == i_loc + start
+        row = local_sol.index_select(0, i_loc.reshape(1))
+        # select, not multiply: a non-owner's inf/NaN row times 0 would poison the sum
+        row = torch.where(mine, row, torch.zeros_like(row))
         d.all_reduce_(row)
         return val.reshape(1), row
 

@@ -24,7 +24,8 @@ def _sqdist_rows(X, Y, chunk=512):
 def knn(X: torch.Tensor, Y: torch.Tensor, T: int):
     """(distances (N, T), indices (N, T) int64) of the T nearest rows of ``Y`` for every
     row of ``X``, ascending by (squared euclidean distance, index) — a stable argsort of
-    the direct-form distance row, as the reference's ``argsort(pairwise_euclidean_dist)``."""
+    the direct-form distance row, as the reference's ``argsort(pairwise_euclidean_dist)``.
+    NaN distances rank first (reported as NaN); inf distances are ordinary candidates."""
     X = X.to(torch.float32).contiguous()
     Y = Y.to(torch.float32).contiguous()
     T = int(T)
@@ -34,7 +35,10 @@ def knn(X: torch.Tensor, Y: torch.Tensor, T: int):
     out_d, out_i = [], []
     for s in range(0, X.shape[0], 512):
         d2 = _sqdist_rows(X[s : s + 512], Y, 512)
-        i = torch.argsort(d2, dim=1, stable=True)[:, :T]
+        # a NaN distance ranks first so the nearest distance propagates it (as
+        # torch.cdist(..).min() and the reference's min do); the kernel uses the same order
+        key = torch.where(torch.isnan(d2), torch.full_like(d2, float("-inf")), d2)
+        i = torch.argsort(key, dim=1, stable=True)[:, :T]
         out_d.append(torch.sqrt(torch.gather(d2, 1, i)))
         out_i.append(i)
     return torch.cat(out_d), torch.cat(out_i)

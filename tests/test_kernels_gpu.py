@@ -777,6 +777,28 @@ def test_knn_kernel_ties_by_index():
 
 
 @pytest.mark.gpu
+def test_knn_kernel_nan_and_inf_rows():
+    from evoxmi.ops import geom
+
+    g = torch.Generator().manual_seed(5)
+    X, Y = torch.rand(300, 3, generator=g), torch.rand(40, 3, generator=g)
+    X[3, 1] = float("nan")       # every distance of row 3 is NaN
+    X[4, 0] = float("inf")       # every distance of row 4 is inf
+    Y[7, 2] = float("nan")       # candidate 7 is NaN for every row
+    for T in (1, 5):
+        d_ref, i_ref = geom.knn(X, Y, T)
+        d, i = geom.knn(X.cuda(), Y.cuda(), T)
+        assert torch.equal(i.cpu(), i_ref)
+        assert torch.allclose(d.cpu(), d_ref, equal_nan=True)
+    md = geom.min_dist(X.cuda(), Y.cuda()).cpu()
+    ref = torch.cdist(X.double(), Y.double()).min(1).values.float()
+    assert torch.isnan(md).all() and torch.isnan(ref).all()  # candidate 7 poisons every row
+    md = geom.min_dist(X[:, :2].cuda(), Y[:, :2].cuda()).cpu()
+    ref = torch.cdist(X[:, :2].double(), Y[:, :2].double()).min(1).values.float()
+    assert torch.isnan(md[3]) and torch.isinf(md[4]) and torch.allclose(md, ref, equal_nan=True, rtol=1e-5)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("strict", [True, False])
 def test_hv_count_kernel(strict):
     from evoxmi.ops import geom
@@ -868,6 +890,12 @@ def test_radix_argsort_matches_stable_torch_sort(n, descending):
     k[0, 3] = float("inf")
     k[0, 9] = float("nan")
     k[1, 5] = float("-inf")
+    # a NaN with the sign bit set (x86 0/0) must still sort as the largest value, and
+    # -0.0 ties with +0.0 (index order), as in torch.sort
+    k[0, 11] = torch.tensor([0xFFC00000], dtype=torch.int64).to(torch.int32).view(torch.float32)[0]
+    k[1, 6] = -0.0
+    k[1, 7] = 0.0
+    k[1, 8] = -0.0
     kd = k.cuda()
     ok, oi = _ext.ops().radix_argsort_f32(kd, descending)
     rv, ri = torch.sort(k, dim=1, descending=bool(descending), stable=True)
