@@ -142,6 +142,94 @@ at::Tensor gemm_f32(const at::Tensor& A, int64_t a_rc, const c10::optional<at::T
   return C;
 }
 
+// K-split register-direct f32 GEMM (gemm_ks.hip).  A: a_kc → (M, K) rows, else (K, M);
+// B: b_kc → (N, K) rows (C = A·Bᵀ), else (K, N) (C = A·B).  Inner strides must be 1.
+at::Tensor gemm_ks(const at::Tensor& A, int64_t a_kc, const at::Tensor& B, int64_t b_kc, int64_t M, int64_t N, int64_t K,
+                   int64_t mode, double alpha, const c10::optional<at::Tensor>& alpha_ptr,
+                   const c10::optional<at::Tensor>& bias_n, double beta, const c10::optional<at::Tensor>& Cin,
+                   const c10::optional<at::Tensor>& out, const c10::optional<at::Tensor>& skip,
+                   const c10::optional<at::Tensor>& a_sub_k) {
+  CHECK_DEV(A); CHECK_F32(A); CHECK_DEV(B); CHECK_F32(B);
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.stride(1) == 1 && B.stride(1) == 1, "gemm_ks: 2-D operands with unit inner stride");
+  TORCH_CHECK(M > 0 && N > 0 && K > 0, "gemm_ks: empty shape");
+  TORCH_CHECK(mode >= 0 && mode <= 2, "gemm_ks: mode");
+  if (a_kc) { TORCH_CHECK(A.size(0) >= M && A.size(1) >= K, "gemm_ks: A shape"); } else { TORCH_CHECK(A.size(0) >= K && A.size(1) >= M, "gemm_ks: A shape"); }
+  if (b_kc) { TORCH_CHECK(B.size(0) >= N && B.size(1) >= K, "gemm_ks: B shape"); } else { TORCH_CHECK(B.size(0) >= K && B.size(1) >= N, "gemm_ks: B shape"); }
+  auto vec4_ok = [](const at::Tensor& t) {
+    return (reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0) && (t.stride(0) % 4 == 0);
+  };
+  if (a_kc || b_kc) { TORCH_CHECK(K % 4 == 0, "gemm_ks: K-contiguous operands need K % 4 == 0"); }
+  if (a_kc) { TORCH_CHECK(vec4_ok(A), "gemm_ks: A must be 16-byte aligned with a row stride divisible by 4"); }
+  if (b_kc) { TORCH_CHECK(vec4_ok(B), "gemm_ks: B must be 16-byte aligned with a row stride divisible by 4"); }
+  if (mode != 0) {
+    TORCH_CHECK(M == N, "gemm_ks: symmetric / skew outputs need M == N");
+    TORCH_CHECK(!(bias_n.has_value() && bias_n->defined()) && !(Cin.has_value() && Cin->defined()),
+                "gemm_ks: symmetric / skew outputs take no bias / Cin");
+  }
+  c10::DeviceGuard g(A.device());
+  at::Tensor C;
+  if (out.has_value() && out->defined()) {
+    C = *out;
+    CHECK_DEV(C); CHECK_F32(C);
+    TORCH_CHECK(C.dim() == 2 && C.stride(1) == 1 && C.size(0) >= M && C.size(1) >= N, "gemm_ks: out shape");
+  } else {
+    C = at::empty({M, N}, A.options());
+  }
+  EvxGemmKs a{};
+  a.A = A.data_ptr<float>();
+  a.lda = A.stride(0);
+  a.B = B.data_ptr<float>();
+  a.ldb = B.stride(0);
+  a.C = C.data_ptr<float>();
+  a.ldc = C.stride(0);
+  a.M = (int)M; a.N = (int)N; a.K = (int)K;
+  a.a_kc = (int)a_kc; a.b_kc = (int)b_kc; a.mode = (int)mode;
+  a.alpha = (float)alpha;
+  a.alpha_ptr = optf(alpha_ptr);
+  if (bias_n.has_value() && bias_n->defined()) {
+    CHECK_DEV(*bias_n); CHECK_F32(*bias_n); CHECK_CONTIG(*bias_n);
+    TORCH_CHECK(bias_n->numel() >= N, "gemm_ks: bias length");
+    a.bias_n = bias_n->data_ptr<float>();
+  }
+  a.beta = (float)beta;
+  if (Cin.has_value() && Cin->defined()) {
+    CHECK_DEV(*Cin); CHECK_F32(*Cin);
+    TORCH_CHECK(Cin->dim() == 2 && Cin->stride(1) == 1 && Cin->size(0) >= M && Cin->size(1) >= N, "gemm_ks: Cin shape");
+    a.Cin = Cin->data_ptr<float>();
+    a.ldcin = Cin->stride(0);
+  }
+  if (skip.has_value() && skip->defined()) {
+    CHECK_DEV(*skip);
+    TORCH_CHECK(skip->scalar_type() == at::kInt && skip->numel() >= 1, "gemm_ks: skip must be int32");
+    a.skip = skip->data_ptr<int32_t>();
+  }
+  if (a_sub_k.has_value() && a_sub_k->defined()) {
+    CHECK_DEV(*a_sub_k); CHECK_F32(*a_sub_k); CHECK_CONTIG(*a_sub_k);
+    TORCH_CHECK(a_kc && a_sub_k->numel() >= K && reinterpret_cast<uintptr_t>(a_sub_k->data_ptr()) % 16 == 0,
+                "gemm_ks: a_sub_k needs a K-contiguous A and a 16-byte aligned vector of length ≥ K");
+    a.a_sub_k = a_sub_k->data_ptr<float>();
+  }
+  a.c_vec4 = vec4_ok(C) ? 1 : 0;
+  evx_gemm_ks(a, cur_stream());
+  return C;
+}
+
+void gemm_ks_set_tile(int64_t t) { evx_gemm_ks_set_tile((int)t); }
+
+at::Tensor gemm_ks_new(const at::Tensor& A, int64_t a_kc, const at::Tensor& B, int64_t b_kc, int64_t M, int64_t N, int64_t K,
+                       int64_t mode, double alpha, const c10::optional<at::Tensor>& alpha_ptr,
+                       const c10::optional<at::Tensor>& bias_n, double beta, const c10::optional<at::Tensor>& Cin,
+                       const c10::optional<at::Tensor>& skip, const c10::optional<at::Tensor>& a_sub_k) {
+  return gemm_ks(A, a_kc, B, b_kc, M, N, K, mode, alpha, alpha_ptr, bias_n, beta, Cin, c10::nullopt, skip, a_sub_k);
+}
+
+void gemm_ks_out(const at::Tensor& A, int64_t a_kc, const at::Tensor& B, int64_t b_kc, int64_t M, int64_t N, int64_t K,
+                 int64_t mode, double alpha, const c10::optional<at::Tensor>& alpha_ptr, const c10::optional<at::Tensor>& bias_n,
+                 double beta, const c10::optional<at::Tensor>& Cin, const at::Tensor& out, const c10::optional<at::Tensor>& skip,
+                 const c10::optional<at::Tensor>& a_sub_k) {
+  gemm_ks(A, a_kc, B, b_kc, M, N, K, mode, alpha, alpha_ptr, bias_n, beta, Cin, out, skip, a_sub_k);
+}
+
 std::vector<at::Tensor> argsort_f32(const at::Tensor& keys, int64_t descending) {
   // 1-D keys, or (B, n): B independent rows sorted by B workgroups of one launch
   CHECK_DEV(keys); CHECK_F32(keys); CHECK_CONTIG(keys);
@@ -364,7 +452,7 @@ at::Tensor sbr_damping(const at::Tensor& X2, const at::Tensor& V, double tau, co
   return alpha;
 }
 
-std::vector<at::Tensor> sbr_taylor4_prep(const at::Tensor& X, const at::Tensor& X2, const c10::optional<at::Tensor>& alpha) {
+std::vector<at::Tensor> sbr_taylor4_prep(const at::Tensor& X, const at::Tensor& X2, const c10::optional<at::Tensor>& alpha, int64_t mt) {
   CHECK_DEV(X); CHECK_F32(X); CHECK_CONTIG(X); CHECK_CONTIG(X2);
   const int64_t n = X.size(0);
   TORCH_CHECK(X.dim() == 2 && X.size(1) == n && X2.sizes() == X.sizes(), "sbr_taylor4_prep: n×n");
@@ -375,7 +463,8 @@ std::vector<at::Tensor> sbr_taylor4_prep(const at::Tensor& X, const at::Tensor& 
   }
   c10::DeviceGuard g(X.device());
   auto P = at::empty_like(X), M = at::empty_like(X);
-  evx_sbr_taylor4_prep(X.data_ptr<float>(), X2.data_ptr<float>(), (int)n, ap, P.data_ptr<float>(), M.data_ptr<float>(), cur_stream());
+  evx_sbr_taylor4_prep(X.data_ptr<float>(), X2.data_ptr<float>(), (int)n, ap, P.data_ptr<float>(), M.data_ptr<float>(), cur_stream(),
+                       (int)mt);
   return {P, M};
 }
 
@@ -457,7 +546,7 @@ void sbr_symstats_out(const at::Tensor& T, at::Tensor& A, at::Tensor& st) {
 }
 
 std::vector<at::Tensor> sbr_taylor_prep(const at::Tensor& X, const at::Tensor& X2, const at::Tensor& X3,
-                                        const c10::optional<at::Tensor>& alpha) {
+                                        const c10::optional<at::Tensor>& alpha, int64_t mt) {
   for (auto* t : {&X, &X2, &X3}) { CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t); }
   const int64_t n = X.size(0);
   TORCH_CHECK(X.dim() == 2 && X.size(1) == n && X2.sizes() == X.sizes() && X3.sizes() == X.sizes(), "sbr_taylor_prep: n×n");
@@ -470,7 +559,7 @@ std::vector<at::Tensor> sbr_taylor_prep(const at::Tensor& X, const at::Tensor& X
   c10::DeviceGuard g(X.device());
   auto P = at::empty_like(X), M = at::empty_like(X);
   evx_sbr_taylor_prep(X.data_ptr<float>(), X2.data_ptr<float>(), X3.data_ptr<float>(), (int)n, ap, P.data_ptr<float>(), M.data_ptr<float>(),
-                      cur_stream());
+                      cur_stream(), (int)mt);
   return {P, M};
 }
 
@@ -896,6 +985,9 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("dtlz(Tensor X, int m, int variant) -> Tensor");
   m.def("classic_eval(Tensor X, int func, float a, float b, float c) -> Tensor");
   m.def("gemm_f32(Tensor A, int a_rc, Tensor? a_gather, Tensor? a_sub, int a_sub_on_k, Tensor? a_kscale, Tensor? a_kw, Tensor? a_sscale, int a_sscale_inv, Tensor B, int b_rc, Tensor? b_gather, Tensor? b_sub, int b_sub_on_k, Tensor? b_kscale, Tensor? b_kw, Tensor? b_sscale, int b_sscale_inv, Tensor? alpha_ptr, Tensor? bias_n, float beta, Tensor? Cin, int M, int N, int K, int splits, float alpha) -> Tensor");
+  m.def("gemm_ks(Tensor A, int a_kc, Tensor B, int b_kc, int M, int N, int K, int mode, float alpha, Tensor? alpha_ptr, Tensor? bias_n, float beta, Tensor? Cin, Tensor? skip, Tensor? a_sub_k=None) -> Tensor");
+  m.def("gemm_ks_out(Tensor A, int a_kc, Tensor B, int b_kc, int M, int N, int K, int mode, float alpha, Tensor? alpha_ptr, Tensor? bias_n, float beta, Tensor? Cin, Tensor(a!) out, Tensor? skip, Tensor? a_sub_k=None) -> ()");
+  m.def("gemm_ks_set_tile(int t) -> ()");
   m.def("lsmop_g(Tensor X, int[] start, int[] sublen, int[] func, int nk, int cosine) -> Tensor");
   m.def("cma_delta_gemv(Tensor M, Tensor mean, Tensor dm, float cm) -> Tensor[]");
   m.def("cma_center_rows(Tensor pop, Tensor? rows, Tensor mean, Tensor sigma, Tensor w) -> Tensor");
@@ -915,17 +1007,18 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("sbr16_block(Tensor A, int shift, int sweeps, int sb=16) -> Tensor[]");
   m.def("sbr16_far(Tensor A, Tensor perm, Tensor Q, Tensor dq, Tensor stats, float thr_fac, float theta) -> Tensor");
   m.def("sbr16_bq(Tensor B, Tensor perm, Tensor Q) -> Tensor");
-  m.def("sbr_taylor4_prep(Tensor X, Tensor X2, Tensor? alpha=None) -> Tensor[]");
+  m.def("sbr_taylor4_prep(Tensor X, Tensor X2, Tensor? alpha=None, int mt=0) -> Tensor[]");
   m.def("linear_gp_fit(Tensor a, Tensor b, Tensor c, Tensor n, int steps, float lr) -> Tensor[]");
   m.def("sbr_damping(Tensor X2, Tensor V, float tau, Tensor(a!)? out=None) -> Tensor");
   m.def("sbr_symstats_out(Tensor T, Tensor(a!) A, Tensor(b!) st) -> ()");
-  m.def("sbr_taylor_prep(Tensor X, Tensor X2, Tensor X3, Tensor? alpha=None) -> Tensor[]");
+  m.def("sbr_taylor_prep(Tensor X, Tensor X2, Tensor X3, Tensor? alpha=None, int mt=0) -> Tensor[]");
   m.def("pso_update(Tensor pop, Tensor vel, Tensor lbl, Tensor lbf, Tensor fit, Tensor gbl, Tensor kp, Tensor kg, float w, float phip, float phig, Tensor lb, Tensor ub) -> Tensor[]");
 }
 
 TORCH_LIBRARY_IMPL(evoxmi, CompositeExplicitAutograd, m) {
   m.impl("stochastic_ranking", &stochastic_ranking);
   m.impl("gemm_set_config", &gemm_set_config);
+  m.impl("gemm_ks_set_tile", &gemm_ks_set_tile);
 }
 
 TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
@@ -945,6 +1038,8 @@ TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
   m.impl("argsort_f32", &argsort_f32);
   m.impl("radix_argsort_f32", &radix_argsort_f32);
   m.impl("gemm_f32", &gemm_f32);
+  m.impl("gemm_ks", &gemm_ks_new);
+  m.impl("gemm_ks_out", &gemm_ks_out);
   m.impl("pso_update", &pso_update);
   m.impl("lsmop_g", &lsmop_g);
   m.impl("cma_delta_gemv", &cma_delta_gemv);

@@ -25,6 +25,32 @@ struct EvxOperand {
 void evx_gemm_f32(EvxOperand a, EvxOperand b, float* C, int64_t ldc, int M, int N, int K, int splits, float alpha,
                   const float* alpha_ptr, const float* bias_n, float beta, const float* Cin, int64_t ldcin, hipStream_t s);
 int evx_gemm_splits_used(int K, int splits);
+// K-split register-direct f32 GEMM (gemm_ks.hip): C = s·A·B (+ bias_n) (+ beta·Cin), s = alpha·(*alpha_ptr)
+// a_kc: A(m, k) at A[m·lda + k] (else A[k·lda + m]);  b_kc: B(k, n) at B[n·ldb + k] (else B[k·ldb + n])
+// mode 0: full; 1: symmetric output (tiles tm ≤ tn computed, mirrored); 2: skew-symmetric output
+struct EvxGemmKs {
+  const float* A;
+  int64_t lda;
+  const float* B;
+  int64_t ldb;
+  float* C;
+  int64_t ldc;
+  int M, N, K;
+  int a_kc, b_kc, mode;
+  float alpha;
+  const float* alpha_ptr;
+  const float* bias_n;
+  float beta;
+  const float* Cin;
+  int64_t ldcin;
+  const int32_t* skip;
+  const float* a_sub_k;  // A(m, k) − a_sub_k[k] before the product (K-contiguous A only), may be null
+  int c_vec4;
+  int tiles_m, tiles_n;  // set by the launcher
+};
+void evx_gemm_ks(const EvxGemmKs& a, hipStream_t s);
+int evx_gemm_ks_tile(int M, int N, int mode);
+void evx_gemm_ks_set_tile(int t);
 void evx_cma_center_rows(const float* pop, int64_t ldp, const int32_t* rows, const float* mean, const float* sigma, const float* w, int K,
                          int d, float* Y, hipStream_t s);
 void evx_radix_argsort(const float* keys, int n, int descending, float* out_keys, int32_t* out_idx, hipStream_t s, int batch);
@@ -110,7 +136,7 @@ int evx_sbr_symstats_parts(int n);
 // 16-wide blocks in a shifted sorted order (eigh_sbr16.hip)
 int evx_sbr16_nblocks(int n, int sb);
 int evx_sbr16_max_n();
-void evx_sbr_taylor4_prep(const float* X, const float* X2, int n, const float* alpha, float* P, float* M, hipStream_t s);
+void evx_sbr_taylor4_prep(const float* X, const float* X2, int n, const float* alpha, float* P, float* M, hipStream_t s, int mt = 0);
 void evx_sbr_damping(const float* X2, int n, int64_t ldx, const float* V, float* work, float tau, float* alpha, hipStream_t s);
 void evx_sbr16_block(const float* A, int n, int64_t lda, int shift, int sweeps, int* perm, float* Q, float* dq, int sb, hipStream_t s);
 void evx_sbr16_far(const float* A, int n, int64_t lda, const int* perm, const float* Q, const float* dq, const double* stats,
@@ -119,7 +145,7 @@ void evx_sbr16_bq(const float* B, int rows, int n, int64_t ldb, const int* perm,
                   hipStream_t s);
 void evx_sbr_symstats(const float* T, int n, int64_t ldt, float* A, int64_t lda, double* part, double* out, hipStream_t s);
 void evx_sbr_taylor_prep(const float* X, const float* X2, const float* X3, int n, const float* alpha, float* P, float* M,
-                         hipStream_t s);
+                         hipStream_t s, int mt = 0);
 
 // mo_geom.hip (K17 k-nearest rows, K18 Monte-Carlo hypervolume)
 int evx_knn_max_t();

@@ -161,16 +161,19 @@ __global__ void __launch_bounds__(256) sbr_symstats_kernel(const float* __restri
 // Taylor terms of exp(αX) (α: damping factor on the device, 1 if null):
 // P = α³(Y/24 + Y²/120 + Y³/720), M = I + Y + Y²/2 + Y³/6 with Y = αX, so that
 // exp(αX) ≈ M + X³·P (one pass; X³·P carries the α³ of Y³)
+// mt = 1: M of exp(−αX) = exp(αX)ᵀ (odd terms negated) — with P unchanged the transposed
+// product Vᵀ = M(−α) − X³·Pᵀ is an A·Bᵀ GEMM on P's rows (ops/sbr.py)
 __global__ void __launch_bounds__(256) sbr_taylor_prep_kernel(const float* __restrict__ X, const float* __restrict__ X2,
                                                               const float* __restrict__ X3, int n, const float* __restrict__ alpha,
-                                                              float* __restrict__ P, float* __restrict__ M) {
+                                                              float* __restrict__ P, float* __restrict__ M, int mt) {
   const float a = alpha ? alpha[0] : 1.f, a2 = a * a, a3 = a2 * a;
+  const float so = mt ? -1.f : 1.f;
   const int64_t total = (int64_t)n * n;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
     const float x = a * X[e], x2 = a2 * X2[e], x3 = a3 * X3[e];
     P[e] = a3 * (x * (1.f / 24.f) + x2 * (1.f / 120.f) + x3 * (1.f / 720.f));
     const int64_t i = e / n, j = e - i * n;
-    M[e] = (i == j ? 1.f : 0.f) + x + 0.5f * x2 + x3 * (1.f / 6.f);
+    M[e] = (i == j ? 1.f : 0.f) + so * x + 0.5f * x2 + so * x3 * (1.f / 6.f);
   }
 }
 
@@ -703,11 +706,11 @@ void evx_sbr_symstats(const float* T, int n, int64_t ldt, float* A, int64_t lda,
 }
 
 void evx_sbr_taylor_prep(const float* X, const float* X2, const float* X3, int n, const float* alpha, float* P, float* M,
-                         hipStream_t s) {
+                         hipStream_t s, int mt) {
   const int64_t total = (int64_t)n * n;
   int g = (int)((total + 255) / 256);
   if (g > 2048) g = 2048;
-  sbr_taylor_prep_kernel<<<g, 256, 0, s>>>(X, X2, X3, n, alpha, P, M);
+  sbr_taylor_prep_kernel<<<g, 256, 0, s>>>(X, X2, X3, n, alpha, P, M, mt);
 }
 
 void evx_sbr_block(const float* A, int n, int64_t lda, int off, int sweeps, int* perm, float* Q, float* dq, hipStream_t s,

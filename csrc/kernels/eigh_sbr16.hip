@@ -414,14 +414,16 @@ __global__ void __launch_bounds__(256) sbr_damping_final_kernel(const float* __r
 // Taylor-4 operands: exp(αX) ≈ M + X²·P with M = I + αX + α²X²/2, P = α²(αX/6 + α²X²/24)
 __global__ void __launch_bounds__(256) sbr_taylor4_prep_kernel(const float* __restrict__ X, const float* __restrict__ X2, int n,
                                                                const float* __restrict__ alpha, float* __restrict__ P,
-                                                               float* __restrict__ M) {
+                                                               float* __restrict__ M, int mt) {
+  // mt = 1: M of exp(−αX) (odd term negated): Vᵀ = M(−α) + X²·Pᵀ (ops/sbr.py)
   const float a = alpha ? alpha[0] : 1.f, a2 = a * a;
+  const float so = mt ? -1.f : 1.f;
   const int64_t total = (int64_t)n * n;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
     const float x = a * X[e], x2 = a2 * X2[e];
     P[e] = a2 * (x * (1.f / 6.f) + x2 * (1.f / 24.f));
     const int64_t i = e / n, j = e - i * n;
-    M[e] = (i == j ? 1.f : 0.f) + x + 0.5f * x2;
+    M[e] = (i == j ? 1.f : 0.f) + so * x + 0.5f * x2;
   }
 }
 
@@ -467,9 +469,9 @@ void evx_sbr_damping(const float* X2, int n, int64_t ldx, const float* V, float*
   sbr_damping_final_kernel<<<1, 256, 0, s>>>(V2, V3, n, tau, alpha);
 }
 
-void evx_sbr_taylor4_prep(const float* X, const float* X2, int n, const float* alpha, float* P, float* M, hipStream_t s) {
+void evx_sbr_taylor4_prep(const float* X, const float* X2, int n, const float* alpha, float* P, float* M, hipStream_t s, int mt) {
   const int64_t total = (int64_t)n * n;
   int g = (int)((total + 255) / 256);
   if (g > 2048) g = 2048;
-  sbr_taylor4_prep_kernel<<<g, 256, 0, s>>>(X, X2, n, alpha, P, M);
+  sbr_taylor4_prep_kernel<<<g, 256, 0, s>>>(X, X2, n, alpha, P, M, mt);
 }

@@ -1,0 +1,415 @@
+// f32 GEMM family for the CMA-ES / SBR hot path on CDNA4 matrix cores
+// (v_mfma_f32_16x16x4_f32: exact f32 fmaf chains, 32-cycle issue, 40-cycle latency).
+//
+//   C[m, n] = s · Σ_k A[m, k] · B[k, n]  (+ bias_n[n])  (+ beta · Cin[m, n]),  s = alpha · (*alpha_ptr)
+//
+// Why a second GEMM next to gemm_f32.hip.  The flagship's products are 1000 × 1000 × 1000
+// (eigensolver, invsqrtC), 1000 × 1000 × 5000 (rank-μ) and 10 000 × 1000 × 1000 (sampling,
+// CEC rotation), all f32.  At 1000² a chip of 256 CUs holds exactly one 64 × 64 output tile
+// per CU, so the classic LDS-shared 2 × 2-wave tile spends its time in per-K-tile barriers
+// and pipeline refills instead of MFMAs (hipBLASLt: 22–23 µs per 1000³ product = 56 % of
+// the f32 matrix peak).  Here the four waves of a workgroup split K instead of the tile:
+//
+//   * every wave accumulates the WHOLE BM × BN tile (TM × TN 16 × 16 accumulators) over a
+//     quarter of K, loading its operand fragments straight from global memory into
+//     registers (float4 along k for K-contiguous operands) three 16-k groups ahead — no LDS
+//     and no barrier in the main loop, so each SIMD's matrix pipe sees back-to-back MFMAs;
+//   * the four partial tiles are summed once through LDS in the epilogue;
+//   * operand bytes per CU are the same as with a shared tile (each wave reads a disjoint
+//     K range of the same row panels), and an XCD-aware grouped tile order keeps the row
+//     panels a group of workgroups shares inside that XCD's 4 MB L2.
+//
+// Symmetric / skew-symmetric outputs (MODE 1 / 2: Bᵀ C B, X², BᵀB, the rank-μ product,
+// (B/D)Bᵀ / X²·X) compute only the tiles with tm ≤ tn and write the mirrored tile
+// transposed (negated for skew): 231 instead of 441 48 × 48 tiles at n = 1000, i.e. one
+// tile per CU, ≈0.56× the time of the full product.
+//
+// Operand layouts (template): KC = element (row, k) at p[row·ld + k] (k contiguous),
+// RC = element (row, k) at p[k·ld + row] (rows contiguous: four dword loads per group).
+// A skew-symmetric or symmetric operand can always be read KC (Xᵀ = −X, Cᵀ = C).
+//
+// ``skip``: a device word; when non-null and non-zero every workgroup returns at once
+// (device-side control of the eigensolver's fixed iteration schedule, ops/sbr_device.py).
+#include "evoxmi_common.h"
+#include "evoxmi_launchers.h"
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+namespace {
+
+
+// One lane's four k values k .. k + 3 of one operand row.  Full 16-k groups load without
+// masks; only the tail group (K % 16 != 0, handled once after the main loop) masks, with
+// a clamped (valid) address and a select (KC operands need K % 4 == 0: a float4 is either
+// wholly inside K or wholly outside; the launcher checks).
+template <bool KC>
+__device__ __forceinline__ float4 load_full(const float* __restrict__ p, int64_t ld, int k) {
+  if (KC) return *reinterpret_cast<const float4*>(p + k);
+  const float* q = p + (int64_t)k * ld;
+  return make_float4(q[0], q[ld], q[2 * ld], q[3 * ld]);
+}
+
+template <bool KC>
+__device__ __forceinline__ float4 load_tail(const float* __restrict__ p, int64_t ld, int k, int K) {
+  if (KC) {
+    const bool in = k < K;
+    const float4 t = *reinterpret_cast<const float4*>(p + (in ? k : 0));
+    return in ? t : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  float v[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const bool in = k + c < K;
+    const float t = p[(int64_t)(in ? k + c : 0) * ld];
+    v[c] = in ? t : 0.f;
+  }
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+
+// (tm, tn) of workgroup `bid` (already XCD-remapped: consecutive ids share an XCD).
+// Full grid: groups of 4 tile rows, column-major inside a group.  Triangle (tm ≤ tn):
+// 4 × 4 super-tiles enumerated row-major over the upper triangle, tiles row-major inside.
+template <int MODE>
+__device__ __forceinline__ void decode_tile(int bid, int tiles_m, int tiles_n, int& tm, int& tn) {
+  if (MODE == 0) {
+    constexpr int GM = 4;
+    const int width = GM * tiles_n;
+    const int grp = bid / width, fm = grp * GM;
+    const int gm = min(GM, tiles_m - fm), rem = bid - grp * width;
+    tm = fm + rem % gm;
+    tn = rem / gm;
+    return;
+  }
+  constexpr int G = 4;
+  const int T = tiles_m;
+  const int S = (T + G - 1) / G;
+  int acc = 0;
+  for (int I = 0; I < S; ++I) {
+    const int rI = min(G, T - I * G);
+    for (int J = I; J < S; ++J) {
+      const int cJ = min(G, T - J * G);
+      const int cnt = (I == J) ? rI * (rI + 1) / 2 : rI * cJ;
+      if (bid < acc + cnt) {
+        int t = bid - acc;
+        if (I < J) {
+          tm = I * G + t / cJ;
+          tn = J * G + t % cJ;
+        } else {
+          int row = 0;
+          while (t >= rI - row) {
+            t -= rI - row;
+            ++row;
+          }
+          tm = I * G + row;
+          tn = I * G + row + t;
+        }
+        return;
+      }
+      acc += cnt;
+    }
+  }
+  tm = tn = 0;
+}
+
+template <int TM, int TN, int KH, bool AKC, bool BKC, int MODE>
+__global__ void __launch_bounds__(256) gemm_ks_kernel(EvxGemmKs p) {
+  if (p.skip && *p.skip) return;
+  constexpr int BM = 16 * TM, BN = 16 * TN;
+  constexpr int KG = 16 * KH;  // k per group: KH float4 per lane and 16-row block
+  // LDS row pitch ≡ 16 (mod 32) floats: the partial-tile writes (16 columns × 4 rows per
+  // wave instruction) hit 32 distinct banks per half-wave
+  constexpr int P = (BN % 32 == 16) ? BN : BN + 16;
+  // two partial-tile buffers (the four K-partials are summed pairwise): 40 KB for a 64 × 64
+  // tile, so LDS never limits residency below what the registers allow
+  __shared__ __attribute__((aligned(16))) float red[2 * BM * P];
+
+  int tm, tn;
+  decode_tile<MODE>(evx::xcd_remap(blockIdx.x, gridDim.x), p.tiles_m, p.tiles_n, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int lane = threadIdx.x & 63;
+  // wave index as a scalar: the K range, loop bounds and slot branches below are then
+  // wave-uniform (scalar branches, and the waitcnt pass can count loads across them)
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 15, q = lane >> 4;
+
+  // this wave's K range in full KG-groups (wave 0 has the fewest and also takes the tail)
+  const int K = p.K;
+  const int ngf = K / KG;
+  const int g0 = (w * ngf) >> 2, g1 = ((w + 1) * ngf) >> 2;
+
+  const float* ap[TM];
+  const float* bp[TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int row = min(m0 + 16 * i + r, p.M - 1);
+    ap[i] = AKC ? p.A + (int64_t)row * p.lda : p.A + row;
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = min(n0 + 16 * j + r, p.N - 1);
+    bp[j] = BKC ? p.B + (int64_t)col * p.ldb : p.B + col;
+  }
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // loads per slot: one float4 (KC) or four dwords (RC) per 16-row block and 16 k; at most
+  // 63 vector loads can be counted in flight (vmcnt)
+  constexpr int LPS = KH * (TM * (AKC ? 1 : 4) + TN * (BKC ? 1 : 4));
+#ifdef EVX_KS_DEPTH  // tools/gemm_ks_probe.cpp experiments
+  constexpr int D = EVX_KS_DEPTH;
+#else
+  constexpr int D = (3 * LPS <= 63) ? 3 : 2;
+#endif
+  float4 fa[D][KH][TM], fb[D][KH][TN];
+  const int64_t lda = p.lda, ldb = p.ldb;
+  // lane (r, q), float4 h, component c ↔ k = KG·group + 16h + 4q + c (same map for A and B)
+  // fused A prologue A(m, k) − sub[k] (the CEC shift x − o): the shift float4 of a lane's k
+  // values rides along with the operand loads, the subtraction runs just before the MFMAs
+  const float* __restrict__ asub = p.a_sub_k;
+  float4 fs[D][KH];
+  auto load_slot = [&](float4 (&xa)[KH][TM], float4 (&xb)[KH][TN], float4 (&xs)[KH], int grp) {
+#pragma unroll
+    for (int h = 0; h < KH; ++h) {
+      const int k = KG * grp + 16 * h + 4 * q;
+      if (AKC && asub) xs[h] = *reinterpret_cast<const float4*>(asub + k);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) xa[h][i] = load_full<AKC>(ap[i], lda, k);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) xb[h][j] = load_full<BKC>(bp[j], ldb, k);
+    }
+  };
+  auto compute_slot = [&](float4 (&xa)[KH][TM], const float4 (&xb)[KH][TN], const float4 (&xs)[KH]) {
+    if (AKC && asub) {
+#pragma unroll
+      for (int h = 0; h < KH; ++h)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          xa[h][i].x -= xs[h].x;
+          xa[h][i].y -= xs[h].y;
+          xa[h][i].z -= xs[h].z;
+          xa[h][i].w -= xs[h].w;
+        }
+    }
+#pragma unroll
+    for (int h = 0; h < KH; ++h)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32((&xa[h][i].x)[e], (&xb[h][j].x)[e], acc[i][j], 0, 0, 0);
+  };
+  // Loads are issued unconditionally (group index clamped to the wave's last group, so the
+  // addresses stay valid and the surplus loads are never consumed): the loop body is then
+  // straight-line between scalar branches and the waitcnt pass keeps D − 1 groups in flight
+  // (a conditional issue makes it wait for everything at the join).
+  const int glast = max(g1 - 1, g0);
+#pragma unroll
+  for (int s = 0; s < D - 1; ++s) load_slot(fa[s], fb[s], fs[s], min(g0 + s, glast));
+  // chunks of D groups with no branch inside (load group g + s + D − 1, compute group g + s),
+  // then the < D remaining groups, whose data the last chunk (or the prologue) loaded
+  int g = g0;
+  for (; g + D <= g1; g += D) {
+#pragma unroll
+    for (int s = 0; s < D; ++s) {
+#ifndef EVX_KS_NO_LOADS  // probe: MFMA loop alone (operands of the prologue reused)
+#ifdef EVX_KS_FAKE_LOADS  // probe: every group re-reads group g0 (L1-resident operands)
+      load_slot(fa[(s + D - 1) % D], fb[(s + D - 1) % D], fs[(s + D - 1) % D], g0);
+#else
+      load_slot(fa[(s + D - 1) % D], fb[(s + D - 1) % D], fs[(s + D - 1) % D], min(g + s + D - 1, glast));
+#endif
+#endif
+      // keep the issue order (loads of group g + s + D − 1 before the MFMAs of group g + s):
+      // left alone, the scheduler sinks the loads behind the MFMAs and the prefetch distance
+      // collapses to one group
+      __builtin_amdgcn_sched_barrier(0);
+      compute_slot(fa[s], fb[s], fs[s]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < D - 1; ++s)
+    if (g + s < g1) compute_slot(fa[s], fb[s], fs[s]);
+  if (w == 0 && K % KG) {  // tail (masked loads)
+#pragma unroll
+    for (int h = 0; h < KH; ++h) {
+      const int k = KG * ngf + 16 * h + 4 * q;
+      if (AKC && asub) fs[0][h] = load_tail<true>(asub, 0, k, K);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[0][h][i] = load_tail<AKC>(ap[i], lda, k, K);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[0][h][j] = load_tail<BKC>(bp[j], ldb, k, K);
+    }
+    compute_slot(fa[0], fb[0], fs[0]);
+  }
+
+  // ---- epilogue: sum the four K-partials through LDS, pairwise: waves 2, 3 park theirs,
+  // waves 0, 1 add them (fixed order: deterministic), park the sums; all threads add the two
+  // accumulator map (16x16): col = lane & 15, row = 4·(lane >> 4) + reg
+  auto park = [&](int buf) {
+    float* my = red + buf * BM * P;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) my[(16 * i + 4 * q + e) * P + 16 * j + r] = acc[i][j][e];
+  };
+  if (w >= 2) park(w - 2);
+  __syncthreads();
+  if (w < 2) {
+    const float* his = red + w * BM * P;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[i][j][e] += his[(16 * i + 4 * q + e) * P + 16 * j + r];
+  }
+  __syncthreads();
+  if (w < 2) park(w);
+  __syncthreads();
+  const float sc = p.alpha * (p.alpha_ptr ? p.alpha_ptr[0] : 1.f);
+  constexpr int NV4 = BM * BN / 4;
+  constexpr int PER = (NV4 + 255) / 256;
+  float4 out[PER];
+#pragma unroll
+  for (int v = 0; v < PER; ++v) {
+    const int e = threadIdx.x + 256 * v;
+    if (e < NV4) {
+      const int row = e / (BN / 4), c = (e % (BN / 4)) * 4;
+      float4 t = *reinterpret_cast<const float4*>(&red[row * P + c]);
+      {
+        const float4 u = *reinterpret_cast<const float4*>(&red[BM * P + row * P + c]);
+        t.x += u.x;
+        t.y += u.y;
+        t.z += u.z;
+        t.w += u.w;
+      }
+      t.x *= sc;
+      t.y *= sc;
+      t.z *= sc;
+      t.w *= sc;
+      const int gr = m0 + row, gc = n0 + c;
+      if (p.bias_n) {
+        if (gc < p.N) t.x += p.bias_n[gc];
+        if (gc + 1 < p.N) t.y += p.bias_n[gc + 1];
+        if (gc + 2 < p.N) t.z += p.bias_n[gc + 2];
+        if (gc + 3 < p.N) t.w += p.bias_n[gc + 3];
+      }
+      if (gr < p.M) {
+        float* crow = p.C + (int64_t)gr * p.ldc;
+        if (p.Cin) {
+          const float* cin = p.Cin + (int64_t)gr * p.ldcin;
+          if (gc < p.N) t.x += p.beta * cin[gc];
+          if (gc + 1 < p.N) t.y += p.beta * cin[gc + 1];
+          if (gc + 2 < p.N) t.z += p.beta * cin[gc + 2];
+          if (gc + 3 < p.N) t.w += p.beta * cin[gc + 3];
+        }
+        if (MODE != 0 && tm == tn) {
+          // diagonal tile: only its upper triangle is stored here (the mirror pass writes the
+          // lower one from it), so the output is exactly (skew-)symmetric; skew diagonal = 0
+          const float vv[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+          for (int e2 = 0; e2 < 4; ++e2) {
+            const int cc = c + e2;
+            if (gc + e2 < p.N && row <= cc) crow[gc + e2] = (MODE == 2 && row == cc) ? 0.f : vv[e2];
+          }
+        } else if (gc + 3 < p.N && p.c_vec4) {
+          *reinterpret_cast<float4*>(crow + gc) = t;
+        } else {
+          if (gc < p.N) crow[gc] = t.x;
+          if (gc + 1 < p.N) crow[gc + 1] = t.y;
+          if (gc + 2 < p.N) crow[gc + 2] = t.z;
+          if (gc + 3 < p.N) crow[gc + 3] = t.w;
+        }
+      }
+      out[v] = t;
+    }
+  }
+  if (MODE == 0) return;
+  // mirrored tile C[n0 + c][m0 + r] = ±v(r, c), stored with consecutive threads on
+  // consecutive r (coalesced rows of the mirrored tile)
+  __syncthreads();
+#pragma unroll
+  for (int v = 0; v < PER; ++v) {
+    const int e = threadIdx.x + 256 * v;
+    if (e < NV4) {
+      const int row = e / (BN / 4), c = (e % (BN / 4)) * 4;
+      *reinterpret_cast<float4*>(&red[row * P + c]) = out[v];
+    }
+  }
+  __syncthreads();
+  const float sgn = MODE == 2 ? -1.f : 1.f;
+  const bool diag = tm == tn;
+  for (int e = threadIdx.x; e < BM * BN; e += 256) {
+    const int rr = e % BM, cc = e / BM;
+    const int gr = n0 + cc, gc = m0 + rr;
+    if (gr < p.N && gc < p.M && (!diag || rr < cc)) p.C[(int64_t)gr * p.ldc + gc] = sgn * red[rr * P + cc];
+  }
+}
+
+#ifndef EVX_KS_KH
+#define EVX_KS_KH 1
+#endif
+
+template <int TM, int TN, int MODE>
+void launch_layout(const EvxGemmKs& a, int tiles, hipStream_t s) {
+  constexpr int KH = EVX_KS_KH;
+  const dim3 grid(tiles), block(256);
+  if (a.a_kc && a.b_kc) gemm_ks_kernel<TM, TN, KH, true, true, MODE><<<grid, block, 0, s>>>(a);
+  else if (a.a_kc && !a.b_kc) gemm_ks_kernel<TM, TN, KH, true, false, MODE><<<grid, block, 0, s>>>(a);
+  else if (!a.a_kc && a.b_kc) gemm_ks_kernel<TM, TN, KH, false, true, MODE><<<grid, block, 0, s>>>(a);
+  else gemm_ks_kernel<TM, TN, KH, false, false, MODE><<<grid, block, 0, s>>>(a);
+}
+
+template <int TM, int TN>
+void launch_tile(EvxGemmKs a, hipStream_t s) {
+  a.tiles_m = (a.M + 16 * TM - 1) / (16 * TM);
+  a.tiles_n = (a.N + 16 * TN - 1) / (16 * TN);
+  if (a.mode == 0) launch_layout<TM, TN, 0>(a, a.tiles_m * a.tiles_n, s);
+  else if (a.mode == 1) launch_layout<TM, TN, 1>(a, a.tiles_m * (a.tiles_m + 1) / 2, s);
+  else launch_layout<TM, TN, 2>(a, a.tiles_m * (a.tiles_m + 1) / 2, s);
+}
+
+int g_ks_tile_override = 0;
+
+}  // namespace
+
+void evx_gemm_ks_set_tile(int t) { g_ks_tile_override = t; }
+
+int evx_gemm_ks_tile(int M, int N, int mode) {
+  if (g_ks_tile_override) return (g_ks_tile_override == 8 && mode != 0) ? 4 : g_ks_tile_override;
+  // tall full products (sampling / CEC rotation, 10 000 × 1000 × 1000): 128 × 64 tiles —
+  // half the B-panel reloads per output of 64 × 64 (tools/gemm_ks_probe.cpp: 210 vs 317 µs)
+  if (mode == 0 && M >= 2048 && N >= 64) return 8;
+  // fewest workgroup rounds over the 256 CUs × tile work, larger tile on ties
+  int best = 4;
+  double best_cost = 1e300;
+  for (int t : {4, 3, 2}) {
+    const int b = 16 * t;
+    const long tm = (M + b - 1) / b, tn = (N + b - 1) / b;
+    const long tiles = mode == 0 ? tm * tn : tm * (tm + 1) / 2;
+    const double cost = (double)((tiles + 255) / 256) * (double)(b * b);
+    if (cost < best_cost * 0.999) {
+      best_cost = cost;
+      best = t;
+    }
+  }
+  return best;
+}
+
+void evx_gemm_ks(const EvxGemmKs& a, hipStream_t s) {
+  if (a.M <= 0 || a.N <= 0) return;
+  switch (evx_gemm_ks_tile(a.M, a.N, a.mode)) {
+    case 2: launch_tile<2, 2>(a, s); break;
+    case 3: launch_tile<3, 3>(a, s); break;
+    case 8: launch_tile<8, 4>(a, s); break;  // tall products (M ≫ N), full mode only
+    default: launch_tile<4, 4>(a, s); break;
+  }
+}

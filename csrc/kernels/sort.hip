@@ -137,14 +137,15 @@ __global__ void __launch_bounds__(1024) radix_argsort_kernel(const float* __rest
   int32_t v[IT];
   // padding sorts behind every real key, NaNs included (largest / smallest NaN bit patterns)
   const float pad = __uint_as_float(descending ? 0xffffffffu : 0x7fffffffu);
-  // every NaN (either sign bit) becomes the canonical padding key so NaNs sort last when
-  // ascending and first when descending, as torch.sort does; -0.0 becomes +0.0 (torch
-  // treats them as equal keys: ties keep index order)
+  // every NaN (either sign bit) becomes the largest key 0x7fffffff, so NaNs sort last when
+  // ascending (tied with the padding, which follows by index) and first when descending, as
+  // torch.sort does; -0.0 becomes +0.0 (torch treats them as equal keys: index order)
+  const float qnan = __uint_as_float(0x7fffffffu);
 #pragma unroll
   for (int r = 0; r < IT; ++r) {
     const int i = threadIdx.x * IT + r;
     float x = i < n ? kb[i] : pad;
-    x = (x != x) ? pad : (x == 0.f ? 0.f : x);
+    if (i < n) x = (x != x) ? qnan : (x == 0.f ? 0.f : x);
     k[r] = x;
     v[r] = i;
   }

@@ -9,17 +9,17 @@ cμ ≈ 4.98e-3 and the eigendecomposition runs every generation.
 MI355X execution of one generation on a GPU (everything stays in HBM, no host
 synchronisation, hipGraph-capturable):
 
-* ``ask``: Philox normals (``rng.hip``) → ONE plain f32 GEMM
-  ``X = mean + Z (σ·B∘D)ᵀ`` (σ folded into the d×d factor on the device; the
-  ``mean`` bias in the epilogue) — hipBLASLt by default (``EVOXMI_PLAIN_GEMM``),
-  or the framework MFMA kernel with ``mean + σ·`` fused in its epilogue.
+* ``ask``: Philox normals (``rng.hip``) → ONE f32 GEMM ``X = mean + σ·Z (B∘D)ᵀ``
+  on the framework kernel (``gemm_ks.hip``: σ as a device scale, ``mean`` as the
+  bias epilogue).
 * ``tell``: argsort of the fitness; the weighted mean is a gathered weighted row
-  sum (``reduce.hip``); the rank-μ update ``Σ wᵢ yᵢ yᵢᵀ`` is either a plain vendor
-  GEMM on the materialised ``Y = (x_sel − m)/σ`` (default) or the framework GEMM
-  whose prologue *gathers* the selected rows by index and applies
-  ``(x − m)/σ · w`` on the fly, split-K into deterministic slabs;
-  warm-started block-Jacobi ``eigh`` (:mod:`evoxmi.ops.eigh`); ``invsqrtC`` as a
-  GEMM with ``1/D`` fused in the prologue.
+  sum (``reduce.hip``); the rank-μ update ``Σ wᵢ yᵢ yᵢᵀ`` is a symmetric-output
+  framework GEMM (upper tiles only) on the materialised ``Yw = (x_sel − m)/σ·√w``
+  (``cma_center_rows``), or the older framework GEMM whose prologue *gathers* the
+  selected rows (``EVOXMI_PLAIN_GEMM`` ≠ evoxmi/blas);
+  converged sorted-block-refinement ``eigh`` (:mod:`evoxmi.ops.sbr`); ``invsqrtC``
+  = (B/D)Bᵀ as a symmetric-output GEMM.  ``EVOXMI_PLAIN_GEMM=blas`` swaps the plain
+  products for hipBLASLt (an A/B baseline only).
 * Sharded (``ask_sharded``/``tell_sharded``): each rank generates only its rows
   (Philox counters are global row indices, so 1/2/4/8 GPUs sample the same
   population), fitness is all-gathered, and each rank all-reduces its partial
@@ -37,7 +37,7 @@ from ....ops.eigh import sbr_phase, symmetrize_upper, warm_eigh
 from ....runtime import host_phase
 from ....utils import profiling
 from .... import config
-from ....ops.linalg import Operand, gemm, plain_nt
+from ....ops.linalg import Operand, gemm, mm, plain_nt
 from ....ops.reduce import weighted_rowsum
 from ....ops.sort import argsort, argsort_i32
 
@@ -122,7 +122,7 @@ class CMAES(Algorithm):
             if config.get("plain_gemm") == "blas":
                 return plain_nt(z, (state.B * (state.D * state.sigma)).contiguous(), bias_n=state.mean)
             BD = (state.B * state.D).contiguous()
-            return gemm(Operand(z), Operand(BD), rows, d, d, alpha_ptr=state.sigma.reshape(1), bias_n=state.mean)
+            return mm(z, BD, tb=True, alpha_ptr=state.sigma.reshape(1), bias_n=state.mean)
         return state.mean + state.sigma * (state.D * z) @ state.B.T
 
     def ask(self, state):
@@ -139,16 +139,19 @@ class CMAES(Algorithm):
             one_over = state.sigma.reshape(1)
             # weighted mean shift: gathered weighted row sum (reduce.hip), deterministic
             dm = weighted_rowsum(population, rows, wvec, state.mean, K)
-            if config.get("plain_gemm") == "blas":
+            if config.get("plain_gemm") in ("blas", "evoxmi"):
                 # materialise Y = (x_sel − m)/σ once (K×d, 20 MB at the north-star shape) and
-                # run the rank-μ product as a plain vendor GEMM Yᵀ·(w∘Y)
-                # (weights are positive: Σ wᵢ yᵢ yᵢᵀ = Ywᵀ Yw with Yw = y·sqrt(w), one fused
-                # gather/centre/scale pass, cmaes.hip)
+                # run the rank-μ product Yᵀ·(w∘Y) as one GEMM (weights are positive:
+                # Σ wᵢ yᵢ yᵢᵀ = Ywᵀ Yw with Yw = y·sqrt(w), one fused gather/centre/scale pass,
+                # cmaes.hip); the framework GEMM computes only the upper tiles of the
+                # symmetric product
                 from ....ops import _ext
 
                 Yw = _ext.ops().cma_center_rows(population, rows, state.mean.contiguous(), state.sigma.reshape(1),
                                                 wvec.contiguous())
-                return dm, torch.mm(Yw.t(), Yw)
+                if config.get("plain_gemm") == "blas":
+                    return dm, torch.mm(Yw.t(), Yw)
+                return dm, mm(Yw, Yw, ta=True, mode=1)
             splits = max(1, min(16, K // 256))
             S = gemm(
                 Operand(population, rc=True, gather=rows, sub=state.mean, kw=wvec, sscale=one_over, sscale_inv=True),
@@ -197,7 +200,8 @@ class CMAES(Algorithm):
             with profiling.phase("eigh"):
                 w, Bp = jacobi.warm_eigh_padded(Cp, Bp, d, max_sweeps=self.eig_sweeps)
             B, D, BdivD = ops.cma_eig_out(Bp, w, d)
-        invsqrtC = plain_nt(BdivD, B) if config.get("plain_gemm") == "blas" else gemm(Operand(BdivD), Operand(B), d, d, d)
+        # (B/D)·Bᵀ is symmetric: upper tiles only
+        invsqrtC = plain_nt(BdivD, B) if config.get("plain_gemm") == "blas" else mm(BdivD, B, tb=True, mode=1)
         return state.update(mean=mean, ps=ps, pc=pc, C=C, sigma=sigma.reshape(state.sigma.shape), B=B, D=D, invsqrtC=invsqrtC,
                             count_eigen=state.count_eigen + 1, eig_stats=eig_stats)
 
@@ -229,7 +233,7 @@ class CMAES(Algorithm):
         w = torch.clamp(w, min=1e-30)
         D = torch.sqrt(w)
         if B.is_cuda:
-            invsqrtC = plain_nt(B / D, B) if config.get("plain_gemm") == "blas" else gemm(Operand(B, kscale=1.0 / D), Operand(B), self.dim, self.dim, self.dim)
+            invsqrtC = plain_nt(B / D, B) if config.get("plain_gemm") == "blas" else mm((B / D).contiguous(), B, tb=True, mode=1)
         else:
             invsqrtC = (B / D) @ B.T
         return B, D, invsqrtC

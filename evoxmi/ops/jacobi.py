@@ -81,8 +81,23 @@ def reorthonormalize(B: torch.Tensor) -> torch.Tensor:
     B = B.contiguous()
     if config.get("plain_gemm") == "blas":
         return torch.addmm(B, B, B.t() @ B, beta=1.5, alpha=-0.5)
-    X = gemm(Operand(B, rc=True), Operand(B, rc=True), n, n, n)
-    return gemm(Operand(B), Operand(X), n, n, n, alpha=-0.5, beta=1.5, Cin=B)
+    if not B.is_cuda:
+        X = gemm(Operand(B, rc=True), Operand(B, rc=True), n, n, n)
+        return gemm(Operand(B), Operand(X), n, n, n, alpha=-0.5, beta=1.5, Cin=B)
+    from .linalg import mm
+
+    G = mm(B, B, ta=True, mode=1)  # BᵀB, symmetric: upper tiles only
+    return mm(B, G, tb=True, alpha=-0.5, beta=1.5, Cin=B)
+
+
+def _btcb(C: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
+    """Bᵀ C B for symmetric C: framework GEMMs on the device (Bᵀ·C with C's rows, then a
+    symmetric-output product), the GEMM oracle path on the CPU."""
+    if C.is_cuda:
+        from .linalg import mm
+
+        return mm(mm(B, C, ta=True, tb=True), B, mode=1)
+    return matmul_tn(B, matmul(C, B)).contiguous()
 
 
 def warm_eigh(C: torch.Tensor, B_prev: torch.Tensor = None, max_sweeps: int = None, tol: float = None, return_stats: bool = False):
@@ -104,7 +119,7 @@ def warm_eigh(C: torch.Tensor, B_prev: torch.Tensor = None, max_sweeps: int = No
         if config.get("plain_gemm") == "blas":
             A = (Bp.t() @ (Cp @ Bp)).contiguous()
         else:
-            A = matmul_tn(Bp, matmul(Cp, Bp)).contiguous()
+            A = _btcb(Cp, Bp)
         sweeps = config.get("jacobi_sweeps") if max_sweeps is None else max_sweeps
     tol = tol or config.get("jacobi_tol_factor") * 1.1920929e-07 * max(n, 16) ** 0.5
     w, stats = _ext.ops().jacobi_sweeps(A, Bp, schedule(np_ // 16, dev), int(sweeps), float(tol),
@@ -126,7 +141,7 @@ def warm_eigh_padded(Cp: torch.Tensor, Bp: torch.Tensor, n: int, max_sweeps: int
     if config.get("plain_gemm") == "blas":
         A = (Bp.t() @ (Cp @ Bp)).contiguous()
     else:
-        A = matmul_tn(Bp, matmul(Cp, Bp)).contiguous()
+        A = _btcb(Cp, Bp)
     Bp = Bp.contiguous()
     sweeps = config.get("jacobi_sweeps") if max_sweeps is None else max_sweeps
     tol = tol or config.get("jacobi_tol_factor") * 1.1920929e-07 * max(n, 16) ** 0.5

@@ -13,6 +13,12 @@ Operands are described by :class:`Operand`; ``rc=False`` means the tensor is
 
 The CPU branch materialises Ã and B̃ with torch and is the numerics oracle of
 the GPU tests.
+
+``mm`` is the flagship's product (``csrc/kernels/gemm_ks.hip``: the four waves of a
+workgroup split K, operand fragments go global → registers with no LDS staging and no
+barrier in the main loop, ``v_mfma_f32_16x16x4_f32``), with symmetric / skew-symmetric
+output modes that compute only the upper tiles, a fused bias / Cin epilogue, a device
+scale and a device ``skip`` word (device-side control of fixed iteration schedules).
 """
 from __future__ import annotations
 
@@ -109,17 +115,72 @@ def matmul_tn(A: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
     return gemm(Operand(A, rc=True), Operand(B, rc=True), A.shape[1], B.shape[1], A.shape[0])
 
 
-def plain_nt(A: torch.Tensor, B: torch.Tensor, alpha: float = 1.0, bias_n: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``alpha·A·Bᵀ (+ bias_n)`` for PLAIN operands (no gather/prologue): on a GPU this goes to
-    the vendor GEMM (hipBLASLt via ``torch.addmm``) when ``EVOXMI_PLAIN_GEMM=blas`` (default;
-    10 000×1000×1000 f32 on MI355X: 0.217 ms vs 0.266 ms for the framework kernel, see
-    profiles/r1_kernel_microbench.json), else to :func:`gemm`.  Fused-prologue GEMMs
-    (row gathers, shifts, per-k weights) always use the framework kernel."""
+def plain_nt(A: torch.Tensor, B: torch.Tensor, alpha: float = 1.0, bias_n: Optional[torch.Tensor] = None,
+             a_sub_k: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``alpha·(A − a_sub_k)·Bᵀ (+ bias_n)`` for plain row-major operands: the framework GEMM
+    (:func:`mm`).  ``EVOXMI_PLAIN_GEMM=blas`` routes it to the vendor GEMM instead (hipBLASLt
+    via ``torch.addmm``) — an A/B baseline, never the default."""
     from .. import config
 
-    M, K = A.shape
-    N = B.shape[0]
     if A.is_cuda and config.get("plain_gemm") == "blas":
+        if a_sub_k is not None:
+            A = A - a_sub_k
         bias = bias_n if bias_n is not None else A.new_zeros(())
         return torch.addmm(bias, A, B.t(), beta=1.0 if bias_n is not None else 0.0, alpha=alpha)
-    return gemm(Operand(A), Operand(B), M, N, K, alpha=alpha, bias_n=bias_n)
+    return mm(A, B, tb=True, alpha=alpha, bias_n=bias_n, a_sub_k=a_sub_k)
+
+
+def mm(A: torch.Tensor, B: torch.Tensor, *, ta: bool = False, tb: bool = False, mode: int = 0, alpha: float = 1.0,
+       alpha_ptr: Optional[torch.Tensor] = None, bias_n: Optional[torch.Tensor] = None, beta: float = 0.0,
+       Cin: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+       skip: Optional[torch.Tensor] = None, a_sub_k: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``alpha·(*alpha_ptr)·op(A)·op(B) (+ bias_n) (+ beta·Cin)`` with ``op(X) = Xᵀ`` when
+    ``ta`` / ``tb`` (transposes are layouts, never copies).  ``mode`` 1 / 2: the result is
+    symmetric / skew-symmetric by construction of the caller (Bᵀ C B, X·X for skew X, …);
+    only tiles with tm ≤ tn are computed and the rest mirrored.  ``out``: written in place.
+    ``skip``: int32 device word — the kernel does nothing while it is non-zero.
+    ``a_sub_k``: op(A)(m, k) − a_sub_k[k] (fused shift, ``op(A) = A`` only).
+
+    On a GPU this is always the framework kernel (no vendor GEMM); shapes the kernel does
+    not take (K % 4 ≠ 0 with a K-contiguous operand) go to :func:`gemm`."""
+    M = A.shape[1] if ta else A.shape[0]
+    K = A.shape[0] if ta else A.shape[1]
+    N = B.shape[0] if tb else B.shape[1]
+    if A.is_cuda:
+        a_kc, b_kc = not ta, tb
+        ok = (K % 4 == 0) or not (a_kc or b_kc)
+        A_ = A if A.stride(-1) == 1 else A.contiguous()
+        B_ = B if B.stride(-1) == 1 else B.contiguous()
+        sub_ok = a_sub_k is None or (a_kc and a_sub_k.is_contiguous() and a_sub_k.data_ptr() % 16 == 0)
+        if ok and sub_ok and A_.data_ptr() % 16 == 0 and B_.data_ptr() % 16 == 0:
+            args = (A_, int(a_kc), B_, int(b_kc), int(M), int(N), int(K), int(mode), float(alpha), alpha_ptr, bias_n,
+                    float(beta), Cin)
+            if out is not None:
+                _ext.ops().gemm_ks_out(*args, out, skip, a_sub_k)
+                return out
+            return _ext.ops().gemm_ks(*args, skip, a_sub_k)
+        if skip is not None:
+            raise ValueError("mm: skip needs a shape the gemm_ks kernel takes")
+        Ao = Operand(A_, rc=ta, sub=a_sub_k, sub_on_k=a_sub_k is not None)
+        C = gemm(Ao, Operand(B_, rc=not tb), M, N, K, alpha=alpha, alpha_ptr=alpha_ptr, bias_n=bias_n, beta=beta, Cin=Cin)
+        if out is not None:
+            out.copy_(C)
+            return out
+        return C
+    Am = A.t() if ta else A
+    Bm = B.t() if tb else B
+    s = alpha * (alpha_ptr.reshape(()) if alpha_ptr is not None else 1.0)
+    Am = Am[:M, :K].to(torch.float32)
+    if a_sub_k is not None:
+        Am = Am - a_sub_k[None, :K]
+    C = s * (Am @ Bm[:K, :N].to(torch.float32))
+    if bias_n is not None:
+        C = C + bias_n[None, :N]
+    if Cin is not None:
+        C = C + beta * Cin[:M, :N]
+    if skip is not None and int(skip.reshape(-1)[0]) != 0:
+        return out if out is not None else torch.zeros(M, N, dtype=torch.float32)
+    if out is not None:
+        out.copy_(C)
+        return out
+    return C

@@ -41,6 +41,7 @@ from typing import List
 import torch
 
 from . import _ext
+from .linalg import mm
 
 BK = 64
 
@@ -272,11 +273,13 @@ def expm_taylor6(X: torch.Tensor, X2: torch.Tensor = None, alpha: torch.Tensor =
     """exp(αX) to 6th order with 3 GEMMs (Paterson–Stockmeyer), Y = αX:
     I + Y + Y²/2 + Y³/6 + Y³(Y/24 + Y²/120 + Y³/720).  ``alpha`` is a 1-element device
     tensor (no host sync), folded into the elementwise prep."""
+    if X.is_cuda:
+        X2 = mm(X, X, tb=True, mode=1, alpha=-1.0) if X2 is None else X2
+        X3 = mm(X2, X, tb=True, mode=2, alpha=-1.0)
+        P, M = _ext.ops().sbr_taylor_prep(X.contiguous(), X2, X3, alpha)
+        return mm(X3, P, beta=1.0, Cin=M, out=M)  # in place: no copy of M into a fresh output
     X2 = X @ X if X2 is None else X2
     X3 = X2 @ X
-    if X.is_cuda:
-        P, M = _ext.ops().sbr_taylor_prep(X.contiguous(), X2, X3, alpha)
-        return torch.addmm(M, X3, P, out=M)  # in place: no copy of M into a fresh output
     a = 1.0 if alpha is None else alpha.reshape(())
     Y, Y2, Y3 = a * X, (a * a) * X2, (a * a * a) * X3
     P = Y / 24 + Y2 / 120 + Y3 / 720
@@ -292,13 +295,32 @@ def expm_taylor4(X: torch.Tensor, X2: torch.Tensor, alpha: torch.Tensor = None) 
     ‖Y‖ is small (κ below ``SBRConfig.t4_kappa``)."""
     if X.is_cuda:
         P, M = _ext.ops().sbr_taylor4_prep(X.contiguous(), X2, alpha)
-        return torch.addmm(M, X2, P, out=M)
+        return mm(X2, P, beta=1.0, Cin=M, out=M)
     a = 1.0 if alpha is None else alpha.reshape(())
     Y, Y2 = a * X, (a * a) * X2
     V = Y2 @ (Y / 6 + Y2 / 24)
     V += Y + Y2 / 2
     V.diagonal().add_(1.0)
     return V
+
+
+def expm_t_device(X: torch.Tensor, X2: torch.Tensor, alpha: torch.Tensor = None, order: int = 6) -> torch.Tensor:
+    """Vᵀ = exp(αX)ᵀ = exp(−αX) on the device, every product an A·Bᵀ GEMM on row-major
+    operands (gemm_ks K-contiguous loads): with P = P(α) of the Taylor prep and
+    M(−α) (the prep's ``mt`` flag, odd terms negated), Pᵀ(α) = −P(−α) for order 6 and
+    +P(−α) for order 4 (X skew), so
+
+        order 6:  Vᵀ = M(−α) − X³·P(α)ᵀ      (X³ = X²·X = −X²·Xᵀ, skew: upper tiles only)
+        order 4:  Vᵀ = M(−α) + X²·P(α)ᵀ
+
+    and the basis update B·V = B·(Vᵀ)ᵀ reads Vᵀ's rows too."""
+    ops = _ext.ops()
+    if order == 6:
+        X3 = mm(X2, X, tb=True, mode=2, alpha=-1.0)
+        P, MT = ops.sbr_taylor_prep(X.contiguous(), X2, X3, alpha, 1)
+        return mm(X3, P, tb=True, alpha=-1.0, beta=1.0, Cin=MT, out=MT)
+    P, MT = ops.sbr_taylor4_prep(X.contiguous(), X2, alpha, 1)
+    return mm(X2, P, tb=True, alpha=1.0, beta=1.0, Cin=MT, out=MT)
 
 
 @functools.lru_cache(maxsize=8)
@@ -326,23 +348,35 @@ def damping(X2: torch.Tensor, tau: float, out: torch.Tensor = None) -> torch.Ten
     return torch.clamp(tau / torch.sqrt(lam.clamp_min(1e-30)), max=1.0).reshape(1).to(torch.float32)
 
 
-def newton_schulz(B: torch.Tensor) -> torch.Tensor:
+def newton_schulz(B: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
     """One step toward the nearest orthonormal matrix, B(1.5 I − 0.5 BᵀB)."""
+    if B.is_cuda:
+        G = mm(B, B, ta=True, mode=1)  # BᵀB: symmetric, upper tiles only
+        return mm(B, G, tb=True, alpha=-0.5, beta=1.5, Cin=B, out=out)
     return torch.addmm(B, B, B.t() @ B, beta=1.5, alpha=-0.5)
+
+
+def _btcb_device(C: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
+    """Bᵀ C B on the device as two framework GEMMs: W = Bᵀ·C (C symmetric: its rows are
+    read K-contiguous) and T = W·B with a symmetric output (upper tiles only)."""
+    W = mm(B, C, ta=True, tb=True)
+    return mm(W, B, mode=1)
 
 
 def sym_product(C: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
     """A = Bᵀ C B, symmetrised."""
+    if C.is_cuda:
+        return _btcb_device(C, B)
     A = B.t() @ (C @ B)
     return (A + A.t()) * 0.5
 
 
 def sym_product_stats(C: torch.Tensor, B: torch.Tensor):
     """(A = sym(Bᵀ C B), stats(A)); on the device symmetrisation and stats are one kernel."""
-    T = B.t() @ (C @ B)
-    if T.is_cuda:
-        A, st = _ext.ops().sbr_symstats(T)
+    if C.is_cuda:
+        A, st = _ext.ops().sbr_symstats(_btcb_device(C, B))
         return A, st
+    T = B.t() @ (C @ B)
     A = (T + T.t()) * 0.5
     return A, stats_ref(A)
 
@@ -409,6 +443,7 @@ def _refine_core(C, A, B, st, off: int, ns: bool, damp: bool, cfg: SBRConfig, ou
     fewer)."""
     perm, Q, dq = block_solve(A, off, cfg.block_sweeps, cfg.block)
     alpha = None
+    dev = A.is_cuda
     if not far_on:
         Bn = bq(B, off, perm, Q, cfg.block)
         if out:
@@ -416,20 +451,24 @@ def _refine_core(C, A, B, st, off: int, ns: bool, damp: bool, cfg: SBRConfig, ou
             Bn = out[1]
     else:
         X = far(A, off, perm, Q, dq, st, cfg.thr_fac, cfg.block, theta)
-        X2 = X @ X
+        # X is skew: X² = −X·Xᵀ is symmetric (upper tiles only)
+        X2 = mm(X, X, tb=True, mode=1, alpha=-1.0) if dev else X @ X
         if damp and cfg.damp_tau > 0:
             alpha = damping(X2, cfg.damp_tau, out=out[3] if out else None)
         Bq = bq(B, off, perm, Q, cfg.block)
-        V = expm_taylor6(X, X2, alpha) if order == 6 else expm_taylor4(X, X2, alpha)
-        if ns:
-            Bn = Bq @ V
-            BtB = Bn.t() @ Bn
-            Bn = torch.addmm(Bn, Bn, BtB, beta=1.5, alpha=-0.5, out=out[1]) if out else newton_schulz(Bn)
+        if dev:
+            # every product A·Bᵀ on row-major operands: Bq·V = Bq·(Vᵀ)ᵀ (expm_t_device)
+            VT = expm_t_device(X, X2, alpha, order)
+            if ns:
+                Bn = mm(Bq, VT, tb=True)
+                Bn = newton_schulz(Bn, out=out[1] if out else None)
+            else:
+                Bn = mm(Bq, VT, tb=True, out=out[1] if out else None)
         else:
-            Bn = torch.mm(Bq, V, out=out[1]) if out else Bq @ V
-    if out and Bn.is_cuda:
-        T = Bn.t() @ (C @ Bn)
-        _ext.ops().sbr_symstats_out(T, out[0], out[2])
+            V = expm_taylor6(X, X2, alpha) if order == 6 else expm_taylor4(X, X2, alpha)
+            Bn = newton_schulz(Bq @ V) if ns else Bq @ V
+    if out and dev:
+        _ext.ops().sbr_symstats_out(_btcb_device(C, Bn), out[0], out[2])
         A, st = out[0], out[2]
     else:
         A, st = sym_product_stats(C, Bn)
@@ -511,8 +550,7 @@ class _Workspace:
     def init(self):
         # no re-orthonormalisation here: iteration 0 always applies Newton–Schulz to its result
         def body():
-            T = self.B.t() @ (self.C @ self.B)
-            _ext.ops().sbr_symstats_out(T, self.A, self.hist[0])
+            _ext.ops().sbr_symstats_out(_btcb_device(self.C, self.B), self.A, self.hist[0])
             self.alpha.fill_(1.0)
 
         self._capture(("init",), body).replay()

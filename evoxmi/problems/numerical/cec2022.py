@@ -203,12 +203,13 @@ class _CEC2022(Problem):
             self._cache[key] = c
         return self._cache[key]
 
-    # ssr: z = M (x − o)·s.  The shift is applied before the GEMM (exact zero at the
-    # optimum, as in the reference) and the scale folds into the GEMM epilogue.
+    # ssr: z = M (x − o)·s.  The shift is applied to the operand before the products (exact
+    # zero at the optimum, as in the reference): on the device it is the GEMM's fused A
+    # prologue (no shifted copy of the population), the scale folds into the epilogue.
     def _ssr(self, X, o, M, s):
         N, D = X.shape
         if X.is_cuda:
-            return linalg.plain_nt((X - o).contiguous(), M, alpha=float(s))
+            return linalg.plain_nt(X, M, alpha=float(s), a_sub_k=o.contiguous())
         return ((X - o) * s) @ M.T
 
     def _basic(self, Z, fid, perm=None, start=0, length=None, sub=None, scale=1.0, ysrc=None, ystart=0):

@@ -794,7 +794,8 @@ def test_knn_kernel_nan_and_inf_rows():
     ref = torch.cdist(X.double(), Y.double()).min(1).values.float()
     assert torch.isnan(md).all() and torch.isnan(ref).all()  # candidate 7 poisons every row
     md = geom.min_dist(X[:, :2].cuda(), Y[:, :2].cuda()).cpu()
-    ref = torch.cdist(X[:, :2].double(), Y[:, :2].double()).min(1).values.float()
+    # direct-form distances (torch.cdist's matmul form turns an inf coordinate into NaN)
+    ref = (((X[:, None, :2].double() - Y[None, :, :2].double()) ** 2).sum(-1)).sqrt().min(1).values.float()
     assert torch.isnan(md[3]) and torch.isinf(md[4]) and torch.allclose(md, ref, equal_nan=True, rtol=1e-5)
 
 
