@@ -69,10 +69,13 @@ def main():
 
     from evoxmi.ops import eigh as eigh_mod
 
+    from evoxmi.ops import sbr_device
+
     for _ in range(args.warmup):
         state = wf.step(state)
     sync()
     eigh_mod.HISTORY.clear()
+    dev_counts = sbr_device.snapshot_counts()  # device-mode solves: per-solve ring read after timing
     t0 = time.perf_counter()
     for _ in range(args.steps):
         state = wf.step(state)
@@ -80,7 +83,8 @@ def main():
     elapsed = time.perf_counter() - t0
     # per-phase breakdown (outside the timed region): a few eager generations with
     # stream-ordered hipEvent timers; "tell" includes "eigh" (and "all_reduce" when sharded)
-    hist = list(eigh_mod.HISTORY)  # decompositions of the timed generations only
+    hist = list(eigh_mod.HISTORY)  # decompositions of the timed generations only (host mode)
+    dev_hist = sbr_device.histories_since(dev_counts)  # [off_rel, 0, iterations, fallback] (device mode)
     phases = None
     if args.phase_steps > 0:
         from evoxmi.utils.profiling import PhaseTimer
@@ -123,12 +127,25 @@ def main():
                 "pop_size": args.pop,
                 "dim": args.dim,
                 "hipgraph": use_graph,
-                "eigh": config.get("eigh"),
+                "eigh": config.get("eigh") + ("-" + config.get("sbr_mode") if config.get("eigh") == "sbr" else ""),
             },
         }
         if phases:
             out["phases_ms_eager"] = phases
-        if hist:
+        if dev_hist.shape[0]:
+            # every timed generation's decomposition (device-controlled schedule, read back
+            # once after the timed loop): relative off-norm ‖offdiag(BᵀCB)‖/‖diag‖
+            out["eigh_stats"] = {
+                "generations": int(dev_hist.shape[0]),
+                "max_off_rel": float(dev_hist[:, 0].max()),
+                "tol": config.get("eigh_tol"),
+                "mode": "device",
+                "schedule_iters": config.get("sbr_device_iters"),
+                "mean_refine_iters": float(dev_hist[:, 2].mean()),
+                "max_refine_iters": int(dev_hist[:, 2].max()),
+                "fallbacks": int(dev_hist[:, 3].sum()),
+            }
+        elif hist:
             # every timed generation's decomposition: relative off-norm ‖offdiag(BᵀCB)‖/‖diag‖
             out["eigh_stats"] = {
                 "generations": len(hist),

@@ -148,7 +148,9 @@ at::Tensor gemm_ks(const at::Tensor& A, int64_t a_kc, const at::Tensor& B, int64
                    int64_t mode, double alpha, const c10::optional<at::Tensor>& alpha_ptr,
                    const c10::optional<at::Tensor>& bias_n, double beta, const c10::optional<at::Tensor>& Cin,
                    const c10::optional<at::Tensor>& out, const c10::optional<at::Tensor>& skip,
-                   const c10::optional<at::Tensor>& a_sub_k) {
+                   const c10::optional<at::Tensor>& a_sub_k, const c10::optional<at::Tensor>& sel = c10::nullopt,
+                   const c10::optional<at::Tensor>& A2 = c10::nullopt, double alpha2 = 0.0,
+                   const c10::optional<at::Tensor>& C2 = c10::nullopt, const c10::optional<at::Tensor>& stat_part = c10::nullopt) {
   CHECK_DEV(A); CHECK_F32(A); CHECK_DEV(B); CHECK_F32(B);
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.stride(1) == 1 && B.stride(1) == 1, "gemm_ks: 2-D operands with unit inner stride");
   TORCH_CHECK(M > 0 && N > 0 && K > 0, "gemm_ks: empty shape");
@@ -209,6 +211,29 @@ at::Tensor gemm_ks(const at::Tensor& A, int64_t a_kc, const at::Tensor& B, int64
                 "gemm_ks: a_sub_k needs a K-contiguous A and a 16-byte aligned vector of length ≥ K");
     a.a_sub_k = a_sub_k->data_ptr<float>();
   }
+  if (sel.has_value() && sel->defined()) {
+    CHECK_DEV(*sel);
+    TORCH_CHECK(sel->scalar_type() == at::kInt && sel->numel() >= 1, "gemm_ks: sel must be int32");
+    a.sel = sel->data_ptr<int32_t>();
+    a.alpha2 = (float)alpha2;
+    if (A2.has_value() && A2->defined()) {
+      TORCH_CHECK(A2->sizes() == A.sizes() && A2->strides() == A.strides() && A2->scalar_type() == at::kFloat, "gemm_ks: A2 like A");
+      TORCH_CHECK(!a_kc || vec4_ok(*A2), "gemm_ks: A2 alignment");
+      a.A2 = A2->data_ptr<float>();
+    }
+    if (C2.has_value() && C2->defined()) {
+      TORCH_CHECK(C2->sizes() == C.sizes() && C2->strides() == C.strides() && C2->scalar_type() == at::kFloat, "gemm_ks: C2 like out");
+      TORCH_CHECK(vec4_ok(*C2) == vec4_ok(C), "gemm_ks: C2 alignment");
+      a.C2 = C2->data_ptr<float>();
+    }
+  }
+  if (stat_part.has_value() && stat_part->defined()) {
+    TORCH_CHECK(mode == 1, "gemm_ks: stats partials need the symmetric mode");
+    CHECK_DEV(*stat_part);
+    TORCH_CHECK(stat_part->scalar_type() == at::kDouble && stat_part->is_contiguous() &&
+                stat_part->numel() >= 4 * (int64_t)evx_gemm_ks_grid((int)M, (int)N, (int)mode), "gemm_ks: stat_part float64[4·grid]");
+    a.stat_part = stat_part->data_ptr<double>();
+  }
   a.c_vec4 = vec4_ok(C) ? 1 : 0;
   evx_gemm_ks(a, cur_stream());
   return C;
@@ -226,8 +251,82 @@ at::Tensor gemm_ks_new(const at::Tensor& A, int64_t a_kc, const at::Tensor& B, i
 void gemm_ks_out(const at::Tensor& A, int64_t a_kc, const at::Tensor& B, int64_t b_kc, int64_t M, int64_t N, int64_t K,
                  int64_t mode, double alpha, const c10::optional<at::Tensor>& alpha_ptr, const c10::optional<at::Tensor>& bias_n,
                  double beta, const c10::optional<at::Tensor>& Cin, const at::Tensor& out, const c10::optional<at::Tensor>& skip,
-                 const c10::optional<at::Tensor>& a_sub_k) {
-  gemm_ks(A, a_kc, B, b_kc, M, N, K, mode, alpha, alpha_ptr, bias_n, beta, Cin, out, skip, a_sub_k);
+                 const c10::optional<at::Tensor>& a_sub_k, const c10::optional<at::Tensor>& sel, const c10::optional<at::Tensor>& A2,
+                 double alpha2, const c10::optional<at::Tensor>& C2, const c10::optional<at::Tensor>& stat_part) {
+  gemm_ks(A, a_kc, B, b_kc, M, N, K, mode, alpha, alpha_ptr, bias_n, beta, Cin, out, skip, a_sub_k, sel, A2, alpha2, C2, stat_part);
+}
+
+int64_t gemm_ks_grid(int64_t M, int64_t N, int64_t mode) { return evx_gemm_ks_grid((int)M, (int)N, (int)mode); }
+
+// ---- device-controlled SBR schedule (eigh_sbr_dev.hip, ops/sbr_device.py): every op writes
+// into caller-owned buffers and honours a device skip word, so a solve is capturable once
+void sbr16_block_out(const at::Tensor& A, int64_t shift, int64_t sweeps, int64_t sb, at::Tensor& perm, at::Tensor& Q, at::Tensor& dq,
+                     const at::Tensor& skip) {
+  CHECK_DEV(A); CHECK_F32(A);
+  const int64_t n = A.size(0);
+  TORCH_CHECK(A.dim() == 2 && A.size(1) == n && A.stride(1) == 1 && n <= evx_sbr16_max_n(), "sbr16_block_out: A n×n");
+  TORCH_CHECK(sb == 16 || sb == 32, "sbr16_block_out: sb");
+  TORCH_CHECK(perm.numel() >= n && perm.scalar_type() == at::kInt && Q.numel() >= evx_sbr16_nblocks((int)n, (int)sb) * sb * sb &&
+                  dq.numel() >= n, "sbr16_block_out: buffers");
+  evx_sbr16_block(A.data_ptr<float>(), (int)n, A.stride(0), (int)shift, (int)sweeps, perm.data_ptr<int>(), Q.data_ptr<float>(),
+                  dq.data_ptr<float>(), (int)sb, cur_stream(), skip.data_ptr<int>());
+}
+
+void sbr16_far_out(const at::Tensor& A, const at::Tensor& perm, const at::Tensor& Q, const at::Tensor& dq, const at::Tensor& stats,
+                   double thr_fac, const at::Tensor& theta, at::Tensor& X, int64_t sb, const at::Tensor& skip) {
+  const int64_t n = A.size(0);
+  TORCH_CHECK(X.sizes() == A.sizes() && X.stride(1) == 1 && stats.scalar_type() == at::kDouble && theta.scalar_type() == at::kFloat,
+              "sbr16_far_out: shapes");
+  evx_sbr16_far(A.data_ptr<float>(), (int)n, A.stride(0), perm.data_ptr<int>(), Q.data_ptr<float>(), dq.data_ptr<float>(),
+                stats.data_ptr<double>(), (float)thr_fac, 0.f, X.data_ptr<float>(), X.stride(0), (int)sb, cur_stream(),
+                theta.data_ptr<float>(), skip.data_ptr<int>());
+}
+
+void sbr16_bq_out(const at::Tensor& B, const at::Tensor& perm, const at::Tensor& Q, at::Tensor& Bq, int64_t sb, const at::Tensor& skip) {
+  const int64_t n = B.size(1);
+  TORCH_CHECK(Bq.sizes() == B.sizes() && Bq.stride(1) == 1 && B.stride(1) == 1, "sbr16_bq_out: shapes");
+  evx_sbr16_bq(B.data_ptr<float>(), (int)B.size(0), (int)n, B.stride(0), perm.data_ptr<int>(), Q.data_ptr<float>(), Bq.data_ptr<float>(),
+               Bq.stride(0), (int)sb, cur_stream(), skip.data_ptr<int>());
+}
+
+void sbr_damping_out(const at::Tensor& X2, const at::Tensor& V, double tau, at::Tensor& alpha, at::Tensor& work, const at::Tensor& skip) {
+  const int64_t n = X2.size(0);
+  TORCH_CHECK(V.numel() >= n * 8 && work.numel() >= n * 24 && alpha.numel() >= 1, "sbr_damping_out: shapes");
+  evx_sbr_damping(X2.data_ptr<float>(), (int)n, X2.stride(0), V.data_ptr<float>(), work.data_ptr<float>(), (float)tau,
+                  alpha.data_ptr<float>(), cur_stream(), skip.data_ptr<int>());
+}
+
+void sbr_dev_prep(const at::Tensor& X, const at::Tensor& X2, const at::Tensor& X3, const at::Tensor& alpha, at::Tensor& P, at::Tensor& MT,
+                  const at::Tensor& ctrl) {
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&X, &X2, &X3, &P, &MT}) {
+    CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t);
+    TORCH_CHECK(t->sizes() == X.sizes(), "sbr_dev_prep: n×n");
+  }
+  TORCH_CHECK(ctrl.scalar_type() == at::kInt && ctrl.numel() >= 8 && alpha.numel() >= 1, "sbr_dev_prep: ctrl int32[8]");
+  evx_sbr_dev_prep(X.data_ptr<float>(), X2.data_ptr<float>(), X3.data_ptr<float>(), (int)X.size(0), alpha.data_ptr<float>(),
+                   P.data_ptr<float>(), MT.data_ptr<float>(), ctrl.data_ptr<int>(), cur_stream());
+}
+
+void sbr_dev_copy(const at::Tensor& src, at::Tensor& dst, const at::Tensor& skip) {
+  CHECK_CONTIG(src); CHECK_CONTIG(dst);
+  TORCH_CHECK(src.numel() == dst.numel() && src.scalar_type() == at::kFloat && dst.scalar_type() == at::kFloat &&
+                  reinterpret_cast<uintptr_t>(src.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(dst.data_ptr()) % 16 == 0,
+              "sbr_dev_copy: 16-byte aligned float32 of one size");
+  evx_sbr_dev_copy(src.data_ptr<float>(), dst.data_ptr<float>(), src.numel(), skip.data_ptr<int>(), cur_stream());
+}
+
+void sbr_dev_ctrl(const at::Tensor& part, int64_t nparts, int64_t j, int64_t K, at::Tensor& hist, at::Tensor& alpha, at::Tensor& theta,
+                  at::Tensor& ctrl, at::Tensor& st, std::vector<double> prm, int64_t ns_iters, const at::Tensor& A, at::Tensor& w_out,
+                  at::Tensor& eig_stats, at::Tensor& w_init, at::Tensor& log, at::Tensor& log_count) {
+  TORCH_CHECK(log.scalar_type() == at::kDouble && log.is_contiguous() && log_count.scalar_type() == at::kInt, "sbr_dev_ctrl: log");
+  TORCH_CHECK(prm.size() == 5, "sbr_dev_ctrl: params [tol, ns_kappa, damp_kappa, t4_kappa, near_only]");
+  TORCH_CHECK(hist.scalar_type() == at::kDouble && hist.numel() >= 4 * (K + 1) && ctrl.numel() >= 8 * K && alpha.numel() >= K + 1 &&
+                  theta.numel() >= K && st.numel() >= 8 && part.numel() >= 4 * nparts, "sbr_dev_ctrl: buffers");
+  float p6[6] = {(float)prm[0], (float)prm[1], (float)prm[2], (float)prm[3], (float)prm[4], 0.f};
+  evx_sbr_dev_ctrl(part.data_ptr<double>(), (int)nparts, (int)j, (int)K, hist.data_ptr<double>(), alpha.data_ptr<float>(),
+                   theta.data_ptr<float>(), ctrl.data_ptr<int>(), st.data_ptr<int>(), p6, (int)ns_iters, A.data_ptr<float>(), A.stride(0),
+                   (int)A.size(0), w_out.data_ptr<float>(), eig_stats.data_ptr<double>(), w_init.data_ptr<float>(),
+                   log.data_ptr<double>(), (int)(log.numel() / 4), log_count.data_ptr<int>(), cur_stream());
 }
 
 std::vector<at::Tensor> argsort_f32(const at::Tensor& keys, int64_t descending) {
@@ -986,7 +1085,15 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("classic_eval(Tensor X, int func, float a, float b, float c) -> Tensor");
   m.def("gemm_f32(Tensor A, int a_rc, Tensor? a_gather, Tensor? a_sub, int a_sub_on_k, Tensor? a_kscale, Tensor? a_kw, Tensor? a_sscale, int a_sscale_inv, Tensor B, int b_rc, Tensor? b_gather, Tensor? b_sub, int b_sub_on_k, Tensor? b_kscale, Tensor? b_kw, Tensor? b_sscale, int b_sscale_inv, Tensor? alpha_ptr, Tensor? bias_n, float beta, Tensor? Cin, int M, int N, int K, int splits, float alpha) -> Tensor");
   m.def("gemm_ks(Tensor A, int a_kc, Tensor B, int b_kc, int M, int N, int K, int mode, float alpha, Tensor? alpha_ptr, Tensor? bias_n, float beta, Tensor? Cin, Tensor? skip, Tensor? a_sub_k=None) -> Tensor");
-  m.def("gemm_ks_out(Tensor A, int a_kc, Tensor B, int b_kc, int M, int N, int K, int mode, float alpha, Tensor? alpha_ptr, Tensor? bias_n, float beta, Tensor? Cin, Tensor(a!) out, Tensor? skip, Tensor? a_sub_k=None) -> ()");
+  m.def("gemm_ks_out(Tensor A, int a_kc, Tensor B, int b_kc, int M, int N, int K, int mode, float alpha, Tensor? alpha_ptr, Tensor? bias_n, float beta, Tensor? Cin, Tensor(a!) out, Tensor? skip, Tensor? a_sub_k=None, Tensor? sel=None, Tensor? A2=None, float alpha2=0., Tensor(b!)? C2=None, Tensor(c!)? stat_part=None) -> ()");
+  m.def("gemm_ks_grid(int M, int N, int mode) -> int");
+  m.def("sbr16_block_out(Tensor A, int shift, int sweeps, int sb, Tensor(a!) perm, Tensor(b!) Q, Tensor(c!) dq, Tensor skip) -> ()");
+  m.def("sbr16_far_out(Tensor A, Tensor perm, Tensor Q, Tensor dq, Tensor stats, float thr_fac, Tensor theta, Tensor(a!) X, int sb, Tensor skip) -> ()");
+  m.def("sbr16_bq_out(Tensor B, Tensor perm, Tensor Q, Tensor(a!) Bq, int sb, Tensor skip) -> ()");
+  m.def("sbr_damping_out(Tensor X2, Tensor V, float tau, Tensor(a!) alpha, Tensor(b!) work, Tensor skip) -> ()");
+  m.def("sbr_dev_prep(Tensor X, Tensor X2, Tensor X3, Tensor alpha, Tensor(a!) P, Tensor(b!) MT, Tensor ctrl) -> ()");
+  m.def("sbr_dev_copy(Tensor src, Tensor(a!) dst, Tensor skip) -> ()");
+  m.def("sbr_dev_ctrl(Tensor part, int nparts, int j, int K, Tensor(a!) hist, Tensor(b!) alpha, Tensor(c!) theta, Tensor(d!) ctrl, Tensor(e!) st, float[] prm, int ns_iters, Tensor A, Tensor(f!) w_out, Tensor(g!) eig_stats, Tensor(h!) w_init, Tensor(i!) log, Tensor(j!) log_count) -> ()");
   m.def("gemm_ks_set_tile(int t) -> ()");
   m.def("lsmop_g(Tensor X, int[] start, int[] sublen, int[] func, int nk, int cosine) -> Tensor");
   m.def("cma_delta_gemv(Tensor M, Tensor mean, Tensor dm, float cm) -> Tensor[]");
@@ -1019,6 +1126,7 @@ TORCH_LIBRARY_IMPL(evoxmi, CompositeExplicitAutograd, m) {
   m.impl("stochastic_ranking", &stochastic_ranking);
   m.impl("gemm_set_config", &gemm_set_config);
   m.impl("gemm_ks_set_tile", &gemm_ks_set_tile);
+  m.impl("gemm_ks_grid", &gemm_ks_grid);
 }
 
 TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
@@ -1040,6 +1148,13 @@ TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
   m.impl("gemm_f32", &gemm_f32);
   m.impl("gemm_ks", &gemm_ks_new);
   m.impl("gemm_ks_out", &gemm_ks_out);
+  m.impl("sbr16_block_out", &sbr16_block_out);
+  m.impl("sbr16_far_out", &sbr16_far_out);
+  m.impl("sbr16_bq_out", &sbr16_bq_out);
+  m.impl("sbr_damping_out", &sbr_damping_out);
+  m.impl("sbr_dev_prep", &sbr_dev_prep);
+  m.impl("sbr_dev_copy", &sbr_dev_copy);
+  m.impl("sbr_dev_ctrl", &sbr_dev_ctrl);
   m.impl("pso_update", &pso_update);
   m.impl("lsmop_g", &lsmop_g);
   m.impl("cma_delta_gemv", &cma_delta_gemv);

@@ -45,10 +45,21 @@ struct EvxGemmKs {
   int64_t ldcin;
   const int32_t* skip;
   const float* a_sub_k;  // A(m, k) − a_sub_k[k] before the product (K-contiguous A only), may be null
+  // device-selected variant: when *sel != 0 the kernel uses A2 (if non-null), alpha2 and C2 (if
+  // non-null) instead of A, alpha, C (the eigensolver's fixed schedule picks Taylor order /
+  // Newton–Schulz output on the device)
+  const int32_t* sel;
+  const float* A2;
+  float alpha2;
+  float* C2;
+  // symmetric mode: per-workgroup stats partials [Σ offdiag², Σ diag², min diag, max diag]
+  // (double[4] per workgroup, sbr_stats_final layout), may be null
+  double* stat_part;
   int c_vec4;
   int tiles_m, tiles_n;  // set by the launcher
 };
 void evx_gemm_ks(const EvxGemmKs& a, hipStream_t s);
+int evx_gemm_ks_grid(int M, int N, int mode);  // workgroups of a launch (stat_part length)
 int evx_gemm_ks_tile(int M, int N, int mode);
 void evx_gemm_ks_set_tile(int t);
 void evx_cma_center_rows(const float* pop, int64_t ldp, const int32_t* rows, const float* mean, const float* sigma, const float* w, int K,
@@ -137,12 +148,16 @@ int evx_sbr_symstats_parts(int n);
 int evx_sbr16_nblocks(int n, int sb);
 int evx_sbr16_max_n();
 void evx_sbr_taylor4_prep(const float* X, const float* X2, int n, const float* alpha, float* P, float* M, hipStream_t s, int mt = 0);
-void evx_sbr_damping(const float* X2, int n, int64_t ldx, const float* V, float* work, float tau, float* alpha, hipStream_t s);
-void evx_sbr16_block(const float* A, int n, int64_t lda, int shift, int sweeps, int* perm, float* Q, float* dq, int sb, hipStream_t s);
+void evx_sbr_damping(const float* X2, int n, int64_t ldx, const float* V, float* work, float tau, float* alpha, hipStream_t s,
+                     const int* skip = nullptr);
+void evx_sbr16_block(const float* A, int n, int64_t lda, int shift, int sweeps, int* perm, float* Q, float* dq, int sb, hipStream_t s,
+                     const int* skip = nullptr);
 void evx_sbr16_far(const float* A, int n, int64_t lda, const int* perm, const float* Q, const float* dq, const double* stats,
-                   float thr_fac, float theta, float* X, int64_t ldx, int sb, hipStream_t s);
+                   float thr_fac, float theta, float* X, int64_t ldx, int sb, hipStream_t s,
+                   const float* theta_ptr = nullptr, const int* skip = nullptr);
 void evx_sbr16_bq(const float* B, int rows, int n, int64_t ldb, const int* perm, const float* Q, float* Bq, int64_t ldq, int sb,
-                  hipStream_t s);
+                  hipStream_t s,
+                     const int* skip = nullptr);
 void evx_sbr_symstats(const float* T, int n, int64_t ldt, float* A, int64_t lda, double* part, double* out, hipStream_t s);
 void evx_sbr_taylor_prep(const float* X, const float* X2, const float* X3, int n, const float* alpha, float* P, float* M,
                          hipStream_t s, int mt = 0);
@@ -159,3 +174,11 @@ void evx_hv_contrib(const float* S, const float* P, const int32_t* count, const 
 // batched linear-kernel GP hyper-parameter fits (gp_fit.hip, IM-MOEA)
 void evx_linear_gp_fit(const double* a, const double* b, const double* c, const double* n, int64_t models, int steps, double lr,
                        float* v, float* s2, hipStream_t s);
+
+// device-controlled SBR schedule (eigh_sbr_dev.hip)
+void evx_sbr_dev_prep(const float* X, const float* X2, const float* X3, int n, const float* alpha, float* P, float* MT, const int* ctrl,
+                      hipStream_t s);
+void evx_sbr_dev_copy(const float* src, float* dst, int64_t n, const int* skip, hipStream_t s);
+void evx_sbr_dev_ctrl(const double* part, int nparts, int j, int K, double* hist, float* alpha, float* theta, int* ctrl, int* st,
+                      const float* prm6, int ns_iters, const float* A, int64_t lda, int n, float* w_out, double* eig_stats, float* w_init,
+                      double* log, int log_len, int* log_count, hipStream_t s);

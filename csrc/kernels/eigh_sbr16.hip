@@ -39,7 +39,8 @@ __device__ __forceinline__ float sort_key(float v) { return isnan(v) ? INFINITY 
 // ------------------------------------------------------------------ 1. ranks → shifted perm
 // 64 indices per workgroup, the 4 waves each count over a quarter of the keys
 __global__ void __launch_bounds__(256) sbr16_rank_kernel(const float* __restrict__ A, int n, int64_t lda, int shift,
-                                                         int* __restrict__ perm) {
+                                                         int* __restrict__ perm, const int* __restrict__ skip) {
+  if (skip && *skip) return;
   __shared__ __attribute__((aligned(16))) float key[kRankMax + 16];
   __shared__ int part[4][64];
   const int np = (n + 15) & ~15;  // padded with +inf: never below a real key (NaN keys are +inf too, ties by index)
@@ -102,7 +103,8 @@ __device__ __forceinline__ float3 rot16(float app, float aqq, float apq) {
 template <int SB>
 __global__ void __launch_bounds__(SB * SB / 4) sbr16_block_kernel(const float* __restrict__ A, int n, int64_t lda,
                                                                   const int* __restrict__ perm, int sweeps, float* __restrict__ Q_out,
-                                                                  float* __restrict__ dq_out) {
+                                                                  float* __restrict__ dq_out, const int* __restrict__ skip) {
+  if (skip && *skip) return;
   constexpr int SP = SB + 1, NT = SB * SB / 4;
   __shared__ float S[SB * SP];
   __shared__ float Qm[SB * SP];
@@ -199,7 +201,10 @@ template <int SB>
 __global__ void __launch_bounds__(256) sbr16_far_kernel(const float* __restrict__ A, int n, int64_t lda,
                                                         const int* __restrict__ perm, const float* __restrict__ Q,
                                                         const float* __restrict__ dq, const double* __restrict__ stats,
-                                                        float thr_fac, float theta, float* __restrict__ X, int64_t ldx) {
+                                                        float thr_fac, float theta, float* __restrict__ X, int64_t ldx,
+                                                        const float* __restrict__ theta_ptr, const int* __restrict__ skip) {
+  if (skip && *skip) return;
+  if (theta_ptr) theta = *theta_ptr;  // device-side local-threshold switch (ops/sbr_device.py)
   __shared__ __attribute__((aligned(16))) float G[TL * TP];
   __shared__ __attribute__((aligned(16))) float Qk[TL * TP];
   __shared__ __attribute__((aligned(16))) float Ql[TL * TP];
@@ -300,7 +305,8 @@ __global__ void __launch_bounds__(256) sbr16_far_kernel(const float* __restrict_
 template <int SB>
 __global__ void __launch_bounds__(256) sbr16_bq_kernel(const float* __restrict__ B, int rows, int n, int64_t ldb,
                                                        const int* __restrict__ perm, const float* __restrict__ Q,
-                                                       float* __restrict__ Bq, int64_t ldq) {
+                                                       float* __restrict__ Bq, int64_t ldq, const int* __restrict__ skip) {
+  if (skip && *skip) return;
   __shared__ __attribute__((aligned(16))) float G[TL * TP];
   __shared__ __attribute__((aligned(16))) float Ql[TL * TP];
   __shared__ int pl[TL];
@@ -351,7 +357,9 @@ __global__ void __launch_bounds__(256) sbr16_bq_kernel(const float* __restrict__
 // row of Vout = −X²·Vin (n×8, row-major), then one workgroup forms
 // α = min(1, τ / sqrt(max_j ‖V3_j‖ / ‖V2_j‖)).  Replaces ~15 small library launches.
 __global__ void __launch_bounds__(256) sbr_power_step_kernel(const float* __restrict__ X2, int n, int64_t ldx,
-                                                             const float* __restrict__ Vin, float* __restrict__ Vout) {
+                                                             const float* __restrict__ Vin, float* __restrict__ Vout,
+                                                             const int* __restrict__ skip) {
+  if (skip && *skip) return;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= n) return;
   const float* x = X2 + (int64_t)row * ldx;
@@ -377,7 +385,8 @@ __global__ void __launch_bounds__(256) sbr_power_step_kernel(const float* __rest
 }
 
 __global__ void __launch_bounds__(256) sbr_damping_final_kernel(const float* __restrict__ V2, const float* __restrict__ V3, int n,
-                                                                float tau, float* __restrict__ alpha) {
+                                                                float tau, float* __restrict__ alpha, const int* __restrict__ skip) {
+  if (skip && *skip) return;
   __shared__ float red[2][8][4];
   float s2[8] = {}, s3[8] = {};
   for (int j = threadIdx.x; j < n; j += blockDim.x) {
@@ -432,41 +441,44 @@ __global__ void __launch_bounds__(256) sbr_taylor4_prep_kernel(const float* __re
 int evx_sbr16_nblocks(int n, int sb) { return (n + sb - 1) / sb; }
 int evx_sbr16_max_n() { return kRankMax; }
 
-void evx_sbr16_block(const float* A, int n, int64_t lda, int shift, int sweeps, int* perm, float* Q, float* dq, int sb, hipStream_t s) {
-  sbr16_rank_kernel<<<(n + 63) / 64, 256, 0, s>>>(A, n, lda, shift, perm);
+void evx_sbr16_block(const float* A, int n, int64_t lda, int shift, int sweeps, int* perm, float* Q, float* dq, int sb, hipStream_t s,
+                     const int* skip) {
+  sbr16_rank_kernel<<<(n + 63) / 64, 256, 0, s>>>(A, n, lda, shift, perm, skip);
   if (sb == 32)
-    sbr16_block_kernel<32><<<(n + 31) / 32, 256, 0, s>>>(A, n, lda, perm, sweeps, Q, dq);
+    sbr16_block_kernel<32><<<(n + 31) / 32, 256, 0, s>>>(A, n, lda, perm, sweeps, Q, dq, skip);
   else
-    sbr16_block_kernel<16><<<(n + 15) / 16, 64, 0, s>>>(A, n, lda, perm, sweeps, Q, dq);
+    sbr16_block_kernel<16><<<(n + 15) / 16, 64, 0, s>>>(A, n, lda, perm, sweeps, Q, dq, skip);
 }
 
 void evx_sbr16_far(const float* A, int n, int64_t lda, const int* perm, const float* Q, const float* dq, const double* stats,
-                   float thr_fac, float theta, float* X, int64_t ldx, int sb, hipStream_t s) {
+                   float thr_fac, float theta, float* X, int64_t ldx, int sb, hipStream_t s, const float* theta_ptr,
+                   const int* skip) {
   const int nt = (n + TL - 1) / TL;
   if (sb == 32)
-    sbr16_far_kernel<32><<<dim3(nt, nt), 256, 0, s>>>(A, n, lda, perm, Q, dq, stats, thr_fac, theta, X, ldx);
+    sbr16_far_kernel<32><<<dim3(nt, nt), 256, 0, s>>>(A, n, lda, perm, Q, dq, stats, thr_fac, theta, X, ldx, theta_ptr, skip);
   else
-    sbr16_far_kernel<16><<<dim3(nt, nt), 256, 0, s>>>(A, n, lda, perm, Q, dq, stats, thr_fac, theta, X, ldx);
+    sbr16_far_kernel<16><<<dim3(nt, nt), 256, 0, s>>>(A, n, lda, perm, Q, dq, stats, thr_fac, theta, X, ldx, theta_ptr, skip);
 }
 
 void evx_sbr16_bq(const float* B, int rows, int n, int64_t ldb, const int* perm, const float* Q, float* Bq, int64_t ldq, int sb,
-                  hipStream_t s) {
+                  hipStream_t s, const int* skip) {
   const int nt = (n + TL - 1) / TL;
   if (sb == 32)
-    sbr16_bq_kernel<32><<<dim3(nt, (rows + TL - 1) / TL), 256, 0, s>>>(B, rows, n, ldb, perm, Q, Bq, ldq);
+    sbr16_bq_kernel<32><<<dim3(nt, (rows + TL - 1) / TL), 256, 0, s>>>(B, rows, n, ldb, perm, Q, Bq, ldq, skip);
   else
-    sbr16_bq_kernel<16><<<dim3(nt, (rows + TL - 1) / TL), 256, 0, s>>>(B, rows, n, ldb, perm, Q, Bq, ldq);
+    sbr16_bq_kernel<16><<<dim3(nt, (rows + TL - 1) / TL), 256, 0, s>>>(B, rows, n, ldb, perm, Q, Bq, ldq, skip);
 }
 
-void evx_sbr_damping(const float* X2, int n, int64_t ldx, const float* V, float* work, float tau, float* alpha, hipStream_t s) {
+void evx_sbr_damping(const float* X2, int n, int64_t ldx, const float* V, float* work, float tau, float* alpha, hipStream_t s,
+                     const int* skip) {
   float* V1 = work;
   float* V2 = work + (int64_t)n * 8;
   float* V3 = work + (int64_t)n * 16;
   const int g = (n + 3) / 4;
-  sbr_power_step_kernel<<<g, 256, 0, s>>>(X2, n, ldx, V, V1);
-  sbr_power_step_kernel<<<g, 256, 0, s>>>(X2, n, ldx, V1, V2);
-  sbr_power_step_kernel<<<g, 256, 0, s>>>(X2, n, ldx, V2, V3);
-  sbr_damping_final_kernel<<<1, 256, 0, s>>>(V2, V3, n, tau, alpha);
+  sbr_power_step_kernel<<<g, 256, 0, s>>>(X2, n, ldx, V, V1, skip);
+  sbr_power_step_kernel<<<g, 256, 0, s>>>(X2, n, ldx, V1, V2, skip);
+  sbr_power_step_kernel<<<g, 256, 0, s>>>(X2, n, ldx, V2, V3, skip);
+  sbr_damping_final_kernel<<<1, 256, 0, s>>>(V2, V3, n, tau, alpha, skip);
 }
 
 void evx_sbr_taylor4_prep(const float* X, const float* X2, int n, const float* alpha, float* P, float* M, hipStream_t s, int mt) {

@@ -1,0 +1,219 @@
+// Device-controlled schedule of the sorted-block-refinement eigensolver (K4, round 3).
+//
+// The host-driven solver (evoxmi/ops/sbr.py:eigh_warm) reads the convergence statistics
+// back after every iteration (or once per planned solve) to choose the next iteration's
+// variant — Newton–Schulz or not, damping, far step, Taylor order, local threshold — and
+// when to stop.  That split every CMA-ES generation into graph segments around a host
+// phase.  Here the same decisions run on the device: the solve is a fixed schedule of K
+// iterations captured once into the generation's graph, every kernel of an iteration reads
+// a control word and returns at once when its variant is off (or the solve has converged),
+// and one single-workgroup kernel per iteration (sbr_dev_ctrl_kernel) reduces the stats
+// partials that the Bᵀ C B GEMM wrote in its epilogue and writes the next iteration's
+// control words.  No host read, no plan, nothing outside the checkpointed state.
+//
+// Control words per iteration j (int32[8]):
+//   0 skip_all   1 skip_far   2 skip_damp   3 skip_x3 (order 4)   4 sel6 (order 6)
+//   5 skip_ns    6 sel_ns (Bq·V lands in the Newton–Schulz input)   7 skip_copy (near-only: Bq → B)
+// Persistent words st[8]: 0 stopped, 1 fallback (diverged), 2 refinement iterations run,
+//   3 last_far, 4 theta sticky, 5 keep (0 ⇒ restore the warm-start basis), 6 converged.
+#include "evoxmi_common.h"
+#include <float.h>
+#include <math.h>
+
+namespace {
+
+struct SbrDevParams {
+  float tol, ns_kappa, damp_kappa, t4_kappa, near_only;
+  int ns_iters;
+};
+
+__device__ __forceinline__ void rel_kappa(const double* h, double& r, double& k) {
+  const double off = fmax(h[0], 0.0), dg = h[1], mn = h[2], mx = h[3];
+  r = dg > 0.0 ? sqrt(off / dg) : (double)NAN;
+  k = mx > mn ? sqrt(off) / (mx - mn) : (double)INFINITY;
+}
+
+// Taylor operands of exp(αX) for the order the control word selects (sel6), with M of
+// exp(−αX) (the transposed product, ops/sbr.py:expm_t_device)
+__global__ void __launch_bounds__(256) sbr_dev_prep_kernel(const float* __restrict__ X, const float* __restrict__ X2,
+                                                           const float* __restrict__ X3, int n, const float* __restrict__ alpha,
+                                                           float* __restrict__ P, float* __restrict__ MT, const int* __restrict__ ctrl) {
+  if (ctrl[1]) return;
+  const bool six = ctrl[4] != 0;
+  const float a = alpha[0], a2 = a * a, a3 = a2 * a;
+  const int64_t total = (int64_t)n * n;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = e / n, j = e - i * n;
+    const float x = a * X[e], x2 = a2 * X2[e];
+    const float id = i == j ? 1.f : 0.f;
+    if (six) {
+      const float x3 = a3 * X3[e];
+      P[e] = a3 * (x * (1.f / 24.f) + x2 * (1.f / 120.f) + x3 * (1.f / 720.f));
+      MT[e] = id - x + 0.5f * x2 - x3 * (1.f / 6.f);
+    } else {
+      P[e] = a2 * (x * (1.f / 6.f) + x2 * (1.f / 24.f));
+      MT[e] = id - x + 0.5f * x2;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) sbr_dev_copy_kernel(const float* __restrict__ src, float* __restrict__ dst, int64_t n,
+                                                           const int* __restrict__ skip) {
+  if (skip && *skip) return;
+  const int64_t n4 = n / 4;
+  const float4* s4 = reinterpret_cast<const float4*>(src);
+  float4* d4 = reinterpret_cast<float4*>(dst);
+  const int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x, stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e = g; e < n4; e += stride) d4[e] = s4[e];
+  for (int64_t e = 4 * n4 + g; e < n; e += stride) dst[e] = src[e];
+}
+
+// j = −1: the initial Bᵀ C B; j ≥ 0: after iteration j.  One workgroup.
+__global__ void __launch_bounds__(256) sbr_dev_ctrl_kernel(const double* __restrict__ part, int nparts, int j, int K,
+                                                           double* __restrict__ hist, float* __restrict__ alpha,
+                                                           float* __restrict__ theta, int* __restrict__ ctrl, int* __restrict__ st,
+                                                           SbrDevParams prm, const float* __restrict__ A, int64_t lda, int n,
+                                                           float* __restrict__ w_out, double* __restrict__ eig_stats,
+                                                           float* __restrict__ w_init, double* __restrict__ log, int log_len,
+                                                           int* __restrict__ log_count) {
+  __shared__ double s[4][256];
+  __shared__ int s_keep;
+  const int t = threadIdx.x;
+  const bool executed = j < 0 || ctrl[8 * j] == 0;
+  double* hj1 = hist + 4 * (j + 1);
+  if (executed) {
+    double off = 0.0, dg = 0.0, mn = DBL_MAX, mx = -DBL_MAX;
+    for (int i = t; i < nparts; i += 256) {
+      off += part[4 * i];
+      dg += part[4 * i + 1];
+      mn = fmin(mn, part[4 * i + 2]);
+      mx = fmax(mx, part[4 * i + 3]);
+    }
+    s[0][t] = off;
+    s[1][t] = dg;
+    s[2][t] = mn;
+    s[3][t] = mx;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if (t < o) {
+        s[0][t] += s[0][t + o];
+        s[1][t] += s[1][t + o];
+        s[2][t] = fmin(s[2][t], s[2][t + o]);
+        s[3][t] = fmax(s[3][t], s[3][t + o]);
+      }
+      __syncthreads();
+    }
+    if (t < 4) hj1[t] = s[t][0];
+  } else if (t < 4) {
+    hj1[t] = hist[4 * j + t];
+  }
+  if (j < 0) {  // the warm-start diagonal: the result if the refinement has to be abandoned
+    for (int i = t; i < n; i += 256) w_init[i] = A[(int64_t)i * lda + i];
+  }
+  __syncthreads();
+  if (t == 0) {
+    if (j < 0) {
+      st[0] = 0;  // stopped
+      st[1] = 0;  // fallback
+      st[2] = 0;  // iterations run
+      st[3] = 1;  // last_far
+      st[4] = 0;  // theta sticky
+      st[6] = 0;  // converged
+      alpha[0] = 1.f;
+    }
+    double r, k;
+    rel_kappa(hj1, r, k);
+    if (j >= 0 && executed && !st[0]) {
+      st[2] = j + 1;
+      double rp, kp;
+      rel_kappa(hist + 4 * j, rp, kp);
+      const bool far_j = ctrl[8 * j + 1] == 0;
+      if (!isfinite(r) || r > 1.5 * rp) {
+        st[0] = 1;  // diverged: stop, restore the warm-start basis at the end
+        st[1] = 1;
+      } else {
+        // an undamped far iteration close to the tolerance that barely helped: pairs in a
+        // cluster denser than the global threshold assumes — local threshold from now on
+        if (far_j && alpha[j + 1] >= 1.f && r < 100.0 * prm.tol && r > 0.6 * rp) st[4] = 1;
+        st[3] = far_j ? 1 : 0;
+      }
+    }
+    if (!st[0] && r <= prm.tol) {
+      st[0] = 1;
+      st[6] = 1;
+    }
+    const int nx = j + 1;
+    if (nx < K) {
+      int* c = ctrl + 8 * nx;
+      if (st[0]) {
+        c[0] = 1; c[1] = 1; c[2] = 1; c[3] = 1; c[4] = 0; c[5] = 1; c[6] = 0; c[7] = 1;
+      } else {
+        const float a_prev = alpha[nx];  // step size of the iteration just run (1 at the start)
+        const bool ns = nx < prm.ns_iters || a_prev < 1.f || k > prm.ns_kappa;
+        const bool damp = nx == 0 || k > prm.damp_kappa;
+        const bool far = !(nx > 0 && r <= prm.near_only * prm.tol && st[3]);
+        const bool six = !(k < prm.t4_kappa);
+        c[0] = 0;
+        c[1] = far ? 0 : 1;
+        c[2] = (far && damp) ? 0 : 1;
+        c[3] = (far && six) ? 0 : 1;
+        c[4] = six ? 1 : 0;
+        c[5] = (far && ns) ? 0 : 1;
+        c[6] = ns ? 1 : 0;
+        c[7] = far ? 1 : 0;
+        theta[nx] = st[4] ? 1.f : 0.f;
+        alpha[nx + 1] = 1.f;  // the damping kernel of iteration nx overwrites it when it runs
+      }
+    }
+    if (nx == K) {
+      const bool fb = st[1] != 0;
+      double rf, kf;
+      rel_kappa(fb ? hist : hist + 4 * K, rf, kf);
+      eig_stats[0] = rf;
+      eig_stats[1] = 0.0;
+      eig_stats[2] = (double)st[2];
+      eig_stats[3] = fb ? 1.0 : 0.0;
+      st[5] = fb ? 0 : 1;  // keep: the restore copy is skipped unless the refinement diverged
+      if (log && log_len > 0) {  // per-solve history ring (read by benches after the timed loop)
+        const int c = *log_count;
+        double* o = log + 4 * (int64_t)(c % log_len);
+        o[0] = eig_stats[0];
+        o[1] = eig_stats[1];
+        o[2] = eig_stats[2];
+        o[3] = eig_stats[3];
+        *log_count = c + 1;
+      }
+    }
+    s_keep = st[1] ? 0 : 1;
+  }
+  __syncthreads();
+  if (j + 1 == K) {
+    const bool keep = s_keep != 0;
+    for (int i = t; i < n; i += 256) w_out[i] = keep ? A[(int64_t)i * lda + i] : w_init[i];
+  }
+}
+
+}  // namespace
+
+void evx_sbr_dev_prep(const float* X, const float* X2, const float* X3, int n, const float* alpha, float* P, float* MT, const int* ctrl,
+                      hipStream_t s) {
+  const int64_t total = (int64_t)n * n;
+  int g = (int)((total + 255) / 256);
+  if (g > 2048) g = 2048;
+  sbr_dev_prep_kernel<<<g, 256, 0, s>>>(X, X2, X3, n, alpha, P, MT, ctrl);
+}
+
+void evx_sbr_dev_copy(const float* src, float* dst, int64_t n, const int* skip, hipStream_t s) {
+  int g = (int)((n / 4 + 255) / 256);
+  if (g < 1) g = 1;
+  if (g > 2048) g = 2048;
+  sbr_dev_copy_kernel<<<g, 256, 0, s>>>(src, dst, n, skip);
+}
+
+void evx_sbr_dev_ctrl(const double* part, int nparts, int j, int K, double* hist, float* alpha, float* theta, int* ctrl, int* st,
+                      const float* prm6, int ns_iters, const float* A, int64_t lda, int n, float* w_out, double* eig_stats, float* w_init,
+                      double* log, int log_len, int* log_count, hipStream_t s) {
+  SbrDevParams p{prm6[0], prm6[1], prm6[2], prm6[3], prm6[4], ns_iters};
+  sbr_dev_ctrl_kernel<<<1, 256, 0, s>>>(part, nparts, j, K, hist, alpha, theta, ctrl, st, p, A, lda, n, w_out, eig_stats, w_init, log,
+                                        log_len, log_count);
+}

@@ -32,6 +32,7 @@
 // (device-side control of the eigensolver's fixed iteration schedule, ops/sbr_device.py).
 #include "evoxmi_common.h"
 #include "evoxmi_launchers.h"
+#include <float.h>
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -114,6 +115,11 @@ __device__ __forceinline__ void decode_tile(int bid, int tiles_m, int tiles_n, i
 template <int TM, int TN, int KH, bool AKC, bool BKC, int MODE>
 __global__ void __launch_bounds__(256) gemm_ks_kernel(EvxGemmKs p) {
   if (p.skip && *p.skip) return;
+  if (p.sel && *p.sel) {
+    if (p.A2) p.A = p.A2;
+    p.alpha = p.alpha2;
+    if (p.C2) p.C = p.C2;
+  }
   constexpr int BM = 16 * TM, BN = 16 * TN;
   constexpr int KG = 16 * KH;  // k per group: KH float4 per lane and 16-row block
   // LDS row pitch ≡ 16 (mod 32) floats: the partial-tile writes (16 columns × 4 rows per
@@ -275,6 +281,10 @@ __global__ void __launch_bounds__(256) gemm_ks_kernel(EvxGemmKs p) {
   if (w < 2) park(w);
   __syncthreads();
   const float sc = p.alpha * (p.alpha_ptr ? p.alpha_ptr[0] : 1.f);
+  // stats partials (symmetric mode): mirrored tiles count twice, diagonal tiles their upper
+  // triangle twice and the diagonal once
+  double st_off = 0.0, st_dg = 0.0;
+  float st_mn = FLT_MAX, st_mx = -FLT_MAX;
   constexpr int NV4 = BM * BN / 4;
   constexpr int PER = (NV4 + 255) / 256;
   float4 out[PER];
@@ -330,6 +340,42 @@ __global__ void __launch_bounds__(256) gemm_ks_kernel(EvxGemmKs p) {
         }
       }
       out[v] = t;
+      if (MODE == 1 && p.stat_part && gr < p.M) {
+        const float vv[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+        for (int e2 = 0; e2 < 4; ++e2) {
+          const int cc = c + e2;
+          if (gc + e2 >= p.N) continue;
+          const double d2 = (double)vv[e2] * vv[e2];
+          if (tm != tn || row < cc) st_off += 2.0 * d2;
+          else if (row == cc) {
+            st_dg += d2;
+            st_mn = fminf(st_mn, vv[e2]);
+            st_mx = fmaxf(st_mx, vv[e2]);
+          }
+        }
+      }
+    }
+  }
+  if (MODE == 1 && p.stat_part) {
+    st_off = evx::wave_sum_d(st_off);
+    st_dg = evx::wave_sum_d(st_dg);
+    st_mn = evx::wave_min(st_mn);
+    st_mx = evx::wave_max(st_mx);
+    __shared__ double s_st[4][4];
+    if (lane == 0) {
+      s_st[w][0] = st_off;
+      s_st[w][1] = st_dg;
+      s_st[w][2] = st_mn;
+      s_st[w][3] = st_mx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double* o = p.stat_part + 4 * (int64_t)blockIdx.x;
+      o[0] = (s_st[0][0] + s_st[1][0]) + (s_st[2][0] + s_st[3][0]);
+      o[1] = (s_st[0][1] + s_st[1][1]) + (s_st[2][1] + s_st[3][1]);
+      o[2] = fmin(fmin(s_st[0][2], s_st[1][2]), fmin(s_st[2][2], s_st[3][2]));
+      o[3] = fmax(fmax(s_st[0][3], s_st[1][3]), fmax(s_st[2][3], s_st[3][3]));
     }
   }
   if (MODE == 0) return;
@@ -402,6 +448,13 @@ int evx_gemm_ks_tile(int M, int N, int mode) {
     }
   }
   return best;
+}
+
+int evx_gemm_ks_grid(int M, int N, int mode) {
+  const int t = evx_gemm_ks_tile(M, N, mode);
+  const int bm = 16 * t, bn = t == 8 ? 64 : 16 * t;
+  const int tm = (M + bm - 1) / bm, tn = (N + bn - 1) / bn;
+  return mode == 0 ? tm * tn : tm * (tm + 1) / 2;
 }
 
 void evx_gemm_ks(const EvxGemmKs& a, hipStream_t s) {

@@ -186,13 +186,20 @@ class CMAES(Algorithm):
                                                 state.count_iter.reshape(1).contiguous(), consts)
         eig_stats = state.eig_stats
         if config.get("eigh") == "sbr":
-            # converged solve (Jacobi hand-off + sorted-block refinement), host-orchestrated:
-            # a host phase between hipGraph segments under StdWorkflow(graph=True)
             np_ = jacobi.padded_size(d)
             C, Cp, _ = ops.cma_cov_pad(state.C.contiguous(), S.contiguous(), pc, a, float(self.c1), float(self.cmu), state.B.contiguous(), np_)
             # Cp[:d, :d] = triu(C) + triu(C, 1)ᵀ, the reference's symmetrisation (cma_es.py:193-195)
             with profiling.phase("eigh"):
-                w, Bn, eig_stats = host_phase(sbr_phase, Cp[:d, :d], state.B, self.__dict__.setdefault("_eig_plans", {}), out_like=(state.D, state.B, state.eig_stats))
+                if config.get("sbr_mode") == "device" and d % 4 == 0 and d <= 8192:
+                    # converged solve as a fixed device-controlled schedule: part of the
+                    # generation's graph, no host read (ops/sbr_device.py)
+                    from ....ops.sbr_device import eigh_device
+
+                    w, Bn, eig_stats = eigh_device(Cp[:d, :d], state.B)
+                else:
+                    # host-orchestrated solve: a host phase between hipGraph segments
+                    w, Bn, eig_stats = host_phase(sbr_phase, Cp[:d, :d], state.B, self.__dict__.setdefault("_eig_plans", {}),
+                                                  out_like=(state.D, state.B, state.eig_stats))
             B, D, BdivD = ops.cma_eig_out(Bn.contiguous(), w.contiguous(), d)
         else:
             np_ = jacobi.padded_size(d)
@@ -203,7 +210,7 @@ class CMAES(Algorithm):
         # (B/D)·Bᵀ is symmetric: upper tiles only
         invsqrtC = plain_nt(BdivD, B) if config.get("plain_gemm") == "blas" else mm(BdivD, B, tb=True, mode=1)
         return state.update(mean=mean, ps=ps, pc=pc, C=C, sigma=sigma.reshape(state.sigma.shape), B=B, D=D, invsqrtC=invsqrtC,
-                            count_eigen=state.count_eigen + 1, eig_stats=eig_stats)
+                            count_eigen=state.count_eigen + 1, eig_stats=eig_stats.clone())
 
     def _finish_tell(self, state, dm, S):
         if self._fused_epilogue_ok(state):

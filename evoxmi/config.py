@@ -39,6 +39,8 @@ KNOBS: Dict[str, Knob] = {
     "eigh": Knob("EVOXMI_EIGH", "sbr", str, "symmetric eigensolver for CMA-ES: 'sbr' (converged: Jacobi hand-off + sorted-block refinement, ops/sbr.py), 'jacobi' (fixed-sweep warm block Jacobi) or 'torch' (rocSOLVER)"),
     "eigh_tol": Knob("EVOXMI_EIGH_TOL", 1e-5, float, "sbr: target relative off-norm ‖offdiag(BᵀCB)‖_F / ‖diag‖_F of every decomposition"),
     "sbr_block": Knob("EVOXMI_SBR_BLOCK", 32, int, "sbr: near-pair block size — 32 or 16 (blocks in a shifted sorted order, eigh_sbr16.hip; 32 converges in fewer iterations on the bench matrices) or 64 (eigh_sbr.hip)"),
+    "sbr_mode": Knob("EVOXMI_SBR_MODE", "device", str, "sbr: 'device' — fixed device-controlled iteration schedule inside the generation's graph (ops/sbr_device.py, no host read); 'host' — host-driven iterations with planned solves as a host phase between graph segments (ops/sbr.py)"),
+    "sbr_device_iters": Knob("EVOXMI_SBR_DEVICE_ITERS", 8, int, "sbr device mode: refinement iterations in the fixed schedule (kernels of iterations past convergence return at once)"),
     "cma_fused": Knob("EVOXMI_CMA_FUSED", 1, int, "CMA-ES tell epilogue as the fused cmaes.hip kernels (0: reference-shaped torch ops)"),
     "plain_gemm": Knob("EVOXMI_PLAIN_GEMM", "evoxmi", str, "flagship GEMMs: 'evoxmi' (framework MFMA kernels, csrc/kernels/gemm_ks.hip) or 'blas' (hipBLASLt via torch, an A/B baseline only)"),
     "jacobi_sweeps": Knob("EVOXMI_JACOBI_SWEEPS", 2, int, "maximum warm-started Jacobi sweeps per decomposition (stops early once converged)"),

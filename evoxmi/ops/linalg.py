@@ -133,13 +133,20 @@ def plain_nt(A: torch.Tensor, B: torch.Tensor, alpha: float = 1.0, bias_n: Optio
 def mm(A: torch.Tensor, B: torch.Tensor, *, ta: bool = False, tb: bool = False, mode: int = 0, alpha: float = 1.0,
        alpha_ptr: Optional[torch.Tensor] = None, bias_n: Optional[torch.Tensor] = None, beta: float = 0.0,
        Cin: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
-       skip: Optional[torch.Tensor] = None, a_sub_k: Optional[torch.Tensor] = None) -> torch.Tensor:
+       skip: Optional[torch.Tensor] = None, a_sub_k: Optional[torch.Tensor] = None, sel: Optional[torch.Tensor] = None,
+       A2: Optional[torch.Tensor] = None, alpha2: Optional[float] = None, C2: Optional[torch.Tensor] = None,
+       stat_part: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``alpha·(*alpha_ptr)·op(A)·op(B) (+ bias_n) (+ beta·Cin)`` with ``op(X) = Xᵀ`` when
     ``ta`` / ``tb`` (transposes are layouts, never copies).  ``mode`` 1 / 2: the result is
     symmetric / skew-symmetric by construction of the caller (Bᵀ C B, X·X for skew X, …);
     only tiles with tm ≤ tn are computed and the rest mirrored.  ``out``: written in place.
     ``skip``: int32 device word — the kernel does nothing while it is non-zero.
     ``a_sub_k``: op(A)(m, k) − a_sub_k[k] (fused shift, ``op(A) = A`` only).
+    ``sel`` (device only, with ``out``): int32 device word; while non-zero the kernel uses
+    ``A2`` / ``alpha2`` / ``C2`` (when given; ``alpha2`` defaults to ``alpha``) instead of
+    ``A`` / ``alpha`` / ``out``.
+    ``stat_part`` (mode 1): float64 partials of [Σ offdiag², Σ diag², min diag, max diag] per
+    workgroup (``sbr_stats_final`` layout; length ``4·gemm_ks_grid``).
 
     On a GPU this is always the framework kernel (no vendor GEMM); shapes the kernel does
     not take (K % 4 ≠ 0 with a K-contiguous operand) go to :func:`gemm`."""
@@ -156,11 +163,14 @@ def mm(A: torch.Tensor, B: torch.Tensor, *, ta: bool = False, tb: bool = False, 
             args = (A_, int(a_kc), B_, int(b_kc), int(M), int(N), int(K), int(mode), float(alpha), alpha_ptr, bias_n,
                     float(beta), Cin)
             if out is not None:
-                _ext.ops().gemm_ks_out(*args, out, skip, a_sub_k)
+                a2 = float(alpha if alpha2 is None else alpha2)
+                _ext.ops().gemm_ks_out(*args, out, skip, a_sub_k, sel, A2, a2, C2, stat_part)
                 return out
+            if sel is not None or stat_part is not None:
+                raise ValueError("mm: sel / stat_part need out=")
             return _ext.ops().gemm_ks(*args, skip, a_sub_k)
-        if skip is not None:
-            raise ValueError("mm: skip needs a shape the gemm_ks kernel takes")
+        if skip is not None or sel is not None or stat_part is not None:
+            raise ValueError("mm: skip / sel / stat_part need a shape the gemm_ks kernel takes")
         Ao = Operand(A_, rc=ta, sub=a_sub_k, sub_on_k=a_sub_k is not None)
         C = gemm(Ao, Operand(B_, rc=not tb), M, N, K, alpha=alpha, alpha_ptr=alpha_ptr, bias_n=bias_n, beta=beta, Cin=Cin)
         if out is not None:

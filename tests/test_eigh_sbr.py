@@ -240,7 +240,10 @@ def test_cmaes_trajectories_sbr_vs_library_eigh():
     from evoxmi.workflows import StdWorkflow
 
     def traj(impl, seed):
-        with cfg.override(eigh=impl):
+        # a schedule long enough for the cold-start generations (≤ 12 iterations): this test
+        # pins every decomposition to the tolerance; the default schedule (8) caps the first
+        # two generations (tests/test_sbr_device_gpu.py covers the cap)
+        with cfg.override(eigh=impl, sbr_device_iters=16):
             center = (torch.rand(1000, generator=torch.Generator().manual_seed(1)) * 10 - 5).cuda()
             algo = CMAES(center_init=center, init_stdev=1.0, pop_size=10000)
             prob = Ellipsoid()

@@ -1,0 +1,101 @@
+"""Device-controlled SBR schedule (evoxmi/ops/sbr_device.py, csrc/kernels/eigh_sbr_dev.hip).
+
+The fixed schedule must reach the same tolerance as the host-driven solver, run the same
+number of refinement iterations (same decision rules, decided on the device), be bitwise
+reproducible eagerly and when replayed from a hipGraph, and — having no state outside the
+algorithm's State — make a checkpoint-resumed CMA-ES run bitwise identical to the
+uninterrupted one (the host planner's hidden iteration plans could not)."""
+import math
+
+import pytest
+import torch
+
+from evoxmi.ops import sbr, sbr_device
+
+from test_eigh_sbr import _cma_like, _offrel
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("gens", [4, 15, 40])
+def test_device_schedule_converges_like_host_driver(gens):
+    C, B = _cma_like(1000, gens, seed=gens, dev="cuda")
+    w, Bn, st = sbr_device.eigh_device(C, B, iters=16)
+    st = st.cpu()
+    assert float(st[0]) <= 1e-5 and float(st[3]) == 0.0, st
+    A = Bn.T.double() @ C.double() @ Bn.double()
+    assert _offrel(A) <= 2e-5
+    I = torch.eye(1000, device="cuda", dtype=torch.float64)
+    assert float(torch.linalg.matrix_norm(Bn.T.double() @ Bn.double() - I)) < 1e-3
+    ev = torch.linalg.eigvalsh(C.double())
+    assert float((torch.sort(w.double()).values - ev).abs().max()) < 5e-5
+    # the host driver (adaptive, no plans, no graphs) takes the same decisions
+    _, _, info = sbr.eigh_warm(C, B, sbr.SBRConfig(graphs=False, plan=False))
+    assert abs(int(st[2]) - info.refine_iters) <= 1, (int(st[2]), info.refine_iters)
+
+
+def test_device_schedule_bitwise_eager_and_graph_replay():
+    C, B = _cma_like(1000, 8, seed=2, dev="cuda")
+    ws = sbr_device.workspace(1000, C.device, sbr.SBRConfig(), 10)
+    w0, B0, s0 = (t.clone() for t in ws.solve(C, B))
+    w1, B1, s1 = (t.clone() for t in ws.solve(C, B))
+    assert torch.equal(B0, B1) and torch.equal(w0, w1) and torch.equal(s0, s1)
+    Cs, Bs = C.clone(), B.clone()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ws.solve(Cs, Bs)  # warm-up on the capture stream
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        out = ws.solve(Cs, Bs)
+    for _ in range(2):
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out[1], B0) and torch.equal(out[0], w0) and torch.equal(out[2], s0)
+
+
+def test_device_schedule_cap_reports_unconverged():
+    """A schedule too short for a cold start ends capped, not wrong: the basis is the
+    partially refined one (better than the warm start) and the stats say so."""
+    C, B = _cma_like(1000, 1, seed=1, dev="cuda")
+    A0 = B.T.double() @ C.double() @ B.double()
+    w, Bn, st = sbr_device.eigh_device(C, B, iters=2)
+    st = st.cpu()
+    A = Bn.T.double() @ C.double() @ Bn.double()
+    assert int(st[2]) == 2 and float(st[3]) == 0.0
+    assert _offrel(A) < _offrel(A0)
+    assert math.isclose(float(st[0]), _offrel(A), rel_tol=5e-2)
+
+
+def test_cmaes_device_mode_checkpoint_resume_is_bitwise(tmp_path):
+    from evoxmi import config
+    from evoxmi import random as rnd
+    from evoxmi.algorithms import CMAES
+    from evoxmi.core.checkpoint import load_state, save_state
+    from evoxmi.problems.numerical import CEC2022TestSuit
+    from evoxmi.workflows import StdWorkflow
+
+    def make():
+        center = (torch.rand(200, generator=torch.Generator().manual_seed(1)) * 160 - 80).cuda()
+        algo = CMAES(center_init=center, init_stdev=20.0, pop_size=2000)
+        return StdWorkflow(algo, CEC2022TestSuit.create(1), graph=True)
+
+    with config.override(eigh="sbr", sbr_mode="device", sbr_device_iters=12):
+        wf = make()
+        st = wf.init(rnd.PRNGKey(3, device=torch.device("cuda")))
+        for _ in range(4):
+            st = wf.step(st)
+        save_state(st, str(tmp_path / "ck.safetensors"))
+        for _ in range(4):
+            st = wf.step(st)
+        ref = st.get_child_state("algorithm")
+        wf2 = make()
+        wf2.init(rnd.PRNGKey(99, device=torch.device("cuda")))  # module tree only: the state comes from the file
+        st2 = load_state(str(tmp_path / "ck.safetensors"), map_location="cuda")
+        for _ in range(4):
+            st2 = wf2.step(st2)
+        got = st2.get_child_state("algorithm")
+    for k in ("B", "C", "mean", "sigma", "D"):
+        assert torch.equal(getattr(ref, k), getattr(got, k)), k
+    assert float(ref.eig_stats[0]) <= 1e-5
