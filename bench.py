@@ -35,6 +35,9 @@ def main():
     ap.add_argument("--profile-phases", action="store_true")
     ap.add_argument("--force-dist", action="store_true", help="run the distributed (sharded + RCCL) path even on one rank")
     ap.add_argument("--phase-steps", type=int, default=3, help="eager generations timed per phase after the timed loop (0: off)")
+    ap.add_argument("--simulate-rank", type=int, default=None,
+                    help="time rank R's share of a --world N step on this one GPU (collectives replaced by same-size local ops)")
+    ap.add_argument("--world", type=int, default=8, help="world size simulated by --simulate-rank")
     args = ap.parse_args()
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -46,7 +49,12 @@ def main():
     from evoxmi.workflows import StdWorkflow
     import torch.distributed as dist
 
-    rank, world, device = init_distributed(force=args.force_dist)
+    sim = args.simulate_rank is not None
+    if sim:
+        rank, world, device = 0, 1, torch.device("cuda", 0)
+        torch.cuda.set_device(device)
+    else:
+        rank, world, device = init_distributed(force=args.force_dist)
     if device.type != "cuda":
         print("bench.py needs a HIP device", file=sys.stderr)
     torch.manual_seed(0)
@@ -57,9 +65,15 @@ def main():
     use_graph = (not args.no_graph) and device.type == "cuda"
     wf = StdWorkflow(algo, prob, graph=use_graph)
     state = wf.init(key)
-    dist_on = world > 1 or args.force_dist
+    dist_on = (world > 1 or args.force_dist) and not sim
     if dist_on:
         state = wf.enable_distributed(state)
+    sim_ctx = None
+    if sim:
+        from evoxmi.parallel.context import SimulatedDistContext
+
+        sim_ctx = SimulatedDistContext(args.simulate_rank, args.world, algorithm=algo)
+        state = wf.enable_distributed(state, context=sim_ctx)
 
     def sync():
         if device.type == "cuda":
@@ -123,7 +137,7 @@ def main():
                 "model": "CMA-ES on CEC2022 F1 (shifted-rotated Zakharov)",
                 "global_batch": args.pop,
                 "seq_len": args.dim,
-                "parallelism": f"pop-shard{world}",
+                "parallelism": f"pop-shard{world}" if not sim else f"simulated-rank{args.simulate_rank}-of-{args.world}",
                 "pop_size": args.pop,
                 "dim": args.dim,
                 "hipgraph": use_graph,
@@ -132,6 +146,20 @@ def main():
         }
         if phases:
             out["phases_ms_eager"] = phases
+        if sim:
+            # one rank's share of an N-GPU step (the driver's --gpus 1 headline never sets this)
+            out["simulated"] = {
+                "rank": args.simulate_rank,
+                "world": args.world,
+                "rows_per_rank": -(-args.pop // args.world),
+                "collectives": "replaced by same-size local ops (wire time not included)",
+                "all_reduce_bytes_per_step": sim_ctx.bytes_all_reduce // max(1, args.steps + args.warmup + args.phase_steps),
+            }
+            if phases:
+                rep = phases.get("eigh", 0.0)
+                out["simulated"]["replicated_ms_eager"] = rep
+                out["simulated"]["sharded_ms_eager"] = round(phases.get("ask", 0.0) + phases.get("evaluate", 0.0) +
+                                                             phases.get("tell", 0.0) - rep, 4)
         if dev_hist.shape[0]:
             # every timed generation's decomposition (device-controlled schedule, read back
             # once after the timed loop): relative off-norm ‖offdiag(BᵀCB)‖/‖diag‖

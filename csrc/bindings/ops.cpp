@@ -8,6 +8,7 @@
 #include <c10/hip/HIPStream.h>
 #include <c10/core/DeviceGuard.h>
 #include <hip/hip_runtime.h>
+#include <cstring>
 
 #include "evoxmi_launchers.h"
 #include "../host/stochastic_ranking.h"
@@ -849,7 +850,8 @@ std::vector<at::Tensor> moead_parents(const at::Tensor& nb, const at::Tensor& ke
 // win given: output row s = offspring win[s] (regenerated) or pop[s] when win[s] < 0
 at::Tensor moead_variation(const at::Tensor& pop, const at::Tensor& p0, const at::Tensor& p1, const at::Tensor& kx, const at::Tensor& km,
                            const at::Tensor& lb, const at::Tensor& ub, double pro_c, double dis_c, double pro_m, double dis_m, int64_t nm,
-                           int64_t row0, int64_t rows, const c10::optional<at::Tensor>& win) {
+                           int64_t row0, int64_t rows, const c10::optional<at::Tensor>& win,
+                           const c10::optional<at::Tensor>& out_opt) {
   for (auto* t : {&pop, &lb, &ub}) { CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t); }
   for (auto* t : {&p0, &p1}) { CHECK_DEV(*t); CHECK_CONTIG(*t); TORCH_CHECK(t->scalar_type() == at::kInt, "parents must be int32"); }
   TORCH_CHECK(kx.scalar_type() == at::kLong && kx.numel() == 4 && kx.is_contiguous() && kx.is_cuda(), "kx must be int64[2][2] on device");
@@ -868,13 +870,76 @@ at::Tensor moead_variation(const at::Tensor& pop, const at::Tensor& p0, const at
   }
   TORCH_CHECK(row0 >= 0 && (win || row0 + R <= Np), "moead_variation: offspring rows out of range");
   c10::DeviceGuard g(pop.device());
-  auto out = at::empty({R, d}, pop.options());
+  at::Tensor out;
+  if (out_opt.has_value() && out_opt->defined()) {
+    out = *out_opt;
+    TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.is_contiguous() && out.numel() >= R * d,
+                "moead_variation: out must hold rows × d float32");
+  } else {
+    out = at::empty({R, d}, pop.options());
+  }
   if (R > 0 && d > 0)
     evx_moead_variation(pop.data_ptr<float>(), p0.data_ptr<int>(), p1.data_ptr<int>(), out.data_ptr<float>(), (int)R, (int)d, kx.data_ptr<int64_t>(),
                         km.data_ptr<int64_t>(), lb.data_ptr<float>(), ub.data_ptr<float>(), (float)pro_c, (float)dis_c, (float)pro_m, (float)dis_m,
                         (int)nm, cur_stream(), (int)row0, wp);
   return out;
 }
+
+// ---- owner-computes MOEA/D + IPC peer buffers (direct xGMI reads between the ranks of a node)
+void moead_halo_replace(at::Tensor& obj, const at::Tensor& off_obj, const at::Tensor& W, const at::Tensor& z, const at::Tensor& zmax,
+                        const at::Tensor& rowptr, const at::Tensor& owner, const at::Tensor& slots, int64_t func, at::Tensor& win_h) {
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&obj, &off_obj, &W, &z, &zmax}) {
+    CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t);
+  }
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&rowptr, &owner, &slots, &win_h}) {
+    CHECK_DEV(*t); CHECK_CONTIG(*t);
+    TORCH_CHECK(t->scalar_type() == at::kInt, "moead_halo_replace: int32 index tensors");
+  }
+  const int64_t M = obj.size(1);
+  TORCH_CHECK(M <= 16 && off_obj.size(1) == M && win_h.numel() >= slots.numel(), "moead_halo_replace: shapes");
+  evx_moead_halo_replace(obj.data_ptr<float>(), off_obj.data_ptr<float>(), W.data_ptr<float>(), z.data_ptr<float>(), zmax.data_ptr<float>(),
+                         rowptr.data_ptr<int>(), owner.data_ptr<int>(), slots.data_ptr<int>(), (int)slots.numel(), (int)M, (int)func,
+                         win_h.data_ptr<int>(), cur_stream());
+}
+
+void moead_halo_gather(at::Tensor& pop, const at::Tensor& slots, const at::Tensor& win_h, const at::Tensor& peer, const at::Tensor& starts) {
+  CHECK_DEV(pop); CHECK_F32(pop); CHECK_CONTIG(pop);
+  TORCH_CHECK(peer.is_cuda() && peer.scalar_type() == at::kLong && starts.is_cuda() && starts.scalar_type() == at::kInt &&
+                  starts.numel() == peer.numel() + 1, "moead_halo_gather: peer int64[world], starts int32[world + 1] on device");
+  evx_moead_halo_gather(pop.data_ptr<float>(), slots.data_ptr<int>(), win_h.data_ptr<int>(), (int)slots.numel(), peer.data_ptr<int64_t>(),
+                        starts.data_ptr<int>(), (int)peer.numel(), (int)pop.size(1), cur_stream());
+}
+
+// hipMalloc'd buffer (an allocation base, so its IPC handle maps exactly this tensor)
+at::Tensor ipc_alloc(int64_t numel, int64_t device) {
+  c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device));
+  void* p = nullptr;
+  TORCH_CHECK(hipMalloc(&p, std::max<int64_t>(numel, 1) * 4) == hipSuccess, "ipc_alloc: hipMalloc failed");
+  TORCH_CHECK(hipMemset(p, 0, std::max<int64_t>(numel, 1) * 4) == hipSuccess, "ipc_alloc: hipMemset failed");
+  return at::from_blob(p, {numel}, [](void* q) { (void)hipFree(q); },
+                       at::TensorOptions().dtype(at::kFloat).device(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device)));
+}
+
+at::Tensor ipc_handle(const at::Tensor& t) {
+  CHECK_DEV(t);
+  hipIpcMemHandle_t h;
+  TORCH_CHECK(hipIpcGetMemHandle(&h, t.data_ptr()) == hipSuccess, "ipc_handle: hipIpcGetMemHandle failed");
+  auto out = at::empty({(int64_t)sizeof(h)}, at::TensorOptions().dtype(at::kByte));
+  std::memcpy(out.data_ptr(), &h, sizeof(h));
+  return out;
+}
+
+int64_t ipc_open(const at::Tensor& handle, int64_t device) {
+  TORCH_CHECK(handle.numel() == (int64_t)sizeof(hipIpcMemHandle_t) && handle.scalar_type() == at::kByte, "ipc_open: handle bytes");
+  c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device));
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle.contiguous().data_ptr(), sizeof(h));
+  void* p = nullptr;
+  TORCH_CHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess) == hipSuccess, "ipc_open: hipIpcOpenMemHandle failed");
+  return (int64_t)(uintptr_t)p;
+}
+
+void ipc_close(int64_t ptr) { (void)hipIpcCloseMemHandle((void*)(uintptr_t)ptr); }
 
 std::vector<at::Tensor> moead_replace(const at::Tensor& pop_obj, const at::Tensor& off_obj, const at::Tensor& W, const at::Tensor& z,
                                       const at::Tensor& zmax, const at::Tensor& rowptr, const at::Tensor& owner, int64_t func) {
@@ -1103,7 +1168,13 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("cma_eig_out(Tensor Bp, Tensor w, int d) -> Tensor[]");
   m.def("nsga_select(Tensor rank, Tensor f, int N, int mask_pos) -> Tensor");
   m.def("moead_parents(Tensor nb, Tensor key) -> Tensor[]");
-  m.def("moead_variation(Tensor pop, Tensor p0, Tensor p1, Tensor kx, Tensor km, Tensor lb, Tensor ub, float pro_c, float dis_c, float pro_m, float dis_m, int nm, int row0=0, int rows=0, Tensor? win=None) -> Tensor");
+  m.def("moead_variation(Tensor pop, Tensor p0, Tensor p1, Tensor kx, Tensor km, Tensor lb, Tensor ub, float pro_c, float dis_c, float pro_m, float dis_m, int nm, int row0=0, int rows=0, Tensor? win=None, Tensor(a!)? out=None) -> Tensor");
+  m.def("moead_halo_replace(Tensor(a!) obj, Tensor off_obj, Tensor W, Tensor z, Tensor zmax, Tensor rowptr, Tensor owner, Tensor slots, int func, Tensor(b!) win_h) -> ()");
+  m.def("moead_halo_gather(Tensor(a!) pop, Tensor slots, Tensor win_h, Tensor peer, Tensor starts) -> ()");
+  m.def("ipc_alloc(int numel, int device) -> Tensor");
+  m.def("ipc_handle(Tensor t) -> Tensor");
+  m.def("ipc_open(Tensor handle, int device) -> int");
+  m.def("ipc_close(int ptr) -> ()");
   m.def("moead_replace(Tensor pop_obj, Tensor off_obj, Tensor W, Tensor z, Tensor zmax, Tensor rowptr, Tensor owner, int func) -> Tensor[]");
   m.def("moead_select_rows(Tensor pop, Tensor off, Tensor win) -> Tensor");
   m.def("sbr_stats(Tensor A) -> Tensor");
@@ -1127,6 +1198,9 @@ TORCH_LIBRARY_IMPL(evoxmi, CompositeExplicitAutograd, m) {
   m.impl("gemm_set_config", &gemm_set_config);
   m.impl("gemm_ks_set_tile", &gemm_ks_set_tile);
   m.impl("gemm_ks_grid", &gemm_ks_grid);
+  m.impl("ipc_alloc", &ipc_alloc);
+  m.impl("ipc_open", &ipc_open);
+  m.impl("ipc_close", &ipc_close);
 }
 
 TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
@@ -1149,6 +1223,9 @@ TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
   m.impl("gemm_ks", &gemm_ks_new);
   m.impl("gemm_ks_out", &gemm_ks_out);
   m.impl("sbr16_block_out", &sbr16_block_out);
+  m.impl("moead_halo_replace", &moead_halo_replace);
+  m.impl("moead_halo_gather", &moead_halo_gather);
+  m.impl("ipc_handle", &ipc_handle);
   m.impl("sbr16_far_out", &sbr16_far_out);
   m.impl("sbr16_bq_out", &sbr16_bq_out);
   m.impl("sbr_damping_out", &sbr_damping_out);

@@ -182,3 +182,9 @@ void evx_sbr_dev_copy(const float* src, float* dst, int64_t n, const int* skip, 
 void evx_sbr_dev_ctrl(const double* part, int nparts, int j, int K, double* hist, float* alpha, float* theta, int* ctrl, int* st,
                       const float* prm6, int ns_iters, const float* A, int64_t lda, int n, float* w_out, double* eig_stats, float* w_init,
                       double* log, int log_len, int* log_count, hipStream_t s);
+
+// owner-computes MOEA/D (moead.hip)
+void evx_moead_halo_replace(float* obj, const float* off_obj, const float* W, const float* z, const float* zmax, const int32_t* rowptr,
+                            const int32_t* owner, const int32_t* slots, int H, int M, int func, int32_t* win_h, hipStream_t s);
+void evx_moead_halo_gather(float* pop, const int32_t* slots, const int32_t* win_h, int H, const int64_t* peer, const int32_t* starts,
+                           int world, int d, hipStream_t s);

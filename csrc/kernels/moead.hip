@@ -274,6 +274,68 @@ __global__ void __launch_bounds__(256) select_rows_kernel(const float* __restric
   }
 }
 
+// Owner-computes MOEA/D (population-sharded): the replacement of only the slots a rank
+// must keep current (its halo: every neighbour of its own slots), in place on the
+// objective matrix (a slot reads and writes only its own row).
+__global__ void __launch_bounds__(256) halo_replace_kernel(float* __restrict__ obj, const float* __restrict__ off_obj,
+                                                           const float* __restrict__ W, const float* __restrict__ zp,
+                                                           const float* __restrict__ zmaxp, const int32_t* __restrict__ rowptr,
+                                                           const int32_t* __restrict__ owner, const int32_t* __restrict__ slots,
+                                                           int H, int M, int func, int32_t* __restrict__ win_h) {
+  const int lane = threadIdx.x & 63;
+  const int h = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (h >= H) return;
+  const int s = slots[h];
+  float w[MAXM], z[MAXM], zm[MAXM], f[MAXM];
+  for (int k = 0; k < M; ++k) {
+    w[k] = W[(int64_t)s * M + k];
+    z[k] = zp[k];
+    zm[k] = zmaxp[k];
+  }
+  float best = INFINITY;
+  int bi = 0x7fffffff;
+  const int b = rowptr[s], e = rowptr[s + 1];
+  for (int q = b + lane; q < e; q += 64) {
+    const int i = owner[q];
+    for (int k = 0; k < M; ++k) f[k] = off_obj[(int64_t)i * M + k];
+    const float v = agg(func, f, w, z, zm, M);
+    if (v < best || (v == best && i < bi)) { best = v; bi = i; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ob = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ob < best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+  }
+  for (int k = 0; k < M; ++k) f[k] = obj[(int64_t)s * M + k];
+  const float old = agg(func, f, w, z, zm, M);
+  const bool take = bi != 0x7fffffff && best < old;
+  if (lane == 0) win_h[h] = take ? bi : -1;
+  if (take && lane < M) obj[(int64_t)s * M + lane] = off_obj[(int64_t)bi * M + lane];
+}
+
+// halo row update: slot slots[h] takes offspring win_h[h], read straight from the memory of
+// the rank that generated it (peer[q] = that rank's offspring buffer, IPC-mapped over xGMI:
+// a direct mesh read, no collective), rows of rank q start at starts[q]
+__global__ void __launch_bounds__(256) halo_gather_kernel(float* __restrict__ pop, const int32_t* __restrict__ slots,
+                                                          const int32_t* __restrict__ win_h, const int64_t* __restrict__ peer,
+                                                          const int32_t* __restrict__ starts, int world, int d) {
+  const int h = blockIdx.y;
+  const int w = win_h[h];
+  if (w < 0) return;
+  int q = 0;
+  while (q + 1 < world && starts[q + 1] <= w) ++q;
+  const float* src = reinterpret_cast<const float*>(peer[q]) + (int64_t)(w - starts[q]) * d;
+  float* dst = pop + (int64_t)slots[h] * d;
+  if ((d & 3) == 0) {
+    const int n4 = d >> 2;
+    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < n4; c += gridDim.x * blockDim.x)
+      reinterpret_cast<float4*>(dst)[c] = reinterpret_cast<const float4*>(src)[c];
+  } else {
+    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < d; c += gridDim.x * blockDim.x) dst[c] = src[c];
+  }
+}
+
 int grid1(int64_t work) {
   int64_t g = (work + 255) / 256;
   return (int)(g > 65536 ? 65536 : (g < 1 ? 1 : g));
@@ -309,4 +371,17 @@ void evx_moead_select_rows(const float* pop, const float* off, const int32_t* wi
   const int q = (d & 3) == 0 ? d >> 2 : d;
   dim3 grid((q + 255) / 256 < 16 ? (q + 255) / 256 : 16, N);
   select_rows_kernel<<<grid, 256, 0, s>>>(pop, off, win, out, N, d);
+}
+
+void evx_moead_halo_replace(float* obj, const float* off_obj, const float* W, const float* z, const float* zmax, const int32_t* rowptr,
+                            const int32_t* owner, const int32_t* slots, int H, int M, int func, int32_t* win_h, hipStream_t s) {
+  if (H > 0) halo_replace_kernel<<<(H + 3) / 4, 256, 0, s>>>(obj, off_obj, W, z, zmax, rowptr, owner, slots, H, M, func, win_h);
+}
+
+void evx_moead_halo_gather(float* pop, const int32_t* slots, const int32_t* win_h, int H, const int64_t* peer, const int32_t* starts,
+                           int world, int d, hipStream_t s) {
+  if (H <= 0) return;
+  const int q = (d & 3) == 0 ? d >> 2 : d;
+  dim3 grid((q + 255) / 256 < 16 ? (q + 255) / 256 : 16, H);
+  halo_gather_kernel<<<grid, 256, 0, s>>>(pop, slots, win_h, peer, starts, world, d);
 }

@@ -209,7 +209,69 @@ class MOEAD(Algorithm):
     # at N = 16 290); the exact parallel replacement runs redundantly on every rank; each rank
     # then REGENERATES the winning offspring rows from its replica (same parents, keys and
     # counters) instead of receiving them — no d-length row crosses xGMI.
+    #
+    # Owner-computes mode (``shard="owner"``, the default on GPUs): a rank keeps current only
+    # its HALO — every slot its own offspring can draw as a parent (the union of its slots'
+    # neighbourhoods).  It runs the replacement for the halo slots alone and copies each
+    # halo slot's winning offspring row straight out of the memory of the rank that
+    # generated it (IPC-mapped peer buffers, parallel/peer.py: one direct xGMI read per row,
+    # no collective), instead of regenerating every winner of the whole population.  Rows
+    # outside the halo go stale on that rank and are never read by it; the global z_max
+    # comes from an all-reduce of the owners' slot maxima.  Per-rank work falls from
+    # O(N·d) to O(|halo|·d) row updates + O(N·d / world) variation.
     rank_local_fields = ("next_generation",)
+    # owner mode: rows outside a rank's halo go stale there (excluded from replica checks)
+    rank_divergent_fields = ("population", "fitness", "win")
+    shard = "auto"
+
+    def _owner_mode(self, state, dist):
+        if self.shard == "replica":
+            return False
+        return self.shard == "owner" or dist.world_size > 1 or getattr(dist, "backend", "") == "simulated"
+
+    def _owner(self, state, dist):
+        """Halo slots, offspring starts and the peer buffer of this rank (built once)."""
+        cache = getattr(self, "_owner_cache", None)
+        if cache is not None and cache["ctx"] is dist:
+            return cache
+        from ...parallel.context import balanced_slices
+        from ...parallel.peer import PeerBuffer
+
+        n = self.pop_size
+        start, size = dist.slice_of(n)
+        dev = state.population.device
+        halo = self._halo(state, start, size)
+        slices = balanced_slices(n, dist.world_size)
+        starts = [a for a, _ in slices] + [n]
+        rows = max(z for _, z in slices)
+        cache = dict(ctx=dist, start=start, size=size, halo=halo.to(torch.int32).to(dev), halo_long=halo.to(dev),
+                     starts=torch.tensor(starts, dtype=torch.int32, device=dev), starts_list=starts,
+                     peer=PeerBuffer(dist, rows, self.dim, dev), win_h=torch.full((halo.numel(),), -1, dtype=torch.int32, device=dev),
+                     offsets=torch.tensor([4 * a * self.dim for a in starts[:-1]], dtype=torch.int64, device=dev))
+        self._owner_cache = cache
+        return cache
+
+    @staticmethod
+    def _halo(state, start, size):
+        """Sorted slots a rank owning [start, start + size) keeps current: its slots and every
+        neighbour of them (the parents its offspring can draw)."""
+        own_nb = state.neighbors[start : start + size].reshape(-1).to(torch.int64)
+        return torch.unique(torch.cat([own_nb, torch.arange(start, start + size, device=own_nb.device)]))
+
+    def halo_fraction(self, state, rank: int, world: int) -> float:
+        """|halo| / N: the share of the population rank ``rank`` of ``world`` keeps current in
+        owner mode."""
+        from ...parallel.context import balanced_slices
+
+        start, size = balanced_slices(self.pop_size, world)[rank]
+        return float(self._halo(state, start, size).numel()) / self.pop_size
+
+    def fresh_slots(self, state, dist):
+        """Slots whose population / objective rows are current on this rank (all of them in
+        replica mode)."""
+        if self._owner_mode(state, dist):
+            return self._owner(state, dist)["halo_long"]
+        return torch.arange(self.pop_size, device=state.population.device)
 
     def init_ask_sharded(self, state, dist):
         start, size = dist.slice_of(self.pop_size)
@@ -222,13 +284,73 @@ class MOEAD(Algorithm):
         key, sub, sel_key, mut_key = rnd.split(state.key, 4)
         start, size = dist.slice_of(self.pop_size)
         parents = self._parent_pairs(state, sub)
-        off = self._offspring_rows(state, parents, sel_key, mut_key, row0=start, rows=size)
+        if self._owner_mode(state, dist):
+            ow = self._owner(state, dist)
+            buf = ow["peer"].local[:size]  # the peers read this rank's offspring from here
+            if self._fused(state.population):
+                from ...ops import mo as mo_ops
+
+                c, m = self.crossover, self.mutation
+                off = mo_ops.moead_variation(state.population, parents[0].contiguous(), parents[1].contiguous(), sel_key, mut_key,
+                                             self.lb, self.ub, c.pro_c, c.dis_c, m.pro_m, m.dis_m, row0=start, rows=size, out=buf)
+            else:
+                off = buf.copy_(self._offspring_rows(state, parents, sel_key, mut_key, row0=start, rows=size))
+        else:
+            off = self._offspring_rows(state, parents, sel_key, mut_key, row0=start, rows=size)
         return off, state.update(next_generation=off, key=key, parents=parents, var_keys=torch.stack([sel_key, mut_key]))
 
     def tell_sharded(self, state, fitness, dist):
+        if self._owner_mode(state, dist):
+            return self._tell_owner(state, fitness, dist)
         win, new_obj, z = self._replace(state, fitness)
         new_pop = self._offspring_rows(state, state.parents, state.var_keys[0], state.var_keys[1], win=win)
         return state.update(population=new_pop, fitness=new_obj, z=z, win=win)
+
+    def _tell_owner(self, state, fitness, dist):
+        ow = self._owner(state, dist)
+        start, size = ow["start"], ow["size"]
+        z = torch.minimum(state.z, fitness.min(0).values)
+        # global z_max from the owners' (always current) slots
+        z_max = state.fitness[start : start + size].max(0).values.clone()
+        dist.all_reduce_(z_max, op=torch.distributed.ReduceOp.MAX)
+        obj = state.fitness.clone()
+        pop = state.population  # halo rows are updated in place (a full copy would cost more than the update)
+        halo = ow["halo"]
+        if fitness.is_cuda and obj.dtype == torch.float32:
+            from ...ops import mo as mo_ops
+
+            rowptr, _, owner = self._reverse(state)
+            if self._rev32 is None or self._rev32[0].data_ptr() != rowptr.data_ptr():
+                self._rev32 = (rowptr, rowptr.to(torch.int32), owner.to(torch.int32))
+            win_h = ow["win_h"]
+            mo_ops.moead_halo_replace(obj, fitness, state.weight_vector, z, z_max, self._rev32[1], self._rev32[2], halo,
+                                      self.func_name, win_h)
+            table = ow["peer"].peer_table()
+            if table is None:
+                # no device IPC (single-process simulation, gloo): the offspring of every rank
+                # as one buffer, then the same gather (pointer table built on the device:
+                # capturable)
+                full = dist.all_gather_rows(state.next_generation, self.pop_size).contiguous()
+                table = torch.full_like(ow["offsets"], full.data_ptr()) + ow["offsets"]
+                mo_ops.moead_halo_gather(pop, halo, win_h, table, ow["starts"])
+                del full
+            else:
+                mo_ops.moead_halo_gather(pop, halo, win_h, table, ow["starts"])
+                ow["peer"].fence()
+            win = torch.full((self.pop_size,), -1, dtype=torch.int32, device=obj.device)
+            win.index_copy_(0, ow["halo_long"], win_h)
+        else:
+            win_all, new_obj = moead_replace(state.fitness, fitness, state.weight_vector, z, z_max, self.aggregate_func,
+                                                self._reverse(state))
+            hl = ow["halo_long"]
+            win = torch.full((self.pop_size,), -1, dtype=torch.int32, device=obj.device)
+            win[hl] = win_all[hl].to(torch.int32)
+            obj[hl] = new_obj[hl]
+            full = dist.all_gather_rows(state.next_generation, self.pop_size)
+            take = hl[win[hl] >= 0]
+            pop = pop.clone()
+            pop[take] = full[win[take].long()]
+        return state.update(population=pop, fitness=obj, z=z, win=win)
 
 
 def cross_shard_winner_fraction(win: torch.Tensor, world: int):

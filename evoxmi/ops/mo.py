@@ -59,7 +59,7 @@ def moead_parents(neighbors: torch.Tensor, key: torch.Tensor):
     return _ext.ops().moead_parents(neighbors.to(torch.int64).contiguous(), key.contiguous())
 
 
-def moead_variation(pop, p0, p1, key_x, key_m, lb, ub, pro_c, dis_c, pro_m, dis_m, row0=0, rows=0, win=None):
+def moead_variation(pop, p0, p1, key_x, key_m, lb, ub, pro_c, dis_c, pro_m, dis_m, row0=0, rows=0, win=None, out=None):
     """clip(PM(SBX_type2(pop[p0], pop[p1]))) in one pass; ``key_x``/``key_m`` are the keys
     ``SimulatedBinary`` / ``Polynomial`` would receive (bit-identical results).
 
@@ -74,7 +74,22 @@ def moead_variation(pop, p0, p1, key_x, key_m, lb, ub, pro_c, dis_c, pro_m, dis_
     ub = ub.to(device=pop.device, dtype=torch.float32).expand(d).contiguous()
     w = win.to(torch.int32).contiguous() if win is not None else None
     return _ext.ops().moead_variation(pop.contiguous(), p0, p1, rnd.split(key_x, 2).contiguous(), rnd.split(key_m, 2).contiguous(),
-                                      lb, ub, float(pro_c), float(dis_c), float(pro_m), float(dis_m), int(nm), int(row0), int(rows), w)
+                                      lb, ub, float(pro_c), float(dis_c), float(pro_m), float(dis_m), int(nm), int(row0), int(rows), w,
+                                      out)
+
+
+def moead_halo_replace(obj, off_obj, w, z, z_max, rowptr, owner, slots, func, win_h):
+    """In place on ``obj``: the replacement of the slots in ``slots`` only (owner-computes
+    MOEA/D: a rank keeps current just the rows its offspring can draw as parents)."""
+    fid = MOEAD_FUNCS[func] if isinstance(func, str) else int(func)
+    f32 = lambda t: t.to(torch.float32).contiguous()  # noqa: E731
+    _ext.ops().moead_halo_replace(obj, f32(off_obj), f32(w), f32(z), f32(z_max), rowptr, owner, slots, fid, win_h)
+
+
+def moead_halo_gather(pop, slots, win_h, peer, starts):
+    """pop[slots[h]] ← offspring win_h[h] read from the generating rank's buffer (``peer``:
+    int64 device pointers, IPC-mapped; ``starts``: first offspring index of every rank)."""
+    _ext.ops().moead_halo_gather(pop, slots, win_h, peer, starts)
 
 
 def moead_replace(pop_obj, off_obj, w, z, z_max, rowptr, owner, func):

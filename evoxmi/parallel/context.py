@@ -145,3 +145,49 @@ class DistContext:
         dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=self.group)
         dist.all_reduce(mn, op=dist.ReduceOp.MIN, group=self.group)
         return bool((mx - mn).abs().item() <= atol)
+
+
+class SimulatedDistContext(DistContext):
+    """Rank ``rank`` of a ``world``-rank job, simulated in ONE process on one device: every
+    collective is replaced by a local operation on a buffer of the size the real collective
+    would produce (all-gathers tile the local rows ``world`` times, all-reduces touch the
+    buffer in place, broadcasts and barriers are no-ops).  ``bench.py --simulate-rank``
+    uses it to time one rank's share of an N-GPU step (its critical path without the wire
+    time of the collectives) on the single GPU a builder has; the selection then sees the
+    local rows replicated, so the numerics are rank 0's shape of work, not the real run's."""
+
+    def __init__(self, rank: int, world: int, algorithm=None):  # noqa: D401 — no process group
+        self.group = None
+        self.rank = int(rank)
+        self.world_size = int(world)
+        self.backend = "simulated"
+        self.algorithm_sharded = algorithm is not None and hasattr(algorithm, "ask_sharded") and hasattr(algorithm, "tell_sharded")
+        self.global_pop = None
+        self.bytes_all_gather = 0
+        self.bytes_all_reduce = 0
+
+    def all_gather_rows(self, local: torch.Tensor, n_total: Optional[int]) -> torch.Tensor:
+        counts = [s for _, s in balanced_slices(n_total, self.world_size)] if n_total is not None else [local.shape[0]] * self.world_size
+        mx = max(counts)
+        local = local.contiguous()
+        if local.shape[0] < mx:
+            pad = torch.zeros((mx - local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+            local = torch.cat([local, pad], 0)
+        out = local.repeat((self.world_size,) + (1,) * (local.dim() - 1))
+        self.bytes_all_gather += out.numel() * out.element_size()
+        if all(c == mx for c in counts):
+            return out
+        return torch.cat([out[i * mx : i * mx + c] for i, c in enumerate(counts)], 0)
+
+    def all_reduce_(self, t: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
+        self.bytes_all_reduce += t.numel() * t.element_size()
+        return t.mul_(1) if t.is_floating_point() else t
+
+    def all_reduce_min_loc(self, value: torch.Tensor, index: torch.Tensor):
+        return value.reshape(()), index.reshape(())
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        return t
+
+    def barrier(self):
+        return None

@@ -348,6 +348,8 @@ class StdWorkflow(Workflow):
             # race/divergence detector: replicas must stay bit-identical
             chk = state
             local = getattr(self.algorithm, "rank_local_fields", ()) if self._dist.algorithm_sharded else ()
+            # fields an owner-computes algorithm keeps current only where a rank needs them
+            local = tuple(local) + tuple(getattr(self.algorithm, "rank_divergent_fields", ()) if self._dist.algorithm_sharded else ())
             if local:
                 alg = state.get_child_state("algorithm")
                 chk = state.update_child("algorithm", alg.replace(**{f: torch.zeros(0) for f in local}))
@@ -369,15 +371,18 @@ class StdWorkflow(Workflow):
             fitness = self._dist.all_gather_rows(fitness, None)
         return fitness, state
 
-    def enable_distributed(self, state: State, group=None) -> State:
+    def enable_distributed(self, state: State, group=None, context=None) -> State:
         """Population-shard this workflow across the ranks of ``torch.distributed``.
 
         Every rank must call this with an identical state (same key ⇒ identical
         replicas).  The state is broadcast from rank 0 to make that explicit.
+        ``context``: a ready context instead of one over the default process group (e.g.
+        :class:`evoxmi.parallel.context.SimulatedDistContext` for one rank's share of an
+        N-GPU step on one device).
         """
         from ..parallel.context import DistContext
 
-        self._dist = DistContext(group=group, algorithm=self.algorithm)
+        self._dist = context if context is not None else DistContext(group=group, algorithm=self.algorithm)
         self.distributed_step = True
         for m in self.monitors:  # monitors that track sharded rows (EvalMonitor best solution)
             if hasattr(m, "set_dist"):

@@ -31,19 +31,21 @@ def _make(dev):
     return StdWorkflow(MOEAD(lb, ub, m, 105, func_name="tchebycheff"), LSMOP1(d=d, m=m))
 
 
-def _run(wf, dev, gens, dist=False):
+def _run(wf, dev, gens, dist=False, shard="auto"):
     from evoxmi import random as rnd
 
+    wf.algorithm.shard = shard
     st = wf.init(rnd.PRNGKey(5, device=dev))
     if dist:
         st = wf.enable_distributed(st)
     for _ in range(gens):
         st = wf.step(st)
     a = st.get_child_state("algorithm")
-    return a.population.cpu(), a.fitness.cpu(), a.win.cpu()
+    fresh = wf.algorithm.fresh_slots(a, wf._dist).cpu() if dist else torch.arange(a.population.shape[0])
+    return a.population.cpu(), a.fitness.cpu(), a.win.cpu(), fresh
 
 
-def _worker(rank, world, port, dev, gens, out):
+def _worker(rank, world, port, dev, gens, out, shard):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK="0" if dev == "cuda" else str(rank))
     torch.set_num_threads(1)
@@ -52,24 +54,30 @@ def _worker(rank, world, port, dev, gens, out):
     init_distributed(backend="gloo")
     if dev == "cuda":
         torch.cuda.set_device(0)
-    out[rank] = _run(_make(dev), dev, gens, dist=True)
+    out[rank] = _run(_make(dev), dev, gens, dist=True, shard=shard)
     destroy()
 
 
-def _check(dev, gens=8):
-    ref_pop, ref_fit, _ = _run(_make(dev), dev, gens)
+def _check(dev, gens=8, shard="auto"):
+    """Every rank's current rows (all of them in replica mode, its halo in owner mode) are
+    bit-identical to the single process, and the ranks' current rows cover the population."""
+    ref_pop, ref_fit, _, _ = _run(_make(dev), dev, gens)
     mgr = mp.get_context("spawn").Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(2, _free_port(), dev, gens, out), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, _free_port(), dev, gens, out, shard), nprocs=2, join=True)
+    covered = torch.zeros(ref_pop.shape[0], dtype=torch.bool)
     for r in range(2):
-        pop, fit, win = out[r]
-        assert torch.equal(pop, ref_pop), f"rank {r}: population differs from the single process"
-        assert torch.equal(fit, ref_fit), f"rank {r}: objectives differ from the single process"
+        pop, fit, win, fresh = out[r]
+        assert torch.equal(pop[fresh], ref_pop[fresh]), f"rank {r}: population differs from the single process"
+        assert torch.equal(fit[fresh], ref_fit[fresh]), f"rank {r}: objectives differ from the single process"
+        covered[fresh] = True
+    assert bool(covered.all())
     assert bool((out[0][2] >= 0).any())  # the replacement did replace rows
 
 
-def test_moead_sharded_two_gloo_ranks_bit_identical_cpu():
-    _check("cpu")
+@pytest.mark.parametrize("shard", ["owner", "replica"])
+def test_moead_sharded_two_gloo_ranks_bit_identical_cpu(shard):
+    _check("cpu", shard=shard)
 
 
 def test_cross_shard_winner_fraction():
@@ -82,5 +90,8 @@ def test_cross_shard_winner_fraction():
 
 
 @pytest.mark.gpu
-def test_moead_sharded_two_ranks_on_gpu_bit_identical():
-    _check("cuda")
+@pytest.mark.parametrize("shard", ["owner", "replica"])
+def test_moead_sharded_two_ranks_on_gpu_bit_identical(shard):
+    """owner: the halo rows come from the peer's offspring buffer through IPC (two
+    processes on one device; an 8-GPU node reads them over xGMI)."""
+    _check("cuda", shard=shard)

@@ -291,3 +291,27 @@ def test_min_loc_packing_roundtrip_single_process():
         t = torch.tensor(v, dtype=torch.float32)
         val, idx = ctx.all_reduce_min_loc(t, torch.tensor(12345))
         assert torch.equal(val.view(torch.int32), t.view(torch.int32)) and int(idx) == 12345
+
+
+def test_simulated_rank_context_runs_one_rank_share():
+    """bench.py --simulate-rank: rank 0's share of a 4-rank CMA-ES step in one process
+    (collectives replaced by same-size local ops) keeps the sharded shapes."""
+    import torch
+
+    from evoxmi import random as rnd
+    from evoxmi.algorithms import CMAES
+    from evoxmi.parallel.context import SimulatedDistContext
+    from evoxmi.problems.numerical import Sphere
+    from evoxmi.workflows import StdWorkflow
+
+    algo = CMAES(center_init=torch.zeros(8), init_stdev=1.0, pop_size=40)
+    wf = StdWorkflow(algo, Sphere())
+    st = wf.init(rnd.PRNGKey(0))
+    ctx = SimulatedDistContext(0, 4, algorithm=algo)
+    st = wf.enable_distributed(st, context=ctx)
+    for _ in range(3):
+        st = wf.step(st)
+    a = st.get_child_state("algorithm")
+    assert a.population.shape == (10, 8)
+    assert torch.isfinite(a.mean).all() and torch.isfinite(a.C).all()
+    assert ctx.bytes_all_reduce == 3 * (8 + 64) * 4

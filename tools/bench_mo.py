@@ -9,10 +9,12 @@ torchrun --nproc-per-node 8 --master-addr 127.0.0.1 tools/bench_mo.py --algo moe
 Prints one JSON line (rank 0): generations/s and evaluations/s of full generations
 (ask → evaluate → tell), random-init populations, fp32.  Under torchrun (or with
 --force-dist) the workflow is population-sharded: MOEA/D ranks own contiguous slot
-ranges, generate/evaluate only their offspring, all-gather the (N, m) objectives and
-regenerate winning rows locally; the line then also reports the cross-shard winner
-fraction (winning offspring generated on another rank than the slot's owner — the rows
-a row-shipping design would move over xGMI every generation).
+ranges, generate/evaluate only their offspring, all-gather the (N, m) objectives; in the
+owner-computes mode (default) each rank keeps only its halo current and reads the halo's
+winning rows from their generating rank over xGMI (IPC peer buffers), in the replica
+mode it regenerates every winner locally.  The line reports the halo fractions at
+2/4/8 ranks and the cross-shard winner fraction.  ``--simulate-rank R --world N`` times
+rank R's share of an N-GPU step on one GPU (collectives → same-size local operations).
 """
 import argparse
 import json
@@ -52,15 +54,25 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu", action="store_true")
     ap.add_argument("--force-dist", action="store_true", help="sharded protocol even on one rank")
+    ap.add_argument("--simulate-rank", type=int, default=None,
+                    help="time rank R's share of a --world N sharded step on this one GPU (collectives → same-size local ops)")
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--shard", choices=["auto", "owner", "replica"], default="auto", help="MOEA/D sharded mode")
     args = ap.parse_args()
     import torch.distributed as dist
     from evoxmi.parallel import init_distributed
 
-    rank, world, dev = init_distributed(force=args.force_dist, backend="gloo" if args.cpu else None)
+    sim = args.simulate_rank is not None
+    if sim:
+        rank, world, dev = 0, 1, torch.device("cpu" if args.cpu else "cuda")
+    else:
+        rank, world, dev = init_distributed(force=args.force_dist, backend="gloo" if args.cpu else None)
     if args.cpu:
         dev = torch.device("cpu")
     algo, prob = build(args, dev)
-    dist_on = world > 1 or args.force_dist
+    if hasattr(algo, "shard"):
+        algo.shard = args.shard
+    dist_on = (world > 1 or args.force_dist) and not sim
 
     def sync():
         if dev.type == "cuda":
@@ -72,6 +84,10 @@ def main():
     st = wf.init(rnd.PRNGKey(7, device=dev))
     if dist_on:
         st = wf.enable_distributed(st)
+    if sim:
+        from evoxmi.parallel.context import SimulatedDistContext
+
+        st = wf.enable_distributed(st, context=SimulatedDistContext(args.simulate_rank, args.world, algorithm=algo))
     for _ in range(1 + args.warmup):
         st = wf.step(st)
     sync()
@@ -88,7 +104,7 @@ def main():
     pop = algo.pop_size
     out = {
         "config": args.algo, "pop": pop, "dim": algo.dim, "n_objs": 3, "graph": not (args.no_graph or args.cpu), "n_gpus": world,
-        "parallelism": f"pop-shard{world}" if dist_on else "single",
+        "parallelism": (f"simulated-rank{args.simulate_rank}-of-{args.world}" if sim else (f"pop-shard{world}" if dist_on else "single")),
         "ms_per_gen": round(dt * 1e3, 3), "gens_per_sec": round(1 / dt, 2), "evals_per_sec": round(pop / dt, 1),
         "fitness_finite": bool(torch.isfinite(fit).all()), "mean_obj": [round(float(v), 4) for v in fit.mean(0)],
     }
@@ -99,6 +115,12 @@ def main():
         out["winner_fraction"] = round(frac, 4)
         out["cross_shard_winner_fraction"] = round(cross, 4)
         out["cross_shard_fraction_world"] = world if dist_on else 2
+        # owner-computes: the share of the population each rank keeps current (its halo)
+        for w in (2, 4, 8):
+            fr = [algo.halo_fraction(a, r, w) for r in range(w)]
+            out[f"halo_fraction_world{w}"] = {"mean": round(sum(fr) / w, 4), "max": round(max(fr), 4)}
+        if wf._dist is not None:
+            out["shard_mode"] = "owner" if algo._owner_mode(a, wf._dist) else "replica"
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist_on:
