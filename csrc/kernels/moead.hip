@@ -71,11 +71,13 @@ __device__ __forceinline__ void min2_merge(uint64_t& a1, uint64_t& a2, uint64_t 
   a2 = hi < s ? hi : s;
 }
 
+// rows [row0, row0 + N) of the (global) neighbour table; counters use the global row, so a
+// rank drawing only its own slots' parents gets the full launch's values
 __global__ void __launch_bounds__(256) parents_kernel(const int64_t* __restrict__ nb, int N, int T, const int64_t* __restrict__ key,
-                                                      int32_t* __restrict__ p0, int32_t* __restrict__ p1) {
+                                                      int32_t* __restrict__ p0, int32_t* __restrict__ p1, int row0) {
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= N) return;
+  const int row = row0 + blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= row0 + N) return;
   uint32_t k0, k1;
   load_key(key, k0, k1);
   uint64_t m1 = ~0ull, m2 = ~0ull;
@@ -343,8 +345,8 @@ int grid1(int64_t work) {
 
 }  // namespace
 
-void evx_moead_parents(const int64_t* nb, int N, int T, const int64_t* key, int32_t* p0, int32_t* p1, hipStream_t s) {
-  parents_kernel<<<(N + 3) / 4, 256, 0, s>>>(nb, N, T, key, p0, p1);
+void evx_moead_parents(const int64_t* nb, int N, int T, const int64_t* key, int32_t* p0, int32_t* p1, hipStream_t s, int row0) {
+  parents_kernel<<<(N + 3) / 4, 256, 0, s>>>(nb, N, T, key, p0, p1, row0);
 }
 
 void evx_moead_variation(const float* pop, const int32_t* p0, const int32_t* p1, float* out, int N, int d, const int64_t* kx,

@@ -140,13 +140,14 @@ class MOEAD(Algorithm):
                 and type(c) is crossover.SimulatedBinary and c.type == 2
                 and type(m) is mutation.Polynomial and m.boundary[0] is self.lb and m.boundary[1] is self.ub)
 
-    def _parent_pairs(self, state, key):
+    def _parent_pairs(self, state, key, row0=0, rows=0):
         """(2, N) int32: the two parents of every offspring (first two entries of a random
-        permutation of its neighbour row)."""
+        permutation of its neighbour row); ``rows > 0`` (owner mode on a GPU): only those
+        offspring's parents are drawn."""
         if self._fused(state.population):
             from ...ops import mo as mo_ops
 
-            p0, p1 = mo_ops.moead_parents(state.neighbors, key)
+            p0, p1 = mo_ops.moead_parents(state.neighbors, key, row0, rows)
             return torch.stack([p0, p1])
         return self._parents(state, key).T.to(torch.int32).contiguous()
 
@@ -283,8 +284,10 @@ class MOEAD(Algorithm):
     def ask_sharded(self, state, dist):
         key, sub, sel_key, mut_key = rnd.split(state.key, 4)
         start, size = dist.slice_of(self.pop_size)
-        parents = self._parent_pairs(state, sub)
-        if self._owner_mode(state, dist):
+        owner = self._owner_mode(state, dist)
+        # owner mode never regenerates another rank's offspring: its own rows' parents suffice
+        parents = self._parent_pairs(state, sub, *((start, size) if owner else (0, 0)))
+        if owner:
             ow = self._owner(state, dist)
             buf = ow["peer"].local[:size]  # the peers read this rank's offspring from here
             if self._fused(state.population):

@@ -52,11 +52,12 @@ def moead_scan(objs, off_objs, P, W, z, func="tchebycheff", nr=None, update_z=Fa
 MOEAD_FUNCS = {"tchebycheff": 0, "pbi": 1, "weighted_sum": 2, "modified_tchebycheff": 3, "tchebycheff_norm": 4}
 
 
-def moead_parents(neighbors: torch.Tensor, key: torch.Tensor):
+def moead_parents(neighbors: torch.Tensor, key: torch.Tensor, row0: int = 0, rows: int = 0):
     """First two columns of a per-row random permutation of ``neighbors`` (N, T):
     the rows' two smallest ``uniform(key, (N, T))`` entries, ties by column index
-    (= ``argsort(uniform, stable=True)[:, :2]``).  Returns int32 (p0, p1)."""
-    return _ext.ops().moead_parents(neighbors.to(torch.int64).contiguous(), key.contiguous())
+    (= ``argsort(uniform, stable=True)[:, :2]``).  Returns int32 (p0, p1); ``rows > 0``:
+    only rows row0 .. row0+rows−1 are drawn (the rest are 0)."""
+    return _ext.ops().moead_parents(neighbors.to(torch.int64).contiguous(), key.contiguous(), int(row0), int(rows))
 
 
 def moead_variation(pop, p0, p1, key_x, key_m, lb, ub, pro_c, dis_c, pro_m, dis_m, row0=0, rows=0, win=None, out=None):
