@@ -362,6 +362,22 @@ std::vector<at::Tensor> radix_argsort_f32(const at::Tensor& keys, int64_t descen
   return {ok, oi};
 }
 
+// same contract as radix_argsort_f32: rank-by-counting, one launch for n ≤ 16384 (sort.hip)
+std::vector<at::Tensor> rank_argsort_f32(const at::Tensor& keys, int64_t descending) {
+  CHECK_DEV(keys); CHECK_F32(keys); CHECK_CONTIG(keys);
+  TORCH_CHECK(keys.dim() <= 2, "rank_argsort_f32: keys must be (n,) or (B, n)");
+  const int64_t B = keys.dim() == 2 ? keys.size(0) : 1;
+  const int64_t n = keys.dim() == 0 ? 1 : keys.size(-1);
+  TORCH_CHECK(n <= evx_rank_argsort_max_n(), "rank_argsort_f32: n > ", evx_rank_argsort_max_n());
+  TORCH_CHECK(B <= 65535, "rank_argsort_f32: B > 65535");
+  c10::DeviceGuard g(keys.device());
+  auto ok = at::empty_like(keys);
+  auto oi = at::empty(keys.sizes(), keys.options().dtype(at::kInt));
+  if (n > 0 && B > 0)
+    evx_rank_argsort(keys.data_ptr<float>(), (int)n, (int)descending, ok.data_ptr<float>(), oi.data_ptr<int32_t>(), cur_stream(), (int)B);
+  return {ok, oi};
+}
+
 at::Tensor cec_basic(const at::Tensor& Z, int64_t fid, const c10::optional<at::Tensor>& perm, int64_t start, int64_t L,
                      const c10::optional<at::Tensor>& sub, double scale, const c10::optional<at::Tensor>& Y, int64_t ystart,
                      int64_t yperm) {
@@ -836,13 +852,19 @@ std::vector<at::Tensor> ant_rollout(const at::Tensor& W, int64_t h1, int64_t h2,
   return {ret, steps};
 }
 
-std::vector<at::Tensor> moead_parents(const at::Tensor& nb, const at::Tensor& key) {
+// rows > 0: only the parents of offspring row0 .. row0+rows−1 (the rest of p0 / p1 zero)
+std::vector<at::Tensor> moead_parents(const at::Tensor& nb, const at::Tensor& key, int64_t row0, int64_t rows) {
   CHECK_DEV(nb); CHECK_CONTIG(nb); check_key(key);
   TORCH_CHECK(nb.dim() == 2 && nb.scalar_type() == at::kLong && nb.size(1) >= 1 && nb.size(1) < 65536, "neighbours must be int64 (N, T), T < 65536");
   c10::DeviceGuard g(nb.device());
   const int64_t N = nb.size(0);
-  auto p0 = at::empty({N}, nb.options().dtype(at::kInt)), p1 = at::empty({N}, nb.options().dtype(at::kInt));
-  if (N > 0) evx_moead_parents(nb.data_ptr<int64_t>(), (int)N, (int)nb.size(1), key.data_ptr<int64_t>(), p0.data_ptr<int>(), p1.data_ptr<int>(), cur_stream());
+  const int64_t R = rows > 0 ? rows : N;
+  TORCH_CHECK(row0 >= 0 && row0 + R <= N, "moead_parents: rows out of range");
+  auto p0 = rows > 0 ? at::zeros({N}, nb.options().dtype(at::kInt)) : at::empty({N}, nb.options().dtype(at::kInt));
+  auto p1 = rows > 0 ? at::zeros({N}, nb.options().dtype(at::kInt)) : at::empty({N}, nb.options().dtype(at::kInt));
+  if (R > 0)
+    evx_moead_parents(nb.data_ptr<int64_t>(), (int)R, (int)nb.size(1), key.data_ptr<int64_t>(), p0.data_ptr<int>(), p1.data_ptr<int>(),
+                      cur_stream(), (int)row0);
   return {p0, p1};
 }
 
@@ -1134,6 +1156,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("philox_fill(Tensor key, int n, int dist, int offset) -> Tensor");
   m.def("argsort_f32(Tensor keys, int descending) -> Tensor[]");
   m.def("radix_argsort_f32(Tensor keys, int descending) -> Tensor[]");
+  m.def("rank_argsort_f32(Tensor keys, int descending) -> Tensor[]");
   m.def("cec_basic(Tensor Z, int fid, Tensor? perm, int start, int L, Tensor? sub, float scale, Tensor? Y, int ystart, int yperm) -> Tensor");
   m.def("jacobi_sweeps(Tensor A, Tensor B, Tensor sched, int sweeps, float tol, float inner_tol, int max_inner, int fused=2) -> Tensor[]");
   m.def("philox_words(Tensor key, int nblocks, int domain, int offset) -> Tensor");
@@ -1167,7 +1190,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("cma_cov_pad(Tensor C, Tensor S, Tensor pc, Tensor a, float c1, float cmu, Tensor Bprev, int np) -> Tensor[]");
   m.def("cma_eig_out(Tensor Bp, Tensor w, int d) -> Tensor[]");
   m.def("nsga_select(Tensor rank, Tensor f, int N, int mask_pos) -> Tensor");
-  m.def("moead_parents(Tensor nb, Tensor key) -> Tensor[]");
+  m.def("moead_parents(Tensor nb, Tensor key, int row0=0, int rows=0) -> Tensor[]");
   m.def("moead_variation(Tensor pop, Tensor p0, Tensor p1, Tensor kx, Tensor km, Tensor lb, Tensor ub, float pro_c, float dis_c, float pro_m, float dis_m, int nm, int row0=0, int rows=0, Tensor? win=None, Tensor(a!)? out=None) -> Tensor");
   m.def("moead_halo_replace(Tensor(a!) obj, Tensor off_obj, Tensor W, Tensor z, Tensor zmax, Tensor rowptr, Tensor owner, Tensor slots, int func, Tensor(b!) win_h) -> ()");
   m.def("moead_halo_gather(Tensor(a!) pop, Tensor slots, Tensor win_h, Tensor peer, Tensor starts) -> ()");
@@ -1219,6 +1242,7 @@ TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
   m.impl("cec_basic", &cec_basic);
   m.impl("argsort_f32", &argsort_f32);
   m.impl("radix_argsort_f32", &radix_argsort_f32);
+  m.impl("rank_argsort_f32", &rank_argsort_f32);
   m.impl("gemm_f32", &gemm_f32);
   m.impl("gemm_ks", &gemm_ks_new);
   m.impl("gemm_ks_out", &gemm_ks_out);

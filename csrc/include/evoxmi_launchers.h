@@ -110,7 +110,7 @@ void evx_nds(const float* f, int n, int m, int limit, uint32_t* DW, int32_t* ran
              hipStream_t s);
 
 // moead.hip
-void evx_moead_parents(const int64_t* nb, int N, int T, const int64_t* key, int32_t* p0, int32_t* p1, hipStream_t s);
+void evx_moead_parents(const int64_t* nb, int N, int T, const int64_t* key, int32_t* p0, int32_t* p1, hipStream_t s, int row0 = 0);
 void evx_moead_variation(const float* pop, const int32_t* p0, const int32_t* p1, float* out, int N, int d, const int64_t* kx,
                          const int64_t* km, const float* lb, const float* ub, float pro_c, float dis_c, float pro_m, float dis_m,
                          int nm, hipStream_t s, int row0 = 0, const int32_t* win = nullptr);
@@ -188,3 +188,7 @@ void evx_moead_halo_replace(float* obj, const float* off_obj, const float* W, co
                             const int32_t* owner, const int32_t* slots, int H, int M, int func, int32_t* win_h, hipStream_t s);
 void evx_moead_halo_gather(float* pop, const int32_t* slots, const int32_t* win_h, int H, const int64_t* peer, const int32_t* starts,
                            int world, int d, hipStream_t s);
+
+// rank-by-counting stable argsort in one launch (sort.hip), n ≤ evx_rank_argsort_max_n()
+int evx_rank_argsort_max_n();
+void evx_rank_argsort(const float* keys, int n, int descending, float* out_keys, int32_t* out_idx, hipStream_t s, int batch);

@@ -165,6 +165,83 @@ __global__ void __launch_bounds__(1024) radix_argsort_kernel(const float* __rest
   }
 }
 
+// Rank-by-counting argsort (K19 at 10⁴-class n): rank(i) = #{j : k_j < k_i or (k_j = k_i and j < i)}
+// on order-preserving u32 keys, so the result is a stable sort.  All n keys sit in LDS; a
+// workgroup ranks 64 consecutive elements (one per lane), its WAVES waves splitting the key
+// range and reading four keys per LDS broadcast into four independent counters.  The tie
+// test is needed only for j inside the workgroup's own 64 elements: below them every j < i
+// (count k_j ≤ k_i), above them none (count k_j < k_i) — one compare + one add per key.
+// 16 waves per workgroup (4 per SIMD) hide the LDS latency of the broadcast chain; the
+// single-wave-per-SIMD first cut ran 53.6 µs at n = 16384 (profiles/r3_sort_microbench.log).
+__device__ __forceinline__ uint32_t ord_key(float x, bool desc) {
+  x = (x != x) ? __uint_as_float(0x7fffffffu) : (x == 0.f ? 0.f : x);  // NaN largest, -0 == +0
+  const uint32_t o = f2ord(x);
+  return desc ? ~o : o;
+}
+
+template <int WAVES>
+__global__ void __launch_bounds__(64 * WAVES) rank_argsort_kernel(const float* __restrict__ keys, int n, int desc,
+                                                                  float* __restrict__ out_keys, int32_t* __restrict__ out_idx) {
+  extern __shared__ uint4 sk4[];  // 16-byte aligned: the compare loops read four keys per ds_read_b128
+  __shared__ int part[WAVES][64];
+  uint32_t* sk = reinterpret_cast<uint32_t*>(sk4);
+  const float* kb = keys + (int64_t)blockIdx.y * n;
+  const int np = (n + 3) & ~3;
+  const bool d = desc != 0;
+  if ((n & 3) == 0) {  // rows 16-byte aligned: float4 loads, all in flight before the first use
+    const float4* kb4 = reinterpret_cast<const float4*>(kb);
+#pragma unroll 4
+    for (int v = threadIdx.x; v < (n >> 2); v += 64 * WAVES) {
+      const float4 x = kb4[v];
+      sk4[v] = make_uint4(ord_key(x.x, d), ord_key(x.y, d), ord_key(x.z, d), ord_key(x.w, d));
+    }
+  } else {
+#pragma unroll 4
+    for (int i = threadIdx.x; i < np; i += 64 * WAVES) sk[i] = i < n ? ord_key(kb[min(i, n - 1)], d) : 0xffffffffu;  // pads: never counted
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int b = blockIdx.x * 64, i = b + lane;
+  const uint32_t ki = i < n ? sk[i] : 0u;
+  const int q = ((np >> 2) + WAVES - 1) / WAVES * 4;
+  const int lo = min(np, w * q), hi = min(np, lo + q);
+  int c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+  const int e0 = min(hi, b), s1 = max(lo, b), e1 = min(hi, b + 64), s2 = max(lo, b + 64);
+  // [lo, b): every j < i
+  for (int j = lo; j < e0; j += 4) {
+    const uint4 k4 = sk4[j >> 2];
+    c0 += k4.x <= ki;
+    c1 += k4.y <= ki;
+    c2 += k4.z <= ki;
+    c3 += k4.w <= ki;
+  }
+  // the workgroup's own elements: explicit index tie-break
+  for (int j = s1; j < e1; j += 4) {
+    const uint4 k4 = sk4[j >> 2];
+    c0 += (k4.x < ki) | ((k4.x == ki) & (j < i));
+    c1 += (k4.y < ki) | ((k4.y == ki) & (j + 1 < i));
+    c2 += (k4.z < ki) | ((k4.z == ki) & (j + 2 < i));
+    c3 += (k4.w < ki) | ((k4.w == ki) & (j + 3 < i));
+  }
+  // [b + 64, hi): every j > i
+  for (int j = s2; j < hi; j += 4) {
+    const uint4 k4 = sk4[j >> 2];
+    c0 += k4.x < ki;
+    c1 += k4.y < ki;
+    c2 += k4.z < ki;
+    c3 += k4.w < ki;
+  }
+  part[w][lane] = (c0 + c1) + (c2 + c3);
+  __syncthreads();
+  if (w == 0 && i < n) {
+    int r = 0;
+#pragma unroll
+    for (int v = 0; v < WAVES; ++v) r += part[v][lane];
+    out_idx[(int64_t)blockIdx.y * n + r] = i;
+    if (out_keys) out_keys[(int64_t)blockIdx.y * n + r] = kb[i];
+  }
+}
+
 }  // namespace
 
 void evx_radix_argsort(const float* keys, int n, int descending, float* out_keys, int32_t* out_idx, hipStream_t s, int batch) {
@@ -187,5 +264,19 @@ void evx_argsort(const float* keys, int n, int descending, float* out_keys, int3
     case 12: bitonic_argsort_kernel<12><<<batch, 1024, 0, s>>>(keys, n, descending, out_keys, out_idx); break;
     case 13: bitonic_argsort_kernel<13><<<batch, 1024, 0, s>>>(keys, n, descending, out_keys, out_idx); break;
     default: bitonic_argsort_kernel<14><<<batch, 1024, 0, s>>>(keys, n, descending, out_keys, out_idx); break;
+  }
+}
+
+int evx_rank_argsort_max_n() { return 16384; }
+
+void evx_rank_argsort(const float* keys, int n, int descending, float* out_keys, int32_t* out_idx, hipStream_t s, int batch) {
+  const int np = (n + 3) & ~3;
+  const size_t lds = (size_t)np * 4;
+  const dim3 grid((n + 63) / 64, batch);
+  if (n < 256) {
+    rank_argsort_kernel<4><<<grid, 256, lds, s>>>(keys, n, descending, out_keys, out_idx);
+  } else {
+    if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)rank_argsort_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    rank_argsort_kernel<16><<<grid, 1024, lds, s>>>(keys, n, descending, out_keys, out_idx);
   }
 }

@@ -6,7 +6,8 @@ evoxmi HIP ops below would otherwise hit functorch's per-sample fallback (one la
 per run).  Each rule moves the run axis to the front and calls the op's batched form:
 
 * ``philox_words`` / ``philox_fill``: keys (B, 2) → grid.y = run (``rng.hip``);
-* ``argsort_f32`` / ``radix_argsort_f32``: keys (B, n) → one workgroup per row (``sort.hip``);
+* ``argsort_f32`` / ``radix_argsort_f32`` / ``rank_argsort_f32``: keys (B, n) → one workgroup
+  (row of workgroups, rank kernel) per run (``sort.hip``);
 * ``de_trial``: P (B, rows, d), idx (B, R, K), per-row vectors (B, R), keys (B, 2) →
   grid.y = run, all indices run-local (``evo_ops.hip``).
 
@@ -62,6 +63,16 @@ def _radix_argsort_f32(info, in_dims, keys, descending):
     return (ok, oi), (0, 0)
 
 
+def _rank_argsort_f32(info, in_dims, keys, descending):
+    if in_dims[0] is None:
+        return tuple(_ext.ops().rank_argsort_f32(keys, descending)), (None, None)
+    k = _front(keys, in_dims[0], info.batch_size)
+    if k.dim() != 2:
+        raise NotImplementedError("rank_argsort_f32 vmap rule: per-run keys must be 1-D")
+    ok, oi = _ext.ops().rank_argsort_f32(k, descending)
+    return (ok, oi), (0, 0)
+
+
 def _de_trial(info, in_dims, P, idx, coef, cur, mode, CR, jr, L, key, lb, ub, repair, err):
     B = info.batch_size
     if any(d is not None for d in in_dims[9:11]) or in_dims[12] is not None:
@@ -77,6 +88,6 @@ def register():
     if _REGISTERED or not _ext.load(build_if_missing=False):
         return
     for name, fn in (("philox_words", _philox_words), ("philox_fill", _philox_fill), ("argsort_f32", _argsort_f32),
-                     ("radix_argsort_f32", _radix_argsort_f32), ("de_trial", _de_trial)):
+                     ("radix_argsort_f32", _radix_argsort_f32), ("rank_argsort_f32", _rank_argsort_f32), ("de_trial", _de_trial)):
         torch.library.register_vmap(f"evoxmi::{name}", fn)
     _REGISTERED = True

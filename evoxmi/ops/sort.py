@@ -1,22 +1,28 @@
-"""Sorting primitives (K19).  Device path: one-workgroup LDS radix argsort (rocPRIM block
-radix sort, ``sort.hip``) for n ≤ 4096 — one launch, no workspace; larger inputs use the
-ROCm library radix sort, which spreads over the CUs.  Measured on MI355X
-(profiles/r2_sort_microbench.log, µs per call): n = 1000: radix 10.7 / bitonic 11.2 /
-library 21.0; n = 4096: 21.3 / 31.5 / 31.7; n = 10 000: 43.9 / 119.8 / 32.5 — one
-workgroup stops paying off above ≈4k keys.  Ties are broken by index (== stable sort)."""
+"""Sorting primitives (K19).  Device path for n ≤ 16384 (every population size of the
+north-star configs): the rank-by-counting argsort of ``sort.hip`` — all keys in LDS, each
+256-thread workgroup ranks 64 elements against all n keys, one launch, no workspace, and
+n/64 workgroups spread over the CUs (the single-workgroup radix/bitonic kernels cannot:
+round 2 measured them at 43.9 / 119.8 µs for n = 10 000 against the library's 32.5,
+profiles/r2_sort_microbench.log).  Larger inputs use the ROCm library radix sort.  Ties are
+broken by index (== stable sort); NaN sorts as the largest key and −0.0 ties with +0.0, as
+in ``torch.sort``.  Numbers: ``tools/bench_sort.py`` → profiles/r3_sort_microbench.log."""
 from __future__ import annotations
 
 import torch
 
 from . import _ext
 
-MAX_LDS_SORT = 4096
+MAX_RANK_SORT = 16384
+
+
+def _device(keys):
+    return keys.is_cuda and keys.dtype == torch.float32 and keys.dim() <= 2 and keys.shape[-1] <= MAX_RANK_SORT
 
 
 def argsort(keys: torch.Tensor, descending: bool = False):
-    """Return ``(sorted_keys, indices[int64])`` of a 1-D float tensor."""
-    if keys.is_cuda and keys.dtype == torch.float32 and keys.numel() <= MAX_LDS_SORT:
-        k, i = _ext.ops().radix_argsort_f32(keys.contiguous(), int(descending))
+    """Return ``(sorted_keys, indices[int64])`` along the last dim of a 1-D or (B, n) float tensor."""
+    if _device(keys):
+        k, i = _ext.ops().rank_argsort_f32(keys.contiguous(), int(descending))
         return k, i.long()
     v, i = torch.sort(keys, descending=descending, stable=True)
     return v, i
@@ -24,8 +30,8 @@ def argsort(keys: torch.Tensor, descending: bool = False):
 
 def argsort_i32(keys: torch.Tensor):
     """Ascending argsort returning int32 indices (feeds gather prologues directly)."""
-    if keys.is_cuda and keys.dtype == torch.float32 and keys.numel() <= MAX_LDS_SORT:
-        return _ext.ops().radix_argsort_f32(keys.contiguous(), 0)
+    if _device(keys):
+        return _ext.ops().rank_argsort_f32(keys.contiguous(), 0)
     v, i = torch.sort(keys, stable=True)
     return v, i.to(torch.int32)
 

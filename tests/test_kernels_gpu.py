@@ -881,13 +881,20 @@ def test_open_es_gpu_matches_stored_noise_update():
     assert torch.allclose(st2.center, st.center - 0.1 * grad, rtol=1e-4, atol=1e-4)
 
 
-@pytest.mark.parametrize("n", [100, 2048, 5000, 10000, 12000, 16384])
+@pytest.mark.parametrize("n", [1, 3, 100, 2048, 5000, 10000, 12000, 16383, 16384])
 @pytest.mark.parametrize("descending", [0, 1])
-def test_radix_argsort_matches_stable_torch_sort(n, descending):
+@pytest.mark.parametrize("kernel", ["radix_argsort_f32", "rank_argsort_f32"])
+def test_device_argsort_matches_stable_torch_sort(n, descending, kernel):
     from evoxmi.ops import _ext
 
     g = torch.Generator().manual_seed(n + descending)
     k = torch.randint(0, n // 4 + 1, (2, n), generator=g).float() / 7  # many ties
+    if n < 12:
+        k = torch.randn(2, n, generator=g)
+        ok, oi = getattr(_ext.ops(), kernel)(k.cuda(), descending)
+        rv, ri = torch.sort(k, dim=1, descending=bool(descending), stable=True)
+        assert torch.equal(oi.cpu().long(), ri) and torch.equal(ok.cpu(), rv)
+        return
     k[0, 3] = float("inf")
     k[0, 9] = float("nan")
     k[1, 5] = float("-inf")
@@ -898,7 +905,7 @@ def test_radix_argsort_matches_stable_torch_sort(n, descending):
     k[1, 7] = 0.0
     k[1, 8] = -0.0
     kd = k.cuda()
-    ok, oi = _ext.ops().radix_argsort_f32(kd, descending)
+    ok, oi = getattr(_ext.ops(), kernel)(kd, descending)
     rv, ri = torch.sort(k, dim=1, descending=bool(descending), stable=True)
     assert torch.equal(oi.cpu().long(), ri) and torch.allclose(ok.cpu(), rv, equal_nan=True)
 
