@@ -5,16 +5,22 @@
 //  * ant_rollout_reg_kernel (h1, h2 <= 64): weights in VGPRs, lane j = hidden unit j;
 //  * ant_rollout_kernel (larger layers): weights in LDS, lanes stride over units
 //    ((in, out) row-major, so a row read is contiguous across lanes).
-// The torso state is lane-uniform; lane quad position k owns leg k (its two joints and
-// the leg's relative momentum).  Per 10 ms semi-implicit sub-step (5 per control step) a
-// leg lane evaluates the knee/foot capsule-cap contacts, its joint-space dynamics (mass
-// matrix, Coriolis, gravity and contact generalized forces), and the change of the leg's
-// relative linear/angular momentum; the quad sums (DPP) drive the composite torso.  Waves leave
-// the loop independently when their episode ends (sticky done), so there are no
-// block barriers after the weight load.
 //
-// Semantics mirror evoxmi/problems/neuroevolution/reinforcement_learning/envs.py:Ant
-// (the CPU reference); constants below must match ANT there.
+// Physics (mirrors evoxmi/problems/neuroevolution/reinforcement_learning/envs.py:Ant, the CPU
+// oracle; constants below must match ANT / ant_derived there): the free-floating 14-DOF tree
+// (torso + 4 × thigh/shin) in generalized coordinates, integrated in momentum form.  The torso
+// state and the system's world momentum (P, L about the world origin) are quad-uniform; lane
+// quad position k owns leg k: its two hinges, their generalized momenta, and per 10 ms sub-step
+//  1. positions from the current velocities,
+//  2. knee/foot capsule-cap contacts, generalized forces, the closed-form velocity-product
+//     terms ∂T/∂q of its two links, the hinge-momentum update,
+//  3. its Schur-complement share of the 6×6 torso system (composite inertia of the pose minus
+//     b bᵀ/H of its two hinge columns, 21 entries) and of the right-hand side (6), plus its
+//     external wrench (6) — 33 quad sums (DPP) —
+//  4. a lane-uniform 6×6 LDLᵀ solve for the torso velocity, then its hinge rates by
+//     back-substitution.
+// Waves leave the loop independently when their episode ends (sticky done), so there are no
+// block barriers after the weight load.
 #include "evoxmi_common.h"
 
 namespace {
@@ -22,18 +28,21 @@ namespace {
 constexpr float DT = 0.01f, GEAR = 150.f, ARM = 30.f, JD = 1.f, LIMK = 500.f;
 constexpr float HIP_LO = -0.5236f, HIP_HI = 0.5236f, ANK_LO = 0.5236f, ANK_HI = 1.2217f;
 constexpr float L1 = 0.2828f, L2 = 0.5657f, HIPR = 0.2828f, ADAMP = 0.5f, LDAMP = 0.05f;
-constexpr float M1 = 0.8f, M2 = 1.2f;                     // thigh, shin
-constexpr float I1 = M1 * L1 * L1 / 12.f, I2 = M2 * L2 * L2 / 12.f;
-constexpr float MTOT = 10.f + 4.f * (M1 + M2);
-constexpr float IC = 4.474515846961317f;                  // ant_derived()["i_c"] in envs.py
+constexpr float M0 = 10.f, I0 = 1.f, M1 = 0.8f, M2 = 1.2f;  // torso, thigh, shin
 constexpr float RAD = 0.08f, KC = 2000.f, CC = 60.f, MU = 1.f, EPSV = 0.05f, GRAV = 9.81f;
-constexpr float RK = HIPR + L1, R1 = HIPR + 0.5f * L1;
+constexpr float IP1 = M1 * (L1 * L1 / 12.f + RAD * RAD / 4.f), IA1 = M1 * RAD * RAD / 2.f;
+constexpr float IP2 = M2 * (L2 * L2 / 12.f + RAD * RAD / 4.f), IA2 = M2 * RAD * RAD / 2.f;
+constexpr float MTOT = M0 + 4.f * (M1 + M2);
 constexpr int SUB = 5;
 __constant__ float LEG_ANG[4] = {0.7854f, 2.3562f, 3.9270f, 5.4978f};
 __constant__ float ANK_SGN[4] = {1.f, -1.f, -1.f, 1.f};
 
-struct AntBody {
-  float p[3], q[4], v[3], w[3];
+struct AntBody {  // quad-uniform: torso pose / world velocities and the system's world momentum
+  float p[3], q[4], v[3], w[3], P[3], L[3];
+};
+struct AntLeg {  // per lane: this lane's leg (raw joint coordinates)
+  float hq, aq, hqd, aqd, pih, pik;
+  float hx, hy, sg, base;
 };
 
 __device__ __forceinline__ void cross(const float* a, const float* b, float* o) {
@@ -41,20 +50,8 @@ __device__ __forceinline__ void cross(const float* a, const float* b, float* o) 
   o[1] = a[2] * b[0] - a[0] * b[2];
   o[2] = a[0] * b[1] - a[1] * b[0];
 }
+__device__ __forceinline__ float dot3(const float* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 
-__device__ __forceinline__ void qrot(const float* q, const float* v, float* o) {
-  float t[3], u[3];
-  const float xyz[3] = {q[1], q[2], q[3]};
-  cross(xyz, v, t);
-  t[0] *= 2.f; t[1] *= 2.f; t[2] *= 2.f;
-  cross(xyz, t, u);
-  for (int k = 0; k < 3; ++k) o[k] = v[k] + q[0] * t[k] + u[k];
-}
-
-// Lane-split sub-step for the register kernel: the four legs are evaluated in
-// parallel by lane groups (leg = lane & 3) instead of redundantly by every lane,
-// and the per-leg force/torque are summed across each quad with two DPP
-// quad-permutes.  Joint and body integration stay lane-uniform.
 __device__ __forceinline__ float quad_sum(float v) {
   v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));  // xor 1
   v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));  // xor 2
@@ -70,11 +67,6 @@ __device__ __forceinline__ float rl(float v, int l) {
 }
 __device__ __forceinline__ float sel4(int k, float a, float b, float c, float d) {
   return k == 0 ? a : (k == 1 ? b : (k == 2 ? c : d));
-}
-
-__device__ __forceinline__ void qrot_inv(const float* q, const float* v, float* o) {
-  const float qc[4] = {q[0], -q[1], -q[2], -q[3]};
-  qrot(qc, v, o);
 }
 
 // rotation matrix of a unit quaternion (row-major): R v and Rᵀ v then cost 9 FMAs each
@@ -93,158 +85,358 @@ __device__ __forceinline__ void mrot_t(const float* R, const float* v, float* o)
   for (int i = 0; i < 3; ++i) o[i] = R[i] * v[0] + R[3 + i] * v[1] + R[6 + i] * v[2];
 }
 
-// leg's linear / angular momentum relative to the torso frame (angular about the torso
-// origin); mirrors Ant._rel_momentum in envs.py
-__device__ __forceinline__ void leg_momentum(float cphi, float sphi, float ca, float sa, float phid, float ad, float* p, float* L) {
-  const float er[3] = {cphi, sphi, 0.f}, ep[3] = {-sphi, cphi, 0.f};
-  const float r2 = RK + 0.5f * L2 * ca;
-  const float c1[3] = {R1 * cphi, R1 * sphi, 0.f};
-  const float c2[3] = {r2 * cphi, r2 * sphi, -0.5f * L2 * sa};
-  float v1[3], v2[3], t1[3], t2[3];
+// pose of this lane's leg in the torso frame (Ant._kin in envs.py)
+struct LegPose {
+  float cphi, sphi, ca, sa;
+  float er[3], ep[3], d[3], dd[3], c1[3], K[3], c2[3], F[3];
+  float t1[3], t2[3], s2[3];
+};
+__device__ __forceinline__ void leg_pose(const AntLeg& g, LegPose& k) {
+  const float phi = g.base + g.hq, a = g.aq * g.sg;
+  k.cphi = __cosf(phi);
+  k.sphi = __sinf(phi);
+  k.ca = __cosf(a);
+  k.sa = __sinf(a);
+  const float er[3] = {k.cphi, k.sphi, 0.f}, ep[3] = {-k.sphi, k.cphi, 0.f};
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    v1[k] = R1 * phid * ep[k];
-    v2[k] = r2 * phid * ep[k] - 0.5f * L2 * sa * ad * er[k];
+  for (int i = 0; i < 3; ++i) {
+    k.er[i] = er[i];
+    k.ep[i] = ep[i];
+    k.d[i] = k.ca * er[i];
+    k.dd[i] = -k.sa * er[i];
   }
-  v2[2] -= 0.5f * L2 * ca * ad;
-  cross(c1, v1, t1);
-  cross(c2, v2, t2);
+  k.d[2] = -k.sa;
+  k.dd[2] = -k.ca;
+  const float h[3] = {g.hx, g.hy, 0.f};
+  const float r2c = L1 + 0.5f * L2 * k.ca;
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    p[k] = M1 * v1[k] + M2 * v2[k];
-    L[k] = M1 * t1[k] + M2 * t2[k] + I2 * ad * ep[k];
+  for (int i = 0; i < 3; ++i) {
+    k.c1[i] = h[i] + 0.5f * L1 * er[i];
+    k.K[i] = h[i] + L1 * er[i];
+    k.c2[i] = k.K[i] + 0.5f * L2 * k.d[i];
+    k.F[i] = k.K[i] + L2 * k.d[i];
+    k.t1[i] = 0.5f * L1 * ep[i];
+    k.t2[i] = r2c * ep[i];
+    k.s2[i] = 0.5f * L2 * k.dd[i];
   }
-  L[2] += (I1 + I2 * ca * ca) * phid;
 }
 
-// penalty contact of a capsule end-cap sphere at torso-frame point x (joint-driven velocity
-// xd): world force f, its torque about the torso origin, and the torso-frame force
-__device__ __forceinline__ void cap_contact(const AntBody& s, const float* R, const float* x, const float* xd, float* F, float* T,
-                                            float* ft) {
-  float r[3], dr[3], wr[3];
-  mrot(R, x, r);
-  mrot(R, xd, dr);
-  cross(s.w, r, wr);
-  const float pz = s.p[2] + r[2];
-  const float pv[3] = {s.v[0] + wr[0] + dr[0], s.v[1] + wr[1] + dr[1], s.v[2] + wr[2] + dr[2]};
+// columns of M_bj for φ̇ and ȧ (linear | angular about the torso origin) and the joint diagonal
+__device__ __forceinline__ void leg_columns(const LegPose& k, float* bphi, float* ba, float& Hphi, float& Ha) {
+  float x1[3], x2[3], x3[3];
+  cross(k.c1, k.t1, x1);
+  cross(k.c2, k.t2, x2);
+  cross(k.c2, k.s2, x3);
+  const float cz = (IA2 - IP2) * k.sa;  // I2 e_z = IP2 e_z - (IA2 - IP2) sa d
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    bphi[i] = M1 * k.t1[i] + M2 * k.t2[i];
+    bphi[3 + i] = M1 * x1[i] + M2 * x2[i] - cz * k.d[i];
+    ba[i] = M2 * k.s2[i];
+    ba[3 + i] = M2 * x3[i] + IP2 * k.ep[i];
+  }
+  bphi[5] += IP1 + IP2;
+  Hphi = M1 * dot3(k.t1, k.t1) + M2 * dot3(k.t2, k.t2) + IP1 + IP2 + (IA2 - IP2) * k.sa * k.sa + ARM;
+  Ha = M2 * dot3(k.s2, k.s2) + IP2 + ARM;
+}
+
+// link velocities (torso frame) and the rod-inertia angular momenta
+__device__ __forceinline__ void leg_vel(const LegPose& k, const float* vB, const float* wB, float phid, float ad, float* V1, float* V2,
+                                        float* O2, float* IO1, float* IO2) {
+  float a1[3], a2[3];
+  cross(wB, k.c1, a1);
+  cross(wB, k.c2, a2);
+  float O1[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    V1[i] = vB[i] + a1[i] + k.t1[i] * phid;
+    V2[i] = vB[i] + a2[i] + k.t2[i] * phid + k.s2[i] * ad;
+    O1[i] = wB[i];
+    O2[i] = wB[i] + k.ep[i] * ad;
+  }
+  O1[2] += phid;
+  O2[2] += phid;
+  const float e1 = (IA1 - IP1) * dot3(k.er, O1), e2 = (IA2 - IP2) * dot3(k.d, O2);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    IO1[i] = IP1 * O1[i] + e1 * k.er[i];
+    IO2[i] = IP2 * O2[i] + e2 * k.d[i];
+  }
+}
+
+// penalty contact of a capsule end-cap sphere at torso-frame point x with torso-frame velocity
+// vb: the contact force in the torso frame
+__device__ __forceinline__ void cap_contact(const AntBody& s, const float* R, const float* x, const float* vb, float* fb) {
+  float vw[3];
+  mrot(R, vb, vw);
+  const float pz = s.p[2] + R[6] * x[0] + R[7] * x[1] + R[8] * x[2];
   const float pen = fmaxf(RAD - pz, 0.f);
-  const float fn = fmaxf(KC * pen - CC * pv[2] * (pen > 0.f ? 1.f : 0.f), 0.f);
-  const float ivn = rsqrtf(pv[0] * pv[0] + pv[1] * pv[1] + EPSV * EPSV);
-  const float f[3] = {-MU * fn * pv[0] * ivn, -MU * fn * pv[1] * ivn, fn};
-  float tq[3];
-  cross(r, f, tq);
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    F[k] += f[k];
-    T[k] += tq[k];
-  }
-  mrot_t(R, f, ft);
+  const float fn = fmaxf(KC * pen - CC * vw[2] * (pen > 0.f ? 1.f : 0.f), 0.f);
+  const float ivn = rsqrtf(vw[0] * vw[0] + vw[1] * vw[1] + EPSV * EPSV);
+  const float f[3] = {-MU * fn * vw[0] * ivn, -MU * fn * vw[1] * ivn, fn};
+  mrot_t(R, f, fb);
 }
 
-// One sub-step of the articulated Ant for this lane's leg (hip yaw q_h, ankle q_a with
-// sign sg, base yaw angle base); pm / Lm: the leg's relative momentum after the previous
-// sub-step (a function of the joint state, carried to avoid recomputing it).  Mirrors
-// Ant._substep in envs.py.
-__device__ __forceinline__ void art_substep(AntBody& s, float& hq, float& aq, float& hqd, float& aqd, float th, float ta,
-                                            float base, float sg, float* pm, float* Lm, float* tc) {
-  const float phid = hqd, ad = aqd * sg;
-  const float cphi = tc[0], sphi = tc[1], ca = tc[2], sa = tc[3];  // of the current joint state
+// 6×6 SPD solve A x = b (A symmetric, upper part used; fully unrolled, lane-uniform)
+__device__ __forceinline__ void solve6(float (&A)[6][6], float (&b)[6], float (&x)[6]) {
+  float inv[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    inv[k] = __builtin_amdgcn_rcpf(A[k][k]);
+#pragma unroll
+    for (int i = k + 1; i < 6; ++i) {
+      const float f = A[k][i] * inv[k];
+#pragma unroll
+      for (int j = i; j < 6; ++j) A[i][j] -= f * A[k][j];
+      b[i] -= f * b[k];
+    }
+  }
+#pragma unroll
+  for (int k = 5; k >= 0; --k) {
+    float r = b[k];
+#pragma unroll
+    for (int j = k + 1; j < 6; ++j) r -= A[k][j] * x[j];
+    x[k] = r * inv[k];
+  }
+}
+
+// velocities from the momenta at the current pose (Schur complement over the legs)
+__device__ __forceinline__ void solve_velocities(AntBody& s, AntLeg& g, const LegPose& k, const float* R) {
+  float bphi[6], ba[6], Hphi, Ha;
+  leg_columns(k, bphi, ba, Hphi, Ha);
+  const float iHp = __builtin_amdgcn_rcpf(Hphi), iHa = __builtin_amdgcn_rcpf(Ha);
+  const float pphi = g.pih, pa = g.pik * g.sg;
+  // this leg's composite inertia about the torso origin (thigh along er, shin along d)
+  float S1[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) S1[i] = M1 * k.c1[i] + M2 * k.c2[i];
+  const float n1 = M1 * dot3(k.c1, k.c1) + M2 * dot3(k.c2, k.c2) + IP1 + IP2;
+  float sp[6], sa_[6];  // the hinge columns scaled by 1/H
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    sp[i] = bphi[i] * iHp;
+    sa_[i] = ba[i] * iHa;
+  }
+  float A[6][6], b[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+#pragma unroll
+    for (int j = i; j < 6; ++j) {
+      float m = 0.f;
+      if (i >= 3 && j >= 3) {
+        const int r = i - 3, c = j - 3;
+        m = (IA1 - IP1) * k.er[r] * k.er[c] + (IA2 - IP2) * k.d[r] * k.d[c] - M1 * k.c1[r] * k.c1[c] - M2 * k.c2[r] * k.c2[c];
+        if (r == c) m += n1;
+      } else if (i < 3 && j >= 3) {  // −[S1]×
+        const int r = i, c = j - 3;
+        if (r == 0 && c == 1) m = S1[2];
+        if (r == 0 && c == 2) m = -S1[1];
+        if (r == 1 && c == 0) m = -S1[2];
+        if (r == 1 && c == 2) m = S1[0];
+        if (r == 2 && c == 0) m = S1[1];
+        if (r == 2 && c == 1) m = -S1[0];
+      }
+      A[i][j] = quad_sum(m - sp[i] * bphi[j] - sa_[i] * ba[j]);
+    }
+    b[i] = quad_sum(-sp[i] * pphi - sa_[i] * pa);
+  }
+  A[0][0] += MTOT; A[1][1] += MTOT; A[2][2] += MTOT;
+  A[3][3] += I0; A[4][4] += I0; A[5][5] += I0;
+  {
+    float hP[3], pxP[3], Lo[3], hL[3];
+    mrot_t(R, s.P, hP);
+    cross(s.p, s.P, pxP);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) Lo[i] = s.L[i] - pxP[i];
+    mrot_t(R, Lo, hL);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      b[i] += hP[i];
+      b[3 + i] += hL[i];
+    }
+  }
+  float u[6];
+  solve6(A, b, u);
+  float bu = 0.f, au = 0.f;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    bu += bphi[i] * u[i];
+    au += ba[i] * u[i];
+  }
+  g.hqd = (pphi - bu) * iHp;
+  g.aqd = g.sg * (pa - au) * iHa;
+  mrot(R, u, s.v);
+  mrot(R, u + 3, s.w);
+}
+
+// momenta of the initial state (Ant.initial_momenta in envs.py)
+__device__ __forceinline__ void init_momenta(AntBody& s, AntLeg& g) {
   float R[9];
   quat_mat(s.q, R);
-  const float er[3] = {cphi, sphi, 0.f}, ep[3] = {-sphi, cphi, 0.f};
-  const float rf = RK + L2 * ca;
-  float F[3] = {0.f, 0.f, 0.f}, T[3] = {0.f, 0.f, 0.f}, fk[3], ff[3];
-  {
-    const float xk[3] = {RK * cphi, RK * sphi, 0.f};
-    const float vk[3] = {RK * phid * ep[0], RK * phid * ep[1], 0.f};
-    cap_contact(s, R, xk, vk, F, T, fk);
-    const float xf[3] = {rf * cphi, rf * sphi, -L2 * sa};
-    const float vf[3] = {rf * phid * ep[0] - L2 * sa * ad * er[0], rf * phid * ep[1] - L2 * sa * ad * er[1], -L2 * ca * ad};
-    cap_contact(s, R, xf, vf, F, T, ff);
-  }
-  const float gt[3] = {-GRAV * R[6], -GRAV * R[7], -GRAV * R[8]};  // Rᵀ (0, 0, −g)
-  const float r2 = RK + 0.5f * L2 * ca;
-  const float gp = gt[0] * ep[0] + gt[1] * ep[1], gr = gt[0] * er[0] + gt[1] * er[1];
-  const float Qphi = (M1 * R1 + M2 * r2) * gp + RK * (fk[0] * ep[0] + fk[1] * ep[1]) + rf * (ff[0] * ep[0] + ff[1] * ep[1]);
-  const float Qa = M2 * (-0.5f * L2) * (sa * gr + ca * gt[2]) + L2 * (-sa * (ff[0] * er[0] + ff[1] * er[1]) - ca * ff[2]);
-  const float mag = aq * sg;
-  const float vh = fmaxf(HIP_LO - hq, 0.f) - fmaxf(hq - HIP_HI, 0.f);
-  const float va = fmaxf(ANK_LO - mag, 0.f) - fmaxf(mag - ANK_HI, 0.f);
-  const float Qh = th - JD * hqd + LIMK * vh + Qphi;
-  const float Qq = ta - JD * aqd + LIMK * va * sg + sg * Qa;
-  const float H11 = ARM + M1 * R1 * R1 + I1 + M2 * r2 * r2 + I2 * ca * ca;
-  const float H22 = ARM + M2 * (0.25f * L2 * L2) + I2;
-  const float dH = -M2 * L2 * r2 * sa - 2.f * I2 * ca * sa;
-  const float hdd = (Qh - dH * hqd * ad) * __builtin_amdgcn_rcpf(H11);
-  const float add = (Qq + sg * 0.5f * dH * hqd * hqd) * __builtin_amdgcn_rcpf(H22);
-  hqd += DT * hdd;
-  aqd += DT * add;
-  hq += DT * hqd;
-  aq += DT * aqd;
-  float p1[3], L1m[3];
-  {
-    const float phi1 = base + hq, a1 = aq * sg;
-    tc[0] = __cosf(phi1);
-    tc[1] = __sinf(phi1);
-    tc[2] = __cosf(a1);
-    tc[3] = __sinf(a1);
-    leg_momentum(tc[0], tc[1], tc[2], tc[3], hqd, aqd * sg, p1, L1m);
-  }
-  // per leg, torso frame: momentum change, first moment of the link masses
-  // this leg's wrench on the torso (world frame): contact forces / torques, minus the rate
-  // of the leg's relative momentum, plus the gravity torque of its links — rotated per lane
-  // so that only 6 values need the quad sum
-  float dpl[3], dLl[3], cgl[3];
-  {
-    float t0[3], t1[3];
+  LegPose k;
+  leg_pose(g, k);
+  float vB[3], wB[3], V1[3], V2[3], O2[3], IO1[3], IO2[3];
+  mrot_t(R, s.v, vB);
+  mrot_t(R, s.w, wB);
+  const float phid = g.hqd, ad = g.aqd * g.sg;
+  leg_vel(k, vB, wB, phid, ad, V1, V2, O2, IO1, IO2);
+  float x1[3], x2[3], PB[3], LB[3];
+  cross(k.c1, V1, x1);
+  cross(k.c2, V2, x2);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      t0[k] = p1[k] - pm[k];
-      t1[k] = L1m[k] - Lm[k];
-      pm[k] = p1[k];
-      Lm[k] = L1m[k];
-    }
-    const float cg[3] = {(M1 * R1 + M2 * r2) * cphi, (M1 * R1 + M2 * r2) * sphi, -M2 * 0.5f * L2 * sa};
-    mrot(R, t0, dpl);
-    mrot(R, t1, dLl);
-    mrot(R, cg, cgl);
+  for (int i = 0; i < 3; ++i) {
+    PB[i] = M0 * vB[i] + quad_sum(M1 * V1[i] + M2 * V2[i]);
+    LB[i] = I0 * wB[i] + quad_sum(M1 * x1[i] + M2 * x2[i] + IO1[i] + IO2[i]);
   }
-  float X[6];
-  // cross(R·cg, (0, 0, −g)) = (−g·cg_y, g·cg_x, 0)
-  X[0] = F[0] - dpl[0] * (1.f / DT);
-  X[1] = F[1] - dpl[1] * (1.f / DT);
-  X[2] = F[2] - dpl[2] * (1.f / DT);
-  X[3] = T[0] - dLl[0] * (1.f / DT) - GRAV * cgl[1];
-  X[4] = T[1] - dLl[1] * (1.f / DT) + GRAV * cgl[0];
-  X[5] = T[2] - dLl[2] * (1.f / DT);
+  mrot(R, PB, s.P);
+  float Lw[3], pxP[3];
+  mrot(R, LB, Lw);
+  cross(s.p, s.P, pxP);
 #pragma unroll
-  for (int k = 0; k < 6; ++k) X[k] = quad_sum(X[k]);
-  const float gw[3] = {0.f, 0.f, -GRAV};
+  for (int i = 0; i < 3; ++i) s.L[i] = Lw[i] + pxP[i];
+  float bphi[6], ba[6], Hphi, Ha;
+  leg_columns(k, bphi, ba, Hphi, Ha);
+  const float ub[6] = {vB[0], vB[1], vB[2], wB[0], wB[1], wB[2]};
+  float pphi = Hphi * phid, pa = Ha * ad;
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const float force = X[k] + MTOT * gw[k] - LDAMP * s.v[k];
-    const float torque = X[3 + k] - ADAMP * s.w[k];
-    s.v[k] += DT * force * (1.f / MTOT);
-    s.w[k] += DT * torque * (1.f / IC);
-    s.p[k] += DT * s.v[k];
+  for (int i = 0; i < 6; ++i) {
+    pphi += bphi[i] * ub[i];
+    pa += ba[i] * ub[i];
   }
-  const float w = s.q[0], x = s.q[1], y = s.q[2], z = s.q[3];
-  const float ox = s.w[0], oy = s.w[1], oz = s.w[2];
-  float nq[4] = {w + DT * 0.5f * (-ox * x - oy * y - oz * z), x + DT * 0.5f * (ox * w + oy * z - oz * y),
-                 y + DT * 0.5f * (oy * w + oz * x - ox * z), z + DT * 0.5f * (oz * w + ox * y - oy * x)};
-  const float in = rsqrtf(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
-#pragma unroll
-  for (int c = 0; c < 4; ++c) s.q[c] = nq[c] * in;
+  g.pih = pphi;
+  g.pik = g.sg * pa;
 }
 
-__device__ __forceinline__ void init_leg_momentum(float hq, float aq, float hqd, float aqd, float base, float sg, float* pm, float* Lm,
-                                                  float* tc) {
-  const float phi = base + hq, a = aq * sg;
-  tc[0] = __cosf(phi);
-  tc[1] = __sinf(phi);
-  tc[2] = __cosf(a);
-  tc[3] = __sinf(a);
-  leg_momentum(tc[0], tc[1], tc[2], tc[3], hqd, aqd * sg, pm, Lm);
+// One 10 ms sub-step (Ant._substep in envs.py); th / ta: this lane's leg torques
+__device__ __forceinline__ void art_substep(AntBody& s, AntLeg& g, float th, float ta) {
+  // 1. positions with the current velocities
+#pragma unroll
+  for (int i = 0; i < 3; ++i) s.p[i] += DT * s.v[i];
+  {
+    const float w = s.q[0], x = s.q[1], y = s.q[2], z = s.q[3];
+    const float ox = s.w[0], oy = s.w[1], oz = s.w[2];
+    float nq[4] = {w + DT * 0.5f * (-ox * x - oy * y - oz * z), x + DT * 0.5f * (ox * w + oy * z - oz * y),
+                   y + DT * 0.5f * (oy * w + oz * x - ox * z), z + DT * 0.5f * (oz * w + ox * y - oy * x)};
+    const float in = rsqrtf(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) s.q[c] = nq[c] * in;
+  }
+  g.hq += DT * g.hqd;
+  g.aq += DT * g.aqd;
+  // 2. forces and velocity-product terms at the new pose, old velocities
+  float R[9];
+  quat_mat(s.q, R);
+  LegPose k;
+  leg_pose(g, k);
+  float vB[3], wB[3];
+  mrot_t(R, s.v, vB);
+  mrot_t(R, s.w, wB);
+  const float phid = g.hqd, ad = g.aqd * g.sg;
+  float V1[3], V2[3], O2[3], IO1[3], IO2[3];
+  leg_vel(k, vB, wB, phid, ad, V1, V2, O2, IO1, IO2);
+  float fK[3], fF[3];
+  {
+    float a[3], vk[3], vf[3];
+    cross(wB, k.K, a);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) vk[i] = vB[i] + a[i] + L1 * phid * k.ep[i];
+    cross(wB, k.F, a);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) vf[i] = vB[i] + a[i] + L1 * phid * k.ep[i] + L2 * (phid * k.ca * k.ep[i] + ad * k.dd[i]);
+    cap_contact(s, R, k.K, vk, fK);
+    cap_contact(s, R, k.F, vf, fF);
+  }
+  const float gB[3] = {-GRAV * R[6], -GRAV * R[7], -GRAV * R[8]};
+  // contact moments about the hip, the legs' first mass moment S1 = m1 c1 + m2 c2
+  float Tk[3], S1[3], fs[3];
+  {
+    float kh[3] = {k.K[0] - g.hx, k.K[1] - g.hy, k.K[2]}, fh[3] = {k.F[0] - g.hx, k.F[1] - g.hy, k.F[2]}, a[3], b[3];
+    cross(kh, fK, a);
+    cross(fh, fF, b);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      Tk[i] = a[i] + b[i];
+      S1[i] = M1 * k.c1[i] + M2 * k.c2[i];
+      fs[i] = fK[i] + fF[i];
+    }
+  }
+  // e_z · [(S1 − m_leg h) × g + Tk];  e_p · [(c2 − K) × m2 g + (F − K) × fF] = L2 δd · (½ m2 g + fF)
+  const float Qphi = (S1[0] - (M1 + M2) * g.hx) * gB[1] - (S1[1] - (M1 + M2) * g.hy) * gB[0] + Tk[2];
+  const float Qa = L2 * (k.dd[0] * (0.5f * M2 * gB[0] + fF[0]) + k.dd[1] * (0.5f * M2 * gB[1] + fF[1]) + k.dd[2] * (0.5f * M2 * gB[2] + fF[2]));
+  float dphi, da;
+  {
+    float r1[3], r2[3], q1[3], q2[3];
+    const float wz = wB[2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      r1[i] = 0.5f * L1 * k.er[i];
+      r2[i] = L1 * k.er[i] + 0.5f * L2 * k.d[i];
+    }
+    const float wr1 = dot3(wB, r1), wr2 = dot3(wB, r2);
+    const float a2 = (L1 + 0.5f * L2 * k.ca) * phid, b2 = 0.5f * L2 * ad * k.sa;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      q1[i] = -r1[i] * wz - 0.5f * L1 * phid * k.er[i];
+      q2[i] = -r2[i] * wz - a2 * k.er[i] - b2 * k.ep[i];
+    }
+    q1[2] += wr1;
+    q2[2] += wr2;
+    const float IOx = IO1[0] + IO2[0], IOy = IO1[1] + IO2[1];
+    dphi = M1 * dot3(V1, q1) + M2 * dot3(V2, q2) - (wB[0] * IOy - wB[1] * IOx);
+    float dc2[3];
+    cross(wB, k.s2, dc2);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) dc2[i] += 0.5f * L2 * (-phid * k.sa * k.ep[i] - ad * k.d[i]);
+    da = M2 * dot3(V2, dc2) + (IA2 - IP2) * dot3(O2, k.dd) * dot3(O2, k.d);
+  }
+  const float mag = g.aq * g.sg;
+  const float vh = fmaxf(HIP_LO - g.hq, 0.f) - fmaxf(g.hq - HIP_HI, 0.f);
+  const float va = fmaxf(ANK_LO - mag, 0.f) - fmaxf(mag - ANK_HI, 0.f);
+  g.pih += DT * (th - JD * g.hqd + LIMK * vh + Qphi + dphi);
+  g.pik += DT * (ta - JD * g.aqd + LIMK * va * g.sg + g.sg * (Qa + da));
+  // external wrench on the system: contacts and the legs' weight about the torso origin
+  // (Tk + h × fs + S1 × g per leg)
+  {
+    float X[6], a[3], b[3];
+    const float h[3] = {g.hx, g.hy, 0.f};
+    cross(h, fs, a);
+    cross(S1, gB, b);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      X[i] = quad_sum(fs[i]);
+      X[3 + i] = quad_sum(Tk[i] + a[i] + b[i]);
+    }
+    float FW[3], TW[3], pxF[3];
+    mrot(R, X, FW);
+    FW[0] -= LDAMP * s.v[0];
+    FW[1] -= LDAMP * s.v[1];
+    FW[2] += -MTOT * GRAV - LDAMP * s.v[2];
+    mrot(R, X + 3, TW);
+    cross(s.p, FW, pxF);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      s.P[i] += DT * FW[i];
+      s.L[i] += DT * (TW[i] + pxF[i] - ADAMP * s.w[i]);
+    }
+  }
+  // 3. velocities from the momenta at the new pose
+  solve_velocities(s, g, k, R);
+}
+
+__device__ __forceinline__ void load_body(AntBody& s, AntLeg& g, const float* __restrict__ init, int leg) {
+  for (int i = 0; i < 3; ++i) s.p[i] = init[i];
+  for (int i = 0; i < 4; ++i) s.q[i] = init[3 + i];
+  for (int i = 0; i < 3; ++i) s.v[i] = init[7 + i];
+  for (int i = 0; i < 3; ++i) s.w[i] = init[10 + i];
+  g.hq = init[13 + 2 * leg];
+  g.aq = init[14 + 2 * leg];
+  g.hqd = init[21 + 2 * leg];
+  g.aqd = init[22 + 2 * leg];
+  g.base = LEG_ANG[leg];
+  g.sg = ANK_SGN[leg];
+  g.hx = HIPR * __cosf(g.base);
+  g.hy = HIPR * __sinf(g.base);
+  init_momenta(s, g);
 }
 
 // layer sizes: in = 27, hidden h1, h2 (any, ≤ 256), out = 8; tanh everywhere
@@ -271,14 +463,9 @@ __global__ void __launch_bounds__(256) ant_rollout_kernel(const float* __restric
   const float* W3 = B2 + h2;
   const float* B3 = W3 + h2 * 8;
   AntBody s;
-  for (int i = 0; i < 3; ++i) s.p[i] = init[i];
-  for (int i = 0; i < 4; ++i) s.q[i] = init[3 + i];
-  for (int i = 0; i < 3; ++i) s.v[i] = init[7 + i];
-  for (int i = 0; i < 3; ++i) s.w[i] = init[10 + i];
+  AntLeg g;
   const int leg = lane & 3;
-  float hq = init[13 + 2 * leg], aq = init[14 + 2 * leg], hqd = init[21 + 2 * leg], aqd = init[22 + 2 * leg];
-  float pm[3], Lm[3], tc[4];
-  init_leg_momentum(hq, aq, hqd, aqd, LEG_ANG[leg], ANK_SGN[leg], pm, Lm, tc);
+  load_body(s, g, init, leg);
   float total = 0.f;
   int t = 0;
   for (; t < cap; ++t) {
@@ -286,10 +473,10 @@ __global__ void __launch_bounds__(256) ant_rollout_kernel(const float* __restric
     float jq[8], jqd[8];
 #pragma unroll
     for (int l = 0; l < 4; ++l) {
-      jq[2 * l] = rl(hq, l);
-      jq[2 * l + 1] = rl(aq, l);
-      jqd[2 * l] = rl(hqd, l);
-      jqd[2 * l + 1] = rl(aqd, l);
+      jq[2 * l] = rl(g.hq, l);
+      jq[2 * l + 1] = rl(g.aq, l);
+      jqd[2 * l] = rl(g.hqd, l);
+      jqd[2 * l + 1] = rl(g.aqd, l);
     }
     if (lane == 0) {
       a0[0] = s.p[2];
@@ -334,7 +521,7 @@ __global__ void __launch_bounds__(256) ant_rollout_kernel(const float* __restric
     __builtin_amdgcn_wave_barrier();  // a0..a3 are rewritten next step
     const float x0 = s.p[0];
     const float th = sel4(leg, tau[0], tau[2], tau[4], tau[6]), ta = sel4(leg, tau[1], tau[3], tau[5], tau[7]);
-    for (int k = 0; k < SUB; ++k) art_substep(s, hq, aq, hqd, aqd, th, ta, LEG_ANG[leg], ANK_SGN[leg], pm, Lm, tc);
+    for (int k = 0; k < SUB; ++k) art_substep(s, g, th, ta);
     const bool healthy = (s.p[2] >= 0.2f) && (s.p[2] <= 1.0f);
     if (!healthy) break;  // sticky done: the terminating step earns nothing
     total += (s.p[0] - x0) * (1.f / (DT * SUB)) + 1.f - 0.5f * csum;
@@ -397,18 +584,11 @@ __global__ void __launch_bounds__(64, 2) ant_rollout_reg_kernel(const float* __r
     w3[k] = u2 ? W3[lane * 8 + k] : 0.f;
     b3[k] = B3[k];
   }
-  AntBody s;
-  for (int i = 0; i < 3; ++i) s.p[i] = init[i];
-  for (int i = 0; i < 4; ++i) s.q[i] = init[3 + i];
-  for (int i = 0; i < 3; ++i) s.v[i] = init[7 + i];
-  for (int i = 0; i < 3; ++i) s.w[i] = init[10 + i];
-  const int lg = lane & 3;
-  float hq = init[13 + 2 * lg], aq = init[14 + 2 * lg], hqd = init[21 + 2 * lg], aqd = init[22 + 2 * lg];
   const bool hb5 = lane & 32, hb4 = lane & 16, hb3 = lane & 8;
   const int leg = lane & 3;
-  const float lbase = LEG_ANG[leg], lsg = ANK_SGN[leg];
-  float pm[3], Lm[3], tc[4];
-  init_leg_momentum(hq, aq, hqd, aqd, lbase, lsg, pm, Lm, tc);
+  AntBody s;
+  AntLeg g;
+  load_body(s, g, init, leg);
   float total = 0.f;
   int t = 0;
   for (; t < cap; ++t) {
@@ -418,10 +598,10 @@ __global__ void __launch_bounds__(64, 2) ant_rollout_reg_kernel(const float* __r
     for (int i = 0; i < 4; ++i) o[1 + i] = s.q[i];
 #pragma unroll
     for (int l = 0; l < 4; ++l) {
-      o[5 + 2 * l] = rl(hq, l);
-      o[6 + 2 * l] = rl(aq, l);
-      o[19 + 2 * l] = rl(hqd, l);
-      o[20 + 2 * l] = rl(aqd, l);
+      o[5 + 2 * l] = rl(g.hq, l);
+      o[6 + 2 * l] = rl(g.aq, l);
+      o[19 + 2 * l] = rl(g.hqd, l);
+      o[20 + 2 * l] = rl(g.aqd, l);
     }
 #pragma unroll
     for (int i = 0; i < 3; ++i) o[13 + i] = s.v[i];
@@ -478,7 +658,7 @@ __global__ void __launch_bounds__(64, 2) ant_rollout_reg_kernel(const float* __r
     const float x0 = s.p[0];
     const float th = sel4(leg, tau[0], tau[2], tau[4], tau[6]), ta = sel4(leg, tau[1], tau[3], tau[5], tau[7]);
     #pragma unroll 1
-    for (int k = 0; k < SUB; ++k) art_substep(s, hq, aq, hqd, aqd, th, ta, lbase, lsg, pm, Lm, tc);
+    for (int k = 0; k < SUB; ++k) art_substep(s, g, th, ta);
     const bool healthy = (s.p[2] >= 0.2f) && (s.p[2] <= 1.0f);
     if (!healthy) break;
     total += (s.p[0] - x0) * (1.f / (DT * SUB)) + 1.f - 0.5f * csum;

@@ -16,7 +16,8 @@ import torch
 _LOCK = threading.Lock()
 _LOADED = False
 _ERROR = None
-SO_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_C.so")
+SO_PATH = os.environ.get("EVOXMI_SO") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_C.so")
+# EVOXMI_SO: an alternative build of the same extension (compiler-flag A/B runs)
 
 
 def load(build_if_missing: bool = True) -> bool:

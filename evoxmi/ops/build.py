@@ -57,7 +57,10 @@ def _run(cmd):
 # scalar FMAs; SLP vectorisation packs them into v_pk ops that need ~3 v_mov shuffles each
 # mo_geom.hip: its distance loop must stay unfused (bit-identical ties with the CPU
 # oracle); plain "fast" contraction ignores the in-source pragma
-FILE_FLAGS = {"eigh_sbr.hip": ["-fno-slp-vectorize"], "mo_geom.hip": ["-ffp-contract=fast-honor-pragmas"]}
+# neuro.hip: the Ant sub-step is scalar f32 arithmetic; SLP packing adds ~400 v_mov per
+# sub-step and pushes the register-resident rollout from 230 VGPRs (2 waves / SIMD) to 364
+FILE_FLAGS = {"eigh_sbr.hip": ["-fno-slp-vectorize"], "mo_geom.hip": ["-ffp-contract=fast-honor-pragmas"],
+              "neuro.hip": ["-fno-slp-vectorize"]}
 
 
 def build(verbose: bool = True, jobs: int = None) -> str:

@@ -42,6 +42,37 @@ class DTLZTestSuit(Problem):
     def pf(self):
         return self.sample()[0] / 2
 
+    # -- decision-axis sharding (P2, see evoxmi/parallel/dim_sharded.py): the m − 1 position
+    # variables travel as terms (from the rank owning each column), the distance function g
+    # is an additive row reduction over the last d − m + 1 variables
+    dim_halo = 0
+
+    def partial_terms(self, Xb, col0, d, own):
+        m = self.m
+        Xo = Xb[:, :own]
+        T = torch.zeros((Xb.shape[0], m), dtype=Xb.dtype, device=Xb.device)
+        hi = min(col0 + own, m - 1)
+        if hi > col0:
+            T[:, col0:hi] = Xo[:, : hi - col0]
+        s = max(m - 1 - col0, 0)
+        if s < own:
+            T[:, m - 1] = self._g_partial(Xo[:, s:])
+        return T
+
+    def combine_terms(self, T, d):
+        m = self.m
+        return self._objectives(T[:, : m - 1], self._g_from(T[:, m - 1 :], d))
+
+    def _g_partial(self, Y):
+        return ((Y - 0.5) ** 2).sum(1)
+
+    def _g_from(self, S, d):
+        return S
+
+    def evaluate(self, state, X):
+        m = self.m
+        return self._objectives(X[:, : m - 1], self._g_from(self._g_partial(X[:, m - 1 :])[:, None], X.shape[1])), state
+
 
 def _spherical(X, m, g):
     h = torch.clamp(torch.cos(X[:, : m - 1] * math.pi / 2), min=0)
@@ -74,8 +105,15 @@ class DTLZ1(DTLZTestSuit):
         if r is not None:
             return r, state
         m = self.m
-        g = _rastrigin_g(X, m)
-        return 0.5 * (1 + g) * _cumprod_front(X[:, : m - 1], 1 - X[:, : m - 1]), state
+        return self._objectives(X[:, : m - 1], _rastrigin_g(X, m)), state
+
+    _g_partial = staticmethod(lambda Y: ((Y - 0.5) ** 2 - torch.cos(20 * math.pi * (Y - 0.5))).sum(1))
+
+    def _g_from(self, S, d):
+        return 100 * (d - self.m + 1 + S)
+
+    def _objectives(self, Xp, g):
+        return 0.5 * (1 + g) * _cumprod_front(Xp, 1 - Xp)
 
 
 class DTLZ2(DTLZTestSuit):
@@ -92,6 +130,9 @@ class DTLZ2(DTLZTestSuit):
         g = ((X[:, m - 1 :] - 0.5) ** 2).sum(1, keepdim=True)
         return _spherical(X, m, g), state
 
+    def _objectives(self, Xp, g):
+        return _spherical(Xp, self.m, g)
+
     def pf(self):
         f = self.sample()[0]
         return f / torch.sqrt((f * f).sum(1, keepdim=True))
@@ -104,6 +145,9 @@ class DTLZ3(DTLZ2):
             return r, state
         return _spherical(X, self.m, _rastrigin_g(X, self.m)), state
 
+    _g_partial = staticmethod(DTLZ1._g_partial)
+    _g_from = DTLZ1._g_from
+
 
 class DTLZ4(DTLZ2):
     def evaluate(self, state, X):
@@ -114,6 +158,9 @@ class DTLZ4(DTLZ2):
         X = torch.cat([X[:, : m - 1] ** 100, X[:, m - 1 :]], 1)
         g = ((X[:, m - 1 :] - 0.5) ** 2).sum(1, keepdim=True)
         return _spherical(X, m, g), state
+
+    def _objectives(self, Xp, g):
+        return _spherical(Xp**100, self.m, g)
 
 
 def _degenerate_pf(ref_num, m):
@@ -135,23 +182,18 @@ class DTLZ5(DTLZTestSuit):
         d = m + 9 if d is None else d
         super().__init__(d, m, ref_num)
 
-    def _g(self, X):
-        return ((X[:, self.m - 1 :] - 0.5) ** 2).sum(1, keepdim=True)
-
-    def evaluate(self, state, X):
+    def _objectives(self, Xp, g):
         m = self.m
-        g = self._g(X)
         temp = g.expand(-1, max(m - 2, 0))
-        X = torch.cat([X[:, :1], (1 + 2 * temp * X[:, 1 : m - 1]) / (2 + 2 * temp), X[:, m - 1 :]], 1)
-        return _spherical(X, m, g), state
+        Xp = torch.cat([Xp[:, :1], (1 + 2 * temp * Xp[:, 1 : m - 1]) / (2 + 2 * temp)], 1)
+        return _spherical(Xp, m, g)
 
     def pf(self):
         return _degenerate_pf(self.ref_num, self.m)
 
 
 class DTLZ6(DTLZ5):
-    def _g(self, X):
-        return (X[:, self.m - 1 :] ** 0.1).sum(1, keepdim=True)
+    _g_partial = staticmethod(lambda Y: (Y**0.1).sum(1))
 
 
 class DTLZ7(DTLZTestSuit):
@@ -161,12 +203,14 @@ class DTLZ7(DTLZTestSuit):
         super().__init__(d, m, ref_num)
         self.sample = GridSampling(self.ref_num * self.m, self.m - 1)
 
-    def evaluate(self, state, X):
-        m = self.m
-        g = 1 + 9 * X[:, m - 1 :].mean(1, keepdim=True)
-        fm = X[:, : m - 1]
-        last = (1 + g) * (m - (fm / (1 + g) * (1 + torch.sin(3 * math.pi * fm))).sum(1, keepdim=True))
-        return torch.cat([fm, last], 1), state
+    _g_partial = staticmethod(lambda Y: Y.sum(1))
+
+    def _g_from(self, S, d):
+        return 1 + 9 * S / (d - self.m + 1)
+
+    def _objectives(self, fm, g):
+        last = (1 + g) * (self.m - (fm / (1 + g) * (1 + torch.sin(3 * math.pi * fm))).sum(1, keepdim=True))
+        return torch.cat([fm, last], 1)
 
     def pf(self):
         interval = torch.tensor([0, 0.251412, 0.631627, 0.859401])

@@ -18,7 +18,32 @@ class ZDTTestSuit(Problem):
         return X[:, 0]
 
     def _g(self, X):
-        return 1 + 9 * X[:, 1:].mean(1)
+        return self._g_from(self._g_partial(X[:, 1:]))
+
+    def _g_partial(self, Y):
+        return Y.sum(1)
+
+    def _g_from(self, S):
+        return 1 + 9 * S / (self.n - 1)
+
+    # -- decision-axis sharding (P2, evoxmi/parallel/dim_sharded.py): x_1 from its owner and
+    # the additive part of g
+    dim_halo = 0
+
+    def partial_terms(self, Xb, col0, d, own):
+        Xo = Xb[:, :own]
+        T = torch.zeros((Xb.shape[0], 2), dtype=Xb.dtype, device=Xb.device)
+        if col0 == 0 and own > 0:
+            T[:, 0] = Xo[:, 0]
+        s = max(1 - col0, 0)
+        if s < own:
+            T[:, 1] = self._g_partial(Xo[:, s:])
+        return T
+
+    def combine_terms(self, T, d):
+        f1 = self._f1(T[:, :1])
+        g = self._g_from(T[:, 1])
+        return torch.stack([f1, g * self._h(f1, g)], 1)
 
     def _h(self, f1, g):
         return 1 - torch.sqrt(f1 / g)
@@ -59,16 +84,19 @@ class ZDT3(ZDTTestSuit):
 
 
 class ZDT4(ZDTTestSuit):
-    def _g(self, X):
-        return 1 + 10 * (self.n - 1) + (X[:, 1:] ** 2 - 10 * torch.cos(4 * math.pi * X[:, 1:])).sum(1)
+    def _g_partial(self, Y):
+        return (Y**2 - 10 * torch.cos(4 * math.pi * Y)).sum(1)
+
+    def _g_from(self, S):
+        return 1 + 10 * (self.n - 1) + S
 
 
 class ZDT6(ZDTTestSuit):
     def _f1(self, X):
         return 1 - torch.exp(-4 * X[:, 0]) * torch.sin(6 * math.pi * X[:, 0]) ** 6
 
-    def _g(self, X):
-        return 1 + 9 * (X[:, 1:].sum(1) / 9) ** 0.25
+    def _g_from(self, S):
+        return 1 + 9 * (S / 9) ** 0.25
 
     def _h(self, f1, g):
         return 1 - (f1 / g) ** 2

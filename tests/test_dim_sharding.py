@@ -119,3 +119,22 @@ def test_lsmop_partial_terms_reproduce_full_evaluation(fn, world):
         Ts = Ts + ts
         Tm = torch.maximum(Tm, tm) if torch.is_tensor(Tm) else tm
     assert torch.allclose(p.combine_terms((Ts, Tm), 120), full, rtol=1e-9, atol=1e-9)
+
+
+@pytest.mark.parametrize("name", ["DTLZ1", "DTLZ2", "DTLZ3", "DTLZ4", "DTLZ5", "DTLZ6", "DTLZ7", "ZDT1", "ZDT2", "ZDT3", "ZDT4", "ZDT6"])
+@pytest.mark.parametrize("world", [1, 2, 3, 7])
+def test_dtlz_zdt_partial_terms_reproduce_full_evaluation(name, world):
+    """Multi-objective suites: position variables travel as terms from their owners, the
+    distance function g as an additive partial sum (m = 4, so position columns straddle the
+    first blocks' boundaries)."""
+    from evoxmi.problems import numerical as N
+
+    d = 23
+    p = getattr(N, name)(d=d, m=4) if name.startswith("DTLZ") else getattr(N, name)(n=d)
+    assert supports_dim_sharding(p)
+    X = torch.rand(11, d, dtype=torch.float64, generator=torch.Generator().manual_seed(world))
+    full, _ = p.evaluate(None, X)
+    T = 0
+    for col0, own in balanced_slices(d, world):
+        T = T + p.partial_terms(X[:, col0 : col0 + own], col0, d, own)
+    torch.testing.assert_close(p.combine_terms(T, d), full, rtol=1e-10, atol=1e-10)

@@ -1,0 +1,13 @@
+# articulated-body Ant: kernel-vs-oracle tests, latency by population, SLP A/B, OpenES gens
+mkdir -p gpurun_out
+set -o pipefail
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -k "ant" > gpurun_out/r3j_ant_tests.log 2>&1 || { tail -40 gpurun_out/r3j_ant_tests.log; exit 1; }
+tail -3 gpurun_out/r3j_ant_tests.log
+timeout -k 10 200 python -u tools/neuro_latency.py 64 1024 8192 > gpurun_out/r3j_neuro_latency.log 2>&1 || exit 1
+cat gpurun_out/r3j_neuro_latency.log
+EVOXMI_SO=$PWD/evoxmi/_C_noslp.so timeout -k 10 200 python -u tools/neuro_latency.py 64 1024 8192 > gpurun_out/r3j_neuro_latency_noslp.log 2>&1 || exit 1
+cat gpurun_out/r3j_neuro_latency_noslp.log
+timeout -k 10 200 python -u tools/bench_neuro.py --pop 1024 --gens 5 --graph > gpurun_out/r3j_neuro_pop1024.log 2>&1 || exit 1
+tail -1 gpurun_out/r3j_neuro_pop1024.log
+timeout -k 10 300 python -u tools/bench_neuro.py --pop 8192 --gens 5 --graph > gpurun_out/r3j_neuro_pop8192.log 2>&1 || exit 1
+tail -1 gpurun_out/r3j_neuro_pop8192.log

@@ -7,7 +7,8 @@ h = 64
 P = neuro.ant_param_count(h, h)
 s0, _ = get_environment("ant").reset(rnd.PRNGKey(0), 1)
 init = s0[0].cuda()
-for pop in (64, 8192):
+pops = [int(a) for a in sys.argv[1:]] or [64, 8192]
+for pop in pops:
     W = torch.zeros(pop, P, device="cuda")
     for cap in (0, 1, 10, 50, 200, 1000):
         neuro.ant_rollout(W, h, h, init, cap); torch.cuda.synchronize()
