@@ -23,6 +23,8 @@
 // block barriers after the weight load.
 #include "evoxmi_common.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr float DT = 0.01f, GEAR = 150.f, ARM = 30.f, JD = 1.f, LIMK = 500.f;
@@ -556,14 +558,21 @@ __device__ __forceinline__ float xor8(float x) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x128, 0xF, 0xF, false));  // row_ror:8
 }
 
-__global__ void __launch_bounds__(64, 2) ant_rollout_reg_kernel(const float* __restrict__ W, int64_t P, int N, int h1, int h2,
-                                                              const float* __restrict__ init, int cap, float* __restrict__ ret,
-                                                              int* __restrict__ steps_out) {
-  __shared__ float a1s[64];
-  const int lane = threadIdx.x & 63;
-  // one wave per workgroup: a finished episode frees its slot immediately, which
-  // matters because episode lengths differ by orders of magnitude
-  const int ind = blockIdx.x;
+// Four individuals (waves) per workgroup: the waves of one workgroup go to the 4 SIMDs of a CU.
+// Single-wave workgroups were placed by the dispatcher two to a SIMD on 6-7 % of the SIMDs
+// whenever a streaming kernel ran just before the launch (profiles/r3_ant_wave_placement.log);
+// two of these VALU-bound waves on one SIMD take 1.83x the cycles each, so the generation
+// (= the slowest wave) took 16.3 instead of 8.9 ms at pop 1024.
+constexpr int ANT_WAVES = 4;
+
+__global__ void __launch_bounds__(64 * ANT_WAVES, 2) ant_rollout_reg_kernel(const float* __restrict__ W, int64_t P, int N, int h1, int h2,
+                                                                          const float* __restrict__ init, int cap, float* __restrict__ ret,
+                                                                          int* __restrict__ steps_out, int trace) {
+  __shared__ float a1s_all[ANT_WAVES][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float* a1s = a1s_all[wv];
+  const unsigned long long t_start = trace ? __builtin_amdgcn_s_memtime() : 0ull;
+  const int ind = blockIdx.x * ANT_WAVES + wv;  // waves never synchronise with each other
   if (ind >= N) return;
   const float* W1 = W + (int64_t)ind * P;
   const float* B1 = W1 + 27 * h1;
@@ -666,6 +675,10 @@ __global__ void __launch_bounds__(64, 2) ant_rollout_reg_kernel(const float* __r
   if (lane == 0) {
     ret[ind] = total;
     if (steps_out) steps_out[ind] = t;
+    if (trace) {  // diagnostics (EVOXMI_ANT_TRACE): shader cycles and the wave's hardware slot
+      ret[ind] = (float)(__builtin_amdgcn_s_memtime() - t_start);
+      steps_out[ind] = (int)((__builtin_amdgcn_s_getreg((31 << 11) | 4) & 0xFFFFu) | ((__builtin_amdgcn_s_getreg((3 << 11) | 20) & 0xFu) << 16));
+    }
   }
 }
 
@@ -675,7 +688,11 @@ int64_t evx_ant_lds_bytes(int64_t P, int h1, int h2, int waves) { return (P + 32
 
 void evx_ant_rollout(const float* W, int64_t P, int N, int h1, int h2, const float* init, int cap, float* ret, int* steps, hipStream_t s) {
   if (h1 <= 64 && h2 <= 64) {
-    ant_rollout_reg_kernel<<<N, 64, 0, s>>>(W, P, N, h1, h2, init, cap, ret, steps);
+    static const int trace = [] {
+      const char* e = getenv("EVOXMI_ANT_TRACE");
+      return e ? atoi(e) : 0;
+    }();
+    ant_rollout_reg_kernel<<<(N + ANT_WAVES - 1) / ANT_WAVES, 64 * ANT_WAVES, 0, s>>>(W, P, N, h1, h2, init, cap, ret, steps, trace);
     return;
   }
   const int64_t per = (P + 32 + h1 + h2 + 8) * 4;

@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--kernel-only", action="store_true", help="time the fused rollout alone on random policies")
     ap.add_argument("--force-dist", action="store_true", help="distributed path even on one rank")
     ap.add_argument("--graph", action="store_true", help="capture the generation in a hipGraph")
+    ap.add_argument("--per-gen", action="store_true", help="print each generation's wall time and episode lengths")
+    ap.add_argument("--dump-pop", default=None, help="save the last generation's population (rollout-probe input)")
     args = ap.parse_args()
     if args.kernel_only:
         return kernel_only(args)
@@ -59,11 +61,38 @@ def main():
     sync()
     t = time.perf_counter()
     env_steps = torch.zeros((), dtype=torch.int64, device=dev)
-    for _ in range(args.gens):
+    for gi in range(args.gens):
+        if args.per_gen:
+            sync()
+            tg = time.perf_counter()
         st = wf.step(st)
         env_steps += prob.last_episode_lengths.sum()
+        if args.per_gen:
+            sync()
+            L = prob.last_episode_lengths
+            if rank == 0:
+                print(json.dumps({"gen": gi, "ms": round((time.perf_counter() - tg) * 1e3, 3), "max_len": int(L.max()),
+                                  "mean_len": round(float(L.float().mean()), 1)}), flush=True)
     sync()
     dt = torch.tensor([(time.perf_counter() - t) / args.gens], dtype=torch.float64, device=dev)
+    if args.dump_pop:
+        torch.save(st.get_child_state("algorithm").population.cpu(), args.dump_pop)
+        # the last population's rollout timed in this process: workflow init state vs the probe's
+        from evoxmi.ops import neuro
+        from evoxmi.problems.neuroevolution.reinforcement_learning.envs import get_environment
+
+        Wf = policy.flat(tv.batched_to_tree(st.get_child_state("algorithm").population))
+        s_wf = prob._initial_state(st.get_child_state("problem").key, Wf.device)
+        s_pr = get_environment("ant").reset(rnd.PRNGKey(0), 1)[0][0].to(Wf.device)
+        print("init states equal:", bool(torch.equal(s_wf, s_pr)), flush=True)
+        for name, s0 in (("workflow_init", s_wf), ("probe_init", s_pr)):
+            for _ in range(2):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                _, L = neuro.ant_rollout(Wf, args.hidden, args.hidden, s0, args.cap)
+                e1.record()
+                torch.cuda.synchronize()
+                print(name, round(e0.elapsed_time(e1), 3), "ms mean_len", round(float(L.float().mean()), 1), flush=True)
     if dist_on:
         dist.all_reduce(dt, op=dist.ReduceOp.MAX)
         dist.all_reduce(env_steps)

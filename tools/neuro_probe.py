@@ -11,9 +11,23 @@ P = neuro.ant_param_count(h, h)
 s0, _ = get_environment("ant").reset(rnd.PRNGKey(0), 1)
 init = s0[0].cuda()
 g = torch.Generator(device="cuda").manual_seed(0)
-for pop in (64, 1024):
-    for mode in ("zero", "same", "random", "random_x0.02"):
-        if mode == "zero":
+from evoxmi.models import MLPPolicy
+from evoxmi.utils import TreeAndVector
+pol = MLPPolicy([27, h, h, 8])
+center = TreeAndVector(pol.init(rnd.PRNGKey(0), device="cuda")).to_vector(pol.init(rnd.PRNGKey(0), device="cuda"))
+modes = sys.argv[1].split(",") if len(sys.argv) > 1 else ["zero", "same", "random", "random_x0.02", "es", "es_x0.5"]
+for pop in (64, 512, 1024):
+    for mode in modes:
+        if mode.startswith("file:"):
+            W = torch.load(mode[5:], weights_only=True).cuda()
+            half = mode.endswith("#half")
+            W = W[: W.shape[0] // 2] if half else W
+            if W.shape[0] != pop:
+                continue
+        elif mode.startswith("es"):
+            sig = 0.05 * (10 if mode.endswith("0.5") else 1)
+            W = center[None, :] + sig * torch.randn(pop, P, device="cuda", generator=g)
+        elif mode == "zero":
             W = torch.zeros(pop, P, device="cuda")
         elif mode == "same":
             W = (0.1 * torch.randn(1, P, device="cuda", generator=g)).expand(pop, P).contiguous()
