@@ -38,6 +38,9 @@ def main():
     ap.add_argument("--simulate-rank", type=int, default=None,
                     help="time rank R's share of a --world N step on this one GPU (collectives replaced by same-size local ops)")
     ap.add_argument("--world", type=int, default=8, help="world size simulated by --simulate-rank")
+    ap.add_argument("--monitor", nargs="?", const="host", default=None, choices=["host", "device", "best"],
+                    help="attach an EvalMonitor in the timed loop: full fitness history copied to the host "
+                         "asynchronously (host), kept on the device (device), or best-so-far only (best)")
     args = ap.parse_args()
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -63,7 +66,12 @@ def main():
     algo = CMAES(center_init=center, init_stdev=20.0, pop_size=args.pop)
     prob = CEC2022TestSuit.create(args.func)
     use_graph = (not args.no_graph) and device.type == "cuda"
-    wf = StdWorkflow(algo, prob, graph=use_graph)
+    monitors = []
+    if args.monitor:
+        from evoxmi.monitors import EvalMonitor
+
+        monitors = [EvalMonitor(full_fit_history=args.monitor != "best", history_to_host=args.monitor == "host")]
+    wf = StdWorkflow(algo, prob, graph=use_graph, monitors=monitors)
     state = wf.init(key)
     dist_on = (world > 1 or args.force_dist) and not sim
     if dist_on:
@@ -131,10 +139,10 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "fp32",
-            "data": "synthetic (seeded CEC'22 F1 shift + Haar rotation at d=1000; random init mean)",
+            "data": f"synthetic (seeded CEC'22 F{args.func} shift + Haar rotation at d={args.dim}; random init mean)",
             "generations_per_sec": round(gens_per_s, 3),
             "config": {
-                "model": "CMA-ES on CEC2022 F1 (shifted-rotated Zakharov)",
+                "model": "CMA-ES on CEC2022 F1 (shifted-rotated Zakharov)" if args.func == 1 else f"CMA-ES on CEC2022 F{args.func}",
                 "global_batch": args.pop,
                 "seq_len": args.dim,
                 "parallelism": f"pop-shard{world}" if not sim else f"simulated-rank{args.simulate_rank}-of-{args.world}",
@@ -146,6 +154,11 @@ def main():
         }
         if phases:
             out["phases_ms_eager"] = phases
+        if args.monitor:
+            hist = monitors[0].get_history()
+            out["monitor"] = {"type": "EvalMonitor", "mode": args.monitor, "generations_recorded": len(hist),
+                              "host_side": bool(hist) and not hist[-1].is_cuda,
+                              "best_fitness": float(monitors[0].get_best_fitness())}
         if sim:
             # one rank's share of an N-GPU step (the driver's --gpus 1 headline never sets this)
             out["simulated"] = {

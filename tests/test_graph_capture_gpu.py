@@ -83,3 +83,22 @@ def test_lsmop1_moead_graph():
             st = wf.step(st)
         outs.append(st.get_child_state("algorithm").fitness.clone())
     assert torch.allclose(outs[0], outs[1], rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("func", list(range(1, 13)))
+def test_cec2022_generation_captures_and_replays(func):
+    """Every CEC'22 function (hybrid F6-F8 and composition F9-F12 included) evaluates inside a
+    captured CMA-ES generation: no host-to-device copies during capture, same state as eager."""
+    from evoxmi.algorithms import CMAES
+    from evoxmi.problems.numerical import CEC2022TestSuit
+
+    def run(graph):
+        wf = StdWorkflow(CMAES(torch.zeros(20, device="cuda"), 10.0, pop_size=32), CEC2022TestSuit.create(func), graph=graph)
+        st = wf.init(rnd.PRNGKey(5, device="cuda"))
+        for _ in range(4):
+            st = wf.step(st)
+        torch.cuda.synchronize()
+        return st.get_child_state("algorithm")
+
+    a, b = run(True), run(False)
+    assert torch.allclose(a.mean, b.mean, rtol=1e-4, atol=1e-4)
