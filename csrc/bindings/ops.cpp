@@ -258,6 +258,43 @@ void gemm_ks_out(const at::Tensor& A, int64_t a_kc, const at::Tensor& B, int64_t
 }
 
 int64_t gemm_ks_grid(int64_t M, int64_t N, int64_t mode) { return evx_gemm_ks_grid((int)M, (int)N, (int)mode); }
+int64_t gemm_ks_tile(int64_t M, int64_t N, int64_t mode) { return evx_gemm_ks_tile((int)M, (int)N, (int)mode); }
+
+// CEC'22 F1 / F4 on the device without the rotated population: f(row) of
+// z = alpha · (X − o) · Mᵀ from the gemm_ks row-terms epilogue (per column tile, additive) and
+// one finishing kernel (gemm_ks.hip, cec2022.hip).  fid 0 = Zakharov, 3 = Rastrigin.
+at::Tensor cec_rotated_rowterms(const at::Tensor& X, const at::Tensor& Mrot, const at::Tensor& o, double alpha, int64_t fid) {
+  CHECK_DEV(X); CHECK_F32(X); CHECK_DEV(Mrot); CHECK_F32(Mrot); CHECK_DEV(o); CHECK_F32(o); CHECK_CONTIG(o);
+  TORCH_CHECK(fid == 0 || fid == 3, "cec_rotated_rowterms: Zakharov (0) or Rastrigin (3)");
+  TORCH_CHECK(X.dim() == 2 && Mrot.dim() == 2 && X.stride(1) == 1 && Mrot.stride(1) == 1, "cec_rotated_rowterms: 2-D row-major operands");
+  const int64_t N = X.size(0), D = X.size(1);
+  TORCH_CHECK(Mrot.size(0) == D && Mrot.size(1) == D && o.numel() >= D, "cec_rotated_rowterms: shapes");
+  TORCH_CHECK(D % 4 == 0 && X.stride(0) % 4 == 0 && Mrot.stride(0) % 4 == 0 && reinterpret_cast<uintptr_t>(X.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(Mrot.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(o.data_ptr()) % 16 == 0,
+              "cec_rotated_rowterms: 16-byte aligned operands, D % 4 == 0");
+  const int t = evx_gemm_ks_tile((int)N, (int)D, 0);
+  TORCH_CHECK(t == 8 || t == 4, "cec_rotated_rowterms: the row-terms epilogue needs a 64-column tile layout");
+  c10::DeviceGuard g(X.device());
+  const int tiles_n = evx_gemm_ks_tiles_n((int)N, (int)D, 0);
+  auto parts = at::empty({tiles_n, N, 2}, X.options());
+  auto out = at::empty({N}, X.options());
+  EvxGemmKs a{};
+  a.A = X.data_ptr<float>();
+  a.lda = X.stride(0);
+  a.B = Mrot.data_ptr<float>();
+  a.ldb = Mrot.stride(0);
+  a.C = parts.data_ptr<float>();  // never written in row-terms mode
+  a.ldc = D;
+  a.M = (int)N; a.N = (int)D; a.K = (int)D;
+  a.a_kc = 1; a.b_kc = 1; a.mode = 0;
+  a.alpha = (float)alpha;
+  a.a_sub_k = o.data_ptr<float>();
+  a.row_terms = parts.data_ptr<float>();
+  a.row_fid = (int)fid;
+  evx_gemm_ks(a, cur_stream());
+  evx_cec_rowterms_final(parts.data_ptr<float>(), tiles_n, (int)N, (int)fid, out.data_ptr<float>(), cur_stream());
+  return out;
+}
 
 // ---- device-controlled SBR schedule (eigh_sbr_dev.hip, ops/sbr_device.py): every op writes
 // into caller-owned buffers and honours a device skip word, so a solve is capturable once
@@ -1175,6 +1212,8 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("gemm_ks(Tensor A, int a_kc, Tensor B, int b_kc, int M, int N, int K, int mode, float alpha, Tensor? alpha_ptr, Tensor? bias_n, float beta, Tensor? Cin, Tensor? skip, Tensor? a_sub_k=None) -> Tensor");
   m.def("gemm_ks_out(Tensor A, int a_kc, Tensor B, int b_kc, int M, int N, int K, int mode, float alpha, Tensor? alpha_ptr, Tensor? bias_n, float beta, Tensor? Cin, Tensor(a!) out, Tensor? skip, Tensor? a_sub_k=None, Tensor? sel=None, Tensor? A2=None, float alpha2=0., Tensor(b!)? C2=None, Tensor(c!)? stat_part=None) -> ()");
   m.def("gemm_ks_grid(int M, int N, int mode) -> int");
+  m.def("gemm_ks_tile(int M, int N, int mode) -> int");
+  m.def("cec_rotated_rowterms(Tensor X, Tensor Mrot, Tensor o, float alpha, int fid) -> Tensor");
   m.def("sbr16_block_out(Tensor A, int shift, int sweeps, int sb, Tensor(a!) perm, Tensor(b!) Q, Tensor(c!) dq, Tensor skip) -> ()");
   m.def("sbr16_far_out(Tensor A, Tensor perm, Tensor Q, Tensor dq, Tensor stats, float thr_fac, Tensor theta, Tensor(a!) X, int sb, Tensor skip) -> ()");
   m.def("sbr16_bq_out(Tensor B, Tensor perm, Tensor Q, Tensor(a!) Bq, int sb, Tensor skip) -> ()");
@@ -1221,12 +1260,14 @@ TORCH_LIBRARY_IMPL(evoxmi, CompositeExplicitAutograd, m) {
   m.impl("gemm_set_config", &gemm_set_config);
   m.impl("gemm_ks_set_tile", &gemm_ks_set_tile);
   m.impl("gemm_ks_grid", &gemm_ks_grid);
+  m.impl("gemm_ks_tile", &gemm_ks_tile);
   m.impl("ipc_alloc", &ipc_alloc);
   m.impl("ipc_open", &ipc_open);
   m.impl("ipc_close", &ipc_close);
 }
 
 TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
+  m.impl("cec_rotated_rowterms", &cec_rotated_rowterms);
   m.impl("philox_fill", &philox_fill);
   m.impl("classic_eval", &classic_eval);
   m.impl("sbx", &sbx);

@@ -57,8 +57,16 @@ struct EvxGemmKs {
   double* stat_part;
   int c_vec4;
   int tiles_m, tiles_n;  // set by the launcher
+  // row-terms epilogue (MODE 0, CEC'22 F1 / F4 on the rotated population): C is not written;
+  // per output tile and row the additive terms of the basic function over the tile's columns
+  // go to row_terms[(tn · M + row) · 2 + {0, 1}] (Zakharov: Σ z², Σ ½(j+1) z; Rastrigin:
+  // Σ y² − 10 cos 2πy + 10 with y = 0.0512 z, 0), finished by evx_cec_rowterms_final
+  float* row_terms;
+  int row_fid;
 };
 void evx_gemm_ks(const EvxGemmKs& a, hipStream_t s);
+int evx_gemm_ks_tiles_n(int M, int N, int mode);  // column tiles of a launch (row-terms partial count)
+void evx_cec_rowterms_final(const float* parts, int tiles_n, int M, int fid, float* out, hipStream_t s);
 int evx_gemm_ks_grid(int M, int N, int mode);  // workgroups of a launch (stat_part length)
 int evx_gemm_ks_tile(int M, int N, int mode);
 void evx_gemm_ks_set_tile(int t);

@@ -170,3 +170,25 @@ void evx_cec_basic(const float* Z, int64_t ld, int N, int fid, const int32_t* pe
   dim3 grid((N + 3) / 4);
   cec_basic_kernel<<<grid, 256, 0, s>>>(Z, ld, N, fid, perm, start, L, sub, scale, Y, ldy, ystart, yperm, out);
 }
+
+namespace {
+// f of every row from the per-column-tile additive terms of the fused rotation GEMM
+// (gemm_ks row-terms epilogue), summed in tile order (deterministic); the < 1e-8 clamp of
+// the CEC'22 evaluation is applied here
+__global__ void cec_rowterms_final_kernel(const float* __restrict__ parts, int tiles_n, int M, int fid, float* __restrict__ out) {
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= M) return;
+  float a = 0.f, b = 0.f;
+  for (int t = 0; t < tiles_n; ++t) {
+    const float2 v = *reinterpret_cast<const float2*>(parts + ((int64_t)t * M + row) * 2);
+    a += v.x;
+    b += v.y;
+  }
+  const float f = fid == 0 ? a + b * b + b * b * b * b : a;
+  out[row] = f < 1e-8f ? 0.f : f;
+}
+}  // namespace
+
+void evx_cec_rowterms_final(const float* parts, int tiles_n, int M, int fid, float* out, hipStream_t s) {
+  cec_rowterms_final_kernel<<<(M + 255) / 256, 256, 0, s>>>(parts, tiles_n, M, fid, out);
+}

@@ -34,10 +34,22 @@
 #include "evoxmi_launchers.h"
 #include <float.h>
 
+#include "../host/gemm_tiles.h"
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
+
+// DPP row_ror:m (rotation by m lanes inside each 16-lane row)
+__device__ __forceinline__ float row_ror(float v, int m) {
+  switch (m) {
+    case 8: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, false));
+    case 4: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xF, 0xF, false));
+    case 2: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x122, 0xF, 0xF, false));
+    default: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x121, 0xF, 0xF, false));
+  }
+}
 
 // One lane's four k values k .. k + 3 of one operand row.  Full 16-k groups load without
 // masks; only the tail group (K % 16 != 0, handled once after the main loop) masks, with
@@ -288,6 +300,8 @@ __global__ void __launch_bounds__(256) gemm_ks_kernel(EvxGemmKs p) {
   constexpr int NV4 = BM * BN / 4;
   constexpr int PER = (NV4 + 255) / 256;
   float4 out[PER];
+  float rt1[PER], rt2[PER];  // row-terms partials (MODE 0 with row_terms)
+  const bool zak = p.row_fid == 0;
 #pragma unroll
   for (int v = 0; v < PER; ++v) {
     const int e = threadIdx.x + 256 * v;
@@ -306,6 +320,26 @@ __global__ void __launch_bounds__(256) gemm_ks_kernel(EvxGemmKs p) {
       t.z *= sc;
       t.w *= sc;
       const int gr = m0 + row, gc = n0 + c;
+      if (MODE == 0 && BN == 64 && p.row_terms) {
+        // fused CEC'22 basic-function row reduction: this float4's two additive terms
+        // (branch-free; columns past N contribute 0), reduced across the row after the loop
+        const float vv[4] = {t.x, t.y, t.z, t.w};
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int e2 = 0; e2 < 4; ++e2) {
+          const float z = gc + e2 < p.N ? vv[e2] : 0.f;
+          if (zak) {
+            s1 = fmaf(z, z, s1);
+            s2 = fmaf(0.5f * (float)(gc + e2 + 1), z, s2);
+          } else {  // Rastrigin (z · 0.0512 as in the CEC'22 basic function); v_cos takes revolutions
+            const float y = 0.0512f * z;
+            s1 += y * y - 10.f * __builtin_amdgcn_cosf(y) + 10.f;
+          }
+        }
+        rt1[v] = s1;
+        rt2[v] = s2;
+        continue;
+      }
       if (p.bias_n) {
         if (gc < p.N) t.x += p.bias_n[gc];
         if (gc + 1 < p.N) t.y += p.bias_n[gc + 1];
@@ -356,6 +390,26 @@ __global__ void __launch_bounds__(256) gemm_ks_kernel(EvxGemmKs p) {
         }
       }
     }
+  }
+  if (MODE == 0 && BN == 64 && p.row_terms) {
+    // DPP row rotations by 8, 4, 2, 1 inside the 16-lane row that holds one tile row, all
+    // PER rows of this thread interleaved (independent chains); every lane ends with the sum
+#pragma unroll
+    for (int m = 8; m >= 1; m >>= 1) {
+#pragma unroll
+      for (int v = 0; v < PER; ++v) {
+        rt1[v] += row_ror(rt1[v], m);
+        rt2[v] += row_ror(rt2[v], m);
+      }
+    }
+    if ((threadIdx.x & 15) == 0) {
+#pragma unroll
+      for (int v = 0; v < PER; ++v) {
+        const int gr = m0 + (threadIdx.x + 256 * v) / (BN / 4);
+        if (gr < p.M) *reinterpret_cast<float2*>(p.row_terms + ((int64_t)tn * p.M + gr) * 2) = make_float2(rt1[v], rt2[v]);
+      }
+    }
+    return;
   }
   if (MODE == 1 && p.stat_part) {
     st_off = evx::wave_sum_d(st_off);
@@ -429,33 +483,11 @@ int g_ks_tile_override = 0;
 
 void evx_gemm_ks_set_tile(int t) { g_ks_tile_override = t; }
 
-int evx_gemm_ks_tile(int M, int N, int mode) {
-  if (g_ks_tile_override) return (g_ks_tile_override == 8 && mode != 0) ? 4 : g_ks_tile_override;
-  // tall full products (sampling / CEC rotation, 10 000 × 1000 × 1000): 128 × 64 tiles —
-  // half the B-panel reloads per output of 64 × 64 (tools/gemm_ks_probe.cpp: 210 vs 317 µs)
-  if (mode == 0 && M >= 2048 && N >= 64) return 8;
-  // fewest workgroup rounds over the 256 CUs × tile work, larger tile on ties
-  int best = 4;
-  double best_cost = 1e300;
-  for (int t : {4, 3, 2}) {
-    const int b = 16 * t;
-    const long tm = (M + b - 1) / b, tn = (N + b - 1) / b;
-    const long tiles = mode == 0 ? tm * tn : tm * (tm + 1) / 2;
-    const double cost = (double)((tiles + 255) / 256) * (double)(b * b);
-    if (cost < best_cost * 0.999) {
-      best_cost = cost;
-      best = t;
-    }
-  }
-  return best;
-}
+int evx_gemm_ks_tile(int M, int N, int mode) { return evx_host::gemm_ks_tile(M, N, mode, g_ks_tile_override); }
 
-int evx_gemm_ks_grid(int M, int N, int mode) {
-  const int t = evx_gemm_ks_tile(M, N, mode);
-  const int bm = 16 * t, bn = t == 8 ? 64 : 16 * t;
-  const int tm = (M + bm - 1) / bm, tn = (N + bn - 1) / bn;
-  return mode == 0 ? tm * tn : tm * (tm + 1) / 2;
-}
+int evx_gemm_ks_grid(int M, int N, int mode) { return (int)evx_host::gemm_ks_grid(M, N, mode, g_ks_tile_override); }
+
+int evx_gemm_ks_tiles_n(int M, int N, int mode) { return (int)evx_host::gemm_ks_tiles_n(M, N, mode, g_ks_tile_override); }
 
 void evx_gemm_ks(const EvxGemmKs& a, hipStream_t s) {
   if (a.M <= 0 || a.N <= 0) return;

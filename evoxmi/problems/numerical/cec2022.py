@@ -34,6 +34,7 @@ import torch
 
 from ...core import Problem
 from ...ops import linalg
+from ...ops import _ext
 from ...ops import numerical as nops
 
 _DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "cec2022_input_data")
@@ -266,6 +267,27 @@ class _CEC2022(Problem):
         return self._evaluate(X, c), state
 
 
+def _rowterms(X, o, M, s, fid):
+    """K6 fused: f of every row of z = s·(X − o)·Mᵀ straight from the rotation GEMM's epilogue
+    (per column tile additive terms + one finishing kernel) — the rotated population is never
+    written.  None when the device path does not apply (CPU, odd shapes, a tile layout other
+    than 64 columns wide)."""
+    if not X.is_cuda or X.dtype != torch.float32:
+        return None
+    from ... import config
+
+    if config.get("plain_gemm") == "blas" or not config.get("cec_fused"):
+        return None
+    N, D = X.shape
+    ops = _ext.ops()
+    if D % 4 or int(ops.gemm_ks_tile(N, D, 0)) not in (4, 8) or X.stride(1) != 1 or X.stride(0) % 4 or X.data_ptr() % 16:
+        return None
+    o = o.contiguous()
+    if o.data_ptr() % 16:
+        return None
+    return ops.cec_rotated_rowterms(X, M, o, float(s), int(fid))
+
+
 class _RowSharded:
     """Decision-axis sharding (strategy P2, ``evoxmi.parallel.dim_sharded``) of a shifted-
     rotated function: the rotation mixes every column, so a rank does not take a column
@@ -290,6 +312,9 @@ class F1_CEC2022(_RowSharded, _CEC2022):
 
     def _evaluate(self, X, c):
         D = X.shape[1]
+        f = _rowterms(X, c["Os"][:D], c["M"], 1.0, ZAKHAROV)
+        if f is not None:
+            return f
         Z = self._ssr(X, c["Os"][:D], c["M"], 1.0)
         return self._clamp(self._basic(Z, ZAKHAROV))
 
@@ -352,6 +377,9 @@ class F4_CEC2022(_RowSharded, _CEC2022):
 
     def _evaluate(self, X, c):
         D = X.shape[1]
+        f = _rowterms(X, c["Os"][:D], c["M"], 1.0, RASTRIGIN)
+        if f is not None:
+            return f
         return self._clamp(self._basic(self._ssr(X, c["Os"][:D], c["M"], 1.0), RASTRIGIN))
 
     def partial_terms(self, X, col0, d, own):

@@ -954,3 +954,26 @@ def test_weighted_rowsum_kernel(K, D):
     ref = (w.double()[:, None] * (X[idx.long()].double() - sub.double())).sum(0)
     out = weighted_rowsum(X.cuda(), idx.cuda(), w.cuda(), sub.cuda(), K).cpu()
     assert torch.allclose(out.double(), ref, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("fn", [1, 4])
+@pytest.mark.parametrize("N,D", [(10000, 1000), (700, 128), (300, 20), (257, 64)])
+def test_cec_rotation_rowterms_epilogue_matches_cpu(fn, N, D):
+    """K6: F1 (Zakharov) / F4 (Rastrigin) evaluated from the rotation GEMM's row-terms epilogue
+    (the rotated population is never written) vs the fp64 CPU evaluation of the same function."""
+    from evoxmi.ops import _ext
+    from evoxmi.problems.numerical import CEC2022TestSuit
+
+    from evoxmi import config
+
+    p = CEC2022TestSuit.create(fn)
+    g = torch.Generator().manual_seed(N + D)
+    X = (torch.rand(N, D, generator=g) * 40 - 20).float()
+    ref, _ = p.evaluate(None, X.double())
+    with config.override(cec_fused=1):
+        out, _ = p.evaluate(None, X.cuda())
+    fused = int(_ext.ops().gemm_ks_tile(N, D, 0)) in (4, 8) and D % 4 == 0
+    assert out.shape == (N,) and torch.isfinite(out).all()
+    torch.testing.assert_close(out.cpu().double(), ref.double(), rtol=2e-4, atol=1e-3)
+    if fused:  # the bench shape must take the fused path
+        assert N != 10000 or int(_ext.ops().gemm_ks_tile(N, D, 0)) == 8

@@ -56,3 +56,37 @@ def test_stochastic_ranking_under_asan_ubsan(harness):
     assert "runtime error" not in out.stderr and "AddressSanitizer" not in out.stderr, out.stderr[-2000:]
     got = [list(map(int, l.split())) for l in out.stdout.splitlines()]
     assert got == refs
+
+
+def _tile_reference(M, N, mode, ov):
+    if ov:
+        t = 4 if (ov == 8 and mode != 0) else ov
+    elif mode == 0 and M >= 2048 and N >= 64:
+        t = 8
+    else:
+        t, best = 4, float("inf")
+        for c in (4, 3, 2):
+            b = 16 * c
+            tm, tn = -(-M // b), -(-N // b)
+            tiles = tm * tn if mode == 0 else tm * (tm + 1) // 2
+            cost = ((tiles + 255) // 256) * float(b * b)
+            if cost < best * 0.999:
+                best, t = cost, c
+    bm, bn = 16 * t, (64 if t == 8 else 16 * t)
+    tm, tn = -(-M // bm), -(-N // bn)
+    return t, (tm * tn if mode == 0 else tm * (tm + 1) // 2), tn
+
+
+def test_gemm_tile_selection_under_asan_ubsan(harness):
+    """The GEMM launch geometry (tile code, workgroups, column tiles — the latter two size the
+    stats / row-terms partial buffers) for edge and flagship shapes, incl. 64-bit grids."""
+    cases = [(1, 1, 0, 0), (16, 16, 1, 0), (1000, 1000, 1, 0), (1000, 1000, 2, 0), (10000, 1000, 0, 0), (5000, 1000, 0, 0),
+             (2047, 64, 0, 0), (2048, 63, 0, 0), (300, 20, 0, 0), (257, 64, 0, 0), (1000, 1000, 0, 8), (1000, 1000, 1, 8),
+             (123, 4567, 0, 3), (3_000_000, 100_000, 0, 0), (70_000, 70_000, 1, 0)]
+    lines = [f"tile {M} {N} {mode} {ov}" for M, N, mode, ov in cases]
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
+    out = subprocess.run([harness], input="\n".join(lines) + "\n", capture_output=True, text=True, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert "runtime error" not in out.stderr and "AddressSanitizer" not in out.stderr, out.stderr[-2000:]
+    got = [tuple(map(int, l.split())) for l in out.stdout.splitlines()]
+    assert got == [_tile_reference(*c) for c in cases]
