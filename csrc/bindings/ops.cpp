@@ -62,7 +62,7 @@ at::Tensor classic_eval(const at::Tensor& X, int64_t func, double a, double b, d
 std::vector<at::Tensor> pso_update(const at::Tensor& pop, const at::Tensor& vel, const at::Tensor& lbl,
                                    const at::Tensor& lbf, const at::Tensor& fit, const at::Tensor& gbl,
                                    const at::Tensor& kp, const at::Tensor& kg, double w, double phip, double phig,
-                                   const at::Tensor& lb, const at::Tensor& ub) {
+                                   const at::Tensor& lb, const at::Tensor& ub, int64_t col0, int64_t d_total) {
   for (auto* t : {&pop, &vel, &lbl, &lbf, &fit, &gbl, &lb, &ub}) { CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t); }
   check_key(kp); check_key(kg);
   const int64_t N = pop.size(0), D = pop.size(1);
@@ -70,10 +70,19 @@ std::vector<at::Tensor> pso_update(const at::Tensor& pop, const at::Tensor& vel,
   TORCH_CHECK(lbf.numel() == N && fit.numel() == N && gbl.numel() == D && lb.numel() == D && ub.numel() == D, "shape mismatch");
   c10::DeviceGuard g(pop.device());
   auto opop = at::empty_like(pop), ovel = at::empty_like(pop), olbl = at::empty_like(pop), olbf = at::empty_like(lbf);
-  evx_pso_update(pop.data_ptr<float>(), vel.data_ptr<float>(), lbl.data_ptr<float>(), lbf.data_ptr<float>(),
-                 fit.data_ptr<float>(), gbl.data_ptr<float>(), kp.data_ptr<int64_t>(), kg.data_ptr<int64_t>(), (float)w,
-                 (float)phip, (float)phig, lb.data_ptr<float>(), ub.data_ptr<float>(), opop.data_ptr<float>(),
-                 ovel.data_ptr<float>(), olbl.data_ptr<float>(), olbf.data_ptr<float>(), (int)N, (int)D, cur_stream());
+  if (d_total <= 0) d_total = D;
+  TORCH_CHECK(col0 >= 0 && col0 + D <= d_total, "pso_update: column block outside [0, d_total)");
+  if (col0 == 0 && d_total == D)
+    evx_pso_update(pop.data_ptr<float>(), vel.data_ptr<float>(), lbl.data_ptr<float>(), lbf.data_ptr<float>(),
+                   fit.data_ptr<float>(), gbl.data_ptr<float>(), kp.data_ptr<int64_t>(), kg.data_ptr<int64_t>(), (float)w,
+                   (float)phip, (float)phig, lb.data_ptr<float>(), ub.data_ptr<float>(), opop.data_ptr<float>(),
+                   ovel.data_ptr<float>(), olbl.data_ptr<float>(), olbf.data_ptr<float>(), (int)N, (int)D, cur_stream());
+  else
+    evx_pso_update_cols(pop.data_ptr<float>(), vel.data_ptr<float>(), lbl.data_ptr<float>(), lbf.data_ptr<float>(),
+                        fit.data_ptr<float>(), gbl.data_ptr<float>(), kp.data_ptr<int64_t>(), kg.data_ptr<int64_t>(), (float)w,
+                        (float)phip, (float)phig, lb.data_ptr<float>(), ub.data_ptr<float>(), opop.data_ptr<float>(),
+                        ovel.data_ptr<float>(), olbl.data_ptr<float>(), olbf.data_ptr<float>(), (int)N, (int)D, (int)col0,
+                        (int)d_total, cur_stream());
   return {opop, ovel, olbl, olbf};
 }
 
@@ -1252,7 +1261,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("sbr_damping(Tensor X2, Tensor V, float tau, Tensor(a!)? out=None) -> Tensor");
   m.def("sbr_symstats_out(Tensor T, Tensor(a!) A, Tensor(b!) st) -> ()");
   m.def("sbr_taylor_prep(Tensor X, Tensor X2, Tensor X3, Tensor? alpha=None, int mt=0) -> Tensor[]");
-  m.def("pso_update(Tensor pop, Tensor vel, Tensor lbl, Tensor lbf, Tensor fit, Tensor gbl, Tensor kp, Tensor kg, float w, float phip, float phig, Tensor lb, Tensor ub) -> Tensor[]");
+  m.def("pso_update(Tensor pop, Tensor vel, Tensor lbl, Tensor lbf, Tensor fit, Tensor gbl, Tensor kp, Tensor kg, float w, float phip, float phig, Tensor lb, Tensor ub, int col0=0, int d_total=0) -> Tensor[]");
 }
 
 TORCH_LIBRARY_IMPL(evoxmi, CompositeExplicitAutograd, m) {

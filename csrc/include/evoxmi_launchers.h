@@ -9,6 +9,10 @@ void evx_pso_update(const float* pop, const float* vel, const float* lbl, const 
                     const float* gbl, const int64_t* kp, const int64_t* kg, float w, float phip, float phig,
                     const float* lb, const float* ub, float* opop, float* ovel, float* olbl, float* olbf, int N, int D,
                     hipStream_t s);
+void evx_pso_update_cols(const float* pop, const float* vel, const float* lbl, const float* lbf, const float* fit,
+                         const float* gbl, const int64_t* kp, const int64_t* kg, float w, float phip, float phig,
+                         const float* lb, const float* ub, float* opop, float* ovel, float* olbl, float* olbf, int N, int D,
+                         int col0, int Dtot, hipStream_t s);
 
 struct EvxOperand {
   const float* ptr;

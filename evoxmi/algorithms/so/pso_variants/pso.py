@@ -54,6 +54,19 @@ class PSO(Algorithm):
     def ask(self, state):
         return state.population, state
 
+    # -- decision-axis state sharding (P2, StdWorkflow.enable_multi_devices): every (N, d) / (d,)
+    # field is column-separable in the tell (the only row coupling is through the replicated
+    # fitness), so a rank keeps only its column block and nothing but the evaluation's per-row
+    # terms crosses the ranks
+    _cols = None
+
+    def dim_shard(self, state, col0: int, own: int):
+        self._cols = (int(col0), int(own), self.dim)
+        c = slice(col0, col0 + own)
+        return state.update(population=state.population[:, c].contiguous(), velocity=state.velocity[:, c].contiguous(),
+                            local_best_location=state.local_best_location[:, c].contiguous(),
+                            global_best_location=state.global_best_location[c].contiguous())
+
     def tell(self, state, fitness):
         key, rg_key, rp_key = rnd.split(state.key, 3)
         # global best over [gbest; swarm] — device argmin, no host sync
@@ -62,9 +75,11 @@ class PSO(Algorithm):
         better = cand_f < state.global_best_fitness
         global_best_fitness = torch.where(better, cand_f, state.global_best_fitness)
         global_best_location = torch.where(better, state.population[i], state.global_best_location)
+        c0, own, d = self._cols if self._cols is not None else (0, self.dim, self.dim)
         pos, vel, lbl, lbf = pso_ops.pso_update(
             state.population, state.velocity, state.local_best_location, state.local_best_fitness, fitness,
-            global_best_location, rp_key, rg_key, self.w, self.phi_p, self.phi_g, self.lb, self.ub,
+            global_best_location, rp_key, rg_key, self.w, self.phi_p, self.phi_g, self.lb[c0 : c0 + own], self.ub[c0 : c0 + own],
+            col0=c0, d_total=d,
         )
         return state.update(
             population=pos,

@@ -52,6 +52,30 @@ def dim_sharded_fitness(problem, X: torch.Tensor, group=None) -> torch.Tensor:
     return problem.combine_terms(T, d)
 
 
+def dim_sharded_fitness_local(problem, Xloc: torch.Tensor, col0: int, d: int, group=None) -> torch.Tensor:
+    """Fitness when the population itself is column-sharded (``Xloc`` = this rank's columns
+    [col0, col0 + own) of every row; problems with ``dim_halo == 0`` that take column blocks)."""
+    own = Xloc.shape[1]
+    T = problem.partial_terms(Xloc, col0, d, own)
+    if isinstance(T, tuple):
+        Ts, Tm = T[0].contiguous(), T[1].contiguous()
+        if dist.is_available() and dist.is_initialized():
+            dist.all_reduce(Ts, op=dist.ReduceOp.SUM, group=group)
+            dist.all_reduce(Tm, op=dist.ReduceOp.MAX, group=group)
+        return problem.combine_terms((Ts, Tm), d)
+    T = T.contiguous()
+    if dist.is_available() and dist.is_initialized():
+        dist.all_reduce(T, op=dist.ReduceOp.SUM, group=group)
+    return problem.combine_terms(T, d)
+
+
+def supports_state_sharding(algorithm, problem) -> bool:
+    """Full P2 (state and evaluation column-sharded): the algorithm can slice its state into
+    column blocks and the problem's terms need no halo and no full rows."""
+    return (hasattr(algorithm, "dim_shard") and supports_dim_sharding(problem) and getattr(problem, "dim_halo", 1) == 0
+            and not getattr(problem, "dim_shard_full_rows", False))
+
+
 class DimShardedProblem(Problem):
     def __init__(self, problem: Problem, group=None):
         super().__init__()

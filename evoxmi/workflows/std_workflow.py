@@ -126,8 +126,11 @@ class StdWorkflow(Workflow):
 
     def _evaluate(self, state, transformed):
         if self._dim_shard_group is not None:
-            from ..parallel.dim_sharded import dim_sharded_fitness
+            from ..parallel.dim_sharded import dim_sharded_fitness, dim_sharded_fitness_local
 
+            if len(self._dim_shard_group) > 1:  # state-sharded: `transformed` is this rank's column block
+                _, col0, d = self._dim_shard_group
+                return dim_sharded_fitness_local(self.problem, transformed, col0, d, self._dim_shard_group[0]), state
             return dim_sharded_fitness(self.problem, transformed, self._dim_shard_group[0]), state
         if self.jit_problem:
             return use_state(self.problem.evaluate)(state, transformed)
@@ -402,7 +405,7 @@ class StdWorkflow(Workflow):
                 state = state.update_child("algorithm", alg.update(**{f: alg[f][start : start + size].clone() for f in local}))
         return state
 
-    def enable_multi_devices(self, state: State, devices=None) -> State:
+    def enable_multi_devices(self, state: State, devices=None, shard_state=None) -> State:
         """Shard the evaluation along the decision axis (reference
         ``std_workflow.py:272-309``, GSPMD over ``PositionalSharding(devices)``).
 
@@ -411,7 +414,13 @@ class StdWorkflow(Workflow):
         column block and the per-row partial terms are all-reduced
         (:class:`evoxmi.parallel.DimShardedProblem`); the algorithm stays replicated
         (same key on every rank).  Other problems fall back to population sharding.
-        The state structure is unchanged, so this may be called after ``init``."""
+        The state structure is unchanged, so this may be called after ``init``.
+
+        ``shard_state`` (default: whenever possible) shards the algorithm state too, as GSPMD
+        does for every (pop, dim) array: algorithms with ``dim_shard`` (PSO) keep only their
+        column block of the population / velocity / bests on each rank, and problems without
+        a halo evaluate that block — the only traffic is the (N, k) term all-reduce.  Solutions
+        seen by monitors are then the rank's column block."""
         if not self.jit_problem:
             raise ValueError("multi-devices with non jit problem isn't currently supported")
         if not (torch.distributed.is_available() and torch.distributed.is_initialized()):
@@ -421,7 +430,23 @@ class StdWorkflow(Workflow):
         if supports_dim_sharding(self.problem):
             from ..parallel.context import DistContext
 
+            from ..parallel.context import balanced_slices
+            from ..parallel.dim_sharded import supports_state_sharding
+
             ctx = DistContext(group=devices if isinstance(devices, torch.distributed.ProcessGroup) else None)
-            self._dim_shard_group = (ctx.group,)
-            return ctx.broadcast_state(state)
+            state = ctx.broadcast_state(state)
+            if shard_state is None:
+                shard_state = supports_state_sharding(self.algorithm, self.problem)
+            if shard_state:
+                if not supports_state_sharding(self.algorithm, self.problem):
+                    raise ValueError("state sharding needs an algorithm with dim_shard and a problem without halo / full rows")
+                d = int(self.algorithm.dim)
+                rank, world = torch.distributed.get_rank(ctx.group), torch.distributed.get_world_size(ctx.group)
+                col0, own = balanced_slices(d, world)[rank]
+                alg = state.get_child_state("algorithm")
+                state = state.update_child("algorithm", self.algorithm.dim_shard(alg, col0, own))
+                self._dim_shard_group = (ctx.group, col0, d)
+            else:
+                self._dim_shard_group = (ctx.group,)
+            return state
         return self.enable_distributed(state)

@@ -48,7 +48,7 @@ def _make():
     return StdWorkflow(PSO(lb=lb, ub=ub, pop_size=40), Ackley())
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, out, shard_state=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     torch.set_num_threads(1)
     from evoxmi.parallel import destroy, init_distributed
@@ -56,11 +56,11 @@ def _worker(rank, world, port, out):
     init_distributed(backend="gloo")
     wf = _make()
     st = wf.init(rnd.PRNGKey(3))
-    st = wf.enable_multi_devices(st)
+    st = wf.enable_multi_devices(st, shard_state=shard_state)
     for _ in range(20):
         st = wf.step(st)
     a = st.get_child_state("algorithm")
-    out[rank] = (a.global_best_fitness.clone(), a.population.clone())
+    out[rank] = (a.global_best_fitness.clone(), a.population.clone(), a.global_best_location.clone())
     destroy()
 
 
@@ -73,11 +73,36 @@ def test_enable_multi_devices_gloo_matches_single_process():
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
-    g0, p0 = out[0]
-    g1, p1 = out[1]
+    g0, p0, _ = out[0]
+    g1, p1, _ = out[1]
     assert torch.equal(p0, p1)  # replicas stay identical: every rank combines the same all-reduced terms
     assert torch.allclose(g0, ref.global_best_fitness, rtol=1e-4, atol=1e-4)
     assert torch.allclose(p0, ref.population, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_state_sharded_pso_gloo_matches_single_process(world):
+    """Full P2: every rank keeps only its column block of the swarm (population, velocity,
+    personal / global best locations) and draws the same Philox words for it as the unsharded
+    swarm; the concatenated blocks follow the single-process trajectory and the replicated
+    scalars agree bitwise across ranks."""
+    wf = _make()
+    st = wf.init(rnd.PRNGKey(3))
+    for _ in range(20):
+        st = wf.step(st)
+    ref = st.get_child_state("algorithm")
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), out, True), nprocs=world, join=True)
+    blocks = [out[r] for r in range(world)]
+    assert all(torch.equal(b[0], blocks[0][0]) for b in blocks)  # global best fitness replicated
+    widths = [b[1].shape[1] for b in blocks]
+    assert widths == [own for _, own in balanced_slices(30, world)]
+    pop = torch.cat([b[1] for b in blocks], 1)
+    gbl = torch.cat([b[2] for b in blocks], 0)
+    assert torch.allclose(blocks[0][0], ref.global_best_fitness, rtol=1e-4, atol=1e-4)
+    assert torch.allclose(pop, ref.population, rtol=1e-3, atol=1e-3)
+    assert torch.allclose(gbl, ref.global_best_location, rtol=1e-3, atol=1e-3)
 
 
 @pytest.mark.parametrize("fn", [1, 2, 3, 4, 5])

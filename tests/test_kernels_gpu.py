@@ -977,3 +977,29 @@ def test_cec_rotation_rowterms_epilogue_matches_cpu(fn, N, D):
     torch.testing.assert_close(out.cpu().double(), ref.double(), rtol=2e-4, atol=1e-3)
     if fused:  # the bench shape must take the fused path
         assert N != 10000 or int(_ext.ops().gemm_ks_tile(N, D, 0)) == 8
+
+
+@pytest.mark.parametrize("col0,own,d", [(0, 30, 30), (7, 11, 30), (13, 17, 30), (1, 1000, 1003)])
+def test_pso_column_block_update_matches_unsharded(col0, own, d):
+    """P2 state sharding: the column-block PSO kernel (Philox counter = row·d_total + column)
+    reproduces the corresponding columns of the unsharded update bit for bit."""
+    from evoxmi.ops.pso import pso_update
+
+    n = 37
+    g = torch.Generator().manual_seed(col0 + own)
+    pop, vel, lbl = (torch.rand(n, d, generator=g) * 10 - 5 for _ in range(3))
+    lbf, fit = torch.rand(n, generator=g), torch.rand(n, generator=g)
+    gbl, lb, ub = torch.rand(d, generator=g), torch.full((d,), -4.0), torch.full((d,), 4.0)
+    kp, kg = rnd.PRNGKey(11), rnd.PRNGKey(12)
+    cu = lambda t: t.cuda()
+    full = pso_update(cu(pop), cu(vel), cu(lbl), cu(lbf), cu(fit), cu(gbl), cu(kp), cu(kg), 0.6, 2.5, 0.8, cu(lb), cu(ub))
+    c = slice(col0, col0 + own)
+    part = pso_update(cu(pop[:, c].contiguous()), cu(vel[:, c].contiguous()), cu(lbl[:, c].contiguous()), cu(lbf), cu(fit),
+                      cu(gbl[c].contiguous()), cu(kp), cu(kg), 0.6, 2.5, 0.8, cu(lb[c].contiguous()), cu(ub[c].contiguous()),
+                      col0=col0, d_total=d)
+    for a, b in zip(full[:3], part[:3]):
+        assert torch.equal(a[:, c], b)
+    assert torch.equal(full[3], part[3])
+    cpu = pso_update(pop[:, c].contiguous(), vel[:, c].contiguous(), lbl[:, c].contiguous(), lbf, fit, gbl[c].contiguous(), kp, kg,
+                     0.6, 2.5, 0.8, lb[c].contiguous(), ub[c].contiguous(), col0=col0, d_total=d)
+    assert torch.allclose(cpu[0], part[0].cpu(), rtol=1e-5, atol=1e-5)
