@@ -336,9 +336,17 @@ void sbr16_bq_out(const at::Tensor& B, const at::Tensor& perm, const at::Tensor&
                Bq.stride(0), (int)sb, cur_stream(), skip.data_ptr<int>());
 }
 
-void sbr_damping_out(const at::Tensor& X2, const at::Tensor& V, double tau, at::Tensor& alpha, at::Tensor& work, const at::Tensor& skip) {
+void sbr_damping_out(const at::Tensor& X2, const at::Tensor& V, double tau, at::Tensor& alpha, at::Tensor& work, const at::Tensor& skip,
+                     const c10::optional<at::Tensor>& bar) {
   const int64_t n = X2.size(0);
   TORCH_CHECK(V.numel() >= n * 8 && work.numel() >= n * 24 && alpha.numel() >= 1, "sbr_damping_out: shapes");
+  if (bar.has_value() && bar->defined()) {  // one persistent launch (grid barriers), see eigh_sbr16.hip
+    CHECK_DEV(*bar);
+    TORCH_CHECK(bar->scalar_type() == at::kInt && bar->numel() >= 3 && bar->is_contiguous(), "sbr_damping_out: bar int32[3]");
+    evx_sbr_damping_fused(X2.data_ptr<float>(), (int)n, X2.stride(0), V.data_ptr<float>(), work.data_ptr<float>(), (float)tau,
+                          alpha.data_ptr<float>(), cur_stream(), skip.data_ptr<int>(), reinterpret_cast<uint32_t*>(bar->data_ptr<int>()));
+    return;
+  }
   evx_sbr_damping(X2.data_ptr<float>(), (int)n, X2.stride(0), V.data_ptr<float>(), work.data_ptr<float>(), (float)tau,
                   alpha.data_ptr<float>(), cur_stream(), skip.data_ptr<int>());
 }
@@ -817,7 +825,7 @@ at::Tensor dtlz(const at::Tensor& X, int64_t m, int64_t variant) {
 
 at::Tensor de_trial(const at::Tensor& P, const at::Tensor& idx, const at::Tensor& coef, const at::Tensor& cur, const at::Tensor& mode,
                     const at::Tensor& CR, const at::Tensor& jr, const at::Tensor& L, const at::Tensor& key, const at::Tensor& lb,
-                    const at::Tensor& ub, int64_t repair, const at::Tensor& err) {
+                    const at::Tensor& ub, int64_t repair, const at::Tensor& err, int64_t col0, int64_t d_total) {
   CHECK_DEV(P); CHECK_F32(P); CHECK_CONTIG(P);
   TORCH_CHECK(err.is_cuda() && err.scalar_type() == at::kInt && err.numel() >= 1, "de_trial: err must be int32[1] on the device");
   // single run: P (rows, d), idx (R, K), key (2,); B batched runs: P (B, rows, d), idx (B, R, K),
@@ -843,7 +851,7 @@ at::Tensor de_trial(const at::Tensor& P, const at::Tensor& idx, const at::Tensor
     evx_de_trial(P.data_ptr<float>(), i32(idx, Bn * R * K, "idx"), f32(coef, Bn * R * K, "coef"), (int)K, i32(cur, Bn * R, "cur"),
                  i32(mode, Bn * R, "mode"), f32(CR, Bn * R, "CR"), i32(jr, Bn * R, "jr"), i32(L, Bn * R, "L"), key.data_ptr<int64_t>(),
                  f32(lb, d, "lb"), f32(ub, d, "ub"), (int)repair, out.data_ptr<float>(), (int)R, (int)d, (int)rows, err.data_ptr<int>(),
-                 cur_stream(), (int)Bn);
+                 cur_stream(), (int)Bn, (int)col0, (int)d_total);
   return out;
 }
 
@@ -1214,7 +1222,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("ant_rollout(Tensor W, int h1, int h2, Tensor init, int cap) -> Tensor[]");
   m.def("stochastic_ranking(Tensor I1, Tensor I2, Tensor rnd, float pc) -> Tensor");
   m.def("moead_scan(Tensor objs, Tensor off_objs, Tensor P, Tensor W, Tensor z, int func, int nr, int update_z) -> Tensor[]");
-  m.def("de_trial(Tensor P, Tensor idx, Tensor coef, Tensor cur, Tensor mode, Tensor CR, Tensor jr, Tensor L, Tensor key, Tensor lb, Tensor ub, int repair, Tensor err) -> Tensor");
+  m.def("de_trial(Tensor P, Tensor idx, Tensor coef, Tensor cur, Tensor mode, Tensor CR, Tensor jr, Tensor L, Tensor key, Tensor lb, Tensor ub, int repair, Tensor err, int col0=0, int d_total=0) -> Tensor");
   m.def("dtlz(Tensor X, int m, int variant) -> Tensor");
   m.def("classic_eval(Tensor X, int func, float a, float b, float c) -> Tensor");
   m.def("gemm_f32(Tensor A, int a_rc, Tensor? a_gather, Tensor? a_sub, int a_sub_on_k, Tensor? a_kscale, Tensor? a_kw, Tensor? a_sscale, int a_sscale_inv, Tensor B, int b_rc, Tensor? b_gather, Tensor? b_sub, int b_sub_on_k, Tensor? b_kscale, Tensor? b_kw, Tensor? b_sscale, int b_sscale_inv, Tensor? alpha_ptr, Tensor? bias_n, float beta, Tensor? Cin, int M, int N, int K, int splits, float alpha) -> Tensor");
@@ -1226,7 +1234,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("sbr16_block_out(Tensor A, int shift, int sweeps, int sb, Tensor(a!) perm, Tensor(b!) Q, Tensor(c!) dq, Tensor skip) -> ()");
   m.def("sbr16_far_out(Tensor A, Tensor perm, Tensor Q, Tensor dq, Tensor stats, float thr_fac, Tensor theta, Tensor(a!) X, int sb, Tensor skip) -> ()");
   m.def("sbr16_bq_out(Tensor B, Tensor perm, Tensor Q, Tensor(a!) Bq, int sb, Tensor skip) -> ()");
-  m.def("sbr_damping_out(Tensor X2, Tensor V, float tau, Tensor(a!) alpha, Tensor(b!) work, Tensor skip) -> ()");
+  m.def("sbr_damping_out(Tensor X2, Tensor V, float tau, Tensor(a!) alpha, Tensor(b!) work, Tensor skip, Tensor(c!)? bar=None) -> ()");
   m.def("sbr_dev_prep(Tensor X, Tensor X2, Tensor X3, Tensor alpha, Tensor(a!) P, Tensor(b!) MT, Tensor ctrl) -> ()");
   m.def("sbr_dev_copy(Tensor src, Tensor(a!) dst, Tensor skip) -> ()");
   m.def("sbr_dev_ctrl(Tensor part, int nparts, int j, int K, Tensor(a!) hist, Tensor(b!) alpha, Tensor(c!) theta, Tensor(d!) ctrl, Tensor(e!) st, float[] prm, int ns_iters, Tensor A, Tensor(f!) w_out, Tensor(g!) eig_stats, Tensor(h!) w_init, Tensor(i!) log, Tensor(j!) log_count) -> ()");

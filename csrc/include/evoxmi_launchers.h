@@ -112,7 +112,7 @@ void evx_pm(const float* x, float* out, int n, int d, int nm, const float* lb, c
 void evx_dtlz(const float* X, float* F, int N, int D, int M, int variant, hipStream_t s);
 void evx_de_trial(const float* P, const int32_t* idx, const float* coef, int K, const int32_t* cur, const int32_t* mode,
                   const float* CR, const int32_t* jr, const int32_t* L, const int64_t* key, const float* lb, const float* ub,
-                  int repair, float* out, int R, int d, int rows, int* err, hipStream_t s, int batch = 1);
+                  int repair, float* out, int R, int d, int rows, int* err, hipStream_t s, int batch, int col0 = 0, int dtot = 0 = 1);
 void evx_moead_scan(float* objs, const float* off_objs, const int32_t* P, const float* W, float* z, int32_t* owner, int N, int R,
                     int T, int M, int func, int nr, int update_z, hipStream_t s);
 void evx_ant_rollout(const float* W, int64_t P, int N, int h1, int h2, const float* init, int cap, float* ret, int* steps, hipStream_t s);
@@ -162,6 +162,8 @@ int evx_sbr16_max_n();
 void evx_sbr_taylor4_prep(const float* X, const float* X2, int n, const float* alpha, float* P, float* M, hipStream_t s, int mt = 0);
 void evx_sbr_damping(const float* X2, int n, int64_t ldx, const float* V, float* work, float tau, float* alpha, hipStream_t s,
                      const int* skip = nullptr);
+void evx_sbr_damping_fused(const float* X2, int n, int64_t ldx, const float* V, float* work, float tau, float* alpha, hipStream_t s,
+                           const int* skip, uint32_t* bar);
 void evx_sbr16_block(const float* A, int n, int64_t lda, int shift, int sweeps, int* perm, float* Q, float* dq, int sb, hipStream_t s,
                      const int* skip = nullptr);
 void evx_sbr16_far(const float* A, int n, int64_t lda, const int* perm, const float* Q, const float* dq, const double* stats,

@@ -67,7 +67,7 @@ __global__ void __launch_bounds__(256) pm_kernel(const float* __restrict__ x, fl
   const float e1 = dis_m + 1.f, inv = 1.f / (dis_m + 1.f);
   const float pr = pro_m / d;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    const int i = (int)(t / d), j = (int)(t - (int64_t)i * d);
+    const int i = (int)(t / d), j = (int)(t - (int64_t)i * d), jg = col0 + j;
     float v = x[t];
     if (i < nm) {
       const float lo = lb[j], hi = ub[j], span = hi - lo;
@@ -111,7 +111,10 @@ __global__ void __launch_bounds__(256) de_trial_kernel(const float* __restrict__
                                                        const int32_t* __restrict__ jr, const int32_t* __restrict__ L,
                                                        const int64_t* __restrict__ key, const float* __restrict__ lb,
                                                        const float* __restrict__ ub, int repair, float* __restrict__ out, int R,
-                                                       int d, int rows, int* __restrict__ err) {
+                                                       int d, int rows, int* __restrict__ err, int col0, int dtot) {
+  // column block (decision-axis state sharding): P / out hold columns [col0, col0 + d) of a
+  // dtot-dimensional population; the Philox word, j_rand and the exponential window use the
+  // global column, so every block equals the same columns of the unsharded trials
   // batched runs: grid.y = run b; its R trial rows, P rows and key are run-local
   const int64_t b = blockIdx.y;
   P += b * rows * (int64_t)d;
@@ -123,7 +126,7 @@ __global__ void __launch_bounds__(256) de_trial_kernel(const float* __restrict__
   const uint32_t k0 = (uint32_t)key[0], k1 = (uint32_t)key[1];
   const int64_t total = (int64_t)R * d;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    const int i = (int)(t / d), j = (int)(t - (int64_t)i * d);
+    const int i = (int)(t / d), j = (int)(t - (int64_t)i * d), jg = col0 + j;
     float m = 0.f;
     for (int k = 0; k < K; ++k) {
       const float c = coef[i * K + k];
@@ -143,11 +146,11 @@ __global__ void __launch_bounds__(256) de_trial_kernel(const float* __restrict__
     const int md = mode[i];
     float v;
     if (md == 0) {
-      const float u = evx::u24(word_at((uint64_t)t, k0, k1));
-      v = (u < CR[i] || j == jr[i]) ? m : x;
+      const float u = evx::u24(word_at((uint64_t)i * dtot + jg, k0, k1));
+      v = (u < CR[i] || jg == jr[i]) ? m : x;
     } else if (md == 1) {
-      int pos = j - jr[i];
-      if (pos < 0) pos += d;
+      int pos = jg - jr[i];
+      if (pos < 0) pos += dtot;
       v = pos < L[i] ? m : x;
     } else {
       v = x + CR[i] * (m - x);
@@ -175,8 +178,9 @@ void evx_pm(const float* x, float* out, int n, int d, int nm, const float* lb, c
 
 void evx_de_trial(const float* P, const int32_t* idx, const float* coef, int K, const int32_t* cur, const int32_t* mode,
                   const float* CR, const int32_t* jr, const int32_t* L, const int64_t* key, const float* lb, const float* ub,
-                  int repair, float* out, int R, int d, int rows, int* err, hipStream_t s, int batch) {
+                  int repair, float* out, int R, int d, int rows, int* err, hipStream_t s, int batch, int col0, int dtot) {
   const int64_t total = (int64_t)R * d;
   const dim3 grid((int)std::min<int64_t>((total + 255) / 256, 8192), batch);
-  de_trial_kernel<<<grid, 256, 0, s>>>(P, idx, coef, K, cur, mode, CR, jr, L, key, lb, ub, repair, out, R, d, rows, err);
+  de_trial_kernel<<<grid, 256, 0, s>>>(P, idx, coef, K, cur, mode, CR, jr, L, key, lb, ub, repair, out, R, d, rows, err, col0,
+                                       dtot > 0 ? dtot : d);
 }

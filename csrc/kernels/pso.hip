@@ -6,6 +6,27 @@
 
 namespace {
 
+// one element's update, shared by both kernels so the column-block variant rounds exactly
+// like the unsharded one
+__device__ __forceinline__ void pso_elem(int64_t i, int r, int c, uint32_t up, uint32_t ug, const float* __restrict__ pop,
+                                         const float* __restrict__ vel, const float* __restrict__ lbl,
+                                         const float* __restrict__ lbf, const float* __restrict__ fit,
+                                         const float* __restrict__ gbl, float w, float phip, float phig,
+                                         const float* __restrict__ lb, const float* __restrict__ ub, float* __restrict__ opop,
+                                         float* __restrict__ ovel, float* __restrict__ olbl, float* __restrict__ olbf) {
+  // explicit FMA order, no compiler contraction: the same rounding in every kernel that inlines it
+#pragma clang fp contract(off)
+  const float x = pop[i];
+  const bool better = lbf[r] > fit[r];
+  const float lb_loc = better ? x : lbl[i];
+  const float social = (phig * evx::u24(ug)) * (gbl[c] - x);
+  const float v = fmaf(w, vel[i], fmaf(phip * evx::u24(up), lb_loc - x, social));
+  opop[i] = fminf(fmaxf(x + v, lb[c]), ub[c]);
+  ovel[i] = v;
+  olbl[i] = lb_loc;
+  if (c == 0) olbf[r] = fminf(lbf[r], fit[r]);
+}
+
 __global__ void __launch_bounds__(256) pso_kernel(const float* __restrict__ pop, const float* __restrict__ vel,
                                                   const float* __restrict__ lbl, const float* __restrict__ lbf,
                                                   const float* __restrict__ fit, const float* __restrict__ gbl,
@@ -29,15 +50,7 @@ __global__ void __launch_bounds__(256) pso_kernel(const float* __restrict__ pop,
       int64_t i = (b << 2) + j;
       if (i >= total) break;
       int r = (int)(i / D), c = (int)(i - (int64_t)r * D);
-      float x = pop[i];
-      bool better = lbf[r] > fit[r];
-      float lb_loc = better ? x : lbl[i];
-      float v = w * vel[i] + phip * evx::u24(rpw[j]) * (lb_loc - x) + phig * evx::u24(rgw[j]) * (gbl[c] - x);
-      float nx = fminf(fmaxf(x + v, lb[c]), ub[c]);
-      opop[i] = nx;
-      ovel[i] = v;
-      olbl[i] = lb_loc;
-      if (c == 0) olbf[r] = fminf(lbf[r], fit[r]);
+      pso_elem(i, r, c, rpw[j], rgw[j], pop, vel, lbl, lbf, fit, gbl, w, phip, phig, lb, ub, opop, ovel, olbl, olbf);
     }
   }
 }
@@ -64,14 +77,7 @@ __global__ void __launch_bounds__(256) pso_cols_kernel(const float* __restrict__
     const int j = (int)(gi & 3);
     const uint32_t up = j == 0 ? wp.x : (j == 1 ? wp.y : (j == 2 ? wp.z : wp.w));
     const uint32_t ug = j == 0 ? wg.x : (j == 1 ? wg.y : (j == 2 ? wg.z : wg.w));
-    const float x = pop[i];
-    const bool better = lbf[r] > fit[r];
-    const float lb_loc = better ? x : lbl[i];
-    const float v = w * vel[i] + phip * evx::u24(up) * (lb_loc - x) + phig * evx::u24(ug) * (gbl[c] - x);
-    opop[i] = fminf(fmaxf(x + v, lb[c]), ub[c]);
-    ovel[i] = v;
-    olbl[i] = lb_loc;
-    if (c == 0) olbf[r] = fminf(lbf[r], fit[r]);
+    pso_elem(i, r, c, up, ug, pop, vel, lbl, lbf, fit, gbl, w, phip, phig, lb, ub, opop, ovel, olbl, olbf);
   }
 }
 

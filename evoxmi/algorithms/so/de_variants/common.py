@@ -175,14 +175,18 @@ def as_strategy(strat, R, device):
 
 
 def generate_trials(key, population, fitness, best_index, cur, strategy, F, CR, diff_padding_num: int, lb, ub, *,
-                    p=0.05, reduced=None, archive=None, rank_k=None, Fw=None, repair="clip", choices=None):
+                    p=0.05, reduced=None, archive=None, rank_k=None, Fw=None, repair="clip", choices=None, cols=None):
     """Trial vectors for target rows ``cur`` (R,) under per-row strategies.
 
     Returns ``(trials (R, d), rand_idx (R,))``.  ``Fw`` scales the pbest term
     (jSO's F_w).  ``choices`` optionally provides pre-drawn difference indices into
-    the population (plain DE / ODE path).
+    the population (plain DE / ODE path).  ``cols = (col0, d_total)``: ``population`` is this
+    rank's column block of a d_total-dim population (decision-axis state sharding); every
+    per-row draw is the unsharded one and the trial block equals those columns of the
+    unsharded trials.
     """
     N, d = population.shape
+    col0, d_tot = cols if cols is not None else (0, d)
     R = cur.shape[0]
     dev = population.device
     k_sel, k_pb, k_jr, k_u, k_exp = rnd.split(key, 5)
@@ -212,12 +216,12 @@ def generate_trials(key, population, fitness, best_index, cur, strategy, F, CR, 
     keep = (j < 2 * nd[:, None] + 1).to(torch.float32)
     sign = torch.where(j % 2 == 1, 1.0, -1.0)
     coef = torch.cat([base_coef, F[:, None] * keep * sign], 1)
-    jr = rnd.randint(k_jr, (R,), 0, d).to(dev)
+    jr = rnd.randint(k_jr, (R,), 0, d_tot).to(dev)
     # exponential crossover: window length min(Geometric(CR), d) − 1 from a random start
     u = rnd.uniform(k_exp, (R,)).to(dev)
     geo = torch.where(CR >= 1, torch.ones_like(u), torch.ceil(torch.log(u) / torch.log1p(-CR.clamp(max=1 - 1e-7))))
-    L = (torch.minimum(geo, torch.full_like(geo, d)) - 1).to(torch.int32)
-    trials = evo_ops.de_trial(k_u, Pext, idx, coef, cur + off, cross, CR, jr, L, lb, ub, repair)
+    L = (torch.minimum(geo, torch.full_like(geo, d_tot)) - 1).to(torch.int32)
+    trials = evo_ops.de_trial(k_u, Pext, idx, coef, cur + off, cross, CR, jr, L, lb, ub, repair, col0=col0, d_total=d_tot)
     return trials, choices[:, 0]
 
 

@@ -46,6 +46,16 @@ class DE(Algorithm):
             ch = C.sample_distinct(key, cur.shape[0], k, N, None, cur.device)
         return C._remap_self(ch, cur, N)
 
+    # -- decision-axis state sharding (P2): mutation, crossover and the greedy replacement are
+    # column-separable given the replicated per-row draws (difference rows, j_rand) and the
+    # replicated fitness, so a rank keeps only its column block of population and trials
+    _cols = None
+
+    def dim_shard(self, state, col0: int, own: int):
+        self._cols = (int(col0), int(own), self.dim)
+        c = slice(col0, col0 + own)
+        return state.update(population=state.population[:, c].contiguous(), trial_vectors=state.trial_vectors[:, c].contiguous())
+
     def _trials(self, state, key):
         pop = state.population
         N = pop.shape[0]
@@ -53,8 +63,10 @@ class DE(Algorithm):
         cur = torch.arange(N, device=pop.device)
         b = C.BEST if self.base_vector == "best" else C.RAND
         strat = (b, b, self.num_difference_vectors, C.BIN)
+        c0, own, d = self._cols if self._cols is not None else (0, self.dim, self.dim)
         trials, _ = C.generate_trials(k_tr, pop, state.fitness, state.best_index, cur, strat, self.differential_weight,
-                                      self.cross_probability, 0, self.lb, self.ub, choices=self._choices(k_ch, N, cur))
+                                      self.cross_probability, 0, self.lb[c0 : c0 + own], self.ub[c0 : c0 + own],
+                                      choices=self._choices(k_ch, N, cur), cols=(c0, d))
         return trials
 
     def ask(self, state):

@@ -73,12 +73,12 @@ def _rank_argsort_f32(info, in_dims, keys, descending):
     return (ok, oi), (0, 0)
 
 
-def _de_trial(info, in_dims, P, idx, coef, cur, mode, CR, jr, L, key, lb, ub, repair, err):
+def _de_trial(info, in_dims, P, idx, coef, cur, mode, CR, jr, L, key, lb, ub, repair, err, col0=0, d_total=0):
     B = info.batch_size
     if any(d is not None for d in in_dims[9:11]) or in_dims[12] is not None:
         raise NotImplementedError("de_trial vmap rule: bounds and the error word must be shared by all runs")
     args = [_front(t, d, B) for t, d in zip((P, idx, coef, cur, mode, CR, jr, L, key), in_dims[:9])]
-    return _ext.ops().de_trial(*args, lb, ub, repair, err), 0
+    return _ext.ops().de_trial(*args, lb, ub, repair, err, col0, d_total), 0
 
 
 def register():

@@ -36,7 +36,7 @@ def kernel_error_flags(device="cuda") -> int:
 _REPAIR = {"none": 0, "clip": 1, "midpoint": 2}
 
 
-def de_trial(key, P, idx, coef, cur, mode, CR, jr, L, lb, ub, repair="clip"):
+def de_trial(key, P, idx, coef, cur, mode, CR, jr, L, lb, ub, repair="clip", col0: int = 0, d_total: int = None):
     """Fused DE trial vectors (``evo_ops.hip: de_trial_kernel``).
 
     P: (rows, d) candidate matrix (population, or population ∪ archive);
@@ -45,6 +45,8 @@ def de_trial(key, P, idx, coef, cur, mode, CR, jr, L, lb, ub, repair="clip"):
     CR: (R,) crossover rate (arith: recombination weight); jr: (R,) j_rand (bin) or
     window start (exp); L: (R,) exp window length; ``key`` seeds u(i, j) exactly as
     ``uniform(key, (R, d))``.  The CPU branch is the numerics oracle.
+    ``col0`` / ``d_total``: ``P`` holds the column block [col0, col0 + d) of a d_total-dim
+    population (decision-axis state sharding); draws, j_rand and windows use global columns.
     """
     R, K = idx.shape
     d = P.shape[1]
@@ -57,7 +59,7 @@ def de_trial(key, P, idx, coef, cur, mode, CR, jr, L, lb, ub, repair="clip"):
         f32 = lambda t: t.to(device=dev, dtype=torch.float32).contiguous()
         err = _err_flag(dev)
         out = _ext.ops().de_trial(P.contiguous(), i32(idx), f32(coef), i32(cur), i32(mode), f32(CR), i32(jr), i32(L),
-                                  key.contiguous(), lb, ub, rep, err)
+                                  key.contiguous(), lb, ub, rep, err, int(col0), int(d if d_total is None else d_total))
         if config.get("debug") and not torch.cuda.is_current_stream_capturing():
             bad = int(err.item())
             if bad:
@@ -66,10 +68,11 @@ def de_trial(key, P, idx, coef, cur, mode, CR, jr, L, lb, ub, repair="clip"):
         return out
     m = torch.einsum("rk,rkd->rd", coef.to(P.dtype), P[idx.long()])
     x = P[cur.long()]
-    j = torch.arange(d, device=dev)[None, :]
-    u = rnd.uniform(key, (R, d))
+    dt = d if d_total is None else int(d_total)
+    j = torch.arange(col0, col0 + d, device=dev)[None, :]
+    u = rnd.uniform(key, (R, dt))[:, col0 : col0 + d]
     bin_mask = (u < CR[:, None]) | (j == jr[:, None])
-    pos = (j - jr[:, None]) % d
+    pos = (j - jr[:, None]) % dt
     exp_mask = pos < L[:, None]
     mode = mode[:, None]
     v = torch.where(mode == 0, torch.where(bin_mask, m, x),

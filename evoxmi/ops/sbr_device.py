@@ -37,6 +37,12 @@ from .sbr import SBRConfig, _probe_vectors
 LOG_LEN = 4096
 
 
+def config_fused_damping() -> bool:
+    from .. import config
+
+    return bool(config.get("sbr_fused_damping"))
+
+
 class DeviceSBR:
     """Persistent buffers + the fixed iteration schedule for one (n, device, config)."""
 
@@ -66,6 +72,8 @@ class DeviceSBR:
         self.ctrl = torch.ones(8 * max(K, 1), dtype=torch.int32, device=dev)
         self.st = torch.zeros(8, dtype=torch.int32, device=dev)
         self.never = torch.zeros(1, dtype=torch.int32, device=dev)
+        # grid-barrier words of the one-launch damping ([count, generation, error])
+        self.bar = torch.zeros(4, dtype=torch.int32, device=dev) if config_fused_damping() else None
         self.V = _probe_vectors(n, str(dev))
         self.work = torch.zeros(24 * n, device=dev)
         self.w = torch.zeros(n, device=dev)
@@ -98,7 +106,7 @@ class DeviceSBR:
         # X skew ⇒ X² = −X·Xᵀ, symmetric (upper tiles only)
         mm(self.X, self.X, tb=True, mode=1, alpha=-1.0, out=self.X2, skip=sk_far)
         if cfg.damp_tau > 0:
-            ops.sbr_damping_out(self.X2, self.V, float(cfg.damp_tau), self.alpha[j + 1 : j + 2], self.work, sk_damp)
+            ops.sbr_damping_out(self.X2, self.V, float(cfg.damp_tau), self.alpha[j + 1 : j + 2], self.work, sk_damp, self.bar)
         ops.sbr16_bq_out(self.B, self.perm, self.Q, self.Bq, sb, sk_all)
         # order 6 only: X³ = X²·X = −X²·Xᵀ (skew)
         mm(self.X2, self.X, tb=True, mode=2, alpha=-1.0, out=self.X3, skip=sk_x3)

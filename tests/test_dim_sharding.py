@@ -80,6 +80,49 @@ def test_enable_multi_devices_gloo_matches_single_process():
     assert torch.allclose(p0, ref.population, rtol=1e-3, atol=1e-3)
 
 
+def _de_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from evoxmi.parallel import destroy, init_distributed
+
+    init_distributed(backend="gloo")
+    wf = _make_de()
+    st = wf.init(rnd.PRNGKey(4))
+    st = wf.enable_multi_devices(st)
+    for _ in range(15):
+        st = wf.step(st)
+    a = st.get_child_state("algorithm")
+    out[rank] = (a.fitness.clone(), a.population.clone())
+    destroy()
+
+
+def _make_de():
+    from evoxmi.algorithms import DE
+
+    lb, ub = torch.full((30,), -5.0), torch.full((30,), 5.0)
+    return StdWorkflow(DE(lb, ub, 40), Rastrigin())
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_state_sharded_de_gloo_matches_single_process(world):
+    """Full P2 for DE: mutation, binomial crossover (global j_rand and Philox words) and the
+    greedy replacement run on each rank's column block; the blocks reassemble the
+    single-process population."""
+    wf = _make_de()
+    st = wf.init(rnd.PRNGKey(4))
+    for _ in range(15):
+        st = wf.step(st)
+    ref = st.get_child_state("algorithm")
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_de_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    blocks = [out[r] for r in range(world)]
+    assert all(torch.equal(b[0], blocks[0][0]) for b in blocks)
+    assert [b[1].shape[1] for b in blocks] == [own for _, own in balanced_slices(30, world)]
+    assert torch.allclose(blocks[0][0], ref.fitness, rtol=1e-4, atol=1e-3)
+    assert torch.allclose(torch.cat([b[1] for b in blocks], 1), ref.population, rtol=1e-4, atol=1e-4)
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_state_sharded_pso_gloo_matches_single_process(world):
     """Full P2: every rank keeps only its column block of the swarm (population, velocity,

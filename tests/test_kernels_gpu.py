@@ -1003,3 +1003,33 @@ def test_pso_column_block_update_matches_unsharded(col0, own, d):
     cpu = pso_update(pop[:, c].contiguous(), vel[:, c].contiguous(), lbl[:, c].contiguous(), lbf, fit, gbl[c].contiguous(), kp, kg,
                      0.6, 2.5, 0.8, lb[c].contiguous(), ub[c].contiguous(), col0=col0, d_total=d)
     assert torch.allclose(cpu[0], part[0].cpu(), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("col0,own,d", [(0, 30, 30), (7, 11, 30), (29, 1, 30), (3, 500, 1001)])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_de_trial_column_block_matches_unsharded(col0, own, d, mode):
+    """P2 state sharding for DE: a column block of the trial vectors (global Philox word, j_rand
+    and exponential window) equals those columns of the unsharded fused trials, and the CPU
+    oracle of the block."""
+    from evoxmi.ops.evo import de_trial
+
+    R, rows, K = 23, 40, 3
+    g = torch.Generator().manual_seed(col0 + own + mode)
+    P = torch.rand(rows, d, generator=g) * 10 - 5
+    idx = torch.randint(0, rows, (R, K), generator=g, dtype=torch.int32)
+    coef = torch.rand(R, K, generator=g)
+    cur = torch.arange(R, dtype=torch.int32)
+    md = torch.full((R,), mode, dtype=torch.int32)
+    CR = torch.rand(R, generator=g)
+    jr = torch.randint(0, d, (R,), generator=g, dtype=torch.int32)
+    L = torch.randint(0, d, (R,), generator=g, dtype=torch.int32)
+    lb, ub = torch.full((d,), -4.0), torch.full((d,), 4.0)
+    key = rnd.PRNGKey(7)
+    cu = lambda t: t.cuda()
+    full = de_trial(cu(key), cu(P), cu(idx), cu(coef), cu(cur), cu(md), cu(CR), cu(jr), cu(L), cu(lb), cu(ub))
+    c = slice(col0, col0 + own)
+    part = de_trial(cu(key), cu(P[:, c].contiguous()), cu(idx), cu(coef), cu(cur), cu(md), cu(CR), cu(jr), cu(L), cu(lb[c].contiguous()),
+                    cu(ub[c].contiguous()), col0=col0, d_total=d)
+    assert torch.equal(full[:, c], part)
+    cpu = de_trial(key, P[:, c].contiguous(), idx, coef, cur, md, CR, jr, L, lb[c].contiguous(), ub[c].contiguous(), col0=col0, d_total=d)
+    assert torch.allclose(cpu, part.cpu(), rtol=1e-5, atol=1e-5)
