@@ -67,7 +67,7 @@ __global__ void __launch_bounds__(256) pm_kernel(const float* __restrict__ x, fl
   const float e1 = dis_m + 1.f, inv = 1.f / (dis_m + 1.f);
   const float pr = pro_m / d;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    const int i = (int)(t / d), j = (int)(t - (int64_t)i * d), jg = col0 + j;
+    const int i = (int)(t / d), j = (int)(t - (int64_t)i * d);
     float v = x[t];
     if (i < nm) {
       const float lo = lb[j], hi = ub[j], span = hi - lo;
