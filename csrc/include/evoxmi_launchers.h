@@ -112,7 +112,7 @@ void evx_pm(const float* x, float* out, int n, int d, int nm, const float* lb, c
 void evx_dtlz(const float* X, float* F, int N, int D, int M, int variant, hipStream_t s);
 void evx_de_trial(const float* P, const int32_t* idx, const float* coef, int K, const int32_t* cur, const int32_t* mode,
                   const float* CR, const int32_t* jr, const int32_t* L, const int64_t* key, const float* lb, const float* ub,
-                  int repair, float* out, int R, int d, int rows, int* err, hipStream_t s, int batch, int col0 = 0, int dtot = 0 = 1);
+                  int repair, float* out, int R, int d, int rows, int* err, hipStream_t s, int batch = 1, int col0 = 0, int dtot = 0);
 void evx_moead_scan(float* objs, const float* off_objs, const int32_t* P, const float* W, float* z, int32_t* owner, int N, int R,
                     int T, int M, int func, int nr, int update_z, hipStream_t s);
 void evx_ant_rollout(const float* W, int64_t P, int N, int h1, int h2, const float* init, int cap, float* ret, int* steps, hipStream_t s);
