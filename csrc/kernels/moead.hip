@@ -279,16 +279,23 @@ __global__ void __launch_bounds__(256) select_rows_kernel(const float* __restric
 // Owner-computes MOEA/D (population-sharded): the replacement of only the slots a rank
 // must keep current (its halo: every neighbour of its own slots), in place on the
 // objective matrix (a slot reads and writes only its own row).
+// One wave per slot; each slot has ~T candidates (T = ⌈N/10⌉, the reference's neighbourhood:
+// 1629 at the north-star shape), so the scan is the work: every lane keeps several independent
+// candidate chains (owner index → objective row → aggregation) in flight per iteration instead
+// of one dependent chain per candidate (eight with a compile-time objective count MT > 0).
+template <int MT>
 __global__ void __launch_bounds__(256) halo_replace_kernel(float* __restrict__ obj, const float* __restrict__ off_obj,
                                                            const float* __restrict__ W, const float* __restrict__ zp,
                                                            const float* __restrict__ zmaxp, const int32_t* __restrict__ rowptr,
                                                            const int32_t* __restrict__ owner, const int32_t* __restrict__ slots,
-                                                           int H, int M, int func, int32_t* __restrict__ win_h) {
+                                                           int H, int Mrt, int func, int32_t* __restrict__ win_h) {
+  constexpr int MA = MT > 0 ? MT : MAXM;
+  const int M = MT > 0 ? MT : Mrt;
   const int lane = threadIdx.x & 63;
   const int h = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (h >= H) return;
   const int s = slots[h];
-  float w[MAXM], z[MAXM], zm[MAXM], f[MAXM];
+  float w[MA], z[MA], zm[MA];
   for (int k = 0; k < M; ++k) {
     w[k] = W[(int64_t)s * M + k];
     z[k] = zp[k];
@@ -297,11 +304,21 @@ __global__ void __launch_bounds__(256) halo_replace_kernel(float* __restrict__ o
   float best = INFINITY;
   int bi = 0x7fffffff;
   const int b = rowptr[s], e = rowptr[s + 1];
-  for (int q = b + lane; q < e; q += 64) {
-    const int i = owner[q];
-    for (int k = 0; k < M; ++k) f[k] = off_obj[(int64_t)i * M + k];
-    const float v = agg(func, f, w, z, zm, M);
-    if (v < best || (v == best && i < bi)) { best = v; bi = i; }
+  constexpr int U = MT > 0 ? 8 : 4;  // candidate chains in flight per lane
+  for (int q0 = b + lane; q0 < e; q0 += U * 64) {
+    int ii[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) ii[u] = q0 + 64 * u < e ? owner[q0 + 64 * u] : -1;
+    float fv[U][MA];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      for (int k = 0; k < M; ++k) fv[u][k] = ii[u] >= 0 ? off_obj[(int64_t)ii[u] * M + k] : 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (ii[u] < 0) continue;
+      const float v = agg(func, fv[u], w, z, zm, M);
+      if (v < best || (v == best && ii[u] < bi)) { best = v; bi = ii[u]; }
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -309,6 +326,7 @@ __global__ void __launch_bounds__(256) halo_replace_kernel(float* __restrict__ o
     const int oi = __shfl_xor(bi, o, 64);
     if (ob < best || (ob == best && oi < bi)) { best = ob; bi = oi; }
   }
+  float f[MA];
   for (int k = 0; k < M; ++k) f[k] = obj[(int64_t)s * M + k];
   const float old = agg(func, f, w, z, zm, M);
   const bool take = bi != 0x7fffffff && best < old;
@@ -377,7 +395,11 @@ void evx_moead_select_rows(const float* pop, const float* off, const int32_t* wi
 
 void evx_moead_halo_replace(float* obj, const float* off_obj, const float* W, const float* z, const float* zmax, const int32_t* rowptr,
                             const int32_t* owner, const int32_t* slots, int H, int M, int func, int32_t* win_h, hipStream_t s) {
-  if (H > 0) halo_replace_kernel<<<(H + 3) / 4, 256, 0, s>>>(obj, off_obj, W, z, zmax, rowptr, owner, slots, H, M, func, win_h);
+  if (H <= 0) return;
+  const int g = (H + 3) / 4;
+  if (M == 3) halo_replace_kernel<3><<<g, 256, 0, s>>>(obj, off_obj, W, z, zmax, rowptr, owner, slots, H, M, func, win_h);
+  else if (M == 2) halo_replace_kernel<2><<<g, 256, 0, s>>>(obj, off_obj, W, z, zmax, rowptr, owner, slots, H, M, func, win_h);
+  else halo_replace_kernel<0><<<g, 256, 0, s>>>(obj, off_obj, W, z, zmax, rowptr, owner, slots, H, M, func, win_h);
 }
 
 void evx_moead_halo_gather(float* pop, const int32_t* slots, const int32_t* win_h, int H, const int64_t* peer, const int32_t* starts,
