@@ -1044,6 +1044,19 @@ at::Tensor moead_select_rows(const at::Tensor& pop, const at::Tensor& off, const
   return out;
 }
 
+// pop[s] = off[win[s]] for the winning slots, in place (hipGraph path: no new population and no
+// state write-back copy)
+void moead_select_rows_(at::Tensor& pop, const at::Tensor& off, const at::Tensor& win) {
+  CHECK_DEV(pop); CHECK_F32(pop); CHECK_CONTIG(pop); CHECK_DEV(off); CHECK_F32(off); CHECK_CONTIG(off);
+  TORCH_CHECK(win.is_cuda() && win.scalar_type() == at::kInt && win.is_contiguous() && win.numel() == pop.size(0), "moead_select_rows_: win int32[N]");
+  TORCH_CHECK(off.dim() == 2 && off.size(1) == pop.size(1), "moead_select_rows_: off (rows, d)");
+  TORCH_CHECK(pop.data_ptr() != off.data_ptr(), "moead_select_rows_: off must not alias pop");
+  c10::DeviceGuard g(pop.device());
+  if (pop.size(0) > 0 && pop.size(1) > 0)
+    evx_moead_select_rows_inplace(pop.data_ptr<float>(), off.data_ptr<float>(), win.data_ptr<int>(), (int)pop.size(0), (int)pop.size(1),
+                                  cur_stream());
+}
+
 at::Tensor lsmop_g(const at::Tensor& X, std::vector<int64_t> start, std::vector<int64_t> sublen, std::vector<int64_t> func, int64_t nk, int64_t cosine) {
   CHECK_DEV(X); CHECK_F32(X); CHECK_CONTIG(X);
   const int64_t ng = (int64_t)start.size();
@@ -1256,6 +1269,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("ipc_close(int ptr) -> ()");
   m.def("moead_replace(Tensor pop_obj, Tensor off_obj, Tensor W, Tensor z, Tensor zmax, Tensor rowptr, Tensor owner, int func) -> Tensor[]");
   m.def("moead_select_rows(Tensor pop, Tensor off, Tensor win) -> Tensor");
+  m.def("moead_select_rows_(Tensor(a!) pop, Tensor off, Tensor win) -> ()");
   m.def("sbr_stats(Tensor A) -> Tensor");
   m.def("sbr_block(Tensor A, int off, int sweeps, Tensor? dbg=None) -> Tensor[]");
   m.def("sbr_far(Tensor A, int off, Tensor perm, Tensor Q, Tensor dq, Tensor stats, float thr_fac) -> Tensor");
@@ -1325,6 +1339,7 @@ TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
   m.impl("moead_parents", &moead_parents);
   m.impl("moead_variation", &moead_variation);
   m.impl("moead_replace", &moead_replace);
+  m.impl("moead_select_rows_", &moead_select_rows_);
   m.impl("moead_select_rows", &moead_select_rows);
   m.impl("sbr_stats", &sbr_stats);
   m.impl("sbr_block", &sbr_block);

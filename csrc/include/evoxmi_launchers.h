@@ -130,6 +130,7 @@ void evx_moead_replace(const float* pop_obj, const float* off_obj, const float* 
                        const int32_t* rowptr, const int32_t* owner, int N, int M, int func, int32_t* win, float* new_obj,
                        hipStream_t s);
 void evx_moead_select_rows(const float* pop, const float* off, const int32_t* win, float* out, int N, int d, hipStream_t s);
+void evx_moead_select_rows_inplace(float* pop, const float* off, const int32_t* win, int N, int d, hipStream_t s);
 void evx_lsmop_g(const float* X, float* G, int N, int D, int ng, int nk, int cosine, const int* start, const int* sublen, const int* func,
                  hipStream_t s);
 

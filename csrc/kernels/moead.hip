@@ -276,6 +276,26 @@ __global__ void __launch_bounds__(256) select_rows_kernel(const float* __restric
   }
 }
 
+// in-place variant: only the winning slots' rows are written (pop[s] = off[win[s]]); the
+// hipGraph path updates the captured population buffer directly instead of building a new
+// population that the graph's state write-back then copies back (2 × 651 MB per generation at
+// the north-star shape)
+__global__ void __launch_bounds__(256) select_rows_inplace_kernel(float* __restrict__ pop, const float* __restrict__ off,
+                                                                  const int32_t* __restrict__ win, int N, int d) {
+  const int row = blockIdx.y;
+  const int w = win[row];
+  if (w < 0) return;
+  const float* src = off + (int64_t)w * d;
+  float* dst = pop + (int64_t)row * d;
+  if ((d & 3) == 0) {
+    const int q = d >> 2;
+    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < q; c += gridDim.x * blockDim.x)
+      reinterpret_cast<float4*>(dst)[c] = reinterpret_cast<const float4*>(src)[c];
+  } else {
+    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < d; c += gridDim.x * blockDim.x) dst[c] = src[c];
+  }
+}
+
 // Owner-computes MOEA/D (population-sharded): the replacement of only the slots a rank
 // must keep current (its halo: every neighbour of its own slots), in place on the
 // objective matrix (a slot reads and writes only its own row).
@@ -391,6 +411,12 @@ void evx_moead_select_rows(const float* pop, const float* off, const int32_t* wi
   const int q = (d & 3) == 0 ? d >> 2 : d;
   dim3 grid((q + 255) / 256 < 16 ? (q + 255) / 256 : 16, N);
   select_rows_kernel<<<grid, 256, 0, s>>>(pop, off, win, out, N, d);
+}
+
+void evx_moead_select_rows_inplace(float* pop, const float* off, const int32_t* win, int N, int d, hipStream_t s) {
+  const int q = (d & 3) == 0 ? d >> 2 : d;
+  dim3 grid((q + 255) / 256 < 16 ? (q + 255) / 256 : 16, N);
+  select_rows_inplace_kernel<<<grid, 256, 0, s>>>(pop, off, win, N, d);
 }
 
 void evx_moead_halo_replace(float* obj, const float* off_obj, const float* W, const float* z, const float* zmax, const int32_t* rowptr,

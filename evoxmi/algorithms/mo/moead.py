@@ -171,7 +171,17 @@ class MOEAD(Algorithm):
     def ask(self, state):
         key, sub, sel_key, mut_key = rnd.split(state.key, 4)
         parents = self._parent_pairs(state, sub)
-        off = self._offspring_rows(state, parents, sel_key, mut_key)
+        buf = state.next_generation
+        if (torch.cuda.is_current_stream_capturing() and self._fused(state.population) and buf is not None
+                and buf.shape == state.population.shape and buf.is_contiguous() and buf.data_ptr() != state.population.data_ptr()):
+            # hipGraph: generate straight into the captured offspring buffer (no state write-back copy)
+            from ...ops import mo as mo_ops
+
+            c, m = self.crossover, self.mutation
+            off = mo_ops.moead_variation(state.population, parents[0].contiguous(), parents[1].contiguous(), sel_key, mut_key, self.lb,
+                                         self.ub, c.pro_c, c.dis_c, m.pro_m, m.dis_m, out=buf)
+        else:
+            off = self._offspring_rows(state, parents, sel_key, mut_key)
         return off, state.update(next_generation=off, key=key, parents=parents, var_keys=torch.stack([sel_key, mut_key]))
 
     def _reverse(self, state):
@@ -198,7 +208,12 @@ class MOEAD(Algorithm):
         if state.population.is_cuda and state.population.dtype == torch.float32:
             from ...ops import mo as mo_ops
 
-            new_pop = mo_ops.moead_select_rows(state.population, state.next_generation, win)
+            if torch.cuda.is_current_stream_capturing() and state.population.is_contiguous():
+                # hipGraph: the captured population buffer is the one the next replay reads, so
+                # only the winning rows are written and the state write-back has nothing to copy
+                new_pop = mo_ops.moead_select_rows_(state.population, state.next_generation, win)
+            else:
+                new_pop = mo_ops.moead_select_rows(state.population, state.next_generation, win)
         else:
             new_pop = torch.where((win >= 0)[:, None], state.next_generation[win.long().clamp_min(0)], state.population)
         return state.update(population=new_pop, fitness=new_obj, z=z, win=win)

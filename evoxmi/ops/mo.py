@@ -104,3 +104,9 @@ def moead_replace(pop_obj, off_obj, w, z, z_max, rowptr, owner, func):
 def moead_select_rows(pop, off, win):
     """pop'[s] = off[win[s]] if win[s] >= 0 else pop[s]."""
     return _ext.ops().moead_select_rows(pop.contiguous(), off.contiguous(), win.to(torch.int32).contiguous())
+
+
+def moead_select_rows_(pop, off, win):
+    """In place: pop[s] = off[win[s]] for every s with win[s] >= 0 (returns ``pop``)."""
+    _ext.ops().moead_select_rows_(pop, off.contiguous(), win.to(torch.int32).contiguous())
+    return pop
