@@ -69,6 +69,37 @@ __device__ __forceinline__ float wave_reduce(float v, int op) {  // op 0 sum, 1 
   return v;
 }
 
+// one segment's partial terms for inner function FN (a: sum / max, b: product / second sum),
+// this lane's elements i = lane, lane + 64, …; four loads in flight per lane (the loop body is
+// straight-line, the function chosen at compile time) — one load per iteration left the kernel
+// waiting on HBM latency 79 % of its cycles
+template <int FN>
+__device__ __forceinline__ void seg_terms(const float* __restrict__ x, int s0, int L, int lane, float x0, float invd, int cosine,
+                                          float& a, float& b) {
+  auto link = [&](int c) {
+    const float t = cosine ? cosf((float)(c + 1) * invd * (PI_F * 0.5f)) : (float)(c + 1) * invd;
+    return (1.f + t) * x[c] - 10.f * x0;
+  };
+  auto acc = [&](int i, float z) {
+    if (FN == 0) a += z * z;                                                                  // sphere
+    else if (FN == 1) { a += z * z; b *= cosf(z * rsqrtf((float)(i + 1))); }                 // griewank
+    else if (FN == 2) {                                                                       // rosenbrock
+      if (i + 1 < L) { const float zn = link(s0 + i + 1), u = zn - z * z; a += 100.f * u * u + (z - 1.f) * (z - 1.f); }
+    } else if (FN == 3) { a += z * z; b += cosf(2.f * PI_F * z); }                          // ackley
+    else if (FN == 4) a = fmaxf(a, fabsf(z));                                                // schwefel (max |z|)
+    else a += z * z - 10.f * cosf(2.f * PI_F * z) + 10.f;                                     // rastrigin
+  };
+  int i = lane;
+  for (; i + 192 < L; i += 256) {
+    const float z0 = link(s0 + i), z1 = link(s0 + i + 64), z2 = link(s0 + i + 128), z3 = link(s0 + i + 192);
+    acc(i, z0);
+    acc(i + 64, z1);
+    acc(i + 128, z2);
+    acc(i + 192, z3);
+  }
+  for (; i < L; i += 64) acc(i, link(s0 + i));
+}
+
 // one wave64 per row (no block barriers: every reduction is a 6-step xor butterfly)
 __global__ void __launch_bounds__(256) lsmop_g_kernel(const float* __restrict__ X, float* __restrict__ G, int N, int D, LsmopGroups gr) {
   const int lane = threadIdx.x & 63;
@@ -77,10 +108,6 @@ __global__ void __launch_bounds__(256) lsmop_g_kernel(const float* __restrict__ 
   const float* x = X + (int64_t)row * D;
   const float x0 = x[0];
   const float invd = 1.f / (float)D;
-  auto link = [&](int c) {
-    const float t = gr.cosine ? cosf((float)(c + 1) * invd * (PI_F * 0.5f)) : (float)(c + 1) * invd;
-    return (1.f + t) * x[c] - 10.f * x0;
-  };
   float gout = 0.f;
   for (int k = 0; k < gr.ng; ++k) {
     const int L = gr.sublen[k], fn = gr.func[k];
@@ -88,17 +115,13 @@ __global__ void __launch_bounds__(256) lsmop_g_kernel(const float* __restrict__ 
     for (int sub = 0; sub < gr.nk; ++sub) {
       const int s0 = gr.start[k] + sub * L;
       float a = 0.f, b = (fn == 1) ? 1.f : 0.f;
-      for (int i = lane; i < L; i += 64) {
-        const float z = link(s0 + i);
-        switch (fn) {
-          case 0: a += z * z; break;                                                     // sphere
-          case 1: a += z * z; b *= cosf(z * rsqrtf((float)(i + 1))); break;              // griewank
-          case 2: if (i + 1 < L) { const float zn = link(s0 + i + 1), u = zn - z * z;    // rosenbrock
-                    a += 100.f * u * u + (z - 1.f) * (z - 1.f); } break;
-          case 3: a += z * z; b += cosf(2.f * PI_F * z); break;                          // ackley
-          case 4: a = fmaxf(a, fabsf(z)); break;                                         // schwefel (max |z|)
-          default: a += z * z - 10.f * cosf(2.f * PI_F * z) + 10.f; break;               // rastrigin
-        }
+      switch (fn) {
+        case 0: seg_terms<0>(x, s0, L, lane, x0, invd, gr.cosine, a, b); break;
+        case 1: seg_terms<1>(x, s0, L, lane, x0, invd, gr.cosine, a, b); break;
+        case 2: seg_terms<2>(x, s0, L, lane, x0, invd, gr.cosine, a, b); break;
+        case 3: seg_terms<3>(x, s0, L, lane, x0, invd, gr.cosine, a, b); break;
+        case 4: seg_terms<4>(x, s0, L, lane, x0, invd, gr.cosine, a, b); break;
+        default: seg_terms<5>(x, s0, L, lane, x0, invd, gr.cosine, a, b); break;
       }
       float v;
       if (fn == 4) {
