@@ -565,6 +565,16 @@ __device__ __forceinline__ float xor8(float x) {
 // (= the slowest wave) took 16.3 instead of 8.9 ms at pop 1024.
 constexpr int ANT_WAVES = 4;
 
+typedef float ant_f4 __attribute__((ext_vector_type(4)));
+
+// KM > 0: layer 2's first KM inputs go through the matrix cores while the VALU takes the rest, both
+// issued from the same wave so the two pipes run concurrently.  v_mfma_f32_4x4x1_16b_f32 with
+// A = the lane's weight (block b = output units 4b..4b+3) and B = a1[k] in all four columns: every
+// block column holds the same four sums, so c[lane & 3] is unit `lane` whatever the column order.
+// tools/k15_mfma_probe.hip measured the isolated 64x64 layer (one wave): VALU 1100 cycles, MFMA-only
+// 4x4x1 1078, 16x16x4 with the vector padded to 16 columns 2755, split 16 / 48 907
+// (profiles/r3_k15_mfma_probe.log).
+template <int KM>
 __global__ void __launch_bounds__(64 * ANT_WAVES, 2) ant_rollout_reg_kernel(const float* __restrict__ W, int64_t P, int N, int h1, int h2,
                                                                           const float* __restrict__ init, int cap, float* __restrict__ ret,
                                                                           int* __restrict__ steps_out, int trace) {
@@ -625,16 +635,37 @@ __global__ void __launch_bounds__(64 * ANT_WAVES, 2) ant_rollout_reg_kernel(cons
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    float c4[4] = {b2, 0.f, 0.f, 0.f};
+    float a2;
+    if constexpr (KM == 0) {
+      float c4[4] = {b2, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const float4 a = reinterpret_cast<const float4*>(a1s)[i];
-      c4[0] = fmaf(a.x, w2[4 * i], c4[0]);
-      c4[1] = fmaf(a.y, w2[4 * i + 1], c4[1]);
-      c4[2] = fmaf(a.z, w2[4 * i + 2], c4[2]);
-      c4[3] = fmaf(a.w, w2[4 * i + 3], c4[3]);
+      for (int i = 0; i < 16; ++i) {
+        const float4 a = reinterpret_cast<const float4*>(a1s)[i];
+        c4[0] = fmaf(a.x, w2[4 * i], c4[0]);
+        c4[1] = fmaf(a.y, w2[4 * i + 1], c4[1]);
+        c4[2] = fmaf(a.z, w2[4 * i + 2], c4[2]);
+        c4[3] = fmaf(a.w, w2[4 * i + 3], c4[3]);
+      }
+      a2 = fast_tanh((c4[0] + c4[1]) + (c4[2] + c4[3]));
+    } else {
+      ant_f4 m[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+      float c2[2] = {b2, 0.f};
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float4 a = reinterpret_cast<const float4*>(a1s)[i];
+        const float av[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int k = 4 * i + q;
+          if (k < KM)
+            m[q & 1] = __builtin_amdgcn_mfma_f32_4x4x1f32(w2[k], av[q], m[q & 1], 0, 0, 0);
+          else
+            c2[q & 1] = fmaf(av[q], w2[k], c2[q & 1]);
+        }
+      }
+      const int r = lane & 3;
+      a2 = fast_tanh((m[0][r] + m[1][r]) + (c2[0] + c2[1]));
     }
-    const float a2 = fast_tanh((c4[0] + c4[1]) + (c4[2] + c4[3]));
     // 8 partial products → transposing butterfly reduction
     float v4[4], v2[2], v1;
 #pragma unroll
@@ -692,7 +723,22 @@ void evx_ant_rollout(const float* W, int64_t P, int N, int h1, int h2, const flo
       const char* e = getenv("EVOXMI_ANT_TRACE");
       return e ? atoi(e) : 0;
     }();
-    ant_rollout_reg_kernel<<<(N + ANT_WAVES - 1) / ANT_WAVES, 64 * ANT_WAVES, 0, s>>>(W, P, N, h1, h2, init, cap, ret, steps, trace);
+    // EVOXMI_ANT_L2_MFMA: inputs of layer 2 on the matrix cores.  Default 0 (VALU only): inside the
+    // rollout the split saves nothing measurable (1000-step latency 8.63 ms at 0, 8.70 at 16, 8.67 at 32;
+    // profiles/r3_k15_ant_l2_mfma_ab.txt) - layer 2 is ≈5 % of a control step, the rest is the body.
+    static const int km = [] {
+      const char* e = getenv("EVOXMI_ANT_L2_MFMA");
+      return e ? atoi(e) : 0;
+    }();
+    const dim3 grid((N + ANT_WAVES - 1) / ANT_WAVES), block(64 * ANT_WAVES);
+    if (km >= 32)
+      ant_rollout_reg_kernel<32><<<grid, block, 0, s>>>(W, P, N, h1, h2, init, cap, ret, steps, trace);
+    else if (km >= 16)
+      ant_rollout_reg_kernel<16><<<grid, block, 0, s>>>(W, P, N, h1, h2, init, cap, ret, steps, trace);
+    else if (km >= 8)
+      ant_rollout_reg_kernel<8><<<grid, block, 0, s>>>(W, P, N, h1, h2, init, cap, ret, steps, trace);
+    else
+      ant_rollout_reg_kernel<0><<<grid, block, 0, s>>>(W, P, N, h1, h2, init, cap, ret, steps, trace);
     return;
   }
   const int64_t per = (P + 32 + h1 + h2 + 8) * 4;
