@@ -172,7 +172,7 @@ class MOEAD(Algorithm):
         key, sub, sel_key, mut_key = rnd.split(state.key, 4)
         parents = self._parent_pairs(state, sub)
         buf = state.next_generation
-        if (torch.cuda.is_current_stream_capturing() and self._fused(state.population) and buf is not None
+        if (state.population.is_cuda and torch.cuda.is_current_stream_capturing() and self._fused(state.population) and buf is not None
                 and buf.shape == state.population.shape and buf.is_contiguous() and buf.data_ptr() != state.population.data_ptr()):
             # hipGraph: generate straight into the captured offspring buffer (no state write-back copy)
             from ...ops import mo as mo_ops
