@@ -417,6 +417,24 @@ std::vector<at::Tensor> radix_argsort_f32(const at::Tensor& keys, int64_t descen
 }
 
 // same contract as radix_argsort_f32: rank-by-counting, one launch for n ≤ 16384 (sort.hip)
+std::vector<at::Tensor> merge_argsort_f32(const at::Tensor& keys, int64_t descending) {
+  CHECK_DEV(keys); CHECK_F32(keys); CHECK_CONTIG(keys);
+  TORCH_CHECK(keys.dim() <= 2, "merge_argsort_f32: keys must be (n,) or (B, n)");
+  const int64_t B = keys.dim() == 2 ? keys.size(0) : 1;
+  const int64_t n = keys.dim() == 0 ? 1 : keys.size(-1);
+  TORCH_CHECK(n <= evx_merge_argsort_max_n(), "merge_argsort_f32: n > ", evx_merge_argsort_max_n());
+  TORCH_CHECK(B * ((n + 4095) / 4096) <= 65535, "merge_argsort_f32: B * chunks > 65535");
+  c10::DeviceGuard g(keys.device());
+  auto ok = at::empty_like(keys);
+  auto oi = at::empty(keys.sizes(), keys.options().dtype(at::kInt));
+  auto wk = at::empty(keys.sizes(), keys.options().dtype(at::kInt));
+  auto wi = at::empty(keys.sizes(), keys.options().dtype(at::kInt));
+  if (n > 0 && B > 0)
+    evx_merge_argsort(keys.data_ptr<float>(), (int)n, (int)descending, ok.data_ptr<float>(), oi.data_ptr<int32_t>(),
+                      reinterpret_cast<uint32_t*>(wk.data_ptr<int32_t>()), wi.data_ptr<int32_t>(), cur_stream(), (int)B);
+  return {ok, oi};
+}
+
 std::vector<at::Tensor> rank_argsort_f32(const at::Tensor& keys, int64_t descending) {
   CHECK_DEV(keys); CHECK_F32(keys); CHECK_CONTIG(keys);
   TORCH_CHECK(keys.dim() <= 2, "rank_argsort_f32: keys must be (n,) or (B, n)");
@@ -1224,6 +1242,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("argsort_f32(Tensor keys, int descending) -> Tensor[]");
   m.def("radix_argsort_f32(Tensor keys, int descending) -> Tensor[]");
   m.def("rank_argsort_f32(Tensor keys, int descending) -> Tensor[]");
+  m.def("merge_argsort_f32(Tensor keys, int descending) -> Tensor[]");
   m.def("cec_basic(Tensor Z, int fid, Tensor? perm, int start, int L, Tensor? sub, float scale, Tensor? Y, int ystart, int yperm) -> Tensor");
   m.def("jacobi_sweeps(Tensor A, Tensor B, Tensor sched, int sweeps, float tol, float inner_tol, int max_inner, int fused=2) -> Tensor[]");
   m.def("philox_words(Tensor key, int nblocks, int domain, int offset) -> Tensor");
@@ -1315,6 +1334,7 @@ TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
   m.impl("argsort_f32", &argsort_f32);
   m.impl("radix_argsort_f32", &radix_argsort_f32);
   m.impl("rank_argsort_f32", &rank_argsort_f32);
+  m.impl("merge_argsort_f32", &merge_argsort_f32);
   m.impl("gemm_f32", &gemm_f32);
   m.impl("gemm_ks", &gemm_ks_new);
   m.impl("gemm_ks_out", &gemm_ks_out);

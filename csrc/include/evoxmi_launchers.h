@@ -207,3 +207,8 @@ void evx_moead_halo_gather(float* pop, const int32_t* slots, const int32_t* win_
 // rank-by-counting stable argsort in one launch (sort.hip), n ≤ evx_rank_argsort_max_n()
 int evx_rank_argsort_max_n();
 void evx_rank_argsort(const float* keys, int n, int descending, float* out_keys, int32_t* out_idx, hipStream_t s, int batch);
+// two-pass stable argsort for n ≤ evx_merge_argsort_max_n(): rank inside 4096-key chunks, then co-rank
+// merge by lockstep binary searches; ws_keys / ws_idx hold batch * n entries each
+int evx_merge_argsort_max_n();
+void evx_merge_argsort(const float* keys, int n, int descending, float* out_keys, int32_t* out_idx, uint32_t* ws_keys,
+                       int32_t* ws_idx, hipStream_t s, int batch);

@@ -179,16 +179,24 @@ __device__ __forceinline__ uint32_t ord_key(float x, bool desc) {
   return desc ? ~o : o;
 }
 
+//
+// Chunked mode (m > 0, the first pass of the merge sort below): blockIdx.y = row * C + chunk, the
+// workgroup ranks inside its m-key chunk only and writes the chunk-sorted ORDERED keys to ws_keys and
+// the row-global indices to out_idx, both at row * N + chunk * m + rank.
 template <int WAVES>
-__global__ void __launch_bounds__(64 * WAVES) rank_argsort_kernel(const float* __restrict__ keys, int n, int desc,
-                                                                  float* __restrict__ out_keys, int32_t* __restrict__ out_idx) {
+__global__ void __launch_bounds__(64 * WAVES) rank_argsort_kernel(const float* __restrict__ keys, int N, int desc,
+                                                                  float* __restrict__ out_keys, int32_t* __restrict__ out_idx,
+                                                                  int m = 0, uint32_t* __restrict__ ws_keys = nullptr) {
   extern __shared__ uint4 sk4[];  // 16-byte aligned: the compare loops read four keys per ds_read_b128
   __shared__ int part[WAVES][64];
   uint32_t* sk = reinterpret_cast<uint32_t*>(sk4);
-  const float* kb = keys + (int64_t)blockIdx.y * n;
+  const int C = m > 0 ? (N + m - 1) / m : 1;
+  const int row = blockIdx.y / C, cb = m > 0 ? (int)(blockIdx.y % C) * m : 0;
+  const int n = m > 0 ? min(m, N - cb) : N;  // keys in this workgroup's chunk
+  const float* kb = keys + (int64_t)row * N + cb;
   const int np = (n + 3) & ~3;
   const bool d = desc != 0;
-  if ((n & 3) == 0) {  // rows 16-byte aligned: float4 loads, all in flight before the first use
+  if (((n | N | cb) & 3) == 0) {  // 16-byte aligned: float4 loads, all in flight before the first use
     const float4* kb4 = reinterpret_cast<const float4*>(kb);
 #pragma unroll 4
     for (int v = threadIdx.x; v < (n >> 2); v += 64 * WAVES) {
@@ -237,9 +245,93 @@ __global__ void __launch_bounds__(64 * WAVES) rank_argsort_kernel(const float* _
     int r = 0;
 #pragma unroll
     for (int v = 0; v < WAVES; ++v) r += part[v][lane];
-    out_idx[(int64_t)blockIdx.y * n + r] = i;
-    if (out_keys) out_keys[(int64_t)blockIdx.y * n + r] = kb[i];
+    const int64_t o = (int64_t)row * N + cb + r;
+    out_idx[o] = cb + i;
+    if (ws_keys) ws_keys[o] = ki;
+    else if (out_keys) out_keys[o] = kb[i];
   }
+}
+
+// Second pass of the merge sort for n beyond one LDS-resident row: element p of chunk c (sorted by the
+// chunked rank pass) lands at  p - c·m + Σ_{c' ≠ c} #{keys of chunk c' before it}, counting equal keys of
+// earlier chunks (smaller indices) and not those of later ones — the stable-sort position.  The CMAX
+// binary searches run in lockstep, branch-free over the fixed log2(m) + 1 levels, so each level issues up to
+// CMAX - 1 independent L2 loads per lane instead of one dependent chain per chunk.
+template <int CMAX, int LOGM>
+__global__ void __launch_bounds__(256) corank_merge_kernel(const float* __restrict__ keys, const uint32_t* __restrict__ wk,
+                                                           const int32_t* __restrict__ wi, int N, float* __restrict__ out_keys,
+                                                           int32_t* __restrict__ out_idx) {
+  constexpr int M = 1 << LOGM;
+  const int row = blockIdx.y, p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= N) return;
+  const int C = (N + M - 1) >> LOGM;
+  const uint32_t* rk = wk + (int64_t)row * N;
+  const uint32_t k = rk[p];
+  const int c = p >> LOGM;
+  int base[CMAX];
+#pragma unroll
+  for (int c2 = 0; c2 < CMAX; ++c2) base[c2] = 0;  // #keys of chunk c2 that go before k
+#pragma unroll
+  for (int half = M; half >= 1; half >>= 1) {  // halves sum to 2M - 1: a whole chunk of M keys can be before k
+#pragma unroll
+    for (int c2 = 0; c2 < CMAX; ++c2) {
+      if (c2 >= C || c2 == c) continue;
+      const int len = min(M, N - (c2 << LOGM));
+      const int probe = base[c2] + half;  // is the key at position probe - 1 before k?
+      if (probe <= len) {
+        const uint32_t v = rk[(c2 << LOGM) + probe - 1];
+        if (c2 < c ? v <= k : v < k) base[c2] = probe;
+      }
+    }
+  }
+  int pos = p - (c << LOGM);
+#pragma unroll
+  for (int c2 = 0; c2 < CMAX; ++c2) pos += base[c2];
+  const int gi = wi[(int64_t)row * N + p];
+  out_idx[(int64_t)row * N + pos] = gi;
+  if (out_keys) out_keys[(int64_t)row * N + pos] = keys[(int64_t)row * N + gi];
+}
+
+
+// The same merge with the row's chunk-sorted keys staged in LDS (n ≤ 32768: 128 KiB), so the
+// log2(m) + 1 search levels are LDS round trips instead of L2 ones.
+template <int CMAX, int LOGM>
+__global__ void __launch_bounds__(1024) corank_merge_lds_kernel(const float* __restrict__ keys, const uint32_t* __restrict__ wk,
+                                                                const int32_t* __restrict__ wi, int N, float* __restrict__ out_keys,
+                                                                int32_t* __restrict__ out_idx) {
+  extern __shared__ uint32_t srk[];
+  constexpr int M = 1 << LOGM;
+  const int row = blockIdx.y, p = blockIdx.x * 1024 + threadIdx.x;
+  const uint32_t* rk = wk + (int64_t)row * N;
+#pragma unroll 4
+  for (int j = threadIdx.x; j < N; j += 1024) srk[j] = rk[j];
+  __syncthreads();
+  if (p >= N) return;
+  const int C = (N + M - 1) >> LOGM;
+  const uint32_t k = srk[p];
+  const int c = p >> LOGM;
+  int base[CMAX];
+#pragma unroll
+  for (int c2 = 0; c2 < CMAX; ++c2) base[c2] = 0;
+#pragma unroll
+  for (int half = M; half >= 1; half >>= 1) {
+#pragma unroll
+    for (int c2 = 0; c2 < CMAX; ++c2) {
+      if (c2 >= C || c2 == c) continue;
+      const int len = min(M, N - (c2 << LOGM));
+      const int probe = base[c2] + half;
+      if (probe <= len) {
+        const uint32_t v = srk[(c2 << LOGM) + probe - 1];
+        if (c2 < c ? v <= k : v < k) base[c2] = probe;
+      }
+    }
+  }
+  int pos = p - (c << LOGM);
+#pragma unroll
+  for (int c2 = 0; c2 < CMAX; ++c2) pos += base[c2];
+  const int gi = wi[(int64_t)row * N + p];
+  out_idx[(int64_t)row * N + pos] = gi;
+  if (out_keys) out_keys[(int64_t)row * N + pos] = keys[(int64_t)row * N + gi];
 }
 
 }  // namespace
@@ -279,4 +371,33 @@ void evx_rank_argsort(const float* keys, int n, int descending, float* out_keys,
     if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)rank_argsort_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     rank_argsort_kernel<16><<<grid, 1024, lds, s>>>(keys, n, descending, out_keys, out_idx);
   }
+}
+
+int evx_merge_argsort_max_n() { return 16 * 4096; }
+
+void evx_merge_argsort(const float* keys, int n, int descending, float* out_keys, int32_t* out_idx, uint32_t* ws_keys,
+                       int32_t* ws_idx, hipStream_t s, int batch) {
+  constexpr int LOGM = 12, M = 1 << LOGM;
+  const int C = (n + M - 1) / M;
+  rank_argsort_kernel<16><<<dim3(M / 64, batch * C), 1024, M * 4, s>>>(keys, n, descending, nullptr, ws_idx, M, ws_keys);
+  if ((size_t)n * 4 <= 128 * 1024) {  // the whole chunk-sorted row fits in LDS: search there
+    const dim3 g((n + 1023) / 1024, batch);
+    const size_t lds = (size_t)n * 4;
+    if (lds > 64 * 1024) {
+      (void)hipFuncSetAttribute((const void*)corank_merge_lds_kernel<4, LOGM>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      (void)hipFuncSetAttribute((const void*)corank_merge_lds_kernel<8, LOGM>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    }
+    if (C <= 4)
+      corank_merge_lds_kernel<4, LOGM><<<g, 1024, lds, s>>>(keys, ws_keys, ws_idx, n, out_keys, out_idx);
+    else
+      corank_merge_lds_kernel<8, LOGM><<<g, 1024, lds, s>>>(keys, ws_keys, ws_idx, n, out_keys, out_idx);
+    return;
+  }
+  const dim3 grid((n + 255) / 256, batch);
+  if (C <= 4)
+    corank_merge_kernel<4, LOGM><<<grid, 256, 0, s>>>(keys, ws_keys, ws_idx, n, out_keys, out_idx);
+  else if (C <= 8)
+    corank_merge_kernel<8, LOGM><<<grid, 256, 0, s>>>(keys, ws_keys, ws_idx, n, out_keys, out_idx);
+  else
+    corank_merge_kernel<16, LOGM><<<grid, 256, 0, s>>>(keys, ws_keys, ws_idx, n, out_keys, out_idx);
 }

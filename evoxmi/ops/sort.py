@@ -3,7 +3,11 @@ north-star configs): the rank-by-counting argsort of ``sort.hip`` — all keys i
 256-thread workgroup ranks 64 elements against all n keys, one launch, no workspace, and
 n/64 workgroups spread over the CUs (the single-workgroup radix/bitonic kernels cannot:
 round 2 measured them at 43.9 / 119.8 µs for n = 10 000 against the library's 32.5,
-profiles/r2_sort_microbench.log).  Larger inputs use the ROCm library radix sort.  Ties are
+profiles/r2_sort_microbench.log).  From 8192 to 32768 keys the two-pass merge sort takes over:
+rank inside 4096-key chunks, then place every element by lockstep binary searches of the other
+sorted chunks staged in LDS (17.4 µs at 16 384, 33 µs at 30 000 against torch.sort's 32.8 / 42.6;
+reference primitives: src/evox/algorithms/so/es_variants/sort_utils.py:5-12,
+src/evox/operators/selection/topk_fit.py:7-12).  Larger inputs use the ROCm library radix sort.  Ties are
 broken by index (== stable sort); NaN sorts as the largest key and −0.0 ties with +0.0, as
 in ``torch.sort``.  Numbers: ``tools/bench_sort.py`` → profiles/r3_sort_microbench.log."""
 from __future__ import annotations
@@ -12,17 +16,24 @@ import torch
 
 from . import _ext
 
-MAX_RANK_SORT = 16384
+MAX_RANK_SORT = 8192     # one-launch rank-by-counting up to here (profiles/r3_sort_microbench.log)
+MAX_DEVICE_SORT = 32768  # two-pass merge up to here; the library radix sort beyond
 
 
 def _device(keys):
-    return keys.is_cuda and keys.dtype == torch.float32 and keys.dim() <= 2 and keys.shape[-1] <= MAX_RANK_SORT
+    return keys.is_cuda and keys.dtype == torch.float32 and keys.dim() <= 2 and keys.shape[-1] <= MAX_DEVICE_SORT
+
+
+def _sort(keys, descending):
+    ops = _ext.ops()
+    fn = ops.rank_argsort_f32 if keys.shape[-1] <= MAX_RANK_SORT else ops.merge_argsort_f32
+    return fn(keys.contiguous(), int(descending))
 
 
 def argsort(keys: torch.Tensor, descending: bool = False):
     """Return ``(sorted_keys, indices[int64])`` along the last dim of a 1-D or (B, n) float tensor."""
     if _device(keys):
-        k, i = _ext.ops().rank_argsort_f32(keys.contiguous(), int(descending))
+        k, i = _sort(keys, descending)
         return k, i.long()
     v, i = torch.sort(keys, descending=descending, stable=True)
     return v, i
@@ -31,7 +42,7 @@ def argsort(keys: torch.Tensor, descending: bool = False):
 def argsort_i32(keys: torch.Tensor):
     """Ascending argsort returning int32 indices (feeds gather prologues directly)."""
     if _device(keys):
-        return _ext.ops().rank_argsort_f32(keys.contiguous(), 0)
+        return _sort(keys, False)
     v, i = torch.sort(keys, stable=True)
     return v, i.to(torch.int32)
 
@@ -58,6 +69,8 @@ def topk(x: torch.Tensor, k: int, dim: int = -1, largest: bool = True):
             idx.append(j)
             work = work.scatter(-1, j, fill)  # out of place: also runs under vmap
         ind = torch.cat(idx, -1)
+    elif _device(x):
+        ind = argsort(x, descending=largest)[1][..., :k]
     else:
         ind = torch.argsort(x, dim=-1, descending=largest, stable=True)[..., :k]
     return torch.gather(x, -1, ind), ind
