@@ -122,6 +122,12 @@ class CMAES(Algorithm):
             if config.get("plain_gemm") == "blas":
                 return plain_nt(z, (state.B * (state.D * state.sigma)).contiguous(), bias_n=state.mean)
             BD = (state.B * state.D).contiguous()
+            buf = state.population
+            if (rows == self.pop_size and torch.cuda.is_current_stream_capturing() and buf.is_contiguous()
+                    and buf.shape == (rows, d)):
+                # hipGraph: sample straight into the captured population buffer (the previous
+                # generation's rows are dead once ask runs), so the state write-back has no 40 MB copy
+                return mm(z, BD, tb=True, alpha_ptr=state.sigma.reshape(1), bias_n=state.mean, out=buf)
             return mm(z, BD, tb=True, alpha_ptr=state.sigma.reshape(1), bias_n=state.mean)
         return state.mean + state.sigma * (state.D * z) @ state.B.T
 
@@ -208,9 +214,19 @@ class CMAES(Algorithm):
                 w, Bp = jacobi.warm_eigh_padded(Cp, Bp, d, max_sweeps=self.eig_sweeps)
             B, D, BdivD = ops.cma_eig_out(Bp, w, d)
         # (B/D)·Bᵀ is symmetric: upper tiles only
-        invsqrtC = plain_nt(BdivD, B) if config.get("plain_gemm") == "blas" else mm(BdivD, B, tb=True, mode=1)
+        capturing = torch.cuda.is_current_stream_capturing()
+        if config.get("plain_gemm") == "blas":
+            invsqrtC = plain_nt(BdivD, B)
+        elif capturing and state.invsqrtC.is_contiguous():
+            # hipGraph: the old invsqrtC was last read by cma_delta_gemv above (stream order), so the
+            # new one goes straight into the captured buffer
+            invsqrtC = mm(BdivD, B, tb=True, mode=1, out=state.invsqrtC)
+        else:
+            invsqrtC = mm(BdivD, B, tb=True, mode=1)
+        # outside a graph the stats buffer is the solver's own and is reused: the state keeps a copy
+        # (under capture the state write-back is that copy)
         return state.update(mean=mean, ps=ps, pc=pc, C=C, sigma=sigma.reshape(state.sigma.shape), B=B, D=D, invsqrtC=invsqrtC,
-                            count_eigen=state.count_eigen + 1, eig_stats=eig_stats.clone())
+                            count_eigen=state.count_eigen + 1, eig_stats=eig_stats if capturing else eig_stats.clone())
 
     def _finish_tell(self, state, dm, S):
         if self._fused_epilogue_ok(state):

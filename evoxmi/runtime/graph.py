@@ -30,12 +30,34 @@ def capturing() -> bool:
     return _ACTIVE is not None and torch.cuda.is_current_stream_capturing()
 
 
+def _words(t: torch.Tensor):
+    """A contiguous tensor whose size is a whole number of 32-bit words, viewed as int32 words."""
+    if t.is_contiguous() and t.element_size() in (4, 8) and t.numel() > 0:
+        return t.reshape(-1).view(torch.int32)
+    return None
+
+
 def copy_into(dst: Sequence[torch.Tensor], src: Sequence[torch.Tensor]):
-    """dst[i].copy_(src[i]) for all i as one multi-tensor launch when the tensors share a
-    dtype and device (``torch._foreach_copy_``), else tensor by tensor."""
+    """dst[i].copy_(src[i]) for all i.  Same-dtype pairs on one device share one multi-tensor launch
+    (``torch._foreach_copy_``); pairs of different 4- and 8-byte dtypes are copied as int32 words so
+    that, e.g., a float32 / int64 / float64 state write-back is still one launch."""
     dst, src = list(dst), list(src)
     if not dst:
         return
+    if len(dst) > 1 and hasattr(torch, "_foreach_copy_") and len({d.dtype for d in dst}) > 1:
+        wd, ws, rest = [], [], []
+        for d, s_ in zip(dst, src):
+            a, b = _words(d), _words(s_)
+            if a is not None and b is not None and d.dtype == s_.dtype and d.device == s_.device == dst[0].device:
+                wd.append(a)
+                ws.append(b)
+            else:
+                rest.append((d, s_))
+        if len(wd) > 1:
+            torch._foreach_copy_(wd, ws)
+            for d, s_ in rest:
+                d.copy_(s_)
+            return
     same = all(d.dtype == dst[0].dtype and d.device == dst[0].device and s.dtype == d.dtype and s.device == d.device
                for d, s in zip(dst, src))
     if same and len(dst) > 1 and hasattr(torch, "_foreach_copy_"):

@@ -265,11 +265,12 @@ class StdWorkflow(Workflow):
                         if a.shape != b.shape or a.dtype != b.dtype:
                             raise RuntimeError("graph=True: a state tensor changed shape/dtype across a step")
                         if a.data_ptr() != b.data_ptr():
-                            groups.setdefault((a.dtype, a.device), ([], []))
-                            groups[(a.dtype, a.device)][0].append(a)
-                            groups[(a.dtype, a.device)][1].append(b)
+                            groups.setdefault(a.device, ([], []))
+                            groups[a.device][0].append(a)
+                            groups[a.device][1].append(b)
                 # write the new state into the static buffers with one multi-tensor copy per
-                # dtype (a dozen small leaves would otherwise be a dozen copy launches per replay)
+                # device (a dozen small leaves of mixed dtypes would otherwise be a dozen copy
+                # launches per replay; copy_into moves them as 32-bit words)
                 for dst, src in groups.values():
                     copy_into(dst, src)
                 return in_leaves, out_leaves
