@@ -452,7 +452,7 @@ std::vector<at::Tensor> rank_argsort_f32(const at::Tensor& keys, int64_t descend
 
 at::Tensor cec_basic(const at::Tensor& Z, int64_t fid, const c10::optional<at::Tensor>& perm, int64_t start, int64_t L,
                      const c10::optional<at::Tensor>& sub, double scale, const c10::optional<at::Tensor>& Y, int64_t ystart,
-                     int64_t yperm) {
+                     int64_t yperm, double clamp) {
   CHECK_DEV(Z); CHECK_F32(Z);
   TORCH_CHECK(Z.dim() == 2 && Z.stride(1) == 1, "Z must be 2-D row-major");
   const int32_t* pp = nullptr;
@@ -475,7 +475,7 @@ at::Tensor cec_basic(const at::Tensor& Z, int64_t fid, const c10::optional<at::T
   auto out = at::empty({Z.size(0)}, Z.options());
   if (Z.size(0) > 0)
     evx_cec_basic(Z.data_ptr<float>(), Z.stride(0), (int)Z.size(0), (int)fid, pp, (int)start, (int)L, optf(sub), (float)scale,
-                  yp, ldy, (int)ystart, (int)yperm, out.data_ptr<float>(), cur_stream());
+                  yp, ldy, (int)ystart, (int)yperm, out.data_ptr<float>(), cur_stream(), (float)clamp);
   return out;
 }
 
@@ -1243,7 +1243,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("radix_argsort_f32(Tensor keys, int descending) -> Tensor[]");
   m.def("rank_argsort_f32(Tensor keys, int descending) -> Tensor[]");
   m.def("merge_argsort_f32(Tensor keys, int descending) -> Tensor[]");
-  m.def("cec_basic(Tensor Z, int fid, Tensor? perm, int start, int L, Tensor? sub, float scale, Tensor? Y, int ystart, int yperm) -> Tensor");
+  m.def("cec_basic(Tensor Z, int fid, Tensor? perm, int start, int L, Tensor? sub, float scale, Tensor? Y, int ystart, int yperm, float clamp=0.0) -> Tensor");
   m.def("jacobi_sweeps(Tensor A, Tensor B, Tensor sched, int sweeps, float tol, float inner_tol, int max_inner, int fused=2) -> Tensor[]");
   m.def("philox_words(Tensor key, int nblocks, int domain, int offset) -> Tensor");
   m.def("weighted_rowsum(Tensor X, Tensor? idx, Tensor w, Tensor? sub, int K) -> Tensor");

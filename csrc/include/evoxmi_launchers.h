@@ -80,7 +80,7 @@ void evx_radix_argsort(const float* keys, int n, int descending, float* out_keys
 int evx_argsort_max_n();
 void evx_argsort(const float* keys, int n, int descending, float* out_keys, int32_t* out_idx, hipStream_t s, int batch = 1);
 void evx_cec_basic(const float* Z, int64_t ld, int N, int fid, const int32_t* perm, int start, int L, const float* sub,
-                   float scale, const float* Y, int64_t ldy, int ystart, int yperm, float* out, hipStream_t s);
+                   float scale, const float* Y, int64_t ldy, int ystart, int yperm, float* out, hipStream_t s, float clamp = 0.f);
 // outer round `round` of a sweep (0: within-block pairing, ≥1: circle-method rounds; the
 // pairing is computed in-kernel and equals jacobi.py:_schedule_cpu row `round`)
 void evx_jacobi_round(float* A, float* B, int np, int round, float* Vbuf, const int* flag, float inner_tol, int max_inner,

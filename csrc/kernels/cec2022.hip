@@ -33,7 +33,7 @@ __global__ void __launch_bounds__(256) cec_basic_kernel(const float* __restrict_
                                                         const int32_t* __restrict__ perm, int start, int L,
                                                         const float* __restrict__ sub, float scale,
                                                         const float* __restrict__ Y, int64_t ldy, int ystart, int yperm,
-                                                        float* __restrict__ out) {
+                                                        float* __restrict__ out, float clamp) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (row >= N) return;
@@ -160,15 +160,15 @@ __global__ void __launch_bounds__(256) cec_basic_kernel(const float* __restrict_
     case GRIEWANK: f = a / 4000.f - p + 1.f; break;
     default: f = a; break;
   }
-  out[row] = f;
+  out[row] = (clamp > 0.f && f < clamp) ? 0.f : f;  // the CEC'22 f < 1e-8 -> 0 clamp when clamp > 0 (NaN stays NaN)
 }
 
 }  // namespace
 
 void evx_cec_basic(const float* Z, int64_t ld, int N, int fid, const int32_t* perm, int start, int L, const float* sub,
-                   float scale, const float* Y, int64_t ldy, int ystart, int yperm, float* out, hipStream_t s) {
+                   float scale, const float* Y, int64_t ldy, int ystart, int yperm, float* out, hipStream_t s, float clamp) {
   dim3 grid((N + 3) / 4);
-  cec_basic_kernel<<<grid, 256, 0, s>>>(Z, ld, N, fid, perm, start, L, sub, scale, Y, ldy, ystart, yperm, out);
+  cec_basic_kernel<<<grid, 256, 0, s>>>(Z, ld, N, fid, perm, start, L, sub, scale, Y, ldy, ystart, yperm, out, clamp);
 }
 
 namespace {

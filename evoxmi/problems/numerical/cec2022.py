@@ -213,12 +213,15 @@ class _CEC2022(Problem):
             return linalg.plain_nt(X, M, alpha=float(s), a_sub_k=o.contiguous())
         return ((X - o) * s) @ M.T
 
-    def _basic(self, Z, fid, perm=None, start=0, length=None, sub=None, scale=1.0, ysrc=None, ystart=0):
-        """fid on z_eff[:, j] = (Z[:, idx_j] − sub[idx_j])·scale, idx_j = perm[start+j] (or start+j)."""
+    def _basic(self, Z, fid, perm=None, start=0, length=None, sub=None, scale=1.0, ysrc=None, ystart=0, clamp=None):
+        """fid on z_eff[:, j] = (Z[:, idx_j] − sub[idx_j])·scale, idx_j = perm[start+j] (or start+j).
+        ``clamp``: the f < clamp → 0 rule of the CEC'22 evaluation, fused into the device kernel."""
         N, D = Z.shape
         L = D - start if length is None else length
         if Z.is_cuda:
-            return nops.cec_basic(Z, fid, perm, start, L, sub, scale, ysrc, ystart)
+            return nops.cec_basic(Z, fid, perm, start, L, sub, scale, ysrc, ystart, clamp=clamp or 0.0)
+        if clamp:
+            return self._clamp(self._basic(Z, fid, perm, start, length, sub, scale, ysrc, ystart), clamp)
         idx = torch.arange(start, start + L, device=Z.device)
         if perm is not None:
             idx = perm.long()[idx]
@@ -316,7 +319,7 @@ class F1_CEC2022(_RowSharded, _CEC2022):
         if f is not None:
             return f
         Z = self._ssr(X, c["Os"][:D], c["M"], 1.0)
-        return self._clamp(self._basic(Z, ZAKHAROV))
+        return self._basic(Z, ZAKHAROV, clamp=1e-8)
 
     def partial_terms(self, X, col0, d, own):
         z = self._zblock(X, col0, d, own)
@@ -334,7 +337,7 @@ class F2_CEC2022(_RowSharded, _CEC2022):
     def _evaluate(self, X, c):
         D = X.shape[1]
         Z = self._ssr(X, c["Os"][:D], c["M"], 2.048 / 100.0)
-        return self._clamp(self._basic(Z, ROSENBROCK))
+        return self._basic(Z, ROSENBROCK, clamp=1e-8)
 
     def partial_terms(self, X, col0, d, own):
         z = self._zblock(X, col0, d, own, halo=1) + 1  # pair terms whose left index is owned
@@ -356,7 +359,7 @@ class F3_CEC2022(_CEC2022):
     def _evaluate(self, X, c):
         D = X.shape[1]
         o = c["Os"][:D]
-        return self._clamp(self._basic(X, SCHAFFERF7, sub=o))
+        return self._basic(X, SCHAFFERF7, sub=o, clamp=1e-8)
 
     def partial_terms(self, Xb, col0, d, own):
         y = Xb.to(torch.float32) - self._consts(d, Xb.device)["Os"][col0 : col0 + Xb.shape[1]]
@@ -380,7 +383,7 @@ class F4_CEC2022(_RowSharded, _CEC2022):
         f = _rowterms(X, c["Os"][:D], c["M"], 1.0, RASTRIGIN)
         if f is not None:
             return f
-        return self._clamp(self._basic(self._ssr(X, c["Os"][:D], c["M"], 1.0), RASTRIGIN))
+        return self._basic(self._ssr(X, c["Os"][:D], c["M"], 1.0), RASTRIGIN, clamp=1e-8)
 
     def partial_terms(self, X, col0, d, own):
         z = self._zblock(X, col0, d, own) * 0.0512
@@ -395,7 +398,7 @@ class F5_CEC2022(_RowSharded, _CEC2022):
 
     def _evaluate(self, X, c):
         D = X.shape[1]
-        return self._clamp(self._basic(self._ssr(X, c["Os"][:D], c["M"], 1.0), LEVY))
+        return self._basic(self._ssr(X, c["Os"][:D], c["M"], 1.0), LEVY, clamp=1e-8)
 
     def partial_terms(self, X, col0, d, own):
         w = 1 + self._zblock(X, col0, d, own) / 4

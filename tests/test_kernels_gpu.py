@@ -1036,3 +1036,24 @@ def test_de_trial_column_block_matches_unsharded(col0, own, d, mode):
     assert torch.equal(full[:, c], part)
     cpu = de_trial(key, P[:, c].contiguous(), idx, coef, cur, md, CR, jr, L, lb[c].contiguous(), ub[c].contiguous(), col0=col0, d_total=d)
     assert torch.allclose(cpu, part.cpu(), rtol=1e-5, atol=1e-5)
+
+
+def test_cec_basic_fused_clamp_matches_where():
+    """The f < 1e-8 → 0 rule of the CEC'22 evaluation fused into cec_basic_kernel (clamp > 0); clamp = 0
+    leaves negative values alone; NaN rows stay NaN."""
+    from evoxmi.ops import numerical as nops
+    from evoxmi.problems.numerical.cec2022 import SCHWEFEL, ZAKHAROV
+
+    g = torch.Generator().manual_seed(3)
+    Z = torch.randn(8, 64, generator=g)
+    Z[0] = 0.0
+    Z[1] = 1e-9  # f ≈ (0.5·Σ(j+1)·1e-9)² ≈ 1e-12 < 1e-8
+    Z[2, 5] = float("nan")
+    Zd = Z.cuda()
+    plain = nops.cec_basic(Zd, ZAKHAROV, None, 0, 64).cpu()
+    fused = nops.cec_basic(Zd, ZAKHAROV, None, 0, 64, clamp=1e-8).cpu()
+    ref = torch.where(plain < 1e-8, torch.zeros_like(plain), plain)
+    assert torch.equal(fused[~torch.isnan(ref)], ref[~torch.isnan(ref)]) and torch.isnan(fused[2])
+    assert fused[0] == 0 and fused[1] == 0
+    s = nops.cec_basic(Zd * 50, SCHWEFEL, None, 0, 64).cpu()
+    assert torch.equal(nops.cec_basic(Zd * 50, SCHWEFEL, None, 0, 64, clamp=0.0).cpu()[~torch.isnan(s)], s[~torch.isnan(s)])
