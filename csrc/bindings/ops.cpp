@@ -250,6 +250,7 @@ at::Tensor gemm_ks(const at::Tensor& A, int64_t a_kc, const at::Tensor& B, int64
 }
 
 void gemm_ks_set_tile(int64_t t) { evx_gemm_ks_set_tile((int)t); }
+void gemm_ks_set_prec(int64_t p) { evx_gemm_ks_set_prec((int)p); }
 
 at::Tensor gemm_ks_new(const at::Tensor& A, int64_t a_kc, const at::Tensor& B, int64_t b_kc, int64_t M, int64_t N, int64_t K,
                        int64_t mode, double alpha, const c10::optional<at::Tensor>& alpha_ptr,
@@ -1271,6 +1272,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("sbr_dev_copy(Tensor src, Tensor(a!) dst, Tensor skip) -> ()");
   m.def("sbr_dev_ctrl(Tensor part, int nparts, int j, int K, Tensor(a!) hist, Tensor(b!) alpha, Tensor(c!) theta, Tensor(d!) ctrl, Tensor(e!) st, float[] prm, int ns_iters, Tensor A, Tensor(f!) w_out, Tensor(g!) eig_stats, Tensor(h!) w_init, Tensor(i!) log, Tensor(j!) log_count) -> ()");
   m.def("gemm_ks_set_tile(int t) -> ()");
+  m.def("gemm_ks_set_prec(int prec) -> ()");
   m.def("lsmop_g(Tensor X, int[] start, int[] sublen, int[] func, int nk, int cosine) -> Tensor");
   m.def("cma_delta_gemv(Tensor M, Tensor mean, Tensor dm, float cm) -> Tensor[]");
   m.def("cma_center_rows(Tensor pop, Tensor? rows, Tensor mean, Tensor sigma, Tensor w) -> Tensor");
@@ -1309,6 +1311,7 @@ TORCH_LIBRARY_IMPL(evoxmi, CompositeExplicitAutograd, m) {
   m.impl("stochastic_ranking", &stochastic_ranking);
   m.impl("gemm_set_config", &gemm_set_config);
   m.impl("gemm_ks_set_tile", &gemm_ks_set_tile);
+  m.impl("gemm_ks_set_prec", &gemm_ks_set_prec);
   m.impl("gemm_ks_grid", &gemm_ks_grid);
   m.impl("gemm_ks_tile", &gemm_ks_tile);
   m.impl("ipc_alloc", &ipc_alloc);

@@ -74,6 +74,9 @@ void evx_cec_rowterms_final(const float* parts, int tiles_n, int M, int fid, flo
 int evx_gemm_ks_grid(int M, int N, int mode);  // workgroups of a launch (stat_part length)
 int evx_gemm_ks_tile(int M, int N, int mode);
 void evx_gemm_ks_set_tile(int t);
+// 1: bf16x6 split products on the bf16 matrix pipe (default), 0: f32 MFMA
+void evx_gemm_ks_set_prec(int prec);
+int evx_gemm_ks_prec();
 void evx_cma_center_rows(const float* pop, int64_t ldp, const int32_t* rows, const float* mean, const float* sigma, const float* w, int K,
                          int d, float* Y, hipStream_t s);
 void evx_radix_argsort(const float* keys, int n, int descending, float* out_keys, int32_t* out_idx, hipStream_t s, int batch);

@@ -33,12 +33,103 @@
 #include "evoxmi_common.h"
 #include "evoxmi_launchers.h"
 #include <float.h>
+#include <type_traits>
 
 #include "../host/gemm_tiles.h"
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 namespace {
+
+// ---- bf16x6: f32-accurate products on the bf16 matrix pipe (PREC = 1) ----
+// An f32 value splits EXACTLY into three bf16 (8-bit significand) parts a = h + m + l
+// (round-to-nearest-even at each step: |m| ≤ 2⁻⁹|a|, |l| ≤ 2⁻¹⁸|a|; exact because the
+// f32 significand has 24 bits).  a·b is then the sum of nine bf16 × bf16 products, each
+// exact in the f32 accumulator; the six kept (hh, hm, mh, hl, lh, mm) leave out terms of
+// at most 2⁻²⁶|a·b|, below the f32 rounding of the accumulation itself.  The bf16 MFMA
+// (v_mfma_f32_16x16x32_bf16, ≈16 cycles for 8192 MACs) runs 16× the f32 MFMA rate
+// (v_mfma_f32_16x16x4_f32, 32 cycles for 1024 MACs), so six of them cost 3/8 of the f32
+// product; the split is ≈4.5 VALU instructions per operand element, co-issued with the
+// MFMAs of the previous block.
+#ifndef EVX_X6_SPLIT
+// 0: round-to-nearest parts (v_cvt_pk_bf16_f32, unbiased); 1: truncated parts (and / sub / perm):
+// 15 % fewer loop cycles but its dropped terms share the sign of a·b, so a same-sign sum (a
+// Gram diagonal over K = 5000) drifts past the f32 bound — measured, not used
+#define EVX_X6_SPLIT 0
+#endif
+__device__ __forceinline__ void split3(const float4& v0, const float4& v1, bf16x8& h, bf16x8& m, bf16x8& l) {
+  u32x4 H, M, L;
+#if EVX_X6_SPLIT == 0
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const float4& q = p < 2 ? v0 : v1;
+    // scalar residuals (gemm_ks.hip is built without SLP vectorisation: a packed
+    // v_pk_add_f32 beside MFMAs costs ≈3× two scalar subtractions, MI355X_MICROARCH.md)
+    const float a0 = (p & 1) ? q.z : q.x, a1 = (p & 1) ? q.w : q.y;
+    const bf16x2 hb = __builtin_convertvector(f32x2{a0, a1}, bf16x2);
+    const f32x2 hf = __builtin_convertvector(hb, f32x2);
+    const float r10 = a0 - hf.x, r11 = a1 - hf.y;
+    const bf16x2 mb = __builtin_convertvector(f32x2{r10, r11}, bf16x2);
+    const f32x2 mf = __builtin_convertvector(mb, f32x2);
+    const bf16x2 lb = __builtin_convertvector(f32x2{r10 - mf.x, r11 - mf.y}, bf16x2);
+    H[p] = __builtin_bit_cast(unsigned, hb);
+    M[p] = __builtin_bit_cast(unsigned, mb);
+    L[p] = __builtin_bit_cast(unsigned, lb);
+  }
+#else
+  // truncated parts: h = the top 8 significand bits of a (mask), m = the top 8 of the exact
+  // remainder, l = what is left — at most 8 significant bits, so l is a bf16 exactly; every
+  // part is an f32 with a zero low half, packed pairwise with one byte permute
+  const float a[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+  unsigned hu[8], mu[8], lu[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const unsigned ab = __float_as_uint(a[c]);
+    hu[c] = ab & 0xFFFF0000u;
+    const float r1 = a[c] - __uint_as_float(hu[c]);
+    mu[c] = __float_as_uint(r1) & 0xFFFF0000u;
+    lu[c] = __float_as_uint(r1 - __uint_as_float(mu[c]));
+  }
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    // high halves of (x0, x1) → one dword (x1 in the high half)
+    H[p] = __builtin_amdgcn_perm(hu[2 * p + 1], hu[2 * p], 0x07060302u);
+    M[p] = __builtin_amdgcn_perm(mu[2 * p + 1], mu[2 * p], 0x07060302u);
+    L[p] = __builtin_amdgcn_perm(lu[2 * p + 1], lu[2 * p], 0x07060302u);
+  }
+#endif
+  h = __builtin_bit_cast(bf16x8, H);
+  m = __builtin_bit_cast(bf16x8, M);
+  l = __builtin_bit_cast(bf16x8, L);
+}
+
+__device__ __forceinline__ f32x16 mfma_x6w(const bf16x8& ah, const bf16x8& am, const bf16x8& al, const bf16x8& bh,
+                                           const bf16x8& bm, const bf16x8& bl, f32x16 c) {
+  // v_mfma_f32_32x32x16_bf16: 32 cycles, holds vector issue for 8 of them (24 free cycles per
+  // MFMA for the split VALU work, against 8 of 16 for the 16x16x32 form)
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ f32x4 mfma_x6(const bf16x8& ah, const bf16x8& am, const bf16x8& al, const bf16x8& bh,
+                                         const bf16x8& bm, const bf16x8& bl, f32x4 c) {
+  // smallest terms first
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bm, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bm, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, c, 0, 0, 0);
+}
 
 
 // DPP row_ror:m (rotation by m lanes inside each 16-lane row)
@@ -124,8 +215,14 @@ __device__ __forceinline__ void decode_tile(int bid, int tiles_m, int tiles_n, i
   tm = tn = 0;
 }
 
-template <int TM, int TN, int KH, bool AKC, bool BKC, int MODE>
+// PREC 0: f32 MFMA (16x16x4, KH float4 per lane and 16-row block per k-group);
+// PREC 1: bf16x6 (KH = 2: a 32-k group is one 16x16x32 bf16 step — lane (r, q) holds
+// fragment element j ↔ k = 32·group + 16·(j >> 2) + 4q + (j & 3), the same k map for A and B,
+// so the f32 path's loads are reused unchanged).
+template <int TM, int TN, int KH, bool AKC, bool BKC, int MODE, int PREC>
 __global__ void __launch_bounds__(256) gemm_ks_kernel(EvxGemmKs p) {
+  static_assert(PREC == 0 || KH == 2, "bf16x6 groups hold two float4 per lane and block");
+  static_assert(PREC != 2 || (TM % 2 == 0 && TN % 2 == 0), "32x32 MFMA tiles need even 16-blocks");
   if (p.skip && *p.skip) return;
   if (p.sel && *p.sel) {
     if (p.A2) p.A = p.A2;
@@ -133,7 +230,13 @@ __global__ void __launch_bounds__(256) gemm_ks_kernel(EvxGemmKs p) {
     if (p.C2) p.C = p.C2;
   }
   constexpr int BM = 16 * TM, BN = 16 * TN;
-  constexpr int KG = 16 * KH;  // k per group: KH float4 per lane and 16-row block
+  // PREC 2 works on 32-row operand blocks (v_mfma_f32_32x32x16_bf16), the others on 16-row ones
+  constexpr int RB = PREC == 2 ? 32 : 16;
+  constexpr int NA = BM / RB, NB = BN / RB;
+  constexpr int NE = PREC == 2 ? 16 : 4;  // accumulator registers per block pair
+  // k per group: PREC 0: KH float4 per lane (16-row blocks, 4 lanes along k); PREC 1: 32
+  // (16x16x32 step); PREC 2: 16 (32x32x16 step, two lane halves along k)
+  constexpr int KG = PREC == 2 ? 16 : 16 * KH;
   // LDS row pitch ≡ 16 (mod 32) floats: the partial-tile writes (16 columns × 4 rows per
   // wave instruction) hit 32 distinct banks per half-wave
   constexpr int P = (BN % 32 == 16) ? BN : BN + 16;
@@ -149,78 +252,102 @@ __global__ void __launch_bounds__(256) gemm_ks_kernel(EvxGemmKs p) {
   // wave-uniform (scalar branches, and the waitcnt pass can count loads across them)
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 15, q = lane >> 4;
+  const int rw = lane & 31, hw = lane >> 5;  // PREC 2 lane map: operand row, k half
+  const int rl = PREC == 2 ? rw : r;
 
   // this wave's K range in full KG-groups (wave 0 has the fewest and also takes the tail)
   const int K = p.K;
   const int ngf = K / KG;
   const int g0 = (w * ngf) >> 2, g1 = ((w + 1) * ngf) >> 2;
 
-  const float* ap[TM];
-  const float* bp[TN];
+  const float* ap[NA];
+  const float* bp[NB];
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int row = min(m0 + 16 * i + r, p.M - 1);
+  for (int i = 0; i < NA; ++i) {
+    const int row = min(m0 + RB * i + rl, p.M - 1);
     ap[i] = AKC ? p.A + (int64_t)row * p.lda : p.A + row;
   }
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int col = min(n0 + 16 * j + r, p.N - 1);
+  for (int j = 0; j < NB; ++j) {
+    const int col = min(n0 + RB * j + rl, p.N - 1);
     bp[j] = BKC ? p.B + (int64_t)col * p.ldb : p.B + col;
   }
 
-  f32x4 acc[TM][TN];
+  using AccT = typename std::conditional<PREC == 2, f32x16, f32x4>::type;
+  AccT acc[NA][NB];
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+  for (int i = 0; i < NA; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int e = 0; e < NE; ++e) acc[i][j][e] = 0.f;
 
-  // loads per slot: one float4 (KC) or four dwords (RC) per 16-row block and 16 k; at most
+  // loads per slot: one float4 (KC) or four dwords (RC) per block and float4 slot; at most
   // 63 vector loads can be counted in flight (vmcnt)
-  constexpr int LPS = KH * (TM * (AKC ? 1 : 4) + TN * (BKC ? 1 : 4));
+  constexpr int LPS = KH * (NA * (AKC ? 1 : 4) + NB * (BKC ? 1 : 4));
 #ifdef EVX_KS_DEPTH  // tools/gemm_ks_probe.cpp experiments
   constexpr int D = EVX_KS_DEPTH;
 #else
   constexpr int D = (3 * LPS <= 63) ? 3 : 2;
 #endif
-  float4 fa[D][KH][TM], fb[D][KH][TN];
+  float4 fa[D][KH][NA], fb[D][KH][NB];
   const int64_t lda = p.lda, ldb = p.ldb;
-  // lane (r, q), float4 h, component c ↔ k = KG·group + 16h + 4q + c (same map for A and B)
+  // k of float4 h of a lane: PREC 0/1: KG·group + 16h + 4q + c (lane (r, q));
+  // PREC 2: KG·group + 8·hw + 4h + c (lane (rw, hw)) — the same map for A and B, so the
+  // MFMA k order inside a group is a consistent permutation
+  auto kof = [&](int grp, int h) { return PREC == 2 ? KG * grp + 8 * hw + 4 * h : KG * grp + 16 * h + 4 * q; };
   // fused A prologue A(m, k) − sub[k] (the CEC shift x − o): the shift float4 of a lane's k
   // values rides along with the operand loads, the subtraction runs just before the MFMAs
   const float* __restrict__ asub = p.a_sub_k;
   float4 fs[D][KH];
-  auto load_slot = [&](float4 (&xa)[KH][TM], float4 (&xb)[KH][TN], float4 (&xs)[KH], int grp) {
+  auto load_slot = [&](float4 (&xa)[KH][NA], float4 (&xb)[KH][NB], float4 (&xs)[KH], int grp) {
 #pragma unroll
     for (int h = 0; h < KH; ++h) {
-      const int k = KG * grp + 16 * h + 4 * q;
+      const int k = kof(grp, h);
       if (AKC && asub) xs[h] = *reinterpret_cast<const float4*>(asub + k);
 #pragma unroll
-      for (int i = 0; i < TM; ++i) xa[h][i] = load_full<AKC>(ap[i], lda, k);
+      for (int i = 0; i < NA; ++i) xa[h][i] = load_full<AKC>(ap[i], lda, k);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) xb[h][j] = load_full<BKC>(bp[j], ldb, k);
+      for (int j = 0; j < NB; ++j) xb[h][j] = load_full<BKC>(bp[j], ldb, k);
     }
   };
-  auto compute_slot = [&](float4 (&xa)[KH][TM], const float4 (&xb)[KH][TN], const float4 (&xs)[KH]) {
+  auto compute_slot = [&](float4 (&xa)[KH][NA], const float4 (&xb)[KH][NB], const float4 (&xs)[KH]) {
     if (AKC && asub) {
 #pragma unroll
       for (int h = 0; h < KH; ++h)
 #pragma unroll
-        for (int i = 0; i < TM; ++i) {
+        for (int i = 0; i < NA; ++i) {
           xa[h][i].x -= xs[h].x;
           xa[h][i].y -= xs[h].y;
           xa[h][i].z -= xs[h].z;
           xa[h][i].w -= xs[h].w;
         }
     }
+    if constexpr (PREC >= 1) {
+      bf16x8 bh[NB], bm[NB], bl[NB];
 #pragma unroll
-    for (int h = 0; h < KH; ++h)
+      for (int j = 0; j < NB; ++j) split3(xb[0][j], xb[1][j], bh[j], bm[j], bl[j]);
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
+      for (int i = 0; i < NA; ++i) {
+        bf16x8 ah, am, al;
+        split3(xa[0][i], xa[1][i], ah, am, al);
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+        for (int j = 0; j < NB; ++j) {
+          if constexpr (PREC == 2) acc[i][j] = mfma_x6w(ah, am, al, bh[j], bm[j], bl[j], acc[i][j]);
+          else acc[i][j] = mfma_x6(ah, am, al, bh[j], bm[j], bl[j], acc[i][j]);
+        }
+      }
+    } else {
 #pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32((&xa[h][i].x)[e], (&xb[h][j].x)[e], acc[i][j], 0, 0, 0);
+      for (int h = 0; h < KH; ++h)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int i = 0; i < NA; ++i)
+#pragma unroll
+            for (int j = 0; j < NB; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32((&xa[h][i].x)[e], (&xb[h][j].x)[e], acc[i][j], 0, 0, 0);
+    }
   };
   // Loads are issued unconditionally (group index clamped to the wave's last group, so the
   // addresses stay valid and the surplus loads are never consumed): the loop body is then
@@ -256,38 +383,42 @@ __global__ void __launch_bounds__(256) gemm_ks_kernel(EvxGemmKs p) {
   if (w == 0 && K % KG) {  // tail (masked loads)
 #pragma unroll
     for (int h = 0; h < KH; ++h) {
-      const int k = KG * ngf + 16 * h + 4 * q;
+      const int k = kof(ngf, h);
       if (AKC && asub) fs[0][h] = load_tail<true>(asub, 0, k, K);
 #pragma unroll
-      for (int i = 0; i < TM; ++i) fa[0][h][i] = load_tail<AKC>(ap[i], lda, k, K);
+      for (int i = 0; i < NA; ++i) fa[0][h][i] = load_tail<AKC>(ap[i], lda, k, K);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) fb[0][h][j] = load_tail<BKC>(bp[j], ldb, k, K);
+      for (int j = 0; j < NB; ++j) fb[0][h][j] = load_tail<BKC>(bp[j], ldb, k, K);
     }
     compute_slot(fa[0], fb[0], fs[0]);
   }
 
   // ---- epilogue: sum the four K-partials through LDS, pairwise: waves 2, 3 park theirs,
   // waves 0, 1 add them (fixed order: deterministic), park the sums; all threads add the two
-  // accumulator map (16x16): col = lane & 15, row = 4·(lane >> 4) + reg
+  // accumulator maps: 16x16: col = lane & 15, row = 4·(lane >> 4) + reg;
+  // 32x32: col = lane & 31, row = (reg & 3) + 8·(reg >> 2) + 4·(lane >> 5)
+  auto elem = [&](int i, int j, int e) {
+    return PREC == 2 ? (32 * i + (e & 3) + 8 * (e >> 2) + 4 * hw) * P + 32 * j + rw : (16 * i + 4 * q + e) * P + 16 * j + r;
+  };
   auto park = [&](int buf) {
     float* my = red + buf * BM * P;
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < NA; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
+      for (int j = 0; j < NB; ++j)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) my[(16 * i + 4 * q + e) * P + 16 * j + r] = acc[i][j][e];
+        for (int e = 0; e < NE; ++e) my[elem(i, j, e)] = acc[i][j][e];
   };
   if (w >= 2) park(w - 2);
   __syncthreads();
   if (w < 2) {
     const float* his = red + w * BM * P;
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < NA; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
+      for (int j = 0; j < NB; ++j)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) acc[i][j][e] += his[(16 * i + 4 * q + e) * P + 16 * j + r];
+        for (int e = 0; e < NE; ++e) acc[i][j][e] += his[elem(i, j, e)];
   }
   __syncthreads();
   if (w < 2) park(w);
@@ -458,14 +589,29 @@ __global__ void __launch_bounds__(256) gemm_ks_kernel(EvxGemmKs p) {
 #define EVX_KS_KH 1
 #endif
 
+int g_ks_prec = 1;  // 1: bf16x6 on 16x16x32 (default), 2: bf16x6 on 32x32x16 where the tile allows, 0: f32 MFMA
+
+template <int TM, int TN, int MODE, int PREC>
+void launch_prec(const EvxGemmKs& a, int tiles, hipStream_t s) {
+  constexpr int KH = PREC >= 1 ? 2 : EVX_KS_KH;
+  const dim3 grid(tiles), block(256);
+  if (a.a_kc && a.b_kc) gemm_ks_kernel<TM, TN, KH, true, true, MODE, PREC><<<grid, block, 0, s>>>(a);
+  else if (a.a_kc && !a.b_kc) gemm_ks_kernel<TM, TN, KH, true, false, MODE, PREC><<<grid, block, 0, s>>>(a);
+  else if (!a.a_kc && a.b_kc) gemm_ks_kernel<TM, TN, KH, false, true, MODE, PREC><<<grid, block, 0, s>>>(a);
+  else gemm_ks_kernel<TM, TN, KH, false, false, MODE, PREC><<<grid, block, 0, s>>>(a);
+}
+
 template <int TM, int TN, int MODE>
 void launch_layout(const EvxGemmKs& a, int tiles, hipStream_t s) {
-  constexpr int KH = EVX_KS_KH;
-  const dim3 grid(tiles), block(256);
-  if (a.a_kc && a.b_kc) gemm_ks_kernel<TM, TN, KH, true, true, MODE><<<grid, block, 0, s>>>(a);
-  else if (a.a_kc && !a.b_kc) gemm_ks_kernel<TM, TN, KH, true, false, MODE><<<grid, block, 0, s>>>(a);
-  else if (!a.a_kc && a.b_kc) gemm_ks_kernel<TM, TN, KH, false, true, MODE><<<grid, block, 0, s>>>(a);
-  else gemm_ks_kernel<TM, TN, KH, false, false, MODE><<<grid, block, 0, s>>>(a);
+  if constexpr (TM * TN > 32) {  // 128 × 128: the 32x32 bf16x6 form only (256 accumulator registers)
+    launch_prec<TM, TN, MODE, 2>(a, tiles, s);
+    return;
+  }
+  if constexpr (TM % 2 == 0 && TN % 2 == 0) {
+    if (g_ks_prec == 2) return launch_prec<TM, TN, MODE, 2>(a, tiles, s);
+  }
+  if (g_ks_prec >= 1) launch_prec<TM, TN, MODE, 1>(a, tiles, s);
+  else launch_prec<TM, TN, MODE, 0>(a, tiles, s);
 }
 
 template <int TM, int TN>
@@ -483,6 +629,10 @@ int g_ks_tile_override = 0;
 
 void evx_gemm_ks_set_tile(int t) { g_ks_tile_override = t; }
 
+void evx_gemm_ks_set_prec(int prec) { g_ks_prec = prec; }
+
+int evx_gemm_ks_prec() { return g_ks_prec; }
+
 int evx_gemm_ks_tile(int M, int N, int mode) { return evx_host::gemm_ks_tile(M, N, mode, g_ks_tile_override); }
 
 int evx_gemm_ks_grid(int M, int N, int mode) { return (int)evx_host::gemm_ks_grid(M, N, mode, g_ks_tile_override); }
@@ -495,6 +645,7 @@ void evx_gemm_ks(const EvxGemmKs& a, hipStream_t s) {
     case 2: launch_tile<2, 2>(a, s); break;
     case 3: launch_tile<3, 3>(a, s); break;
     case 8: launch_tile<8, 4>(a, s); break;  // tall products (M ≫ N), full mode only
+    case 9: launch_tile<8, 8>(a, s); break;  // 128 × 128 (bf16x6 on 32x32x16 only)
     default: launch_tile<4, 4>(a, s); break;
   }
 }

@@ -11,10 +11,11 @@ import torch
 
 from ....core import Algorithm, State
 from ....ops import random as rnd
+from ....parallel.dim_sharded import ColumnSeparable
 from . import common as C
 
 
-class DE(Algorithm):
+class DE(ColumnSeparable, Algorithm):
     def __init__(self, lb, ub, pop_size, base_vector="rand", num_difference_vectors=1, differential_weight=0.5,
                  cross_probability=0.9, batch_size=100, replace=False, mean=None, stdvar=None):
         super().__init__()
@@ -49,12 +50,10 @@ class DE(Algorithm):
     # -- decision-axis state sharding (P2): mutation, crossover and the greedy replacement are
     # column-separable given the replicated per-row draws (difference rows, j_rand) and the
     # replicated fitness, so a rank keeps only its column block of population and trials
-    _cols = None
-
-    def dim_shard(self, state, col0: int, own: int):
-        self._cols = (int(col0), int(own), self.dim)
-        c = slice(col0, col0 + own)
-        return state.update(population=state.population[:, c].contiguous(), trial_vectors=state.trial_vectors[:, c].contiguous())
+    # opt-in flag (parallel.dim_sharded.algorithm_column_separable): a subclass with its own
+    # ask / tell must declare itself column-separable again
+    column_separable = True
+    dim_fields = ("population", "trial_vectors")
 
     def _trials(self, state, key):
         pop = state.population
@@ -63,7 +62,7 @@ class DE(Algorithm):
         cur = torch.arange(N, device=pop.device)
         b = C.BEST if self.base_vector == "best" else C.RAND
         strat = (b, b, self.num_difference_vectors, C.BIN)
-        c0, own, d = self._cols if self._cols is not None else (0, self.dim, self.dim)
+        c0, own, d = self.cols()
         trials, _ = C.generate_trials(k_tr, pop, state.fitness, state.best_index, cur, strat, self.differential_weight,
                                       self.cross_probability, 0, self.lb[c0 : c0 + own], self.ub[c0 : c0 + own],
                                       choices=self._choices(k_ch, N, cur), cols=(c0, d))

@@ -17,6 +17,9 @@ from .de import DE
 
 
 class ODE(DE):
+    # decision-axis state sharding: the opposite point lb + ub − base is per column too
+    column_separable = True
+
     def __init__(self, lb, ub, pop_size, base_vector="rand", num_difference_vectors=1, differential_weight=0.5,
                  cross_probability=0.9, batch_size=100, replace=False, mean=None, stdvar=None):
         super().__init__(lb, ub, pop_size, base_vector, num_difference_vectors, differential_weight, cross_probability,
@@ -42,10 +45,13 @@ class ODE(DE):
         ch = self._choices(k_ch, N, cur)
         b = C.BEST if self.base_vector == "best" else C.RAND
         strat = (b, b, self.num_difference_vectors, C.BIN)
+        # column block of a decision-axis-sharded state (dim_shard), else all columns
+        c0, own, d = self.cols()
+        lb, ub = self.lb[c0 : c0 + own], self.ub[c0 : c0 + own]
         de_trials, _ = C.generate_trials(k_tr, pop, state.fitness, state.best_index, cur, strat, self.differential_weight,
-                                         self.cross_probability, 0, self.lb, self.ub, choices=ch)
+                                         self.cross_probability, 0, lb, ub, choices=ch, cols=(c0, d))
         base = pop.index_select(0, state.best_index.reshape(1)).expand(cur.shape[0], -1) if self.base_vector == "best" else pop[ch[:, 0]]
-        opposite = self.ub + self.lb - base
+        opposite = ub + lb - base
         trials = torch.where(state.counter % 2 == 0, de_trials, opposite)
         return trials, state.update(trial_vectors=trials, key=key)
 

@@ -14,9 +14,10 @@ import torch
 from ....core import Algorithm, State
 from ....ops import random as rnd
 from ....ops import pso as pso_ops
+from ....parallel.dim_sharded import ColumnSeparable
 
 
-class PSO(Algorithm):
+class PSO(ColumnSeparable, Algorithm):
     def __init__(self, lb, ub, pop_size, inertia_weight=0.6, cognitive_coefficient=2.5, social_coefficient=0.8, mean=None, stdev=None):
         super().__init__()
         self.dim = lb.shape[0]
@@ -58,14 +59,8 @@ class PSO(Algorithm):
     # field is column-separable in the tell (the only row coupling is through the replicated
     # fitness), so a rank keeps only its column block and nothing but the evaluation's per-row
     # terms crosses the ranks
-    _cols = None
-
-    def dim_shard(self, state, col0: int, own: int):
-        self._cols = (int(col0), int(own), self.dim)
-        c = slice(col0, col0 + own)
-        return state.update(population=state.population[:, c].contiguous(), velocity=state.velocity[:, c].contiguous(),
-                            local_best_location=state.local_best_location[:, c].contiguous(),
-                            global_best_location=state.global_best_location[c].contiguous())
+    column_separable = True
+    dim_fields = ("population", "velocity", "local_best_location", "global_best_location")
 
     def tell(self, state, fitness):
         key, rg_key, rp_key = rnd.split(state.key, 3)
@@ -75,7 +70,7 @@ class PSO(Algorithm):
         better = cand_f < state.global_best_fitness
         global_best_fitness = torch.where(better, cand_f, state.global_best_fitness)
         global_best_location = torch.where(better, state.population[i], state.global_best_location)
-        c0, own, d = self._cols if self._cols is not None else (0, self.dim, self.dim)
+        c0, own, d = self.cols()
         pos, vel, lbl, lbf = pso_ops.pso_update(
             state.population, state.velocity, state.local_best_location, state.local_best_fitness, fitness,
             global_best_location, rp_key, rg_key, self.w, self.phi_p, self.phi_g, self.lb[c0 : c0 + own], self.ub[c0 : c0 + own],

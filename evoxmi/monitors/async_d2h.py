@@ -61,7 +61,6 @@ class _Group:
         if self.event is None:  # not yet flushed: issue the copy now
             self.copier._flush(self)
         self.event.synchronize()
-        self.dev_buf = None
 
 
 class D2HCopier:
@@ -121,6 +120,10 @@ class D2HCopier:
             g.event.record(s)
         if self.side_stream:
             g.dev_buf.record_stream(s)
+        # release the staging chunk now: the caching allocator orders its reuse after the copy
+        # already enqueued on the compute stream (record_stream covers the side-stream case), so
+        # a history read only at the end of a run does not keep every snapshot on the device too
+        g.dev_buf = None
 
     def submit(self, x: torch.Tensor):
         if not x.is_cuda:

@@ -59,8 +59,10 @@ def _run(cmd):
 # oracle); plain "fast" contraction ignores the in-source pragma
 # neuro.hip: the Ant sub-step is scalar f32 arithmetic; SLP packing adds ~400 v_mov per
 # sub-step and pushes the register-resident rollout from 230 VGPRs (2 waves / SIMD) to 364
+# gemm_ks.hip: the bf16x6 split's residual subtractions must stay scalar (v_pk_add_f32 issued
+# beside MFMAs costs ≈13 cycles more than two v_sub_f32)
 FILE_FLAGS = {"eigh_sbr.hip": ["-fno-slp-vectorize"], "mo_geom.hip": ["-ffp-contract=fast-honor-pragmas"],
-              "neuro.hip": ["-fno-slp-vectorize"]}
+              "neuro.hip": ["-fno-slp-vectorize"], "gemm_ks.hip": ["-fno-slp-vectorize"]}
 
 
 def build(verbose: bool = True, jobs: int = None) -> str:

@@ -130,6 +130,22 @@ def plain_nt(A: torch.Tensor, B: torch.Tensor, alpha: float = 1.0, bias_n: Optio
     return mm(A, B, tb=True, alpha=alpha, bias_n=bias_n, a_sub_k=a_sub_k)
 
 
+_PREC = {"x6": 1, "x6w": 2, "f32": 0}
+_prec_set = [None]
+
+
+def _sync_prec():
+    """Push the ``gemm_prec`` knob to the kernel launcher (read at launch / capture time)."""
+    from .. import config
+
+    p = config.get("gemm_prec")
+    if p != _prec_set[0]:
+        if p not in _PREC:
+            raise ValueError(f"EVOXMI_GEMM_PREC must be one of {sorted(_PREC)}, got {p!r}")
+        _ext.ops().gemm_ks_set_prec(_PREC[p])
+        _prec_set[0] = p
+
+
 def mm(A: torch.Tensor, B: torch.Tensor, *, ta: bool = False, tb: bool = False, mode: int = 0, alpha: float = 1.0,
        alpha_ptr: Optional[torch.Tensor] = None, bias_n: Optional[torch.Tensor] = None, beta: float = 0.0,
        Cin: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
@@ -160,6 +176,7 @@ def mm(A: torch.Tensor, B: torch.Tensor, *, ta: bool = False, tb: bool = False, 
         B_ = B if B.stride(-1) == 1 else B.contiguous()
         sub_ok = a_sub_k is None or (a_kc and a_sub_k.is_contiguous() and a_sub_k.data_ptr() % 16 == 0)
         if ok and sub_ok and A_.data_ptr() % 16 == 0 and B_.data_ptr() % 16 == 0:
+            _sync_prec()
             args = (A_, int(a_kc), B_, int(b_kc), int(M), int(N), int(K), int(mode), float(alpha), alpha_ptr, bias_n,
                     float(beta), Cin)
             if out is not None:

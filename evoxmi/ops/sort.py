@@ -20,8 +20,17 @@ MAX_RANK_SORT = 8192     # one-launch rank-by-counting up to here (profiles/r3_s
 MAX_DEVICE_SORT = 32768  # two-pass merge up to here; the library radix sort beyond
 
 
+def _batched(x) -> bool:
+    """Inside ``torch.vmap`` (BatchedRuns): the custom ops carry no batching rule there."""
+    try:
+        return bool(torch._C._functorch.is_batchedtensor(x))
+    except AttributeError:  # pragma: no cover - older torch
+        return False
+
+
 def _device(keys):
-    return keys.is_cuda and keys.dtype == torch.float32 and keys.dim() <= 2 and keys.shape[-1] <= MAX_DEVICE_SORT
+    return (keys.is_cuda and keys.dtype == torch.float32 and 1 <= keys.dim() <= 2 and keys.shape[-1] <= MAX_DEVICE_SORT
+            and not _batched(keys))
 
 
 def _sort(keys, descending):

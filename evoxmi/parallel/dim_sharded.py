@@ -69,10 +69,69 @@ def dim_sharded_fitness_local(problem, Xloc: torch.Tensor, col0: int, d: int, gr
     return problem.combine_terms(T, d)
 
 
+def algorithm_column_separable(algorithm) -> bool:
+    """The class that implements the algorithm's ``ask`` / ``tell`` (the first in the MRO to
+    define either) declares ``column_separable = True`` itself or is a subclass of one that
+    does and adds no ``ask`` / ``tell`` of its own — a subclass that inherits ``dim_shard`` but
+    overrides ``ask`` / ``tell`` (e.g. ODE over DE) is not assumed to handle column blocks."""
+    if not hasattr(algorithm, "dim_shard"):
+        return False
+    mro = type(algorithm).__mro__
+    impl = next((i for i, c in enumerate(mro) if "ask" in vars(c) or "tell" in vars(c)), None)
+    flag = next((i for i, c in enumerate(mro) if "column_separable" in vars(c)), None)
+    return impl is not None and flag is not None and flag <= impl and bool(vars(mro[flag])["column_separable"])
+
+
+class ColumnSeparable:
+    """Decision-axis (column) state sharding for algorithms whose ``ask`` / ``tell`` act on each
+    column independently given replicated per-row quantities (fitness, row draws) — the
+    reference's GSPMD ``_auto_shard`` (``std_workflow.py:253-270``) shards every (pop, dim) and
+    (dim,) array of such a state along dim.  A subclass lists those fields in ``dim_fields``
+    and sets ``column_separable = True`` in the class that defines its ``ask`` / ``tell``;
+    per-column constants (bounds) are read through :meth:`cols` / :meth:`col_vec`, and its
+    random draws must be indexed by global column (Philox counters) so that every split
+    reproduces the single-process run."""
+
+    dim_fields: tuple = ()
+    _cols = None
+
+    def dim_shard(self, state, col0: int, own: int):
+        self._cols = (int(col0), int(own), int(self.dim))
+        return state.update(**{f: state[f][..., col0 : col0 + own].contiguous() for f in self.dim_fields})
+
+    def cols(self):
+        """(first column, columns owned, total columns) of this rank's block."""
+        return self._cols if self._cols is not None else (0, int(self.dim), int(self.dim))
+
+    def col_vec(self, v):
+        """This rank's block of a per-column vector (bounds, means)."""
+        c0, own, _ = self.cols()
+        return v[..., c0 : c0 + own]
+
+    def dim_gather(self, state, group=None):
+        """The state with every ``dim_fields`` array reassembled to full width on every rank
+        (one all-gather per field; for checkpoints, monitors and final results)."""
+        if self._cols is None or not (dist.is_available() and dist.is_initialized()):
+            return state
+        world = dist.get_world_size(group)
+        d = self._cols[2]
+        sl = balanced_slices(d, world)
+        w = max(o for _, o in sl)
+        upd = {}
+        for f in self.dim_fields:
+            x = state[f]
+            pad = torch.zeros(*x.shape[:-1], w, dtype=x.dtype, device=x.device)
+            pad[..., : x.shape[-1]] = x
+            parts = [torch.empty_like(pad) for _ in range(world)]
+            dist.all_gather(parts, pad, group=group)
+            upd[f] = torch.cat([p[..., :o] for p, (_, o) in zip(parts, sl)], -1)
+        return state.update(**upd)
+
+
 def supports_state_sharding(algorithm, problem) -> bool:
     """Full P2 (state and evaluation column-sharded): the algorithm can slice its state into
     column blocks and the problem's terms need no halo and no full rows."""
-    return (hasattr(algorithm, "dim_shard") and supports_dim_sharding(problem) and getattr(problem, "dim_halo", 1) == 0
+    return (algorithm_column_separable(algorithm) and supports_dim_sharding(problem) and getattr(problem, "dim_halo", 1) == 0
             and not getattr(problem, "dim_shard_full_rows", False))
 
 

@@ -406,7 +406,7 @@ class StdWorkflow(Workflow):
                 state = state.update_child("algorithm", alg.update(**{f: alg[f][start : start + size].clone() for f in local}))
         return state
 
-    def enable_multi_devices(self, state: State, devices=None, shard_state=None) -> State:
+    def enable_multi_devices(self, state: State, devices=None, shard_state: bool = False) -> State:
         """Shard the evaluation along the decision axis (reference
         ``std_workflow.py:272-309``, GSPMD over ``PositionalSharding(devices)``).
 
@@ -414,14 +414,17 @@ class StdWorkflow(Workflow):
         (:func:`evoxmi.parallel.supports_dim_sharding`), each rank evaluates its
         column block and the per-row partial terms are all-reduced
         (:class:`evoxmi.parallel.DimShardedProblem`); the algorithm stays replicated
-        (same key on every rank).  Other problems fall back to population sharding.
-        The state structure is unchanged, so this may be called after ``init``.
+        (same key on every rank).  A problem without the protocol falls back to population
+        sharding (:meth:`enable_distributed`) with a warning.  The state structure is
+        unchanged, so this may be called after ``init``.
 
-        ``shard_state`` (default: whenever possible) shards the algorithm state too, as GSPMD
-        does for every (pop, dim) array: algorithms with ``dim_shard`` (PSO) keep only their
-        column block of the population / velocity / bests on each rank, and problems without
-        a halo evaluate that block — the only traffic is the (N, k) term all-reduce.  Solutions
-        seen by monitors are then the rank's column block."""
+        ``shard_state=True`` shards the algorithm state too, as GSPMD does for every (pop, dim)
+        array: column-separable algorithms (:class:`evoxmi.parallel.ColumnSeparable` — PSO, DE,
+        ODE, …) keep only their column block of every ``dim_fields`` array on each rank, and
+        problems without a halo evaluate that block — the only traffic is the (N, k) term
+        all-reduce.  The state then holds column blocks: :meth:`gather_state` reassembles the
+        full arrays (the reference's sharded arrays stay logically global).  Default ``False``:
+        a state read after the run has the reference's full shapes."""
         if not self.jit_problem:
             raise ValueError("multi-devices with non jit problem isn't currently supported")
         if not (torch.distributed.is_available() and torch.distributed.is_initialized()):
@@ -436,11 +439,10 @@ class StdWorkflow(Workflow):
 
             ctx = DistContext(group=devices if isinstance(devices, torch.distributed.ProcessGroup) else None)
             state = ctx.broadcast_state(state)
-            if shard_state is None:
-                shard_state = supports_state_sharding(self.algorithm, self.problem)
             if shard_state:
                 if not supports_state_sharding(self.algorithm, self.problem):
-                    raise ValueError("state sharding needs an algorithm with dim_shard and a problem without halo / full rows")
+                    raise ValueError("state sharding needs a column-separable algorithm (parallel.ColumnSeparable) and a "
+                                     "problem without halo / full rows")
                 d = int(self.algorithm.dim)
                 rank, world = torch.distributed.get_rank(ctx.group), torch.distributed.get_world_size(ctx.group)
                 col0, own = balanced_slices(d, world)[rank]
@@ -450,4 +452,15 @@ class StdWorkflow(Workflow):
             else:
                 self._dim_shard_group = (ctx.group,)
             return state
+        warnings.warn(f"enable_multi_devices: {type(self.problem).__name__} has no dim-sharding terms "
+                      "(partial_terms / combine_terms / dim_halo); sharding the population instead")
         return self.enable_distributed(state)
+
+    def gather_state(self, state: State) -> State:
+        """The state with a decision-axis-sharded algorithm state reassembled to full-width
+        arrays on every rank (identity otherwise)."""
+        grp = getattr(self, "_dim_shard_group", None)
+        if grp is None or len(grp) < 3:
+            return state
+        alg = state.get_child_state("algorithm")
+        return state.update_child("algorithm", self.algorithm.dim_gather(alg, grp[0]))

@@ -80,47 +80,69 @@ def test_enable_multi_devices_gloo_matches_single_process():
     assert torch.allclose(p0, ref.population, rtol=1e-3, atol=1e-3)
 
 
-def _de_worker(rank, world, port, out):
+def _de_worker(rank, world, port, out, cls="DE", prob="Rastrigin"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     torch.set_num_threads(1)
     from evoxmi.parallel import destroy, init_distributed
 
     init_distributed(backend="gloo")
-    wf = _make_de()
+    wf = _make_de(cls, prob)
     st = wf.init(rnd.PRNGKey(4))
-    st = wf.enable_multi_devices(st)
+    st = wf.enable_multi_devices(st, shard_state=True)
     for _ in range(15):
         st = wf.step(st)
     a = st.get_child_state("algorithm")
-    out[rank] = (a.fitness.clone(), a.population.clone())
+    full = wf.gather_state(st).get_child_state("algorithm")
+    out[rank] = (a.fitness.clone(), a.population.clone(), full.population.clone())
     destroy()
 
 
-def _make_de():
-    from evoxmi.algorithms import DE
+def _make_de(cls="DE", prob="Rastrigin"):
+    import evoxmi.algorithms as A
+    import evoxmi.problems.numerical as P
 
     lb, ub = torch.full((30,), -5.0), torch.full((30,), 5.0)
-    return StdWorkflow(DE(lb, ub, 40), Rastrigin())
+    return StdWorkflow(getattr(A, cls)(lb, ub, 40), getattr(P, prob)())
 
 
 @pytest.mark.parametrize("world", [2, 3])
-def test_state_sharded_de_gloo_matches_single_process(world):
-    """Full P2 for DE: mutation, binomial crossover (global j_rand and Philox words) and the
-    greedy replacement run on each rank's column block; the blocks reassemble the
-    single-process population."""
-    wf = _make_de()
+@pytest.mark.parametrize("cls", ["DE", "ODE"])
+def test_state_sharded_de_gloo_matches_single_process(world, cls):
+    """Full P2 for DE and ODE: mutation, binomial crossover (global j_rand and Philox words),
+    the opposite points lb + ub − x and the greedy replacement run on each rank's column
+    block; the blocks reassemble the single-process population, and ``gather_state`` returns
+    it whole on every rank."""
+    wf = _make_de(cls)
     st = wf.init(rnd.PRNGKey(4))
     for _ in range(15):
         st = wf.step(st)
     ref = st.get_child_state("algorithm")
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_de_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    mp.spawn(_de_worker, args=(world, _free_port(), out, cls), nprocs=world, join=True)
     blocks = [out[r] for r in range(world)]
     assert all(torch.equal(b[0], blocks[0][0]) for b in blocks)
     assert [b[1].shape[1] for b in blocks] == [own for _, own in balanced_slices(30, world)]
     assert torch.allclose(blocks[0][0], ref.fitness, rtol=1e-4, atol=1e-3)
-    assert torch.allclose(torch.cat([b[1] for b in blocks], 1), ref.population, rtol=1e-4, atol=1e-4)
+    cat = torch.cat([b[1] for b in blocks], 1)
+    assert torch.allclose(cat, ref.population, rtol=1e-4, atol=1e-4)
+    assert all(torch.equal(b[2], cat) for b in blocks)
+
+
+def test_column_separable_needs_the_implementing_class_to_opt_in():
+    """A subclass that inherits dim_shard but brings its own ask / tell is not state-sharded."""
+    from evoxmi.algorithms import DE, ODE, PSO
+    from evoxmi.parallel.dim_sharded import algorithm_column_separable
+
+    lb, ub = torch.zeros(4), torch.ones(4)
+
+    class MyDE(DE):
+        def ask(self, state):
+            return super().ask(state)
+
+    assert algorithm_column_separable(DE(lb, ub, 8)) and algorithm_column_separable(ODE(lb, ub, 8))
+    assert algorithm_column_separable(PSO(lb, ub, 8))
+    assert not algorithm_column_separable(MyDE(lb, ub, 8))
 
 
 @pytest.mark.parametrize("world", [2, 3])

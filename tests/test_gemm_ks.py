@@ -4,7 +4,10 @@ skew-symmetric), K tails, ragged M/N edges and the fused epilogue."""
 import pytest
 import torch
 
+from evoxmi import config
 from evoxmi.ops import linalg
+
+PRECS = ["x6", "x6w", "f32"]  # bf16x6 split products on 16x16x32 / 32x32x16 MFMA, and the f32 MFMA path
 
 
 def _ref(A, B, ta, tb, alpha=1.0, bias=None, beta=0.0, Cin=None):
@@ -39,20 +42,28 @@ def _tol(A, B, ta, tb, K):
 @pytest.mark.parametrize("M,N,K", [(1000, 1000, 1000), (257, 130, 72), (64, 48, 20), (1000, 1000, 5000), (333, 1000, 1000),
                                    (10000, 1000, 1000)])
 @pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])
-def test_gemm_ks_full_matches_fp64(M, N, K, ta, tb):
+@pytest.mark.parametrize("prec", PRECS)
+def test_gemm_ks_full_matches_fp64(M, N, K, ta, tb, prec):
     if M * N * K > 2e9 and (ta, tb) != (False, True):
         pytest.skip("large shape: the NT layout only")
     g = torch.Generator().manual_seed(M + 3 * N + 7 * K + 2 * ta + tb)
     A = torch.randn((K, M) if ta else (M, K), generator=g)
     B = torch.randn((N, K) if tb else (K, N), generator=g)
-    C = linalg.mm(A.cuda(), B.cuda(), ta=ta, tb=tb).cpu().double()
+    with config.override(gemm_prec=prec):
+        C = linalg.mm(A.cuda(), B.cuda(), ta=ta, tb=tb).cpu().double()
     R = _ref(A, B, ta, tb)
     assert ((C - R).abs() <= _tol(A, B, ta, tb, K)).all(), float((C - R).abs().max())
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,K", [(1000, 1000), (1000, 5000), (200, 36), (48, 16), (97, 1000)])
-def test_gemm_ks_symmetric_and_skew_outputs(n, K):
+@pytest.mark.parametrize("prec", PRECS)
+def test_gemm_ks_symmetric_and_skew_outputs(n, K, prec):
+    with config.override(gemm_prec=prec):
+        _sym_skew(n, K)
+
+
+def _sym_skew(n, K):
     g = torch.Generator().manual_seed(n + K)
     Y = torch.randn(K, n, generator=g)
     # symmetric: Yᵀ Y (both operands RC) and Z Zᵀ (both KC)
@@ -98,6 +109,20 @@ def test_gemm_ks_epilogue_alpha_ptr_bias_cin_out_and_skip():
     skip.zero_()
     linalg.mm(A.cuda(), B.cuda(), tb=True, out=sentinel, skip=skip)
     assert ((sentinel.cpu().double() - _ref(A, B, False, True)).abs() <= _tol(A, B, False, True, K)).all()
+
+
+@pytest.mark.gpu
+def test_gemm_x6_scaled_and_mixed_magnitude_operands():
+    """bf16x6 keeps f32 accuracy over operand magnitudes spanning many binades (each part is
+    split relative to its own value, so no shared exponent is assumed): rows scaled by
+    10^-20 … 10^20 and columns of mixed sign and size."""
+    g = torch.Generator().manual_seed(3)
+    A = torch.randn(300, 256, generator=g) * torch.logspace(-20, 20, 300)[:, None]
+    B = torch.randn(200, 256, generator=g) * torch.logspace(-3, 3, 256)[None, :]
+    with config.override(gemm_prec="x6"):
+        C = linalg.mm(A.cuda(), B.cuda(), tb=True).cpu().double()
+    R = _ref(A, B, False, True)
+    assert ((C - R).abs() <= _tol(A, B, False, True, 256)).all()
 
 
 @pytest.mark.gpu

@@ -881,6 +881,21 @@ def test_open_es_gpu_matches_stored_noise_update():
     assert torch.allclose(st2.center, st.center - 0.1 * grad, rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("n", [100, 10000, 20000])
+def test_sort_ops_under_vmap_and_on_scalars(n):
+    """ops.sort under torch.vmap (BatchedRuns: the custom ops have no batching rule, so the
+    batched call must take the torch.sort path) and on 0-d keys."""
+    from evoxmi.ops import sort
+
+    x = torch.randn(3, n, device="cuda")
+    vi = torch.vmap(lambda r: sort.topk(r, 12, largest=False)[1])(x)
+    assert torch.equal(vi, torch.sort(x, dim=1, stable=True)[1][:, :12])
+    va = torch.vmap(lambda r: sort.argsort(r)[1])(x)
+    assert torch.equal(va, torch.sort(x, dim=1, stable=True)[1])
+    v, i = sort.argsort(torch.tensor(2.5, device="cuda"))
+    assert float(v) == 2.5 and int(i) == 0
+
+
 @pytest.mark.parametrize("n", [1, 3, 100, 2048, 5000, 10000, 12000, 16383, 16384, 30001, 65536])
 @pytest.mark.parametrize("descending", [0, 1])
 @pytest.mark.parametrize("kernel", ["radix_argsort_f32", "rank_argsort_f32", "merge_argsort_f32"])
@@ -943,6 +958,18 @@ def test_eval_monitor_async_host_history_matches_device_history():
     assert len(hh) == len(hd) >= 6
     for a, b in zip(hh, hd):
         assert not a.is_cuda and torch.equal(a, b.cpu())
+
+
+def test_d2h_copier_releases_device_staging_at_flush():
+    """A flushed snapshot group keeps no device staging chunk alive until the host entry is
+    read (a history read only at the end of a run must not also sit on the device)."""
+    from evoxmi.monitors.async_d2h import D2HCopier
+
+    cp = D2HCopier(flush_every=4)
+    xs = [torch.full((1000,), float(i), device="cuda") for i in range(8)]
+    pend = [cp.submit(x) for x in xs]
+    assert all(p.group is None or p.group.dev_buf is None for p in pend)  # both groups flushed
+    assert [float(p.get()[0]) for p in pend] == [float(i) for i in range(8)]
 
 
 @pytest.mark.parametrize("K,D", [(5000, 1000), (7, 33), (130, 257)])

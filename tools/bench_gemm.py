@@ -1,5 +1,7 @@
-"""Microbenchmark of the flagship's f32 GEMM shapes: gemm_ks (hand-written MFMA) vs
-torch.mm (hipBLASLt).  Device time per call from HIP events over back-to-back calls.
+"""Microbenchmark of the flagship's f32 GEMM shapes: gemm_ks (hand-written MFMA) in both
+precision modes ('x6': exact three-way bf16 split, six bf16 MFMA products; 'f32': f32 MFMA)
+vs torch.mm (hipBLASLt).  Device time per call from HIP events over back-to-back calls;
+``err_x6`` / ``err_f32`` = max |C − C_fp64| / Σ_k |a·b| of one call (the test bound is 2e-6).
 
     python tools/bench_gemm.py [--reps 100] [--tile 0]
 """
@@ -59,13 +61,28 @@ def main():
         ("10000x1000x1000 Z·Bt + bias (NT)", 2 * 10000 * n * n, lambda: linalg.mm(Z, B, tb=True, bias_n=bias, out=out_t),
          lambda: torch.addmm(bias, Z, B.t(), out=out_t)),
     ]
+    from evoxmi import config
+
+    # accuracy of both modes on the NT product (fp64 reference on the device)
+    Ad, Bd = A.double(), B.double()
+    R = Ad @ Bd.t()
+    Bound = Ad.abs() @ Bd.abs().t()
+    errs = {}
+    for prec in ("x6", "f32"):
+        with config.override(gemm_prec=prec):
+            C = linalg.mm(A, B, tb=True)
+        errs[prec] = float(((C.double() - R).abs() / Bound).max())
+    print(json.dumps({"err_x6": errs["x6"], "err_f32": errs["f32"]}), flush=True)
     rows = []
     for name, flops, f_ks, f_t in cases:
-        t_ks = timeit(f_ks, a.reps)
+        t = {}
+        for prec in ("x6", "f32"):
+            with config.override(gemm_prec=prec):
+                t[prec] = timeit(f_ks, a.reps)
         t_t = timeit(f_t, a.reps)
-        rows.append({"case": name, "gemm_ks_us": round(t_ks, 2), "torch_us": round(t_t, 2),
-                     "gemm_ks_tflops": round(flops / t_ks / 1e6, 1), "torch_tflops": round(flops / t_t / 1e6, 1),
-                     "speedup": round(t_t / t_ks, 3)})
+        rows.append({"case": name, "x6_us": round(t["x6"], 2), "f32_us": round(t["f32"], 2), "torch_us": round(t_t, 2),
+                     "x6_tflops": round(flops / t["x6"] / 1e6, 1), "f32_tflops": round(flops / t["f32"] / 1e6, 1),
+                     "torch_tflops": round(flops / t_t / 1e6, 1), "x6_vs_torch": round(t_t / t["x6"], 3)})
         print(json.dumps(rows[-1]), flush=True)
 
 

@@ -1,5 +1,6 @@
 // Standalone timing probe for gemm_ks.hip variants (compile-time macros EVX_KS_DEPTH,
-// EVX_KS_FAKE_LOADS): hipcc --offload-arch=gfx950 -O3 -I csrc/include [-D...] tools/gemm_ks_probe.cpp
+// EVX_KS_FAKE_LOADS, EVX_KS_NO_LOADS): hipcc --offload-arch=gfx950 -O3 -I csrc/include [-D...] tools/gemm_ks_probe.cpp
+// Every case runs in both precision modes (bf16x6 split products, f32 MFMA).
 #include "../csrc/kernels/gemm_ks.hip"
 #include <cstdio>
 #include <vector>
@@ -52,14 +53,20 @@ int main() {
     {"10000x1000x1000 NT t4", 10000, 1000, 1000, 1, 1, 0, 4},
     {"10000x1000x1000 NT t3", 10000, 1000, 1000, 1, 1, 0, 3},
     {"10000x1000x1000 NT t8", 10000, 1000, 1000, 1, 1, 0, 8},
+    {"10000x1000x1000 NT t9", 10000, 1000, 1000, 1, 1, 0, 9},
     {"1000x1000x5000 TN sym t3", 1000, 1000, 5000, 0, 0, 1, 3},
     {"1000x1000x5000 NT sym t3", 1000, 1000, 5000, 1, 1, 1, 3},
     {"2048^3 NT full t4", 2048, 2048, 2048, 1, 1, 0, 4},
+    {"2048^3 NT full t9", 2048, 2048, 2048, 1, 1, 0, 9},
   };
   for (auto& c : cs) {
-    const double us = run(c.M, c.N, c.K, c.akc, c.bkc, c.mode, c.tile, 50);
-    double flops = 2.0 * c.M * c.N * c.K;
-    printf("%-26s %9.2f us  %7.1f TF/s (full-product equivalent)\n", c.name, us, flops / us / 1e6);
+    for (int prec : {2, 1, 0}) {
+      if (c.tile == 9 && prec != 2) continue;
+      evx_gemm_ks_set_prec(prec);
+      const double us = run(c.M, c.N, c.K, c.akc, c.bkc, c.mode, c.tile, 50);
+      double flops = 2.0 * c.M * c.N * c.K;
+      printf("%-26s %-3s %9.2f us  %7.1f TF/s (full-product equivalent)\n", c.name, prec == 2 ? "x6w" : prec ? "x6" : "f32", us, flops / us / 1e6);
+    }
   }
   return 0;
 }
