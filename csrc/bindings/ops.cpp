@@ -330,6 +330,20 @@ void sbr16_far_out(const at::Tensor& A, const at::Tensor& perm, const at::Tensor
                 theta.data_ptr<float>(), skip.data_ptr<int>());
 }
 
+void sbr16_far_bq_out(const at::Tensor& A, const at::Tensor& perm, const at::Tensor& Q, const at::Tensor& dq, const at::Tensor& stats,
+                      double thr_fac, const at::Tensor& theta, at::Tensor& X, const at::Tensor& B, at::Tensor& Bq, int64_t sb,
+                      const at::Tensor& skip_far, const at::Tensor& skip_bq) {
+  const int64_t n = A.size(0);
+  TORCH_CHECK(X.sizes() == A.sizes() && X.stride(1) == 1 && A.stride(1) == 1 && stats.scalar_type() == at::kDouble &&
+                  theta.scalar_type() == at::kFloat, "sbr16_far_bq_out: generator shapes");
+  TORCH_CHECK(Bq.sizes() == B.sizes() && B.size(1) == n && Bq.stride(1) == 1 && B.stride(1) == 1, "sbr16_far_bq_out: Bq shapes");
+  TORCH_CHECK(perm.numel() >= n && dq.numel() >= n && Q.numel() >= evx_sbr16_nblocks((int)n, (int)sb) * sb * sb, "sbr16_far_bq_out: perm / Q");
+  TORCH_CHECK(skip_far.scalar_type() == at::kInt && skip_bq.scalar_type() == at::kInt, "sbr16_far_bq_out: skip words int32");
+  evx_sbr16_far_bq(A.data_ptr<float>(), (int)n, A.stride(0), perm.data_ptr<int>(), Q.data_ptr<float>(), dq.data_ptr<float>(),
+                   stats.data_ptr<double>(), (float)thr_fac, theta.data_ptr<float>(), X.data_ptr<float>(), X.stride(0), B.data_ptr<float>(),
+                   (int)B.size(0), B.stride(0), Bq.data_ptr<float>(), Bq.stride(0), (int)sb, cur_stream(), skip_far.data_ptr<int>(),
+                   skip_bq.data_ptr<int>());
+}
 void sbr16_bq_out(const at::Tensor& B, const at::Tensor& perm, const at::Tensor& Q, at::Tensor& Bq, int64_t sb, const at::Tensor& skip) {
   const int64_t n = B.size(1);
   TORCH_CHECK(Bq.sizes() == B.sizes() && Bq.stride(1) == 1 && B.stride(1) == 1, "sbr16_bq_out: shapes");
@@ -375,14 +389,14 @@ void sbr_dev_ctrl(const at::Tensor& part, int64_t nparts, int64_t j, int64_t K, 
                   at::Tensor& ctrl, at::Tensor& st, std::vector<double> prm, int64_t ns_iters, const at::Tensor& A, at::Tensor& w_out,
                   at::Tensor& eig_stats, at::Tensor& w_init, at::Tensor& log, at::Tensor& log_count) {
   TORCH_CHECK(log.scalar_type() == at::kDouble && log.is_contiguous() && log_count.scalar_type() == at::kInt, "sbr_dev_ctrl: log");
-  TORCH_CHECK(prm.size() == 5, "sbr_dev_ctrl: params [tol, ns_kappa, damp_kappa, t4_kappa, near_only]");
+  TORCH_CHECK(prm.size() == 8, "sbr_dev_ctrl: params [tol, ns_kappa, damp_kappa, t4_kappa, near_only, theta0, theta_kappa, lean_from]");
   TORCH_CHECK(hist.scalar_type() == at::kDouble && hist.numel() >= 4 * (K + 1) && ctrl.numel() >= 8 * K && alpha.numel() >= K + 1 &&
                   theta.numel() >= K && st.numel() >= 8 && part.numel() >= 4 * nparts, "sbr_dev_ctrl: buffers");
-  float p6[6] = {(float)prm[0], (float)prm[1], (float)prm[2], (float)prm[3], (float)prm[4], 0.f};
+  float p6[7] = {(float)prm[0], (float)prm[1], (float)prm[2], (float)prm[3], (float)prm[4], (float)prm[5], (float)prm[6]};
   evx_sbr_dev_ctrl(part.data_ptr<double>(), (int)nparts, (int)j, (int)K, hist.data_ptr<double>(), alpha.data_ptr<float>(),
                    theta.data_ptr<float>(), ctrl.data_ptr<int>(), st.data_ptr<int>(), p6, (int)ns_iters, A.data_ptr<float>(), A.stride(0),
                    (int)A.size(0), w_out.data_ptr<float>(), eig_stats.data_ptr<double>(), w_init.data_ptr<float>(),
-                   log.data_ptr<double>(), (int)(log.numel() / 4), log_count.data_ptr<int>(), cur_stream());
+                   log.data_ptr<double>(), (int)(log.numel() / 4), log_count.data_ptr<int>(), cur_stream(), (int)prm[7]);
 }
 
 std::vector<at::Tensor> argsort_f32(const at::Tensor& keys, int64_t descending) {
@@ -1273,6 +1287,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("sbr_dev_ctrl(Tensor part, int nparts, int j, int K, Tensor(a!) hist, Tensor(b!) alpha, Tensor(c!) theta, Tensor(d!) ctrl, Tensor(e!) st, float[] prm, int ns_iters, Tensor A, Tensor(f!) w_out, Tensor(g!) eig_stats, Tensor(h!) w_init, Tensor(i!) log, Tensor(j!) log_count) -> ()");
   m.def("gemm_ks_set_tile(int t) -> ()");
   m.def("gemm_ks_set_prec(int prec) -> ()");
+  m.def("sbr16_far_bq_out(Tensor A, Tensor perm, Tensor Q, Tensor dq, Tensor stats, float thr_fac, Tensor theta, Tensor(a!) X, Tensor B, Tensor(b!) Bq, int sb, Tensor skip_far, Tensor skip_bq) -> ()");
   m.def("lsmop_g(Tensor X, int[] start, int[] sublen, int[] func, int nk, int cosine) -> Tensor");
   m.def("cma_delta_gemv(Tensor M, Tensor mean, Tensor dm, float cm) -> Tensor[]");
   m.def("cma_center_rows(Tensor pop, Tensor? rows, Tensor mean, Tensor sigma, Tensor w) -> Tensor");
@@ -1312,6 +1327,7 @@ TORCH_LIBRARY_IMPL(evoxmi, CompositeExplicitAutograd, m) {
   m.impl("gemm_set_config", &gemm_set_config);
   m.impl("gemm_ks_set_tile", &gemm_ks_set_tile);
   m.impl("gemm_ks_set_prec", &gemm_ks_set_prec);
+  m.impl("sbr16_far_bq_out", &sbr16_far_bq_out);
   m.impl("gemm_ks_grid", &gemm_ks_grid);
   m.impl("gemm_ks_tile", &gemm_ks_tile);
   m.impl("ipc_alloc", &ipc_alloc);

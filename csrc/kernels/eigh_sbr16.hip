@@ -197,20 +197,27 @@ __device__ __forceinline__ void load_qtile(const float* __restrict__ Q, int nb, 
 }
 
 // ------------------------------------------------------------------ 3. far-pair generator
+struct FarSmem {
+  float G[TL * TP];
+  float Qk[TL * TP];
+  float Ql[TL * TP];
+  int pk[TL], pl[TL];
+  float dk[TL], dl[TL], tk[TL], tl[TL];
+};
+
 template <int SB>
-__global__ void __launch_bounds__(256) sbr16_far_kernel(const float* __restrict__ A, int n, int64_t lda,
-                                                        const int* __restrict__ perm, const float* __restrict__ Q,
-                                                        const float* __restrict__ dq, const double* __restrict__ stats,
-                                                        float thr_fac, float theta, float* __restrict__ X, int64_t ldx,
-                                                        const float* __restrict__ theta_ptr, const int* __restrict__ skip) {
-  if (skip && *skip) return;
-  if (theta_ptr) theta = *theta_ptr;  // device-side local-threshold switch (ops/sbr_device.py)
-  __shared__ __attribute__((aligned(16))) float G[TL * TP];
-  __shared__ __attribute__((aligned(16))) float Qk[TL * TP];
-  __shared__ __attribute__((aligned(16))) float Ql[TL * TP];
-  __shared__ int pk[TL], pl[TL];
-  __shared__ float dk[TL], dl[TL], tk[TL], tl[TL];
-  const int K = blockIdx.y, L = blockIdx.x;
+__device__ __forceinline__ void far_tile(const float* __restrict__ A, int n, int64_t lda, const int* __restrict__ perm,
+                                         const float* __restrict__ Q, const float* __restrict__ dq, const double* __restrict__ stats,
+                                         float thr_fac, float theta, float* __restrict__ X, int64_t ldx, int K, int L, FarSmem& sm) {
+  float* G = sm.G;
+  float* Qk = sm.Qk;
+  float* Ql = sm.Ql;
+  int* pk = sm.pk;
+  int* pl = sm.pl;
+  float* dk = sm.dk;
+  float* dl = sm.dl;
+  float* tk = sm.tk;
+  float* tl = sm.tl;
   const int nb = (n + SB - 1) / SB;
   const int sk = K * TL, sl = L * TL;
   const int mk = min(TL, n - sk), ml = min(TL, n - sl);
@@ -301,16 +308,23 @@ __global__ void __launch_bounds__(256) sbr16_far_kernel(const float* __restrict_
   }
 }
 
+template <int SB>
+__global__ void __launch_bounds__(256) sbr16_far_kernel(const float* __restrict__ A, int n, int64_t lda,
+                                                        const int* __restrict__ perm, const float* __restrict__ Q,
+                                                        const float* __restrict__ dq, const double* __restrict__ stats,
+                                                        float thr_fac, float theta, float* __restrict__ X, int64_t ldx,
+                                                        const float* __restrict__ theta_ptr, const int* __restrict__ skip) {
+  if (skip && *skip) return;
+  if (theta_ptr) theta = *theta_ptr;  // device-side local-threshold switch (ops/sbr_device.py)
+  __shared__ __attribute__((aligned(16))) FarSmem sm;
+  far_tile<SB>(A, n, lda, perm, Q, dq, stats, thr_fac, theta, X, ldx, blockIdx.y, blockIdx.x, sm);
+}
+
 // ------------------------------------------------------------------ 4. Bq = B[:, perm]·blockdiag(Q)
 template <int SB>
-__global__ void __launch_bounds__(256) sbr16_bq_kernel(const float* __restrict__ B, int rows, int n, int64_t ldb,
-                                                       const int* __restrict__ perm, const float* __restrict__ Q,
-                                                       float* __restrict__ Bq, int64_t ldq, const int* __restrict__ skip) {
-  if (skip && *skip) return;
-  __shared__ __attribute__((aligned(16))) float G[TL * TP];
-  __shared__ __attribute__((aligned(16))) float Ql[TL * TP];
-  __shared__ int pl[TL];
-  const int rt = blockIdx.y, L = blockIdx.x;
+__device__ __forceinline__ void bq_tile(const float* __restrict__ B, int rows, int n, int64_t ldb, const int* __restrict__ perm,
+                                        const float* __restrict__ Q, float* __restrict__ Bq, int64_t ldq, int rt, int L, float* G,
+                                        float* Ql, int* pl) {
   const int nb = (n + SB - 1) / SB;
   const int sl = L * TL, ml = min(TL, n - sl);
   if (threadIdx.x < TL) pl[threadIdx.x] = threadIdx.x < ml ? perm[sl + threadIdx.x] : -1;
@@ -351,6 +365,39 @@ __global__ void __launch_bounds__(256) sbr16_bq_kernel(const float* __restrict__
   }
 }
 
+
+template <int SB>
+__global__ void __launch_bounds__(256) sbr16_bq_kernel(const float* __restrict__ B, int rows, int n, int64_t ldb,
+                                                       const int* __restrict__ perm, const float* __restrict__ Q,
+                                                       float* __restrict__ Bq, int64_t ldq, const int* __restrict__ skip) {
+  if (skip && *skip) return;
+  __shared__ __attribute__((aligned(16))) float G[TL * TP];
+  __shared__ __attribute__((aligned(16))) float Ql[TL * TP];
+  __shared__ int pl[TL];
+  bq_tile<SB>(B, rows, n, ldb, perm, Q, Bq, ldq, blockIdx.y, blockIdx.x, G, Ql, pl);
+}
+
+// far generator and Bq in ONE launch (device schedule): both read only the block solve's
+// perm / Q, so the (nt × nt) far tiles and the (row tiles × nt) Bq tiles run side by side —
+// one launch boundary fewer per refinement iteration, and the Bq tiles fill the CUs the far
+// tiles leave idle.  skip_far / skip_bq: the two parts' own control words.
+template <int SB>
+__global__ void __launch_bounds__(256) sbr16_far_bq_kernel(const float* __restrict__ A, int n, int64_t lda, const int* __restrict__ perm,
+                                                           const float* __restrict__ Q, const float* __restrict__ dq,
+                                                           const double* __restrict__ stats, float thr_fac,
+                                                           const float* __restrict__ theta_ptr, float* __restrict__ X, int64_t ldx,
+                                                           const float* __restrict__ B, int rows, int64_t ldb, float* __restrict__ Bq,
+                                                           int64_t ldq, const int* __restrict__ skip_far, const int* __restrict__ skip_bq) {
+  __shared__ __attribute__((aligned(16))) FarSmem sm;
+  const int nt = gridDim.x;
+  if ((int)blockIdx.y < nt) {
+    if (*skip_far) return;
+    far_tile<SB>(A, n, lda, perm, Q, dq, stats, thr_fac, *theta_ptr, X, ldx, blockIdx.y, blockIdx.x, sm);
+  } else {
+    if (*skip_bq) return;
+    bq_tile<SB>(B, rows, n, ldb, perm, Q, Bq, ldq, blockIdx.y - nt, blockIdx.x, sm.G, sm.Ql, sm.pl);
+  }
+}
 
 // ------------------------------------------------------------------ 5. step-size cap (damping)
 // ‖X‖₂ of the skew generator from three power steps on −X² (8 probe vectors): one wave per
@@ -583,6 +630,19 @@ void evx_sbr16_bq(const float* B, int rows, int n, int64_t ldb, const int* perm,
     sbr16_bq_kernel<32><<<dim3(nt, (rows + TL - 1) / TL), 256, 0, s>>>(B, rows, n, ldb, perm, Q, Bq, ldq, skip);
   else
     sbr16_bq_kernel<16><<<dim3(nt, (rows + TL - 1) / TL), 256, 0, s>>>(B, rows, n, ldb, perm, Q, Bq, ldq, skip);
+}
+
+void evx_sbr16_far_bq(const float* A, int n, int64_t lda, const int* perm, const float* Q, const float* dq, const double* stats,
+                      float thr_fac, const float* theta_ptr, float* X, int64_t ldx, const float* B, int rows, int64_t ldb, float* Bq,
+                      int64_t ldq, int sb, hipStream_t s, const int* skip_far, const int* skip_bq) {
+  const int nt = (n + TL - 1) / TL, rt = (rows + TL - 1) / TL;
+  const dim3 grid(nt, nt + rt);
+  if (sb == 32)
+    sbr16_far_bq_kernel<32><<<grid, 256, 0, s>>>(A, n, lda, perm, Q, dq, stats, thr_fac, theta_ptr, X, ldx, B, rows, ldb, Bq, ldq, skip_far,
+                                                 skip_bq);
+  else
+    sbr16_far_bq_kernel<16><<<grid, 256, 0, s>>>(A, n, lda, perm, Q, dq, stats, thr_fac, theta_ptr, X, ldx, B, rows, ldb, Bq, ldq, skip_far,
+                                                 skip_bq);
 }
 
 void evx_sbr_damping_fused(const float* X2, int n, int64_t ldx, const float* V, float* work, float tau, float* alpha, hipStream_t s,

@@ -24,7 +24,10 @@ namespace {
 
 struct SbrDevParams {
   float tol, ns_kappa, damp_kappa, t4_kappa, near_only;
+  float theta0;  // local far threshold factor once κ ≤ theta_kappa (0: only after a stall)
+  float theta_kappa;
   int ns_iters;
+  int lean_from;  // slots ≥ lean_from carry no damping / Newton–Schulz / X³ kernels (order 4, undamped)
 };
 
 __device__ __forceinline__ void rel_kappa(const double* h, double& r, double& k) {
@@ -149,10 +152,11 @@ __global__ void __launch_bounds__(256) sbr_dev_ctrl_kernel(const double* __restr
         c[0] = 1; c[1] = 1; c[2] = 1; c[3] = 1; c[4] = 0; c[5] = 1; c[6] = 0; c[7] = 1;
       } else {
         const float a_prev = alpha[nx];  // step size of the iteration just run (1 at the start)
-        const bool ns = nx < prm.ns_iters || a_prev < 1.f || k > prm.ns_kappa;
-        const bool damp = nx == 0 || k > prm.damp_kappa;
+        const bool lean = nx >= prm.lean_from;
+        const bool ns = !lean && (nx < prm.ns_iters || a_prev < 1.f || k > prm.ns_kappa);
+        const bool damp = !lean && (nx == 0 || k > prm.damp_kappa);
         const bool far = !(nx > 0 && r <= prm.near_only * prm.tol && st[3]);
-        const bool six = !(k < prm.t4_kappa);
+        const bool six = !lean && !(k < prm.t4_kappa);
         c[0] = 0;
         c[1] = far ? 0 : 1;
         c[2] = (far && damp) ? 0 : 1;
@@ -161,7 +165,11 @@ __global__ void __launch_bounds__(256) sbr_dev_ctrl_kernel(const double* __restr
         c[5] = (far && ns) ? 0 : 1;
         c[6] = ns ? 1 : 0;
         c[7] = far ? 1 : 0;
-        theta[nx] = st[4] ? 1.f : 0.f;
+        // local far threshold: sticky after a stalled far iteration, or (theta0) once the far
+        // step is small (κ ≤ theta_kappa: with larger steps the extra strongly coupled far pairs
+        // rotated at once can make a cold-start iteration diverge)
+        const bool th = st[4] || (prm.theta0 > 0.f && k <= prm.theta_kappa);
+        theta[nx] = th ? (prm.theta0 > 0.f ? prm.theta0 : 1.f) : 0.f;
         alpha[nx + 1] = 1.f;  // the damping kernel of iteration nx overwrites it when it runs
       }
     }
@@ -197,23 +205,25 @@ __global__ void __launch_bounds__(256) sbr_dev_ctrl_kernel(const double* __restr
 
 void evx_sbr_dev_prep(const float* X, const float* X2, const float* X3, int n, const float* alpha, float* P, float* MT, const int* ctrl,
                       hipStream_t s) {
+  // a grid-stride loop over 256 workgroups: the schedule skips this kernel in most
+  // iterations, and an empty launch costs in proportion to its workgroup count
   const int64_t total = (int64_t)n * n;
   int g = (int)((total + 255) / 256);
-  if (g > 2048) g = 2048;
+  if (g > 256) g = 256;
   sbr_dev_prep_kernel<<<g, 256, 0, s>>>(X, X2, X3, n, alpha, P, MT, ctrl);
 }
 
 void evx_sbr_dev_copy(const float* src, float* dst, int64_t n, const int* skip, hipStream_t s) {
   int g = (int)((n / 4 + 255) / 256);
   if (g < 1) g = 1;
-  if (g > 2048) g = 2048;
+  if (g > 256) g = 256;  // mostly skipped: keep the empty launch small
   sbr_dev_copy_kernel<<<g, 256, 0, s>>>(src, dst, n, skip);
 }
 
 void evx_sbr_dev_ctrl(const double* part, int nparts, int j, int K, double* hist, float* alpha, float* theta, int* ctrl, int* st,
                       const float* prm6, int ns_iters, const float* A, int64_t lda, int n, float* w_out, double* eig_stats, float* w_init,
-                      double* log, int log_len, int* log_count, hipStream_t s) {
-  SbrDevParams p{prm6[0], prm6[1], prm6[2], prm6[3], prm6[4], ns_iters};
+                      double* log, int log_len, int* log_count, hipStream_t s, int lean_from) {
+  SbrDevParams p{prm6[0], prm6[1], prm6[2], prm6[3], prm6[4], prm6[5], prm6[6], ns_iters, lean_from};
   sbr_dev_ctrl_kernel<<<1, 256, 0, s>>>(part, nparts, j, K, hist, alpha, theta, ctrl, st, p, A, lda, n, w_out, eig_stats, w_init, log,
                                         log_len, log_count);
 }

@@ -112,6 +112,26 @@ class CMAES(Algorithm):
             eig_stats=torch.zeros(4, dtype=torch.float64, device=dev),
         )
 
+    # ------------------------------------------------------------------ step variants
+    def _device_eigh(self) -> bool:
+        return (self.center_init.is_cuda and self.decomp_per_iter == 1 and config.get("cma_fused") and config.get("eigh") == "sbr"
+                and config.get("sbr_mode") == "device" and self.dim % 4 == 0 and self.dim <= 8192)
+
+    def graph_variant(self, generation: int):
+        """The first ``sbr_cold_gens`` generations decompose with the longer cold-start
+        schedule (``sbr_cold_iters`` refinement slots): the warm start is C ≈ I there, the
+        damped steps need ≈10–12 iterations, and later generations converge in 4–7 within the
+        default 8-slot schedule (profiles/r4_sbr_threshold_variants.txt).  The generation
+        index is host-known, so the choice costs no device read."""
+        if self._device_eigh() and generation < int(config.get("sbr_cold_gens")):
+            return "cold"
+        return None
+
+    def graph_variant_context(self, variant):
+        if variant == "cold":
+            return config.override(sbr_device_iters=int(config.get("sbr_cold_iters")))
+        return super().graph_variant_context(variant)
+
     # ------------------------------------------------------------------ sampling
     def _sample(self, state, key, row0: int, rows: int):
         d = self.dim

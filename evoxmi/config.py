@@ -41,6 +41,13 @@ KNOBS: Dict[str, Knob] = {
     "sbr_block": Knob("EVOXMI_SBR_BLOCK", 32, int, "sbr: near-pair block size — 32 or 16 (blocks in a shifted sorted order, eigh_sbr16.hip; 32 converges in fewer iterations on the bench matrices) or 64 (eigh_sbr.hip)"),
     "sbr_mode": Knob("EVOXMI_SBR_MODE", "device", str, "sbr: 'device' — fixed device-controlled iteration schedule inside the generation's graph (ops/sbr_device.py, no host read); 'host' — host-driven iterations with planned solves as a host phase between graph segments (ops/sbr.py)"),
     "sbr_device_iters": Knob("EVOXMI_SBR_DEVICE_ITERS", 8, int, "sbr device mode: refinement iterations in the fixed schedule (kernels of iterations past convergence return at once)"),
+    "sbr_cold_gens": Knob("EVOXMI_SBR_COLD_GENS", 4, int, "CMA-ES device eigensolver: the first generations that use the cold-start schedule (their own hipGraph; the generation index is host-known)"),
+    "sbr_cold_iters": Knob("EVOXMI_SBR_COLD_ITERS", 16, int, "CMA-ES device eigensolver: refinement slots of the cold-start schedule"),
+    "sbr_full_slots": Knob("EVOXMI_SBR_FULL_SLOTS", 5, int, "sbr device schedule (warm, 8 slots): slots past this carry no damping / Newton–Schulz / X³ kernels (those variants are chosen only in the first iterations of a warm-started solve), so a skipped tail slot costs 7 launches fewer"),
+    "sbr_near_only": Knob("EVOXMI_SBR_NEAR_ONLY", 3.0, float, "sbr: a refinement iteration skips the far step once off_rel ≤ this·tol (0: never)"),
+    "sbr_theta0": Knob("EVOXMI_SBR_THETA0", 1.0, float, "sbr: local far-pair threshold factor θ in every iteration whose κ ≤ sbr_theta_kappa (0: switched on only after a stalled far iteration). θ = 1 keeps steady-state CMA-ES solves at 4 iterations where θ = 0 stalls at ≈1.3e-5 for tens of generations (profiles/r4_sbr_threshold_variants.txt)"),
+    "sbr_theta_kappa": Knob("EVOXMI_SBR_THETA_KAPPA", 0.05, float, "sbr: κ below which the local far threshold θ applies (larger far steps with it diverged in cold-start solves)"),
+    "sbr_thr_fac": Knob("EVOXMI_SBR_THR_FAC", 0.3, float, "sbr: global far-pair threshold factor (gap > thr_fac·(block/2)·spread/n)"),
     "cma_fused": Knob("EVOXMI_CMA_FUSED", 1, int, "CMA-ES tell epilogue as the fused cmaes.hip kernels (0: reference-shaped torch ops)"),
     "sbr_fused_damping": Knob("EVOXMI_SBR_FUSED_DAMPING", 0, int, "device-controlled eigensolver: the step-size damping (3 power steps + final) as one grid-barrier launch (1) or four launches (0, default: the grid barriers' agent-scope fences cost more than the three launch boundaries they remove — 1.939 vs 1.888 ms/gen, profiles/NOTES.md)"),
     "cec_fused": Knob("EVOXMI_CEC_FUSED", 0, int, "CEC'22 F1 / F4 on the device: 1 = row terms from the rotation GEMM's epilogue (rotated population never written), 0 = GEMM + basic-function kernel (default: the fused epilogue measured 7 µs slower at pop 10 000 × d 1000, profiles/r3_cec_fused_epilogue.txt)"),

@@ -5,7 +5,8 @@
 ``init_tell`` are optional: when overridden, the workflow uses them at
 generation 0 (the first population may differ in size from later ones).
 """
-from typing import Tuple
+import contextlib
+from typing import Hashable, Optional, Tuple
 
 import torch
 
@@ -27,6 +28,19 @@ class Algorithm(Stateful):
 
     def tell(self, state: State, fitness: torch.Tensor) -> State:
         return State()
+
+    # ---- step variants: a host-known choice of how a generation runs (no device read)
+    def graph_variant(self, generation: int) -> Optional[Hashable]:
+        """Key of the step variant for workflow generation ``generation`` (``None``: the one
+        default).  A hipGraph-capturing workflow captures one graph per distinct key over the
+        same state buffers and replays the matching one; eager steps run inside
+        :meth:`graph_variant_context` too (e.g. CMA-ES's longer cold-start eigensolver
+        schedule for its first generations)."""
+        return None
+
+    def graph_variant_context(self, variant: Hashable):
+        """Context manager active while a step of ``variant`` is captured or run eagerly."""
+        return contextlib.nullcontext()
 
 
 def algorithm_has_init_ask(algorithm: Algorithm, state: State = None) -> bool:

@@ -406,6 +406,8 @@ class SBRConfig:
     damp_kappa: float = 1.0    # estimate ‖X‖₂ in the first iteration and while κ exceeds this
                                # (steady-state CMA-ES: κ ≈ 1.3 → 0.45 → 0.1: only iteration 0)
     near_only: float = 3.0     # near-only (no far step) iteration once off_rel ≤ near_only·tol
+    theta0: float = 0.0        # local far threshold factor once κ ≤ theta_kappa (0: after a stall only)
+    theta_kappa: float = 0.05
     max_jacobi: int = 16
     block_sweeps: int = 2
     block: int = 32            # 16 / 32: blocks in a shifted sorted order (eigh_sbr16.hip; 16 = one
@@ -496,6 +498,10 @@ def decide(cfg: SBRConfig, it: int, off_rel: float, kappa: float, alpha_prev: fl
     # Taylor-4 (one GEMM fewer) only for small steps: a damped ‖αX‖₂ ≈ 1 step loses ~1e-2 of
     # orthogonality at 4th order, more than one Newton–Schulz step repairs
     order = 4 if kappa < cfg.t4_kappa else 6
+    # the local far threshold from the start once the step is undamped (the device schedule's
+    # rule, eigh_sbr_dev.hip)
+    if cfg.theta0 > 0 and kappa <= cfg.theta_kappa:
+        theta = max(theta, cfg.theta0)
     return (ns, damp, far_on, theta, order)
 
 

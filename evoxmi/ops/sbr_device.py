@@ -46,10 +46,14 @@ def config_fused_damping() -> bool:
 class DeviceSBR:
     """Persistent buffers + the fixed iteration schedule for one (n, device, config)."""
 
-    def __init__(self, n: int, device, cfg: SBRConfig, iters: int):
+    def __init__(self, n: int, device, cfg: SBRConfig, iters: int, lean_from: int = None):
         if cfg.block not in (16, 32):
             raise ValueError("the device schedule uses the shifted-layout blocks (16 / 32)")
         self.n, self.cfg, self.K = n, cfg, int(iters)
+        # slots ≥ lean_from launch no damping / Newton–Schulz / X³ kernels (their variants are
+        # only chosen in the first iterations of a warm-started solve): a skipped lean slot
+        # costs 7 launch boundaries fewer
+        self.lean_from = self.K if lean_from is None else min(int(lean_from), self.K)
         dev = torch.device(device)
         ops = _ext.ops()
 
@@ -81,7 +85,8 @@ class DeviceSBR:
         self.eig_stats = torch.zeros(4, dtype=torch.float64, device=dev)
         self.log = torch.zeros(LOG_LEN, 4, dtype=torch.float64, device=dev)
         self.log_count = torch.zeros(1, dtype=torch.int32, device=dev)
-        self.prm = [float(cfg.tol), float(cfg.ns_kappa), float(cfg.damp_kappa), float(cfg.t4_kappa), float(cfg.near_only)]
+        self.prm = [float(cfg.tol), float(cfg.ns_kappa), float(cfg.damp_kappa), float(cfg.t4_kappa), float(cfg.near_only),
+                    float(cfg.theta0), float(cfg.theta_kappa), float(self.lean_from)]
 
     # ------------------------------------------------------------------ pieces
     def _btcb(self, C, skip):
@@ -100,23 +105,26 @@ class DeviceSBR:
         c = self.ctrl[8 * j : 8 * j + 8]
         sk_all, sk_far, sk_damp, sk_x3, sel6, sk_ns, sel_ns, sk_copy = (c[i : i + 1] for i in range(8))
         shift = (j % 2) * (sb // 2)
+        full = j < self.lean_from
         ops.sbr16_block_out(self.A, shift, int(cfg.block_sweeps), sb, self.perm, self.Q, self.dq, sk_all)
-        ops.sbr16_far_out(self.A, self.perm, self.Q, self.dq, self.hist[4 * j : 4 * j + 4], float(cfg.thr_fac),
-                          self.theta[j : j + 1], self.X, sb, sk_far)
+        # far generator X and Bq = B[:, perm]·blockdiag(Q) in one launch
+        ops.sbr16_far_bq_out(self.A, self.perm, self.Q, self.dq, self.hist[4 * j : 4 * j + 4], float(cfg.thr_fac),
+                             self.theta[j : j + 1], self.X, self.B, self.Bq, sb, sk_far, sk_all)
         # X skew ⇒ X² = −X·Xᵀ, symmetric (upper tiles only)
         mm(self.X, self.X, tb=True, mode=1, alpha=-1.0, out=self.X2, skip=sk_far)
-        if cfg.damp_tau > 0:
+        if cfg.damp_tau > 0 and full:
             ops.sbr_damping_out(self.X2, self.V, float(cfg.damp_tau), self.alpha[j + 1 : j + 2], self.work, sk_damp, self.bar)
-        ops.sbr16_bq_out(self.B, self.perm, self.Q, self.Bq, sb, sk_all)
-        # order 6 only: X³ = X²·X = −X²·Xᵀ (skew)
-        mm(self.X2, self.X, tb=True, mode=2, alpha=-1.0, out=self.X3, skip=sk_x3)
+        if full:
+            # order 6 only: X³ = X²·X = −X²·Xᵀ (skew)
+            mm(self.X2, self.X, tb=True, mode=2, alpha=-1.0, out=self.X3, skip=sk_x3)
         ops.sbr_dev_prep(self.X, self.X2, self.X3, self.alpha[j + 1 : j + 2], self.P, self.VT, c)
         # Vᵀ = M(−α) + X²·Pᵀ (order 4) or M(−α) − X³·Pᵀ (order 6): the control word selects
         mm(self.X2, self.P, tb=True, alpha=1.0, beta=1.0, Cin=self.VT, out=self.VT, skip=sk_far, sel=sel6, A2=self.X3, alpha2=-1.0)
         # B·V → B, or into T when Newton–Schulz follows
         mm(self.Bq, self.VT, tb=True, out=self.B, skip=sk_far, sel=sel_ns, C2=self.T)
-        mm(self.T, self.T, ta=True, mode=1, out=self.G, skip=sk_ns)
-        mm(self.T, self.G, tb=True, alpha=-0.5, beta=1.5, Cin=self.T, out=self.B, skip=sk_ns)
+        if full:
+            mm(self.T, self.T, ta=True, mode=1, out=self.G, skip=sk_ns)
+            mm(self.T, self.G, tb=True, alpha=-0.5, beta=1.5, Cin=self.T, out=self.B, skip=sk_ns)
         # near-only iteration: the block-rotated basis is the new basis
         ops.sbr_dev_copy(self.Bq, self.B, sk_copy)
         self._btcb(C, sk_all)
@@ -153,11 +161,11 @@ class DeviceSBR:
 _WS = {}
 
 
-def workspace(n: int, device, cfg: SBRConfig, iters: int) -> DeviceSBR:
+def workspace(n: int, device, cfg: SBRConfig, iters: int, lean_from: int = None) -> DeviceSBR:
     key = (n, str(device), cfg.block, cfg.block_sweeps, cfg.thr_fac, cfg.ns_iters, cfg.damp_tau, cfg.tol, cfg.ns_kappa,
-           cfg.damp_kappa, cfg.t4_kappa, cfg.near_only, int(iters))
+           cfg.damp_kappa, cfg.t4_kappa, cfg.near_only, cfg.theta0, cfg.theta_kappa, int(iters), lean_from)
     if key not in _WS:
-        _WS[key] = DeviceSBR(n, device, cfg, iters)
+        _WS[key] = DeviceSBR(n, device, cfg, iters, lean_from)
     return _WS[key]
 
 
@@ -166,9 +174,17 @@ def eigh_device(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None, it
     ``B_prev``, entirely on the device (see module docstring).  Returns ``(w, B, stats)``."""
     from .. import config
 
-    cfg = cfg or SBRConfig(tol=config.get("eigh_tol"), block=config.get("sbr_block"))
-    iters = config.get("sbr_device_iters") if iters is None else iters
-    return workspace(C.shape[0], C.device, cfg, iters).solve(C, B_prev)
+    cfg = cfg or SBRConfig(tol=config.get("eigh_tol"), block=config.get("sbr_block"), near_only=config.get("sbr_near_only"),
+                           theta0=config.get("sbr_theta0"), theta_kappa=config.get("sbr_theta_kappa"),
+                           thr_fac=config.get("sbr_thr_fac"))
+    if iters is None:
+        iters = config.get("sbr_device_iters")
+        # lean tail slots only in a schedule that does not start cold (CMA-ES's cold-start
+        # variant passes a longer schedule with every slot full)
+        lean = config.get("sbr_full_slots") if iters < config.get("sbr_cold_iters") else None
+    else:
+        lean = None
+    return workspace(C.shape[0], C.device, cfg, iters, lean).solve(C, B_prev)
 
 
 def all_histories():

@@ -107,6 +107,7 @@ class StdWorkflow(Workflow):
         self._dim_shard_group = None  # set by enable_multi_devices (decision-axis sharding)
         # graph-mode bookkeeping
         self._graph = None
+        self._graphs = {}  # graph variant (Algorithm.graph_variant) → (graph, hook record)
         self._graph_failed = False
         self._static = None
         self._static_out = None
@@ -213,14 +214,21 @@ class StdWorkflow(Workflow):
             stack.enter_context(timer.phase(name))
         return stack
 
+    def _variant(self, state):
+        gv = getattr(self.algorithm, "graph_variant", None)
+        return gv(int(state.generation)) if gv is not None else None
+
     def _step_eager(self, state):
         from ..utils import profiling
 
         is_init = self._has_init_ask and state.generation == 0
         prev = profiling._ACTIVE_TIMER
         profiling._ACTIVE_TIMER = self.phase_timer
+        variant = self._variant(state)
+        ctx = self.algorithm.graph_variant_context(variant) if variant is not None else contextlib.nullcontext()
         try:
-            return self._proto_step(bool(is_init), state)
+            with ctx:
+                return self._proto_step(bool(is_init), state)
         finally:
             profiling._ACTIVE_TIMER = prev
 
@@ -228,8 +236,13 @@ class StdWorkflow(Workflow):
     def _hooks_inside_step(self):
         return any(self.registered_hooks[h] for h in HOOKS[1:-1])
 
-    def _capture(self, state):
-        """Capture one (non-init) generation into a hipGraph."""
+    def _capture(self, state, variant=None):
+        """Capture one (non-init) generation into a hipGraph.
+
+        ``variant``: the algorithm's graph variant for this generation
+        (:meth:`evoxmi.core.Algorithm.graph_variant`, e.g. CMA-ES's longer cold-start
+        eigensolver schedule).  Every variant is captured once, over the SAME static state
+        buffers, and replayed by generation index from then on."""
         dev = None
         for x in tree_flatten(state)[0]:
             if isinstance(x, torch.Tensor) and x.is_cuda:
@@ -237,13 +250,17 @@ class StdWorkflow(Workflow):
                 break
         if dev is None:
             raise RuntimeError("graph=True requires the state to live on a GPU")
-        static = tree_map(lambda x: x.clone() if isinstance(x, torch.Tensor) else x, state)
+        static = self._static if self._static is not None else tree_map(lambda x: x.clone() if isinstance(x, torch.Tensor) else x, state)
+        if self._static is not None and state is not static and state is not self._static_out:
+            self._load_static(static, state)
+        ctx = self.algorithm.graph_variant_context(variant) if variant is not None else contextlib.nullcontext()
         # warm-up on a side stream (allocator / lazy init), as required for capture
         s = torch.cuda.Stream(device=dev)
         s.wait_stream(torch.cuda.current_stream(dev))
         saved_hooks = self.registered_hooks
         self.registered_hooks = {h: [] for h in HOOKS}
         try:
+            ctx.__enter__()
             with torch.cuda.stream(s):
                 self._proto_step(False, tree_map(lambda x: x.clone() if isinstance(x, torch.Tensor) else x, static))
             torch.cuda.current_stream(dev).wait_stream(s)
@@ -277,6 +294,7 @@ class StdWorkflow(Workflow):
 
             in_leaves, out_leaves = g.capture(body, s)
         finally:
+            ctx.__exit__(None, None, None)
             self.registered_hooks = saved_hooks
         # python (non-tensor) leaves must be step-invariant, except the generation counter
         py_changed = [
@@ -287,24 +305,31 @@ class StdWorkflow(Workflow):
         if len(py_changed) > 1:
             raise RuntimeError(f"graph=True: host-side state fields change every step {py_changed}; not graph-safe")
         self._graph = g
+        self._graphs[variant] = (g, record)
         self._static = static
         self._hook_args = record
         return static
 
+    @staticmethod
+    def _load_static(static, state):
+        """A foreign state (e.g. a restored checkpoint) into the static buffers."""
+        for a, b in zip(tree_flatten(static)[0], tree_flatten(state)[0]):
+            if isinstance(a, torch.Tensor):
+                if isinstance(b, torch.Tensor):
+                    if b.data_ptr() != a.data_ptr():
+                        a.copy_(b)
+                else:  # e.g. a harness writing progress=0.3 into a tensor field
+                    a.fill_(b)
+
     def _step_graph(self, state):
-        if self._graph is None:
-            static = self._capture(state)
+        variant = self._variant(state)
+        if variant not in self._graphs:
+            static = self._capture(state, variant)
         else:
+            self._graph, self._hook_args = self._graphs[variant]
             static = self._static
             if state is not static and state is not self._static_out:
-                # a foreign state (e.g. restored checkpoint): load it into the static buffers
-                for a, b in zip(tree_flatten(static)[0], tree_flatten(state)[0]):
-                    if isinstance(a, torch.Tensor):
-                        if isinstance(b, torch.Tensor):
-                            if b.data_ptr() != a.data_ptr():
-                                a.copy_(b)
-                        else:  # e.g. a harness writing progress=0.3 into a tensor field
-                            a.fill_(b)
+                self._load_static(static, state)
         with self._phase("graph_replay"):
             self._graph.replay()
         gen = state.generation + 1
@@ -338,6 +363,8 @@ class StdWorkflow(Workflow):
                     # the capture was invalidated, the input state is untouched — run eagerly from now on
                     self._graph_failed = True
                     self._graph = None
+                    self._graphs = {}
+                    self._static = None
                     torch.cuda.synchronize()
                     warnings.warn(f"graph='auto': {type(self.algorithm).__name__} step is not capturable ({str(e).splitlines()[0]}); running eagerly")
                     state = self._step_eager(state)

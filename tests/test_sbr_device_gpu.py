@@ -30,7 +30,10 @@ def test_device_schedule_converges_like_host_driver(gens):
     ev = torch.linalg.eigvalsh(C.double())
     assert float((torch.sort(w.double()).values - ev).abs().max()) < 5e-5
     # the host driver (adaptive, no plans, no graphs) takes the same decisions
-    _, _, info = sbr.eigh_warm(C, B, sbr.SBRConfig(graphs=False, plan=False))
+    from evoxmi import config
+
+    _, _, info = sbr.eigh_warm(C, B, sbr.SBRConfig(graphs=False, plan=False, theta0=config.get("sbr_theta0"),
+                                                  near_only=config.get("sbr_near_only"), thr_fac=config.get("sbr_thr_fac")))
     assert abs(int(st[2]) - info.refine_iters) <= 1, (int(st[2]), info.refine_iters)
 
 
@@ -99,3 +102,31 @@ def test_cmaes_device_mode_checkpoint_resume_is_bitwise(tmp_path):
     for k in ("B", "C", "mean", "sigma", "D"):
         assert torch.equal(getattr(ref, k), getattr(got, k)), k
     assert float(ref.eig_stats[0]) <= 1e-5
+
+
+def test_cmaes_default_schedule_converges_every_generation_from_cold_start():
+    """The north-star configuration (d = 1000, λ = 10 000, CEC'22 F1) with the DEFAULT
+    device schedule for 200 generations from a cold start (C = I): the first generations
+    replay the cold-start graph variant (CMAES.graph_variant), later ones the 8-slot schedule,
+    and every logged solve reaches the tolerance — no capped, no fallen-back decomposition
+    (the reference decomposes exactly every generation, cma_es.py:155-160,193-198)."""
+    from evoxmi import config
+    from evoxmi import random as rnd
+    from evoxmi.algorithms import CMAES
+    from evoxmi.problems.numerical import CEC2022TestSuit
+    from evoxmi.workflows import StdWorkflow
+
+    assert config.get("sbr_mode") == "device" and config.get("eigh") == "sbr"
+    center = (torch.rand(1000, generator=torch.Generator().manual_seed(1)) * 160 - 80).cuda()
+    wf = StdWorkflow(CMAES(center_init=center, init_stdev=20.0, pop_size=10000), CEC2022TestSuit.create(1), graph=True)
+    st = wf.init(rnd.PRNGKey(2024, device=torch.device("cuda")))
+    snap = sbr_device.snapshot_counts()
+    for _ in range(200):
+        st = wf.step(st)
+    h = sbr_device.histories_since(snap)
+    assert h.shape[0] >= 200  # + one capture warm-up solve per graph variant
+    tol = config.get("eigh_tol")
+    assert float(h[:, 0].max()) <= tol, h[h[:, 0] > tol]
+    assert float(h[:, 3].sum()) == 0.0
+    assert set(wf._graphs) == {"cold", None}
+    assert int(h[:, 2].max()) <= max(config.get("sbr_device_iters"), config.get("sbr_cold_iters"))
