@@ -249,6 +249,106 @@ at::Tensor gemm_ks(const at::Tensor& A, int64_t a_kc, const at::Tensor& B, int64
   return C;
 }
 
+// C = alpha·(*alpha_ptr)·op(A)·op(B)ᵀ (+ bias_n) for K-contiguous operands, either of which may be
+// given as bf16x6 fragment planes (int16 [3][rows][kp], split_planes / philox_normal_planes)
+at::Tensor gemm_ks_pl(const c10::optional<at::Tensor>& A, const c10::optional<at::Tensor>& a_pl, const c10::optional<at::Tensor>& B,
+                      const c10::optional<at::Tensor>& b_pl, int64_t M, int64_t N, int64_t K, double alpha,
+                      const c10::optional<at::Tensor>& alpha_ptr, const c10::optional<at::Tensor>& bias_n,
+                      const c10::optional<at::Tensor>& out, const c10::optional<at::Tensor>& a_sub_k) {
+  const bool ha = A.has_value() && A->defined(), hap = a_pl.has_value() && a_pl->defined();
+  const bool hb = B.has_value() && B->defined(), hbp = b_pl.has_value() && b_pl->defined();
+  TORCH_CHECK(ha != hap && hb != hbp, "gemm_ks_pl: give each operand as f32 or as planes");
+  TORCH_CHECK(M > 0 && N > 0 && K > 0 && K % 4 == 0, "gemm_ks_pl: shape (K % 4 == 0)");
+  const int64_t kp = (K + 31) / 32 * 32;
+  auto vec4_ok = [](const at::Tensor& t) { return (reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0) && (t.stride(0) % 4 == 0); };
+  auto check_pl = [&](const at::Tensor& t, int64_t rows, const char* w) {
+    CHECK_DEV(t);
+    TORCH_CHECK(t.scalar_type() == at::kShort && t.dim() == 3 && t.size(0) == 3 && t.size(1) >= rows && t.size(2) == kp && t.is_contiguous(),
+                "gemm_ks_pl: ", w, " planes int16 [3, rows, kp]");
+  };
+  EvxGemmKs a{};
+  const at::Tensor& ref = ha ? *A : *a_pl;
+  if (ha) {
+    CHECK_DEV(*A); CHECK_F32(*A);
+    TORCH_CHECK(A->dim() == 2 && A->stride(1) == 1 && A->size(0) >= M && A->size(1) >= K && vec4_ok(*A), "gemm_ks_pl: A");
+    a.A = A->data_ptr<float>();
+    a.lda = A->stride(0);
+  } else {
+    check_pl(*a_pl, M, "A");
+    a.a_pl = reinterpret_cast<const uint16_t*>(a_pl->data_ptr<int16_t>());
+    a.a_pl_rows = a_pl->size(1);
+  }
+  if (hb) {
+    CHECK_DEV(*B); CHECK_F32(*B);
+    TORCH_CHECK(B->dim() == 2 && B->stride(1) == 1 && B->size(0) >= N && B->size(1) >= K && vec4_ok(*B), "gemm_ks_pl: B");
+    a.B = B->data_ptr<float>();
+    a.ldb = B->stride(0);
+  } else {
+    check_pl(*b_pl, N, "B");
+    a.b_pl = reinterpret_cast<const uint16_t*>(b_pl->data_ptr<int16_t>());
+    a.b_pl_rows = b_pl->size(1);
+  }
+  a.pl_kp = kp;
+  c10::DeviceGuard g(ref.device());
+  at::Tensor C;
+  if (out.has_value() && out->defined()) {
+    C = *out;
+    CHECK_DEV(C); CHECK_F32(C);
+    TORCH_CHECK(C.dim() == 2 && C.stride(1) == 1 && C.size(0) >= M && C.size(1) >= N, "gemm_ks_pl: out shape");
+  } else {
+    C = at::empty({M, N}, ref.options().dtype(at::kFloat));
+  }
+  a.C = C.data_ptr<float>();
+  a.ldc = C.stride(0);
+  a.M = (int)M; a.N = (int)N; a.K = (int)K;
+  a.a_kc = 1; a.b_kc = 1; a.mode = 0;
+  a.alpha = (float)alpha;
+  a.alpha_ptr = optf(alpha_ptr);
+  if (bias_n.has_value() && bias_n->defined()) {
+    CHECK_DEV(*bias_n); CHECK_F32(*bias_n); CHECK_CONTIG(*bias_n);
+    TORCH_CHECK(bias_n->numel() >= N, "gemm_ks_pl: bias length");
+    a.bias_n = bias_n->data_ptr<float>();
+  }
+  if (a_sub_k.has_value() && a_sub_k->defined()) {
+    CHECK_DEV(*a_sub_k); CHECK_F32(*a_sub_k); CHECK_CONTIG(*a_sub_k);
+    TORCH_CHECK(ha && a_sub_k->numel() >= K && reinterpret_cast<uintptr_t>(a_sub_k->data_ptr()) % 16 == 0,
+                "gemm_ks_pl: a_sub_k needs an f32 A (16-byte aligned, length ≥ K)");
+    a.a_sub_k = a_sub_k->data_ptr<float>();
+  }
+  a.c_vec4 = vec4_ok(C) ? 1 : 0;
+  evx_gemm_ks(a, cur_stream());
+  return C;
+}
+
+at::Tensor split_planes(const at::Tensor& X, const c10::optional<at::Tensor>& colscale) {
+  CHECK_DEV(X); CHECK_F32(X);
+  TORCH_CHECK(X.dim() == 2 && X.stride(1) == 1, "split_planes: 2-D, unit inner stride");
+  const int64_t rows = X.size(0), K = X.size(1), kp = (K + 31) / 32 * 32;
+  const float* cs = nullptr;
+  if (colscale.has_value() && colscale->defined()) {
+    CHECK_DEV(*colscale); CHECK_F32(*colscale); CHECK_CONTIG(*colscale);
+    TORCH_CHECK(colscale->numel() >= K, "split_planes: colscale length");
+    cs = colscale->data_ptr<float>();
+  }
+  c10::DeviceGuard g(X.device());
+  at::Tensor out = at::empty({3, rows, kp}, X.options().dtype(at::kShort));
+  evx_split_planes(X.data_ptr<float>(), X.stride(0), rows, (int)K, cs, reinterpret_cast<uint16_t*>(out.data_ptr<int16_t>()), kp,
+                   cur_stream());
+  return out;
+}
+
+at::Tensor philox_normal_planes(const at::Tensor& key, int64_t rows, int64_t d, int64_t row0) {
+  CHECK_DEV(key);
+  TORCH_CHECK(key.scalar_type() == at::kLong && key.numel() >= 2 && key.is_contiguous(), "philox_normal_planes: key int64[2]");
+  TORCH_CHECK(d % 4 == 0 && rows > 0, "philox_normal_planes: d % 4 == 0");
+  const int64_t kp = (d + 31) / 32 * 32;
+  c10::DeviceGuard g(key.device());
+  at::Tensor out = at::empty({3, rows, kp}, key.options().dtype(at::kShort));
+  evx_philox_normal_planes(key.data_ptr<int64_t>(), rows, (int)d, row0, reinterpret_cast<uint16_t*>(out.data_ptr<int16_t>()), kp,
+                           cur_stream());
+  return out;
+}
+
 void gemm_ks_set_tile(int64_t t) { evx_gemm_ks_set_tile((int)t); }
 void gemm_ks_set_prec(int64_t p) { evx_gemm_ks_set_prec((int)p); }
 
@@ -1287,6 +1387,9 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("sbr_dev_ctrl(Tensor part, int nparts, int j, int K, Tensor(a!) hist, Tensor(b!) alpha, Tensor(c!) theta, Tensor(d!) ctrl, Tensor(e!) st, float[] prm, int ns_iters, Tensor A, Tensor(f!) w_out, Tensor(g!) eig_stats, Tensor(h!) w_init, Tensor(i!) log, Tensor(j!) log_count) -> ()");
   m.def("gemm_ks_set_tile(int t) -> ()");
   m.def("gemm_ks_set_prec(int prec) -> ()");
+  m.def("gemm_ks_pl(Tensor? A, Tensor? a_pl, Tensor? B, Tensor? b_pl, int M, int N, int K, float alpha, Tensor? alpha_ptr, Tensor? bias_n, Tensor(a!)? out, Tensor? a_sub_k) -> Tensor");
+  m.def("split_planes(Tensor X, Tensor? colscale) -> Tensor");
+  m.def("philox_normal_planes(Tensor key, int rows, int d, int row0) -> Tensor");
   m.def("sbr16_far_bq_out(Tensor A, Tensor perm, Tensor Q, Tensor dq, Tensor stats, float thr_fac, Tensor theta, Tensor(a!) X, Tensor B, Tensor(b!) Bq, int sb, Tensor skip_far, Tensor skip_bq) -> ()");
   m.def("lsmop_g(Tensor X, int[] start, int[] sublen, int[] func, int nk, int cosine) -> Tensor");
   m.def("cma_delta_gemv(Tensor M, Tensor mean, Tensor dm, float cm) -> Tensor[]");
@@ -1327,6 +1430,9 @@ TORCH_LIBRARY_IMPL(evoxmi, CompositeExplicitAutograd, m) {
   m.impl("gemm_set_config", &gemm_set_config);
   m.impl("gemm_ks_set_tile", &gemm_ks_set_tile);
   m.impl("gemm_ks_set_prec", &gemm_ks_set_prec);
+  m.impl("gemm_ks_pl", &gemm_ks_pl);
+  m.impl("split_planes", &split_planes);
+  m.impl("philox_normal_planes", &philox_normal_planes);
   m.impl("sbr16_far_bq_out", &sbr16_far_bq_out);
   m.impl("gemm_ks_grid", &gemm_ks_grid);
   m.impl("gemm_ks_tile", &gemm_ks_tile);

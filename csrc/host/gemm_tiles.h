@@ -7,10 +7,10 @@
 
 namespace evx_host {
 
-// tile code t: output tile 16t × 16t, except t = 8: 128 × 64 (tall full products) and
-// t = 9: 128 × 128 (bf16x6 on the 32x32x16 MFMA only)
+// tile code t: output tile 16t × 16t, except t = 8: 128 × 64 (tall full products).  (A
+// 128 × 128 tile on the 32x32x16 bf16x6 form spills 85 registers: measured slower, dropped.)
 inline int gemm_ks_tile(int64_t M, int64_t N, int mode, int override_tile = 0) {
-  if (override_tile) return ((override_tile == 8 || override_tile == 9) && mode != 0) ? 4 : override_tile;
+  if (override_tile) return (override_tile == 8 && mode != 0) ? 4 : override_tile;
   // tall full products (sampling / CEC rotation, 10 000 × 1000 × 1000): 128 × 64 tiles —
   // half the B-panel reloads per output of 64 × 64 (tools/gemm_ks_probe.cpp: 210 vs 317 µs)
   if (mode == 0 && M >= 2048 && N >= 64) return 8;
@@ -30,8 +30,8 @@ inline int gemm_ks_tile(int64_t M, int64_t N, int mode, int override_tile = 0) {
   return best;
 }
 
-inline int64_t gemm_ks_tile_rows(int t) { return t == 9 ? 128 : 16 * (int64_t)t; }
-inline int64_t gemm_ks_tile_cols(int t) { return t == 8 ? 64 : t == 9 ? 128 : 16 * (int64_t)t; }
+inline int64_t gemm_ks_tile_rows(int t) { return 16 * (int64_t)t; }
+inline int64_t gemm_ks_tile_cols(int t) { return t == 8 ? 64 : 16 * (int64_t)t; }
 
 // workgroups of a launch: full grid, or the upper-triangle tiles of a (skew-)symmetric output
 inline int64_t gemm_ks_grid(int64_t M, int64_t N, int mode, int override_tile = 0) {

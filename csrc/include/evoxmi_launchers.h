@@ -67,8 +67,18 @@ struct EvxGemmKs {
   // Σ y² − 10 cos 2πy + 10 with y = 0.0512 z, 0), finished by evx_cec_rowterms_final
   float* row_terms;
   int row_fid;
+  // bf16x6 only: operands pre-split into fragment planes (evx_split_planes / evx_philox_normal_planes):
+  // uint16 [3][rows][kp] (h, m, l), kp = K rounded up to 32, each 32-k group in fragment order —
+  // the operand's f32 pointer is then not read (a K-contiguous operand of the same shape)
+  const uint16_t* a_pl;
+  const uint16_t* b_pl;
+  int64_t a_pl_rows, b_pl_rows, pl_kp;
 };
 void evx_gemm_ks(const EvxGemmKs& a, hipStream_t s);
+// fragment planes of X (rows × K, K-contiguous, row stride ld), X[r][k]·colscale[k] when colscale
+void evx_split_planes(const float* X, int64_t ld, int64_t rows, int K, const float* colscale, uint16_t* out, int64_t kp, hipStream_t s);
+// fragment planes of rows [row0, row0 + rows) of the virtual normal matrix normal(key, (·, d)) (d % 4 == 0)
+void evx_philox_normal_planes(const int64_t* key, int64_t rows, int d, int64_t row0, uint16_t* out, int64_t kp, hipStream_t s);
 int evx_gemm_ks_tiles_n(int M, int N, int mode);  // column tiles of a launch (row-terms partial count)
 void evx_cec_rowterms_final(const float* parts, int tiles_n, int M, int fid, float* out, hipStream_t s);
 int evx_gemm_ks_grid(int M, int N, int mode);  // workgroups of a launch (stat_part length)

@@ -219,9 +219,11 @@ __device__ __forceinline__ void decode_tile(int bid, int tiles_m, int tiles_n, i
 // PREC 1: bf16x6 (KH = 2: a 32-k group is one 16x16x32 bf16 step — lane (r, q) holds
 // fragment element j ↔ k = 32·group + 16·(j >> 2) + 4q + (j & 3), the same k map for A and B,
 // so the f32 path's loads are reused unchanged).
-template <int TM, int TN, int KH, bool AKC, bool BKC, int MODE, int PREC>
+template <int TM, int TN, int KH, bool AKC, bool BKC, int MODE, int PREC, int PL = 0>
 __global__ void __launch_bounds__(256) gemm_ks_kernel(EvxGemmKs p) {
   static_assert(PREC == 0 || KH == 2, "bf16x6 groups hold two float4 per lane and block");
+  static_assert(PL == 0 || (PREC == 1 && AKC && BKC), "fragment planes: bf16x6 on 16x16x32, K-contiguous operands");
+  constexpr bool APL = PL & 1, BPL = PL & 2;
   static_assert(PREC != 2 || (TM % 2 == 0 && TN % 2 == 0), "32x32 MFMA tiles need even 16-blocks");
   if (p.skip && *p.skip) return;
   if (p.sel && *p.sel) {
@@ -273,6 +275,21 @@ __global__ void __launch_bounds__(256) gemm_ks_kernel(EvxGemmKs p) {
     bp[j] = BKC ? p.B + (int64_t)col * p.ldb : p.B + col;
   }
 
+  // fragment-plane operands: lane (r, q) reads the 16 bytes of its 8 k values of a 32-k group at
+  // plane[row][32·group + 8q] (h, m and l planes 3 × 16 B apart by a plane stride)
+  const uint16_t* apl[APL ? NA : 1];
+  const uint16_t* bpl[BPL ? NB : 1];
+  const int64_t pl_kp = p.pl_kp;
+  if constexpr (APL) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) apl[i] = p.a_pl + (int64_t)min(m0 + RB * i + rl, p.M - 1) * pl_kp + 8 * q;
+  }
+  if constexpr (BPL) {
+#pragma unroll
+    for (int j = 0; j < NB; ++j) bpl[j] = p.b_pl + (int64_t)min(n0 + RB * j + rl, p.N - 1) * pl_kp + 8 * q;
+  }
+  const int64_t a_plane = (int64_t)p.a_pl_rows * pl_kp, b_plane = (int64_t)p.b_pl_rows * pl_kp;
+
   using AccT = typename std::conditional<PREC == 2, f32x16, f32x4>::type;
   AccT acc[NA][NB];
 #pragma unroll
@@ -284,13 +301,14 @@ __global__ void __launch_bounds__(256) gemm_ks_kernel(EvxGemmKs p) {
 
   // loads per slot: one float4 (KC) or four dwords (RC) per block and float4 slot; at most
   // 63 vector loads can be counted in flight (vmcnt)
-  constexpr int LPS = KH * (NA * (AKC ? 1 : 4) + NB * (BKC ? 1 : 4));
+  constexpr int LPS = KH * (NA * (AKC ? 1 : 4) + NB * (BKC ? 1 : 4)) + (APL ? NA : 0) + (BPL ? NB : 0);
 #ifdef EVX_KS_DEPTH  // tools/gemm_ks_probe.cpp experiments
   constexpr int D = EVX_KS_DEPTH;
 #else
   constexpr int D = (3 * LPS <= 63) ? 3 : 2;
 #endif
-  float4 fa[D][KH][NA], fb[D][KH][NB];
+  float4 fa[D][KH][APL ? 1 : NA], fb[D][KH][BPL ? 1 : NB];
+  uint4 pa[D][3][APL ? NA : 1], pb[D][3][BPL ? NB : 1];
   const int64_t lda = p.lda, ldb = p.ldb;
   // k of float4 h of a lane: PREC 0/1: KG·group + 16h + 4q + c (lane (r, q));
   // PREC 2: KG·group + 8·hw + 4h + c (lane (rw, hw)) — the same map for A and B, so the
@@ -300,19 +318,38 @@ __global__ void __launch_bounds__(256) gemm_ks_kernel(EvxGemmKs p) {
   // values rides along with the operand loads, the subtraction runs just before the MFMAs
   const float* __restrict__ asub = p.a_sub_k;
   float4 fs[D][KH];
-  auto load_slot = [&](float4 (&xa)[KH][NA], float4 (&xb)[KH][NB], float4 (&xs)[KH], int grp) {
+  constexpr int NAF = APL ? 1 : NA, NBF = BPL ? 1 : NB;
+  auto load_slot = [&](float4 (&xa)[KH][NAF], float4 (&xb)[KH][NBF], float4 (&xs)[KH], uint4 (&ya)[3][APL ? NA : 1],
+                       uint4 (&yb)[3][BPL ? NB : 1], int grp) {
 #pragma unroll
     for (int h = 0; h < KH; ++h) {
       const int k = kof(grp, h);
-      if (AKC && asub) xs[h] = *reinterpret_cast<const float4*>(asub + k);
+      if (AKC && asub && !APL) xs[h] = *reinterpret_cast<const float4*>(asub + k);
+      if constexpr (!APL) {
 #pragma unroll
-      for (int i = 0; i < NA; ++i) xa[h][i] = load_full<AKC>(ap[i], lda, k);
+        for (int i = 0; i < NA; ++i) xa[h][i] = load_full<AKC>(ap[i], lda, k);
+      }
+      if constexpr (!BPL) {
 #pragma unroll
-      for (int j = 0; j < NB; ++j) xb[h][j] = load_full<BKC>(bp[j], ldb, k);
+        for (int j = 0; j < NB; ++j) xb[h][j] = load_full<BKC>(bp[j], ldb, k);
+      }
+    }
+    if constexpr (APL) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int i = 0; i < NA; ++i) ya[c][i] = *reinterpret_cast<const uint4*>(apl[i] + c * a_plane + 32 * grp);
+    }
+    if constexpr (BPL) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) yb[c][j] = *reinterpret_cast<const uint4*>(bpl[j] + c * b_plane + 32 * grp);
     }
   };
-  auto compute_slot = [&](float4 (&xa)[KH][NA], const float4 (&xb)[KH][NB], const float4 (&xs)[KH]) {
-    if (AKC && asub) {
+  auto compute_slot = [&](float4 (&xa)[KH][NAF], const float4 (&xb)[KH][NBF], const float4 (&xs)[KH], const uint4 (&ya)[3][APL ? NA : 1],
+                          const uint4 (&yb)[3][BPL ? NB : 1]) {
+    if (AKC && asub && !APL) {
 #pragma unroll
       for (int h = 0; h < KH; ++h)
 #pragma unroll
@@ -326,11 +363,25 @@ __global__ void __launch_bounds__(256) gemm_ks_kernel(EvxGemmKs p) {
     if constexpr (PREC >= 1) {
       bf16x8 bh[NB], bm[NB], bl[NB];
 #pragma unroll
-      for (int j = 0; j < NB; ++j) split3(xb[0][j], xb[1][j], bh[j], bm[j], bl[j]);
+      for (int j = 0; j < NB; ++j) {
+        if constexpr (BPL) {
+          bh[j] = __builtin_bit_cast(bf16x8, yb[0][j]);
+          bm[j] = __builtin_bit_cast(bf16x8, yb[1][j]);
+          bl[j] = __builtin_bit_cast(bf16x8, yb[2][j]);
+        } else {
+          split3(xb[0][BPL ? 0 : j], xb[1][BPL ? 0 : j], bh[j], bm[j], bl[j]);
+        }
+      }
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
         bf16x8 ah, am, al;
-        split3(xa[0][i], xa[1][i], ah, am, al);
+        if constexpr (APL) {
+          ah = __builtin_bit_cast(bf16x8, ya[0][i]);
+          am = __builtin_bit_cast(bf16x8, ya[1][i]);
+          al = __builtin_bit_cast(bf16x8, ya[2][i]);
+        } else {
+          split3(xa[0][APL ? 0 : i], xa[1][APL ? 0 : i], ah, am, al);
+        }
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
           if constexpr (PREC == 2) acc[i][j] = mfma_x6w(ah, am, al, bh[j], bm[j], bl[j], acc[i][j]);
@@ -346,7 +397,7 @@ __global__ void __launch_bounds__(256) gemm_ks_kernel(EvxGemmKs p) {
           for (int i = 0; i < NA; ++i)
 #pragma unroll
             for (int j = 0; j < NB; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32((&xa[h][i].x)[e], (&xb[h][j].x)[e], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32((&xa[h][APL ? 0 : i].x)[e], (&xb[h][BPL ? 0 : j].x)[e], acc[i][j], 0, 0, 0);
     }
   };
   // Loads are issued unconditionally (group index clamped to the wave's last group, so the
@@ -355,7 +406,7 @@ __global__ void __launch_bounds__(256) gemm_ks_kernel(EvxGemmKs p) {
   // (a conditional issue makes it wait for everything at the join).
   const int glast = max(g1 - 1, g0);
 #pragma unroll
-  for (int s = 0; s < D - 1; ++s) load_slot(fa[s], fb[s], fs[s], min(g0 + s, glast));
+  for (int s = 0; s < D - 1; ++s) load_slot(fa[s], fb[s], fs[s], pa[s], pb[s], min(g0 + s, glast));
   // chunks of D groups with no branch inside (load group g + s + D − 1, compute group g + s),
   // then the < D remaining groups, whose data the last chunk (or the prologue) loaded
   int g = g0;
@@ -364,33 +415,50 @@ __global__ void __launch_bounds__(256) gemm_ks_kernel(EvxGemmKs p) {
     for (int s = 0; s < D; ++s) {
 #ifndef EVX_KS_NO_LOADS  // probe: MFMA loop alone (operands of the prologue reused)
 #ifdef EVX_KS_FAKE_LOADS  // probe: every group re-reads group g0 (L1-resident operands)
-      load_slot(fa[(s + D - 1) % D], fb[(s + D - 1) % D], fs[(s + D - 1) % D], g0);
+      load_slot(fa[(s + D - 1) % D], fb[(s + D - 1) % D], fs[(s + D - 1) % D], pa[(s + D - 1) % D], pb[(s + D - 1) % D], g0);
 #else
-      load_slot(fa[(s + D - 1) % D], fb[(s + D - 1) % D], fs[(s + D - 1) % D], min(g + s + D - 1, glast));
+      load_slot(fa[(s + D - 1) % D], fb[(s + D - 1) % D], fs[(s + D - 1) % D], pa[(s + D - 1) % D], pb[(s + D - 1) % D],
+                min(g + s + D - 1, glast));
 #endif
 #endif
       // keep the issue order (loads of group g + s + D − 1 before the MFMAs of group g + s):
       // left alone, the scheduler sinks the loads behind the MFMAs and the prefetch distance
       // collapses to one group
       __builtin_amdgcn_sched_barrier(0);
-      compute_slot(fa[s], fb[s], fs[s]);
+      compute_slot(fa[s], fb[s], fs[s], pa[s], pb[s]);
       __builtin_amdgcn_sched_barrier(0);
     }
   }
 #pragma unroll
   for (int s = 0; s < D - 1; ++s)
-    if (g + s < g1) compute_slot(fa[s], fb[s], fs[s]);
-  if (w == 0 && K % KG) {  // tail (masked loads)
+    if (g + s < g1) compute_slot(fa[s], fb[s], fs[s], pa[s], pb[s]);
+  if (w == 0 && K % KG) {  // tail (masked loads; fragment planes are zero-padded to kp)
 #pragma unroll
     for (int h = 0; h < KH; ++h) {
       const int k = kof(ngf, h);
-      if (AKC && asub) fs[0][h] = load_tail<true>(asub, 0, k, K);
+      if (AKC && asub && !APL) fs[0][h] = load_tail<true>(asub, 0, k, K);
+      if constexpr (!APL) {
 #pragma unroll
-      for (int i = 0; i < NA; ++i) fa[0][h][i] = load_tail<AKC>(ap[i], lda, k, K);
+        for (int i = 0; i < NA; ++i) fa[0][h][i] = load_tail<AKC>(ap[i], lda, k, K);
+      }
+      if constexpr (!BPL) {
 #pragma unroll
-      for (int j = 0; j < NB; ++j) fb[0][h][j] = load_tail<BKC>(bp[j], ldb, k, K);
+        for (int j = 0; j < NB; ++j) fb[0][h][j] = load_tail<BKC>(bp[j], ldb, k, K);
+      }
     }
-    compute_slot(fa[0], fb[0], fs[0]);
+    if constexpr (APL) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int i = 0; i < NA; ++i) pa[0][c][i] = *reinterpret_cast<const uint4*>(apl[i] + c * a_plane + 32 * ngf);
+    }
+    if constexpr (BPL) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) pb[0][c][j] = *reinterpret_cast<const uint4*>(bpl[j] + c * b_plane + 32 * ngf);
+    }
+    compute_slot(fa[0], fb[0], fs[0], pa[0], pb[0]);
   }
 
   // ---- epilogue: sum the four K-partials through LDS, pairwise: waves 2, 3 park theirs,
@@ -603,15 +671,20 @@ void launch_prec(const EvxGemmKs& a, int tiles, hipStream_t s) {
 
 template <int TM, int TN, int MODE>
 void launch_layout(const EvxGemmKs& a, int tiles, hipStream_t s) {
-  if constexpr (TM * TN > 32) {  // 128 × 128: the 32x32 bf16x6 form only (256 accumulator registers)
-    launch_prec<TM, TN, MODE, 2>(a, tiles, s);
-    return;
+  {
+    if (a.a_pl || a.b_pl) {  // fragment planes: bf16x6 on 16x16x32, K-contiguous operands
+      const dim3 grid(tiles), block(256);
+      if (a.a_pl && a.b_pl) gemm_ks_kernel<TM, TN, 2, true, true, MODE, 1, 3><<<grid, block, 0, s>>>(a);
+      else if (a.a_pl) gemm_ks_kernel<TM, TN, 2, true, true, MODE, 1, 1><<<grid, block, 0, s>>>(a);
+      else gemm_ks_kernel<TM, TN, 2, true, true, MODE, 1, 2><<<grid, block, 0, s>>>(a);
+      return;
+    }
+    if constexpr (TM % 2 == 0 && TN % 2 == 0) {
+      if (g_ks_prec == 2) return launch_prec<TM, TN, MODE, 2>(a, tiles, s);
+    }
+    if (g_ks_prec >= 1) launch_prec<TM, TN, MODE, 1>(a, tiles, s);
+    else launch_prec<TM, TN, MODE, 0>(a, tiles, s);
   }
-  if constexpr (TM % 2 == 0 && TN % 2 == 0) {
-    if (g_ks_prec == 2) return launch_prec<TM, TN, MODE, 2>(a, tiles, s);
-  }
-  if (g_ks_prec >= 1) launch_prec<TM, TN, MODE, 1>(a, tiles, s);
-  else launch_prec<TM, TN, MODE, 0>(a, tiles, s);
 }
 
 template <int TM, int TN>
@@ -623,6 +696,67 @@ void launch_tile(EvxGemmKs a, hipStream_t s) {
   else launch_layout<TM, TN, 2>(a, a.tiles_m * (a.tiles_m + 1) / 2, s);
 }
 
+// fragment planes (see EvxGemmKs::a_pl): thread (row, group, q) splits the 8 values
+// k = 32·group + 16h + 4q + c (h = 0, 1; c = 0..3) and stores each part's 16 bytes
+__global__ void __launch_bounds__(256) split_planes_kernel(const float* __restrict__ X, int64_t ld, int64_t rows, int K,
+                                                           const float* __restrict__ colscale, uint16_t* __restrict__ out, int64_t kp) {
+  const int64_t ng = kp / 32, total = rows * ng * 4, plane = rows * kp;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int q = (int)(t & 3);
+    const int64_t rg = t >> 2, r = rg / ng, g = rg - r * ng;
+    float v[8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = (int)(32 * g) + 16 * h + 4 * q;
+      const float* x = X + r * ld + k;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const bool in = k + c < K;
+        float a = in ? x[c] : 0.f;
+        if (colscale && in) a *= colscale[k + c];
+        v[4 * h + c] = a;
+      }
+    }
+    bf16x8 hh, mm, ll;
+    split3(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), hh, mm, ll);
+    uint16_t* o = out + r * kp + 32 * g + 8 * q;
+    *reinterpret_cast<uint4*>(o) = __builtin_bit_cast(uint4, hh);
+    *reinterpret_cast<uint4*>(o + plane) = __builtin_bit_cast(uint4, mm);
+    *reinterpret_cast<uint4*>(o + 2 * plane) = __builtin_bit_cast(uint4, ll);
+  }
+}
+
+// the same planes of rows [row0, row0 + rows) of normal(key, (·, d)) (rng.hip's philox_fill
+// arithmetic: element e of the virtual matrix is word (e mod 4) of Philox block e / 4, Box–Muller
+// on word pairs), generated in place: the f32 noise matrix is never written
+__global__ void __launch_bounds__(256) philox_normal_planes_kernel(const int64_t* __restrict__ key, int64_t rows, int d, int64_t row0,
+                                                                   uint16_t* __restrict__ out, int64_t kp) {
+  uint32_t k0, k1;
+  evx::load_key(key, k0, k1);
+  const int64_t ng = kp / 32, total = rows * ng * 4, plane = rows * kp;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int q = (int)(t & 3);
+    const int64_t rg = t >> 2, r = rg / ng, g = rg - r * ng;
+    float4 v[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = (int)(32 * g) + 16 * h + 4 * q;
+      if (k < d) {  // d % 4 == 0: the four values are one Philox block
+        const int64_t e = (row0 + r) * (int64_t)d + k;
+        v[h] = evx::normal4(evx::philox_block((uint64_t)(e >> 2), k0, k1));
+      } else {
+        v[h] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+    bf16x8 hh, mm, ll;
+    split3(v[0], v[1], hh, mm, ll);
+    uint16_t* o = out + r * kp + 32 * g + 8 * q;
+    *reinterpret_cast<uint4*>(o) = __builtin_bit_cast(uint4, hh);
+    *reinterpret_cast<uint4*>(o + plane) = __builtin_bit_cast(uint4, mm);
+    *reinterpret_cast<uint4*>(o + 2 * plane) = __builtin_bit_cast(uint4, ll);
+  }
+}
+
 int g_ks_tile_override = 0;
 
 }  // namespace
@@ -630,6 +764,20 @@ int g_ks_tile_override = 0;
 void evx_gemm_ks_set_tile(int t) { g_ks_tile_override = t; }
 
 void evx_gemm_ks_set_prec(int prec) { g_ks_prec = prec; }
+
+void evx_split_planes(const float* X, int64_t ld, int64_t rows, int K, const float* colscale, uint16_t* out, int64_t kp, hipStream_t s) {
+  const int64_t total = rows * (kp / 32) * 4;
+  int g = (int)((total + 255) / 256);
+  if (g > 4096) g = 4096;
+  if (g > 0) split_planes_kernel<<<g, 256, 0, s>>>(X, ld, rows, K, colscale, out, kp);
+}
+
+void evx_philox_normal_planes(const int64_t* key, int64_t rows, int d, int64_t row0, uint16_t* out, int64_t kp, hipStream_t s) {
+  const int64_t total = rows * (kp / 32) * 4;
+  int g = (int)((total + 255) / 256);
+  if (g > 8192) g = 8192;
+  if (g > 0) philox_normal_planes_kernel<<<g, 256, 0, s>>>(key, rows, d, row0, out, kp);
+}
 
 int evx_gemm_ks_prec() { return g_ks_prec; }
 
@@ -645,7 +793,6 @@ void evx_gemm_ks(const EvxGemmKs& a, hipStream_t s) {
     case 2: launch_tile<2, 2>(a, s); break;
     case 3: launch_tile<3, 3>(a, s); break;
     case 8: launch_tile<8, 4>(a, s); break;  // tall products (M ≫ N), full mode only
-    case 9: launch_tile<8, 8>(a, s); break;  // 128 × 128 (bf16x6 on 32x32x16 only)
     default: launch_tile<4, 4>(a, s); break;
   }
 }

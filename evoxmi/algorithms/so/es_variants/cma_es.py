@@ -135,6 +135,19 @@ class CMAES(Algorithm):
     # ------------------------------------------------------------------ sampling
     def _sample(self, state, key, row0: int, rows: int):
         d = self.dim
+        if (state.B.is_cuda and config.get("gemm_planes") and config.get("gemm_prec") == "x6" and config.get("plain_gemm") == "evoxmi"
+                and d % 4 == 0):
+            # bf16x6 operands pre-split once per generation: the noise is generated straight into
+            # its fragment planes (the f32 noise matrix is never written) and B·diag(D) is split
+            # by one pass with D as the column scale — the sampling GEMM does no split work
+            from ....ops.linalg import mm_nt, normal_planes, split_planes
+
+            zp = normal_planes(key.to(state.B.device), rows, d, row0)
+            bdp = split_planes(state.B, colscale=state.D)
+            buf = state.population
+            out = buf if (rows == self.pop_size and torch.cuda.is_current_stream_capturing() and buf.is_contiguous()
+                          and buf.shape == (rows, d)) else None
+            return mm_nt(zp, bdp, alpha_ptr=state.sigma.reshape(1), bias_n=state.mean, out=out)
         z = rnd.normal(key, (rows, d), offset=row0 * d)
         if z.is_cuda:
             # X = mean + σ (Z∘D) Bᵀ = mean + Z (σ·B∘D)ᵀ : σ (a device scalar, no host sync)
