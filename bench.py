@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--simulate-rank", type=int, default=None,
                     help="time rank R's share of a --world N step on this one GPU (collectives replaced by same-size local ops)")
     ap.add_argument("--world", type=int, default=8, help="world size simulated by --simulate-rank")
+    ap.add_argument("--link-gbps", type=float, default=None, help="--simulate-rank wire model: GB/s per xGMI link and direction")
+    ap.add_argument("--latency-us", type=float, default=None, help="--simulate-rank wire model: latency per collective (µs)")
     ap.add_argument("--monitor", nargs="?", const="host", default=None, choices=["host", "device", "best"],
                     help="attach an EvalMonitor in the timed loop: full fitness history copied to the host "
                          "asynchronously (host), kept on the device (device), or best-so-far only (best)")
@@ -81,6 +83,10 @@ def main():
         from evoxmi.parallel.context import SimulatedDistContext
 
         sim_ctx = SimulatedDistContext(args.simulate_rank, args.world, algorithm=algo)
+        if args.link_gbps:
+            sim_ctx.wire.link_gbps = args.link_gbps
+        if args.latency_us is not None:
+            sim_ctx.wire.latency_us = args.latency_us
         state = wf.enable_distributed(state, context=sim_ctx)
 
     def sync():
@@ -98,11 +104,14 @@ def main():
     sync()
     eigh_mod.HISTORY.clear()
     dev_counts = sbr_device.snapshot_counts()  # device-mode solves: per-solve ring read after timing
+    if sim_ctx is not None:
+        sim_ctx.counters.reset()  # wire accounting of the timed generations only
     t0 = time.perf_counter()
     for _ in range(args.steps):
         state = wf.step(state)
     sync()
     elapsed = time.perf_counter() - t0
+    wire = sim_ctx.counters.summary(args.steps, sim_ctx.wire, args.world, graph=use_graph) if sim_ctx is not None else None
     # per-phase breakdown (outside the timed region): a few eager generations with
     # stream-ordered hipEvent timers; "tell" includes "eigh" (and "all_reduce" when sharded)
     hist = list(eigh_mod.HISTORY)  # decompositions of the timed generations only (host mode)
@@ -165,8 +174,10 @@ def main():
                 "rank": args.simulate_rank,
                 "world": args.world,
                 "rows_per_rank": -(-args.pop // args.world),
-                "collectives": "replaced by same-size local ops (wire time not included)",
-                "all_reduce_bytes_per_step": sim_ctx.bytes_all_reduce // max(1, args.steps + args.warmup + args.phase_steps),
+                "collectives": "replaced by same-size local ops; wire time modelled below (parallel/wire.py)",
+                "wire_model": sim_ctx.wire.describe(),
+                **{k: round(v, 4) for k, v in wire.items()},
+                "projected_ms_with_wire": round(ms + wire["wire_ms_per_gen"], 4),
             }
             if phases:
                 rep = phases.get("eigh", 0.0)

@@ -254,7 +254,7 @@ at::Tensor gemm_ks(const at::Tensor& A, int64_t a_kc, const at::Tensor& B, int64
 at::Tensor gemm_ks_pl(const c10::optional<at::Tensor>& A, const c10::optional<at::Tensor>& a_pl, const c10::optional<at::Tensor>& B,
                       const c10::optional<at::Tensor>& b_pl, int64_t M, int64_t N, int64_t K, double alpha,
                       const c10::optional<at::Tensor>& alpha_ptr, const c10::optional<at::Tensor>& bias_n,
-                      const c10::optional<at::Tensor>& out, const c10::optional<at::Tensor>& a_sub_k) {
+                      const c10::optional<at::Tensor>& out, const c10::optional<at::Tensor>& a_sub_k, int64_t sub_cols, int64_t sub_ld) {
   const bool ha = A.has_value() && A->defined(), hap = a_pl.has_value() && a_pl->defined();
   const bool hb = B.has_value() && B->defined(), hbp = b_pl.has_value() && b_pl->defined();
   TORCH_CHECK(ha != hap && hb != hbp, "gemm_ks_pl: give each operand as f32 or as planes");
@@ -314,6 +314,15 @@ at::Tensor gemm_ks_pl(const c10::optional<at::Tensor>& A, const c10::optional<at
     TORCH_CHECK(ha && a_sub_k->numel() >= K && reinterpret_cast<uintptr_t>(a_sub_k->data_ptr()) % 16 == 0,
                 "gemm_ks_pl: a_sub_k needs an f32 A (16-byte aligned, length ≥ K)");
     a.a_sub_k = a_sub_k->data_ptr<float>();
+    if (sub_cols > 0) {
+      int t = evx_gemm_ks_tile((int)M, (int)N, 0);
+      if (sub_cols % (t == 8 ? 64 : 16 * t)) t = a.force_tile = (M >= 2048 ? 8 : 4);  // 64-wide tiles
+      const int bn = t == 8 ? 64 : 16 * t;
+      TORCH_CHECK(sub_cols % bn == 0 && sub_ld % 4 == 0 && sub_ld >= K && a_sub_k->numel() >= ((N + sub_cols - 1) / sub_cols - 1) * sub_ld + K,
+                  "gemm_ks_pl: per-block shifts need sub_cols a multiple of the tile width (", bn, ") and one shift row per block");
+      a.sub_cols = (int)sub_cols;
+      a.sub_ld = sub_ld;
+    }
   }
   a.c_vec4 = vec4_ok(C) ? 1 : 0;
   evx_gemm_ks(a, cur_stream());
@@ -1387,7 +1396,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("sbr_dev_ctrl(Tensor part, int nparts, int j, int K, Tensor(a!) hist, Tensor(b!) alpha, Tensor(c!) theta, Tensor(d!) ctrl, Tensor(e!) st, float[] prm, int ns_iters, Tensor A, Tensor(f!) w_out, Tensor(g!) eig_stats, Tensor(h!) w_init, Tensor(i!) log, Tensor(j!) log_count) -> ()");
   m.def("gemm_ks_set_tile(int t) -> ()");
   m.def("gemm_ks_set_prec(int prec) -> ()");
-  m.def("gemm_ks_pl(Tensor? A, Tensor? a_pl, Tensor? B, Tensor? b_pl, int M, int N, int K, float alpha, Tensor? alpha_ptr, Tensor? bias_n, Tensor(a!)? out, Tensor? a_sub_k) -> Tensor");
+  m.def("gemm_ks_pl(Tensor? A, Tensor? a_pl, Tensor? B, Tensor? b_pl, int M, int N, int K, float alpha, Tensor? alpha_ptr, Tensor? bias_n, Tensor(a!)? out, Tensor? a_sub_k, int sub_cols=0, int sub_ld=0) -> Tensor");
   m.def("split_planes(Tensor X, Tensor? colscale) -> Tensor");
   m.def("philox_normal_planes(Tensor key, int rows, int d, int row0) -> Tensor");
   m.def("sbr16_far_bq_out(Tensor A, Tensor perm, Tensor Q, Tensor dq, Tensor stats, float thr_fac, Tensor theta, Tensor(a!) X, Tensor B, Tensor(b!) Bq, int sb, Tensor skip_far, Tensor skip_bq) -> ()");

@@ -73,6 +73,12 @@ struct EvxGemmKs {
   const uint16_t* a_pl;
   const uint16_t* b_pl;
   int64_t a_pl_rows, b_pl_rows, pl_kp;
+  // per-column-block A shift (stacked products sharing A, e.g. the CEC'22 composition
+  // rotations): output columns [c·sub_cols, (c+1)·sub_cols) use a_sub_k + c·sub_ld
+  // (sub_cols a multiple of the tile width; 0: one shift for all columns)
+  int sub_cols;
+  int64_t sub_ld;
+  int force_tile;  // tile code for this launch (0: the shape heuristic)
 };
 void evx_gemm_ks(const EvxGemmKs& a, hipStream_t s);
 // fragment planes of X (rows × K, K-contiguous, row stride ld), X[r][k]·colscale[k] when colscale

@@ -316,7 +316,7 @@ __global__ void __launch_bounds__(256) gemm_ks_kernel(EvxGemmKs p) {
   auto kof = [&](int grp, int h) { return PREC == 2 ? KG * grp + 8 * hw + 4 * h : KG * grp + 16 * h + 4 * q; };
   // fused A prologue A(m, k) − sub[k] (the CEC shift x − o): the shift float4 of a lane's k
   // values rides along with the operand loads, the subtraction runs just before the MFMAs
-  const float* __restrict__ asub = p.a_sub_k;
+  const float* __restrict__ asub = (p.a_sub_k && p.sub_cols > 0) ? p.a_sub_k + (int64_t)(n0 / p.sub_cols) * p.sub_ld : p.a_sub_k;
   float4 fs[D][KH];
   constexpr int NAF = APL ? 1 : NA, NBF = BPL ? 1 : NB;
   auto load_slot = [&](float4 (&xa)[KH][NAF], float4 (&xb)[KH][NBF], float4 (&xs)[KH], uint4 (&ya)[3][APL ? NA : 1],
@@ -789,7 +789,7 @@ int evx_gemm_ks_tiles_n(int M, int N, int mode) { return (int)evx_host::gemm_ks_
 
 void evx_gemm_ks(const EvxGemmKs& a, hipStream_t s) {
   if (a.M <= 0 || a.N <= 0) return;
-  switch (evx_gemm_ks_tile(a.M, a.N, a.mode)) {
+  switch (a.force_tile ? a.force_tile : evx_gemm_ks_tile(a.M, a.N, a.mode)) {
     case 2: launch_tile<2, 2>(a, s); break;
     case 3: launch_tile<3, 3>(a, s); break;
     case 8: launch_tile<8, 4>(a, s); break;  // tall products (M ≫ N), full mode only

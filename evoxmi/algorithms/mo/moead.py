@@ -344,6 +344,11 @@ class MOEAD(Algorithm):
             mo_ops.moead_halo_replace(obj, fitness, state.weight_vector, z, z_max, self._rev32[1], self._rev32[2], halo,
                                       self.func_name, win_h)
             table = ow["peer"].peer_table()
+            if getattr(dist, "backend", "") == "simulated":
+                # wire accounting of the simulated rank: halo winners generated on another rank are
+                # the rows a real rank reads over xGMI (device-side count, no host sync)
+                gen_rank = torch.bucketize(win_h.to(torch.int64), ow["starts"][1:].to(torch.int64), right=True)
+                dist.count_peer_rows(((win_h >= 0) & (gen_rank != dist.rank)).sum(), self.dim * 4)
             if table is None:
                 # no device IPC (single-process simulation, gloo): the offspring of every rank
                 # as one buffer, then the same gather (pointer table built on the device:

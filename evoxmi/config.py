@@ -50,6 +50,7 @@ KNOBS: Dict[str, Knob] = {
     "sbr_thr_fac": Knob("EVOXMI_SBR_THR_FAC", 0.3, float, "sbr: global far-pair threshold factor (gap > thr_fac·(block/2)·spread/n)"),
     "cma_fused": Knob("EVOXMI_CMA_FUSED", 1, int, "CMA-ES tell epilogue as the fused cmaes.hip kernels (0: reference-shaped torch ops)"),
     "sbr_fused_damping": Knob("EVOXMI_SBR_FUSED_DAMPING", 0, int, "device-controlled eigensolver: the step-size damping (3 power steps + final) as one grid-barrier launch (1) or four launches (0, default: the grid barriers' agent-scope fences cost more than the three launch boundaries they remove — 1.939 vs 1.888 ms/gen, profiles/NOTES.md)"),
+    "cec_stack": Knob("EVOXMI_CEC_STACK", 1, int, "CEC'22 compositions (F9–F12) on the device: every rotated component from ONE GEMM over the stacked rotations with per-block exact shifts (1) or one GEMM per component (0)"),
     "cec_fused": Knob("EVOXMI_CEC_FUSED", 0, int, "CEC'22 F1 / F4 on the device: 1 = row terms from the rotation GEMM's epilogue (rotated population never written), 0 = GEMM + basic-function kernel (default: the fused epilogue measured 7 µs slower at pop 10 000 × d 1000, profiles/r3_cec_fused_epilogue.txt)"),
     "gemm_prec": Knob("EVOXMI_GEMM_PREC", "x6", str, "framework f32 GEMMs (gemm_ks.hip): 'x6' — each f32 operand split exactly into three bf16 parts, six bf16 MFMA products (f32-accurate, 3/8 of the f32 MFMA time) — or 'f32' (v_mfma_f32_16x16x4_f32)"),
     "gemm_planes": Knob("EVOXMI_GEMM_PLANES", 0, int, "x6 GEMMs: operands that are constant (CEC rotations) or produced once per generation (CMA-ES noise, B·D) pre-split into bf16 fragment planes (1) instead of split inside the GEMM (0, default: the 3 × 16-byte plane loads cost more than the split arithmetic they remove — sampling GEMM 224 vs 173 µs, 1.852 vs 1.799 ms/gen, profiles/NOTES.md)"),

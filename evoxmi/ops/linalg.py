@@ -251,9 +251,22 @@ def normal_planes(key: torch.Tensor, rows: int, d: int, row0: int = 0) -> Planes
 
 
 def mm_nt(A, B, *, alpha: float = 1.0, alpha_ptr: Optional[torch.Tensor] = None, bias_n: Optional[torch.Tensor] = None,
-          out: Optional[torch.Tensor] = None, a_sub_k: Optional[torch.Tensor] = None) -> torch.Tensor:
+          out: Optional[torch.Tensor] = None, a_sub_k: Optional[torch.Tensor] = None, sub_cols: int = 0) -> torch.Tensor:
     """``alpha·(*alpha_ptr)·(A − a_sub_k)·Bᵀ (+ bias_n)`` where A (M × K) and B (N × K) are f32
-    tensors or :class:`Planes` (bf16x6 fragment planes: no split work for that operand)."""
+    tensors or :class:`Planes` (bf16x6 fragment planes: no split work for that operand).
+
+    ``sub_cols > 0``: ``a_sub_k`` is a (blocks, K) matrix and output columns
+    [c·sub_cols, (c+1)·sub_cols) use shift row c — several shifted products that share A (the
+    CEC'22 composition rotations) in ONE launch that reads A's row panels once per tile."""
+    if sub_cols:
+        if not A.is_cuda:
+            blocks = [((A - a_sub_k[c][None, :]) @ B[c * sub_cols : (c + 1) * sub_cols].T) for c in range(a_sub_k.shape[0])]
+            C = alpha * torch.cat(blocks, 1)[:, : B.shape[0]]
+            return C if alpha_ptr is None else C * alpha_ptr.reshape(())
+        N = B.rows if isinstance(B, Planes) else B.shape[0]
+        bp, bf = (B.t, None) if isinstance(B, Planes) else (None, B)
+        return _ext.ops().gemm_ks_pl(A, None, bf, bp, int(A.shape[0]), int(N), int(A.shape[1]), float(alpha), alpha_ptr, bias_n, out,
+                                     a_sub_k.contiguous(), int(sub_cols), int(a_sub_k.stride(0)))
     if not isinstance(A, Planes) and not isinstance(B, Planes):
         return mm(A, B, tb=True, alpha=alpha, alpha_ptr=alpha_ptr, bias_n=bias_n, out=out, a_sub_k=a_sub_k)
     M = A.rows if isinstance(A, Planes) else A.shape[0]

@@ -163,8 +163,53 @@ class SimulatedDistContext(DistContext):
         self.backend = "simulated"
         self.algorithm_sharded = algorithm is not None and hasattr(algorithm, "ask_sharded") and hasattr(algorithm, "tell_sharded")
         self.global_pop = None
-        self.bytes_all_gather = 0
-        self.bytes_all_reduce = 0
+        from .wire import WireCounters, WireModel
+
+        self.wire = WireModel()
+        self.counters = WireCounters()
+
+    @property
+    def bytes_all_reduce(self):
+        return self.counters.all_reduce_bytes
+
+    @property
+    def bytes_all_gather(self):
+        return self.counters.all_gather_bytes
+
+    def _count(self, kind: str, nbytes: int):
+        c = self.counters
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            # a graph capture: these calls repeat on every replay without running Python again
+            from .wire import WireCounters
+
+            if c.captured is None or not getattr(c, "_capturing", False):
+                c.captured = WireCounters()
+                c._capturing = True
+            c = c.captured
+        else:
+            c._capturing = False
+        if kind == "all_reduce":
+            c.all_reduce_calls += 1
+            c.all_reduce_bytes += nbytes
+            c.wire_us += self.wire.all_reduce_us(nbytes, self.world_size)
+        else:
+            c.all_gather_calls += 1
+            c.all_gather_bytes += nbytes
+            c.wire_us += self.wire.all_gather_us(nbytes, self.world_size)
+
+    def count_peer_rows(self, rows: torch.Tensor, row_bytes: int):
+        """A peer row gather of ``rows`` (device scalar: rows that a real rank would read from
+        other ranks' buffers) — accumulated on the device, read once after timing."""
+        c = self.counters
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing() and c.captured is not None:
+            c.captured.peer_gathers += 1
+        else:
+            c.peer_gathers += 1
+        c.row_bytes = int(row_bytes)
+        r = rows.to(torch.float64).reshape(())
+        if c.peer_rows is None:
+            c.peer_rows = torch.zeros((), dtype=torch.float64, device=r.device)
+        c.peer_rows.add_(r)
 
     def all_gather_rows(self, local: torch.Tensor, n_total: Optional[int]) -> torch.Tensor:
         counts = [s for _, s in balanced_slices(n_total, self.world_size)] if n_total is not None else [local.shape[0]] * self.world_size
@@ -174,16 +219,17 @@ class SimulatedDistContext(DistContext):
             pad = torch.zeros((mx - local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
             local = torch.cat([local, pad], 0)
         out = local.repeat((self.world_size,) + (1,) * (local.dim() - 1))
-        self.bytes_all_gather += out.numel() * out.element_size()
+        self._count("all_gather", out.numel() * out.element_size())
         if all(c == mx for c in counts):
             return out
         return torch.cat([out[i * mx : i * mx + c] for i, c in enumerate(counts)], 0)
 
     def all_reduce_(self, t: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
-        self.bytes_all_reduce += t.numel() * t.element_size()
+        self._count("all_reduce", t.numel() * t.element_size())
         return t.mul_(1) if t.is_floating_point() else t
 
     def all_reduce_min_loc(self, value: torch.Tensor, index: torch.Tensor):
+        self._count("all_reduce", 8)  # one packed u64 MINLOC
         return value.reshape(()), index.reshape(())
 
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:

@@ -78,6 +78,8 @@ class PeerBuffer:
         """All ranks have finished reading every peer buffer (before the owners rewrite them)."""
         if self.ipc:
             self.ctx.all_reduce_(self._one)
+        elif getattr(self.ctx, "backend", "") == "simulated":
+            self.ctx._count("all_reduce", 4)  # the real run's one-float fence (wire accounting)
 
     def close(self):
         for p in self._opened:

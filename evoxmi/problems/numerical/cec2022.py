@@ -474,14 +474,46 @@ class _Composition(_CEC2022):
     parts = ()
     threshold = 1e-8
 
+    STACK = 1024  # column block of one component in the stacked rotation GEMM (multiple of every tile width)
+
+    def _stacked(self, X, c):
+        """Every rotated component's M_c·(x − o_c) from ONE GEMM over the stacked rotations
+        (output column block c·STACK uses shift row c: the shift stays exact, applied to the
+        operand before the products as in the reference ``cec2022_so.py:109-119,121-135``).
+        None when the device path does not apply."""
+        from ... import config
+
+        D = X.shape[1]
+        if not X.is_cuda or not config.get("cec_stack") or D % 4 or D > self.STACK or config.get("plain_gemm") != "evoxmi":
+            return None
+        key = ("stack", D, str(X.device))
+        st = self._cache.get(key)
+        if st is None:
+            # one block per distinct (shift, rotation) component — F12's last two parts share one
+            comps = sorted({comp for fid, comp, scale, rotate in self.parts if rotate})
+            Ms = torch.zeros(len(comps) * self.STACK, D, device=X.device)
+            Osh = torch.zeros(len(comps), D, device=X.device)
+            for j, comp in enumerate(comps):
+                Ms[j * self.STACK : j * self.STACK + D] = c["M"][comp * D : (comp + 1) * D]
+                Osh[j] = c["Os"][comp, :D]
+            slot = {i: comps.index(comp) for i, (fid, comp, scale, rotate) in enumerate(self.parts) if rotate}
+            st = self._cache[key] = (Ms, Osh, slot)
+        Ms, Osh, slot = st
+        Z = linalg.mm_nt(X, Ms, a_sub_k=Osh, sub_cols=self.STACK)
+        return Z, slot
+
     def _evaluate(self, X, c):
         D = X.shape[1]
         Os = c["Os"][:, :D]
         M = c["M"]
         fs = []
-        for fid, comp, scale, rotate in self.parts:
+        stacked = self._stacked(X, c)
+        for i, (fid, comp, scale, rotate) in enumerate(self.parts):
             o = Os[comp]
-            if rotate:
+            if rotate and stacked is not None:
+                Z, slot = stacked
+                fs.append(self._basic(Z, fid, start=slot[i] * self.STACK, length=D, scale=scale))
+            elif rotate:
                 Z = self._ssr(X, o, M[comp * D : (comp + 1) * D], scale)
                 fs.append(self._basic(Z, fid))
             else:

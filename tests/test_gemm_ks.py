@@ -204,3 +204,39 @@ def test_gemm_planes_matches_fp64(M, N, K, which):
         Z = linalg.mm_nt(Ad, b, a_sub_k=o.cuda()).cpu().double()
         ref = (A.double() - o.double()) @ B.double().t()
         assert ((Z - ref).abs() <= 2e-6 * ((A - o).double().abs() @ B.double().abs().t()) + 1e-30).all()
+
+
+@pytest.mark.gpu
+def test_gemm_per_block_shifts():
+    """Stacked shifted products in one launch: column block c uses shift row c (exact zero when
+    a row equals its block's shift)."""
+    g = torch.Generator().manual_seed(9)
+    M, K, blocks, W = 3000, 1000, 3, 1024
+    X = torch.randn(M, K, generator=g)
+    Bs = torch.randn(blocks * W, K, generator=g)
+    O = torch.randn(blocks, K, generator=g)
+    X[5] = O[1]
+    Z = linalg.mm_nt(X.cuda(), Bs.cuda(), a_sub_k=O.cuda(), sub_cols=W).cpu().double()
+    for c in range(blocks):
+        ref = (X.double() - O[c].double()) @ Bs[c * W : (c + 1) * W].double().t()
+        tol = 2e-6 * ((X - O[c]).double().abs() @ Bs[c * W : (c + 1) * W].double().abs().t())
+        assert ((Z[:, c * W : (c + 1) * W] - ref).abs() <= tol + 1e-30).all(), c
+    assert bool((Z[5, W : 2 * W] == 0).all())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("f", [9, 10, 11, 12])
+def test_cec2022_composition_stacked_gemm_matches_per_component(f):
+    """F9–F12 at the synthetic d = 1000: the one-GEMM stacked rotations give the per-component
+    GEMM result (and the CPU fp32 evaluation)."""
+    from evoxmi.problems.numerical import CEC2022TestSuit
+
+    p = CEC2022TestSuit.create(f)
+    X = torch.rand(300, 1000, generator=torch.Generator().manual_seed(f)) * 200 - 100
+    with config.override(cec_stack=1):
+        a, _ = p.evaluate(None, X.cuda())
+    with config.override(cec_stack=0):
+        b, _ = p.evaluate(None, X.cuda())
+    ref, _ = p.evaluate(None, X)
+    assert torch.allclose(a.cpu(), b.cpu(), rtol=1e-5, atol=1e-4)
+    assert torch.allclose(a.cpu(), ref, rtol=2e-3, atol=1e-3)

@@ -58,6 +58,7 @@ def main():
                     help="time rank R's share of a --world N sharded step on this one GPU (collectives → same-size local ops)")
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--shard", choices=["auto", "owner", "replica"], default="auto", help="MOEA/D sharded mode")
+    ap.add_argument("--link-gbps", type=float, default=None, help="--simulate-rank wire model: GB/s per xGMI link and direction")
     args = ap.parse_args()
     import torch.distributed as dist
     from evoxmi.parallel import init_distributed
@@ -87,10 +88,15 @@ def main():
     if sim:
         from evoxmi.parallel.context import SimulatedDistContext
 
-        st = wf.enable_distributed(st, context=SimulatedDistContext(args.simulate_rank, args.world, algorithm=algo))
+        sim_ctx = SimulatedDistContext(args.simulate_rank, args.world, algorithm=algo)
+        if args.link_gbps:
+            sim_ctx.wire.link_gbps = args.link_gbps
+        st = wf.enable_distributed(st, context=sim_ctx)
     for _ in range(1 + args.warmup):
         st = wf.step(st)
     sync()
+    if sim:
+        sim_ctx.counters.reset()
     t = time.perf_counter()
     for _ in range(args.gens):
         st = wf.step(st)
@@ -108,6 +114,11 @@ def main():
         "ms_per_gen": round(dt * 1e3, 3), "gens_per_sec": round(1 / dt, 2), "evals_per_sec": round(pop / dt, 1),
         "fitness_finite": bool(torch.isfinite(fit).all()), "mean_obj": [round(float(v), 4) for v in fit.mean(0)],
     }
+    if sim:
+        w = sim_ctx.counters.summary(args.gens, sim_ctx.wire, args.world, graph=not (args.no_graph or args.cpu))
+        out["wire_model"] = sim_ctx.wire.describe()
+        out.update({k: round(v, 4) for k, v in w.items()})
+        out["projected_ms_with_wire"] = round(dt * 1e3 + w["wire_ms_per_gen"], 4)
     if args.algo == "moead":
         from evoxmi.algorithms.mo.moead import cross_shard_winner_fraction
 
