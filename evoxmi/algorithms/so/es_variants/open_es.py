@@ -20,6 +20,7 @@ import torch
 from ....core import Algorithm, State, use_state
 from ....ops import _ext
 from ....ops import random as rnd
+from ....parallel.dim_sharded import ColumnSeparable
 from ._common import make_optimizer
 
 
@@ -44,8 +45,14 @@ def _noise_grad(key, w, d: int, row0: int, dev):
     return _normal_rows(key, w.shape[0], d, row0, dev).T @ w.to(torch.float32)
 
 
-class OpenES(Algorithm):
+class OpenES(ColumnSeparable, Algorithm):
     rank_local_fields = ("population",)
+    # decision-axis state sharding (StdWorkflow.enable_multi_devices(shard_state=True)): the
+    # centre, the population and an element-wise optimiser's state are column blocks; every
+    # rank regenerates its columns of the (virtual) Philox noise and reduces εᵀf over them
+    column_separable = True
+    dim_fields = ("population", "center")
+    dim_child_fields = {"optimizer": ("opt_state",)}
 
     def __init__(self, center_init, pop_size, learning_rate, noise_stdev, optimizer=None, mirrored_sampling=True):
         super().__init__()
@@ -59,15 +66,26 @@ class OpenES(Algorithm):
         self.noise_stdev = noise_stdev
         self.mirrored_sampling = mirrored_sampling
         self.optimizer = make_optimizer(optimizer, learning_rate, center_init) if optimizer == "adam" else None
+        self._opt_name = optimizer
 
     def setup(self, key):
         pop = self.center_init.expand(self.pop_size, -1).clone()
         return State(population=pop, center=self.center_init.clone(), noise_key=key.clone(), key=key)
 
+    def dim_shard(self, state, col0: int, own: int):
+        if self.optimizer is not None and getattr(self, "_opt_name", "adam") not in ("adam", "sgd"):
+            raise ValueError("OpenES column sharding needs an element-wise optimiser (none, 'sgd' or 'adam')")
+        if self.optimizer is None:
+            self.dim_child_fields = {}
+        return super().dim_shard(state, col0, own)
+
     def ask(self, state):
         key, noise_key = rnd.split(state.key)
         dev = state.center.device
-        population = state.center[None, :] + self.noise_stdev * self._noise_rows(noise_key, 0, self.pop_size, dev)
+        noise = self._noise_rows(noise_key, 0, self.pop_size, dev)
+        if self._cols is not None:  # column block of a decision-axis-sharded state
+            noise = self.col_vec(noise)
+        population = state.center[None, :] + self.noise_stdev * noise
         return population, state.update(population=population, key=key, noise_key=noise_key.to(state.noise_key.device))
 
     def _grad_rows(self, noise_key, fitness, start: int, size: int, dev):
@@ -91,6 +109,8 @@ class OpenES(Algorithm):
 
     def tell(self, state, fitness):
         grad = self._grad_rows(state.noise_key, fitness, 0, self.pop_size, state.center.device) / self.pop_size / self.noise_stdev
+        if self._cols is not None:
+            grad = self.col_vec(grad).contiguous()
         if self.optimizer is None:
             center = state.center - self.learning_rate * grad
         else:

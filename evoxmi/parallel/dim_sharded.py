@@ -24,49 +24,89 @@ from .context import balanced_slices
 
 
 def supports_dim_sharding(problem) -> bool:
+    """The problem returns per-rank partial terms (``partial_terms`` / ``combine_terms`` /
+    ``dim_halo``).  Problems without them are still evaluated under decision-axis sharding,
+    by the generic column all-gather (:func:`dim_sharded_fitness_local`)."""
     return all(hasattr(problem, a) for a in ("partial_terms", "combine_terms", "dim_halo"))
 
 
-def dim_sharded_fitness(problem, X: torch.Tensor, group=None) -> torch.Tensor:
-    """Fitness of the replicated population ``X`` with the column work split over
-    the ranks of ``group`` (whole evaluation when no process group exists)."""
+def _world(group):
     if dist.is_available() and dist.is_initialized():
-        rank, world = dist.get_rank(group), dist.get_world_size(group)
-    else:
-        rank, world = 0, 1
-    d = X.shape[1]
-    col0, own = balanced_slices(d, world)[rank]
-    hi = min(col0 + own + problem.dim_halo, d)
-    # shifted-rotated problems shard the rotated coordinates: they take the full rows
-    Xb = X if getattr(problem, "dim_shard_full_rows", False) else X[:, col0:hi]
-    T = problem.partial_terms(Xb, col0, d, own)
+        return dist.get_rank(group), dist.get_world_size(group)
+    return 0, 1
+
+
+def _gather_cols(block: torch.Tensor, d: int, group) -> torch.Tensor:
+    """All-gather per-rank column blocks (balanced slices of ``d``; trailing dims on the
+    last axis) into the full (…, d) matrix on every rank."""
+    rank, world = _world(group)
+    if world == 1:
+        return block
+    sl = balanced_slices(d, world)
+    w = max(o for _, o in sl)
+    pad = block.new_zeros(*block.shape[:-1], w)
+    pad[..., : block.shape[-1]] = block
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad.contiguous(), group=group)
+    return torch.cat([p[..., :o] for p, (_, o) in zip(parts, sl)], -1)
+
+
+def _reduce_terms(T, d: int, group):
+    """The collective of one partial-terms result.  ``T`` is a tensor (SUM-reduced), a
+    ``(sum, max)`` tuple, or a dict with any of ``"sum"`` / ``"max"`` (reduced) and ``"cat"``
+    (a (…, own) block or a list of them, all-gathered along the decision axis — for
+    functions whose value needs every coordinate of a sharded intermediate, e.g. the rotated
+    z of the CEC'22 hybrids; GSPMD inserts the same all-gather)."""
+    _, world = _world(group)
+    if isinstance(T, dict):
+        out = {}
+        for k, op in (("sum", dist.ReduceOp.SUM), ("max", dist.ReduceOp.MAX)):
+            if k in T:
+                v = T[k].contiguous()
+                if world > 1:
+                    dist.all_reduce(v, op=op, group=group)
+                out[k] = v
+        if "cat" in T:
+            c = T["cat"]
+            out["cat"] = [_gather_cols(x, d, group) for x in c] if isinstance(c, (list, tuple)) else _gather_cols(c, d, group)
+        return out
     if isinstance(T, tuple):  # (sum terms, max terms), e.g. LSMOP's Schwefel groups
         Ts, Tm = T[0].contiguous(), T[1].contiguous()
         if world > 1:
             dist.all_reduce(Ts, op=dist.ReduceOp.SUM, group=group)
             dist.all_reduce(Tm, op=dist.ReduceOp.MAX, group=group)
-        return problem.combine_terms((Ts, Tm), d)
+        return (Ts, Tm)
     T = T.contiguous()
     if world > 1:
         dist.all_reduce(T, op=dist.ReduceOp.SUM, group=group)
-    return problem.combine_terms(T, d)
+    return T
+
+
+def dim_sharded_fitness(problem, X: torch.Tensor, group=None) -> torch.Tensor:
+    """Fitness of the replicated population ``X`` with the column work split over
+    the ranks of ``group`` (whole evaluation when no process group exists, or when the
+    problem has no partial terms: the rows are replicated, so it evaluates them itself)."""
+    if not supports_dim_sharding(problem):
+        return problem.evaluate(None, X)[0]
+    rank, world = _world(group)
+    d = X.shape[1]
+    col0, own = balanced_slices(d, world)[rank]
+    hi = min(col0 + own + problem.dim_halo, d)
+    # shifted-rotated problems shard the rotated coordinates: they take the full rows
+    Xb = X if getattr(problem, "dim_shard_full_rows", False) else X[:, col0:hi]
+    return problem.combine_terms(_reduce_terms(problem.partial_terms(Xb, col0, d, own), d, group), d)
 
 
 def dim_sharded_fitness_local(problem, Xloc: torch.Tensor, col0: int, d: int, group=None) -> torch.Tensor:
     """Fitness when the population itself is column-sharded (``Xloc`` = this rank's columns
-    [col0, col0 + own) of every row; problems with ``dim_halo == 0`` that take column blocks)."""
+    [col0, col0 + own) of every row).  Problems whose partial terms need no halo and no full
+    rows reduce their terms; every other problem is evaluated on the all-gathered rows (the
+    generic rule: the state stays column-sharded, the evaluation replicated)."""
     own = Xloc.shape[1]
-    T = problem.partial_terms(Xloc, col0, d, own)
-    if isinstance(T, tuple):
-        Ts, Tm = T[0].contiguous(), T[1].contiguous()
-        if dist.is_available() and dist.is_initialized():
-            dist.all_reduce(Ts, op=dist.ReduceOp.SUM, group=group)
-            dist.all_reduce(Tm, op=dist.ReduceOp.MAX, group=group)
-        return problem.combine_terms((Ts, Tm), d)
-    T = T.contiguous()
-    if dist.is_available() and dist.is_initialized():
-        dist.all_reduce(T, op=dist.ReduceOp.SUM, group=group)
-    return problem.combine_terms(T, d)
+    if supports_dim_sharding(problem) and getattr(problem, "dim_halo", 1) == 0 and not getattr(problem, "dim_shard_full_rows", False):
+        return problem.combine_terms(_reduce_terms(problem.partial_terms(Xloc, col0, d, own), d, group), d)
+    X = _gather_cols(Xloc, d, group)
+    return dim_sharded_fitness(problem, X, group)
 
 
 def algorithm_column_separable(algorithm) -> bool:
@@ -93,11 +133,28 @@ class ColumnSeparable:
     reproduces the single-process run."""
 
     dim_fields: tuple = ()
+    # child-module state fields with a trailing decision axis (tensors, or tuples of them such
+    # as an optimiser's (t, m, v): elements whose last dimension is d are sliced)
+    dim_child_fields: dict = {}
     _cols = None
 
+    @staticmethod
+    def _map_d(x, d, fn):
+        if isinstance(x, (tuple, list)):
+            return type(x)(ColumnSeparable._map_d(v, d, fn) for v in x)
+        if torch.is_tensor(x) and x.dim() >= 1 and x.shape[-1] == d:
+            return fn(x)
+        return x
+
     def dim_shard(self, state, col0: int, own: int):
-        self._cols = (int(col0), int(own), int(self.dim))
-        return state.update(**{f: state[f][..., col0 : col0 + own].contiguous() for f in self.dim_fields})
+        d = int(self.dim)
+        self._cols = (int(col0), int(own), d)
+        state = state.update(**{f: state[f][..., col0 : col0 + own].contiguous() for f in self.dim_fields})
+        for child, fields in self.dim_child_fields.items():
+            cs = state.get_child_state(child)
+            cs = cs.update(**{f: self._map_d(cs[f], d, lambda x: x[..., col0 : col0 + own].contiguous()) for f in fields})
+            state = state.update_child(child, cs)
+        return state
 
     def cols(self):
         """(first column, columns owned, total columns) of this rank's block."""
@@ -113,34 +170,26 @@ class ColumnSeparable:
         (one all-gather per field; for checkpoints, monitors and final results)."""
         if self._cols is None or not (dist.is_available() and dist.is_initialized()):
             return state
-        world = dist.get_world_size(group)
         d = self._cols[2]
-        sl = balanced_slices(d, world)
-        w = max(o for _, o in sl)
-        upd = {}
-        for f in self.dim_fields:
-            x = state[f]
-            pad = torch.zeros(*x.shape[:-1], w, dtype=x.dtype, device=x.device)
-            pad[..., : x.shape[-1]] = x
-            parts = [torch.empty_like(pad) for _ in range(world)]
-            dist.all_gather(parts, pad, group=group)
-            upd[f] = torch.cat([p[..., :o] for p, (_, o) in zip(parts, sl)], -1)
-        return state.update(**upd)
+        own = self._cols[1]
+        state = state.update(**{f: _gather_cols(state[f], d, group) for f in self.dim_fields})
+        for child, fields in self.dim_child_fields.items():
+            cs = state.get_child_state(child)
+            cs = cs.update(**{f: self._map_d(cs[f], own, lambda x: _gather_cols(x, d, group)) for f in fields})
+            state = state.update_child(child, cs)
+        return state
 
 
 def supports_state_sharding(algorithm, problem) -> bool:
-    """Full P2 (state and evaluation column-sharded): the algorithm can slice its state into
-    column blocks and the problem's terms need no halo and no full rows."""
-    return (algorithm_column_separable(algorithm) and supports_dim_sharding(problem) and getattr(problem, "dim_halo", 1) == 0
-            and not getattr(problem, "dim_shard_full_rows", False))
+    """Full P2 (state column-sharded): the algorithm can slice its state into column blocks.
+    Any problem then works — halo-free partial terms reduce per-row terms, every other problem
+    sees the all-gathered rows (:func:`dim_sharded_fitness_local`)."""
+    return algorithm_column_separable(algorithm)
 
 
 class DimShardedProblem(Problem):
     def __init__(self, problem: Problem, group=None):
         super().__init__()
-        if not supports_dim_sharding(problem):
-            raise TypeError(f"{type(problem).__name__} does not implement the dim-sharding protocol "
-                            "(partial_terms / combine_terms / dim_halo)")
         self.problem = problem
         self.group = group
 

@@ -248,10 +248,11 @@ class _CEC2022(Problem):
     def _clamp(f, thr=1e-8):
         return torch.where(f < thr, torch.zeros_like(f), f)
 
-    def _compose(self, X, fs, Os, bias, sigma, lamb):
+    def _compose(self, X, fs, Os, bias, sigma, lamb, d2=None):
         N, D = X.shape
         n = fs.shape[1]
-        d2 = torch.stack([self._basic(X, SPHERE, sub=Os[i]) for i in range(n)], 1)
+        if d2 is None:
+            d2 = torch.stack([self._basic(X, SPHERE, sub=Os[i]) for i in range(n)], 1)
         t1 = 1 / torch.sqrt(d2)
         t2 = torch.exp(-0.5 * d2 / (self._const_vec(sigma, X) ** 2 * D))
         W = t1 * t2
@@ -425,13 +426,29 @@ class F5_CEC2022(_RowSharded, _CEC2022):
         return self._clamp(T[:, 0])
 
 
-class _Hybrid(_CEC2022):
+class _Hybrid(_RowSharded, _CEC2022):
+    """Hybrid functions: z = M(x − o), shuffled, cut into groups with different basic
+    functions (reference ``cec2022_so.py:545-608``).  Decision-axis sharding: a rank rotates
+    its block of z (rows of M); the blocks are all-gathered (``"cat"`` terms) because the
+    shuffle mixes every coordinate into the groups."""
+
     p = ()
     funcs = ()
 
+    def partial_terms(self, X, col0, d, own):
+        return {"cat": self._zblock(X, col0, d, own)}
+
+    def combine_terms(self, T, d):
+        Z = T["cat"]
+        return self._from_z(Z, self._consts(d, Z.device))
+
     def _evaluate(self, X, c):
         D = X.shape[1]
-        Z = self._ssr(X, c["Os"][:D], c["M"], 1.0)
+        return self._from_z(self._ssr(X, c["Os"][:D], c["M"], 1.0), c)
+
+    def _from_z(self, Z, c):
+        D = Z.shape[1]
+        X = Z
         perm = c["S"] if c["S"] is not None else torch.arange(D, dtype=torch.int32, device=X.device)
         groups = _group_ids(self.p, D)
         f = 0
@@ -467,12 +484,42 @@ class F8_CEC2022(_Hybrid):
 
 
 class _Composition(_CEC2022):
+    """Composition functions (reference ``cec2022_so.py:121-135,610-738``).  Decision-axis
+    sharding: a rank computes its block of every component's rotated z (rows of each M_c) and
+    its columns' share of every ‖x − o_c‖² (additive ``"sum"`` terms); the z blocks are
+    all-gathered (``"cat"``) and every rank finishes the weighted composition."""
+
     bias = ()
     lamb = ()
     sigma = ()
     # (fid, component index of shift/rotation, scale, rotate?)
     parts = ()
     threshold = 1e-8
+    dim_shard_full_rows = True
+    dim_halo = 0
+
+    def partial_terms(self, X, col0, d, own):
+        X = X.to(torch.float32).contiguous()
+        c = self._consts(d, X.device)
+        Os, M = c["Os"][:, :d], c["M"]
+        cols = slice(col0, col0 + own)
+        blocks = []
+        for fid, comp, scale, rotate in self.parts:
+            o = Os[comp]
+            if rotate:
+                blocks.append(self._ssr(X, o, M[comp * d + col0 : comp * d + col0 + own].contiguous(), scale))
+            else:
+                blocks.append((X[:, cols] - o[cols]).contiguous())
+        d2 = torch.stack([((X[:, cols] - Os[i, cols]) ** 2).sum(1) for i in range(len(self.parts))], 1)
+        return {"cat": blocks, "sum": d2}
+
+    def combine_terms(self, T, d):
+        Zs = T["cat"]
+        c = self._consts(d, Zs[0].device)
+        Os = c["Os"][:, :d]
+        fs = torch.stack([self._basic(z, fid) for (fid, comp, scale, rotate), z in zip(self.parts, Zs)], 1)
+        f = self._compose(Zs[0], fs, Os[: len(self.parts)], self.bias, self.sigma, self.lamb, d2=T["sum"])
+        return self._clamp(f, self._thr(d))
 
     STACK = 1024  # column block of one component in the stacked rotation GEMM (multiple of every tile width)
 

@@ -447,41 +447,39 @@ class StdWorkflow(Workflow):
 
         ``shard_state=True`` shards the algorithm state too, as GSPMD does for every (pop, dim)
         array: column-separable algorithms (:class:`evoxmi.parallel.ColumnSeparable` — PSO, DE,
-        ODE, …) keep only their column block of every ``dim_fields`` array on each rank, and
-        problems without a halo evaluate that block — the only traffic is the (N, k) term
-        all-reduce.  The state then holds column blocks: :meth:`gather_state` reassembles the
+        ODE, …) keep only their column block of every ``dim_fields`` array on each rank; problems
+        with halo-free terms evaluate that block (the only traffic is the (N, k) term all-reduce),
+        every other problem evaluates the all-gathered rows (GSPMD's all-gather of a sharded
+        operand).  The state then holds column blocks: :meth:`gather_state` reassembles the
         full arrays (the reference's sharded arrays stay logically global).  Default ``False``:
         a state read after the run has the reference's full shapes."""
         if not self.jit_problem:
             raise ValueError("multi-devices with non jit problem isn't currently supported")
         if not (torch.distributed.is_available() and torch.distributed.is_initialized()):
             return state
-        from ..parallel.dim_sharded import supports_dim_sharding
+        from ..parallel.context import DistContext, balanced_slices
+        from ..parallel.dim_sharded import supports_dim_sharding, supports_state_sharding
 
-        if supports_dim_sharding(self.problem):
-            from ..parallel.context import DistContext
-
-            from ..parallel.context import balanced_slices
-            from ..parallel.dim_sharded import supports_state_sharding
-
-            ctx = DistContext(group=devices if isinstance(devices, torch.distributed.ProcessGroup) else None)
-            state = ctx.broadcast_state(state)
-            if shard_state:
-                if not supports_state_sharding(self.algorithm, self.problem):
-                    raise ValueError("state sharding needs a column-separable algorithm (parallel.ColumnSeparable) and a "
-                                     "problem without halo / full rows")
-                d = int(self.algorithm.dim)
-                rank, world = torch.distributed.get_rank(ctx.group), torch.distributed.get_world_size(ctx.group)
-                col0, own = balanced_slices(d, world)[rank]
-                alg = state.get_child_state("algorithm")
-                state = state.update_child("algorithm", self.algorithm.dim_shard(alg, col0, own))
-                self._dim_shard_group = (ctx.group, col0, d)
-            else:
-                self._dim_shard_group = (ctx.group,)
-            return state
-        warnings.warn(f"enable_multi_devices: {type(self.problem).__name__} has no dim-sharding terms "
-                      "(partial_terms / combine_terms / dim_halo); sharding the population instead")
-        return self.enable_distributed(state)
+        if not supports_dim_sharding(self.problem) and not shard_state:
+            warnings.warn(f"enable_multi_devices: {type(self.problem).__name__} has no dim-sharding terms "
+                          "(partial_terms / combine_terms / dim_halo); sharding the population instead "
+                          "(shard_state=True keeps the decision axis sharded and all-gathers the rows to evaluate)")
+            return self.enable_distributed(state)
+        ctx = DistContext(group=devices if isinstance(devices, torch.distributed.ProcessGroup) else None)
+        state = ctx.broadcast_state(state)
+        if shard_state:
+            if not supports_state_sharding(self.algorithm, self.problem):
+                raise ValueError(f"state sharding needs a column-separable algorithm (parallel.ColumnSeparable); "
+                                 f"{type(self.algorithm).__name__} is not")
+            d = int(self.algorithm.dim)
+            rank, world = torch.distributed.get_rank(ctx.group), torch.distributed.get_world_size(ctx.group)
+            col0, own = balanced_slices(d, world)[rank]
+            alg = state.get_child_state("algorithm")
+            state = state.update_child("algorithm", self.algorithm.dim_shard(alg, col0, own))
+            self._dim_shard_group = (ctx.group, col0, d)
+        else:
+            self._dim_shard_group = (ctx.group,)
+        return state
 
     def gather_state(self, state: State) -> State:
         """The state with a decision-axis-sharded algorithm state reassembled to full-width

@@ -170,11 +170,32 @@ def test_state_sharded_pso_gloo_matches_single_process(world):
     assert torch.allclose(gbl, ref.global_best_location, rtol=1e-3, atol=1e-3)
 
 
-@pytest.mark.parametrize("fn", [1, 2, 3, 4, 5])
+def _reduce_blocks(terms):
+    """What dim_sharded._reduce_terms does across ranks, for per-rank results in rank order:
+    tensors / "sum" add, "max" maximise, "cat" blocks concatenate along the decision axis."""
+    if isinstance(terms[0], dict):
+        out = {}
+        if "sum" in terms[0]:
+            out["sum"] = sum(t["sum"] for t in terms)
+        if "max" in terms[0]:
+            out["max"] = torch.stack([t["max"] for t in terms]).max(0).values
+        if "cat" in terms[0]:
+            c0 = terms[0]["cat"]
+            if isinstance(c0, (list, tuple)):
+                out["cat"] = [torch.cat([t["cat"][i] for t in terms], -1) for i in range(len(c0))]
+            else:
+                out["cat"] = torch.cat([t["cat"] for t in terms], -1)
+        return out
+    return sum(terms)
+
+
+@pytest.mark.parametrize("fn", range(1, 13))
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
 def test_cec2022_partial_terms_reproduce_full_evaluation(fn, world):
     """Shifted-rotated CEC'22 functions shard the rotated coordinates (their rows of M);
-    F3 (no rotation) takes plain column blocks with a halo of one."""
+    F3 (no rotation) takes plain column blocks with a halo of one; the hybrids (F6–F8) and
+    compositions (F9–F12) all-gather their rotated blocks ("cat" terms) and sum the
+    composition distances."""
     from evoxmi.problems.numerical import CEC2022TestSuit
 
     p = CEC2022TestSuit.create(fn)
@@ -182,12 +203,12 @@ def test_cec2022_partial_terms_reproduce_full_evaluation(fn, world):
     d = 20
     X = (torch.rand(13, d, generator=torch.Generator().manual_seed(fn)) * 20 - 10)
     full, _ = p.evaluate(None, X)
-    T = 0
+    Ts = []
     for col0, own in balanced_slices(d, world):
         hi = min(col0 + own + p.dim_halo, d)
         Xb = X if getattr(p, "dim_shard_full_rows", False) else X[:, col0:hi]
-        T = T + p.partial_terms(Xb, col0, d, own)
-    assert torch.allclose(p.combine_terms(T, d), full, rtol=2e-5, atol=1e-4)
+        Ts.append(p.partial_terms(Xb, col0, d, own))
+    assert torch.allclose(p.combine_terms(_reduce_blocks(Ts), d), full, rtol=2e-5, atol=1e-4)
 
 
 @pytest.mark.parametrize("fn", range(1, 10))
@@ -228,3 +249,61 @@ def test_dtlz_zdt_partial_terms_reproduce_full_evaluation(name, world):
     for col0, own in balanced_slices(d, world):
         T = T + p.partial_terms(X[:, col0 : col0 + own], col0, d, own)
     torch.testing.assert_close(p.combine_terms(T, d), full, rtol=1e-10, atol=1e-10)
+
+
+def _make_coupled():
+    """A non-separable problem with no partial terms: f(x) = (Σ x)² + Σ x² (the generic
+    decision-axis path all-gathers the rows)."""
+    from evoxmi.core import Problem
+
+    class Coupled(Problem):
+        def evaluate(self, state, X):
+            return X.sum(1) ** 2 + (X * X).sum(1), state
+
+    return Coupled()
+
+
+def _generic_worker(rank, world, port, out, algo):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from evoxmi.parallel import destroy, init_distributed
+
+    init_distributed(backend="gloo")
+    wf = _make_generic(algo)
+    st = wf.init(rnd.PRNGKey(5))
+    st = wf.enable_multi_devices(st, shard_state=True)
+    for _ in range(8):
+        st = wf.step(st)
+    full = wf.gather_state(st).get_child_state("algorithm")
+    out[rank] = {k: full[k].clone() for k in ("population", "center") if k in full.keys()}
+    destroy()
+
+
+def _make_generic(algo):
+    import evoxmi.algorithms as A
+    from evoxmi.problems.numerical import Sphere
+
+    d = 24
+    if algo == "de":
+        return StdWorkflow(A.DE(torch.full((d,), -5.0), torch.full((d,), 5.0), 32), _make_coupled())
+    opt = "adam" if algo == "openes_adam" else None
+    return StdWorkflow(A.OpenES(torch.full((d,), 2.0), 32, 0.05, 0.1, optimizer=opt), Sphere())
+
+
+@pytest.mark.parametrize("algo", ["de", "openes", "openes_adam"])
+def test_state_sharded_generic_gloo_matches_single_process(algo):
+    """Generic decision-axis state sharding: DE on a problem without partial terms (rows
+    all-gathered for the evaluation), OpenES (SGD and Adam: centre, population and the
+    optimiser's moments as column blocks) on Sphere's terms — world 3 reproduces one process."""
+    wf = _make_generic(algo)
+    st = wf.init(rnd.PRNGKey(5))
+    for _ in range(8):
+        st = wf.step(st)
+    ref = st.get_child_state("algorithm")
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_generic_worker, args=(3, _free_port(), out, algo), nprocs=3, join=True)
+    for k, v in out[0].items():
+        assert torch.allclose(v, ref[k], rtol=1e-4, atol=1e-4), k
+        assert all(torch.equal(out[r][k], v) for r in range(3))
+
