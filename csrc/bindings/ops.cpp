@@ -910,28 +910,31 @@ at::Tensor weighted_rowsum(const at::Tensor& X, const c10::optional<at::Tensor>&
 
 void gemm_set_config(int64_t cfg) { evx_gemm_set_config((int)cfg); }
 
-at::Tensor sbx(const at::Tensor& x, const at::Tensor& keys, double pro_c, double dis_c, int64_t type) {
+at::Tensor sbx(const at::Tensor& x, const at::Tensor& keys, double pro_c, double dis_c, int64_t type, int64_t col0, int64_t dtot) {
   CHECK_DEV(x); CHECK_F32(x); CHECK_CONTIG(x); CHECK_DEV(keys);
   TORCH_CHECK(x.dim() == 2, "x must be (n, d)");
   TORCH_CHECK(keys.scalar_type() == at::kLong && keys.is_contiguous() && keys.numel() == 4, "keys must be int64[2,2]");
   TORCH_CHECK(type == 1 || type == 2, "type must be 1 or 2");
   const int64_t n = x.size(0), d = x.size(1);
+  TORCH_CHECK(dtot == 0 || (col0 >= 0 && col0 + d <= dtot), "column block outside the decision axis");
   c10::DeviceGuard g(x.device());
   const int64_t rows = type == 1 ? n : n / 2;
   auto out = at::empty({rows, d}, x.options());
-  if (rows > 0 && d > 0) evx_sbx(x.data_ptr<float>(), out.data_ptr<float>(), (int)n, (int)d, keys.data_ptr<int64_t>(), (float)pro_c, (float)dis_c, (int)type, cur_stream());
+  if (rows > 0 && d > 0) evx_sbx(x.data_ptr<float>(), out.data_ptr<float>(), (int)n, (int)d, keys.data_ptr<int64_t>(), (float)pro_c, (float)dis_c, (int)type, cur_stream(), (int)col0, (int)dtot);
   return out;
 }
 
-at::Tensor pm(const at::Tensor& x, const at::Tensor& lb, const at::Tensor& ub, const at::Tensor& keys, double pro_m, double dis_m, int64_t nm) {
+at::Tensor pm(const at::Tensor& x, const at::Tensor& lb, const at::Tensor& ub, const at::Tensor& keys, double pro_m, double dis_m, int64_t nm,
+              int64_t col0, int64_t dtot) {
   CHECK_DEV(x); CHECK_F32(x); CHECK_CONTIG(x); CHECK_DEV(lb); CHECK_F32(lb); CHECK_CONTIG(lb); CHECK_DEV(ub); CHECK_F32(ub); CHECK_CONTIG(ub);
   TORCH_CHECK(keys.scalar_type() == at::kLong && keys.is_contiguous() && keys.numel() == 4, "keys must be int64[2,2]");
   TORCH_CHECK(x.dim() == 2 && lb.numel() == x.size(1) && ub.numel() == x.size(1), "shape mismatch");
+  TORCH_CHECK(dtot == 0 || (col0 >= 0 && col0 + x.size(1) <= dtot), "column block outside the decision axis");
   c10::DeviceGuard g(x.device());
   auto out = at::empty_like(x);
   if (x.numel() > 0)
     evx_pm(x.data_ptr<float>(), out.data_ptr<float>(), (int)x.size(0), (int)x.size(1), (int)nm, lb.data_ptr<float>(), ub.data_ptr<float>(),
-           keys.data_ptr<int64_t>(), (float)pro_m, (float)dis_m, cur_stream());
+           keys.data_ptr<int64_t>(), (float)pro_m, (float)dis_m, cur_stream(), (int)col0, (int)dtot);
   return out;
 }
 
@@ -1372,8 +1375,8 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("philox_words(Tensor key, int nblocks, int domain, int offset) -> Tensor");
   m.def("weighted_rowsum(Tensor X, Tensor? idx, Tensor w, Tensor? sub, int K) -> Tensor");
   m.def("gemm_set_config(int cfg) -> ()");
-  m.def("sbx(Tensor x, Tensor keys, float pro_c, float dis_c, int type) -> Tensor");
-  m.def("pm(Tensor x, Tensor lb, Tensor ub, Tensor keys, float pro_m, float dis_m, int nm) -> Tensor");
+  m.def("sbx(Tensor x, Tensor keys, float pro_c, float dis_c, int type, int col0=0, int dtot=0) -> Tensor");
+  m.def("pm(Tensor x, Tensor lb, Tensor ub, Tensor keys, float pro_m, float dis_m, int nm, int col0=0, int dtot=0) -> Tensor");
   m.def("nds(Tensor f, int limit=0, Tensor? err=None) -> Tensor");
   m.def("ant_rollout(Tensor W, int h1, int h2, Tensor init, int cap) -> Tensor[]");
   m.def("stochastic_ranking(Tensor I1, Tensor I2, Tensor rnd, float pc) -> Tensor");

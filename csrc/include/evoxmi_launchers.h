@@ -125,9 +125,10 @@ void evx_colsum(const float* partial, int chunks, int D, float* out, hipStream_t
 void evx_weighted_rowsum(const float* X, int64_t ldx, const int32_t* idx, const float* w, const float* sub, int K, int D,
                          float* partial, int chunks, hipStream_t s);
 void evx_gemm_set_config(int cfg);
-void evx_sbx(const float* x, float* out, int n, int d, const int64_t* keys, float pro_c, float dis_c, int type, hipStream_t s);
+void evx_sbx(const float* x, float* out, int n, int d, const int64_t* keys, float pro_c, float dis_c, int type, hipStream_t s, int col0 = 0,
+             int dtot = 0);
 void evx_pm(const float* x, float* out, int n, int d, int nm, const float* lb, const float* ub, const int64_t* keys, float pro_m,
-            float dis_m, hipStream_t s);
+            float dis_m, hipStream_t s, int col0 = 0, int dtot = 0);
 void evx_dtlz(const float* X, float* F, int N, int D, int M, int variant, hipStream_t s);
 void evx_de_trial(const float* P, const int32_t* idx, const float* coef, int K, const int32_t* cur, const int32_t* mode,
                   const float* CR, const int32_t* jr, const int32_t* L, const int64_t* key, const float* lb, const float* ub,

@@ -14,7 +14,10 @@ __device__ __forceinline__ uint32_t word_at(uint64_t i, uint32_t k0, uint32_t k1
 
 // keys: split(key, 2) → per-gene word (μ = top 24 bits, bit 0 = sign of β, bit 1 = skip),
 // per-pair rate uniform.  One thread per 4 consecutive genes when they share a Philox
-// block (d % 4 == 0), else one gene per thread.
+// block, else one gene per thread.  Column block (decision-axis state sharding): x / out
+// hold columns [col0, col0 + d) of a dtot-dimensional population and every gene word is
+// drawn at its global counter i·dtot + col0 + j, so a block equals those columns of the
+// unsharded offspring.
 __device__ __forceinline__ float sbx_beta(uint32_t w, float e) {
   const float mu = evx::u24(w);
   float beta = mu <= 0.5f ? exp2f(e * __log2f(2.f * mu)) : exp2f(-e * __log2f(2.f - 2.f * mu));
@@ -24,23 +27,25 @@ __device__ __forceinline__ float sbx_beta(uint32_t w, float e) {
 }
 
 __global__ void __launch_bounds__(256) sbx_kernel(const float* __restrict__ x, float* __restrict__ out, int n, int d,
-                                                  const int64_t* __restrict__ keys, float pro_c, float dis_c, int type) {
+                                                  const int64_t* __restrict__ keys, float pro_c, float dis_c, int type, int col0,
+                                                  int dtot) {
   const int np = n / 2;
   const uint32_t kg0 = (uint32_t)keys[0], kg1 = (uint32_t)keys[1];
   const uint32_t kp0 = (uint32_t)keys[2], kp1 = (uint32_t)keys[3];
   const float e = 1.f / (dis_c + 1.f);
-  const int vec = (d & 3) == 0 ? 4 : 1;
+  const int vec = ((d | col0 | dtot) & 3) == 0 ? 4 : 1;
   const int64_t total = (int64_t)np * d / vec;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t g0 = t * vec;
     const int i = (int)(g0 / d), j0 = (int)(g0 - (int64_t)i * d);
+    const uint64_t gg = (uint64_t)i * dtot + col0 + j0;  // global gene counter
     const bool no_x = evx::u24(word_at((uint64_t)i, kp0, kp1)) > pro_c;
     uint32_t ws[4];
     if (vec == 4) {
-      const evx::u4 w = evx::philox_block((uint64_t)g0 >> 2, kg0, kg1);
+      const evx::u4 w = evx::philox_block(gg >> 2, kg0, kg1);
       ws[0] = w.x; ws[1] = w.y; ws[2] = w.z; ws[3] = w.w;
     } else {
-      ws[0] = word_at((uint64_t)g0, kg0, kg1);
+      ws[0] = word_at(gg, kg0, kg1);
     }
     for (int v = 0; v < vec; ++v) {
       const int j = j0 + v;
@@ -60,21 +65,23 @@ __global__ void __launch_bounds__(256) sbx_kernel(const float* __restrict__ x, f
 // keys: split(key, 2) → site, mu.  Rows beyond the even prefix pass through.
 __global__ void __launch_bounds__(256) pm_kernel(const float* __restrict__ x, float* __restrict__ out, int n, int d, int nm,
                                                  const float* __restrict__ lb, const float* __restrict__ ub,
-                                                 const int64_t* __restrict__ keys, float pro_m, float dis_m) {
+                                                 const int64_t* __restrict__ keys, float pro_m, float dis_m, int col0, int dtot) {
+  // column block: lb / ub are the block's, site probability and counters use the global column
   const int64_t total = (int64_t)n * d;
   uint32_t ks0 = (uint32_t)keys[0], ks1 = (uint32_t)keys[1];
   uint32_t ku0 = (uint32_t)keys[2], ku1 = (uint32_t)keys[3];
   const float e1 = dis_m + 1.f, inv = 1.f / (dis_m + 1.f);
-  const float pr = pro_m / d;
+  const float pr = pro_m / dtot;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
     const int i = (int)(t / d), j = (int)(t - (int64_t)i * d);
+    const uint64_t tg = (uint64_t)i * dtot + col0 + j;
     float v = x[t];
     if (i < nm) {
       const float lo = lb[j], hi = ub[j], span = hi - lo;
       v = fmaxf(fminf(v, hi), lo);
-      const bool site = evx::u24(word_at((uint64_t)t, ks0, ks1)) < pr;
+      const bool site = evx::u24(word_at(tg, ks0, ks1)) < pr;
       if (site) {
-        const float mu = evx::u24(word_at((uint64_t)t, ku0, ku1));  // drawn only at mutation sites
+        const float mu = evx::u24(word_at(tg, ku0, ku1));  // drawn only at mutation sites
         if (mu <= 0.5f) {
           const float nrm = (v - lo) / span;
           v = v + span * (powf(2.f * mu + (1.f - 2.f * mu) * powf(1.f - nrm, e1), inv) - 1.f);
@@ -167,13 +174,14 @@ __global__ void __launch_bounds__(256) de_trial_kernel(const float* __restrict__
 
 }  // namespace
 
-void evx_sbx(const float* x, float* out, int n, int d, const int64_t* keys, float pro_c, float dis_c, int type, hipStream_t s) {
-  sbx_kernel<<<grid_for((int64_t)(n / 2) * d), 256, 0, s>>>(x, out, n, d, keys, pro_c, dis_c, type);
+void evx_sbx(const float* x, float* out, int n, int d, const int64_t* keys, float pro_c, float dis_c, int type, hipStream_t s, int col0,
+             int dtot) {
+  sbx_kernel<<<grid_for((int64_t)(n / 2) * d), 256, 0, s>>>(x, out, n, d, keys, pro_c, dis_c, type, col0, dtot > 0 ? dtot : d);
 }
 
 void evx_pm(const float* x, float* out, int n, int d, int nm, const float* lb, const float* ub, const int64_t* keys, float pro_m,
-            float dis_m, hipStream_t s) {
-  pm_kernel<<<grid_for((int64_t)n * d), 256, 0, s>>>(x, out, n, d, nm, lb, ub, keys, pro_m, dis_m);
+            float dis_m, hipStream_t s, int col0, int dtot) {
+  pm_kernel<<<grid_for((int64_t)n * d), 256, 0, s>>>(x, out, n, d, nm, lb, ub, keys, pro_m, dis_m, col0, dtot > 0 ? dtot : d);
 }
 
 void evx_de_trial(const float* P, const int32_t* idx, const float* coef, int K, const int32_t* cur, const int32_t* mode,

@@ -7,11 +7,39 @@ import torch
 
 from ...core import Algorithm, State
 from ...operators import crossover, mutation
+from ...parallel.dim_sharded import ColumnSeparable
 from ...operators.selection.non_dominate import crowding_distance, lexsort, non_dominated_sort
 from ...ops import random as rnd
 
 
-class MOAlgorithm(Algorithm):
+class ColumnVariation(ColumnSeparable):
+    """SBX + polynomial mutation on this rank's column block (decision-axis state sharding,
+    the reference's GSPMD dim sharding ``std_workflow.py:253-270``): the operators draw every
+    gene at its global column (``cols=``), the bounds are the block's, and the survivor
+    selection only gathers rows by indices computed from the replicated fitness — so a subclass
+    whose ``ask`` / ``tell`` use nothing else of the decision vectors declares
+    ``column_separable = True`` and keeps only its column block of the population."""
+
+    dim_fields = ("population", "next_generation")
+
+    def dim_shard(self, state, col0: int, own: int):
+        for op in (self.crossover, self.mutation):
+            if not getattr(op, "column_blocks", False):
+                raise ValueError(f"{type(op).__name__} does not draw per global column (no cols=): the state cannot be column-sharded")
+        return super().dim_shard(state, col0, own)
+
+    def _vary(self, x_key, mut_key, parents, clip=True):
+        c0, own, d = self.cols()
+        if own == d:
+            off = self.mutation(mut_key, self.crossover(x_key, parents))
+            return torch.clamp(off, self.lb, self.ub) if clip else off
+        lb, ub = self.col_vec(self.lb), self.col_vec(self.ub)
+        cols = (c0, d)
+        off = self.mutation(mut_key, self.crossover(x_key, parents, cols=cols), cols=cols, boundary=(lb, ub))
+        return torch.clamp(off, lb, ub) if clip else off
+
+
+class MOAlgorithm(ColumnVariation, Algorithm):
     def __init__(self, lb, ub, n_objs, pop_size, mutation_op=None, crossover_op=None):
         super().__init__()
         self.lb, self.ub = lb, ub
@@ -36,8 +64,7 @@ class MOAlgorithm(Algorithm):
         return state.update(fitness=fitness)
 
     def _variation(self, x_key, mut_key, parents, clip=True):
-        off = self.mutation(mut_key, self.crossover(x_key, parents))
-        return torch.clamp(off, self.lb, self.ub) if clip else off
+        return self._vary(x_key, mut_key, parents, clip)
 
 
 def nsga2_select(fitness, n):

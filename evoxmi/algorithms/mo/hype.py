@@ -30,6 +30,8 @@ def cal_hv(points, ref, k, n_sample, key):
 
 
 class HypE(MOAlgorithm):
+    column_separable = True  # variation per global column, selection by the replicated fitness
+
     def __init__(self, lb, ub, n_objs, pop_size, n_sample=10000, mutation_op=None, crossover_op=None):
         super().__init__(lb, ub, n_objs, pop_size, mutation_op, crossover_op)
         self.n_sample = n_sample
@@ -45,7 +47,7 @@ class HypE(MOAlgorithm):
         key, sub, sel_key, x_key, mut_key = rnd.split(state.key, 5)
         hv = cal_hv(state.fitness, state.ref_point, self.pop_size, self.n_sample, sub)
         selected, _ = self.selection(sel_key, state.population, -hv[:, None])
-        off = self.mutation(mut_key, self.crossover(x_key, selected))
+        off = self._variation(x_key, mut_key, selected, clip=False)
         return off, state.update(next_generation=off, key=key)
 
     def tell(self, state, fitness):

@@ -40,6 +40,8 @@ def ibea_truncate(fitness, I, C, kappa, n_remove):
 
 
 class IBEA(MOAlgorithm):
+    column_separable = True  # variation per global column, selection by the replicated fitness
+
     def __init__(self, lb, ub, n_objs, pop_size, kappa=0.05, mutation_op=None, crossover_op=None):
         super().__init__(lb, ub, n_objs, pop_size, mutation_op, crossover_op)
         self.kappa = kappa
@@ -49,7 +51,7 @@ class IBEA(MOAlgorithm):
         key, sel_key, x_key, mut_key = rnd.split(state.key, 4)
         fit = cal_fitness(state.fitness, self.kappa)[0]
         selected, _ = self.selection(sel_key, state.population, -fit)
-        off = self.mutation(mut_key, self.crossover(x_key, selected))
+        off = self._variation(x_key, mut_key, selected, clip=False)
         return off, state.update(next_generation=off, key=key)
 
     def tell(self, state, fitness):

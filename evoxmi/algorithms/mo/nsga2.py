@@ -12,11 +12,16 @@ import torch
 
 from ...core import Algorithm, State
 from ...operators import crossover, mutation, selection
+from .common import ColumnVariation
 from ...operators.selection.non_dominate import crowding_distance, lexsort, non_dominated_sort
 from ...ops import random as rnd
 
 
-class NSGA2(Algorithm):
+class NSGA2(ColumnVariation, Algorithm):
+    # SBX / PM per global column and row selection from the replicated fitness: the state can
+    # be column-sharded (StdWorkflow.enable_multi_devices(shard_state=True))
+    column_separable = True
+
     def __init__(self, lb, ub, n_objs, pop_size, selection_op=None, mutation_op=None, crossover_op=None):
         super().__init__()
         self.lb, self.ub = lb, ub
@@ -41,9 +46,7 @@ class NSGA2(Algorithm):
 
     def ask(self, state):
         key, _sel, x_key, mut_key = rnd.split(state.key, 4)
-        off = self.crossover(x_key, state.population)
-        off = self.mutation(mut_key, off)
-        off = torch.clamp(off, self.lb, self.ub)
+        off = self._vary(x_key, mut_key, state.population)
         return off, state.update(next_generation=off, key=key)
 
     def tell(self, state, fitness):

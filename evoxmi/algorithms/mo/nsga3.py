@@ -27,6 +27,8 @@ from .common import MOAlgorithm
 
 
 class NSGA3(MOAlgorithm):
+    column_separable = True  # variation per global column, selection by the replicated fitness
+
     def __init__(self, lb, ub, n_objs, pop_size, selection_op=None, mutation_op=None, crossover_op=None):
         super().__init__(lb, ub, n_objs, pop_size, mutation_op, crossover_op)
         self.selection = selection_op if selection_op is not None else selection.UniformRand(1)

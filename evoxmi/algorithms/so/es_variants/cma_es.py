@@ -137,17 +137,20 @@ class CMAES(Algorithm):
         d = self.dim
         if (state.B.is_cuda and config.get("gemm_planes") and config.get("gemm_prec") == "x6" and config.get("plain_gemm") == "evoxmi"
                 and d % 4 == 0):
-            # bf16x6 operands pre-split once per generation: the noise is generated straight into
-            # its fragment planes (the f32 noise matrix is never written) and B·diag(D) is split
-            # by one pass with D as the column scale — the sampling GEMM does no split work
+            # B·diag(D) pre-split into its bf16x6 fragment planes once per generation (one pass, D as
+            # the column scale): the sampling GEMM splits only the noise on the fly (10k×1000×1000:
+            # 162.6 vs 174.3 µs, profiles/r4_gemm_planes.log).  gemm_planes = 2 also generates the
+            # noise straight into planes (the f32 noise is never written) — slower: the A side is
+            # then 1.5× the bytes of a load-bound loop (205 µs)
             from ....ops.linalg import mm_nt, normal_planes, split_planes
 
-            zp = normal_planes(key.to(state.B.device), rows, d, row0)
+            za = normal_planes(key.to(state.B.device), rows, d, row0) if config.get("gemm_planes") >= 2 else \
+                rnd.normal(key, (rows, d), offset=row0 * d)
             bdp = split_planes(state.B, colscale=state.D)
             buf = state.population
             out = buf if (rows == self.pop_size and torch.cuda.is_current_stream_capturing() and buf.is_contiguous()
                           and buf.shape == (rows, d)) else None
-            return mm_nt(zp, bdp, alpha_ptr=state.sigma.reshape(1), bias_n=state.mean, out=out)
+            return mm_nt(za, bdp, alpha_ptr=state.sigma.reshape(1), bias_n=state.mean, out=out)
         z = rnd.normal(key, (rows, d), offset=row0 * d)
         if z.is_cuda:
             # X = mean + σ (Z∘D) Bᵀ = mean + Z (σ·B∘D)ᵀ : σ (a device scalar, no host sync)

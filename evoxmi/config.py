@@ -53,7 +53,7 @@ KNOBS: Dict[str, Knob] = {
     "cec_stack": Knob("EVOXMI_CEC_STACK", 1, int, "CEC'22 compositions (F9–F12) on the device: every rotated component from ONE GEMM over the stacked rotations with per-block exact shifts (1) or one GEMM per component (0)"),
     "cec_fused": Knob("EVOXMI_CEC_FUSED", 0, int, "CEC'22 F1 / F4 on the device: 1 = row terms from the rotation GEMM's epilogue (rotated population never written), 0 = GEMM + basic-function kernel (default: the fused epilogue measured 7 µs slower at pop 10 000 × d 1000, profiles/r3_cec_fused_epilogue.txt)"),
     "gemm_prec": Knob("EVOXMI_GEMM_PREC", "x6", str, "framework f32 GEMMs (gemm_ks.hip): 'x6' — each f32 operand split exactly into three bf16 parts, six bf16 MFMA products (f32-accurate, 3/8 of the f32 MFMA time) — or 'f32' (v_mfma_f32_16x16x4_f32)"),
-    "gemm_planes": Knob("EVOXMI_GEMM_PLANES", 0, int, "x6 GEMMs: operands that are constant (CEC rotations) or produced once per generation (CMA-ES noise, B·D) pre-split into bf16 fragment planes (1) instead of split inside the GEMM (0, default: the 3 × 16-byte plane loads cost more than the split arithmetic they remove — sampling GEMM 224 vs 173 µs, 1.852 vs 1.799 ms/gen, profiles/NOTES.md)"),
+    "gemm_planes": Knob("EVOXMI_GEMM_PLANES", 1, int, "x6 GEMMs: the d×d operand that is constant (CEC rotations) or produced once per generation (CMA-ES B·D) pre-split into bf16 fragment planes (1, default: the 10k sampling GEMM 162.6 vs 174.3 µs); 2 also generates the CMA-ES noise straight into planes (slower: the A side of the load-bound loop grows 1.5×, 205 µs); 0 splits both inside the GEMM"),
     "plain_gemm": Knob("EVOXMI_PLAIN_GEMM", "evoxmi", str, "flagship GEMMs: 'evoxmi' (framework MFMA kernels, csrc/kernels/gemm_ks.hip) or 'blas' (hipBLASLt via torch, an A/B baseline only)"),
     "jacobi_sweeps": Knob("EVOXMI_JACOBI_SWEEPS", 2, int, "maximum warm-started Jacobi sweeps per decomposition (stops early once converged)"),
     "jacobi_tol_factor": Knob("EVOXMI_JACOBI_TOL_FACTOR", 4.0, float, "convergence: ‖offdiag‖ ≤ factor·eps_f32·sqrt(n)·‖diag‖"),

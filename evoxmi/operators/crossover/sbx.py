@@ -7,25 +7,30 @@ import torch
 from ...ops import random as rnd
 
 
-def simulated_binary(key, x, pro_c=1.0, dis_c=20.0, type=1):
+def simulated_binary(key, x, pro_c=1.0, dis_c=20.0, type=1, cols=None):
     """PlatEMO SBX: first half × second half; ``type=1`` → 2 children per pair
     (+ the odd last row passes through), ``type=2`` → 1 child per pair.
 
     Random streams (shared bit-for-bit with the HIP kernels): ``split(key, 2)`` →
     a per-gene word ``w`` whose top 24 bits give μ, bit 0 the sign of β and bit 1
     the 50 % "no crossover on this gene" coin; and a per-pair uniform compared with
-    ``pro_c``.  One Philox word per gene instead of three."""
+    ``pro_c``.  One Philox word per gene instead of three.
+
+    ``cols = (col0, d_total)``: ``x`` is the column block [col0, col0 + d) of a d_total-dim
+    population (decision-axis state sharding); gene words are drawn at their global columns,
+    so the block equals those columns of the unsharded offspring."""
     if x.is_cuda and x.dtype == torch.float32:
         from ...ops import evo as evo_ops
 
-        return evo_ops.sbx(key, x, float(pro_c), float(dis_c), int(type))
+        return evo_ops.sbx(key, x, float(pro_c), float(dis_c), int(type), cols)
     gene_key, pair_key = rnd.split(key, 2)
     n, d = x.shape
+    c0, dt = cols if cols is not None else (0, d)
     p1 = x[: n // 2]
     p2 = x[n // 2 : n // 2 * 2]
     n_p = p1.shape[0]
     dev = x.device
-    w = rnd.bits(gene_key, (n_p, d)).to(dev)
+    w = rnd.bits(gene_key, (n_p, dt)).to(dev)[:, c0 : c0 + d]
     mu = rnd._u24(w)
     beta = torch.where(mu <= 0.5, (2 * mu) ** (1 / (dis_c + 1)), (2 - 2 * mu) ** (-1 / (dis_c + 1)))
     beta = torch.where((w & 1) == 1, -beta, beta)
@@ -42,11 +47,13 @@ def simulated_binary(key, x, pro_c=1.0, dis_c=20.0, type=1):
 
 
 class SimulatedBinary:
+    column_blocks = True  # accepts cols= (decision-axis state sharding)
+
     def __init__(self, pro_c=1, dis_c=20, type=1):
         self.pro_c, self.dis_c, self.type = pro_c, dis_c, type
 
-    def __call__(self, key, x):
-        return simulated_binary(key, x, self.pro_c, self.dis_c, self.type)
+    def __call__(self, key, x, cols=None):
+        return simulated_binary(key, x, self.pro_c, self.dis_c, self.type, cols)
 
 
 def _random_pairing(key, x):

@@ -6,18 +6,23 @@ import torch
 from ...ops import random as rnd
 
 
-def polynomial(key, x, boundary, pro_m=1.0, dis_m=20.0):
-    """PlatEMO polynomial mutation; per-gene probability ``pro_m / d``; an odd last row passes through."""
+def polynomial(key, x, boundary, pro_m=1.0, dis_m=20.0, cols=None):
+    """PlatEMO polynomial mutation; per-gene probability ``pro_m / d``; an odd last row passes through.
+
+    ``cols = (col0, d_total)``: ``x`` and ``boundary`` are the column block [col0, col0 + d) of
+    a d_total-dim problem; the site probability is ``pro_m / d_total`` and the draws are
+    those of the global columns."""
     if x.is_cuda and x.dtype == torch.float32 and x.shape[0] > 1:
         from ...ops import evo as evo_ops
 
-        return evo_ops.polynomial(key, x, boundary[0], boundary[1], float(pro_m), float(dis_m))
+        return evo_ops.polynomial(key, x, boundary[0], boundary[1], float(pro_m), float(dis_m), cols)
     k1, k2 = rnd.split(key)
     pop = x if x.shape[0] == 1 else x[: (x.shape[0] // 2) * 2]
     n, d = pop.shape
     dev = x.device
-    site = rnd.uniform(k1, (n, d)).to(dev) < pro_m / d
-    mu = rnd.uniform(k2, (n, d)).to(dev)
+    c0, dt = cols if cols is not None else (0, d)
+    site = rnd.uniform(k1, (n, dt)).to(dev)[:, c0 : c0 + d] < pro_m / dt
+    mu = rnd.uniform(k2, (n, dt)).to(dev)[:, c0 : c0 + d]
     lower = boundary[0].to(dev).expand(n, d)
     upper = boundary[1].to(dev).expand(n, d)
     pop = torch.maximum(torch.minimum(pop, upper), lower)
@@ -33,11 +38,13 @@ def polynomial(key, x, boundary, pro_m=1.0, dis_m=20.0):
 
 
 class Polynomial:
+    column_blocks = True  # accepts cols= and a column-block boundary
+
     def __init__(self, boundary, pro_m=1, dis_m=20):
         self.boundary, self.pro_m, self.dis_m = boundary, pro_m, dis_m
 
-    def __call__(self, key, x):
-        return polynomial(key, x, self.boundary, self.pro_m, self.dis_m)
+    def __call__(self, key, x, cols=None, boundary=None):
+        return polynomial(key, x, self.boundary if boundary is None else boundary, self.pro_m, self.dis_m, cols)
 
 
 def gaussian(key, x, stdvar):

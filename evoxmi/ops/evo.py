@@ -9,18 +9,21 @@ from .. import config
 from . import random as rnd
 
 
-def sbx(key, x, pro_c, dis_c, type):
+def sbx(key, x, pro_c, dis_c, type, cols=None):
+    """``cols = (col0, d_total)``: x is that column block of a d_total-dim population."""
     keys = rnd.split(key, 2).contiguous()
-    return _ext.ops().sbx(x.contiguous(), keys, float(pro_c), float(dis_c), int(type))
+    c0, dt = cols if cols is not None else (0, 0)
+    return _ext.ops().sbx(x.contiguous(), keys, float(pro_c), float(dis_c), int(type), int(c0), int(dt))
 
 
-def polynomial(key, x, lb, ub, pro_m, dis_m):
+def polynomial(key, x, lb, ub, pro_m, dis_m, cols=None):
     keys = rnd.split(key, 2).contiguous()
+    c0, dt = cols if cols is not None else (0, 0)
     nm = x.shape[0] if x.shape[0] == 1 else (x.shape[0] // 2) * 2
     d = x.shape[1]
     lb = lb.to(device=x.device, dtype=torch.float32).expand(d).contiguous()
     ub = ub.to(device=x.device, dtype=torch.float32).expand(d).contiguous()
-    return _ext.ops().pm(x.contiguous(), lb, ub, keys, float(pro_m), float(dis_m), int(nm))
+    return _ext.ops().pm(x.contiguous(), lb, ub, keys, float(pro_m), float(dis_m), int(nm), int(c0), int(dt))
 
 
 _CROSS = {"bin": 0, "exp": 1, "arith": 2}

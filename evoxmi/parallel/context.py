@@ -176,18 +176,22 @@ class SimulatedDistContext(DistContext):
     def bytes_all_gather(self):
         return self.counters.all_gather_bytes
 
-    def _count(self, kind: str, nbytes: int):
+    def _target(self):
+        """The counters a call records into: during a graph capture the captured step's own
+        counters (those calls repeat on every replay without running Python again)."""
         c = self.counters
         if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
-            # a graph capture: these calls repeat on every replay without running Python again
             from .wire import WireCounters
 
             if c.captured is None or not getattr(c, "_capturing", False):
                 c.captured = WireCounters()
                 c._capturing = True
-            c = c.captured
-        else:
-            c._capturing = False
+            return c.captured
+        c._capturing = False
+        return c
+
+    def _count(self, kind: str, nbytes: int):
+        c = self._target()
         if kind == "all_reduce":
             c.all_reduce_calls += 1
             c.all_reduce_bytes += nbytes
@@ -200,11 +204,8 @@ class SimulatedDistContext(DistContext):
     def count_peer_rows(self, rows: torch.Tensor, row_bytes: int):
         """A peer row gather of ``rows`` (device scalar: rows that a real rank would read from
         other ranks' buffers) — accumulated on the device, read once after timing."""
-        c = self.counters
-        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing() and c.captured is not None:
-            c.captured.peer_gathers += 1
-        else:
-            c.peer_gathers += 1
+        self._target().peer_gathers += 1
+        c = self.counters  # the row count itself accumulates on the device, replays included
         c.row_bytes = int(row_bytes)
         r = rows.to(torch.float64).reshape(())
         if c.peer_rows is None:

@@ -18,7 +18,7 @@ measured compute time (no overlap credited).
 """
 from __future__ import annotations
 
-from dataclasses import dataclass, field
+from dataclasses import dataclass, field, replace
 from typing import Dict
 
 
@@ -70,12 +70,13 @@ class WireCounters:
     def reset(self):
         """Zero the host counters and the device peer-row count (in place: a captured graph keeps
         accumulating into the same tensor on every replay)."""
-        pr, cap = self.peer_rows, self.captured
+        pr, cap, rb = self.peer_rows, self.captured, self.row_bytes
         self.__init__()
         if pr is not None:
             pr.zero_()
             self.peer_rows = pr
         self.captured = cap
+        self.row_bytes = rb  # a property of the problem (bytes of one decision row), not a count
 
     def summary(self, steps: int, model: WireModel, world: int, graph: bool = False) -> Dict[str, float]:
         """Per-generation volumes over ``steps`` generations.  ``graph``: the generations were
@@ -84,15 +85,12 @@ class WireCounters:
         accumulated on every replay."""
         steps = max(1, int(steps))
         if graph and self.captured is not None:
-            c = self.captured
-            c.peer_rows, c.row_bytes = self.peer_rows, self.row_bytes
-            c.peer_gathers = c.peer_gathers * steps
-            out = WireCounters.summary(c, 1, model, world)
-            # peer rows accumulated over `steps` replays
-            pb = (0.0 if self.peer_rows is None else float(self.peer_rows)) * self.row_bytes / steps
-            out["peer_bytes_per_gen"] = pb
-            return out
-        peer_rows = 0.0 if self.peer_rows is None else float(self.peer_rows)
+            # one generation = the captured step's host counters, with the device peer-row count
+            # (accumulated over `steps` replays) averaged to one generation
+            rows = 0.0 if self.peer_rows is None else float(self.peer_rows) / steps
+            c = replace(self.captured, peer_rows=rows, row_bytes=self.row_bytes or self.captured.row_bytes, captured=None)
+            return WireCounters.summary(c, 1, model, world)
+        peer_rows = 0.0 if self.peer_rows is None else float(self.peer_rows)  # tensor or float
         peer_bytes = peer_rows * self.row_bytes
         peer_us = sum(model.peer_read_us(peer_bytes / max(1, self.peer_gathers), world) for _ in range(self.peer_gathers)) \
             if self.peer_gathers else 0.0

@@ -82,6 +82,51 @@ def _pow2(exps, like):
     return torch.pow(2.0, exps.to(like.dtype)).to(like.device)
 
 
+class _PositionDistance:
+    """Decision-axis sharding (P2, ``evoxmi/parallel/dim_sharded.py``) for the MaF problems of
+    DTLZ form: the first ``n_pos`` (position) variables travel as terms from the rank owning
+    each column, and the distance part is ``n_sums`` additive per-row sums over the remaining
+    columns (``_sums(Y, gcol0, d)``, Y = this rank's distance columns starting at global column
+    gcol0).  ``_finish(Xp, S, d)`` forms the objectives; ``evaluate`` is the same formula on the
+    whole row (the reference's ``maf.py`` evaluates rows whole under GSPMD)."""
+
+    dim_halo = 0
+    n_sums = 1
+
+    def _n_pos(self):
+        return self.m - 1
+
+    def partial_terms(self, Xb, col0, d, own):
+        k = self._n_pos()
+        Xo = Xb[:, :own]
+        T = torch.zeros((Xb.shape[0], k + self.n_sums), dtype=Xb.dtype, device=Xb.device)
+        hi = min(col0 + own, k)
+        if hi > col0:
+            T[:, col0:hi] = Xo[:, : hi - col0]
+        s = max(k - col0, 0)
+        if s < own and self.n_sums:
+            T[:, k:] = self._sums(Xo[:, s:], col0 + s, d)
+        return T
+
+    def combine_terms(self, T, d):
+        k = self._n_pos()
+        return self._finish(T[:, :k], T[:, k:], d)
+
+    def evaluate(self, state, X):
+        k = self._n_pos()
+        d = X.shape[1]
+        return self._finish(X[:, :k], self._sums(X[:, k:], k, d) if self.n_sums else X[:, :0], d), state
+
+
+def _sq_half(Y, gcol0, d):
+    return ((Y - 0.5) ** 2).sum(1, keepdim=True)
+
+
+def _rastrigin_sum(Y, gcol0, d):
+    Y = Y - 0.5
+    return (Y * Y - torch.cos(20 * PI * Y)).sum(1, keepdim=True)
+
+
 class MaF(Problem):
     def __init__(self, d=None, m=None, ref_num=1000):
         super().__init__()
@@ -99,31 +144,34 @@ class MaF(Problem):
         return 1 - self._uniform()
 
 
-class MaF1(MaF):
+class MaF1(_PositionDistance, MaF):
     """Inverted linear front (maf.py:98-130)."""
 
-    def evaluate(self, state, X):
-        m = self.m
-        g = ((X[:, m - 1 :] - 0.5) ** 2).sum(1, keepdim=True)
-        return (1 + g) - (1 + g) * _front(X[:, : m - 1], 1 - X[:, : m - 1]), state
+    _sums = staticmethod(_sq_half)
+
+    def _finish(self, Xp, g, d):
+        return (1 + g) - (1 + g) * _front(Xp, 1 - Xp)
 
 
-class MaF2(MaF):
+class MaF2(_PositionDistance, MaF):
     """DTLZ2BZ: per-objective distance groups (maf.py:133-218)."""
 
-    def evaluate(self, state, X):
+    @property
+    def n_sums(self):
+        return self.m
+
+    def _sums(self, Y, gcol0, d):
+        # group i of objective i: columns [m − 1 + i·interval, m − 1 + (i + 1)·interval), the last to d
         m = self.m
-        n, d = X.shape
         interval = int((d - m + 1) / m)
-        Z = (X / 2 + 0.25 - 0.5) ** 2
-        cols = []
-        for i in range(m):
-            start = m + i * interval - 1
-            end = start + interval if i < m - 1 else d
-            cols.append(Z[:, start:end].sum(1))
-        g = torch.stack(cols, 1)
-        Y = X[:, : m - 1] / 2 + 0.25
-        return (1 + g) * _front(torch.cos(Y * PI / 2), torch.sin(Y * PI / 2)), state
+        c = torch.arange(gcol0, gcol0 + Y.shape[1], device=Y.device) - (m - 1)
+        grp = torch.clamp(c // interval, max=m - 1) if interval > 0 else torch.full_like(c, m - 1)
+        Z = (Y / 2 + 0.25 - 0.5) ** 2
+        return torch.zeros((Y.shape[0], m), dtype=Y.dtype, device=Y.device).index_add_(1, grp, Z)
+
+    def _finish(self, Xp, g, d):
+        Y = Xp / 2 + 0.25
+        return (1 + g) * _front(torch.cos(Y * PI / 2), torch.sin(Y * PI / 2))
 
     def pf(self):
         m = self.m
@@ -140,19 +188,15 @@ class MaF2(MaF):
         return _front(c[:, : m - 1], torch.sqrt(1 - c[:, : m - 1] ** 2))
 
 
-def _rastrigin_g(X, m):
-    d = X.shape[1]
-    Y = X[:, m - 1 :] - 0.5
-    return 100 * (d - m + 1 + (Y * Y - torch.cos(20 * PI * Y)).sum(1, keepdim=True))
-
-
-class MaF3(MaF):
+class MaF3(_PositionDistance, MaF):
     """Convex DTLZ3 (maf.py:221-259)."""
 
-    def evaluate(self, state, X):
+    _sums = staticmethod(_rastrigin_sum)
+
+    def _finish(self, Xp, S, d):
         m = self.m
-        f1 = (1 + _rastrigin_g(X, m)) * _sphere_front(X, m)
-        return torch.cat([f1[:, : m - 1] ** 4, f1[:, m - 1 :] ** 2], 1), state
+        f1 = (1 + 100 * (d - m + 1 + S)) * _sphere_front(Xp, m)
+        return torch.cat([f1[:, : m - 1] ** 4, f1[:, m - 1 :] ** 2], 1)
 
     def pf(self):
         r = self._uniform() ** 2
@@ -160,43 +204,45 @@ class MaF3(MaF):
         return r / torch.cat([(temp * temp).expand(-1, r.shape[1] - 1), temp], 1)
 
 
-class MaF4(MaF):
+class MaF4(_PositionDistance, MaF):
     """Inverted, badly-scaled DTLZ3 (maf.py:262-299)."""
 
-    def evaluate(self, state, X):
+    _sums = staticmethod(_rastrigin_sum)
+
+    def _finish(self, Xp, S, d):
         m = self.m
-        g1 = 1 + _rastrigin_g(X, m)
-        f1 = g1 - g1 * _sphere_front(X, m)
-        return f1 * _pow2(torch.arange(1, m + 1), X)[None], state
+        g1 = 1 + 100 * (d - m + 1 + S)
+        f1 = g1 - g1 * _sphere_front(Xp, m)
+        return f1 * _pow2(torch.arange(1, m + 1), Xp)[None]
 
     def pf(self):
         r1 = _normalise_rows(self._uniform())
         return (1 - r1) * _pow2(torch.arange(1, self.m + 1), r1)[None]
 
 
-class MaF5(MaF):
+class MaF5(_PositionDistance, MaF):
     """Concave, badly-scaled DTLZ4 (maf.py:302-338)."""
 
-    def evaluate(self, state, X):
+    _sums = staticmethod(_sq_half)
+
+    def _finish(self, Xp, g, d):
         m = self.m
-        X = torch.cat([X[:, : m - 1] ** 100, X[:, m - 1 :]], 1)
-        g = ((X[:, m - 1 :] - 0.5) ** 2).sum(1, keepdim=True)
-        return (1 + g) * _sphere_front(X, m) * _pow2(torch.arange(m, 0, -1), X)[None], state
+        return (1 + g) * _sphere_front(Xp**100, m) * _pow2(torch.arange(m, 0, -1), Xp)[None]
 
     def pf(self):
         r1 = _normalise_rows(self._uniform())
         return r1 * _pow2(torch.arange(self.m, 0, -1), r1)[None]
 
 
-class MaF6(MaF):
+class MaF6(_PositionDistance, MaF):
     """Degenerate DTLZ5 with I = 2 (maf.py:341-386)."""
 
-    def evaluate(self, state, X):
+    _sums = staticmethod(_sq_half)
+
+    def _finish(self, Xp, g, d):
         m, i = self.m, 2
-        g = ((X[:, m - 1 :] - 0.5) ** 2).sum(1, keepdim=True)
-        mid = (1 + 2 * g * X[:, i - 1 : m - 1]) / (2 + 2 * g)
-        X = torch.cat([X[:, : i - 1], mid, X[:, m - 1 :]], 1)
-        return (1 + 100 * g) * _sphere_front(X, m), state
+        mid = (1 + 2 * g * Xp[:, i - 1 : m - 1]) / (2 + 2 * g)
+        return (1 + 100 * g) * _sphere_front(torch.cat([Xp[:, : i - 1], mid], 1), m)
 
     def pf(self):
         i, m = 2, self.m
@@ -207,15 +253,16 @@ class MaF6(MaF):
         return r1 / math.sqrt(2) ** max(m - i, 0)
 
 
-class MaF7(MaF):
+class MaF7(_PositionDistance, MaF):
     """Disconnected DTLZ7 front (maf.py:389-443)."""
 
-    def evaluate(self, state, X):
+    _sums = staticmethod(lambda Y, gcol0, d: Y.sum(1, keepdim=True))
+
+    def _finish(self, fm, S, d):
         m = self.m
-        g = 1 + 9 * X[:, m - 1 :].mean(1, keepdim=True)
-        fm = X[:, : m - 1]
+        g = 1 + 9 * S / (d - m + 1)
         last = (1 + g) * (m - (fm / (1 + g) * (1 + torch.sin(3 * PI * fm))).sum(1, keepdim=True))
-        return torch.cat([fm, last], 1), state
+        return torch.cat([fm, last], 1)
 
     @staticmethod
     def _grid(N, M):
@@ -254,23 +301,33 @@ class _Polygon(MaF):
         return pts[point_in_polygon(self._points(), pts)]
 
 
-class MaF8(_Polygon):
-    """Multi-point distance minimisation, 2-D decision space (maf.py:449-500)."""
+class MaF8(_PositionDistance, _Polygon):
+    """Multi-point distance minimisation, 2-D decision space (maf.py:449-500); under
+    decision-axis sharding the two used columns travel as terms."""
+
+    n_sums = 0
+    _n_pos = staticmethod(lambda: 2)
+
+    def _finish(self, X2, S, d):
+        return torch.cdist(X2, self._points(X2.device).to(X2.dtype))
 
     def __init__(self, d=None, m=None, ref_num=1000):
         super().__init__(2, m, ref_num)
-
-    def evaluate(self, state, X):
-        P = self._points(X.device).to(X.dtype)
-        return torch.cdist(X[:, :2], P), state
 
     def pf(self):
         pts = self._pf_grid("F")
         return torch.cdist(pts, self._points())
 
 
-class MaF9(_Polygon):
-    """Multi-line distance minimisation (maf.py:503-560)."""
+class MaF9(_PositionDistance, _Polygon):
+    """Multi-line distance minimisation (maf.py:503-560); the two used columns travel as
+    terms under decision-axis sharding."""
+
+    n_sums = 0
+    _n_pos = staticmethod(lambda: 2)
+
+    def _finish(self, X2, S, d):
+        return self._eval(X2)
 
     def _eval(self, X):
         P = self._points(X.device).to(X.dtype)
@@ -278,9 +335,6 @@ class MaF9(_Polygon):
         num = torch.abs((A[None, :, 0] - X[:, None, 0]) * (B[None, :, 1] - X[:, None, 1])
                         - (B[None, :, 0] - X[:, None, 0]) * (A[None, :, 1] - X[:, None, 1]))
         return num / torch.sqrt((A[:, 0] - B[:, 0]) ** 2 + (A[:, 1] - B[:, 1]) ** 2)[None]
-
-    def evaluate(self, state, X):
-        return self._eval(X), state
 
     def pf(self):
         return self._eval(self._pf_grid("C"))

@@ -275,7 +275,7 @@ def _generic_worker(rank, world, port, out, algo):
     for _ in range(8):
         st = wf.step(st)
     full = wf.gather_state(st).get_child_state("algorithm")
-    out[rank] = {k: full[k].clone() for k in ("population", "center") if k in full.keys()}
+    out[rank] = {k: full[k].clone() for k in ("population", "center", "fitness") if k in full.keys()}
     destroy()
 
 
@@ -284,17 +284,25 @@ def _make_generic(algo):
     from evoxmi.problems.numerical import Sphere
 
     d = 24
+    if algo in ("nsga2", "nsga3", "ibea", "hype"):
+        from evoxmi.problems.numerical import DTLZ2
+
+        cls = {"nsga2": A.NSGA2, "nsga3": A.NSGA3, "ibea": A.IBEA, "hype": A.HypE}[algo]
+        kw = {"n_sample": 500} if algo == "hype" else {}
+        return StdWorkflow(cls(torch.zeros(d), torch.ones(d), 3, 32, **kw), DTLZ2(d=d, m=3))
     if algo == "de":
         return StdWorkflow(A.DE(torch.full((d,), -5.0), torch.full((d,), 5.0), 32), _make_coupled())
     opt = "adam" if algo == "openes_adam" else None
     return StdWorkflow(A.OpenES(torch.full((d,), 2.0), 32, 0.05, 0.1, optimizer=opt), Sphere())
 
 
-@pytest.mark.parametrize("algo", ["de", "openes", "openes_adam"])
+@pytest.mark.parametrize("algo", ["de", "openes", "openes_adam", "nsga2", "nsga3", "ibea", "hype"])
 def test_state_sharded_generic_gloo_matches_single_process(algo):
     """Generic decision-axis state sharding: DE on a problem without partial terms (rows
     all-gathered for the evaluation), OpenES (SGD and Adam: centre, population and the
-    optimiser's moments as column blocks) on Sphere's terms — world 3 reproduces one process."""
+    optimiser's moments as column blocks) on Sphere's terms, the SBX + PM MOEAs (operators
+    drawn per global column, selection from the replicated objectives) on DTLZ2's terms —
+    world 3 reproduces one process."""
     wf = _make_generic(algo)
     st = wf.init(rnd.PRNGKey(5))
     for _ in range(8):
@@ -307,3 +315,52 @@ def test_state_sharded_generic_gloo_matches_single_process(algo):
         assert torch.allclose(v, ref[k], rtol=1e-4, atol=1e-4), k
         assert all(torch.equal(out[r][k], v) for r in range(3))
 
+
+
+def test_mo_column_sharding_rejects_operators_without_column_blocks():
+    import evoxmi.algorithms as A
+
+    class RowOnly:
+        def __call__(self, key, x):
+            return x
+
+    algo = A.NSGA2(torch.zeros(8), torch.ones(8), 2, 16, crossover_op=RowOnly())
+    st = algo.setup(rnd.PRNGKey(0))
+    with pytest.raises(ValueError, match="column"):
+        algo.dim_shard(st, 0, 4)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sbx_pm_column_blocks_equal_full_columns(world):
+    """The operators' cols= draws: every column block equals those columns of the full result."""
+    from evoxmi.operators import crossover, mutation
+
+    d = 30
+    x = torch.rand(20, d, generator=torch.Generator().manual_seed(1))
+    lb, ub = torch.zeros(d), torch.ones(d)
+    key = rnd.PRNGKey(3)
+    full_x = crossover.simulated_binary(key, x)
+    full_m = mutation.polynomial(key, full_x, (lb, ub))
+    for c0, own in balanced_slices(d, world):
+        blk = crossover.simulated_binary(key, x[:, c0 : c0 + own], cols=(c0, d))
+        assert torch.equal(blk, full_x[:, c0 : c0 + own])
+        mb = mutation.polynomial(key, blk, (lb[c0 : c0 + own], ub[c0 : c0 + own]), cols=(c0, d))
+        assert torch.equal(mb, full_m[:, c0 : c0 + own])
+
+
+@pytest.mark.parametrize("name", [f"MaF{i}" for i in range(1, 10)])
+@pytest.mark.parametrize("world", [1, 2, 3, 7])
+def test_maf_partial_terms_reproduce_full_evaluation(name, world):
+    """MaF1-MaF9: position variables (MaF8/9: the two used columns) as terms from their owners,
+    the distance sums (MaF2: one per objective group, by global column) additive."""
+    from evoxmi.problems import numerical as N
+
+    p = getattr(N, name)(d=23, m=4)
+    d = p.d
+    assert supports_dim_sharding(p)
+    X = torch.rand(11, d, dtype=torch.float64, generator=torch.Generator().manual_seed(world))
+    full, _ = p.evaluate(None, X)
+    T = 0
+    for col0, own in balanced_slices(d, min(world, d)):
+        T = T + p.partial_terms(X[:, col0 : col0 + own], col0, d, own)
+    torch.testing.assert_close(p.combine_terms(T, d), full, rtol=1e-10, atol=1e-10)

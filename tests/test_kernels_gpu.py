@@ -1084,3 +1084,24 @@ def test_cec_basic_fused_clamp_matches_where():
     assert fused[0] == 0 and fused[1] == 0
     s = nops.cec_basic(Zd * 50, SCHWEFEL, None, 0, 64).cpu()
     assert torch.equal(nops.cec_basic(Zd * 50, SCHWEFEL, None, 0, 64, clamp=0.0).cpu()[~torch.isnan(s)], s[~torch.isnan(s)])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d,world", [(32, 2), (30, 3), (1000, 8)])
+def test_sbx_pm_kernels_column_blocks(d, world):
+    """evo_ops.hip sbx / pm with (col0, dtot): every column block equals those columns of the
+    full-width kernels (both the 4-gene Philox path and the scalar path) and the CPU oracle."""
+    from evoxmi.operators import crossover, mutation
+    from evoxmi.parallel.context import balanced_slices
+
+    x = torch.rand(64, d, generator=torch.Generator().manual_seed(2)).cuda()
+    lb, ub = torch.zeros(d, device="cuda"), torch.ones(d, device="cuda")
+    key = rnd.PRNGKey(9, device="cuda")
+    full_x = crossover.simulated_binary(key, x)
+    full_m = mutation.polynomial(key, full_x, (lb, ub))
+    assert torch.allclose(full_x.cpu(), crossover.simulated_binary(key.cpu(), x.cpu()), atol=1e-5)
+    for c0, own in balanced_slices(d, world):
+        blk = crossover.simulated_binary(key, x[:, c0 : c0 + own].contiguous(), cols=(c0, d))
+        assert torch.equal(blk, full_x[:, c0 : c0 + own])
+        mb = mutation.polynomial(key, blk, (lb[c0 : c0 + own], ub[c0 : c0 + own]), cols=(c0, d))
+        assert torch.equal(mb, full_m[:, c0 : c0 + own])
