@@ -196,6 +196,8 @@ def main():
                 "mean_refine_iters": float(dev_hist[:, 2].mean()),
                 "max_refine_iters": int(dev_hist[:, 2].max()),
                 "fallbacks": int(dev_hist[:, 3].sum()),
+                # refinement iterations of each timed generation, in order
+                "iters_per_gen": "".join(str(min(int(v), 9)) if v < 10 else "+" for v in dev_hist[:, 2].tolist()),
             }
         elif hist:
             # every timed generation's decomposition: relative off-norm ‖offdiag(BᵀCB)‖/‖diag‖

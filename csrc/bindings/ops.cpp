@@ -1123,12 +1123,20 @@ void moead_halo_replace(at::Tensor& obj, const at::Tensor& off_obj, const at::Te
                          win_h.data_ptr<int>(), cur_stream());
 }
 
-void moead_halo_gather(at::Tensor& pop, const at::Tensor& slots, const at::Tensor& win_h, const at::Tensor& peer, const at::Tensor& starts) {
+void moead_halo_gather(at::Tensor& pop, const at::Tensor& slots, const at::Tensor& win_h, const at::Tensor& peer, const at::Tensor& starts,
+                       const c10::optional<at::Tensor>& first) {
   CHECK_DEV(pop); CHECK_F32(pop); CHECK_CONTIG(pop);
   TORCH_CHECK(peer.is_cuda() && peer.scalar_type() == at::kLong && starts.is_cuda() && starts.scalar_type() == at::kInt &&
                   starts.numel() == peer.numel() + 1, "moead_halo_gather: peer int64[world], starts int32[world + 1] on device");
+  int32_t* fp = nullptr;
+  int nf = 0;
+  if (first && first->defined()) {  // deduplicated: every offspring row read once, duplicates copied locally
+    TORCH_CHECK(first->is_cuda() && first->scalar_type() == at::kInt && first->is_contiguous(), "moead_halo_gather: first int32 on device");
+    fp = first->data_ptr<int>();
+    nf = (int)first->numel();
+  }
   evx_moead_halo_gather(pop.data_ptr<float>(), slots.data_ptr<int>(), win_h.data_ptr<int>(), (int)slots.numel(), peer.data_ptr<int64_t>(),
-                        starts.data_ptr<int>(), (int)peer.numel(), (int)pop.size(1), cur_stream());
+                        starts.data_ptr<int>(), (int)peer.numel(), (int)pop.size(1), cur_stream(), fp, nf);
 }
 
 // hipMalloc'd buffer (an allocation base, so its IPC handle maps exactly this tensor)
@@ -1413,7 +1421,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("moead_parents(Tensor nb, Tensor key, int row0=0, int rows=0) -> Tensor[]");
   m.def("moead_variation(Tensor pop, Tensor p0, Tensor p1, Tensor kx, Tensor km, Tensor lb, Tensor ub, float pro_c, float dis_c, float pro_m, float dis_m, int nm, int row0=0, int rows=0, Tensor? win=None, Tensor(a!)? out=None) -> Tensor");
   m.def("moead_halo_replace(Tensor(a!) obj, Tensor off_obj, Tensor W, Tensor z, Tensor zmax, Tensor rowptr, Tensor owner, Tensor slots, int func, Tensor(b!) win_h) -> ()");
-  m.def("moead_halo_gather(Tensor(a!) pop, Tensor slots, Tensor win_h, Tensor peer, Tensor starts) -> ()");
+  m.def("moead_halo_gather(Tensor(a!) pop, Tensor slots, Tensor win_h, Tensor peer, Tensor starts, Tensor(b!)? first=None) -> ()");
   m.def("ipc_alloc(int numel, int device) -> Tensor");
   m.def("ipc_handle(Tensor t) -> Tensor");
   m.def("ipc_open(Tensor handle, int device) -> int");

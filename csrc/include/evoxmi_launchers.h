@@ -226,7 +226,8 @@ void evx_sbr16_far_bq(const float* A, int n, int64_t lda, const int* perm, const
 void evx_moead_halo_replace(float* obj, const float* off_obj, const float* W, const float* z, const float* zmax, const int32_t* rowptr,
                             const int32_t* owner, const int32_t* slots, int H, int M, int func, int32_t* win_h, hipStream_t s);
 void evx_moead_halo_gather(float* pop, const int32_t* slots, const int32_t* win_h, int H, const int64_t* peer, const int32_t* starts,
-                           int world, int d, hipStream_t s);
+                           int world, int d, hipStream_t s, int32_t* first = nullptr,
+                           int N = 0);
 
 // rank-by-counting stable argsort in one launch (sort.hip), n ≤ evx_rank_argsort_max_n()
 int evx_rank_argsort_max_n();

@@ -95,23 +95,20 @@ __device__ __forceinline__ float3 rot16(float app, float aqq, float apq) {
 }
 
 // ------------------------------------------------------------------ 2. block solve
-// SB²/4 lanes per block (one wave for SB = 16, four for SB = 32).  S is double-buffered so a
-// round needs ONE barrier: every lane recomputes the rotations it uses from the read buffer
-// (lane {u ≤ v} of the 2×2-block items — SB/2·(SB/2+1)/2 of them — the pairs u and v; every
-// lane the pair of its Q column pair), forms S'[u, v] = J_uᵀ S[u, v] J_v and its transpose in
-// the write buffer, and rotates its 2×2 block of Q' = Q J in place (rows 2(L/(SB/2))+{0,1},
-// column pair L mod SB/2).  The 2×2 blocks of one round partition S and Q, so the round's
-// reads and writes never overlap; identical inputs make the redundant rotations identical.
-// (The single-buffered form — rotations on SB/2 lanes → LDS → barrier → updates → barrier —
-// spent ≈1000 cycles a round on the two LDS round trips and barriers: 26.6 µs a solve.)
+// One wave per block.  Per round: lanes 0-7 compute the 8 rotations (→ LDS), then lane
+// {u ≤ v} (36 items) forms the 2×2 blocks (u, v) and (v, u) of S' = Jᵀ S J (written as exact
+// transposes: S stays symmetric; pair u's own block set exactly), and every lane rotates a
+// 2×2 block of Q' = Q J (rows 2(L/8)+{0,1}, column pair L mod 8).  All updates are in place:
+// the 2×2 blocks of one round partition S and Q.
 template <int SB>
 __global__ void __launch_bounds__(SB * SB / 4) sbr16_block_kernel(const float* __restrict__ A, int n, int64_t lda,
                                                                   const int* __restrict__ perm, int sweeps, float* __restrict__ Q_out,
                                                                   float* __restrict__ dq_out, const int* __restrict__ skip) {
   if (skip && *skip) return;
   constexpr int SP = SB + 1, NT = SB * SB / 4;
-  __shared__ float S[2][SB * SP];
+  __shared__ float S[SB * SP];
   __shared__ float Qm[SB * SP];
+  __shared__ float4 rot[SB / 2];
   __shared__ int members[SB];
   const int lane = threadIdx.x;
   const int s0 = blockIdx.x * SB, m = min(SB, n - s0);
@@ -121,11 +118,11 @@ __global__ void __launch_bounds__(SB * SB / 4) sbr16_block_kernel(const float* _
   for (int e = lane; e < SB * SB; e += NT) {
     const int a = e / SB, c = e % SB;
     const int ra = members[a], rc = members[c];
-    S[0][a * SP + c] = (ra >= 0 && rc >= 0) ? A[(int64_t)ra * lda + rc] : 0.f;
+    S[a * SP + c] = (ra >= 0 && rc >= 0) ? A[(int64_t)ra * lda + rc] : 0.f;
     Qm[a * SP + c] = a == c ? 1.f : 0.f;
   }
   __syncthreads();
-  // item {u ≤ v} of the lane
+  // item {u ≤ v} of the lane (36 of them; lanes 36..63 only rotate Q)
   int u = 0, rem = lane;
   while (u < SB / 2 - 1 && rem >= SB / 2 - u) {
     rem -= SB / 2 - u;
@@ -138,11 +135,15 @@ __global__ void __launch_bounds__(SB * SB / 4) sbr16_block_kernel(const float* _
   const int G = (SB - 1) * sweeps;
   for (int g = 0; g < G; ++g) {
     const int r = g % (SB - 1);
-    const float* Sc = S[g & 1];
-    float* Sn = S[(g & 1) ^ 1];
+    if (lane < SB / 2) {
+      const int2 p = rr16<SB>(r, lane);
+      const float3 cs = rot16(S[p.x * SP + p.x], S[p.y * SP + p.y], S[p.x * SP + p.y]);
+      rot[lane] = make_float4(cs.x, cs.y, cs.z, 0.f);
+    }
+    __syncthreads();
     {
       const int2 pq = rr16<SB>(r, qv);
-      const float3 rq = rot16(Sc[pq.x * SP + pq.x], Sc[pq.y * SP + pq.y], Sc[pq.x * SP + pq.y]);
+      const float4 rq = rot[qv];
       const float x0 = Qm[qr * SP + pq.x], y0 = Qm[qr * SP + pq.y];
       const float x1 = Qm[(qr + 1) * SP + pq.x], y1 = Qm[(qr + 1) * SP + pq.y];
       Qm[qr * SP + pq.x] = rq.x * x0 - rq.y * y0;
@@ -152,10 +153,9 @@ __global__ void __launch_bounds__(SB * SB / 4) sbr16_block_kernel(const float* _
     }
     if (item) {
       const int2 pu = rr16<SB>(r, u), pv = rr16<SB>(r, v);
+      const float4 ru = rot[u], rv = rot[v];
       const int ux = pu.x * SP, uy = pu.y * SP, vx = pv.x * SP, vy = pv.y * SP;
-      const float3 ru = rot16(Sc[ux + pu.x], Sc[uy + pu.y], Sc[ux + pu.y]);
-      const float3 rv = dg ? ru : rot16(Sc[vx + pv.x], Sc[vy + pv.y], Sc[vx + pv.y]);
-      const float a = Sc[ux + pv.x], b = Sc[ux + pv.y], c = Sc[uy + pv.x], d = Sc[uy + pv.y];
+      const float a = S[ux + pv.x], b = S[ux + pv.y], c = S[uy + pv.x], d = S[uy + pv.y];
       // O = J_uᵀ S[u rows, v cols] J_v: columns first (p' = c·p − s·q, q' = s·p + c·q), then rows
       const float a1 = rv.x * a - rv.y * b, b1 = rv.y * a + rv.x * b;
       const float c1 = rv.x * c - rv.y * d, d1 = rv.y * c + rv.x * d;
@@ -165,24 +165,23 @@ __global__ void __launch_bounds__(SB * SB / 4) sbr16_block_kernel(const float* _
       o11 = dg ? d + ru.z * b : o11;
       o01 = dg ? 0.f : o01;
       o10 = dg ? 0.f : o10;
-      Sn[ux + pv.x] = o00;
-      Sn[ux + pv.y] = o01;
-      Sn[uy + pv.x] = o10;
-      Sn[uy + pv.y] = o11;
+      S[ux + pv.x] = o00;
+      S[ux + pv.y] = o01;
+      S[uy + pv.x] = o10;
+      S[uy + pv.y] = o11;
       if (!dg) {
-        Sn[vx + pu.x] = o00;
-        Sn[vy + pu.x] = o01;
-        Sn[vx + pu.y] = o10;
-        Sn[vy + pu.y] = o11;
+        S[vx + pu.x] = o00;
+        S[vy + pu.x] = o01;
+        S[vx + pu.y] = o10;
+        S[vy + pu.y] = o11;
       }
     }
     __syncthreads();
   }
-  const float* Sf = S[G & 1];
   float* Qo = Q_out + (int64_t)blockIdx.x * SB * SB;
 #pragma unroll
   for (int e = lane; e < SB * SB; e += NT) Qo[e] = Qm[(e / SB) * SP + (e % SB)];
-  if (lane < m) dq_out[s0 + lane] = Sf[lane * SP + lane];
+  if (lane < m) dq_out[s0 + lane] = S[lane * SP + lane];
 }
 
 // ------------------------------------------------------------------ block-diagonal tile helpers

@@ -357,15 +357,53 @@ __global__ void __launch_bounds__(256) halo_replace_kernel(float* __restrict__ o
 // halo row update: slot slots[h] takes offspring win_h[h], read straight from the memory of
 // the rank that generated it (peer[q] = that rank's offspring buffer, IPC-mapped over xGMI:
 // a direct mesh read, no collective), rows of rank q start at starts[q]
+// first[w] = INT_MAX for every offspring, then the lowest halo index that takes offspring w
+__global__ void __launch_bounds__(256) halo_first_fill_kernel(int32_t* __restrict__ first, int N) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < N) first[i] = INT_MAX;
+}
+
+__global__ void __launch_bounds__(256) halo_first_kernel(const int32_t* __restrict__ win_h, int H, int32_t* __restrict__ first, int N) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < H) {
+    const int w = win_h[i];
+    if (w >= 0 && w < N) atomicMin(first + w, i);
+  }
+}
+
+// pop[slots[h]] ← offspring win_h[h] from the generating rank's buffer.  With `first`
+// (deduplicated form) only the first halo slot taking an offspring reads it — an offspring that
+// wins several of this rank's halo slots crosses xGMI once — and dup_copy_kernel then fills the
+// other slots from that local row.
 __global__ void __launch_bounds__(256) halo_gather_kernel(float* __restrict__ pop, const int32_t* __restrict__ slots,
                                                           const int32_t* __restrict__ win_h, const int64_t* __restrict__ peer,
-                                                          const int32_t* __restrict__ starts, int world, int d) {
+                                                          const int32_t* __restrict__ starts, int world, int d,
+                                                          const int32_t* __restrict__ first) {
   const int h = blockIdx.y;
   const int w = win_h[h];
   if (w < 0) return;
+  if (first && first[w] != h) return;
   int q = 0;
   while (q + 1 < world && starts[q + 1] <= w) ++q;
   const float* src = reinterpret_cast<const float*>(peer[q]) + (int64_t)(w - starts[q]) * d;
+  float* dst = pop + (int64_t)slots[h] * d;
+  if ((d & 3) == 0) {
+    const int n4 = d >> 2;
+    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < n4; c += gridDim.x * blockDim.x)
+      reinterpret_cast<float4*>(dst)[c] = reinterpret_cast<const float4*>(src)[c];
+  } else {
+    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < d; c += gridDim.x * blockDim.x) dst[c] = src[c];
+  }
+}
+
+__global__ void __launch_bounds__(256) halo_dup_copy_kernel(float* __restrict__ pop, const int32_t* __restrict__ slots,
+                                                            const int32_t* __restrict__ win_h, const int32_t* __restrict__ first, int d) {
+  const int h = blockIdx.y;
+  const int w = win_h[h];
+  if (w < 0) return;
+  const int f = first[w];
+  if (f == h) return;
+  const float* src = pop + (int64_t)slots[f] * d;
   float* dst = pop + (int64_t)slots[h] * d;
   if ((d & 3) == 0) {
     const int n4 = d >> 2;
@@ -432,9 +470,14 @@ void evx_moead_halo_replace(float* obj, const float* off_obj, const float* W, co
 }
 
 void evx_moead_halo_gather(float* pop, const int32_t* slots, const int32_t* win_h, int H, const int64_t* peer, const int32_t* starts,
-                           int world, int d, hipStream_t s) {
+                           int world, int d, hipStream_t s, int32_t* first, int N) {
   if (H <= 0) return;
   const int q = (d & 3) == 0 ? d >> 2 : d;
   dim3 grid((q + 255) / 256 < 16 ? (q + 255) / 256 : 16, H);
-  halo_gather_kernel<<<grid, 256, 0, s>>>(pop, slots, win_h, peer, starts, world, d);
+  if (first) {
+    halo_first_fill_kernel<<<(N + 255) / 256, 256, 0, s>>>(first, N);
+    halo_first_kernel<<<(H + 255) / 256, 256, 0, s>>>(win_h, H, first, N);
+  }
+  halo_gather_kernel<<<grid, 256, 0, s>>>(pop, slots, win_h, peer, starts, world, d, first);
+  if (first) halo_dup_copy_kernel<<<grid, 256, 0, s>>>(pop, slots, win_h, first, d);
 }

@@ -263,6 +263,7 @@ class MOEAD(Algorithm):
         cache = dict(ctx=dist, start=start, size=size, halo=halo.to(torch.int32).to(dev), halo_long=halo.to(dev),
                      starts=torch.tensor(starts, dtype=torch.int32, device=dev), starts_list=starts,
                      peer=PeerBuffer(dist, rows, self.dim, dev), win_h=torch.full((halo.numel(),), -1, dtype=torch.int32, device=dev),
+                     first=torch.empty((self.pop_size,), dtype=torch.int32, device=dev),
                      offsets=torch.tensor([4 * a * self.dim for a in starts[:-1]], dtype=torch.int64, device=dev))
         self._owner_cache = cache
         return cache
@@ -344,22 +345,26 @@ class MOEAD(Algorithm):
             mo_ops.moead_halo_replace(obj, fitness, state.weight_vector, z, z_max, self._rev32[1], self._rev32[2], halo,
                                       self.func_name, win_h)
             table = ow["peer"].peer_table()
-            if getattr(dist, "backend", "") == "simulated":
-                # wire accounting of the simulated rank: halo winners generated on another rank are
-                # the rows a real rank reads over xGMI (device-side count, no host sync)
-                gen_rank = torch.bucketize(win_h.to(torch.int64), ow["starts"][1:].to(torch.int64), right=True)
-                dist.count_peer_rows(((win_h >= 0) & (gen_rank != dist.rank)).sum(), self.dim * 4)
+            first = ow["first"]
             if table is None:
                 # no device IPC (single-process simulation, gloo): the offspring of every rank
                 # as one buffer, then the same gather (pointer table built on the device:
                 # capturable)
                 full = dist.all_gather_rows(state.next_generation, self.pop_size).contiguous()
                 table = torch.full_like(ow["offsets"], full.data_ptr()) + ow["offsets"]
-                mo_ops.moead_halo_gather(pop, halo, win_h, table, ow["starts"])
+                mo_ops.moead_halo_gather(pop, halo, win_h, table, ow["starts"], first)
                 del full
             else:
-                mo_ops.moead_halo_gather(pop, halo, win_h, table, ow["starts"])
+                mo_ops.moead_halo_gather(pop, halo, win_h, table, ow["starts"], first)
                 ow["peer"].fence()
+            if getattr(dist, "backend", "") == "simulated":
+                # wire accounting of the simulated rank: the distinct offspring generated on another
+                # rank that win one of this rank's halo slots are the rows a real rank reads over
+                # xGMI (each once: the gather is deduplicated); device-side count, no host sync
+                gen_rank = torch.bucketize(win_h.to(torch.int64), ow["starts"][1:].to(torch.int64), right=True)
+                h_idx = torch.arange(win_h.numel(), device=win_h.device, dtype=torch.int32)
+                is_first = first[win_h.clamp_min(0).long()] == h_idx
+                dist.count_peer_rows(((win_h >= 0) & (gen_rank != dist.rank) & is_first).sum(), self.dim * 4)
             win = torch.full((self.pop_size,), -1, dtype=torch.int32, device=obj.device)
             win.index_copy_(0, ow["halo_long"], win_h)
         else:

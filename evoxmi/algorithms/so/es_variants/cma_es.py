@@ -123,13 +123,22 @@ class CMAES(Algorithm):
         damped steps need ≈10–12 iterations, and later generations converge in 4–7 within the
         default 8-slot schedule (profiles/r4_sbr_threshold_variants.txt).  The generation
         index is host-known, so the choice costs no device read."""
-        if self._device_eigh() and generation < int(config.get("sbr_cold_gens")):
+        if not self._device_eigh():
+            return None
+        if generation < int(config.get("sbr_cold_gens")):
             return "cold"
+        late = int(config.get("sbr_late_gens"))
+        if late > 0 and generation >= late:
+            # settled runs converge in ≤ 5 iterations: a shorter schedule drops the launch
+            # boundaries of the always-skipped tail slots
+            return "late"
         return None
 
     def graph_variant_context(self, variant):
         if variant == "cold":
             return config.override(sbr_device_iters=int(config.get("sbr_cold_iters")))
+        if variant == "late":
+            return config.override(sbr_device_iters=int(config.get("sbr_late_iters")))
         return super().graph_variant_context(variant)
 
     # ------------------------------------------------------------------ sampling
@@ -137,11 +146,11 @@ class CMAES(Algorithm):
         d = self.dim
         if (state.B.is_cuda and config.get("gemm_planes") and config.get("gemm_prec") == "x6" and config.get("plain_gemm") == "evoxmi"
                 and d % 4 == 0):
-            # B·diag(D) pre-split into its bf16x6 fragment planes once per generation (one pass, D as
-            # the column scale): the sampling GEMM splits only the noise on the fly (10k×1000×1000:
-            # 162.6 vs 174.3 µs, profiles/r4_gemm_planes.log).  gemm_planes = 2 also generates the
-            # noise straight into planes (the f32 noise is never written) — slower: the A side is
-            # then 1.5× the bytes of a load-bound loop (205 µs)
+            # opt-in (gemm_planes ≥ 1): B·diag(D) pre-split into its bf16x6 fragment planes once per
+            # generation (one pass, D as the column scale), so the sampling GEMM splits only the noise
+            # on the fly — 162.6 vs 174.3 µs alone, but no gain inside the generation (175.8 vs
+            # 172.6 µs, profiles/r4_gemm_planes.log); gemm_planes = 2 also generates the noise straight
+            # into planes (the A side of the load-bound loop grows 1.5×: 205 µs)
             from ....ops.linalg import mm_nt, normal_planes, split_planes
 
             za = normal_planes(key.to(state.B.device), rows, d, row0) if config.get("gemm_planes") >= 2 else \

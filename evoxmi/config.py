@@ -38,11 +38,14 @@ def _bool(s: str) -> bool:
 KNOBS: Dict[str, Knob] = {
     "eigh": Knob("EVOXMI_EIGH", "sbr", str, "symmetric eigensolver for CMA-ES: 'sbr' (converged: Jacobi hand-off + sorted-block refinement, ops/sbr.py), 'jacobi' (fixed-sweep warm block Jacobi) or 'torch' (rocSOLVER)"),
     "eigh_tol": Knob("EVOXMI_EIGH_TOL", 1e-5, float, "sbr: target relative off-norm ‖offdiag(BᵀCB)‖_F / ‖diag‖_F of every decomposition"),
+    "sbr_sweeps": Knob("EVOXMI_SBR_SWEEPS", 2, int, "sbr: cyclic Jacobi sweeps of the near-pair block solve per refinement iteration"),
     "sbr_block": Knob("EVOXMI_SBR_BLOCK", 32, int, "sbr: near-pair block size — 32 or 16 (blocks in a shifted sorted order, eigh_sbr16.hip; 32 converges in fewer iterations on the bench matrices) or 64 (eigh_sbr.hip)"),
     "sbr_mode": Knob("EVOXMI_SBR_MODE", "device", str, "sbr: 'device' — fixed device-controlled iteration schedule inside the generation's graph (ops/sbr_device.py, no host read); 'host' — host-driven iterations with planned solves as a host phase between graph segments (ops/sbr.py)"),
     "sbr_device_iters": Knob("EVOXMI_SBR_DEVICE_ITERS", 8, int, "sbr device mode: refinement iterations in the fixed schedule (kernels of iterations past convergence return at once)"),
     "sbr_cold_gens": Knob("EVOXMI_SBR_COLD_GENS", 4, int, "CMA-ES device eigensolver: the first generations that use the cold-start schedule (their own hipGraph; the generation index is host-known)"),
     "sbr_cold_iters": Knob("EVOXMI_SBR_COLD_ITERS", 16, int, "CMA-ES device eigensolver: refinement slots of the cold-start schedule"),
+    "sbr_late_gens": Knob("EVOXMI_SBR_LATE_GENS", 24, int, "CMA-ES: generations from this index on replay a shorter 'late' eigensolver graph of sbr_late_iters slots (0: off) — at the bench config every solve from generation ≈22 to ≈305 converges in 4 iterations (5-7 before; profiles/r4_iters_per_gen_300.txt), so 6 slots keep a margin of 2"),
+    "sbr_late_iters": Knob("EVOXMI_SBR_LATE_ITERS", 6, int, "refinement slots of the late-generation eigensolver schedule"),
     "sbr_full_slots": Knob("EVOXMI_SBR_FULL_SLOTS", 5, int, "sbr device schedule (warm, 8 slots): slots past this carry no damping / Newton–Schulz / X³ kernels (those variants are chosen only in the first iterations of a warm-started solve), so a skipped tail slot costs 7 launches fewer"),
     "sbr_near_only": Knob("EVOXMI_SBR_NEAR_ONLY", 3.0, float, "sbr: a refinement iteration skips the far step once off_rel ≤ this·tol (0: never)"),
     "sbr_theta0": Knob("EVOXMI_SBR_THETA0", 1.0, float, "sbr: local far-pair threshold factor θ in every iteration whose κ ≤ sbr_theta_kappa (0: switched on only after a stalled far iteration). θ = 1 keeps steady-state CMA-ES solves at 4 iterations where θ = 0 stalls at ≈1.3e-5 for tens of generations (profiles/r4_sbr_threshold_variants.txt)"),
@@ -53,7 +56,7 @@ KNOBS: Dict[str, Knob] = {
     "cec_stack": Knob("EVOXMI_CEC_STACK", 1, int, "CEC'22 compositions (F9–F12) on the device: every rotated component from ONE GEMM over the stacked rotations with per-block exact shifts (1) or one GEMM per component (0)"),
     "cec_fused": Knob("EVOXMI_CEC_FUSED", 0, int, "CEC'22 F1 / F4 on the device: 1 = row terms from the rotation GEMM's epilogue (rotated population never written), 0 = GEMM + basic-function kernel (default: the fused epilogue measured 7 µs slower at pop 10 000 × d 1000, profiles/r3_cec_fused_epilogue.txt)"),
     "gemm_prec": Knob("EVOXMI_GEMM_PREC", "x6", str, "framework f32 GEMMs (gemm_ks.hip): 'x6' — each f32 operand split exactly into three bf16 parts, six bf16 MFMA products (f32-accurate, 3/8 of the f32 MFMA time) — or 'f32' (v_mfma_f32_16x16x4_f32)"),
-    "gemm_planes": Knob("EVOXMI_GEMM_PLANES", 1, int, "x6 GEMMs: the d×d operand that is constant (CEC rotations) or produced once per generation (CMA-ES B·D) pre-split into bf16 fragment planes (1, default: the 10k sampling GEMM 162.6 vs 174.3 µs); 2 also generates the CMA-ES noise straight into planes (slower: the A side of the load-bound loop grows 1.5×, 205 µs); 0 splits both inside the GEMM"),
+    "gemm_planes": Knob("EVOXMI_GEMM_PLANES", 0, int, "x6 GEMMs: the d×d operand that is constant (CEC rotations) or produced once per generation (CMA-ES B·D) pre-split into bf16 fragment planes (1) — alone 162.6 vs 174.3 µs for the 10k sampling GEMM, but in the flagship generation 175.8 vs 172.6 µs (the planes leave L2 between calls) and 1.825 vs 1.811 ms/gen, so off by default; 2 also generates the CMA-ES noise into planes (205 µs); 0 splits both inside the GEMM (profiles/r4_gemm_planes.log)"),
     "plain_gemm": Knob("EVOXMI_PLAIN_GEMM", "evoxmi", str, "flagship GEMMs: 'evoxmi' (framework MFMA kernels, csrc/kernels/gemm_ks.hip) or 'blas' (hipBLASLt via torch, an A/B baseline only)"),
     "jacobi_sweeps": Knob("EVOXMI_JACOBI_SWEEPS", 2, int, "maximum warm-started Jacobi sweeps per decomposition (stops early once converged)"),
     "jacobi_tol_factor": Knob("EVOXMI_JACOBI_TOL_FACTOR", 4.0, float, "convergence: ‖offdiag‖ ≤ factor·eps_f32·sqrt(n)·‖diag‖"),

@@ -87,10 +87,13 @@ def moead_halo_replace(obj, off_obj, w, z, z_max, rowptr, owner, slots, func, wi
     _ext.ops().moead_halo_replace(obj, f32(off_obj), f32(w), f32(z), f32(z_max), rowptr, owner, slots, fid, win_h)
 
 
-def moead_halo_gather(pop, slots, win_h, peer, starts):
+def moead_halo_gather(pop, slots, win_h, peer, starts, first=None):
     """pop[slots[h]] ← offspring win_h[h] read from the generating rank's buffer (``peer``:
-    int64 device pointers, IPC-mapped; ``starts``: first offspring index of every rank)."""
-    _ext.ops().moead_halo_gather(pop, slots, win_h, peer, starts)
+    int64 device pointers, IPC-mapped; ``starts``: first offspring index of every rank).
+    ``first`` (int32[N] workspace): deduplicated — an offspring that wins several of this rank's
+    slots is read over xGMI once (into its lowest halo slot, whose index ``first[w]`` holds
+    afterwards) and copied locally to the others."""
+    _ext.ops().moead_halo_gather(pop, slots, win_h, peer, starts, first)
 
 
 def moead_replace(pop_obj, off_obj, w, z, z_max, rowptr, owner, func):
