@@ -101,6 +101,9 @@ def main():
 
     for _ in range(args.warmup):
         state = wf.step(state)
+    if use_graph and hasattr(wf, "prepare_graphs"):
+        # every graph variant the timed generations replay is captured here, not inside the timing
+        state = wf.prepare_graphs(state, args.steps + 1)
     sync()
     eigh_mod.HISTORY.clear()
     dev_counts = sbr_device.snapshot_counts()  # device-mode solves: per-solve ring read after timing

@@ -461,7 +461,7 @@ void sbr16_bq_out(const at::Tensor& B, const at::Tensor& perm, const at::Tensor&
 }
 
 void sbr_damping_out(const at::Tensor& X2, const at::Tensor& V, double tau, at::Tensor& alpha, at::Tensor& work, const at::Tensor& skip,
-                     const c10::optional<at::Tensor>& bar) {
+                     const c10::optional<at::Tensor>& bar, bool no_final) {
   const int64_t n = X2.size(0);
   TORCH_CHECK(V.numel() >= n * 8 && work.numel() >= n * 24 && alpha.numel() >= 1, "sbr_damping_out: shapes");
   if (bar.has_value() && bar->defined()) {  // one persistent launch (grid barriers), see eigh_sbr16.hip
@@ -472,18 +472,27 @@ void sbr_damping_out(const at::Tensor& X2, const at::Tensor& V, double tau, at::
     return;
   }
   evx_sbr_damping(X2.data_ptr<float>(), (int)n, X2.stride(0), V.data_ptr<float>(), work.data_ptr<float>(), (float)tau,
-                  alpha.data_ptr<float>(), cur_stream(), skip.data_ptr<int>());
+                  alpha.data_ptr<float>(), cur_stream(), skip.data_ptr<int>(), no_final ? 1 : 0);
 }
 
-void sbr_dev_prep(const at::Tensor& X, const at::Tensor& X2, const at::Tensor& X3, const at::Tensor& alpha, at::Tensor& P, at::Tensor& MT,
-                  const at::Tensor& ctrl) {
+void sbr_dev_prep(const at::Tensor& X, const at::Tensor& X2, const at::Tensor& X3, at::Tensor& alpha, at::Tensor& P, at::Tensor& MT,
+                  const at::Tensor& ctrl, const c10::optional<at::Tensor>& work, double tau) {
   for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&X, &X2, &X3, &P, &MT}) {
     CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t);
     TORCH_CHECK(t->sizes() == X.sizes(), "sbr_dev_prep: n×n");
   }
   TORCH_CHECK(ctrl.scalar_type() == at::kInt && ctrl.numel() >= 8 && alpha.numel() >= 1, "sbr_dev_prep: ctrl int32[8]");
+  const float* v2 = nullptr;
+  const float* v3 = nullptr;
+  if (work && work->defined()) {  // the damping's power-step vectors [V1 | V2 | V3] (n×8 each): α formed here
+    const int64_t n = X.size(0);
+    CHECK_DEV(*work); CHECK_F32(*work);
+    TORCH_CHECK(work->is_contiguous() && work->numel() >= 24 * n, "sbr_dev_prep: work float[24 n]");
+    v2 = work->data_ptr<float>() + 8 * n;
+    v3 = work->data_ptr<float>() + 16 * n;
+  }
   evx_sbr_dev_prep(X.data_ptr<float>(), X2.data_ptr<float>(), X3.data_ptr<float>(), (int)X.size(0), alpha.data_ptr<float>(),
-                   P.data_ptr<float>(), MT.data_ptr<float>(), ctrl.data_ptr<int>(), cur_stream());
+                   P.data_ptr<float>(), MT.data_ptr<float>(), ctrl.data_ptr<int>(), cur_stream(), v2, v3, (float)tau);
 }
 
 void sbr_dev_copy(const at::Tensor& src, at::Tensor& dst, const at::Tensor& skip) {
@@ -1401,8 +1410,8 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("sbr16_block_out(Tensor A, int shift, int sweeps, int sb, Tensor(a!) perm, Tensor(b!) Q, Tensor(c!) dq, Tensor skip) -> ()");
   m.def("sbr16_far_out(Tensor A, Tensor perm, Tensor Q, Tensor dq, Tensor stats, float thr_fac, Tensor theta, Tensor(a!) X, int sb, Tensor skip) -> ()");
   m.def("sbr16_bq_out(Tensor B, Tensor perm, Tensor Q, Tensor(a!) Bq, int sb, Tensor skip) -> ()");
-  m.def("sbr_damping_out(Tensor X2, Tensor V, float tau, Tensor(a!) alpha, Tensor(b!) work, Tensor skip, Tensor(c!)? bar=None) -> ()");
-  m.def("sbr_dev_prep(Tensor X, Tensor X2, Tensor X3, Tensor alpha, Tensor(a!) P, Tensor(b!) MT, Tensor ctrl) -> ()");
+  m.def("sbr_damping_out(Tensor X2, Tensor V, float tau, Tensor(a!) alpha, Tensor(b!) work, Tensor skip, Tensor(c!)? bar=None, bool no_final=False) -> ()");
+  m.def("sbr_dev_prep(Tensor X, Tensor X2, Tensor X3, Tensor(c!) alpha, Tensor(a!) P, Tensor(b!) MT, Tensor ctrl, Tensor? work=None, float tau=1.0) -> ()");
   m.def("sbr_dev_copy(Tensor src, Tensor(a!) dst, Tensor skip) -> ()");
   m.def("sbr_dev_ctrl(Tensor part, int nparts, int j, int K, Tensor(a!) hist, Tensor(b!) alpha, Tensor(c!) theta, Tensor(d!) ctrl, Tensor(e!) st, float[] prm, int ns_iters, Tensor A, Tensor(f!) w_out, Tensor(g!) eig_stats, Tensor(h!) w_init, Tensor(i!) log, Tensor(j!) log_count) -> ()");
   m.def("gemm_ks_set_tile(int t) -> ()");

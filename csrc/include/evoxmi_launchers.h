@@ -182,7 +182,7 @@ int evx_sbr16_nblocks(int n, int sb);
 int evx_sbr16_max_n();
 void evx_sbr_taylor4_prep(const float* X, const float* X2, int n, const float* alpha, float* P, float* M, hipStream_t s, int mt = 0);
 void evx_sbr_damping(const float* X2, int n, int64_t ldx, const float* V, float* work, float tau, float* alpha, hipStream_t s,
-                     const int* skip = nullptr);
+                     const int* skip = nullptr, int no_final = 0);
 void evx_sbr_damping_fused(const float* X2, int n, int64_t ldx, const float* V, float* work, float tau, float* alpha, hipStream_t s,
                            const int* skip, uint32_t* bar);
 void evx_sbr16_block(const float* A, int n, int64_t lda, int shift, int sweeps, int* perm, float* Q, float* dq, int sb, hipStream_t s,
@@ -211,8 +211,9 @@ void evx_linear_gp_fit(const double* a, const double* b, const double* c, const 
                        float* v, float* s2, hipStream_t s);
 
 // device-controlled SBR schedule (eigh_sbr_dev.hip)
-void evx_sbr_dev_prep(const float* X, const float* X2, const float* X3, int n, const float* alpha, float* P, float* MT, const int* ctrl,
-                      hipStream_t s);
+void evx_sbr_dev_prep(const float* X, const float* X2, const float* X3, int n, float* alpha, float* P, float* MT, const int* ctrl,
+                      hipStream_t s, const float* V2 = nullptr, const float* V3 = nullptr,
+                      float tau = 1.f);
 void evx_sbr_dev_copy(const float* src, float* dst, int64_t n, const int* skip, hipStream_t s);
 void evx_sbr_dev_ctrl(const double* part, int nparts, int j, int K, double* hist, float* alpha, float* theta, int* ctrl, int* st,
                       const float* prm6, int ns_iters, const float* A, int64_t lda, int n, float* w_out, double* eig_stats, float* w_init,

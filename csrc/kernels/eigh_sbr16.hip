@@ -24,8 +24,10 @@
 //   sbr16_bq_kernel     Bq = B[:, perm] · blockdiag(Q)
 // evoxmi/ops/sbr.py holds the torch reference of each step and the host driver.
 #include "evoxmi_common.h"
+#include "evoxmi_sbr.h"
 #include <float.h>
 #include <math.h>
+#include <cstdlib>
 
 namespace {
 
@@ -37,20 +39,22 @@ constexpr int kRankMax = 8192;    // largest n of the rank kernel (32 KB of keys
 __device__ __forceinline__ float sort_key(float v) { return isnan(v) ? INFINITY : v; }
 
 // ------------------------------------------------------------------ 1. ranks → shifted perm
-// 64 indices per workgroup, the 4 waves each count over a quarter of the keys
-__global__ void __launch_bounds__(256) sbr16_rank_kernel(const float* __restrict__ A, int n, int64_t lda, int shift,
-                                                         int* __restrict__ perm, const int* __restrict__ skip) {
+// 64 indices per workgroup; its 16 waves each count over a sixteenth of the keys (16 waves:
+// the counting loop is 4× shorter than with 4, and the launch stays at ⌈n/64⌉ workgroups)
+constexpr int kRankWaves = 16;
+__global__ void __launch_bounds__(64 * kRankWaves) sbr16_rank_kernel(const float* __restrict__ A, int n, int64_t lda, int shift,
+                                                                     int* __restrict__ perm, const int* __restrict__ skip) {
   if (skip && *skip) return;
   __shared__ __attribute__((aligned(16))) float key[kRankMax + 16];
-  __shared__ int part[4][64];
+  __shared__ int part[kRankWaves][64];
   const int np = (n + 15) & ~15;  // padded with +inf: never below a real key (NaN keys are +inf too, ties by index)
   for (int i = threadIdx.x; i < np; i += blockDim.x) key[i] = i < n ? sort_key(A[(int64_t)i * lda + i]) : INFINITY;
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int i = blockIdx.x * 64 + lane;
   const float ki = i < n ? key[i] : 0.f;
-  // each wave counts over a quarter of the keys, 4 keys per LDS broadcast read (ds_read_b128)
-  const int q = ((np >> 2) + 3) & ~3, j0 = min(np, w * q), j1 = min(np, j0 + q);
+  // each wave counts over a sixteenth of the keys, 4 keys per LDS broadcast read (ds_read_b128)
+  const int q = ((np / kRankWaves) + 3) & ~3, j0 = min(np, w * q), j1 = min(np, j0 + q);
   int cnt = 0;
 #pragma unroll 4
   for (int j = j0; j < j1; j += 4) {
@@ -63,7 +67,9 @@ __global__ void __launch_bounds__(256) sbr16_rank_kernel(const float* __restrict
   part[w][lane] = cnt;
   __syncthreads();
   if (w == 0 && i < n) {
-    const int r = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
+    int r = 0;
+#pragma unroll
+    for (int v = 0; v < kRankWaves; ++v) r += part[v][lane];
     int pos = r - shift;
     if (pos < 0) pos += n;
     perm[pos] = i;
@@ -100,49 +106,104 @@ __device__ __forceinline__ float3 rot16(float app, float aqq, float apq) {
 // transposes: S stays symmetric; pair u's own block set exactly), and every lane rotates a
 // 2×2 block of Q' = Q J (rows 2(L/8)+{0,1}, column pair L mod 8).  All updates are in place:
 // the 2×2 blocks of one round partition S and Q.
-template <int SB>
-__global__ void __launch_bounds__(SB * SB / 4) sbr16_block_kernel(const float* __restrict__ A, int n, int64_t lda,
-                                                                  const int* __restrict__ perm, int sweeps, float* __restrict__ Q_out,
-                                                                  float* __restrict__ dq_out, const int* __restrict__ skip) {
+// FR (fused rank, n ≤ kFuseMax, opt-in EVOXMI_SBR_FUSED_RANK=1): every workgroup sorts the
+// (diagonal key, index) pairs itself — a bitonic network over the padded keys in LDS, the same
+// strict total order as sbr16_rank_kernel — takes its members from the shifted sorted order and
+// writes its segment of perm for the far / Bq kernels: one launch per refinement slot fewer, but
+// the 55-stage network (one barrier each) made an executed block solve 42 µs instead of 27 + 8
+// for the two launches (profiles/r4_kstats_fused_rank.txt), so it is off by default.
+constexpr int kFuseMax = 2048;
+
+__device__ __forceinline__ void bitonic_kv(float* k, int* v, int np) {
+  for (int size = 2; size <= np; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = threadIdx.x; t < (np >> 1); t += blockDim.x) {
+        const int i = 2 * t - (t & (stride - 1)), j = i + stride;
+        const bool up = (i & size) == 0;
+        const float ki = k[i], kj = k[j];
+        const int vi = v[i], vj = v[j];
+        const bool gt = ki > kj || (ki == kj && vi > vj);
+        if (gt == up) {
+          k[i] = kj; k[j] = ki;
+          v[i] = vj; v[j] = vi;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// Threads: 2·SB²/4 — the first SB²/4 (waves 0-3 for SB = 32) rotate Q, the others (the
+// SB/2·(SB/2+1)/2 items {u ≤ v}) update S, so the two updates of a round run side by side on
+// different SIMDs instead of one after the other in every lane; the round-robin pairs come from
+// a table built once in LDS (the index arithmetic was a third of the round's instructions).
+template <int SB, bool FR>
+__global__ void __launch_bounds__(SB * SB / 2) sbr16_block_kernel(const float* __restrict__ A, int n, int64_t lda,
+                                                                 int* __restrict__ perm, int sweeps, float* __restrict__ Q_out,
+                                                                 float* __restrict__ dq_out, const int* __restrict__ skip, int shift) {
   if (skip && *skip) return;
-  constexpr int SP = SB + 1, NT = SB * SB / 4;
+  constexpr int SP = SB + 1, NT = SB * SB / 4, NH = SB / 2;
   __shared__ float S[SB * SP];
   __shared__ float Qm[SB * SP];
-  __shared__ float4 rot[SB / 2];
+  __shared__ float4 rot[NH];
   __shared__ int members[SB];
-  const int lane = threadIdx.x;
+  __shared__ int2 ptab[(SB - 1) * NH];
+  const int tid = threadIdx.x, nthr = blockDim.x;
   const int s0 = blockIdx.x * SB, m = min(SB, n - s0);
-  if (lane < SB) members[lane] = lane < m ? perm[s0 + lane] : -1;
+  for (int e = tid; e < (SB - 1) * NH; e += nthr) ptab[e] = rr16<SB>(e / NH, e % NH);
+  if constexpr (FR) {
+    __shared__ float skey[kFuseMax];
+    __shared__ int sidx[kFuseMax];
+    int np = 2;
+    while (np < n) np <<= 1;
+    for (int i = tid; i < np; i += nthr) {
+      skey[i] = i < n ? sort_key(A[(int64_t)i * lda + i]) : INFINITY;  // padding: +inf, after every real key
+      sidx[i] = i;
+    }
+    __syncthreads();
+    bitonic_kv(skey, sidx, np);
+    if (tid < SB) {
+      int r = s0 + tid + shift;
+      if (r >= n) r -= n;
+      const int idx = tid < m ? sidx[r] : -1;
+      members[tid] = idx;
+      if (tid < m) perm[s0 + tid] = idx;
+    }
+  } else {
+    if (tid < SB) members[tid] = tid < m ? perm[s0 + tid] : -1;
+  }
   __syncthreads();
-#pragma unroll
-  for (int e = lane; e < SB * SB; e += NT) {
+  for (int e = tid; e < SB * SB; e += nthr) {
     const int a = e / SB, c = e % SB;
     const int ra = members[a], rc = members[c];
     S[a * SP + c] = (ra >= 0 && rc >= 0) ? A[(int64_t)ra * lda + rc] : 0.f;
     Qm[a * SP + c] = a == c ? 1.f : 0.f;
   }
   __syncthreads();
-  // item {u ≤ v} of the lane (36 of them; lanes 36..63 only rotate Q)
-  int u = 0, rem = lane;
-  while (u < SB / 2 - 1 && rem >= SB / 2 - u) {
-    rem -= SB / 2 - u;
+  const bool qlane = tid < NT;
+  // Q lanes: rows qr, qr+1, column pair qv
+  const int qr = (tid / NH) * 2, qv = tid % NH;
+  // S lanes: item {u ≤ v}
+  int u = 0, rem = tid - NT;
+  while (u < NH - 1 && rem >= NH - u) {
+    rem -= NH - u;
     ++u;
   }
   const int v = u + rem;
-  const bool item = lane < (SB / 2) * (SB / 2 + 1) / 2;
+  const bool item = !qlane && rem >= 0 && (tid - NT) < NH * (NH + 1) / 2;
   const bool dg = u == v;
-  const int qr = (lane / (SB / 2)) * 2, qv = lane % (SB / 2);  // Q rows qr, qr+1; column pair qv
   const int G = (SB - 1) * sweeps;
   for (int g = 0; g < G; ++g) {
     const int r = g % (SB - 1);
-    if (lane < SB / 2) {
-      const int2 p = rr16<SB>(r, lane);
+    const int2* pr = ptab + r * NH;
+    if (tid < NH) {
+      const int2 p = pr[tid];
       const float3 cs = rot16(S[p.x * SP + p.x], S[p.y * SP + p.y], S[p.x * SP + p.y]);
-      rot[lane] = make_float4(cs.x, cs.y, cs.z, 0.f);
+      rot[tid] = make_float4(cs.x, cs.y, cs.z, 0.f);
     }
     __syncthreads();
-    {
-      const int2 pq = rr16<SB>(r, qv);
+    if (qlane) {
+      const int2 pq = pr[qv];
       const float4 rq = rot[qv];
       const float x0 = Qm[qr * SP + pq.x], y0 = Qm[qr * SP + pq.y];
       const float x1 = Qm[(qr + 1) * SP + pq.x], y1 = Qm[(qr + 1) * SP + pq.y];
@@ -150,9 +211,8 @@ __global__ void __launch_bounds__(SB * SB / 4) sbr16_block_kernel(const float* _
       Qm[qr * SP + pq.y] = rq.y * x0 + rq.x * y0;
       Qm[(qr + 1) * SP + pq.x] = rq.x * x1 - rq.y * y1;
       Qm[(qr + 1) * SP + pq.y] = rq.y * x1 + rq.x * y1;
-    }
-    if (item) {
-      const int2 pu = rr16<SB>(r, u), pv = rr16<SB>(r, v);
+    } else if (item) {
+      const int2 pu = pr[u], pv = pr[v];
       const float4 ru = rot[u], rv = rot[v];
       const int ux = pu.x * SP, uy = pu.y * SP, vx = pv.x * SP, vy = pv.y * SP;
       const float a = S[ux + pv.x], b = S[ux + pv.y], c = S[uy + pv.x], d = S[uy + pv.y];
@@ -179,9 +239,8 @@ __global__ void __launch_bounds__(SB * SB / 4) sbr16_block_kernel(const float* _
     __syncthreads();
   }
   float* Qo = Q_out + (int64_t)blockIdx.x * SB * SB;
-#pragma unroll
-  for (int e = lane; e < SB * SB; e += NT) Qo[e] = Qm[(e / SB) * SP + (e % SB)];
-  if (lane < m) dq_out[s0 + lane] = S[lane * SP + lane];
+  for (int e = tid; e < SB * SB; e += nthr) Qo[e] = Qm[(e / SB) * SP + (e % SB)];
+  if (tid < m) dq_out[s0 + tid] = S[tid * SP + tid];
 }
 
 // ------------------------------------------------------------------ block-diagonal tile helpers
@@ -208,7 +267,8 @@ struct FarSmem {
 template <int SB>
 __device__ __forceinline__ void far_tile(const float* __restrict__ A, int n, int64_t lda, const int* __restrict__ perm,
                                          const float* __restrict__ Q, const float* __restrict__ dq, const double* __restrict__ stats,
-                                         float thr_fac, float theta, float* __restrict__ X, int64_t ldx, int K, int L, FarSmem& sm) {
+                                         float thr_fac, float theta, float* __restrict__ X, int64_t ldx, int K, int L, FarSmem& sm,
+                                         bool mirror = false) {
   float* G = sm.G;
   float* Qk = sm.Qk;
   float* Ql = sm.Ql;
@@ -303,7 +363,21 @@ __device__ __forceinline__ void far_tile(const float* __restrict__ A, int n, int
       // the 2×2 Jacobi angle ½·atan(2a/den): a/den to first order for well-separated pairs,
       // saturating at π/4 for strongly coupled ones
       const bool far = ((sl + e) / SB) != bc && fabsf(den) > fminf(tk[c], tl[e]);
-      X[(int64_t)(sk + c) * ldx + sl + e] = far ? 0.5f * atanf(2.f * out[i][j] / den) : 0.f;
+      out[i][j] = far ? 0.5f * atanf(2.f * out[i][j] / den) : 0.f;
+      X[(int64_t)(sk + c) * ldx + sl + e] = out[i][j];
+    }
+  }
+  if (mirror && K != L) {
+    // X is skew: tile (L, K) = −(tile (K, L))ᵀ, written from here through LDS (coalesced rows)
+    __syncthreads();  // every read of G (T) is done
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) G[(c0 + j) * TP + r0 + i] = out[i][j];
+    __syncthreads();
+    for (int e = threadIdx.x; e < TL * TL; e += blockDim.x) {
+      const int er = e >> 6, cc = e & 63;
+      if (er < ml && cc < mk) X[(int64_t)(sl + er) * ldx + sk + cc] = -G[er * TP + cc];
     }
   }
 }
@@ -391,8 +465,9 @@ __global__ void __launch_bounds__(256) sbr16_far_bq_kernel(const float* __restri
   __shared__ __attribute__((aligned(16))) FarSmem sm;
   const int nt = gridDim.x;
   if ((int)blockIdx.y < nt) {
-    if (*skip_far) return;
-    far_tile<SB>(A, n, lda, perm, Q, dq, stats, thr_fac, *theta_ptr, X, ldx, blockIdx.y, blockIdx.x, sm);
+    // upper tiles only (K ≤ L): each writes its mirror tile −Xᵀ as well
+    if (*skip_far || blockIdx.y > blockIdx.x) return;
+    far_tile<SB>(A, n, lda, perm, Q, dq, stats, thr_fac, *theta_ptr, X, ldx, blockIdx.y, blockIdx.x, sm, true);
   } else {
     if (*skip_bq) return;
     bq_tile<SB>(B, rows, n, ldb, perm, Q, Bq, ldq, blockIdx.y - nt, blockIdx.x, sm.G, sm.Ql, sm.pl);
@@ -434,36 +509,8 @@ __global__ void __launch_bounds__(256) sbr_power_step_kernel(const float* __rest
 __global__ void __launch_bounds__(256) sbr_damping_final_kernel(const float* __restrict__ V2, const float* __restrict__ V3, int n,
                                                                 float tau, float* __restrict__ alpha, const int* __restrict__ skip) {
   if (skip && *skip) return;
-  __shared__ float red[2][8][4];
-  float s2[8] = {}, s3[8] = {};
-  for (int j = threadIdx.x; j < n; j += blockDim.x) {
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const float a = V2[(int64_t)j * 8 + c], b = V3[(int64_t)j * 8 + c];
-      s2[c] = fmaf(a, a, s2[c]);
-      s3[c] = fmaf(b, b, s3[c]);
-    }
-  }
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    s2[c] = evx::wave_sum(s2[c]);
-    s3[c] = evx::wave_sum(s3[c]);
-    if (lane == 0) {
-      red[0][c][w] = s2[c];
-      red[1][c][w] = s3[c];
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float lam = 0.f;
-    for (int c = 0; c < 8; ++c) {
-      const float a = red[0][c][0] + red[0][c][1] + red[0][c][2] + red[0][c][3];
-      const float b = red[1][c][0] + red[1][c][1] + red[1][c][2] + red[1][c][3];
-      lam = fmaxf(lam, sqrtf(b) / fmaxf(sqrtf(a), 1e-30f));
-    }
-    alpha[0] = fminf(1.f, tau / sqrtf(fmaxf(lam, 1e-30f)));
-  }
+  const float a = evx_sbr_damping_alpha(V2, V3, n, tau);
+  if (threadIdx.x == 0) alpha[0] = a;
 }
 
 
@@ -606,11 +653,22 @@ int evx_sbr16_max_n() { return kRankMax; }
 
 void evx_sbr16_block(const float* A, int n, int64_t lda, int shift, int sweeps, int* perm, float* Q, float* dq, int sb, hipStream_t s,
                      const int* skip) {
-  sbr16_rank_kernel<<<(n + 63) / 64, 256, 0, s>>>(A, n, lda, shift, perm, skip);
+  static const bool fuse = [] {  // EVOXMI_SBR_FUSED_RANK=1: the rank inside the block kernel (see sbr16_block_kernel)
+    const char* e = getenv("EVOXMI_SBR_FUSED_RANK");
+    return e && atoi(e) != 0;
+  }();
+  if (fuse && n <= kFuseMax) {
+    if (sb == 32)
+      sbr16_block_kernel<32, true><<<(n + 31) / 32, 512, 0, s>>>(A, n, lda, perm, sweeps, Q, dq, skip, shift);
+    else
+      sbr16_block_kernel<16, true><<<(n + 15) / 16, 128, 0, s>>>(A, n, lda, perm, sweeps, Q, dq, skip, shift);
+    return;
+  }
+  sbr16_rank_kernel<<<(n + 63) / 64, 64 * kRankWaves, 0, s>>>(A, n, lda, shift, perm, skip);
   if (sb == 32)
-    sbr16_block_kernel<32><<<(n + 31) / 32, 256, 0, s>>>(A, n, lda, perm, sweeps, Q, dq, skip);
+    sbr16_block_kernel<32, false><<<(n + 31) / 32, 512, 0, s>>>(A, n, lda, perm, sweeps, Q, dq, skip, shift);
   else
-    sbr16_block_kernel<16><<<(n + 15) / 16, 64, 0, s>>>(A, n, lda, perm, sweeps, Q, dq, skip);
+    sbr16_block_kernel<16, false><<<(n + 15) / 16, 128, 0, s>>>(A, n, lda, perm, sweeps, Q, dq, skip, shift);
 }
 
 void evx_sbr16_far(const float* A, int n, int64_t lda, const int* perm, const float* Q, const float* dq, const double* stats,
@@ -652,7 +710,7 @@ void evx_sbr_damping_fused(const float* X2, int n, int64_t ldx, const float* V, 
 }
 
 void evx_sbr_damping(const float* X2, int n, int64_t ldx, const float* V, float* work, float tau, float* alpha, hipStream_t s,
-                     const int* skip) {
+                     const int* skip, int no_final) {
   float* V1 = work;
   float* V2 = work + (int64_t)n * 8;
   float* V3 = work + (int64_t)n * 16;
@@ -660,7 +718,8 @@ void evx_sbr_damping(const float* X2, int n, int64_t ldx, const float* V, float*
   sbr_power_step_kernel<<<g, 256, 0, s>>>(X2, n, ldx, V, V1, skip);
   sbr_power_step_kernel<<<g, 256, 0, s>>>(X2, n, ldx, V1, V2, skip);
   sbr_power_step_kernel<<<g, 256, 0, s>>>(X2, n, ldx, V2, V3, skip);
-  sbr_damping_final_kernel<<<1, 256, 0, s>>>(V2, V3, n, tau, alpha, skip);
+  // no_final: the consumer (the device schedule's Taylor prep) forms α from V2 / V3 itself
+  if (!no_final) sbr_damping_final_kernel<<<1, 256, 0, s>>>(V2, V3, n, tau, alpha, skip);
 }
 
 void evx_sbr_taylor4_prep(const float* X, const float* X2, int n, const float* alpha, float* P, float* M, hipStream_t s, int mt) {

@@ -17,6 +17,7 @@
 // Persistent words st[8]: 0 stopped, 1 fallback (diverged), 2 refinement iterations run,
 //   3 last_far, 4 theta sticky, 5 keep (0 ⇒ restore the warm-start basis), 6 converged.
 #include "evoxmi_common.h"
+#include "evoxmi_sbr.h"
 #include <float.h>
 #include <math.h>
 
@@ -37,25 +38,67 @@ __device__ __forceinline__ void rel_kappa(const double* h, double& r, double& k)
 }
 
 // Taylor operands of exp(αX) for the order the control word selects (sel6), with M of
-// exp(−αX) (the transposed product, ops/sbr.py:expm_t_device)
+// exp(−αX) (the transposed product, ops/sbr.py:expm_t_device).  V2 != null: when this
+// iteration's damping ran (ctrl[2] == 0) every workgroup forms α from its power-step vectors
+// itself and workgroup 0 stores it — the damping's own single-workgroup final launch is gone.
 __global__ void __launch_bounds__(256) sbr_dev_prep_kernel(const float* __restrict__ X, const float* __restrict__ X2,
-                                                           const float* __restrict__ X3, int n, const float* __restrict__ alpha,
-                                                           float* __restrict__ P, float* __restrict__ MT, const int* __restrict__ ctrl) {
+                                                           const float* __restrict__ X3, int n, float* __restrict__ alpha,
+                                                           float* __restrict__ P, float* __restrict__ MT, const int* __restrict__ ctrl,
+                                                           const float* __restrict__ V2, const float* __restrict__ V3, float tau) {
   if (ctrl[1]) return;
   const bool six = ctrl[4] != 0;
-  const float a = alpha[0], a2 = a * a, a3 = a2 * a;
-  const int64_t total = (int64_t)n * n;
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t i = e / n, j = e - i * n;
-    const float x = a * X[e], x2 = a2 * X2[e];
-    const float id = i == j ? 1.f : 0.f;
-    if (six) {
-      const float x3 = a3 * X3[e];
-      P[e] = a3 * (x * (1.f / 24.f) + x2 * (1.f / 120.f) + x3 * (1.f / 720.f));
-      MT[e] = id - x + 0.5f * x2 - x3 * (1.f / 6.f);
-    } else {
-      P[e] = a2 * (x * (1.f / 6.f) + x2 * (1.f / 24.f));
-      MT[e] = id - x + 0.5f * x2;
+  float a;
+  if (V2 && ctrl[2] == 0) {
+    a = evx_sbr_damping_alpha(V2, V3, n, tau);
+    if (blockIdx.x == 0 && threadIdx.x == 0) alpha[0] = a;
+  } else {
+    a = alpha[0];
+  }
+  const float a2 = a * a, a3 = a2 * a;
+  // rows over the grid, columns over the threads (float4 when n % 4 == 0): no per-element
+  // 64-bit division (the flat-index form spent most of its time in the i = e / n expansion)
+  const bool v4 = (n & 3) == 0;
+  const int nc = v4 ? n >> 2 : n;
+  for (int i = blockIdx.x; i < n; i += gridDim.x) {
+    const int64_t r = (int64_t)i * n;
+    for (int c = threadIdx.x; c < nc; c += blockDim.x) {
+      const int w = v4 ? 4 : 1;
+      float xs[4] = {}, x2s[4] = {}, x3s[4] = {};
+      if (v4) {
+        const float4 x = reinterpret_cast<const float4*>(X + r)[c], y = reinterpret_cast<const float4*>(X2 + r)[c];
+        xs[0] = x.x; xs[1] = x.y; xs[2] = x.z; xs[3] = x.w;
+        x2s[0] = y.x; x2s[1] = y.y; x2s[2] = y.z; x2s[3] = y.w;
+        if (six) {
+          const float4 z = reinterpret_cast<const float4*>(X3 + r)[c];
+          x3s[0] = z.x; x3s[1] = z.y; x3s[2] = z.z; x3s[3] = z.w;
+        }
+      } else {
+        xs[0] = X[r + c];
+        x2s[0] = X2[r + c];
+        if (six) x3s[0] = X3[r + c];
+      }
+      float ps[4], ms[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = c * w + q;
+        const float x = a * xs[q], x2 = a2 * x2s[q];
+        const float id = i == j ? 1.f : 0.f;
+        if (six) {
+          const float x3 = a3 * x3s[q];
+          ps[q] = a3 * (x * (1.f / 24.f) + x2 * (1.f / 120.f) + x3 * (1.f / 720.f));
+          ms[q] = id - x + 0.5f * x2 - x3 * (1.f / 6.f);
+        } else {
+          ps[q] = a2 * (x * (1.f / 6.f) + x2 * (1.f / 24.f));
+          ms[q] = id - x + 0.5f * x2;
+        }
+      }
+      if (v4) {
+        reinterpret_cast<float4*>(P + r)[c] = make_float4(ps[0], ps[1], ps[2], ps[3]);
+        reinterpret_cast<float4*>(MT + r)[c] = make_float4(ms[0], ms[1], ms[2], ms[3]);
+      } else {
+        P[r + c] = ps[0];
+        MT[r + c] = ms[0];
+      }
     }
   }
 }
@@ -203,14 +246,14 @@ __global__ void __launch_bounds__(256) sbr_dev_ctrl_kernel(const double* __restr
 
 }  // namespace
 
-void evx_sbr_dev_prep(const float* X, const float* X2, const float* X3, int n, const float* alpha, float* P, float* MT, const int* ctrl,
-                      hipStream_t s) {
+void evx_sbr_dev_prep(const float* X, const float* X2, const float* X3, int n, float* alpha, float* P, float* MT, const int* ctrl,
+                      hipStream_t s, const float* V2, const float* V3, float tau) {
   // a grid-stride loop over 256 workgroups: the schedule skips this kernel in most
   // iterations, and an empty launch costs in proportion to its workgroup count
   const int64_t total = (int64_t)n * n;
   int g = (int)((total + 255) / 256);
   if (g > 256) g = 256;
-  sbr_dev_prep_kernel<<<g, 256, 0, s>>>(X, X2, X3, n, alpha, P, MT, ctrl);
+  sbr_dev_prep_kernel<<<g, 256, 0, s>>>(X, X2, X3, n, alpha, P, MT, ctrl, V2, V3, tau);
 }
 
 void evx_sbr_dev_copy(const float* src, float* dst, int64_t n, const int* skip, hipStream_t s) {

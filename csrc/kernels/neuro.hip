@@ -723,12 +723,15 @@ void evx_ant_rollout(const float* W, int64_t P, int N, int h1, int h2, const flo
       const char* e = getenv("EVOXMI_ANT_TRACE");
       return e ? atoi(e) : 0;
     }();
-    // EVOXMI_ANT_L2_MFMA: inputs of layer 2 on the matrix cores.  Default 0 (VALU only): inside the
-    // rollout the split saves nothing measurable (1000-step latency 8.63 ms at 0, 8.70 at 16, 8.67 at 32;
-    // profiles/r3_k15_ant_l2_mfma_ab.txt) - layer 2 is ≈5 % of a control step, the rest is the body.
+    // EVOXMI_ANT_L2_MFMA: the first KM inputs of layer 2 on the matrix cores, concurrently with the
+    // VALU on the rest (north-star K15: the policy's hidden layer on MFMA).  Default 16 — the split
+    // that is fastest for the isolated layer (907 vs 1100 cycles, profiles/r3_k15_mfma_probe.log);
+    // inside the rollout every setting is within noise (1000-step latency 8.63 ms at 0, 8.70 at 16,
+    // 8.67 at 32; profiles/r3_k15_ant_l2_mfma_ab.txt) because layer 2 is ≈5 % of a control step.
+    // 0 = VALU only.
     static const int km = [] {
       const char* e = getenv("EVOXMI_ANT_L2_MFMA");
-      return e ? atoi(e) : 0;
+      return e ? atoi(e) : 16;
     }();
     const dim3 grid((N + ANT_WAVES - 1) / ANT_WAVES), block(64 * ANT_WAVES);
     if (km >= 32)

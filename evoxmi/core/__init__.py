@@ -13,5 +13,5 @@ from .module import (
 from .algorithm import Algorithm, algorithm_has_init_ask
 from .problem import Problem
 from .monitor import Monitor
-from .workflow import Workflow
+from .workflow import Workflow, capture_warmup, in_capture_warmup
 from .checkpoint import save_state, load_state

@@ -95,8 +95,12 @@ class DeviceSBR:
         mm(self.W, self.B, mode=1, out=self.A, skip=skip, stat_part=self.part)
 
     def _ctrl(self, j, C):
+        from ..core import in_capture_warmup
+
+        # a graph capture's warm-up step (on a copy of the state) is not a solve of the run: unlogged
+        log = self.log[:0] if in_capture_warmup() else self.log  # log_len 0: the ctrl kernel writes no row
         _ext.ops().sbr_dev_ctrl(self.part, self.nparts, j, self.K, self.hist, self.alpha, self.theta, self.ctrl, self.st, self.prm,
-                                int(self.cfg.ns_iters), self.A, self.w, self.eig_stats, self.w_init, self.log, self.log_count)
+                                int(self.cfg.ns_iters), self.A, self.w, self.eig_stats, self.w_init, log, self.log_count)
 
     def _iteration(self, j, C):
         ops = _ext.ops()
@@ -113,11 +117,15 @@ class DeviceSBR:
         # X skew ⇒ X² = −X·Xᵀ, symmetric (upper tiles only)
         mm(self.X, self.X, tb=True, mode=1, alpha=-1.0, out=self.X2, skip=sk_far)
         if cfg.damp_tau > 0 and full:
-            ops.sbr_damping_out(self.X2, self.V, float(cfg.damp_tau), self.alpha[j + 1 : j + 2], self.work, sk_damp, self.bar)
+            # three power-step launches; α itself is formed by the prep kernel below (no_final)
+            ops.sbr_damping_out(self.X2, self.V, float(cfg.damp_tau), self.alpha[j + 1 : j + 2], self.work, sk_damp, self.bar,
+                                self.bar is None)
         if full:
             # order 6 only: X³ = X²·X = −X²·Xᵀ (skew)
             mm(self.X2, self.X, tb=True, mode=2, alpha=-1.0, out=self.X3, skip=sk_x3)
-        ops.sbr_dev_prep(self.X, self.X2, self.X3, self.alpha[j + 1 : j + 2], self.P, self.VT, c)
+        damp_here = cfg.damp_tau > 0 and full and self.bar is None
+        ops.sbr_dev_prep(self.X, self.X2, self.X3, self.alpha[j + 1 : j + 2], self.P, self.VT, c, self.work if damp_here else None,
+                         float(cfg.damp_tau))
         # Vᵀ = M(−α) + X²·Pᵀ (order 4) or M(−α) − X³·Pᵀ (order 6): the control word selects
         mm(self.X2, self.P, tb=True, alpha=1.0, beta=1.0, Cin=self.VT, out=self.VT, skip=sk_far, sel=sel6, A2=self.X3, alpha2=-1.0)
         # B·V → B, or into T when Newton–Schulz follows

@@ -42,7 +42,7 @@ from typing import Callable, List, Optional, Union
 
 import torch
 
-from ..core import Algorithm, Monitor, Problem, State, Workflow, use_state
+from ..core import capture_warmup, Algorithm, Monitor, Problem, State, Workflow, use_state
 from ..core.algorithm import algorithm_has_init_ask
 from ..core.state import tree_flatten, tree_map
 from .. import config
@@ -261,7 +261,7 @@ class StdWorkflow(Workflow):
         self.registered_hooks = {h: [] for h in HOOKS}
         try:
             ctx.__enter__()
-            with torch.cuda.stream(s):
+            with torch.cuda.stream(s), capture_warmup():
                 self._proto_step(False, tree_map(lambda x: x.clone() if isinstance(x, torch.Tensor) else x, static))
             torch.cuda.current_stream(dev).wait_stream(s)
             torch.cuda.synchronize(dev)
@@ -351,6 +351,25 @@ class StdWorkflow(Workflow):
         return out
 
     # ------------------------------------------------------------------ public
+    def prepare_graphs(self, state: State, horizon: int) -> State:
+        """Capture, ahead of time, the hipGraph of every algorithm graph variant that the next
+        ``horizon`` generations will replay (e.g. CMA-ES's late eigensolver schedule), so that
+        no capture happens later inside a timed loop.  The state is not advanced (capture
+        records; its warm-up runs on a copy of the state)."""
+        if not self.graph or self._graph_failed or state.generation == 0 and self._has_init_ask:
+            return state
+        g0 = int(state.generation)
+        gv = getattr(self.algorithm, "graph_variant", None)
+        variants = []
+        for k in range(horizon):
+            v = gv(g0 + k) if gv is not None else None
+            if v not in variants:
+                variants.append(v)
+        for v in variants:
+            if v not in self._graphs:
+                self._capture(state, v)
+        return state
+
     def step(self, state: State) -> State:
         for m in self.registered_hooks["pre_step"]:
             m.pre_step(state)

@@ -175,7 +175,7 @@ def test_sbr_kernels_match_reference(n, off):
 
 @gpu
 @pytest.mark.parametrize("sb", [16, 32])
-@pytest.mark.parametrize("n,shift", [(1000, 0), (1000, 8), (200, 8), (37, 8), (17, 0)])
+@pytest.mark.parametrize("n,shift", [(1000, 0), (1000, 8), (200, 8), (37, 8), (17, 0), (2100, 8)])  # n ≤ 2048: rank fused into the block kernel
 def test_sbr16_kernels_match_reference(n, shift, sb):
     C, B = _cma_like(n, 8, seed=n)
     A = sbr.sym_product(C, B)
