@@ -360,6 +360,7 @@ at::Tensor philox_normal_planes(const at::Tensor& key, int64_t rows, int64_t d, 
 
 void gemm_ks_set_tile(int64_t t) { evx_gemm_ks_set_tile((int)t); }
 void gemm_ks_set_prec(int64_t p) { evx_gemm_ks_set_prec((int)p); }
+void gemm_ks_set_nw8(int64_t t) { evx_gemm_ks_set_nw8((int)t); }
 
 at::Tensor gemm_ks_new(const at::Tensor& A, int64_t a_kc, const at::Tensor& B, int64_t b_kc, int64_t M, int64_t N, int64_t K,
                        int64_t mode, double alpha, const c10::optional<at::Tensor>& alpha_ptr,
@@ -441,7 +442,8 @@ void sbr16_far_out(const at::Tensor& A, const at::Tensor& perm, const at::Tensor
 
 void sbr16_far_bq_out(const at::Tensor& A, const at::Tensor& perm, const at::Tensor& Q, const at::Tensor& dq, const at::Tensor& stats,
                       double thr_fac, const at::Tensor& theta, at::Tensor& X, const at::Tensor& B, at::Tensor& Bq, int64_t sb,
-                      const at::Tensor& skip_far, const at::Tensor& skip_bq) {
+                      const at::Tensor& skip_far, const at::Tensor& skip_bq, bool pre) {
+  // pre: A = A[perm, perm] and B = B[:, perm] already (sbr16_permute_out)
   const int64_t n = A.size(0);
   TORCH_CHECK(X.sizes() == A.sizes() && X.stride(1) == 1 && A.stride(1) == 1 && stats.scalar_type() == at::kDouble &&
                   theta.scalar_type() == at::kFloat, "sbr16_far_bq_out: generator shapes");
@@ -451,7 +453,22 @@ void sbr16_far_bq_out(const at::Tensor& A, const at::Tensor& perm, const at::Ten
   evx_sbr16_far_bq(A.data_ptr<float>(), (int)n, A.stride(0), perm.data_ptr<int>(), Q.data_ptr<float>(), dq.data_ptr<float>(),
                    stats.data_ptr<double>(), (float)thr_fac, theta.data_ptr<float>(), X.data_ptr<float>(), X.stride(0), B.data_ptr<float>(),
                    (int)B.size(0), B.stride(0), Bq.data_ptr<float>(), Bq.stride(0), (int)sb, cur_stream(), skip_far.data_ptr<int>(),
-                   skip_bq.data_ptr<int>());
+                   skip_bq.data_ptr<int>(), pre);
+}
+
+void sbr16_permute_out(const at::Tensor& A, const at::Tensor& perm, const at::Tensor& B, at::Tensor& Ap, at::Tensor& Bp,
+                       const at::Tensor& skip_a, const at::Tensor& skip_b) {
+  const int64_t n = A.size(0);
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&A, &B, &Ap, &Bp}) {
+    CHECK_DEV(*t); CHECK_F32(*t);
+    TORCH_CHECK(t->dim() == 2 && t->size(1) == n && t->stride(1) == 1, "sbr16_permute_out: (·, n) row-major");
+  }
+  TORCH_CHECK(A.size(0) == n && Ap.size(0) == n && Ap.stride(0) == n && Bp.sizes() == B.sizes() && Bp.stride(0) == n &&
+                  n <= evx_sbr16_max_n() && perm.scalar_type() == at::kInt && perm.numel() >= n,
+              "sbr16_permute_out: shapes");
+  TORCH_CHECK(skip_a.scalar_type() == at::kInt && skip_b.scalar_type() == at::kInt, "sbr16_permute_out: skip words int32");
+  evx_sbr16_permute(A.data_ptr<float>(), (int)n, A.stride(0), perm.data_ptr<int>(), B.data_ptr<float>(), (int)B.size(0), B.stride(0),
+                    Ap.data_ptr<float>(), Bp.data_ptr<float>(), cur_stream(), skip_a.data_ptr<int>(), skip_b.data_ptr<int>());
 }
 void sbr16_bq_out(const at::Tensor& B, const at::Tensor& perm, const at::Tensor& Q, at::Tensor& Bq, int64_t sb, const at::Tensor& skip) {
   const int64_t n = B.size(1);
@@ -1416,10 +1433,12 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("sbr_dev_ctrl(Tensor part, int nparts, int j, int K, Tensor(a!) hist, Tensor(b!) alpha, Tensor(c!) theta, Tensor(d!) ctrl, Tensor(e!) st, float[] prm, int ns_iters, Tensor A, Tensor(f!) w_out, Tensor(g!) eig_stats, Tensor(h!) w_init, Tensor(i!) log, Tensor(j!) log_count) -> ()");
   m.def("gemm_ks_set_tile(int t) -> ()");
   m.def("gemm_ks_set_prec(int prec) -> ()");
+  m.def("gemm_ks_set_nw8(int tiles) -> ()");
   m.def("gemm_ks_pl(Tensor? A, Tensor? a_pl, Tensor? B, Tensor? b_pl, int M, int N, int K, float alpha, Tensor? alpha_ptr, Tensor? bias_n, Tensor(a!)? out, Tensor? a_sub_k, int sub_cols=0, int sub_ld=0) -> Tensor");
   m.def("split_planes(Tensor X, Tensor? colscale) -> Tensor");
   m.def("philox_normal_planes(Tensor key, int rows, int d, int row0) -> Tensor");
-  m.def("sbr16_far_bq_out(Tensor A, Tensor perm, Tensor Q, Tensor dq, Tensor stats, float thr_fac, Tensor theta, Tensor(a!) X, Tensor B, Tensor(b!) Bq, int sb, Tensor skip_far, Tensor skip_bq) -> ()");
+  m.def("sbr16_far_bq_out(Tensor A, Tensor perm, Tensor Q, Tensor dq, Tensor stats, float thr_fac, Tensor theta, Tensor(a!) X, Tensor B, Tensor(b!) Bq, int sb, Tensor skip_far, Tensor skip_bq, bool pre=False) -> ()");
+  m.def("sbr16_permute_out(Tensor A, Tensor perm, Tensor B, Tensor(a!) Ap, Tensor(b!) Bp, Tensor skip_a, Tensor skip_b) -> ()");
   m.def("lsmop_g(Tensor X, int[] start, int[] sublen, int[] func, int nk, int cosine) -> Tensor");
   m.def("cma_delta_gemv(Tensor M, Tensor mean, Tensor dm, float cm) -> Tensor[]");
   m.def("cma_center_rows(Tensor pop, Tensor? rows, Tensor mean, Tensor sigma, Tensor w) -> Tensor");
@@ -1459,10 +1478,12 @@ TORCH_LIBRARY_IMPL(evoxmi, CompositeExplicitAutograd, m) {
   m.impl("gemm_set_config", &gemm_set_config);
   m.impl("gemm_ks_set_tile", &gemm_ks_set_tile);
   m.impl("gemm_ks_set_prec", &gemm_ks_set_prec);
+  m.impl("gemm_ks_set_nw8", &gemm_ks_set_nw8);
   m.impl("gemm_ks_pl", &gemm_ks_pl);
   m.impl("split_planes", &split_planes);
   m.impl("philox_normal_planes", &philox_normal_planes);
   m.impl("sbr16_far_bq_out", &sbr16_far_bq_out);
+  m.impl("sbr16_permute_out", &sbr16_permute_out);
   m.impl("gemm_ks_grid", &gemm_ks_grid);
   m.impl("gemm_ks_tile", &gemm_ks_tile);
   m.impl("ipc_alloc", &ipc_alloc);

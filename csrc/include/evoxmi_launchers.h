@@ -92,6 +92,7 @@ int evx_gemm_ks_tile(int M, int N, int mode);
 void evx_gemm_ks_set_tile(int t);
 // 1: bf16x6 split products on the bf16 matrix pipe (default), 0: f32 MFMA
 void evx_gemm_ks_set_prec(int prec);
+void evx_gemm_ks_set_nw8(int tiles);  // 8-wave workgroups for grids of at most this many tiles
 int evx_gemm_ks_prec();
 void evx_cma_center_rows(const float* pop, int64_t ldp, const int32_t* rows, const float* mean, const float* sigma, const float* w, int K,
                          int d, float* Y, hipStream_t s);
@@ -221,7 +222,9 @@ void evx_sbr_dev_ctrl(const double* part, int nparts, int j, int K, double* hist
 // far generator + Bq in one launch (skip_far / skip_bq: their control words)
 void evx_sbr16_far_bq(const float* A, int n, int64_t lda, const int* perm, const float* Q, const float* dq, const double* stats,
                       float thr_fac, const float* theta_ptr, float* X, int64_t ldx, const float* B, int rows, int64_t ldb, float* Bq,
-                      int64_t ldq, int sb, hipStream_t s, const int* skip_far, const int* skip_bq);
+                      int64_t ldq, int sb, hipStream_t s, const int* skip_far, const int* skip_bq, bool pre = false);
+void evx_sbr16_permute(const float* A, int n, int64_t lda, const int* perm, const float* B, int rows, int64_t ldb, float* Ap, float* Bp,
+                       hipStream_t s, const int* skip_a, const int* skip_b);
 
 // owner-computes MOEA/D (moead.hip)
 void evx_moead_halo_replace(float* obj, const float* off_obj, const float* W, const float* z, const float* zmax, const int32_t* rowptr,

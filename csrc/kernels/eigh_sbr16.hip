@@ -268,7 +268,7 @@ template <int SB>
 __device__ __forceinline__ void far_tile(const float* __restrict__ A, int n, int64_t lda, const int* __restrict__ perm,
                                          const float* __restrict__ Q, const float* __restrict__ dq, const double* __restrict__ stats,
                                          float thr_fac, float theta, float* __restrict__ X, int64_t ldx, int K, int L, FarSmem& sm,
-                                         bool mirror = false) {
+                                         bool mirror = false, bool pre = false) {
   float* G = sm.G;
   float* Qk = sm.Qk;
   float* Ql = sm.Ql;
@@ -310,8 +310,12 @@ __device__ __forceinline__ void far_tile(const float* __restrict__ A, int n, int
   __syncthreads();
   for (int e = threadIdx.x; e < TL * TL; e += blockDim.x) {
     const int a = e >> 6, f = e & 63;
-    const int ra = pk[a], rf = pl[f];
-    G[a * TP + f] = (ra >= 0 && rf >= 0) ? A[(int64_t)ra * lda + rf] : 0.f;
+    if (pre) {  // A already in the shifted sorted order (sbr16_permute_kernel): a contiguous tile
+      G[a * TP + f] = (a < mk && f < ml) ? A[(int64_t)(sk + a) * lda + sl + f] : 0.f;
+    } else {
+      const int ra = pk[a], rf = pl[f];
+      G[a * TP + f] = (ra >= 0 && rf >= 0) ? A[(int64_t)ra * lda + rf] : 0.f;
+    }
   }
   __syncthreads();
   const int r0 = (threadIdx.x >> 4) << 2, c0 = (threadIdx.x & 15) << 2;
@@ -398,7 +402,7 @@ __global__ void __launch_bounds__(256) sbr16_far_kernel(const float* __restrict_
 template <int SB>
 __device__ __forceinline__ void bq_tile(const float* __restrict__ B, int rows, int n, int64_t ldb, const int* __restrict__ perm,
                                         const float* __restrict__ Q, float* __restrict__ Bq, int64_t ldq, int rt, int L, float* G,
-                                        float* Ql, int* pl) {
+                                        float* Ql, int* pl, bool pre = false) {
   const int nb = (n + SB - 1) / SB;
   const int sl = L * TL, ml = min(TL, n - sl);
   if (threadIdx.x < TL) pl[threadIdx.x] = threadIdx.x < ml ? perm[sl + threadIdx.x] : -1;
@@ -406,8 +410,13 @@ __device__ __forceinline__ void bq_tile(const float* __restrict__ B, int rows, i
   __syncthreads();
   for (int e = threadIdx.x; e < TL * TL; e += blockDim.x) {
     const int r = e >> 6, f = e & 63;
-    const int row = rt * TL + r, col = pl[f];
-    G[r * TP + f] = (row < rows && col >= 0) ? B[(int64_t)row * ldb + col] : 0.f;
+    const int row = rt * TL + r;
+    if (pre) {  // B's columns already permuted: a contiguous tile
+      G[r * TP + f] = (row < rows && f < ml) ? B[(int64_t)row * ldb + sl + f] : 0.f;
+    } else {
+      const int col = pl[f];
+      G[r * TP + f] = (row < rows && col >= 0) ? B[(int64_t)row * ldb + col] : 0.f;
+    }
   }
   __syncthreads();
   const int r0 = (threadIdx.x >> 4) << 2, c0 = (threadIdx.x & 15) << 2;
@@ -455,22 +464,46 @@ __global__ void __launch_bounds__(256) sbr16_bq_kernel(const float* __restrict__
 // perm / Q, so the (nt × nt) far tiles and the (row tiles × nt) Bq tiles run side by side —
 // one launch boundary fewer per refinement iteration, and the Bq tiles fill the CUs the far
 // tiles leave idle.  skip_far / skip_bq: the two parts' own control words.
+// Ap = A[perm, perm] and Bp = B[:, perm] (the shifted sorted order of this iteration), one row
+// per workgroup: the source row is read once, coalesced, into LDS and gathered from there, so the
+// generator / Bq tiles read contiguous 64×64 tiles instead of 64 scattered columns per row (each
+// touching ≈28 of a 4 KB row's 32 cache lines: ≈14× the useful bytes).
+__global__ void __launch_bounds__(256) sbr16_permute_kernel(const float* __restrict__ A, int n, int64_t lda, const int* __restrict__ perm,
+                                                            const float* __restrict__ B, int rows, int64_t ldb, float* __restrict__ Ap,
+                                                            float* __restrict__ Bp, const int* __restrict__ skip_a,
+                                                            const int* __restrict__ skip_b) {
+  __shared__ __attribute__((aligned(16))) float row[kRankMax];
+  const int i = blockIdx.x;
+  const bool isA = i < n;
+  if (isA ? (skip_a && *skip_a) : (skip_b && *skip_b)) return;
+  const float* src = isA ? A + (int64_t)perm[i] * lda : B + (int64_t)(i - n) * ldb;
+  float* dst = isA ? Ap + (int64_t)i * n : Bp + (int64_t)(i - n) * n;
+  if ((n & 3) == 0 && ((isA ? lda : ldb) & 3) == 0) {
+    for (int c = threadIdx.x; c < (n >> 2); c += blockDim.x) reinterpret_cast<float4*>(row)[c] = reinterpret_cast<const float4*>(src)[c];
+  } else {
+    for (int c = threadIdx.x; c < n; c += blockDim.x) row[c] = src[c];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < n; c += blockDim.x) dst[c] = row[perm[c]];
+}
+
 template <int SB>
 __global__ void __launch_bounds__(256) sbr16_far_bq_kernel(const float* __restrict__ A, int n, int64_t lda, const int* __restrict__ perm,
                                                            const float* __restrict__ Q, const float* __restrict__ dq,
                                                            const double* __restrict__ stats, float thr_fac,
                                                            const float* __restrict__ theta_ptr, float* __restrict__ X, int64_t ldx,
                                                            const float* __restrict__ B, int rows, int64_t ldb, float* __restrict__ Bq,
-                                                           int64_t ldq, const int* __restrict__ skip_far, const int* __restrict__ skip_bq) {
+                                                           int64_t ldq, const int* __restrict__ skip_far, const int* __restrict__ skip_bq,
+                                                           bool pre) {
   __shared__ __attribute__((aligned(16))) FarSmem sm;
   const int nt = gridDim.x;
   if ((int)blockIdx.y < nt) {
     // upper tiles only (K ≤ L): each writes its mirror tile −Xᵀ as well
     if (*skip_far || blockIdx.y > blockIdx.x) return;
-    far_tile<SB>(A, n, lda, perm, Q, dq, stats, thr_fac, *theta_ptr, X, ldx, blockIdx.y, blockIdx.x, sm, true);
+    far_tile<SB>(A, n, lda, perm, Q, dq, stats, thr_fac, *theta_ptr, X, ldx, blockIdx.y, blockIdx.x, sm, true, pre);
   } else {
     if (*skip_bq) return;
-    bq_tile<SB>(B, rows, n, ldb, perm, Q, Bq, ldq, blockIdx.y - nt, blockIdx.x, sm.G, sm.Ql, sm.pl);
+    bq_tile<SB>(B, rows, n, ldb, perm, Q, Bq, ldq, blockIdx.y - nt, blockIdx.x, sm.G, sm.Ql, sm.pl, pre);
   }
 }
 
@@ -690,17 +723,22 @@ void evx_sbr16_bq(const float* B, int rows, int n, int64_t ldb, const int* perm,
     sbr16_bq_kernel<16><<<dim3(nt, (rows + TL - 1) / TL), 256, 0, s>>>(B, rows, n, ldb, perm, Q, Bq, ldq, skip);
 }
 
+void evx_sbr16_permute(const float* A, int n, int64_t lda, const int* perm, const float* B, int rows, int64_t ldb, float* Ap, float* Bp,
+                       hipStream_t s, const int* skip_a, const int* skip_b) {
+  sbr16_permute_kernel<<<n + rows, 256, 0, s>>>(A, n, lda, perm, B, rows, ldb, Ap, Bp, skip_a, skip_b);
+}
+
 void evx_sbr16_far_bq(const float* A, int n, int64_t lda, const int* perm, const float* Q, const float* dq, const double* stats,
                       float thr_fac, const float* theta_ptr, float* X, int64_t ldx, const float* B, int rows, int64_t ldb, float* Bq,
-                      int64_t ldq, int sb, hipStream_t s, const int* skip_far, const int* skip_bq) {
+                      int64_t ldq, int sb, hipStream_t s, const int* skip_far, const int* skip_bq, bool pre) {
   const int nt = (n + TL - 1) / TL, rt = (rows + TL - 1) / TL;
   const dim3 grid(nt, nt + rt);
   if (sb == 32)
     sbr16_far_bq_kernel<32><<<grid, 256, 0, s>>>(A, n, lda, perm, Q, dq, stats, thr_fac, theta_ptr, X, ldx, B, rows, ldb, Bq, ldq, skip_far,
-                                                 skip_bq);
+                                                 skip_bq, pre);
   else
     sbr16_far_bq_kernel<16><<<grid, 256, 0, s>>>(A, n, lda, perm, Q, dq, stats, thr_fac, theta_ptr, X, ldx, B, rows, ldb, Bq, ldq, skip_far,
-                                                 skip_bq);
+                                                 skip_bq, pre);
 }
 
 void evx_sbr_damping_fused(const float* X2, int n, int64_t ldx, const float* V, float* work, float tau, float* alpha, hipStream_t s,

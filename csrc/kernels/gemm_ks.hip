@@ -219,8 +219,12 @@ __device__ __forceinline__ void decode_tile(int bid, int tiles_m, int tiles_n, i
 // PREC 1: bf16x6 (KH = 2: a 32-k group is one 16x16x32 bf16 step — lane (r, q) holds
 // fragment element j ↔ k = 32·group + 16·(j >> 2) + 4q + (j & 3), the same k map for A and B,
 // so the f32 path's loads are reused unchanged).
-template <int TM, int TN, int KH, bool AKC, bool BKC, int MODE, int PREC, int PL = 0>
-__global__ void __launch_bounds__(256) gemm_ks_kernel(EvxGemmKs p) {
+// NW: waves per workgroup, each owning 1/NW of K.  8 for grids that cannot fill the chip twice
+// (the 1000³ eigensolver products: 256 tiles for 256 CUs): two waves per SIMD, so one wave's loads
+// are in flight while the other computes; the first 4 waves then run the 4-wave epilogue.
+template <int TM, int TN, int KH, bool AKC, bool BKC, int MODE, int PREC, int PL = 0, int NW = 4>
+__global__ void __launch_bounds__(64 * NW) gemm_ks_kernel(EvxGemmKs p) {
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   static_assert(PREC == 0 || KH == 2, "bf16x6 groups hold two float4 per lane and block");
   static_assert(PL == 0 || (PREC == 1 && AKC && BKC), "fragment planes: bf16x6 on 16x16x32, K-contiguous operands");
   constexpr bool APL = PL & 1, BPL = PL & 2;
@@ -244,7 +248,7 @@ __global__ void __launch_bounds__(256) gemm_ks_kernel(EvxGemmKs p) {
   constexpr int P = (BN % 32 == 16) ? BN : BN + 16;
   // two partial-tile buffers (the four K-partials are summed pairwise): 40 KB for a 64 × 64
   // tile, so LDS never limits residency below what the registers allow
-  __shared__ __attribute__((aligned(16))) float red[2 * BM * P];
+  __shared__ __attribute__((aligned(16))) float red[(NW == 8 ? 4 : 2) * BM * P];
 
   int tm, tn;
   decode_tile<MODE>(evx::xcd_remap(blockIdx.x, gridDim.x), p.tiles_m, p.tiles_n, tm, tn);
@@ -260,7 +264,7 @@ __global__ void __launch_bounds__(256) gemm_ks_kernel(EvxGemmKs p) {
   // this wave's K range in full KG-groups (wave 0 has the fewest and also takes the tail)
   const int K = p.K;
   const int ngf = K / KG;
-  const int g0 = (w * ngf) >> 2, g1 = ((w + 1) * ngf) >> 2;
+  const int g0 = (w * ngf) / NW, g1 = ((w + 1) * ngf) / NW;
 
   const float* ap[NA];
   const float* bp[NB];
@@ -477,7 +481,23 @@ __global__ void __launch_bounds__(256) gemm_ks_kernel(EvxGemmKs p) {
 #pragma unroll
         for (int e = 0; e < NE; ++e) my[elem(i, j, e)] = acc[i][j][e];
   };
-  if (w >= 2) park(w - 2);
+  if constexpr (NW == 8) {  // 8 → 4: waves 4-7 park, waves 0-3 add (fixed order)
+    if (w >= 4) park(w - 4);
+    __syncthreads();
+    if (w < 4) {
+      const float* his = red + w * BM * P;
+#pragma unroll
+      for (int i = 0; i < NA; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j)
+#pragma unroll
+          for (int e = 0; e < NE; ++e) acc[i][j][e] += his[elem(i, j, e)];
+    }
+    __syncthreads();
+  }
+  // the epilogue below runs on the first 256 threads (waves 4-7 only meet its barriers)
+  const bool epi = threadIdx.x < 256;
+  if (w >= 2 && w < 4) park(w - 2);
   __syncthreads();
   if (w < 2) {
     const float* his = red + w * BM * P;
@@ -504,7 +524,7 @@ __global__ void __launch_bounds__(256) gemm_ks_kernel(EvxGemmKs p) {
 #pragma unroll
   for (int v = 0; v < PER; ++v) {
     const int e = threadIdx.x + 256 * v;
-    if (e < NV4) {
+    if (epi && e < NV4) {
       const int row = e / (BN / 4), c = (e % (BN / 4)) * 4;
       float4 t = *reinterpret_cast<const float4*>(&red[row * P + c]);
       {
@@ -601,7 +621,7 @@ __global__ void __launch_bounds__(256) gemm_ks_kernel(EvxGemmKs p) {
         rt2[v] += row_ror(rt2[v], m);
       }
     }
-    if ((threadIdx.x & 15) == 0) {
+    if (epi && (threadIdx.x & 15) == 0) {
 #pragma unroll
       for (int v = 0; v < PER; ++v) {
         const int gr = m0 + (threadIdx.x + 256 * v) / (BN / 4);
@@ -616,7 +636,7 @@ __global__ void __launch_bounds__(256) gemm_ks_kernel(EvxGemmKs p) {
     st_mn = evx::wave_min(st_mn);
     st_mx = evx::wave_max(st_mx);
     __shared__ double s_st[4][4];
-    if (lane == 0) {
+    if (lane == 0 && w < 4) {
       s_st[w][0] = st_off;
       s_st[w][1] = st_dg;
       s_st[w][2] = st_mn;
@@ -638,7 +658,7 @@ __global__ void __launch_bounds__(256) gemm_ks_kernel(EvxGemmKs p) {
 #pragma unroll
   for (int v = 0; v < PER; ++v) {
     const int e = threadIdx.x + 256 * v;
-    if (e < NV4) {
+    if (epi && e < NV4) {
       const int row = e / (BN / 4), c = (e % (BN / 4)) * 4;
       *reinterpret_cast<float4*>(&red[row * P + c]) = out[v];
     }
@@ -646,7 +666,7 @@ __global__ void __launch_bounds__(256) gemm_ks_kernel(EvxGemmKs p) {
   __syncthreads();
   const float sgn = MODE == 2 ? -1.f : 1.f;
   const bool diag = tm == tn;
-  for (int e = threadIdx.x; e < BM * BN; e += 256) {
+  for (int e = threadIdx.x; e < BM * BN; e += 64 * NW) {
     const int rr = e % BM, cc = e / BM;
     const int gr = n0 + cc, gc = m0 + rr;
     if (gr < p.N && gc < p.M && (!diag || rr < cc)) p.C[(int64_t)gr * p.ldc + gc] = sgn * red[rr * P + cc];
@@ -659,14 +679,29 @@ __global__ void __launch_bounds__(256) gemm_ks_kernel(EvxGemmKs p) {
 
 int g_ks_prec = 1;  // 1: bf16x6 on 16x16x32 (default), 2: bf16x6 on 32x32x16 where the tile allows, 0: f32 MFMA
 
+template <int TM, int TN, int MODE, int PREC, int NW>
+void launch_prec_nw(const EvxGemmKs& a, int tiles, hipStream_t s) {
+  constexpr int KH = PREC >= 1 ? 2 : EVX_KS_KH;
+  const dim3 grid(tiles), block(64 * NW);
+  if (a.a_kc && a.b_kc) gemm_ks_kernel<TM, TN, KH, true, true, MODE, PREC, 0, NW><<<grid, block, 0, s>>>(a);
+  else if (a.a_kc && !a.b_kc) gemm_ks_kernel<TM, TN, KH, true, false, MODE, PREC, 0, NW><<<grid, block, 0, s>>>(a);
+  else if (!a.a_kc && a.b_kc) gemm_ks_kernel<TM, TN, KH, false, true, MODE, PREC, 0, NW><<<grid, block, 0, s>>>(a);
+  else gemm_ks_kernel<TM, TN, KH, false, false, MODE, PREC, 0, NW><<<grid, block, 0, s>>>(a);
+}
+
+// 8-wave workgroups for grids of at most this many tiles whose K gives every wave ≥ 12 k-groups
+// (0: never).  Measured (tools/bench_gemm.py, profiles/r4_gemm_nw8.log): the 1000×1000×5000
+// rank-μ product 55.8 → 47.8 µs and the 1000³ symmetric TN 17.9 → 16.8, but the short-K 1000³
+// full products slower (NT 24.4 → 51.7: 4 k-groups per wave leave the prefetch pipeline empty)
+int g_ks_nw8_tiles = 384;
+constexpr int kNw8MinK = 3072;
+
 template <int TM, int TN, int MODE, int PREC>
 void launch_prec(const EvxGemmKs& a, int tiles, hipStream_t s) {
-  constexpr int KH = PREC >= 1 ? 2 : EVX_KS_KH;
-  const dim3 grid(tiles), block(256);
-  if (a.a_kc && a.b_kc) gemm_ks_kernel<TM, TN, KH, true, true, MODE, PREC><<<grid, block, 0, s>>>(a);
-  else if (a.a_kc && !a.b_kc) gemm_ks_kernel<TM, TN, KH, true, false, MODE, PREC><<<grid, block, 0, s>>>(a);
-  else if (!a.a_kc && a.b_kc) gemm_ks_kernel<TM, TN, KH, false, true, MODE, PREC><<<grid, block, 0, s>>>(a);
-  else gemm_ks_kernel<TM, TN, KH, false, false, MODE, PREC><<<grid, block, 0, s>>>(a);
+  if constexpr (TM <= 4 && TN <= 4) {
+    if (tiles <= g_ks_nw8_tiles && a.K >= kNw8MinK) return launch_prec_nw<TM, TN, MODE, PREC, 8>(a, tiles, s);
+  }
+  launch_prec_nw<TM, TN, MODE, PREC, 4>(a, tiles, s);
 }
 
 template <int TM, int TN, int MODE>
@@ -764,6 +799,8 @@ int g_ks_tile_override = 0;
 void evx_gemm_ks_set_tile(int t) { g_ks_tile_override = t; }
 
 void evx_gemm_ks_set_prec(int prec) { g_ks_prec = prec; }
+
+void evx_gemm_ks_set_nw8(int tiles) { g_ks_nw8_tiles = tiles; }
 
 void evx_split_planes(const float* X, int64_t ld, int64_t rows, int K, const float* colscale, uint16_t* out, int64_t kp, hipStream_t s) {
   const int64_t total = rows * (kp / 32) * 4;

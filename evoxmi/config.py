@@ -38,6 +38,7 @@ def _bool(s: str) -> bool:
 KNOBS: Dict[str, Knob] = {
     "eigh": Knob("EVOXMI_EIGH", "sbr", str, "symmetric eigensolver for CMA-ES: 'sbr' (converged: Jacobi hand-off + sorted-block refinement, ops/sbr.py), 'jacobi' (fixed-sweep warm block Jacobi) or 'torch' (rocSOLVER)"),
     "eigh_tol": Knob("EVOXMI_EIGH_TOL", 1e-5, float, "sbr: target relative off-norm ‖offdiag(BᵀCB)‖_F / ‖diag‖_F of every decomposition"),
+    "sbr_prepermute": Knob("EVOXMI_SBR_PREPERMUTE", 0, int, "device eigensolver: gather A[perm, perm] and B[:, perm] row-wise before the far / Bq tiles (1) — measured no faster (far+Bq 30.0 vs 28 µs, plus 6 µs for the gather)"),
     "sbr_sweeps": Knob("EVOXMI_SBR_SWEEPS", 2, int, "sbr: cyclic Jacobi sweeps of the near-pair block solve per refinement iteration"),
     "sbr_block": Knob("EVOXMI_SBR_BLOCK", 32, int, "sbr: near-pair block size — 32 or 16 (blocks in a shifted sorted order, eigh_sbr16.hip; 32 converges in fewer iterations on the bench matrices) or 64 (eigh_sbr.hip)"),
     "sbr_mode": Knob("EVOXMI_SBR_MODE", "device", str, "sbr: 'device' — fixed device-controlled iteration schedule inside the generation's graph (ops/sbr_device.py, no host read); 'host' — host-driven iterations with planned solves as a host phase between graph segments (ops/sbr.py)"),
@@ -56,6 +57,7 @@ KNOBS: Dict[str, Knob] = {
     "cec_stack": Knob("EVOXMI_CEC_STACK", 1, int, "CEC'22 compositions (F9–F12) on the device: every rotated component from ONE GEMM over the stacked rotations with per-block exact shifts (1) or one GEMM per component (0)"),
     "cec_fused": Knob("EVOXMI_CEC_FUSED", 0, int, "CEC'22 F1 / F4 on the device: 1 = row terms from the rotation GEMM's epilogue (rotated population never written), 0 = GEMM + basic-function kernel (default: the fused epilogue measured 7 µs slower at pop 10 000 × d 1000, profiles/r3_cec_fused_epilogue.txt)"),
     "gemm_prec": Knob("EVOXMI_GEMM_PREC", "x6", str, "framework f32 GEMMs (gemm_ks.hip): 'x6' — each f32 operand split exactly into three bf16 parts, six bf16 MFMA products (f32-accurate, 3/8 of the f32 MFMA time) — or 'f32' (v_mfma_f32_16x16x4_f32)"),
+    "gemm_nw8_tiles": Knob("EVOXMI_GEMM_NW8_TILES", 384, int, "gemm_ks: grids of at most this many 64×64 (or smaller) tiles with K ≥ 3072 run 8-wave workgroups (K split 8 ways, two waves per SIMD: one wave's loads overlap the other's MFMAs; the rank-μ product 55.8 → 47.8 µs); 0 = always 4 waves"),
     "gemm_planes": Knob("EVOXMI_GEMM_PLANES", 0, int, "x6 GEMMs: the d×d operand that is constant (CEC rotations) or produced once per generation (CMA-ES B·D) pre-split into bf16 fragment planes (1) — alone 162.6 vs 174.3 µs for the 10k sampling GEMM, but in the flagship generation 175.8 vs 172.6 µs (the planes leave L2 between calls) and 1.825 vs 1.811 ms/gen, so off by default; 2 also generates the CMA-ES noise into planes (205 µs); 0 splits both inside the GEMM (profiles/r4_gemm_planes.log)"),
     "plain_gemm": Knob("EVOXMI_PLAIN_GEMM", "evoxmi", str, "flagship GEMMs: 'evoxmi' (framework MFMA kernels, csrc/kernels/gemm_ks.hip) or 'blas' (hipBLASLt via torch, an A/B baseline only)"),
     "jacobi_sweeps": Knob("EVOXMI_JACOBI_SWEEPS", 2, int, "maximum warm-started Jacobi sweeps per decomposition (stops early once converged)"),

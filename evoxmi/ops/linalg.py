@@ -131,7 +131,7 @@ def plain_nt(A: torch.Tensor, B: torch.Tensor, alpha: float = 1.0, bias_n: Optio
 
 
 _PREC = {"x6": 1, "x6w": 2, "f32": 0}
-_prec_set = [None]
+_prec_set = [None, None]
 
 
 def _sync_prec():
@@ -144,6 +144,10 @@ def _sync_prec():
             raise ValueError(f"EVOXMI_GEMM_PREC must be one of {sorted(_PREC)}, got {p!r}")
         _ext.ops().gemm_ks_set_prec(_PREC[p])
         _prec_set[0] = p
+    t = config.get("gemm_nw8_tiles")
+    if t != _prec_set[1]:
+        _ext.ops().gemm_ks_set_nw8(int(t))
+        _prec_set[1] = t
 
 
 def mm(A: torch.Tensor, B: torch.Tensor, *, ta: bool = False, tb: bool = False, mode: int = 0, alpha: float = 1.0,

@@ -62,6 +62,11 @@ class DeviceSBR:
 
         (self.A, self.B, self.T, self.W, self.X, self.X2, self.X3, self.P, self.VT, self.Bq,
          self.G) = (mat() for _ in range(11))
+        from .. import config
+
+        # opt-in: A[perm, perm] and B[:, perm] gathered row-wise first (measured no faster)
+        self.prepermute = bool(config.get("sbr_prepermute"))
+        self.Ap, self.Bp = (mat(), mat()) if self.prepermute else (None, None)
         sb = cfg.block
         nb = -(-n // sb)
         self.perm = torch.zeros(n, dtype=torch.int32, device=dev)
@@ -112,8 +117,15 @@ class DeviceSBR:
         full = j < self.lean_from
         ops.sbr16_block_out(self.A, shift, int(cfg.block_sweeps), sb, self.perm, self.Q, self.dq, sk_all)
         # far generator X and Bq = B[:, perm]·blockdiag(Q) in one launch
-        ops.sbr16_far_bq_out(self.A, self.perm, self.Q, self.dq, self.hist[4 * j : 4 * j + 4], float(cfg.thr_fac),
-                             self.theta[j : j + 1], self.X, self.B, self.Bq, sb, sk_far, sk_all)
+        if self.prepermute:
+            # A[perm, perm] and B[:, perm] row by row first, so that the tiles read contiguous blocks —
+            # far+Bq 30.0 instead of 28 µs plus 6 µs for the gather (profiles/NOTES.md): off by default
+            ops.sbr16_permute_out(self.A, self.perm, self.B, self.Ap, self.Bp, sk_far, sk_all)
+            ops.sbr16_far_bq_out(self.Ap, self.perm, self.Q, self.dq, self.hist[4 * j : 4 * j + 4], float(cfg.thr_fac),
+                                 self.theta[j : j + 1], self.X, self.Bp, self.Bq, sb, sk_far, sk_all, True)
+        else:
+            ops.sbr16_far_bq_out(self.A, self.perm, self.Q, self.dq, self.hist[4 * j : 4 * j + 4], float(cfg.thr_fac),
+                                 self.theta[j : j + 1], self.X, self.B, self.Bq, sb, sk_far, sk_all)
         # X skew ⇒ X² = −X·Xᵀ, symmetric (upper tiles only)
         mm(self.X, self.X, tb=True, mode=1, alpha=-1.0, out=self.X2, skip=sk_far)
         if cfg.damp_tau > 0 and full:
@@ -170,8 +182,11 @@ _WS = {}
 
 
 def workspace(n: int, device, cfg: SBRConfig, iters: int, lean_from: int = None) -> DeviceSBR:
+    from .. import config
+
     key = (n, str(device), cfg.block, cfg.block_sweeps, cfg.thr_fac, cfg.ns_iters, cfg.damp_tau, cfg.tol, cfg.ns_kappa,
-           cfg.damp_kappa, cfg.t4_kappa, cfg.near_only, cfg.theta0, cfg.theta_kappa, int(iters), lean_from)
+           cfg.damp_kappa, cfg.t4_kappa, cfg.near_only, cfg.theta0, cfg.theta_kappa, int(iters), lean_from,
+           bool(config.get("sbr_prepermute")))
     if key not in _WS:
         _WS[key] = DeviceSBR(n, device, cfg, iters, lean_from)
     return _WS[key]
