@@ -1343,6 +1343,18 @@ at::Tensor nsga_select(const at::Tensor& rank, const at::Tensor& f, int64_t N, i
 }  // namespace
 
 // OpenES gradient with Philox-regenerated noise: g[j] = Σ_i w[i] ε(row0 + i, j)
+at::Tensor es_population(const at::Tensor& key, const at::Tensor& center, double sigma, int64_t rows, int64_t half, int64_t row0) {
+  CHECK_DEV(key); CHECK_DEV(center); CHECK_F32(center); CHECK_CONTIG(center);
+  TORCH_CHECK(key.scalar_type() == at::kLong && key.numel() == 2 && key.is_contiguous(), "es_population: key int64[2]");
+  TORCH_CHECK(center.dim() == 1 && rows >= 0 && half >= 0 && row0 >= 0, "es_population: center (d,)");
+  c10::DeviceGuard g(center.device());
+  const int64_t d = center.size(0);
+  auto out = at::empty({rows, d}, center.options());
+  if (rows > 0 && d > 0)
+    evx_es_population(key.data_ptr<int64_t>(), center.data_ptr<float>(), (float)sigma, rows, d, half, row0, out.data_ptr<float>(), cur_stream());
+  return out;
+}
+
 at::Tensor es_noise_grad(const at::Tensor& key, const at::Tensor& w, int64_t d, int64_t row0) {
   check_key(key);
   CHECK_DEV(w); CHECK_F32(w); CHECK_CONTIG(w);
@@ -1396,6 +1408,7 @@ at::Tensor hv_contrib(const at::Tensor& S, const at::Tensor& P, const at::Tensor
 
 TORCH_LIBRARY(evoxmi, m) {
   m.def("es_noise_grad(Tensor key, Tensor w, int d, int row0) -> Tensor");
+  m.def("es_population(Tensor key, Tensor center, float sigma, int rows, int half, int row0) -> Tensor");
   m.def("knn(Tensor X, Tensor Y, int T) -> Tensor[]");
   m.def("hv_count(Tensor S, Tensor P, int strict) -> Tensor");
   m.def("hv_contrib(Tensor S, Tensor P, Tensor count, Tensor alpha) -> Tensor");
@@ -1541,6 +1554,7 @@ TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
   m.impl("sbr_far", &sbr_far);
   m.impl("sbr_bq", &sbr_bq);
   m.impl("es_noise_grad", &es_noise_grad);
+  m.impl("es_population", &es_population);
   m.impl("knn", &knn);
   m.impl("hv_count", &hv_count);
   m.impl("hv_contrib", &hv_contrib);

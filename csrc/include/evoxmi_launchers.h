@@ -118,6 +118,8 @@ void evx_jacobi_apply_solve(float* A, float* B, int np, const int* sched_t, cons
                             hipStream_t s);
 void evx_jacobi_check(const float* A, int np, double* part, int* flag, double tol2, double* last_off, hipStream_t s);
 int evx_jacobi_parts();
+void evx_es_population(const int64_t* key, const float* center, float sigma, int64_t rows, int64_t d, int64_t half, int64_t row0, float* out,
+                       hipStream_t s);
 void evx_es_noise_grad(const int64_t* key, const float* w, int64_t rows, int64_t d, int64_t row0, int chunks, float* partial,
                        hipStream_t s);
 void evx_philox_words(const int64_t* key, int64_t nblocks, uint32_t domain, int64_t offset, int64_t* out, hipStream_t s,

@@ -113,3 +113,57 @@ void evx_es_noise_grad(const int64_t* key, const float* w, int64_t rows, int64_t
   const dim3 grid((unsigned)((d + 255) / 256), (unsigned)chunks);
   es_noise_grad_kernel<<<grid, 256, 0, s>>>(key, w, rows, d, row0, per, partial);
 }
+
+// ---------------------------------------------------------------------------------------
+// OpenES population rows [row0, row0 + rows) in one pass: x(g, j) = c(j) + s·σ·ε(r, j) with
+// (mirrored sampling, h = pop / 2) r = g mod h and s = +1 for g < h, −1 after; ε(r, j) =
+// normal(key, element r·d + j) — the noise `tell` regenerates (es_noise_grad_kernel).  The
+// f32 noise matrix, its mirrored copy and their concatenation are never written.  The sum is
+// c + (s·σ)·ε with two roundings: bitwise the torch expression it replaces.
+namespace {
+__global__ void __launch_bounds__(256) es_population_kernel(const int64_t* __restrict__ key, const float* __restrict__ center, float sigma,
+                                                            int64_t rows, int64_t d, int64_t half, int64_t row0, float* __restrict__ out) {
+  // two roundings (σ·ε, then + c) like the torch expression: no FMA contraction in this scope
+  // (plain operators: the pragma does not reach the __fmul_rn / __fadd_rn header definitions)
+#pragma clang fp contract(off)
+  uint32_t k0, k1;
+  evx::load_key(key, k0, k1);
+  const bool v4 = (d & 3) == 0;
+  const int64_t per_row = v4 ? d >> 2 : d;
+  const int64_t total = rows * per_row;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = t / per_row, c = t - i * per_row;
+    const int64_t g = row0 + i;
+    const bool neg = half > 0 && g >= half;
+    const int64_t r = neg ? g - half : g;
+    const float ss = neg ? -sigma : sigma;
+    if (v4) {
+      const int64_t j = c << 2;
+      const float4 n = evx::normal4(evx::philox_block((uint64_t)((r * d + j) >> 2), k0, k1));
+      const float4 ce = *reinterpret_cast<const float4*>(center + j);
+      float4 o;
+      o.x = ce.x + ss * n.x;
+      o.y = ce.y + ss * n.y;
+      o.z = ce.z + ss * n.z;
+      o.w = ce.w + ss * n.w;
+      *reinterpret_cast<float4*>(out + i * d + j) = o;
+    } else {
+      const uint64_t e = (uint64_t)(r * d + c);
+      const evx::u4 b = evx::philox_block(e >> 2, k0, k1);
+      const float4 n4 = evx::normal4(b);
+      const int q = (int)(e & 3);
+      const float n = q == 0 ? n4.x : (q == 1 ? n4.y : (q == 2 ? n4.z : n4.w));
+      out[i * d + c] = center[c] + ss * n;
+    }
+  }
+}
+}  // namespace
+
+void evx_es_population(const int64_t* key, const float* center, float sigma, int64_t rows, int64_t d, int64_t half, int64_t row0, float* out,
+                       hipStream_t s) {
+  const int64_t total = rows * ((d & 3) == 0 ? d >> 2 : d);
+  int64_t g = (total + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  es_population_kernel<<<(unsigned)g, 256, 0, s>>>(key, center, sigma, rows, d, half, row0, out);
+}

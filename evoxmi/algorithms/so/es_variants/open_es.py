@@ -82,11 +82,23 @@ class OpenES(ColumnSeparable, Algorithm):
     def ask(self, state):
         key, noise_key = rnd.split(state.key)
         dev = state.center.device
-        noise = self._noise_rows(noise_key, 0, self.pop_size, dev)
-        if self._cols is not None:  # column block of a decision-axis-sharded state
-            noise = self.col_vec(noise)
-        population = state.center[None, :] + self.noise_stdev * noise
+        if self._cols is None:
+            population = self._population_rows(noise_key, state.center, 0, self.pop_size)
+        else:  # column block of a decision-axis-sharded state
+            noise = self.col_vec(self._noise_rows(noise_key, 0, self.pop_size, dev))
+            population = state.center[None, :] + self.noise_stdev * noise
         return population, state.update(population=population, key=key, noise_key=noise_key.to(state.noise_key.device))
+
+    def _population_rows(self, noise_key, center, start: int, size: int):
+        """Rows [start, start + size) of center + σ·ε (mirrored: −ε for the second half).  On the
+        device ONE kernel (rng.hip: es_population_kernel) draws the same Philox noise as
+        :meth:`_noise_rows` and writes the rows; the noise matrix, its negated copy and their
+        concatenation are never materialised."""
+        if center.is_cuda and center.dtype == torch.float32:
+            half = self.pop_size // 2 if self.mirrored_sampling else 0
+            return _ext.ops().es_population(noise_key.to(center.device).contiguous(), center.contiguous(), float(self.noise_stdev),
+                                            int(size), int(half), int(start))
+        return center[None, :] + self.noise_stdev * self._noise_rows(noise_key, start, size, center.device)
 
     def _grad_rows(self, noise_key, fitness, start: int, size: int, dev):
         """Σ over global rows [start, start + size) of f_g ε_g (f indexed by global row)."""
@@ -137,7 +149,7 @@ class OpenES(ColumnSeparable, Algorithm):
     def ask_sharded(self, state, dist):
         start, size = dist.slice_of(self.pop_size)
         key, noise_key = rnd.split(state.key)
-        population = state.center[None, :] + self.noise_stdev * self._noise_rows(noise_key, start, size, state.center.device)
+        population = self._population_rows(noise_key, state.center, start, size)
         return population, state.update(population=population, key=key, noise_key=noise_key.to(state.noise_key.device))
 
     def tell_sharded(self, state, fitness, dist):

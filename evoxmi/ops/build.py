@@ -39,11 +39,29 @@ def _headers():
     return max((os.path.getmtime(h) for h in hs), default=0.0)
 
 
-def _stale(src, obj, hdr_mtime):
+def _stale(src, obj, hdr_mtime, cmd=None):
+    """Rebuild when the object is missing or older than its source / the headers, or when its
+    compile command changed (a per-file flag edit must not leave an object built the old way)."""
     if not os.path.exists(obj):
         return True
     t = os.path.getmtime(obj)
-    return os.path.getmtime(src) > t or hdr_mtime > t
+    if os.path.getmtime(src) > t or hdr_mtime > t:
+        return True
+    if cmd is not None:
+        stamp = obj + ".cmd"
+        try:
+            with open(stamp) as f:
+                return f.read() != " ".join(cmd)
+        except OSError:
+            return True
+    return False
+
+
+def _stamp(cmd):
+    """Record the command line of a compiled object next to it (read by _stale)."""
+    obj = cmd[cmd.index("-o") + 1]
+    with open(obj + ".cmd", "w") as f:
+        f.write(" ".join(cmd))
 
 
 def _run(cmd):
@@ -62,6 +80,7 @@ def _run(cmd):
 # gemm_ks.hip: the bf16x6 split's residual subtractions must stay scalar (v_pk_add_f32 issued
 # beside MFMAs costs ≈13 cycles more than two v_sub_f32)
 FILE_FLAGS = {"eigh_sbr.hip": ["-fno-slp-vectorize"], "mo_geom.hip": ["-ffp-contract=fast-honor-pragmas"],
+              "rng.hip": ["-ffp-contract=fast-honor-pragmas"],
               "neuro.hip": ["-fno-slp-vectorize"], "gemm_ks.hip": ["-fno-slp-vectorize"]}
 
 
@@ -97,22 +116,27 @@ def build(verbose: bool = True, jobs: int = None) -> str:
     for src in sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))):
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
         objs.append(obj)
-        if _stale(src, obj, hdr):
-            tasks.append([hipcc] + dev_flags + FILE_FLAGS.get(os.path.basename(src), []) + ["-c", src, "-o", obj])
+        cmd = [hipcc] + dev_flags + FILE_FLAGS.get(os.path.basename(src), []) + ["-c", src, "-o", obj]
+        if _stale(src, obj, hdr, cmd):
+            tasks.append(cmd)
     for src in sorted(glob.glob(os.path.join(CSRC, "bindings", "*.cpp"))):
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
         objs.append(obj)
-        if _stale(src, obj, hdr):
-            tasks.append(["g++"] + host_flags + ["-c", src, "-o", obj])
+        cmd = ["g++"] + host_flags + ["-c", src, "-o", obj]
+        if _stale(src, obj, hdr, cmd):
+            tasks.append(cmd)
     for src in sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp"))):
         obj = os.path.join(BUILD, "rt_" + os.path.basename(src) + ".o")
         objs.append(obj)
-        if _stale(src, obj, hdr):
-            tasks.append(["g++"] + host_flags + ["-fopenmp", "-c", src, "-o", obj])
+        cmd = ["g++"] + host_flags + ["-fopenmp", "-c", src, "-o", obj]
+        if _stale(src, obj, hdr, cmd):
+            tasks.append(cmd)
     if verbose and tasks:
         print(f"[evoxmi.build] compiling {len(tasks)} translation unit(s) for {ARCH}", flush=True)
     with ThreadPoolExecutor(jobs) as ex:
         list(ex.map(_run, tasks))
+    for cmd in tasks:
+        _stamp(cmd)
     need_link = tasks or not os.path.exists(OUT) or any(os.path.getmtime(o) > os.path.getmtime(OUT) for o in objs)
     if need_link:
         tl = os.path.join(td, "lib")

@@ -1105,3 +1105,21 @@ def test_sbx_pm_kernels_column_blocks(d, world):
         assert torch.equal(blk, full_x[:, c0 : c0 + own])
         mb = mutation.polynomial(key, blk, (lb[c0 : c0 + own], ub[c0 : c0 + own]), cols=(c0, d))
         assert torch.equal(mb, full_m[:, c0 : c0 + own])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d", [6472, 37])
+@pytest.mark.parametrize("mirrored", [True, False])
+def test_openes_population_kernel_matches_noise_rows(d, mirrored):
+    """rng.hip es_population_kernel: center + σ·ε (mirrored halves negated) in one pass equals
+    the materialised form center + σ·noise_rows bit for bit, for whole and partial row ranges."""
+    from evoxmi.algorithms import OpenES
+
+    pop = 64
+    center = torch.randn(d, generator=torch.Generator().manual_seed(3)).cuda()
+    es = OpenES(center, pop, 0.05, 0.1, mirrored_sampling=mirrored)
+    key = rnd.PRNGKey(11, device="cuda")
+    for start, size in [(0, pop), (5, 40), (pop // 2, pop // 2)]:
+        ref = center[None, :] + es.noise_stdev * es._noise_rows(key, start, size, center.device)
+        got = es._population_rows(key, center, start, size)
+        assert torch.equal(got, ref), (start, size)
