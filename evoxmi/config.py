@@ -39,6 +39,9 @@ KNOBS: Dict[str, Knob] = {
     "eigh": Knob("EVOXMI_EIGH", "sbr", str, "symmetric eigensolver for CMA-ES: 'sbr' (converged: Jacobi hand-off + sorted-block refinement, ops/sbr.py), 'jacobi' (fixed-sweep warm block Jacobi) or 'torch' (rocSOLVER)"),
     "eigh_tol": Knob("EVOXMI_EIGH_TOL", 1e-5, float, "sbr: target relative off-norm ‖offdiag(BᵀCB)‖_F / ‖diag‖_F of every decomposition"),
     "sbr_prepermute": Knob("EVOXMI_SBR_PREPERMUTE", 0, int, "device eigensolver: gather A[perm, perm] and B[:, perm] row-wise before the far / Bq tiles (1) — measured no faster (far+Bq 30.0 vs 28 µs, plus 6 µs for the gather)"),
+    "sbr_damp_tau": Knob("EVOXMI_SBR_DAMP_TAU", 1.0, float, "device eigensolver: cap on ‖αX‖₂ of a damped refinement step"),
+    "sbr_damp_kappa": Knob("EVOXMI_SBR_DAMP_KAPPA", 1.0, float, "device eigensolver: estimate ‖X‖₂ (damping) while κ exceeds this"),
+    "sbr_ns_kappa": Knob("EVOXMI_SBR_NS_KAPPA", 0.3, float, "device eigensolver: Newton–Schulz re-orthonormalisation while κ exceeds this"),
     "sbr_sweeps": Knob("EVOXMI_SBR_SWEEPS", 2, int, "sbr: cyclic Jacobi sweeps of the near-pair block solve per refinement iteration"),
     "sbr_block": Knob("EVOXMI_SBR_BLOCK", 32, int, "sbr: near-pair block size — 32 or 16 (blocks in a shifted sorted order, eigh_sbr16.hip; 32 converges in fewer iterations on the bench matrices) or 64 (eigh_sbr.hip)"),
     "sbr_mode": Knob("EVOXMI_SBR_MODE", "device", str, "sbr: 'device' — fixed device-controlled iteration schedule inside the generation's graph (ops/sbr_device.py, no host read); 'host' — host-driven iterations with planned solves as a host phase between graph segments (ops/sbr.py)"),

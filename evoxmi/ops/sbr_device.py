@@ -199,7 +199,9 @@ def eigh_device(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None, it
 
     cfg = cfg or SBRConfig(tol=config.get("eigh_tol"), block=config.get("sbr_block"), near_only=config.get("sbr_near_only"),
                            theta0=config.get("sbr_theta0"), theta_kappa=config.get("sbr_theta_kappa"),
-                           thr_fac=config.get("sbr_thr_fac"), block_sweeps=config.get("sbr_sweeps"))
+                           thr_fac=config.get("sbr_thr_fac"), block_sweeps=config.get("sbr_sweeps"),
+                           damp_tau=config.get("sbr_damp_tau"), damp_kappa=config.get("sbr_damp_kappa"),
+                           ns_kappa=config.get("sbr_ns_kappa"))
     if iters is None:
         iters = config.get("sbr_device_iters")
         # lean tail slots only in a schedule that does not start cold (CMA-ES's cold-start
