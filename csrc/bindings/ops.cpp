@@ -419,7 +419,7 @@ at::Tensor cec_rotated_rowterms(const at::Tensor& X, const at::Tensor& Mrot, con
 // ---- device-controlled SBR schedule (eigh_sbr_dev.hip, ops/sbr_device.py): every op writes
 // into caller-owned buffers and honours a device skip word, so a solve is capturable once
 void sbr16_block_out(const at::Tensor& A, int64_t shift, int64_t sweeps, int64_t sb, at::Tensor& perm, at::Tensor& Q, at::Tensor& dq,
-                     const at::Tensor& skip) {
+                     const at::Tensor& skip, double skip_tol) {
   CHECK_DEV(A); CHECK_F32(A);
   const int64_t n = A.size(0);
   TORCH_CHECK(A.dim() == 2 && A.size(1) == n && A.stride(1) == 1 && n <= evx_sbr16_max_n(), "sbr16_block_out: A n×n");
@@ -427,7 +427,7 @@ void sbr16_block_out(const at::Tensor& A, int64_t shift, int64_t sweeps, int64_t
   TORCH_CHECK(perm.numel() >= n && perm.scalar_type() == at::kInt && Q.numel() >= evx_sbr16_nblocks((int)n, (int)sb) * sb * sb &&
                   dq.numel() >= n, "sbr16_block_out: buffers");
   evx_sbr16_block(A.data_ptr<float>(), (int)n, A.stride(0), (int)shift, (int)sweeps, perm.data_ptr<int>(), Q.data_ptr<float>(),
-                  dq.data_ptr<float>(), (int)sb, cur_stream(), skip.data_ptr<int>());
+                  dq.data_ptr<float>(), (int)sb, cur_stream(), skip.data_ptr<int>(), (float)skip_tol);
 }
 
 void sbr16_far_out(const at::Tensor& A, const at::Tensor& perm, const at::Tensor& Q, const at::Tensor& dq, const at::Tensor& stats,
@@ -1437,7 +1437,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("gemm_ks_grid(int M, int N, int mode) -> int");
   m.def("gemm_ks_tile(int M, int N, int mode) -> int");
   m.def("cec_rotated_rowterms(Tensor X, Tensor Mrot, Tensor o, float alpha, int fid) -> Tensor");
-  m.def("sbr16_block_out(Tensor A, int shift, int sweeps, int sb, Tensor(a!) perm, Tensor(b!) Q, Tensor(c!) dq, Tensor skip) -> ()");
+  m.def("sbr16_block_out(Tensor A, int shift, int sweeps, int sb, Tensor(a!) perm, Tensor(b!) Q, Tensor(c!) dq, Tensor skip, float skip_tol=0.0) -> ()");
   m.def("sbr16_far_out(Tensor A, Tensor perm, Tensor Q, Tensor dq, Tensor stats, float thr_fac, Tensor theta, Tensor(a!) X, int sb, Tensor skip) -> ()");
   m.def("sbr16_bq_out(Tensor B, Tensor perm, Tensor Q, Tensor(a!) Bq, int sb, Tensor skip) -> ()");
   m.def("sbr_damping_out(Tensor X2, Tensor V, float tau, Tensor(a!) alpha, Tensor(b!) work, Tensor skip, Tensor(c!)? bar=None, bool no_final=False) -> ()");

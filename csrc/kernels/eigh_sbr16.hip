@@ -140,7 +140,8 @@ __device__ __forceinline__ void bitonic_kv(float* k, int* v, int np) {
 template <int SB, bool FR>
 __global__ void __launch_bounds__(SB * SB / 2) sbr16_block_kernel(const float* __restrict__ A, int n, int64_t lda,
                                                                  int* __restrict__ perm, int sweeps, float* __restrict__ Q_out,
-                                                                 float* __restrict__ dq_out, const int* __restrict__ skip, int shift) {
+                                                                 float* __restrict__ dq_out, const int* __restrict__ skip, int shift,
+                                                                 float skip_tol) {
   if (skip && *skip) return;
   constexpr int SP = SB + 1, NT = SB * SB / 4, NH = SB / 2;
   __shared__ float S[SB * SP];
@@ -193,8 +194,39 @@ __global__ void __launch_bounds__(SB * SB / 2) sbr16_block_kernel(const float* _
   const bool item = !qlane && rem >= 0 && (tid - NT) < NH * (NH + 1) / 2;
   const bool dg = u == v;
   const int G = (SB - 1) * sweeps;
+  __shared__ float s_off[SB * SB / 128], s_dg[SB * SB / 128];
+  __shared__ int s_done;
   for (int g = 0; g < G; ++g) {
     const int r = g % (SB - 1);
+    if (r == 0 && skip_tol > 0.f) {
+      // before every sweep: a block already diagonal to skip_tol (relative off-diagonal norm)
+      // skips its remaining sweeps — after one sweep of the quadratically converging cyclic
+      // Jacobi the second one is usually below rounding in the later refinement iterations
+      float off = 0.f, dg = 0.f;
+      for (int e = tid; e < SB * SB; e += nthr) {
+        const int a = e / SB, c = e % SB;
+        const float v = S[a * SP + c];
+        if (a == c) dg = fmaf(v, v, dg);
+        else off = fmaf(v, v, off);
+      }
+      off = evx::wave_sum(off);
+      dg = evx::wave_sum(dg);
+      if ((tid & 63) == 0) {
+        s_off[tid >> 6] = off;
+        s_dg[tid >> 6] = dg;
+      }
+      __syncthreads();
+      if (tid == 0) {
+        float o = 0.f, d = 0.f;
+        for (int w = 0; w < nthr / 64; ++w) {
+          o += s_off[w];
+          d += s_dg[w];
+        }
+        s_done = o <= skip_tol * skip_tol * d ? 1 : 0;
+      }
+      __syncthreads();
+      if (s_done) break;
+    }
     const int2* pr = ptab + r * NH;
     if (tid < NH) {
       const int2 p = pr[tid];
@@ -685,23 +717,23 @@ int evx_sbr16_nblocks(int n, int sb) { return (n + sb - 1) / sb; }
 int evx_sbr16_max_n() { return kRankMax; }
 
 void evx_sbr16_block(const float* A, int n, int64_t lda, int shift, int sweeps, int* perm, float* Q, float* dq, int sb, hipStream_t s,
-                     const int* skip) {
+                     const int* skip, float skip_tol) {
   static const bool fuse = [] {  // EVOXMI_SBR_FUSED_RANK=1: the rank inside the block kernel (see sbr16_block_kernel)
     const char* e = getenv("EVOXMI_SBR_FUSED_RANK");
     return e && atoi(e) != 0;
   }();
   if (fuse && n <= kFuseMax) {
     if (sb == 32)
-      sbr16_block_kernel<32, true><<<(n + 31) / 32, 512, 0, s>>>(A, n, lda, perm, sweeps, Q, dq, skip, shift);
+      sbr16_block_kernel<32, true><<<(n + 31) / 32, 512, 0, s>>>(A, n, lda, perm, sweeps, Q, dq, skip, shift, skip_tol);
     else
-      sbr16_block_kernel<16, true><<<(n + 15) / 16, 128, 0, s>>>(A, n, lda, perm, sweeps, Q, dq, skip, shift);
+      sbr16_block_kernel<16, true><<<(n + 15) / 16, 128, 0, s>>>(A, n, lda, perm, sweeps, Q, dq, skip, shift, skip_tol);
     return;
   }
   sbr16_rank_kernel<<<(n + 63) / 64, 64 * kRankWaves, 0, s>>>(A, n, lda, shift, perm, skip);
   if (sb == 32)
-    sbr16_block_kernel<32, false><<<(n + 31) / 32, 512, 0, s>>>(A, n, lda, perm, sweeps, Q, dq, skip, shift);
+    sbr16_block_kernel<32, false><<<(n + 31) / 32, 512, 0, s>>>(A, n, lda, perm, sweeps, Q, dq, skip, shift, skip_tol);
   else
-    sbr16_block_kernel<16, false><<<(n + 15) / 16, 128, 0, s>>>(A, n, lda, perm, sweeps, Q, dq, skip, shift);
+    sbr16_block_kernel<16, false><<<(n + 15) / 16, 128, 0, s>>>(A, n, lda, perm, sweeps, Q, dq, skip, shift, skip_tol);
 }
 
 void evx_sbr16_far(const float* A, int n, int64_t lda, const int* perm, const float* Q, const float* dq, const double* stats,

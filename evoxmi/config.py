@@ -42,6 +42,7 @@ KNOBS: Dict[str, Knob] = {
     "sbr_damp_tau": Knob("EVOXMI_SBR_DAMP_TAU", 1.0, float, "device eigensolver: cap on ‖αX‖₂ of a damped refinement step"),
     "sbr_damp_kappa": Knob("EVOXMI_SBR_DAMP_KAPPA", 1.0, float, "device eigensolver: estimate ‖X‖₂ (damping) while κ exceeds this"),
     "sbr_ns_kappa": Knob("EVOXMI_SBR_NS_KAPPA", 0.3, float, "device eigensolver: Newton–Schulz re-orthonormalisation while κ exceeds this"),
+    "sbr_sweep_tol": Knob("EVOXMI_SBR_SWEEP_TOL", 0.0, float, "device eigensolver: a 32×32 block whose relative off-diagonal norm is at most this before a Jacobi sweep skips its remaining sweeps (0: always every sweep)"),
     "sbr_sweeps": Knob("EVOXMI_SBR_SWEEPS", 2, int, "sbr: cyclic Jacobi sweeps of the near-pair block solve per refinement iteration"),
     "sbr_block": Knob("EVOXMI_SBR_BLOCK", 32, int, "sbr: near-pair block size — 32 or 16 (blocks in a shifted sorted order, eigh_sbr16.hip; 32 converges in fewer iterations on the bench matrices) or 64 (eigh_sbr.hip)"),
     "sbr_mode": Knob("EVOXMI_SBR_MODE", "device", str, "sbr: 'device' — fixed device-controlled iteration schedule inside the generation's graph (ops/sbr_device.py, no host read); 'host' — host-driven iterations with planned solves as a host phase between graph segments (ops/sbr.py)"),

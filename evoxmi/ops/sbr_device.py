@@ -66,6 +66,8 @@ class DeviceSBR:
 
         # opt-in: A[perm, perm] and B[:, perm] gathered row-wise first (measured no faster)
         self.prepermute = bool(config.get("sbr_prepermute"))
+        # a block already diagonal to this relative off-norm skips its remaining Jacobi sweeps
+        self.sweep_tol = float(config.get("sbr_sweep_tol"))
         self.Ap, self.Bp = (mat(), mat()) if self.prepermute else (None, None)
         sb = cfg.block
         nb = -(-n // sb)
@@ -115,7 +117,7 @@ class DeviceSBR:
         sk_all, sk_far, sk_damp, sk_x3, sel6, sk_ns, sel_ns, sk_copy = (c[i : i + 1] for i in range(8))
         shift = (j % 2) * (sb // 2)
         full = j < self.lean_from
-        ops.sbr16_block_out(self.A, shift, int(cfg.block_sweeps), sb, self.perm, self.Q, self.dq, sk_all)
+        ops.sbr16_block_out(self.A, shift, int(cfg.block_sweeps), sb, self.perm, self.Q, self.dq, sk_all, self.sweep_tol)
         # far generator X and Bq = B[:, perm]·blockdiag(Q) in one launch
         if self.prepermute:
             # A[perm, perm] and B[:, perm] row by row first, so that the tiles read contiguous blocks —
@@ -186,7 +188,7 @@ def workspace(n: int, device, cfg: SBRConfig, iters: int, lean_from: int = None)
 
     key = (n, str(device), cfg.block, cfg.block_sweeps, cfg.thr_fac, cfg.ns_iters, cfg.damp_tau, cfg.tol, cfg.ns_kappa,
            cfg.damp_kappa, cfg.t4_kappa, cfg.near_only, cfg.theta0, cfg.theta_kappa, int(iters), lean_from,
-           bool(config.get("sbr_prepermute")))
+           bool(config.get("sbr_prepermute")), float(config.get("sbr_sweep_tol")))
     if key not in _WS:
         _WS[key] = DeviceSBR(n, device, cfg, iters, lean_from)
     return _WS[key]
