@@ -33,7 +33,15 @@ namespace {
 
 // block size SB ∈ {16, 32} is a template parameter; LDS pitch SB + 1 (odd: conflict-free columns)
 constexpr int TL = 64;            // tile of the generator / Bq kernels (four blocks)
-constexpr int TP = 68;            // LDS pitch of a 64-wide tile (float4 aligned)
+// LDS pitches of the 64-wide tiles, chosen for the f32 MFMA fragment reads (ds_read_b32 banks =
+// word address mod 32 per 32-lane half; lanes (m = lane & 15, kq = lane >> 4)):
+//  * TP (≡ 16 mod 32): tiles read along rows, lane m ↔ column, kq ↔ row (Q tiles, the
+//    generator's gathered block as the B operand) — kq = 0 / 1 land on banks 0-15 / 16-31;
+//  * TC (≡ 2 mod 32): tiles read along columns, lane m ↔ row (T and the Bq rows as the A
+//    operand) — rows 2 banks apart, kq = 0 / 1 on the even / odd banks.
+constexpr int TP = 80;
+constexpr int TC = 66;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int kRankMax = 8192;    // largest n of the rank kernel (32 KB of keys in LDS)
 
 __device__ __forceinline__ float sort_key(float v) { return isnan(v) ? INFINITY : v; }
@@ -289,7 +297,7 @@ __device__ __forceinline__ void load_qtile(const float* __restrict__ Q, int nb, 
 
 // ------------------------------------------------------------------ 3. far-pair generator
 struct FarSmem {
-  float G[TL * TP];
+  float G[TL * TP];  // the gathered block (pitch TP), then T (pitch TC ≤ TP)
   float Qk[TL * TP];
   float Ql[TL * TP];
   int pk[TL], pl[TL];
@@ -350,66 +358,67 @@ __device__ __forceinline__ void far_tile(const float* __restrict__ A, int n, int
     }
   }
   __syncthreads();
-  const int r0 = (threadIdx.x >> 4) << 2, c0 = (threadIdx.x & 15) << 2;
-  // T[c][f] = Σ_{a in block(c)} Qk[a][c] G[a][f]: rows r0..r0+3 share one block
-  float acc[4][4] = {};
-  const int ab = r0 & ~(SB - 1);
+  // both contractions on the f32 matrix cores (v_mfma_f32_16x16x4f32: the exact f32 product of
+  // an fmaf chain): wave w owns rows [16w, 16w + 16) of T and A1, four 16×16 column tiles each.
+  // Lane (m, kq): A operand A[m][kq], B operand B[kq][m], accumulator rows 4kq + i, column m.
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, m = lane & 15, kq = lane >> 4;
+  // T[c][f] = Σ_{a in block(c)} Qk[a][c] G[a][f]
+  f32x4 acc[4];
 #pragma unroll
-  for (int a = 0; a < SB; ++a) {
-    const float4 lq = *(const float4*)(Qk + (ab + a) * TP + r0);
-    const float4 g = *(const float4*)(G + (ab + a) * TP + c0);
-    const float l[4] = {lq.x, lq.y, lq.z, lq.w};
+  for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  {
+    const int ab = (16 * w) & ~(SB - 1);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      acc[i][0] = fmaf(l[i], g.x, acc[i][0]);
-      acc[i][1] = fmaf(l[i], g.y, acc[i][1]);
-      acc[i][2] = fmaf(l[i], g.z, acc[i][2]);
-      acc[i][3] = fmaf(l[i], g.w, acc[i][3]);
+    for (int s4 = 0; s4 < SB / 4; ++s4) {
+      const int a = ab + 4 * s4 + kq;
+      const float av = Qk[a * TP + 16 * w + m];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, G[a * TP + 16 * t + m], acc[t], 0, 0, 0);
     }
   }
-  __syncthreads();  // all reads of G done: T overwrites it
+  __syncthreads();  // all reads of G done: T overwrites it (pitch TC: read by columns below)
 #pragma unroll
-  for (int i = 0; i < 4; ++i) *(float4*)(G + (r0 + i) * TP + c0) = make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) G[(16 * w + 4 * kq + i) * TC + 16 * t + m] = acc[t][i];
   __syncthreads();
   // A1[c][e] = Σ_{f in block(e)} T[c][f] Ql[f][e]
-  float out[4][4] = {};
-  const int fb = c0 & ~(SB - 1);
 #pragma unroll
-  for (int f = 0; f < SB; ++f) {
-    const float4 q = *(const float4*)(Ql + (fb + f) * TP + c0);
+  for (int t = 0; t < 4; ++t) {
+    acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int fb = (16 * t) & ~(SB - 1);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float t = G[(r0 + i) * TP + fb + f];
-      out[i][0] = fmaf(t, q.x, out[i][0]);
-      out[i][1] = fmaf(t, q.y, out[i][1]);
-      out[i][2] = fmaf(t, q.z, out[i][2]);
-      out[i][3] = fmaf(t, q.w, out[i][3]);
+    for (int s4 = 0; s4 < SB / 4; ++s4) {
+      const int f = fb + 4 * s4 + kq;
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(G[(16 * w + m) * TC + f], Ql[f * TP + 16 * t + m], acc[t], 0, 0, 0);
     }
   }
+  // element (c, e) = (16w + 4kq + i, 16t + m) of the generator tile
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int c = r0 + i;
-    if (c >= mk) continue;
-    const int bc = (sk + c) / SB;
+  for (int t = 0; t < 4; ++t) {
+    const int e = 16 * t + m;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int e = c0 + j;
-      if (e >= ml) continue;
-      const float den = dl[e] - dk[c];
-      // the 2×2 Jacobi angle ½·atan(2a/den): a/den to first order for well-separated pairs,
-      // saturating at π/4 for strongly coupled ones
-      const bool far = ((sl + e) / SB) != bc && fabsf(den) > fminf(tk[c], tl[e]);
-      out[i][j] = far ? 0.5f * atanf(2.f * out[i][j] / den) : 0.f;
-      X[(int64_t)(sk + c) * ldx + sl + e] = out[i][j];
+    for (int i = 0; i < 4; ++i) {
+      const int c = 16 * w + 4 * kq + i;
+      float x = 0.f;
+      if (c < mk && e < ml) {
+        const float den = dl[e] - dk[c];
+        // the 2×2 Jacobi angle ½·atan(2a/den): a/den to first order for well-separated pairs,
+        // saturating at π/4 for strongly coupled ones
+        const bool far = ((sl + e) / SB) != ((sk + c) / SB) && fabsf(den) > fminf(tk[c], tl[e]);
+        x = far ? 0.5f * atanf(2.f * acc[t][i] / den) : 0.f;
+        X[(int64_t)(sk + c) * ldx + sl + e] = x;
+      }
+      acc[t][i] = x;
     }
   }
   if (mirror && K != L) {
     // X is skew: tile (L, K) = −(tile (K, L))ᵀ, written from here through LDS (coalesced rows)
     __syncthreads();  // every read of G (T) is done
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) G[(c0 + j) * TP + r0 + i] = out[i][j];
+      for (int i = 0; i < 4; ++i) G[(16 * t + m) * TP + 16 * w + 4 * kq + i] = acc[t][i];
     __syncthreads();
     for (int e = threadIdx.x; e < TL * TL; e += blockDim.x) {
       const int er = e >> 6, cc = e & 63;
@@ -444,38 +453,30 @@ __device__ __forceinline__ void bq_tile(const float* __restrict__ B, int rows, i
     const int r = e >> 6, f = e & 63;
     const int row = rt * TL + r;
     if (pre) {  // B's columns already permuted: a contiguous tile
-      G[r * TP + f] = (row < rows && f < ml) ? B[(int64_t)row * ldb + sl + f] : 0.f;
+      G[r * TC + f] = (row < rows && f < ml) ? B[(int64_t)row * ldb + sl + f] : 0.f;
     } else {
       const int col = pl[f];
-      G[r * TP + f] = (row < rows && col >= 0) ? B[(int64_t)row * ldb + col] : 0.f;
+      G[r * TC + f] = (row < rows && col >= 0) ? B[(int64_t)row * ldb + col] : 0.f;
     }
   }
   __syncthreads();
-  const int r0 = (threadIdx.x >> 4) << 2, c0 = (threadIdx.x & 15) << 2;
-  const int fb = c0 & ~(SB - 1);
-  float out[4][4] = {};
+  // Bq rows [16w, 16w + 16) of the tile on the f32 matrix cores (see far_tile for the lane map)
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, m = lane & 15, kq = lane >> 4;
+  const int row0 = rt * TL + 16 * w + 4 * kq;
 #pragma unroll
-  for (int f = 0; f < SB; ++f) {
-    const float4 q = *(const float4*)(Ql + (fb + f) * TP + c0);
+  for (int t = 0; t < 4; ++t) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int fb = (16 * t) & ~(SB - 1);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float g = G[(r0 + i) * TP + fb + f];
-      out[i][0] = fmaf(g, q.x, out[i][0]);
-      out[i][1] = fmaf(g, q.y, out[i][1]);
-      out[i][2] = fmaf(g, q.z, out[i][2]);
-      out[i][3] = fmaf(g, q.w, out[i][3]);
+    for (int s4 = 0; s4 < SB / 4; ++s4) {
+      const int f = fb + 4 * s4 + kq;
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(G[(16 * w + m) * TC + f], Ql[f * TP + 16 * t + m], acc, 0, 0, 0);
     }
-  }
+    const int e = 16 * t + m;
+    if (e < ml) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = rt * TL + r0 + i;
-    if (row >= rows) continue;
-    if (c0 + 3 < ml) {
-      *(float4*)(Bq + (int64_t)row * ldq + sl + c0) = make_float4(out[i][0], out[i][1], out[i][2], out[i][3]);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (c0 + j < ml) Bq[(int64_t)row * ldq + sl + c0 + j] = out[i][j];
+      for (int i = 0; i < 4; ++i)
+        if (row0 + i < rows) Bq[(int64_t)(row0 + i) * ldq + sl + e] = acc[i];
     }
   }
 }
