@@ -42,6 +42,7 @@ constexpr int TL = 64;            // tile of the generator / Bq kernels (four bl
 constexpr int TP = 80;
 constexpr int TC = 66;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int BQR = 32;  // rows of a Bq tile: twice the workgroups of 64-row tiles, better latency hiding
 constexpr int kRankMax = 8192;    // largest n of the rank kernel (32 KB of keys in LDS)
 
 __device__ __forceinline__ float sort_key(float v) { return isnan(v) ? INFINITY : v; }
@@ -449,9 +450,9 @@ __device__ __forceinline__ void bq_tile(const float* __restrict__ B, int rows, i
   if (threadIdx.x < TL) pl[threadIdx.x] = threadIdx.x < ml ? perm[sl + threadIdx.x] : -1;
   load_qtile<SB>(Q, nb, L, Ql);
   __syncthreads();
-  for (int e = threadIdx.x; e < TL * TL; e += blockDim.x) {
+  for (int e = threadIdx.x; e < BQR * TL; e += blockDim.x) {
     const int r = e >> 6, f = e & 63;
-    const int row = rt * TL + r;
+    const int row = rt * BQR + r;
     if (pre) {  // B's columns already permuted: a contiguous tile
       G[r * TC + f] = (row < rows && f < ml) ? B[(int64_t)row * ldb + sl + f] : 0.f;
     } else {
@@ -460,17 +461,20 @@ __device__ __forceinline__ void bq_tile(const float* __restrict__ B, int rows, i
     }
   }
   __syncthreads();
-  // Bq rows [16w, 16w + 16) of the tile on the f32 matrix cores (see far_tile for the lane map)
+  // a BQR (32)-row tile on the f32 matrix cores: wave w takes 16-row tile w & 1 and the column
+  // tiles 2(w >> 1), 2(w >> 1) + 1 (see far_tile for the lane map)
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, m = lane & 15, kq = lane >> 4;
-  const int row0 = rt * TL + 16 * w + 4 * kq;
+  const int rl = 16 * (w & 1);
+  const int row0 = rt * BQR + rl + 4 * kq;
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
+  for (int tt = 0; tt < 2; ++tt) {
+    const int t = 2 * (w >> 1) + tt;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     const int fb = (16 * t) & ~(SB - 1);
 #pragma unroll
     for (int s4 = 0; s4 < SB / 4; ++s4) {
       const int f = fb + 4 * s4 + kq;
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(G[(16 * w + m) * TC + f], Ql[f * TP + 16 * t + m], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(G[(rl + m) * TC + f], Ql[f * TP + 16 * t + m], acc, 0, 0, 0);
     }
     const int e = 16 * t + m;
     if (e < ml) {
@@ -751,9 +755,9 @@ void evx_sbr16_bq(const float* B, int rows, int n, int64_t ldb, const int* perm,
                   hipStream_t s, const int* skip) {
   const int nt = (n + TL - 1) / TL;
   if (sb == 32)
-    sbr16_bq_kernel<32><<<dim3(nt, (rows + TL - 1) / TL), 256, 0, s>>>(B, rows, n, ldb, perm, Q, Bq, ldq, skip);
+    sbr16_bq_kernel<32><<<dim3(nt, (rows + BQR - 1) / BQR), 256, 0, s>>>(B, rows, n, ldb, perm, Q, Bq, ldq, skip);
   else
-    sbr16_bq_kernel<16><<<dim3(nt, (rows + TL - 1) / TL), 256, 0, s>>>(B, rows, n, ldb, perm, Q, Bq, ldq, skip);
+    sbr16_bq_kernel<16><<<dim3(nt, (rows + BQR - 1) / BQR), 256, 0, s>>>(B, rows, n, ldb, perm, Q, Bq, ldq, skip);
 }
 
 void evx_sbr16_permute(const float* A, int n, int64_t lda, const int* perm, const float* B, int rows, int64_t ldb, float* Ap, float* Bp,
@@ -764,7 +768,7 @@ void evx_sbr16_permute(const float* A, int n, int64_t lda, const int* perm, cons
 void evx_sbr16_far_bq(const float* A, int n, int64_t lda, const int* perm, const float* Q, const float* dq, const double* stats,
                       float thr_fac, const float* theta_ptr, float* X, int64_t ldx, const float* B, int rows, int64_t ldb, float* Bq,
                       int64_t ldq, int sb, hipStream_t s, const int* skip_far, const int* skip_bq, bool pre) {
-  const int nt = (n + TL - 1) / TL, rt = (rows + TL - 1) / TL;
+  const int nt = (n + TL - 1) / TL, rt = (rows + BQR - 1) / BQR;
   const dim3 grid(nt, nt + rt);
   if (sb == 32)
     sbr16_far_bq_kernel<32><<<grid, 256, 0, s>>>(A, n, lda, perm, Q, dq, stats, thr_fac, theta_ptr, X, ldx, B, rows, ldb, Bq, ldq, skip_far,
