@@ -138,7 +138,10 @@ class CMAES(Algorithm):
         if variant == "cold":
             return config.override(sbr_device_iters=int(config.get("sbr_cold_iters")))
         if variant == "late":
-            return config.override(sbr_device_iters=int(config.get("sbr_late_iters")))
+            # settled generations: damping / Newton–Schulz / order-6 kernels only in the first
+            # sbr_late_full_slots slots (their κ falls below the order-4 threshold by slot 2)
+            return config.override(sbr_device_iters=int(config.get("sbr_late_iters")),
+                                   sbr_full_slots=int(config.get("sbr_late_full_slots")))
         return super().graph_variant_context(variant)
 
     # ------------------------------------------------------------------ sampling
