@@ -408,9 +408,13 @@ __global__ void __launch_bounds__(64 * NW) gemm_ks_kernel(EvxGemmKs p) {
   // addresses stay valid and the surplus loads are never consumed): the loop body is then
   // straight-line between scalar branches and the waitcnt pass keeps D − 1 groups in flight
   // (a conditional issue makes it wait for everything at the join).
+  // (g0 ≤ ngf − 1 whenever ngf ≥ 1; with K < KG there is no full group at all and group 0
+  // would read past the last row's K floats: nothing is loaded, the tail below does it all)
   const int glast = max(g1 - 1, g0);
+  if (ngf > 0) {
 #pragma unroll
-  for (int s = 0; s < D - 1; ++s) load_slot(fa[s], fb[s], fs[s], pa[s], pb[s], min(g0 + s, glast));
+    for (int s = 0; s < D - 1; ++s) load_slot(fa[s], fb[s], fs[s], pa[s], pb[s], min(g0 + s, glast));
+  }
   // chunks of D groups with no branch inside (load group g + s + D − 1, compute group g + s),
   // then the < D remaining groups, whose data the last chunk (or the prologue) loaded
   int g = g0;

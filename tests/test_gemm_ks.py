@@ -135,7 +135,7 @@ def test_gemm_ks_is_deterministic():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("M,N,K", [(10000, 1000, 1000), (300, 200, 100)])
+@pytest.mark.parametrize("M,N,K", [(10000, 1000, 1000), (300, 200, 100), (32, 5120, 20)])
 def test_gemm_ks_fused_shift_prologue(M, N, K):
     """z = s·(X − o)·Mᵀ with the shift fused into the A loads (CEC shift-rotate)."""
     g = torch.Generator().manual_seed(M + K)
