@@ -122,7 +122,7 @@ __global__ void __launch_bounds__(256) sbr_dev_ctrl_kernel(const double* __restr
                                                            float* __restrict__ w_out, double* __restrict__ eig_stats,
                                                            float* __restrict__ w_init, double* __restrict__ log, int log_len,
                                                            int* __restrict__ log_count) {
-  __shared__ double s[4][256];
+  __shared__ double s[4][4];
   __shared__ int s_keep;
   const int t = threadIdx.x;
   const bool executed = j < 0 || ctrl[8 * j] == 0;
@@ -135,21 +135,28 @@ __global__ void __launch_bounds__(256) sbr_dev_ctrl_kernel(const double* __restr
       mn = fmin(mn, part[4 * i + 2]);
       mx = fmax(mx, part[4 * i + 3]);
     }
-    s[0][t] = off;
-    s[1][t] = dg;
-    s[2][t] = mn;
-    s[3][t] = mx;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-      if (t < o) {
-        s[0][t] += s[0][t + o];
-        s[1][t] += s[1][t + o];
-        s[2][t] = fmin(s[2][t], s[2][t + o]);
-        s[3][t] = fmax(s[3][t], s[3][t + o]);
-      }
-      __syncthreads();
+    // wave reductions (no barrier), then the four wave results through LDS: one barrier
+    // instead of the eight of a 256-wide tree (this kernel sits on the schedule's serial path)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      off += __shfl_xor(off, o);
+      dg += __shfl_xor(dg, o);
+      mn = fmin(mn, __shfl_xor(mn, o));
+      mx = fmax(mx, __shfl_xor(mx, o));
     }
-    if (t < 4) hj1[t] = s[t][0];
+    if ((t & 63) == 0) {
+      s[0][t >> 6] = off;
+      s[1][t >> 6] = dg;
+      s[2][t >> 6] = mn;
+      s[3][t >> 6] = mx;
+    }
+    __syncthreads();
+    if (t == 0) {
+      hj1[0] = (s[0][0] + s[0][1]) + (s[0][2] + s[0][3]);
+      hj1[1] = (s[1][0] + s[1][1]) + (s[1][2] + s[1][3]);
+      hj1[2] = fmin(fmin(s[2][0], s[2][1]), fmin(s[2][2], s[2][3]));
+      hj1[3] = fmax(fmax(s[3][0], s[3][1]), fmax(s[3][2], s[3][3]));
+    }
   } else if (t < 4) {
     hj1[t] = hist[4 * j + t];
   }
