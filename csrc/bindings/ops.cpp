@@ -1304,25 +1304,43 @@ std::vector<at::Tensor> cma_paths(const at::Tensor& ps, const at::Tensor& pc, co
 }
 
 std::vector<at::Tensor> cma_cov_pad(const at::Tensor& C, const at::Tensor& S, const at::Tensor& pc, const at::Tensor& a, double c1,
-                                    double cmu, const at::Tensor& Bprev, int64_t np) {
+                                    double cmu, const at::Tensor& Bprev, int64_t np, const c10::optional<at::Tensor>& Cn_out,
+                                    bool want_bp) {
   for (auto* t : {&C, &S, &pc, &a, &Bprev}) { CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t); }
   const int64_t d = pc.numel();
   TORCH_CHECK(C.dim() == 2 && C.size(0) == d && C.size(1) == d && S.sizes() == C.sizes() && Bprev.sizes() == C.sizes(), "cma_cov_pad: shapes");
   TORCH_CHECK(np >= d && np % 32 == 0 && a.numel() == 1, "cma_cov_pad: np must be a multiple of 32 and >= d");
   c10::DeviceGuard g(C.device());
-  auto Cn = at::empty_like(C);
-  auto Cp = at::empty({np, np}, C.options()), Bp = at::empty({np, np}, C.options());
+  at::Tensor Cn;
+  if (Cn_out.has_value()) {  // may be C itself (in-place covariance update)
+    Cn = *Cn_out;
+    CHECK_DEV(Cn); CHECK_F32(Cn); CHECK_CONTIG(Cn);
+    TORCH_CHECK(Cn.sizes() == C.sizes(), "cma_cov_pad: out shape");
+  } else {
+    Cn = at::empty_like(C);
+  }
+  auto Cp = at::empty({np, np}, C.options());
+  auto Bp = want_bp ? at::empty({np, np}, C.options()) : at::empty({0}, C.options());
   evx_cma_cov_pad(C.data_ptr<float>(), S.data_ptr<float>(), pc.data_ptr<float>(), a.data_ptr<float>(), (float)c1, (float)cmu,
-                  Bprev.data_ptr<float>(), (int)d, (int)np, Cn.data_ptr<float>(), Cp.data_ptr<float>(), Bp.data_ptr<float>(), cur_stream());
+                  Bprev.data_ptr<float>(), (int)d, (int)np, Cn.data_ptr<float>(), Cp.data_ptr<float>(),
+                  want_bp ? Bp.data_ptr<float>() : nullptr, cur_stream());
   return {Cn, Cp, Bp};
 }
 
-std::vector<at::Tensor> cma_eig_out(const at::Tensor& Bp, const at::Tensor& w, int64_t d) {
+std::vector<at::Tensor> cma_eig_out(const at::Tensor& Bp, const at::Tensor& w, int64_t d, const c10::optional<at::Tensor>& B_out) {
   for (auto* t : {&Bp, &w}) { CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t); }
   const int64_t np = Bp.size(0);
   TORCH_CHECK(Bp.dim() == 2 && Bp.size(1) == np && w.numel() >= d && d <= np, "cma_eig_out: shapes");
   c10::DeviceGuard g(Bp.device());
-  auto B = at::empty({d, d}, Bp.options()), BD = at::empty({d, d}, Bp.options()), D = at::empty({d}, Bp.options());
+  at::Tensor B;
+  if (B_out.has_value()) {  // the state's basis buffer (captured generation); must not alias Bp
+    B = *B_out;
+    CHECK_DEV(B); CHECK_F32(B); CHECK_CONTIG(B);
+    TORCH_CHECK(B.dim() == 2 && B.size(0) == d && B.size(1) == d && B.data_ptr() != Bp.data_ptr(), "cma_eig_out: out");
+  } else {
+    B = at::empty({d, d}, Bp.options());
+  }
+  auto BD = at::empty({d, d}, Bp.options()), D = at::empty({d}, Bp.options());
   if (d > 0) evx_cma_eig_out(Bp.data_ptr<float>(), w.data_ptr<float>(), (int)d, (int)np, B.data_ptr<float>(), D.data_ptr<float>(),
                              BD.data_ptr<float>(), cur_stream());
   return {B, D, BD};
@@ -1456,8 +1474,8 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("cma_delta_gemv(Tensor M, Tensor mean, Tensor dm, float cm) -> Tensor[]");
   m.def("cma_center_rows(Tensor pop, Tensor? rows, Tensor mean, Tensor sigma, Tensor w) -> Tensor");
   m.def("cma_paths(Tensor ps, Tensor pc, Tensor y, Tensor delta, Tensor sigma, Tensor count_iter, float[] consts) -> Tensor[]");
-  m.def("cma_cov_pad(Tensor C, Tensor S, Tensor pc, Tensor a, float c1, float cmu, Tensor Bprev, int np) -> Tensor[]");
-  m.def("cma_eig_out(Tensor Bp, Tensor w, int d) -> Tensor[]");
+  m.def("cma_cov_pad(Tensor C, Tensor S, Tensor pc, Tensor a, float c1, float cmu, Tensor Bprev, int np, Tensor? Cn_out=None, bool want_bp=True) -> Tensor[]");
+  m.def("cma_eig_out(Tensor Bp, Tensor w, int d, Tensor? B_out=None) -> Tensor[]");
   m.def("nsga_select(Tensor rank, Tensor f, int N, int mask_pos) -> Tensor");
   m.def("moead_parents(Tensor nb, Tensor key, int row0=0, int rows=0) -> Tensor[]");
   m.def("moead_variation(Tensor pop, Tensor p0, Tensor p1, Tensor kx, Tensor km, Tensor lb, Tensor ub, float pro_c, float dis_c, float pro_m, float dis_m, int nm, int row0=0, int rows=0, Tensor? win=None, Tensor(a!)? out=None) -> Tensor");

@@ -78,16 +78,20 @@ __global__ void __launch_bounds__(1024) paths_kernel(const float* __restrict__ p
 
 constexpr int TS = 32;
 
-// grid (np/32, np/32), 256 threads: tile (ti, tj); each thread handles 4 rows of the tile
-__global__ void __launch_bounds__(256) cov_pad_kernel(const float* __restrict__ C, const float* __restrict__ S,
+// grid (np/32, np/32), 256 threads: tile (ti, tj); each thread handles 4 rows of the tile.
+// Every element of C is read only by the thread that writes its C' (Cn may alias C: the
+// captured generation updates the state's covariance in place): a strictly upper tile also
+// writes its transpose into Cp's lower tile, so no workgroup reads another tile of C.
+// Bp (the padded warm-start basis) is optional: the device eigensolver reads B unpadded.
+__global__ void __launch_bounds__(256) cov_pad_kernel(const float* C, const float* __restrict__ S,
                                                       const float* __restrict__ pc, const float* __restrict__ a_ptr, float c1, float cmu,
-                                                      const float* __restrict__ Bprev, int d, int np, float* __restrict__ Cn,
+                                                      const float* __restrict__ Bprev, int d, int np, float* Cn,
                                                       float* __restrict__ Cp, float* __restrict__ Bp) {
   __shared__ float T[TS][TS + 1];
   const int ti = blockIdx.y, tj = blockIdx.x;
   const int c = threadIdx.x & 31, r0 = threadIdx.x >> 5;  // 8 row groups
   const float a = a_ptr[0];
-  // own tile: C' (state) and Bp
+  // own tile: C' (state), Bp, and the upper / diagonal tiles of Cp
 #pragma unroll
   for (int rr = 0; rr < TS; rr += 8) {
     const int i = ti * TS + r0 + rr, j = tj * TS + c;
@@ -95,36 +99,22 @@ __global__ void __launch_bounds__(256) cov_pad_kernel(const float* __restrict__ 
     if (i < d && j < d) {
       v = a * C[(int64_t)i * d + j] + c1 * pc[i] * pc[j] + cmu * S[(int64_t)i * d + j];
       Cn[(int64_t)i * d + j] = v;
-      b = Bprev[(int64_t)i * d + j];
+      if (Bp) b = Bprev[(int64_t)i * d + j];
     }
-    Bp[(int64_t)i * np + j] = b;
-    if (ti < tj) Cp[(int64_t)i * np + j] = v;     // strictly upper tile: as is
-    else if (ti == tj) T[r0 + rr][c] = v;         // diagonal tile: symmetrise from its upper half
+    if (Bp) Bp[(int64_t)i * np + j] = b;
+    if (ti < tj) Cp[(int64_t)i * np + j] = v;  // strictly upper tile: as is
+    if (ti <= tj) T[r0 + rr][c] = v;           // staged for the diagonal / transposed writes
   }
-  if (ti == tj) {
-    __syncthreads();
-#pragma unroll
-    for (int rr = 0; rr < TS; rr += 8) {
-      const int li = r0 + rr, lj = c;
-      const float v = li <= lj ? T[li][lj] : T[lj][li];
-      Cp[(int64_t)(ti * TS + li) * np + tj * TS + lj] = v;
-    }
-    return;
-  }
-  if (ti < tj) return;
-  // strictly lower tile of Cp = transpose of the upper tile C'(tj, ti)
-#pragma unroll
-  for (int rr = 0; rr < TS; rr += 8) {
-    const int i = tj * TS + r0 + rr, j = ti * TS + c;  // element (i, j) of the upper tile
-    float v = (i == j) ? 1.f : 0.f;
-    if (i < d && j < d) v = a * C[(int64_t)i * d + j] + c1 * pc[i] * pc[j] + cmu * S[(int64_t)i * d + j];
-    T[r0 + rr][c] = v;
-  }
+  if (ti > tj) return;  // strictly lower tiles of Cp come from the upper tile (tj, ti)
   __syncthreads();
 #pragma unroll
   for (int rr = 0; rr < TS; rr += 8) {
     const int li = r0 + rr, lj = c;
-    Cp[(int64_t)(ti * TS + li) * np + tj * TS + lj] = T[lj][li];
+    if (ti == tj) {  // diagonal tile: symmetrise from its upper half
+      Cp[(int64_t)(ti * TS + li) * np + tj * TS + lj] = li <= lj ? T[li][lj] : T[lj][li];
+    } else {  // Cp(tj, ti) = C'(ti, tj)ᵀ
+      Cp[(int64_t)(tj * TS + li) * np + ti * TS + lj] = T[lj][li];
+    }
   }
 }
 

@@ -239,9 +239,16 @@ class CMAES(Algorithm):
         ps, pc, sigma, a, _hsig = ops.cma_paths(state.ps.contiguous(), state.pc.contiguous(), y, delta, state.sigma.reshape(1).contiguous(),
                                                 state.count_iter.reshape(1).contiguous(), consts)
         eig_stats = state.eig_stats
+        # hipGraph: C' and B go straight into the captured state buffers (no write-back copy of
+        # 8 MB per generation): cov_pad reads each C element only where it writes it, and the
+        # old B is last read by the eigensolver, before cma_eig_out
+        capturing = torch.cuda.is_current_stream_capturing()
+        c_out = state.C if capturing and state.C.is_contiguous() else None
+        b_out = state.B if capturing and state.B.is_contiguous() else None
         if config.get("eigh") == "sbr":
             np_ = jacobi.padded_size(d)
-            C, Cp, _ = ops.cma_cov_pad(state.C.contiguous(), S.contiguous(), pc, a, float(self.c1), float(self.cmu), state.B.contiguous(), np_)
+            C, Cp, _ = ops.cma_cov_pad(state.C.contiguous(), S.contiguous(), pc, a, float(self.c1), float(self.cmu), state.B.contiguous(), np_,
+                                       c_out, False)
             # Cp[:d, :d] = triu(C) + triu(C, 1)ᵀ, the reference's symmetrisation (cma_es.py:193-195)
             with profiling.phase("eigh"):
                 if config.get("sbr_mode") == "device" and d % 4 == 0 and d <= 8192:
@@ -254,15 +261,15 @@ class CMAES(Algorithm):
                     # host-orchestrated solve: a host phase between hipGraph segments
                     w, Bn, eig_stats = host_phase(sbr_phase, Cp[:d, :d], state.B, self.__dict__.setdefault("_eig_plans", {}),
                                                   out_like=(state.D, state.B, state.eig_stats))
-            B, D, BdivD = ops.cma_eig_out(Bn.contiguous(), w.contiguous(), d)
+            B, D, BdivD = ops.cma_eig_out(Bn.contiguous(), w.contiguous(), d, b_out)
         else:
             np_ = jacobi.padded_size(d)
-            C, Cp, Bp = ops.cma_cov_pad(state.C.contiguous(), S.contiguous(), pc, a, float(self.c1), float(self.cmu), state.B.contiguous(), np_)
+            C, Cp, Bp = ops.cma_cov_pad(state.C.contiguous(), S.contiguous(), pc, a, float(self.c1), float(self.cmu), state.B.contiguous(), np_,
+                                        c_out, True)
             with profiling.phase("eigh"):
                 w, Bp = jacobi.warm_eigh_padded(Cp, Bp, d, max_sweeps=self.eig_sweeps)
-            B, D, BdivD = ops.cma_eig_out(Bp, w, d)
+            B, D, BdivD = ops.cma_eig_out(Bp, w, d, b_out)
         # (B/D)·Bᵀ is symmetric: upper tiles only
-        capturing = torch.cuda.is_current_stream_capturing()
         if config.get("plain_gemm") == "blas":
             invsqrtC = plain_nt(BdivD, B)
         elif capturing and state.invsqrtC.is_contiguous():
