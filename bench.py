@@ -43,9 +43,21 @@ def main():
     ap.add_argument("--monitor", nargs="?", const="host", default=None, choices=["host", "device", "best"],
                     help="attach an EvalMonitor in the timed loop: full fitness history copied to the host "
                          "asynchronously (host), kept on the device (device), or best-so-far only (best)")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: gloo ranks on the host (tests of the launcher only; not a benchmark)")
     args = ap.parse_args()
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    # --gpus N without torchrun: spawn N rank processes here, before this process makes any
+    # HIP call, or fail loudly when fewer than N GPUs are visible (evoxmi/parallel/launch.py)
+    from evoxmi.parallel.launch import LaunchError, ensure_ranks
+
+    if args.simulate_rank is None:
+        try:
+            ensure_ranks(args.gpus, device=args.device)
+        except LaunchError as e:
+            print(f"bench.py: {e}", file=sys.stderr, flush=True)
+            sys.exit(2)
     from evoxmi import config
     from evoxmi import random as rnd
     from evoxmi.algorithms import CMAES
@@ -59,9 +71,13 @@ def main():
         rank, world, device = 0, 1, torch.device("cuda", 0)
         torch.cuda.set_device(device)
     else:
-        rank, world, device = init_distributed(force=args.force_dist)
-    if device.type != "cuda":
-        print("bench.py needs a HIP device", file=sys.stderr)
+        rank, world, device = init_distributed(backend="gloo" if args.device == "cpu" else None, force=args.force_dist)
+        if world != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but the job has {world} rank(s)", file=sys.stderr, flush=True)
+            sys.exit(2)
+    if device.type != "cuda" and args.device == "cuda":
+        print("bench.py: no HIP device visible", file=sys.stderr, flush=True)
+        sys.exit(2)
     torch.manual_seed(0)
     key = rnd.PRNGKey(2024, device=device)
     center = (torch.rand(args.dim, generator=torch.Generator().manual_seed(1)) * 160 - 80).to(device)
@@ -138,12 +154,16 @@ def main():
     ms = elapsed / args.steps * 1e3
     gens_per_s = args.steps / elapsed
     evals_per_s = gens_per_s * args.pop
+    backend = dist.get_backend() if dist_on else None
     if rank == 0:
         out = {
             "metric": "generations/sec + evaluations/sec, CMA-ES pop=10k on CEC'22 at 1/2/4/8 MI355X",
             "value": round(evals_per_s, 1),
             "unit": "evals/s (evaluations/sec; generations/sec in generations_per_sec)",
-            "n_gpus": world,
+            "n_gpus": dist.get_world_size() if dist_on else 1,
+            # ranks of the process group that ran the step (0: no group, one process)
+            "rccl_world": dist.get_world_size() if backend == "nccl" else 0,
+            "dist_backend": backend,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms, 4),
@@ -151,6 +171,10 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "fp32",
+            # the framework GEMM's arithmetic (gemm_ks.hip): an exact 3-way bf16 split with six
+            # bf16 MFMA products, f32-accurate (tests/test_gemm_ks.py: the 2e-6·Σ|ab| bound)
+            "gemm_precision": {"x6": "bf16x6 (f32-accurate)", "x6w": "bf16x6 32x32 (f32-accurate)",
+                               "f32": "f32 MFMA"}.get(config.get("gemm_prec"), config.get("gemm_prec")),
             "data": f"synthetic (seeded CEC'22 F{args.func} shift + Haar rotation at d={args.dim}; random init mean)",
             "generations_per_sec": round(gens_per_s, 3),
             "config": {

@@ -27,6 +27,7 @@ def init_distributed(backend: str = None, timeout_s: int = 600, force: bool = Fa
     Returns ``(rank, world_size, device)``.
     """
     world, rank, local = env_world()
+    backend = backend or os.environ.get("EVOXMI_DIST_BACKEND") or None
     use_gpu = torch.cuda.is_available() and backend != "gloo"
     if use_gpu:
         torch.cuda.set_device(local)

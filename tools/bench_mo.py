@@ -47,6 +47,7 @@ def main():
 
     ap = argparse.ArgumentParser()
     ap.add_argument("--algo", choices=["nsga2", "moead"], default="nsga2")
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU); spawned here unless torchrun started them")
     ap.add_argument("--pop", type=int, default=0)
     ap.add_argument("--dim", type=int, default=0)
     ap.add_argument("--gens", type=int, default=20)
@@ -62,12 +63,23 @@ def main():
     args = ap.parse_args()
     import torch.distributed as dist
     from evoxmi.parallel import init_distributed
+    from evoxmi.parallel.launch import LaunchError, ensure_ranks
+
+    if args.simulate_rank is None:
+        try:
+            ensure_ranks(args.gpus, device="cpu" if args.cpu else "cuda")
+        except LaunchError as e:
+            print(f"bench_mo.py: {e}", file=sys.stderr, flush=True)
+            sys.exit(2)
 
     sim = args.simulate_rank is not None
     if sim:
         rank, world, dev = 0, 1, torch.device("cpu" if args.cpu else "cuda")
     else:
         rank, world, dev = init_distributed(force=args.force_dist, backend="gloo" if args.cpu else None)
+        if world != args.gpus:
+            print(f"bench_mo.py: --gpus {args.gpus} but the job has {world} rank(s)", file=sys.stderr, flush=True)
+            sys.exit(2)
     if args.cpu:
         dev = torch.device("cpu")
     algo, prob = build(args, dev)
@@ -109,7 +121,7 @@ def main():
     fit = a.fitness
     pop = algo.pop_size
     out = {
-        "config": args.algo, "pop": pop, "dim": algo.dim, "n_objs": 3, "graph": not (args.no_graph or args.cpu), "n_gpus": world,
+        "config": args.algo, "pop": pop, "dim": algo.dim, "n_objs": 3, "graph": not (args.no_graph or args.cpu), "n_gpus": dist.get_world_size() if dist.is_initialized() else 1,
         "parallelism": (f"simulated-rank{args.simulate_rank}-of-{args.world}" if sim else (f"pop-shard{world}" if dist_on else "single")),
         "ms_per_gen": round(dt * 1e3, 3), "gens_per_sec": round(1 / dt, 2), "evals_per_sec": round(pop / dt, 1),
         "fitness_finite": bool(torch.isfinite(fit).all()), "mean_obj": [round(float(v), 4) for v in fit.mean(0)],

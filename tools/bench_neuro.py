@@ -24,6 +24,7 @@ def main():
 
     ap = argparse.ArgumentParser()
     ap.add_argument("--pop", type=int, default=8192)
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU); spawned here unless torchrun started them")
     ap.add_argument("--cap", type=int, default=1000)
     ap.add_argument("--gens", type=int, default=5)
     ap.add_argument("--hidden", type=int, default=64)
@@ -37,9 +38,18 @@ def main():
     if args.kernel_only:
         return kernel_only(args)
     from evoxmi.parallel import init_distributed
+    from evoxmi.parallel.launch import LaunchError, ensure_ranks
     import torch.distributed as dist
 
+    try:
+        ensure_ranks(args.gpus)
+    except LaunchError as e:
+        print(f"bench_neuro.py: {e}", file=sys.stderr, flush=True)
+        sys.exit(2)
     rank, world, dev = init_distributed(force=args.force_dist)
+    if world != args.gpus:
+        print(f"bench_neuro.py: --gpus {args.gpus} but the job has {world} rank(s)", file=sys.stderr, flush=True)
+        sys.exit(2)
     dist_on = world > 1 or args.force_dist
     policy = MLPPolicy([27, args.hidden, args.hidden, 8])
     params = policy.init(rnd.PRNGKey(0), device=dev)
@@ -97,7 +107,7 @@ def main():
         dist.all_reduce(dt, op=dist.ReduceOp.MAX)
         dist.all_reduce(env_steps)
     dt, env_steps = float(dt), int(env_steps)
-    out = {"pop": args.pop, "n_gpus": world, "cap_episode": args.cap, "params": policy.num_params, "ms_per_gen": round(dt * 1e3, 2),
+    out = {"pop": args.pop, "n_gpus": dist.get_world_size() if dist.is_initialized() else 1, "cap_episode": args.cap, "params": policy.num_params, "ms_per_gen": round(dt * 1e3, 2),
            "gens_per_sec": round(1 / dt, 3), "env_steps_per_sec": round(env_steps / args.gens / dt, 1),
            "mean_episode_len": round(env_steps / args.gens / args.pop, 1), "graph": args.graph}
     if rank == 0:
