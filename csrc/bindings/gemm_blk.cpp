@@ -1,0 +1,232 @@
+// torch-op bindings of the blocked-planes bf16x6 GEMM (csrc/kernels/gemm_blk.hip).
+#include <torch/library.h>
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/core/DeviceGuard.h>
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "evoxmi_launchers.h"
+
+namespace {
+
+inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a HIP device tensor")
+#define CHECK_F32(t) TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be float32")
+#define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+
+const float* opt_vec(const c10::optional<at::Tensor>& t, int64_t n, const char* what) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t);
+  TORCH_CHECK(t->numel() >= n, what, ": length ", t->numel(), " < ", n);
+  return t->data_ptr<float>();
+}
+
+// planes buffer of `rows` × K: int16 (evx_blk_elems), 16-byte aligned
+void check_blk(const at::Tensor& t, int64_t rows, int64_t K, const char* what) {
+  CHECK_DEV(t);
+  TORCH_CHECK(t.scalar_type() == at::kShort && t.is_contiguous() && t.numel() >= evx_blk_elems(rows, (int)K) &&
+                  reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+              what, ": blocked planes int16[", evx_blk_elems(rows, (int)K), "] for ", rows, " x ", K);
+}
+
+at::Tensor blk_split(const at::Tensor& X, const c10::optional<at::Tensor>& sub_k, const c10::optional<at::Tensor>& colscale,
+                     const c10::optional<at::Tensor>& out) {
+  CHECK_DEV(X); CHECK_F32(X);
+  TORCH_CHECK(X.dim() == 2 && X.stride(1) == 1, "blk_split: 2-D, unit inner stride");
+  const int64_t rows = X.size(0), K = X.size(1);
+  TORCH_CHECK(rows > 0 && K > 0, "blk_split: empty");
+  c10::DeviceGuard g(X.device());
+  at::Tensor o;
+  if (out.has_value() && out->defined()) {
+    o = *out;
+    check_blk(o, rows, K, "blk_split out");
+  } else {
+    o = at::empty({evx_blk_elems(rows, (int)K)}, X.options().dtype(at::kShort));
+  }
+  evx_split_blk(X.data_ptr<float>(), X.stride(0), rows, (int)K, opt_vec(sub_k, K, "sub_k"), opt_vec(colscale, K, "colscale"),
+                reinterpret_cast<uint16_t*>(o.data_ptr<int16_t>()), cur_stream());
+  return o;
+}
+
+at::Tensor blk_philox_normal(const at::Tensor& key, int64_t rows, int64_t d, int64_t row0, const c10::optional<at::Tensor>& out) {
+  CHECK_DEV(key);
+  TORCH_CHECK(key.scalar_type() == at::kLong && key.numel() >= 2 && key.is_contiguous(), "blk_philox_normal: key int64[2]");
+  TORCH_CHECK(d % 4 == 0 && rows > 0, "blk_philox_normal: d % 4 == 0, rows > 0");
+  c10::DeviceGuard g(key.device());
+  at::Tensor o;
+  if (out.has_value() && out->defined()) {
+    o = *out;
+    check_blk(o, rows, d, "blk_philox_normal out");
+  } else {
+    o = at::empty({evx_blk_elems(rows, (int)d)}, key.options().dtype(at::kShort));
+  }
+  evx_philox_blk(key.data_ptr<int64_t>(), rows, (int)d, row0, reinterpret_cast<uint16_t*>(o.data_ptr<int16_t>()), cur_stream());
+  return o;
+}
+
+at::Tensor gemm_blk(const at::Tensor& A, int64_t M, const at::Tensor& B, int64_t N, int64_t K, double alpha,
+                    const c10::optional<at::Tensor>& alpha_ptr, const c10::optional<at::Tensor>& bias_n,
+                    const c10::optional<at::Tensor>& out, const c10::optional<at::Tensor>& skip) {
+  TORCH_CHECK(M > 0 && N > 0 && K > 0, "gemm_blk: shape");
+  check_blk(A, M, K, "gemm_blk A");
+  check_blk(B, N, K, "gemm_blk B");
+  c10::DeviceGuard g(A.device());
+  at::Tensor C;
+  if (out.has_value() && out->defined()) {
+    C = *out;
+    CHECK_DEV(C); CHECK_F32(C);
+    TORCH_CHECK(C.dim() == 2 && C.stride(1) == 1 && C.size(0) >= M && C.size(1) >= N, "gemm_blk: out shape");
+  } else {
+    C = at::empty({M, N}, A.options().dtype(at::kFloat));
+  }
+  EvxGemmBlk a{};
+  a.A = reinterpret_cast<const uint16_t*>(A.data_ptr<int16_t>());
+  a.a_rows = evx_blk_rows(M);
+  a.B = reinterpret_cast<const uint16_t*>(B.data_ptr<int16_t>());
+  a.b_rows = evx_blk_rows(N);
+  a.KB = (int)((K + 15) / 16);
+  a.M = (int)M;
+  a.N = (int)N;
+  a.C = C.data_ptr<float>();
+  a.ldc = C.stride(0);
+  a.alpha = (float)alpha;
+  a.alpha_ptr = opt_vec(alpha_ptr, 1, "alpha_ptr");
+  a.bias_n = opt_vec(bias_n, N, "bias_n");
+  if (skip.has_value() && skip->defined()) {
+    CHECK_DEV(*skip);
+    TORCH_CHECK(skip->scalar_type() == at::kInt, "gemm_blk: skip int32");
+    a.skip = skip->data_ptr<int32_t>();
+  }
+  evx_gemm_blk(a, cur_stream());
+  return C;
+}
+
+void check_h3(const at::Tensor& t, const at::Tensor& rinv, int64_t rows, int64_t K, const char* what) {
+  CHECK_DEV(t); CHECK_DEV(rinv);
+  TORCH_CHECK(t.scalar_type() == at::kShort && t.is_contiguous() && t.numel() >= evx_h3_elems(rows, (int)K) &&
+                  reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+              what, ": f16x3 planes int16[", evx_h3_elems(rows, (int)K), "] for ", rows, " x ", K);
+  TORCH_CHECK(rinv.scalar_type() == at::kFloat && rinv.is_contiguous() && rinv.numel() >= evx_blk_rows(rows), what,
+              ": row scales float32[", evx_blk_rows(rows), "]");
+}
+
+std::vector<at::Tensor> h3_alloc(const at::Tensor& like, int64_t rows, int64_t K, const c10::optional<at::Tensor>& out,
+                                 const c10::optional<at::Tensor>& rinv_out, const char* what) {
+  at::Tensor o, r;
+  if (out.has_value() && out->defined()) {
+    TORCH_CHECK(rinv_out.has_value() && rinv_out->defined(), what, ": out and rinv_out together");
+    o = *out;
+    r = *rinv_out;
+    check_h3(o, r, rows, K, what);
+  } else {
+    o = at::empty({evx_h3_elems(rows, (int)K)}, like.options().dtype(at::kShort));
+    r = at::empty({evx_blk_rows(rows)}, like.options().dtype(at::kFloat));
+  }
+  return {o, r};
+}
+
+std::vector<at::Tensor> h3_split(const at::Tensor& X, const c10::optional<at::Tensor>& sub_k, const c10::optional<at::Tensor>& colscale,
+                                 const c10::optional<at::Tensor>& out, const c10::optional<at::Tensor>& rinv_out) {
+  CHECK_DEV(X); CHECK_F32(X);
+  TORCH_CHECK(X.dim() == 2 && X.stride(1) == 1, "h3_split: 2-D, unit inner stride");
+  const int64_t rows = X.size(0), K = X.size(1);
+  TORCH_CHECK(rows > 0 && K > 0, "h3_split: empty");
+  c10::DeviceGuard g(X.device());
+  auto v = h3_alloc(X, rows, K, out, rinv_out, "h3_split");
+  evx_split_h3(X.data_ptr<float>(), X.stride(0), rows, (int)K, opt_vec(sub_k, K, "sub_k"), opt_vec(colscale, K, "colscale"),
+               reinterpret_cast<uint16_t*>(v[0].data_ptr<int16_t>()), v[1].data_ptr<float>(), cur_stream());
+  return v;
+}
+
+std::vector<at::Tensor> h3_philox_normal(const at::Tensor& key, int64_t rows, int64_t d, int64_t row0, const c10::optional<at::Tensor>& out,
+                                         const c10::optional<at::Tensor>& rinv_out) {
+  CHECK_DEV(key);
+  TORCH_CHECK(key.scalar_type() == at::kLong && key.numel() >= 2 && key.is_contiguous(), "h3_philox_normal: key int64[2]");
+  TORCH_CHECK(d % 4 == 0 && rows > 0, "h3_philox_normal: d % 4 == 0, rows > 0");
+  c10::DeviceGuard g(key.device());
+  auto v = h3_alloc(key, rows, d, out, rinv_out, "h3_philox_normal");
+  evx_philox_h3(key.data_ptr<int64_t>(), rows, (int)d, row0, reinterpret_cast<uint16_t*>(v[0].data_ptr<int16_t>()), v[1].data_ptr<float>(),
+                cur_stream());
+  return v;
+}
+
+at::Tensor gemm_h3(const at::Tensor& A, const at::Tensor& a_rinv, int64_t M, const at::Tensor& B, const at::Tensor& b_rinv, int64_t N,
+                   int64_t K, double alpha, const c10::optional<at::Tensor>& alpha_ptr, const c10::optional<at::Tensor>& bias_n,
+                   const c10::optional<at::Tensor>& out, const c10::optional<at::Tensor>& skip) {
+  TORCH_CHECK(M > 0 && N > 0 && K > 0, "gemm_h3: shape");
+  check_h3(A, a_rinv, M, K, "gemm_h3 A");
+  check_h3(B, b_rinv, N, K, "gemm_h3 B");
+  c10::DeviceGuard g(A.device());
+  at::Tensor C;
+  if (out.has_value() && out->defined()) {
+    C = *out;
+    CHECK_DEV(C); CHECK_F32(C);
+    TORCH_CHECK(C.dim() == 2 && C.stride(1) == 1 && C.size(0) >= M && C.size(1) >= N, "gemm_h3: out shape");
+  } else {
+    C = at::empty({M, N}, A.options().dtype(at::kFloat));
+  }
+  EvxGemmBlk a{};
+  a.A = reinterpret_cast<const uint16_t*>(A.data_ptr<int16_t>());
+  a.a_rows = evx_blk_rows(M);
+  a.B = reinterpret_cast<const uint16_t*>(B.data_ptr<int16_t>());
+  a.b_rows = evx_blk_rows(N);
+  a.a_rinv = a_rinv.data_ptr<float>();
+  a.b_rinv = b_rinv.data_ptr<float>();
+  a.KB = (int)((K + 15) / 16);
+  a.M = (int)M;
+  a.N = (int)N;
+  a.C = C.data_ptr<float>();
+  a.ldc = C.stride(0);
+  a.alpha = (float)alpha;
+  a.alpha_ptr = opt_vec(alpha_ptr, 1, "alpha_ptr");
+  a.bias_n = opt_vec(bias_n, N, "bias_n");
+  if (skip.has_value() && skip->defined()) {
+    CHECK_DEV(*skip);
+    TORCH_CHECK(skip->scalar_type() == at::kInt, "gemm_h3: skip int32");
+    a.skip = skip->data_ptr<int32_t>();
+  }
+  evx_gemm_h3(a, cur_stream());
+  return C;
+}
+
+int64_t h3_elems(int64_t rows, int64_t K) { return evx_h3_elems(rows, (int)K); }
+
+int64_t blk_elems(int64_t rows, int64_t K) { return evx_blk_elems(rows, (int)K); }
+int64_t blk_rows(int64_t rows) { return evx_blk_rows(rows); }
+int64_t gemm_blk_tile(int64_t which) { return which == 0 ? evx_gemm_blk_tile_m() : evx_gemm_blk_tile_n(); }
+
+}  // namespace
+
+TORCH_LIBRARY_FRAGMENT(evoxmi, m) {
+  m.def("blk_split(Tensor X, Tensor? sub_k=None, Tensor? colscale=None, Tensor(a!)? out=None) -> Tensor");
+  m.def("blk_philox_normal(Tensor key, int rows, int d, int row0=0, Tensor(a!)? out=None) -> Tensor");
+  m.def("gemm_blk(Tensor A, int M, Tensor B, int N, int K, float alpha=1., Tensor? alpha_ptr=None, Tensor? bias_n=None, "
+        "Tensor(a!)? out=None, Tensor? skip=None) -> Tensor");
+  m.def("blk_elems(int rows, int K) -> int");
+  m.def("h3_split(Tensor X, Tensor? sub_k=None, Tensor? colscale=None, Tensor(a!)? out=None, Tensor(b!)? rinv_out=None) -> Tensor[]");
+  m.def("h3_philox_normal(Tensor key, int rows, int d, int row0=0, Tensor(a!)? out=None, Tensor(b!)? rinv_out=None) -> Tensor[]");
+  m.def("gemm_h3(Tensor A, Tensor a_rinv, int M, Tensor B, Tensor b_rinv, int N, int K, float alpha=1., Tensor? alpha_ptr=None, "
+        "Tensor? bias_n=None, Tensor(a!)? out=None, Tensor? skip=None) -> Tensor");
+  m.def("h3_elems(int rows, int K) -> int");
+  m.def("blk_rows(int rows) -> int");
+  m.def("gemm_blk_tile(int which) -> int");
+}
+
+TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
+  m.impl("blk_split", &blk_split);
+  m.impl("blk_philox_normal", &blk_philox_normal);
+  m.impl("gemm_blk", &gemm_blk);
+  m.impl("h3_split", &h3_split);
+  m.impl("h3_philox_normal", &h3_philox_normal);
+  m.impl("gemm_h3", &gemm_h3);
+}
+
+TORCH_LIBRARY_IMPL(evoxmi, CompositeExplicitAutograd, m) {
+  m.impl("blk_elems", &blk_elems);
+  m.impl("h3_elems", &h3_elems);
+  m.impl("blk_rows", &blk_rows);
+  m.impl("gemm_blk_tile", &gemm_blk_tile);
+}

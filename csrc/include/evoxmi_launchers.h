@@ -81,6 +81,43 @@ struct EvxGemmKs {
   int force_tile;  // tile code for this launch (0: the shape heuristic)
 };
 void evx_gemm_ks(const EvxGemmKs& a, hipStream_t s);
+// LDS-staged bf16x6 GEMM on "blocked planes" (gemm_blk.hip): an f32 matrix rows × K stored as
+// bf16 [ceil(K/16)][Rp][3][16] (Rp = evx_blk_rows(rows); the buffer carries kEvxBlkSlackRows
+// spare 96-byte records after the last block, read only for output rows / columns past M / N)
+constexpr int kEvxBlkSlackRows = 512;
+struct EvxGemmBlk {
+  const uint16_t* A;  // blocked planes of the M × K operand
+  int64_t a_rows;     // Rp of A
+  const uint16_t* B;  // blocked planes of the N × K operand (C = A·Bᵀ)
+  int64_t b_rows;
+  int KB;             // 16-k blocks
+  int M, N;
+  float* C;
+  int64_t ldc;
+  float alpha;
+  const float* alpha_ptr;
+  const float* bias_n;
+  const int32_t* skip;
+  int tiles_m, tiles_n;  // set by the launcher
+  const float* a_rinv;   // f16x3 only: per-row inverse scales of A (M) and B (N)
+  const float* b_rinv;
+};
+void evx_gemm_blk(const EvxGemmBlk& a, hipStream_t s);
+int evx_gemm_blk_tile_m();
+int evx_gemm_blk_tile_n();
+int64_t evx_blk_rows(int64_t rows);
+int64_t evx_blk_elems(int64_t rows, int K);  // uint16 elements of a blocked-planes buffer
+// blocked planes of (X[r][k] − sub_k[k])·colscale[k] (sub_k / colscale may be null)
+void evx_split_blk(const float* X, int64_t ld, int64_t rows, int K, const float* sub_k, const float* colscale, uint16_t* out,
+                   hipStream_t s);
+// f16x3 planes (gemm_blk.hip): f16 [ceil(K/16)][Rp][2][16] + per-row inverse scales rinv[Rp]
+int64_t evx_h3_elems(int64_t rows, int K);
+void evx_split_h3(const float* X, int64_t ld, int64_t rows, int K, const float* sub_k, const float* colscale, uint16_t* out,
+                  float* rinv, hipStream_t s);
+void evx_philox_h3(const int64_t* key, int64_t rows, int d, int64_t row0, uint16_t* out, float* rinv, hipStream_t s);
+void evx_gemm_h3(const EvxGemmBlk& a, hipStream_t s);
+// blocked planes of rows [row0, row0 + rows) of normal(key, (·, d)) (d % 4 == 0)
+void evx_philox_blk(const int64_t* key, int64_t rows, int d, int64_t row0, uint16_t* out, hipStream_t s);
 // fragment planes of X (rows × K, K-contiguous, row stride ld), X[r][k]·colscale[k] when colscale
 void evx_split_planes(const float* X, int64_t ld, int64_t rows, int K, const float* colscale, uint16_t* out, int64_t kp, hipStream_t s);
 // fragment planes of rows [row0, row0 + rows) of the virtual normal matrix normal(key, (·, d)) (d % 4 == 0)

@@ -37,6 +37,7 @@ from ....ops.eigh import sbr_phase, symmetrize_upper, warm_eigh
 from ....runtime import host_phase
 from ....utils import profiling
 from .... import config
+from ....ops import linalg
 from ....ops.linalg import Operand, gemm, mm, plain_nt
 from ....ops.reduce import weighted_rowsum
 from ....ops.sort import argsort, argsort_i32
@@ -163,6 +164,17 @@ class CMAES(Algorithm):
             out = buf if (rows == self.pop_size and torch.cuda.is_current_stream_capturing() and buf.is_contiguous()
                           and buf.shape == (rows, d)) else None
             return mm_nt(za, bdp, alpha_ptr=state.sigma.reshape(1), bias_n=state.mean, out=out)
+        if (state.B.is_cuda and d % 4 == 0 and config.get("gemm_prec") == "x6"
+                and linalg.tall_nt_ok(rows, d, d, state.B.device)):
+            # tall sampling product on the f16x3 LDS-staged GEMM: the Philox noise is generated
+            # straight into its split planes (the f32 Z is never written), B·diag(D) split once
+            # per generation with D as the column scale, σ and the mean in the epilogue
+            za = linalg.normal_h3_planes(key.to(state.B.device), rows, d, row0)
+            buf = state.population
+            out = buf if (rows == self.pop_size and torch.cuda.is_current_stream_capturing() and buf.is_contiguous()
+                          and buf.shape == (rows, d)) else None
+            return linalg.tall_nt(za, state.B, alpha_ptr=state.sigma.reshape(1), bias_n=state.mean, b_colscale=state.D,
+                                  out=out)
         z = rnd.normal(key, (rows, d), offset=row0 * d)
         if z.is_cuda:
             # X = mean + σ (Z∘D) Bᵀ = mean + Z (σ·B∘D)ᵀ : σ (a device scalar, no host sync)

@@ -284,3 +284,181 @@ def mm_nt(A, B, *, alpha: float = 1.0, alpha_ptr: Optional[torch.Tensor] = None,
     Am = A.t if isinstance(A, Planes) else A
     Bm = B.t if isinstance(B, Planes) else B
     return mm(Am, Bm, tb=True, alpha=alpha, alpha_ptr=alpha_ptr, bias_n=bias_n, out=out, a_sub_k=a_sub_k)
+
+
+# ---------------------------------------------------------------------------- blocked planes
+class BlkPlanes:
+    """An f32 matrix (rows × K) pre-split for the LDS-staged bf16x6 GEMM (``gemm_blk.hip``):
+    bf16 [ceil(K/16)][Rp][3][16] — per 16-k block and row the high / middle / low bf16 parts
+    of its 16 values in one 96-byte record, so a GEMM stage of BM rows is one contiguous copy.
+    Built by :func:`blk_planes` (split pass, optional fused shift / column scale) or
+    :func:`normal_blk_planes` (Philox noise generated straight into planes).  On the CPU the
+    object holds the (shifted, scaled) f32 matrix itself."""
+
+    __slots__ = ("t", "rows", "K")
+
+    def __init__(self, t: torch.Tensor, rows: int, K: int):
+        self.t, self.rows, self.K = t, int(rows), int(K)
+
+    @property
+    def is_cuda(self) -> bool:
+        return self.t.is_cuda
+
+
+def blk_planes(X: torch.Tensor, sub_k: Optional[torch.Tensor] = None, colscale: Optional[torch.Tensor] = None,
+               out: Optional[torch.Tensor] = None) -> BlkPlanes:
+    """Blocked planes of ``(X − sub_k[None, :])·diag(colscale)`` (shift and scale fused into the
+    split pass; ``out``: a buffer from a previous call of the same shape, reused)."""
+    rows, K = X.shape
+    if X.is_cuda:
+        X_ = X if X.stride(-1) == 1 else X.contiguous()
+        return BlkPlanes(_ext.ops().blk_split(X_, _c(sub_k), _c(colscale), out), rows, K)
+    Y = X.to(torch.float32)
+    if sub_k is not None:
+        Y = Y - sub_k[None, :K]
+    if colscale is not None:
+        Y = Y * colscale[None, :K]
+    return BlkPlanes(Y, rows, K)
+
+
+def normal_blk_planes(key: torch.Tensor, rows: int, d: int, row0: int = 0, out: Optional[torch.Tensor] = None) -> BlkPlanes:
+    """Blocked planes of rows [row0, row0 + rows) of ``random.normal(key, (·, d))``, generated in
+    place (the f32 noise is never written); d % 4 == 0 on the device."""
+    if key.is_cuda and d % 4 == 0:
+        return BlkPlanes(_ext.ops().blk_philox_normal(key.contiguous(), int(rows), int(d), int(row0), out), rows, d)
+    from . import random as rnd
+
+    return BlkPlanes(rnd.normal(key, (rows, d), offset=row0 * d).to(key.device), rows, d)
+
+
+def blk_tile() -> tuple:
+    """(BM, BN) output tile of the blocked-planes GEMM."""
+    return int(_ext.ops().gemm_blk_tile(0)), int(_ext.ops().gemm_blk_tile(1))
+
+
+def blk_worthwhile(M: int, N: int, n_cu: int = 256) -> bool:
+    """True when the 320 × 128-tile launch fills the chip (≥ ¾ of the CUs busy in its last
+    wave of tiles) — smaller products stay on the K-split ``gemm_ks``."""
+    tiles = -(-M // 320) * -(-N // 128)
+    if tiles < (3 * n_cu) // 4:
+        return False
+    rem = tiles % n_cu
+    return rem == 0 or rem >= (3 * n_cu) // 4 or tiles >= 4 * n_cu
+
+
+def mm_blk(A: BlkPlanes, B: BlkPlanes, *, alpha: float = 1.0, alpha_ptr: Optional[torch.Tensor] = None,
+           bias_n: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+           skip: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``alpha·(*alpha_ptr)·A·Bᵀ (+ bias_n)`` for blocked-planes operands (A: M × K, B: N × K)."""
+    if A.K != B.K:
+        raise ValueError(f"mm_blk: K mismatch {A.K} vs {B.K}")
+    if A.is_cuda:
+        return _ext.ops().gemm_blk(A.t, A.rows, B.t, B.rows, A.K, float(alpha), _c(alpha_ptr), _c(bias_n), out, skip)
+    C = alpha * (A.t @ B.t.T)
+    if alpha_ptr is not None:
+        C = C * alpha_ptr.reshape(())
+    if bias_n is not None:
+        C = C + bias_n[None, : B.rows]
+    if skip is not None and int(skip.reshape(-1)[0]) != 0:
+        return out if out is not None else torch.zeros_like(C)
+    if out is not None:
+        out.copy_(C)
+        return out
+    return C
+
+
+# ---------------------------------------------------------------------------- f16x3 planes
+class H3Planes:
+    """An f32 matrix (rows × K) split for the f16x3 GEMM (``gemm_blk.hip: gemm_h3_kernel``):
+    each row scaled by a power of two (largest |x| ≤ 2¹⁵), then split into two f16 parts
+    h + m (RNE; |x − h − m| ≤ 2⁻²²|x|), stored as f16 [ceil(K/16)][Rp][2][16] 64-byte records
+    with the row's inverse scale in ``rinv``.  The product keeps h·h + h·m + m·h (three
+    v_mfma_f32_32x32x16_f16 per 32 × 32 block and 16-k block).  On the CPU ``t`` is the f32
+    matrix and ``rinv`` is None."""
+
+    __slots__ = ("t", "rinv", "rows", "K")
+
+    def __init__(self, t: torch.Tensor, rinv: Optional[torch.Tensor], rows: int, K: int):
+        self.t, self.rinv, self.rows, self.K = t, rinv, int(rows), int(K)
+
+    @property
+    def is_cuda(self) -> bool:
+        return self.t.is_cuda
+
+
+def h3_planes(X: torch.Tensor, sub_k: Optional[torch.Tensor] = None, colscale: Optional[torch.Tensor] = None,
+              out: Optional[H3Planes] = None) -> H3Planes:
+    """f16x3 planes of ``(X − sub_k[None, :])·diag(colscale)`` (shift and scale fused into the
+    split pass; ``out``: planes of the same shape from an earlier call, overwritten)."""
+    rows, K = X.shape
+    if X.is_cuda:
+        X_ = X if X.stride(-1) == 1 else X.contiguous()
+        t, r = _ext.ops().h3_split(X_, _c(sub_k), _c(colscale), None if out is None else out.t, None if out is None else out.rinv)
+        return H3Planes(t, r, rows, K)
+    Y = X.to(torch.float32)
+    if sub_k is not None:
+        Y = Y - sub_k[None, :K]
+    if colscale is not None:
+        Y = Y * colscale[None, :K]
+    return H3Planes(Y, None, rows, K)
+
+
+def normal_h3_planes(key: torch.Tensor, rows: int, d: int, row0: int = 0, out: Optional[H3Planes] = None) -> H3Planes:
+    """f16x3 planes of rows [row0, row0 + rows) of ``random.normal(key, (·, d))`` generated in
+    place (fixed scale 2¹³; the f32 noise is never written); d % 4 == 0 on the device."""
+    if key.is_cuda and d % 4 == 0:
+        t, r = _ext.ops().h3_philox_normal(key.contiguous(), int(rows), int(d), int(row0), None if out is None else out.t,
+                                           None if out is None else out.rinv)
+        return H3Planes(t, r, rows, d)
+    from . import random as rnd
+
+    return H3Planes(rnd.normal(key, (rows, d), offset=row0 * d).to(key.device), None, rows, d)
+
+
+def mm_h3(A: H3Planes, B: H3Planes, *, alpha: float = 1.0, alpha_ptr: Optional[torch.Tensor] = None,
+          bias_n: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+          skip: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``alpha·(*alpha_ptr)·A·Bᵀ (+ bias_n)`` for f16x3-planes operands (A: M × K, B: N × K)."""
+    if A.K != B.K:
+        raise ValueError(f"mm_h3: K mismatch {A.K} vs {B.K}")
+    if A.is_cuda:
+        return _ext.ops().gemm_h3(A.t, A.rinv, A.rows, B.t, B.rinv, B.rows, A.K, float(alpha), _c(alpha_ptr), _c(bias_n), out, skip)
+    C = alpha * (A.t @ B.t.T)
+    if alpha_ptr is not None:
+        C = C * alpha_ptr.reshape(())
+    if bias_n is not None:
+        C = C + bias_n[None, : B.rows]
+    if skip is not None and int(skip.reshape(-1)[0]) != 0:
+        return out if out is not None else torch.zeros_like(C)
+    if out is not None:
+        out.copy_(C)
+        return out
+    return C
+
+
+def tall_nt_ok(M: int, N: int, K: int, device) -> bool:
+    """True when ``tall_nt`` takes the f16x3 LDS-staged path for an M × N × K NT product."""
+    from .. import config
+
+    return (device.type == "cuda" and config.get("gemm_tall") == "h3" and config.get("plain_gemm") == "evoxmi"
+            and blk_worthwhile(M, N))
+
+
+def tall_nt(A: torch.Tensor, B: torch.Tensor, *, alpha: float = 1.0, alpha_ptr: Optional[torch.Tensor] = None,
+            bias_n: Optional[torch.Tensor] = None, a_sub_k: Optional[torch.Tensor] = None,
+            b_colscale: Optional[torch.Tensor] = None, b_planes: Optional[H3Planes] = None,
+            out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``alpha·(*alpha_ptr)·(A − a_sub_k)·(B·diag(b_colscale))ᵀ (+ bias_n)`` for a tall product
+    (A: M × K, B: N × K): the f16x3 path (:func:`mm_h3`) when :func:`tall_nt_ok`, otherwise
+    the bf16x6 ``gemm_ks`` kernel.  ``b_planes``: B's planes already split (a constant operand
+    cached by the caller); ``A`` may be an :class:`H3Planes` (a producer wrote them)."""
+    M = A.rows if isinstance(A, H3Planes) else A.shape[0]
+    K = A.K if isinstance(A, H3Planes) else A.shape[1]
+    N = B.shape[0]
+    dev = A.t.device if isinstance(A, H3Planes) else A.device
+    if isinstance(A, H3Planes) or tall_nt_ok(M, N, K, dev):
+        Ap = A if isinstance(A, H3Planes) else h3_planes(A, sub_k=a_sub_k)
+        Bp = b_planes if b_planes is not None else h3_planes(B, colscale=b_colscale)
+        return mm_h3(Ap, Bp, alpha=alpha, alpha_ptr=alpha_ptr, bias_n=bias_n, out=out)
+    Bs = B if b_colscale is None else (B * b_colscale[None, :]).contiguous()
+    return mm(A, Bs, tb=True, alpha=alpha, alpha_ptr=alpha_ptr, bias_n=bias_n, out=out, a_sub_k=a_sub_k)

@@ -212,6 +212,14 @@ class _CEC2022(Problem):
         if X.is_cuda:
             from ... import config
 
+            if linalg.tall_nt_ok(N, M.shape[0], D, X.device):
+                # tall rotation on the f16x3 LDS-staged GEMM: the population's planes with the
+                # shift fused into the split pass; the constant rotation split once and cached
+                key = ("h3", M.data_ptr(), M.shape)
+                pl = self._cache.get(key)
+                if pl is None:
+                    pl = self._cache[key] = linalg.h3_planes(M)
+                return linalg.tall_nt(X, M, alpha=float(s), a_sub_k=o.contiguous(), b_planes=pl)
             if config.get("gemm_planes") and config.get("gemm_prec") == "x6" and config.get("plain_gemm") == "evoxmi" and D % 4 == 0:
                 # the rotation is constant: its bf16x6 fragment planes are split once and reused
                 # by every evaluation (the GEMM splits only the population on the fly)
