@@ -379,20 +379,184 @@ __global__ void __launch_bounds__(256) split_h_kernel(const float* __restrict__ 
   }
 }
 
+// 16 rows per 256-thread workgroup.  Phase 1: each wave reads 4 whole rows (coalesced, lane j
+// takes the 16-k block j, j + 64, …) and reduces the row's max |x| to its scale (LDS).  Phase
+// 2: thread (record, slot) computes one 16-byte slot (8 values of the h or m plane) of a
+// record, so each store instruction writes 1 KiB contiguous (16 rows of one 16-k block); its
+// 32-byte operand read hits L2 (the workgroup's 64 KiB of rows were just read).
+__global__ void __launch_bounds__(256) split_h2_kernel(const float* __restrict__ X, int64_t ld, int64_t rows, int K,
+                                                       const float* __restrict__ sub_k, const float* __restrict__ colscale,
+                                                       uint16_t* __restrict__ out, float* __restrict__ rinv, int64_t Rp, int KB) {
+  __shared__ float s_sc[16];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t r0 = (int64_t)blockIdx.x * 16;
+  auto val = [&](int64_t row, int k) {
+    float x = X[row * ld + k];
+    if (sub_k) x -= sub_k[k];
+    if (colscale) x *= colscale[k];
+    return x;
+  };
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t row = r0 + 4 * w + i;
+    float mx = 0.f;
+    if (row < rows) {
+      for (int k = 4 * lane; k < K; k += 256) {
+        if (k + 3 < K && ((ld | (int64_t)k) & 3) == 0 && !sub_k && !colscale) {
+          const float4 f = *reinterpret_cast<const float4*>(X + row * ld + k);
+          mx = fmaxf(mx, fmaxf(fmaxf(fabsf(f.x), fabsf(f.y)), fmaxf(fabsf(f.z), fabsf(f.w))));
+        } else {
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            if (k + c < K) mx = fmaxf(mx, fabsf(val(row, k + c)));
+        }
+      }
+    }
+    mx = evx::wave_max(mx);
+    if (lane == 0) {
+      const float sc = row < rows ? row_scale(mx) : 1.f;
+      s_sc[4 * w + i] = sc;
+      if (row < Rp) rinv[row] = row < rows ? 1.f / sc : 0.f;
+    }
+  }
+  __syncthreads();
+  // phase 2: 16 rows × 4 slots = 64 threads per 16-k block, 4 blocks per pass
+  const int rl = (threadIdx.x >> 2) & 15, pos = threadIdx.x & 3;
+  const int64_t row = r0 + rl;
+  const float sc = s_sc[rl];
+  const int sw = (int)((row >> 2) & 3), slot = pos ^ sw, plane = slot >> 1, kh = slot & 1;
+  for (int kb = threadIdx.x >> 6; kb < KB; kb += 4) {
+    const int k0 = 16 * kb + 8 * kh;
+    float v[8];
+    if (row < rows) {
+      if (k0 + 8 <= K && ((ld | (int64_t)k0) & 3) == 0) {
+        const float4 f0 = *reinterpret_cast<const float4*>(X + row * ld + k0);
+        const float4 f1 = *reinterpret_cast<const float4*>(X + row * ld + k0 + 4);
+        v[0] = f0.x; v[1] = f0.y; v[2] = f0.z; v[3] = f0.w;
+        v[4] = f1.x; v[5] = f1.y; v[6] = f1.z; v[7] = f1.w;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          if (sub_k) v[c] -= sub_k[k0 + c];
+          if (colscale) v[c] *= colscale[k0 + c];
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v[c] = k0 + c < K ? val(row, k0 + c) : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) v[c] = 0.f;
+    }
+    unsigned o[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const float a0 = v[2 * p] * sc, a1 = v[2 * p + 1] * sc;
+      const f16x2 hb = __builtin_convertvector(f32x2{a0, a1}, f16x2);
+      if (plane == 0) {
+        o[p] = __builtin_bit_cast(unsigned, hb);
+      } else {
+        const f32x2 hf = __builtin_convertvector(hb, f32x2);
+        o[p] = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{a0 - hf.x, a1 - hf.y}, f16x2));
+      }
+    }
+    *reinterpret_cast<uint4*>(out + (((int64_t)kb * Rp + row) * 4 + pos) * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+// 4 rows per 256-thread workgroup (one per wave; K ≤ 1024).  Phase 1: the wave issues all its
+// row's loads at once (4 float4 per lane), stages the shifted / scaled row in LDS and reduces
+// its max |x| to the row scale.  Phase 2: thread (record, slot) computes one 16-byte slot (8
+// values of the h or m plane) from LDS — 16 consecutive threads write the 4 rows' records of
+// one 16-k block, 256 contiguous bytes.
+__global__ void __launch_bounds__(256) split_h4_kernel(const float* __restrict__ X, int64_t ld, int64_t rows, int K,
+                                                       const float* __restrict__ sub_k, const float* __restrict__ colscale,
+                                                       uint16_t* __restrict__ out, float* __restrict__ rinv, int64_t Rp, int KB, int vec) {
+  __shared__ __attribute__((aligned(16))) float s_row[4][1024 + 16];
+  __shared__ float s_sc[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t r0 = (int64_t)blockIdx.x * 4;
+  {
+    const int64_t row = r0 + w;
+    float4 f[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int k = 4 * lane + 256 * c;
+      f[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (row < rows) {
+        if (vec && k + 3 < K) {
+          f[c] = *reinterpret_cast<const float4*>(X + row * ld + k);
+        } else {
+          float t[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) t[e] = k + e < K ? X[row * ld + k + e] : 0.f;
+          f[c] = make_float4(t[0], t[1], t[2], t[3]);
+        }
+      }
+    }
+    float mx = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int k = 4 * lane + 256 * c;
+      float t[4] = {f[c].x, f[c].y, f[c].z, f[c].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool in = k + e < K && row < rows;
+        if (sub_k && in) t[e] -= sub_k[k + e];
+        if (colscale && in) t[e] *= colscale[k + e];
+        if (!in) t[e] = 0.f;
+        mx = fmaxf(mx, fabsf(t[e]));
+      }
+      *reinterpret_cast<float4*>(&s_row[w][k]) = make_float4(t[0], t[1], t[2], t[3]);
+    }
+    mx = evx::wave_max(mx);
+    if (lane == 0) {
+      const float sc = row < rows ? row_scale(mx) : 1.f;
+      s_sc[w] = sc;
+      if (row < Rp) rinv[row] = row < rows ? 1.f / sc : 0.f;
+    }
+  }
+  __syncthreads();
+  const int rl = (threadIdx.x >> 2) & 3, pos = threadIdx.x & 3;
+  const int64_t row = r0 + rl;
+  const float sc = s_sc[rl];
+  const int sw = (int)((row >> 2) & 3), slot = pos ^ sw, plane = slot >> 1, kh = slot & 1;
+  for (int kb = threadIdx.x >> 4; kb < KB; kb += 16) {
+    const float* src = &s_row[rl][16 * kb + 8 * kh];
+    const float4 f0 = *reinterpret_cast<const float4*>(src);
+    const float4 f1 = *reinterpret_cast<const float4*>(src + 4);
+    const float v[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+    unsigned o[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const float a0 = v[2 * p] * sc, a1 = v[2 * p + 1] * sc;
+      const f16x2 hb = __builtin_convertvector(f32x2{a0, a1}, f16x2);
+      if (plane == 0) {
+        o[p] = __builtin_bit_cast(unsigned, hb);
+      } else {
+        const f32x2 hf = __builtin_convertvector(hb, f32x2);
+        o[p] = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{a0 - hf.x, a1 - hf.y}, f16x2));
+      }
+    }
+    *reinterpret_cast<uint4*>(out + (((int64_t)kb * Rp + row) * 4 + pos) * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 // Philox normals straight into f16x3 records at the fixed scale 2¹³ (|z| < 6.7 for 32-bit
-// uniforms: ≤ 5.5e4 < 65504)
+// uniforms: ≤ 5.5e4 < 65504).  Thread (record, half): 8 normals (two Philox blocks), their h
+// and m slots; consecutive threads fill consecutive records.
 __global__ void __launch_bounds__(256) philox_h_kernel(const int64_t* __restrict__ key, int64_t rows, int d, int64_t row0,
                                                        uint16_t* __restrict__ out, float* __restrict__ rinv, int64_t Rp, int KB) {
   uint32_t k0, k1;
   evx::load_key(key, k0, k1);
-  const int64_t total = (int64_t)KB * Rp;
+  const int64_t total = (int64_t)KB * Rp * 2;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t row = t % Rp;
-    const int kb = (int)(t / Rp);
-    float v[16];
+    const int half = (int)(t & 1);
+    const int64_t rec = t >> 1, row = rec % Rp;
+    const int kb = (int)(rec / Rp);
+    float v[8];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int k = 16 * kb + 4 * c;
+    for (int c = 0; c < 2; ++c) {
+      const int k = 16 * kb + 8 * half + 4 * c;
       float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
       if (row < rows && k < d) {
         const int64_t e = (row0 + row) * (int64_t)d + k;
@@ -403,8 +567,20 @@ __global__ void __launch_bounds__(256) philox_h_kernel(const int64_t* __restrict
       v[4 * c + 2] = f.z;
       v[4 * c + 3] = f.w;
     }
-    split16h_store(v, 8192.f, row, reinterpret_cast<uint4*>(out + t * 32));
-    if (kb == 0) rinv[row] = row < rows ? 1.f / 8192.f : 0.f;
+    unsigned H[4], M[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const float a0 = v[2 * p] * 8192.f, a1 = v[2 * p + 1] * 8192.f;
+      const f16x2 hb = __builtin_convertvector(f32x2{a0, a1}, f16x2);
+      const f32x2 hf = __builtin_convertvector(hb, f32x2);
+      H[p] = __builtin_bit_cast(unsigned, hb);
+      M[p] = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{a0 - hf.x, a1 - hf.y}, f16x2));
+    }
+    const int sw = (int)((row >> 2) & 3);
+    uint4* dst = reinterpret_cast<uint4*>(out + rec * 32);
+    dst[half ^ sw] = make_uint4(H[0], H[1], H[2], H[3]);
+    dst[(2 + half) ^ sw] = make_uint4(M[0], M[1], M[2], M[3]);
+    if (kb == 0 && half == 0) rinv[row] = row < rows ? 1.f / 8192.f : 0.f;
   }
 }
 
@@ -673,12 +849,18 @@ void evx_split_h3(const float* X, int64_t ld, int64_t rows, int K, const float* 
   const int KB = (K + 15) / 16;
   const int64_t Rp = evx_blk_rows(rows);
   const int vec = (reinterpret_cast<uintptr_t>(X) % 16 == 0) && (ld % 4 == 0);
-  split_h_kernel<<<(unsigned)((Rp + 3) / 4), 256, 0, s>>>(X, ld, rows, K, sub_k, colscale, out, rinv, Rp, KB, vec);
+  if (K <= 1024) {
+    split_h4_kernel<<<(unsigned)(Rp / 4), 256, 0, s>>>(X, ld, rows, K, sub_k, colscale, out, rinv, Rp, KB, vec);
+  } else if (reinterpret_cast<uintptr_t>(X) % 16 == 0) {
+    split_h2_kernel<<<(unsigned)(Rp / 16), 256, 0, s>>>(X, ld, rows, K, sub_k, colscale, out, rinv, Rp, KB);
+  } else {
+    split_h_kernel<<<(unsigned)((Rp + 3) / 4), 256, 0, s>>>(X, ld, rows, K, sub_k, colscale, out, rinv, Rp, KB, 0);
+  }
 }
 
 void evx_philox_h3(const int64_t* key, int64_t rows, int d, int64_t row0, uint16_t* out, float* rinv, hipStream_t s) {
   const int KB = (d + 15) / 16;
-  const int64_t Rp = evx_blk_rows(rows), total = (int64_t)KB * Rp;
+  const int64_t Rp = evx_blk_rows(rows), total = (int64_t)KB * Rp * 2;
   int g = (int)((total + 255) / 256);
   if (g > 8192) g = 8192;
   if (g > 0) philox_h_kernel<<<g, 256, 0, s>>>(key, rows, d, row0, out, rinv, Rp, KB);
