@@ -223,6 +223,12 @@ def main():
                 "mean_refine_iters": float(dev_hist[:, 2].mean()),
                 "max_refine_iters": int(dev_hist[:, 2].max()),
                 "fallbacks": int(dev_hist[:, 3].sum()),
+                # status bits of each solve (eigh_sbr_dev.hip): 1 capped (not converged),
+                # 2 recovered from a divergence, 4 stopped by the lean-slot guard
+                "capped": int((dev_hist[:, 1].long() & 1).sum()),
+                "recovered": int(((dev_hist[:, 1].long() & 2) != 0).sum()),
+                "lean_guard_stops": int(((dev_hist[:, 1].long() & 4) != 0).sum()),
+                "schedule_escalations": int(algo.__dict__.get("_esc_count", 0)),
                 # refinement iterations of each timed generation, in order
                 "iters_per_gen": "".join(str(min(int(v), 9)) if v < 10 else "+" for v in dev_hist[:, 2].tolist()),
             }

@@ -160,7 +160,8 @@ at::Tensor gemm_ks(const at::Tensor& A, int64_t a_kc, const at::Tensor& B, int64
                    const c10::optional<at::Tensor>& out, const c10::optional<at::Tensor>& skip,
                    const c10::optional<at::Tensor>& a_sub_k, const c10::optional<at::Tensor>& sel = c10::nullopt,
                    const c10::optional<at::Tensor>& A2 = c10::nullopt, double alpha2 = 0.0,
-                   const c10::optional<at::Tensor>& C2 = c10::nullopt, const c10::optional<at::Tensor>& stat_part = c10::nullopt) {
+                   const c10::optional<at::Tensor>& C2 = c10::nullopt, const c10::optional<at::Tensor>& stat_part = c10::nullopt,
+                   int64_t stat_diag_only = 0) {
   CHECK_DEV(A); CHECK_F32(A); CHECK_DEV(B); CHECK_F32(B);
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.stride(1) == 1 && B.stride(1) == 1, "gemm_ks: 2-D operands with unit inner stride");
   TORCH_CHECK(M > 0 && N > 0 && K > 0, "gemm_ks: empty shape");
@@ -243,6 +244,7 @@ at::Tensor gemm_ks(const at::Tensor& A, int64_t a_kc, const at::Tensor& B, int64
     TORCH_CHECK(stat_part->scalar_type() == at::kDouble && stat_part->is_contiguous() &&
                 stat_part->numel() >= 4 * (int64_t)evx_gemm_ks_grid((int)M, (int)N, (int)mode), "gemm_ks: stat_part float64[4·grid]");
     a.stat_part = stat_part->data_ptr<double>();
+    a.stat_diag_only = (int)stat_diag_only;
   }
   a.c_vec4 = vec4_ok(C) ? 1 : 0;
   evx_gemm_ks(a, cur_stream());
@@ -373,8 +375,9 @@ void gemm_ks_out(const at::Tensor& A, int64_t a_kc, const at::Tensor& B, int64_t
                  int64_t mode, double alpha, const c10::optional<at::Tensor>& alpha_ptr, const c10::optional<at::Tensor>& bias_n,
                  double beta, const c10::optional<at::Tensor>& Cin, const at::Tensor& out, const c10::optional<at::Tensor>& skip,
                  const c10::optional<at::Tensor>& a_sub_k, const c10::optional<at::Tensor>& sel, const c10::optional<at::Tensor>& A2,
-                 double alpha2, const c10::optional<at::Tensor>& C2, const c10::optional<at::Tensor>& stat_part) {
-  gemm_ks(A, a_kc, B, b_kc, M, N, K, mode, alpha, alpha_ptr, bias_n, beta, Cin, out, skip, a_sub_k, sel, A2, alpha2, C2, stat_part);
+                 double alpha2, const c10::optional<at::Tensor>& C2, const c10::optional<at::Tensor>& stat_part, int64_t stat_diag_only) {
+  gemm_ks(A, a_kc, B, b_kc, M, N, K, mode, alpha, alpha_ptr, bias_n, beta, Cin, out, skip, a_sub_k, sel, A2, alpha2, C2, stat_part,
+          stat_diag_only);
 }
 
 int64_t gemm_ks_grid(int64_t M, int64_t N, int64_t mode) { return evx_gemm_ks_grid((int)M, (int)N, (int)mode); }
@@ -477,8 +480,18 @@ void sbr16_bq_out(const at::Tensor& B, const at::Tensor& perm, const at::Tensor&
                Bq.stride(0), (int)sb, cur_stream(), skip.data_ptr<int>());
 }
 
+// X² stats partials (gemm_ks MODE 1 epilogue, double[4·nparts]) for the free ‖X‖ bound, may be absent
+const double* xpart_ptr(const c10::optional<at::Tensor>& xpart, int64_t& nparts) {
+  nparts = 0;
+  if (!xpart.has_value() || !xpart->defined()) return nullptr;
+  CHECK_DEV(*xpart); CHECK_CONTIG(*xpart);
+  TORCH_CHECK(xpart->scalar_type() == at::kDouble && xpart->numel() % 4 == 0, "xpart: float64[4·nparts]");
+  nparts = xpart->numel() / 4;
+  return xpart->data_ptr<double>();
+}
+
 void sbr_damping_out(const at::Tensor& X2, const at::Tensor& V, double tau, at::Tensor& alpha, at::Tensor& work, const at::Tensor& skip,
-                     const c10::optional<at::Tensor>& bar, bool no_final) {
+                     const c10::optional<at::Tensor>& bar, bool no_final, const c10::optional<at::Tensor>& xpart) {
   const int64_t n = X2.size(0);
   TORCH_CHECK(V.numel() >= n * 8 && work.numel() >= n * 24 && alpha.numel() >= 1, "sbr_damping_out: shapes");
   if (bar.has_value() && bar->defined()) {  // one persistent launch (grid barriers), see eigh_sbr16.hip
@@ -488,12 +501,14 @@ void sbr_damping_out(const at::Tensor& X2, const at::Tensor& V, double tau, at::
                           alpha.data_ptr<float>(), cur_stream(), skip.data_ptr<int>(), reinterpret_cast<uint32_t*>(bar->data_ptr<int>()));
     return;
   }
+  int64_t np = 0;
+  const double* xp = xpart_ptr(xpart, np);
   evx_sbr_damping(X2.data_ptr<float>(), (int)n, X2.stride(0), V.data_ptr<float>(), work.data_ptr<float>(), (float)tau,
-                  alpha.data_ptr<float>(), cur_stream(), skip.data_ptr<int>(), no_final ? 1 : 0);
+                  alpha.data_ptr<float>(), cur_stream(), skip.data_ptr<int>(), no_final ? 1 : 0, xp, (int)np);
 }
 
 void sbr_dev_prep(const at::Tensor& X, const at::Tensor& X2, const at::Tensor& X3, at::Tensor& alpha, at::Tensor& P, at::Tensor& MT,
-                  const at::Tensor& ctrl, const c10::optional<at::Tensor>& work, double tau) {
+                  const at::Tensor& ctrl, const c10::optional<at::Tensor>& work, double tau, const c10::optional<at::Tensor>& xpart) {
   for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&X, &X2, &X3, &P, &MT}) {
     CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t);
     TORCH_CHECK(t->sizes() == X.sizes(), "sbr_dev_prep: n×n");
@@ -508,8 +523,10 @@ void sbr_dev_prep(const at::Tensor& X, const at::Tensor& X2, const at::Tensor& X
     v2 = work->data_ptr<float>() + 8 * n;
     v3 = work->data_ptr<float>() + 16 * n;
   }
+  int64_t np = 0;
+  const double* xp = xpart_ptr(xpart, np);
   evx_sbr_dev_prep(X.data_ptr<float>(), X2.data_ptr<float>(), X3.data_ptr<float>(), (int)X.size(0), alpha.data_ptr<float>(),
-                   P.data_ptr<float>(), MT.data_ptr<float>(), ctrl.data_ptr<int>(), cur_stream(), v2, v3, (float)tau);
+                   P.data_ptr<float>(), MT.data_ptr<float>(), ctrl.data_ptr<int>(), cur_stream(), v2, v3, (float)tau, xp, (int)np);
 }
 
 void sbr_dev_copy(const at::Tensor& src, at::Tensor& dst, const at::Tensor& skip) {
@@ -524,14 +541,15 @@ void sbr_dev_ctrl(const at::Tensor& part, int64_t nparts, int64_t j, int64_t K, 
                   at::Tensor& ctrl, at::Tensor& st, std::vector<double> prm, int64_t ns_iters, const at::Tensor& A, at::Tensor& w_out,
                   at::Tensor& eig_stats, at::Tensor& w_init, at::Tensor& log, at::Tensor& log_count) {
   TORCH_CHECK(log.scalar_type() == at::kDouble && log.is_contiguous() && log_count.scalar_type() == at::kInt, "sbr_dev_ctrl: log");
-  TORCH_CHECK(prm.size() == 8, "sbr_dev_ctrl: params [tol, ns_kappa, damp_kappa, t4_kappa, near_only, theta0, theta_kappa, lean_from]");
+  TORCH_CHECK(prm.size() >= 8, "sbr_dev_ctrl: params [tol, ns_kappa, damp_kappa, t4_kappa, near_only, theta0, theta_kappa, lean_from, (recover, lean_guard)]");
   TORCH_CHECK(hist.scalar_type() == at::kDouble && hist.numel() >= 4 * (K + 1) && ctrl.numel() >= 8 * K && alpha.numel() >= K + 1 &&
                   theta.numel() >= K && st.numel() >= 8 && part.numel() >= 4 * nparts, "sbr_dev_ctrl: buffers");
   float p6[7] = {(float)prm[0], (float)prm[1], (float)prm[2], (float)prm[3], (float)prm[4], (float)prm[5], (float)prm[6]};
   evx_sbr_dev_ctrl(part.data_ptr<double>(), (int)nparts, (int)j, (int)K, hist.data_ptr<double>(), alpha.data_ptr<float>(),
                    theta.data_ptr<float>(), ctrl.data_ptr<int>(), st.data_ptr<int>(), p6, (int)ns_iters, A.data_ptr<float>(), A.stride(0),
                    (int)A.size(0), w_out.data_ptr<float>(), eig_stats.data_ptr<double>(), w_init.data_ptr<float>(),
-                   log.data_ptr<double>(), (int)(log.numel() / 4), log_count.data_ptr<int>(), cur_stream(), (int)prm[7]);
+                   log.data_ptr<double>(), (int)(log.numel() / 4), log_count.data_ptr<int>(), cur_stream(), (int)prm[7],
+                   prm.size() > 8 ? (int)prm[8] : 0, prm.size() > 9 ? (int)prm[9] : 0, prm.size() > 10 ? (int)prm[10] : 0);
 }
 
 std::vector<at::Tensor> argsort_f32(const at::Tensor& keys, int64_t descending) {
@@ -1451,15 +1469,15 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("classic_eval(Tensor X, int func, float a, float b, float c) -> Tensor");
   m.def("gemm_f32(Tensor A, int a_rc, Tensor? a_gather, Tensor? a_sub, int a_sub_on_k, Tensor? a_kscale, Tensor? a_kw, Tensor? a_sscale, int a_sscale_inv, Tensor B, int b_rc, Tensor? b_gather, Tensor? b_sub, int b_sub_on_k, Tensor? b_kscale, Tensor? b_kw, Tensor? b_sscale, int b_sscale_inv, Tensor? alpha_ptr, Tensor? bias_n, float beta, Tensor? Cin, int M, int N, int K, int splits, float alpha) -> Tensor");
   m.def("gemm_ks(Tensor A, int a_kc, Tensor B, int b_kc, int M, int N, int K, int mode, float alpha, Tensor? alpha_ptr, Tensor? bias_n, float beta, Tensor? Cin, Tensor? skip, Tensor? a_sub_k=None) -> Tensor");
-  m.def("gemm_ks_out(Tensor A, int a_kc, Tensor B, int b_kc, int M, int N, int K, int mode, float alpha, Tensor? alpha_ptr, Tensor? bias_n, float beta, Tensor? Cin, Tensor(a!) out, Tensor? skip, Tensor? a_sub_k=None, Tensor? sel=None, Tensor? A2=None, float alpha2=0., Tensor(b!)? C2=None, Tensor(c!)? stat_part=None) -> ()");
+  m.def("gemm_ks_out(Tensor A, int a_kc, Tensor B, int b_kc, int M, int N, int K, int mode, float alpha, Tensor? alpha_ptr, Tensor? bias_n, float beta, Tensor? Cin, Tensor(a!) out, Tensor? skip, Tensor? a_sub_k=None, Tensor? sel=None, Tensor? A2=None, float alpha2=0., Tensor(b!)? C2=None, Tensor(c!)? stat_part=None, int stat_diag_only=0) -> ()");
   m.def("gemm_ks_grid(int M, int N, int mode) -> int");
   m.def("gemm_ks_tile(int M, int N, int mode) -> int");
   m.def("cec_rotated_rowterms(Tensor X, Tensor Mrot, Tensor o, float alpha, int fid) -> Tensor");
   m.def("sbr16_block_out(Tensor A, int shift, int sweeps, int sb, Tensor(a!) perm, Tensor(b!) Q, Tensor(c!) dq, Tensor skip, float skip_tol=0.0) -> ()");
   m.def("sbr16_far_out(Tensor A, Tensor perm, Tensor Q, Tensor dq, Tensor stats, float thr_fac, Tensor theta, Tensor(a!) X, int sb, Tensor skip) -> ()");
   m.def("sbr16_bq_out(Tensor B, Tensor perm, Tensor Q, Tensor(a!) Bq, int sb, Tensor skip) -> ()");
-  m.def("sbr_damping_out(Tensor X2, Tensor V, float tau, Tensor(a!) alpha, Tensor(b!) work, Tensor skip, Tensor(c!)? bar=None, bool no_final=False) -> ()");
-  m.def("sbr_dev_prep(Tensor X, Tensor X2, Tensor X3, Tensor(c!) alpha, Tensor(a!) P, Tensor(b!) MT, Tensor ctrl, Tensor? work=None, float tau=1.0) -> ()");
+  m.def("sbr_damping_out(Tensor X2, Tensor V, float tau, Tensor(a!) alpha, Tensor(b!) work, Tensor skip, Tensor(c!)? bar=None, bool no_final=False, Tensor? xpart=None) -> ()");
+  m.def("sbr_dev_prep(Tensor X, Tensor X2, Tensor X3, Tensor(c!) alpha, Tensor(a!) P, Tensor(b!) MT, Tensor ctrl, Tensor? work=None, float tau=1.0, Tensor? xpart=None) -> ()");
   m.def("sbr_dev_copy(Tensor src, Tensor(a!) dst, Tensor skip) -> ()");
   m.def("sbr_dev_ctrl(Tensor part, int nparts, int j, int K, Tensor(a!) hist, Tensor(b!) alpha, Tensor(c!) theta, Tensor(d!) ctrl, Tensor(e!) st, float[] prm, int ns_iters, Tensor A, Tensor(f!) w_out, Tensor(g!) eig_stats, Tensor(h!) w_init, Tensor(i!) log, Tensor(j!) log_count) -> ()");
   m.def("gemm_ks_set_tile(int t) -> ()");

@@ -59,6 +59,7 @@ struct EvxGemmKs {
   // symmetric mode: per-workgroup stats partials [Σ offdiag², Σ diag², min diag, max diag]
   // (double[4] per workgroup, sbr_stats_final layout), may be null
   double* stat_part;
+  int stat_diag_only;  // stats of the diagonal only ([0, Σ diag², min, max]: the X² bounds of the eigensolver)
   int c_vec4;
   int tiles_m, tiles_n;  // set by the launcher
   // row-terms epilogue (MODE 0, CEC'22 F1 / F4 on the rotated population): C is not written;
@@ -222,7 +223,7 @@ int evx_sbr16_nblocks(int n, int sb);
 int evx_sbr16_max_n();
 void evx_sbr_taylor4_prep(const float* X, const float* X2, int n, const float* alpha, float* P, float* M, hipStream_t s, int mt = 0);
 void evx_sbr_damping(const float* X2, int n, int64_t ldx, const float* V, float* work, float tau, float* alpha, hipStream_t s,
-                     const int* skip = nullptr, int no_final = 0);
+                     const int* skip = nullptr, int no_final = 0, const double* xpart = nullptr, int nparts = 0);
 void evx_sbr_damping_fused(const float* X2, int n, int64_t ldx, const float* V, float* work, float tau, float* alpha, hipStream_t s,
                            const int* skip, uint32_t* bar);
 void evx_sbr16_block(const float* A, int n, int64_t lda, int shift, int sweeps, int* perm, float* Q, float* dq, int sb, hipStream_t s,
@@ -253,11 +254,12 @@ void evx_linear_gp_fit(const double* a, const double* b, const double* c, const 
 // device-controlled SBR schedule (eigh_sbr_dev.hip)
 void evx_sbr_dev_prep(const float* X, const float* X2, const float* X3, int n, float* alpha, float* P, float* MT, const int* ctrl,
                       hipStream_t s, const float* V2 = nullptr, const float* V3 = nullptr,
-                      float tau = 1.f);
+                      float tau = 1.f, const double* xpart = nullptr, int nparts = 0);
 void evx_sbr_dev_copy(const float* src, float* dst, int64_t n, const int* skip, hipStream_t s);
+void evx_sbr_report(const double* stats, int* seq, double* ring, int R, hipStream_t s);
 void evx_sbr_dev_ctrl(const double* part, int nparts, int j, int K, double* hist, float* alpha, float* theta, int* ctrl, int* st,
                       const float* prm6, int ns_iters, const float* A, int64_t lda, int n, float* w_out, double* eig_stats, float* w_init,
-                      double* log, int log_len, int* log_count, hipStream_t s, int lean_from = 1 << 30);
+                      double* log, int log_len, int* log_count, hipStream_t s, int lean_from = 1 << 30, int recover = 0, int lean_guard = 0, int xgate = 0);
 // far generator + Bq in one launch (skip_far / skip_bq: their control words)
 void evx_sbr16_far_bq(const float* A, int n, int64_t lda, const int* perm, const float* Q, const float* dq, const double* stats,
                       float thr_fac, const float* theta_ptr, float* X, int64_t ldx, const float* B, int rows, int64_t ldb, float* Bq,

@@ -550,8 +550,13 @@ __global__ void __launch_bounds__(256) sbr16_far_bq_kernel(const float* __restri
 // α = min(1, τ / sqrt(max_j ‖V3_j‖ / ‖V2_j‖)).  Replaces ~15 small library launches.
 __global__ void __launch_bounds__(256) sbr_power_step_kernel(const float* __restrict__ X2, int n, int64_t ldx,
                                                              const float* __restrict__ Vin, float* __restrict__ Vout,
-                                                             const int* __restrict__ skip) {
-  if (skip && *skip) return;
+                                                             const int* __restrict__ skip, const double* __restrict__ xpart = nullptr,
+                                                             int nparts = 0, float tau2 = 0.f) {
+  if (xpart) {  // the free ‖X‖ bounds decide (evx_sbr_damp_runs; the prep kernel applies the same test)
+    if (!evx_sbr_damp_runs(skip ? *skip : 0, evx_sbr_xbounds(xpart, nparts, n), tau2)) return;
+  } else if (skip && *skip) {
+    return;
+  }
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= n) return;
   const float* x = X2 + (int64_t)row * ldx;
@@ -785,14 +790,15 @@ void evx_sbr_damping_fused(const float* X2, int n, int64_t ldx, const float* V, 
 }
 
 void evx_sbr_damping(const float* X2, int n, int64_t ldx, const float* V, float* work, float tau, float* alpha, hipStream_t s,
-                     const int* skip, int no_final) {
+                     const int* skip, int no_final, const double* xpart, int nparts) {
   float* V1 = work;
   float* V2 = work + (int64_t)n * 8;
   float* V3 = work + (int64_t)n * 16;
   const int g = (n + 3) / 4;
-  sbr_power_step_kernel<<<g, 256, 0, s>>>(X2, n, ldx, V, V1, skip);
-  sbr_power_step_kernel<<<g, 256, 0, s>>>(X2, n, ldx, V1, V2, skip);
-  sbr_power_step_kernel<<<g, 256, 0, s>>>(X2, n, ldx, V2, V3, skip);
+  const float t2 = tau * tau;
+  sbr_power_step_kernel<<<g, 256, 0, s>>>(X2, n, ldx, V, V1, skip, xpart, nparts, t2);
+  sbr_power_step_kernel<<<g, 256, 0, s>>>(X2, n, ldx, V1, V2, skip, xpart, nparts, t2);
+  sbr_power_step_kernel<<<g, 256, 0, s>>>(X2, n, ldx, V2, V3, skip, xpart, nparts, t2);
   // no_final: the consumer (the device schedule's Taylor prep) forms α from V2 / V3 itself
   if (!no_final) sbr_damping_final_kernel<<<1, 256, 0, s>>>(V2, V3, n, tau, alpha, skip);
 }

@@ -15,7 +15,23 @@
 //   0 skip_all   1 skip_far   2 skip_damp   3 skip_x3 (order 4)   4 sel6 (order 6)
 //   5 skip_ns    6 sel_ns (Bq·V lands in the Newton–Schulz input)   7 skip_copy (near-only: Bq → B)
 // Persistent words st[8]: 0 stopped, 1 fallback (diverged), 2 refinement iterations run,
-//   3 last_far, 4 theta sticky, 5 keep (0 ⇒ restore the warm-start basis), 6 converged.
+//   3 last_far, 4 theta sticky, 5 keep (0 ⇒ restore the warm-start basis), 6 converged,
+//   7 status bits (1 recovered from a divergence, 2 stopped by the lean-slot guard, 4 the basis
+//     lost orthogonality at some iteration) | recoveries << 8.
+//
+// Divergence (round 5): an iteration whose off-norm grew past 1.5× the previous one no longer
+// ends the solve with the warm-start basis.  While recoveries remain (prm.recover) the next
+// iteration is forced damped (‖αX‖ ≤ τ) with a Newton–Schulz re-orthonormalisation, from the
+// current basis; a non-finite off-norm, or a divergence with no recovery left / no full slot
+// left, stops the solve and keeps the better of the current and the warm-start basis.  A lean
+// slot (no damping / Newton–Schulz / order-6 kernels) whose iteration the full rules would have
+// damped, re-orthonormalised or expanded to order 6 is not taken: the solve stops there,
+// capped.  An iteration after which ‖BᵀCB‖_F moved off ‖C‖_F (the warm start's) by more than
+// 1e-3 relative lost orthogonality: it is treated as a divergence, and such a basis is never
+// kept.  eig_stats = [off_rel, status, iterations, fallback] with status bit 1 = not
+// converged (capped), 2 = recovered from a divergence, 4 = stopped by the lean-slot guard,
+// 8 = orthogonality drift seen —
+// read by the host one generation late (CMAES.graph_variant escalates the schedule).
 #include "evoxmi_common.h"
 #include "evoxmi_sbr.h"
 #include <float.h>
@@ -29,6 +45,9 @@ struct SbrDevParams {
   float theta_kappa;
   int ns_iters;
   int lean_from;  // slots ≥ lean_from carry no damping / Newton–Schulz / X³ kernels (order 4, undamped)
+  int recover;    // divergences recovered by a forced damped step before the solve gives up (0: stop at the first)
+  int lean_guard; // 1: a lean slot whose step would need damping / Newton–Schulz / order 6 stops the solve (capped)
+  int xgate;      // 1: the damping kernels are scheduled for every full-slot far step and gate themselves (sbr_dev_prep)
 };
 
 __device__ __forceinline__ void rel_kappa(const double* h, double& r, double& k) {
@@ -41,19 +60,35 @@ __device__ __forceinline__ void rel_kappa(const double* h, double& r, double& k)
 // exp(−αX) (the transposed product, ops/sbr.py:expm_t_device).  V2 != null: when this
 // iteration's damping ran (ctrl[2] == 0) every workgroup forms α from its power-step vectors
 // itself and workgroup 0 stores it — the damping's own single-workgroup final launch is gone.
+//
+// Step size (round 5).  With the X² GEMM's stats partials (xpart) the damping also follows
+// free bounds of the generator (evx_sbr_xbounds: max row norm² ≤ ‖X‖₂² ≤ sqrt(n·Σ diag(X²)²)):
+// the power iteration never runs when the upper bound proves ‖X‖₂ ≤ τ (α = 1 exact), and a far
+// step the κ rule would leave undamped still gets it when some row of X is longer than τ/2
+// (evx_sbr_damp_runs).  An undamped step on a large generator — which diverged the d = 2000 cold start at
+// κ = 0.4 < damp_kappa (profiles/r5_eigh_recover.txt) — no longer happens.  (Using the
+// Frobenius bound itself as the step size throttled normal solves: ‖X‖_F ≫ ‖X‖₂ when many
+// pairs rotate at once.)
 __global__ void __launch_bounds__(256) sbr_dev_prep_kernel(const float* __restrict__ X, const float* __restrict__ X2,
                                                            const float* __restrict__ X3, int n, float* __restrict__ alpha,
                                                            float* __restrict__ P, float* __restrict__ MT, const int* __restrict__ ctrl,
-                                                           const float* __restrict__ V2, const float* __restrict__ V3, float tau) {
+                                                           const float* __restrict__ V2, const float* __restrict__ V3, float tau,
+                                                           const double* __restrict__ xpart, int nparts) {
   if (ctrl[1]) return;
   const bool six = ctrl[4] != 0;
   float a;
-  if (V2 && ctrl[2] == 0) {
+  if (xpart) {
+    const bool ran = V2 && evx_sbr_damp_runs(ctrl[2], evx_sbr_xbounds(xpart, nparts, n), tau * tau);
+    a = ran ? evx_sbr_damping_alpha(V2, V3, n, tau) : 1.f;
+  } else if (V2 && ctrl[2] == 0) {
     a = evx_sbr_damping_alpha(V2, V3, n, tau);
-    if (blockIdx.x == 0 && threadIdx.x == 0) alpha[0] = a;
   } else {
     a = alpha[0];
   }
+  if (xpart || (V2 && ctrl[2] == 0)) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) alpha[0] = a;
+  }
+
   const float a2 = a * a, a3 = a2 * a;
   // rows over the grid, columns over the threads (float4 when n % 4 == 0): no per-element
   // 64-bit division (the flat-index form spent most of its time in the i = e / n expansion)
@@ -172,18 +207,41 @@ __global__ void __launch_bounds__(256) sbr_dev_ctrl_kernel(const double* __restr
       st[3] = 1;  // last_far
       st[4] = 0;  // theta sticky
       st[6] = 0;  // converged
+      st[7] = 0;  // status bits | recoveries << 8
       alpha[0] = 1.f;
     }
     double r, k;
     rel_kappa(hj1, r, k);
+    double r0, k0;
+    rel_kappa(hist, r0, k0);  // the warm start's off-norm
+    // orthogonality monitor for free: ‖BᵀCB‖_F = ‖C‖_F for an orthogonal B, so the Frobenius
+    // norm of A (off + diag parts, both in the stats) drifting from the warm start's means the
+    // basis lost orthogonality — which the relative off-norm alone does not see
+    const double F0 = hist[0] + hist[1], F = hj1[0] + hj1[1];
+    const bool ortho = F0 > 0.0 && fabs(F / F0 - 1.0) <= 1e-3;
+    bool force = false;       // the next iteration must be damped + re-orthonormalised
+    // the solve stops here keeping the better basis: the current one (finite, orthogonal and
+    // closer to diagonal), or the warm start
+    auto give_up = [&](bool finite_now) {
+      st[0] = 1;
+      st[1] = (finite_now && ortho && r < r0) ? 0 : 1;
+    };
     if (j >= 0 && executed && !st[0]) {
       st[2] = j + 1;
       double rp, kp;
       rel_kappa(hist + 4 * j, rp, kp);
       const bool far_j = ctrl[8 * j + 1] == 0;
-      if (!isfinite(r) || r > 1.5 * rp) {
-        st[0] = 1;  // diverged: stop, restore the warm-start basis at the end
-        st[1] = 1;
+      if (!ortho) st[7] |= 4;
+      if (!isfinite(r)) {
+        give_up(false);  // the basis itself is broken: back to the warm start
+      } else if (r > 1.5 * rp || !ortho) {
+        if ((st[7] >> 8) < prm.recover) {
+          st[7] = (st[7] | 1) + (1 << 8);
+          force = true;
+          st[3] = far_j ? 1 : 0;
+        } else {
+          give_up(true);
+        }
       } else {
         // an undamped far iteration close to the tolerance that barely helped: pairs in a
         // cluster denser than the global threshold assumes — local threshold from now on
@@ -191,36 +249,55 @@ __global__ void __launch_bounds__(256) sbr_dev_ctrl_kernel(const double* __restr
         st[3] = far_j ? 1 : 0;
       }
     }
-    if (!st[0] && r <= prm.tol) {
+    if (!st[0] && r <= prm.tol && ortho) {
       st[0] = 1;
       st[6] = 1;
     }
     const int nx = j + 1;
     if (nx < K) {
       int* c = ctrl + 8 * nx;
+      const bool lean = nx >= prm.lean_from;
+      if (!st[0]) {
+        // step size of the iteration just run (1 at the start); a lean slot's step is bounded
+        // to a negligible Taylor remainder (sbr_dev_prep), so its α < 1 asks for no Newton–Schulz
+        const float a_prev = (nx - 1 >= prm.lean_from) ? 1.f : alpha[nx];
+        // after a divergence every further far step is damped and re-orthonormalised (sticky):
+        // in the clustered spectra that diverge, an undamped step right after the recovery
+        // diverges again (profiles/r5_eigh_recover.txt)
+        const bool sticky = (st[7] & 1) != 0;
+        const bool ns = force || sticky || nx < prm.ns_iters || a_prev < 1.f || k > prm.ns_kappa;
+        const bool damp = force || sticky || nx == 0 || k > prm.damp_kappa;
+
+        const bool far = force || !(nx > 0 && r <= prm.near_only * prm.tol && st[3]);
+        const bool six = !(k < prm.t4_kappa);
+        // (a lean slot still takes an order-4 step where the rules would pick order 6: the
+        // truncation is O(‖X‖⁵/120) and stays orthogonal to that order; damping and
+        // Newton–Schulz are the safety steps it cannot skip)
+        if (lean && far && prm.lean_guard && (ns || damp)) {
+          // the lean slot has no damping / Newton–Schulz / order-6 kernels: taking its plain
+          // order-4 step here is unguarded — stop, capped (the host escalates the schedule)
+          st[7] |= 2;
+          give_up(true);
+        } else {
+          c[0] = 0;
+          c[1] = far ? 0 : 1;
+          // 0: damp (κ rule), 2: the generator's free bounds decide (xgate), 1: no damping
+          c[2] = (far && !lean) ? (damp ? 0 : (prm.xgate ? 2 : 1)) : 1;
+          c[3] = (far && six && !lean) ? 0 : 1;
+          c[4] = (six && !lean) ? 1 : 0;
+          c[5] = (far && ns && !lean) ? 0 : 1;
+          c[6] = (ns && !lean) ? 1 : 0;
+          c[7] = far ? 1 : 0;
+          // local far threshold: sticky after a stalled far iteration, or (theta0) once the far
+          // step is small (κ ≤ theta_kappa: with larger steps the extra strongly coupled far pairs
+          // rotated at once can make a cold-start iteration diverge)
+          const bool th = st[4] || (prm.theta0 > 0.f && k <= prm.theta_kappa);
+          theta[nx] = th ? (prm.theta0 > 0.f ? prm.theta0 : 1.f) : 0.f;
+          alpha[nx + 1] = 1.f;  // the damping kernel of iteration nx overwrites it when it runs
+        }
+      }
       if (st[0]) {
         c[0] = 1; c[1] = 1; c[2] = 1; c[3] = 1; c[4] = 0; c[5] = 1; c[6] = 0; c[7] = 1;
-      } else {
-        const float a_prev = alpha[nx];  // step size of the iteration just run (1 at the start)
-        const bool lean = nx >= prm.lean_from;
-        const bool ns = !lean && (nx < prm.ns_iters || a_prev < 1.f || k > prm.ns_kappa);
-        const bool damp = !lean && (nx == 0 || k > prm.damp_kappa);
-        const bool far = !(nx > 0 && r <= prm.near_only * prm.tol && st[3]);
-        const bool six = !lean && !(k < prm.t4_kappa);
-        c[0] = 0;
-        c[1] = far ? 0 : 1;
-        c[2] = (far && damp) ? 0 : 1;
-        c[3] = (far && six) ? 0 : 1;
-        c[4] = six ? 1 : 0;
-        c[5] = (far && ns) ? 0 : 1;
-        c[6] = ns ? 1 : 0;
-        c[7] = far ? 1 : 0;
-        // local far threshold: sticky after a stalled far iteration, or (theta0) once the far
-        // step is small (κ ≤ theta_kappa: with larger steps the extra strongly coupled far pairs
-        // rotated at once can make a cold-start iteration diverge)
-        const bool th = st[4] || (prm.theta0 > 0.f && k <= prm.theta_kappa);
-        theta[nx] = th ? (prm.theta0 > 0.f ? prm.theta0 : 1.f) : 0.f;
-        alpha[nx + 1] = 1.f;  // the damping kernel of iteration nx overwrites it when it runs
       }
     }
     if (nx == K) {
@@ -228,7 +305,8 @@ __global__ void __launch_bounds__(256) sbr_dev_ctrl_kernel(const double* __restr
       double rf, kf;
       rel_kappa(fb ? hist : hist + 4 * K, rf, kf);
       eig_stats[0] = rf;
-      eig_stats[1] = 0.0;
+      const bool conv = st[6] != 0 && rf <= prm.tol;
+      eig_stats[1] = (double)((conv ? 0 : 1) | ((st[7] & 1) ? 2 : 0) | ((st[7] & 2) ? 4 : 0) | ((st[7] & 4) ? 8 : 0));
       eig_stats[2] = (double)st[2];
       eig_stats[3] = fb ? 1.0 : 0.0;
       st[5] = fb ? 0 : 1;  // keep: the restore copy is skipped unless the refinement diverged
@@ -251,16 +329,37 @@ __global__ void __launch_bounds__(256) sbr_dev_ctrl_kernel(const double* __restr
   }
 }
 
+// the solve's stats → slot (seq mod R) of a host-mapped pinned ring [R][5] ([off_rel, status,
+// iterations, fallback, seq]), then seq + 1: the host reads the slot of the solve it needs
+// after that step's event completed (CMAES.graph_variant: a fixed lag, so the schedule choice
+// is deterministic).  One thread, vector stores.
+__global__ void sbr_report_kernel(const double* __restrict__ stats, int* __restrict__ seq, double* ring, int R) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const int q = *seq;
+  double* o = ring + 5 * (int64_t)(q % R);
+  o[0] = stats[0];
+  o[1] = stats[1];
+  o[2] = stats[2];
+  o[3] = stats[3];
+  o[4] = (double)q;
+  __threadfence_system();
+  *seq = q + 1;
+}
+
 }  // namespace
 
+void evx_sbr_report(const double* stats, int* seq, double* ring, int R, hipStream_t s) {
+  sbr_report_kernel<<<1, 64, 0, s>>>(stats, seq, ring, R);
+}
+
 void evx_sbr_dev_prep(const float* X, const float* X2, const float* X3, int n, float* alpha, float* P, float* MT, const int* ctrl,
-                      hipStream_t s, const float* V2, const float* V3, float tau) {
+                      hipStream_t s, const float* V2, const float* V3, float tau, const double* xpart, int nparts) {
   // a grid-stride loop over 256 workgroups: the schedule skips this kernel in most
   // iterations, and an empty launch costs in proportion to its workgroup count
   const int64_t total = (int64_t)n * n;
   int g = (int)((total + 255) / 256);
   if (g > 256) g = 256;
-  sbr_dev_prep_kernel<<<g, 256, 0, s>>>(X, X2, X3, n, alpha, P, MT, ctrl, V2, V3, tau);
+  sbr_dev_prep_kernel<<<g, 256, 0, s>>>(X, X2, X3, n, alpha, P, MT, ctrl, V2, V3, tau, xpart, nparts);
 }
 
 void evx_sbr_dev_copy(const float* src, float* dst, int64_t n, const int* skip, hipStream_t s) {
@@ -272,8 +371,8 @@ void evx_sbr_dev_copy(const float* src, float* dst, int64_t n, const int* skip, 
 
 void evx_sbr_dev_ctrl(const double* part, int nparts, int j, int K, double* hist, float* alpha, float* theta, int* ctrl, int* st,
                       const float* prm6, int ns_iters, const float* A, int64_t lda, int n, float* w_out, double* eig_stats, float* w_init,
-                      double* log, int log_len, int* log_count, hipStream_t s, int lean_from) {
-  SbrDevParams p{prm6[0], prm6[1], prm6[2], prm6[3], prm6[4], prm6[5], prm6[6], ns_iters, lean_from};
+                      double* log, int log_len, int* log_count, hipStream_t s, int lean_from, int recover, int lean_guard, int xgate) {
+  SbrDevParams p{prm6[0], prm6[1], prm6[2], prm6[3], prm6[4], prm6[5], prm6[6], ns_iters, lean_from, recover, lean_guard, xgate};
   sbr_dev_ctrl_kernel<<<1, 256, 0, s>>>(part, nparts, j, K, hist, alpha, theta, ctrl, st, p, A, lda, n, w_out, eig_stats, w_init, log,
                                         log_len, log_count);
 }

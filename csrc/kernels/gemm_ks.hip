@@ -597,12 +597,13 @@ __global__ void __launch_bounds__(64 * NW) gemm_ks_kernel(EvxGemmKs p) {
         }
       }
       out[v] = t;
-      if (MODE == 1 && p.stat_part && gr < p.M) {
+      if (MODE == 1 && p.stat_part && gr < p.M && (!p.stat_diag_only || tm == tn)) {
         const float vv[4] = {t.x, t.y, t.z, t.w};
 #pragma unroll
         for (int e2 = 0; e2 < 4; ++e2) {
           const int cc = c + e2;
           if (gc + e2 >= p.N) continue;
+          if (p.stat_diag_only && row != cc) continue;
           const double d2 = (double)vv[e2] * vv[e2];
           if (tm != tn || row < cc) st_off += 2.0 * d2;
           else if (row == cc) {

@@ -123,17 +123,99 @@ class CMAES(Algorithm):
         schedule (``sbr_cold_iters`` refinement slots): the warm start is C ≈ I there, the
         damped steps need ≈10–12 iterations, and later generations converge in 4–7 within the
         default 8-slot schedule (profiles/r4_sbr_threshold_variants.txt).  The generation
-        index is host-known, so the choice costs no device read."""
+        index is host-known, so the choice costs no device read.
+
+        Escalation (round 5): each solve writes its ``eig_stats`` into a host-mapped pinned ring
+        inside the generation (one single-thread kernel of its graph) and an event is recorded
+        after the step (:meth:`after_step`).  Choosing the schedule of a step reads the solve of
+        the step ``ESC_LAG`` = 2 back — waiting for that step's event, which never idles the
+        GPU while the step after it is queued (no ``.item()``, no device synchronize) — and,
+        when that solve reports itself capped (not converged) or fell back to the warm-start
+        basis, replays the next longer schedule (late → 8-slot → cold) for
+        ``sbr_escalate_gens`` generations.  The fixed lag keeps the choice, and so the run,
+        deterministic."""
         if not self._device_eigh():
             return None
+        self._poll_eig_health(generation)
         if generation < int(config.get("sbr_cold_gens")):
-            return "cold"
-        late = int(config.get("sbr_late_gens"))
-        if late > 0 and generation >= late:
+            base = "cold"
+        else:
+            late = int(config.get("sbr_late_gens"))
             # settled runs converge in ≤ 5 iterations: a shorter schedule drops the launch
             # boundaries of the always-skipped tail slots
-            return "late"
-        return None
+            base = "late" if late > 0 and generation >= late else None
+        esc = self.__dict__.get("_esc")
+        if esc is not None and generation < esc[0]:
+            order = ["late", None, "cold"]
+            return order[min(order.index(base) + esc[1], 2)]
+        return base
+
+    def graph_variant_set(self):
+        if not self._device_eigh():
+            return ()
+        return ("cold", None, "late") if int(config.get("sbr_late_gens")) > 0 else ("cold", None)
+
+    # fixed lag (in steps) at which the schedule choice reads a solve's health: the step two
+    # back has completed whenever one step is still queued, so the wait below never idles the
+    # GPU, and the same solves decide the same schedules in every run (deterministic)
+    ESC_LAG = 2
+    ESC_RING = 16
+
+    def after_step(self, generation: int) -> None:
+        if self.__dict__.get("_eig_ring") is None or not torch.cuda.is_available():
+            return
+        from collections import deque
+
+        pend = self.__dict__.setdefault("_eig_pending", deque())
+        ev = torch.cuda.Event()
+        ev.record()
+        k = self.__dict__.get("_eig_enqueued", 0)
+        pend.append((k, ev))
+        self._eig_enqueued = k + 1
+        while len(pend) > self.ESC_RING // 2:
+            pend.popleft()
+
+    def _stats_to_host(self, eig_stats: torch.Tensor) -> None:
+        """This solve's [off_rel, status, iterations, fallback] into a host-mapped pinned ring,
+        slot (solve index mod R), by one single-thread kernel (captured into the graph)."""
+        from ....core import in_capture_warmup
+
+        if not eig_stats.is_cuda:
+            return
+        if self.__dict__.get("_eig_ring") is None:
+            # allocated by the eager step or the capture's warm-up, never inside a capture
+            # (no host allocation while capturing; a counter zeroed inside the graph would be
+            # reset by every replay)
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("CMAES: the eigensolver report ring must exist before a graph capture")
+            self._eig_ring = torch.full((self.ESC_RING, 5), -1.0, dtype=torch.float64).pin_memory()
+            self._eig_seq = torch.zeros(1, dtype=torch.int32, device=eig_stats.device)
+        if in_capture_warmup():
+            return
+        from ....ops import _ext
+
+        _ext.ops().sbr_report(eig_stats, self._eig_seq, self._eig_ring)
+
+    def _poll_eig_health(self, generation: int) -> None:
+        n = self.__dict__.get("_eig_enqueued", 0)
+        target = n - self.ESC_LAG
+        if target < 0 or target <= self.__dict__.get("_eig_checked", -1):
+            return
+        self._eig_checked = target
+        pend = self.__dict__.get("_eig_pending")
+        while pend and pend[0][0] < target:
+            pend.popleft()
+        if not pend or pend[0][0] != target:
+            return
+        pend[0][1].synchronize()  # the step two back: the GPU still holds the one after it
+        row = self._eig_ring[target % self.ESC_RING].tolist()
+        if int(row[4]) != target:
+            return
+        if (int(row[1]) & 1) or row[3]:
+            esc = self.__dict__.get("_esc")
+            level = 1 if esc is None or generation >= esc[0] else min(esc[1] + 1, 2)
+            self._esc = (generation + int(config.get("sbr_escalate_gens")), level)
+            self._esc_count = self.__dict__.get("_esc_count", 0) + 1
 
     def graph_variant_context(self, variant):
         if variant == "cold":
@@ -274,6 +356,8 @@ class CMAES(Algorithm):
                     w, Bn, eig_stats = host_phase(sbr_phase, Cp[:d, :d], state.B, self.__dict__.setdefault("_eig_plans", {}),
                                                   out_like=(state.D, state.B, state.eig_stats))
             B, D, BdivD = ops.cma_eig_out(Bn.contiguous(), w.contiguous(), d, b_out)
+            if config.get("sbr_mode") == "device" and d % 4 == 0 and d <= 8192:
+                self._stats_to_host(eig_stats)
         else:
             np_ = jacobi.padded_size(d)
             C, Cp, Bp = ops.cma_cov_pad(state.C.contiguous(), S.contiguous(), pc, a, float(self.c1), float(self.cmu), state.B.contiguous(), np_,

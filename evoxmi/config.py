@@ -58,6 +58,11 @@ KNOBS: Dict[str, Knob] = {
     "sbr_theta_kappa": Knob("EVOXMI_SBR_THETA_KAPPA", 0.05, float, "sbr: κ below which the local far threshold θ applies (larger far steps with it diverged in cold-start solves)"),
     "sbr_thr_fac": Knob("EVOXMI_SBR_THR_FAC", 0.3, float, "sbr: global far-pair threshold factor (gap > thr_fac·(block/2)·spread/n)"),
     "cma_fused": Knob("EVOXMI_CMA_FUSED", 1, int, "CMA-ES tell epilogue as the fused cmaes.hip kernels (0: reference-shaped torch ops)"),
+    "sbr_recover": Knob("EVOXMI_SBR_RECOVER", 2, int, "device eigensolver: divergences (off-norm up > 1.5× in one iteration) answered by a forced damped + re-orthonormalised step from the current basis before the solve gives up and keeps the better of the current and the warm-start basis (0: give up at the first, the round-4 behaviour)"),
+    "sbr_lean_guard": Knob("EVOXMI_SBR_LEAN_GUARD", 1, int, "device eigensolver: a lean slot (no damping / Newton–Schulz / order-6 kernels) whose step the full rules would damp, re-orthonormalise or take to order 6 stops the solve as capped instead of taking an unguarded order-4 step (the host then escalates the schedule)"),
+    "sbr_escalate_gens": Knob("EVOXMI_SBR_ESCALATE_GENS", 8, int, "CMA-ES device eigensolver: after a solve reports itself capped or fell back (seen by the host one generation late through a pinned copy + event query), this many generations replay the next longer schedule (late → 8-slot → cold)"),
+    "sbr_lean_max_n": Knob("EVOXMI_SBR_LEAN_MAX_N", 1024, int, "device eigensolver: lean tail slots only for matrices up to this order (larger ones keep the damping / Newton–Schulz kernels in every slot)"),
+    "sbr_xgate": Knob("EVOXMI_SBR_XGATE", 2, int, "device eigensolver: the damping's power iteration also follows free bounds of the generator (the X² GEMM's diagonal stats): skipped when ‖X‖₂ ≤ τ is proven, run when a row of X is longer than τ/2 whatever κ says — 1 in every schedule, 2 in the cold-start schedule only (where an undamped step on a large generator diverged the d = 2000 cold start; in settled solves it costs ≈3 % of a generation), 0 off"),
     "sbr_fused_damping": Knob("EVOXMI_SBR_FUSED_DAMPING", 0, int, "device-controlled eigensolver: the step-size damping (3 power steps + final) as one grid-barrier launch (1) or four launches (0, default: the grid barriers' agent-scope fences cost more than the three launch boundaries they remove — 1.939 vs 1.888 ms/gen, profiles/NOTES.md)"),
     "cec_stack": Knob("EVOXMI_CEC_STACK", 1, int, "CEC'22 compositions (F9–F12) on the device: every rotated component from ONE GEMM over the stacked rotations with per-block exact shifts (1) or one GEMM per component (0)"),
     "cec_fused": Knob("EVOXMI_CEC_FUSED", 0, int, "CEC'22 F1 / F4 on the device: 1 = row terms from the rotation GEMM's epilogue (rotated population never written), 0 = GEMM + basic-function kernel (default: the fused epilogue measured 7 µs slower at pop 10 000 × d 1000, profiles/r3_cec_fused_epilogue.txt)"),

@@ -42,6 +42,16 @@ class Algorithm(Stateful):
         """Context manager active while a step of ``variant`` is captured or run eagerly."""
         return contextlib.nullcontext()
 
+    def graph_variant_set(self) -> Tuple[Hashable, ...]:
+        """Every variant :meth:`graph_variant` may return, including ones chosen only on a
+        run-time condition (``StdWorkflow.prepare_graphs`` captures them all up front)."""
+        return ()
+
+    def after_step(self, generation: int) -> None:
+        """Called by the workflow once the step that produced ``generation`` is enqueued (host
+        side, no device read): e.g. to record an event whose completion a later
+        :meth:`graph_variant` call polls."""
+
 
 def algorithm_has_init_ask(algorithm: Algorithm, state: State = None) -> bool:
     """True when ``algorithm`` overrides ``init_ask`` (reference ``utils/common.py:15-19``).

@@ -155,7 +155,7 @@ def mm(A: torch.Tensor, B: torch.Tensor, *, ta: bool = False, tb: bool = False, 
        Cin: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
        skip: Optional[torch.Tensor] = None, a_sub_k: Optional[torch.Tensor] = None, sel: Optional[torch.Tensor] = None,
        A2: Optional[torch.Tensor] = None, alpha2: Optional[float] = None, C2: Optional[torch.Tensor] = None,
-       stat_part: Optional[torch.Tensor] = None) -> torch.Tensor:
+       stat_part: Optional[torch.Tensor] = None, stat_diag_only: bool = False) -> torch.Tensor:
     """``alpha·(*alpha_ptr)·op(A)·op(B) (+ bias_n) (+ beta·Cin)`` with ``op(X) = Xᵀ`` when
     ``ta`` / ``tb`` (transposes are layouts, never copies).  ``mode`` 1 / 2: the result is
     symmetric / skew-symmetric by construction of the caller (Bᵀ C B, X·X for skew X, …);
@@ -166,7 +166,8 @@ def mm(A: torch.Tensor, B: torch.Tensor, *, ta: bool = False, tb: bool = False, 
     ``A2`` / ``alpha2`` / ``C2`` (when given; ``alpha2`` defaults to ``alpha``) instead of
     ``A`` / ``alpha`` / ``out``.
     ``stat_part`` (mode 1): float64 partials of [Σ offdiag², Σ diag², min diag, max diag] per
-    workgroup (``sbr_stats_final`` layout; length ``4·gemm_ks_grid``).
+    workgroup (``sbr_stats_final`` layout; length ``4·gemm_ks_grid``); ``stat_diag_only``: the
+    diagonal's terms only (Σ offdiag² left 0 — the cheaper epilogue of the eigensolver's X²).
 
     On a GPU this is always the framework kernel (no vendor GEMM); shapes the kernel does
     not take (K % 4 ≠ 0 with a K-contiguous operand) go to :func:`gemm`."""
@@ -185,7 +186,7 @@ def mm(A: torch.Tensor, B: torch.Tensor, *, ta: bool = False, tb: bool = False, 
                     float(beta), Cin)
             if out is not None:
                 a2 = float(alpha if alpha2 is None else alpha2)
-                _ext.ops().gemm_ks_out(*args, out, skip, a_sub_k, sel, A2, a2, C2, stat_part)
+                _ext.ops().gemm_ks_out(*args, out, skip, a_sub_k, sel, A2, a2, C2, stat_part, int(stat_diag_only))
                 return out
             if sel is not None or stat_part is not None:
                 raise ValueError("mm: sel / stat_part need out=")

@@ -46,7 +46,7 @@ def config_fused_damping() -> bool:
 class DeviceSBR:
     """Persistent buffers + the fixed iteration schedule for one (n, device, config)."""
 
-    def __init__(self, n: int, device, cfg: SBRConfig, iters: int, lean_from: int = None):
+    def __init__(self, n: int, device, cfg: SBRConfig, iters: int, lean_from: int = None, xgate: bool = None):
         if cfg.block not in (16, 32):
             raise ValueError("the device schedule uses the shifted-layout blocks (16 / 32)")
         self.n, self.cfg, self.K = n, cfg, int(iters)
@@ -76,6 +76,9 @@ class DeviceSBR:
         self.dq = torch.zeros(n, device=dev)
         self.nparts = int(ops.gemm_ks_grid(n, n, 1))
         self.part = torch.zeros(4 * self.nparts, dtype=torch.float64, device=dev)
+        # stats partials of X² = −X·Xᵀ: the free ‖X‖_F bound that gates every step size (sbr_dev_prep)
+        self.xgate = bool(config.get("sbr_xgate") == 1) if xgate is None else bool(xgate)
+        self.part2 = torch.zeros(4 * self.nparts, dtype=torch.float64, device=dev) if self.xgate else None
         K = self.K
         self.hist = torch.zeros(4 * (K + 1), dtype=torch.float64, device=dev)
         self.alpha = torch.ones(K + 1, device=dev)
@@ -93,7 +96,8 @@ class DeviceSBR:
         self.log = torch.zeros(LOG_LEN, 4, dtype=torch.float64, device=dev)
         self.log_count = torch.zeros(1, dtype=torch.int32, device=dev)
         self.prm = [float(cfg.tol), float(cfg.ns_kappa), float(cfg.damp_kappa), float(cfg.t4_kappa), float(cfg.near_only),
-                    float(cfg.theta0), float(cfg.theta_kappa), float(self.lean_from)]
+                    float(cfg.theta0), float(cfg.theta_kappa), float(self.lean_from), float(config.get("sbr_recover")),
+                    float(config.get("sbr_lean_guard")), float(self.xgate)]
 
     # ------------------------------------------------------------------ pieces
     def _btcb(self, C, skip):
@@ -129,17 +133,18 @@ class DeviceSBR:
             ops.sbr16_far_bq_out(self.A, self.perm, self.Q, self.dq, self.hist[4 * j : 4 * j + 4], float(cfg.thr_fac),
                                  self.theta[j : j + 1], self.X, self.B, self.Bq, sb, sk_far, sk_all)
         # X skew ⇒ X² = −X·Xᵀ, symmetric (upper tiles only)
-        mm(self.X, self.X, tb=True, mode=1, alpha=-1.0, out=self.X2, skip=sk_far)
+        mm(self.X, self.X, tb=True, mode=1, alpha=-1.0, out=self.X2, skip=sk_far, stat_part=self.part2, stat_diag_only=True)
         if cfg.damp_tau > 0 and full:
-            # three power-step launches; α itself is formed by the prep kernel below (no_final)
+            # three power-step launches (they return at once when the free Frobenius bound already
+            # gives α = 1); α itself is formed by the prep kernel below (no_final)
             ops.sbr_damping_out(self.X2, self.V, float(cfg.damp_tau), self.alpha[j + 1 : j + 2], self.work, sk_damp, self.bar,
-                                self.bar is None)
+                                self.bar is None, self.part2 if self.bar is None else None)
         if full:
             # order 6 only: X³ = X²·X = −X²·Xᵀ (skew)
             mm(self.X2, self.X, tb=True, mode=2, alpha=-1.0, out=self.X3, skip=sk_x3)
         damp_here = cfg.damp_tau > 0 and full and self.bar is None
         ops.sbr_dev_prep(self.X, self.X2, self.X3, self.alpha[j + 1 : j + 2], self.P, self.VT, c, self.work if damp_here else None,
-                         float(cfg.damp_tau))
+                         float(cfg.damp_tau), self.part2)
         # Vᵀ = M(−α) + X²·Pᵀ (order 4) or M(−α) − X³·Pᵀ (order 6): the control word selects
         mm(self.X2, self.P, tb=True, alpha=1.0, beta=1.0, Cin=self.VT, out=self.VT, skip=sk_far, sel=sel6, A2=self.X3, alpha2=-1.0)
         # B·V → B, or into T when Newton–Schulz follows
@@ -183,14 +188,15 @@ class DeviceSBR:
 _WS = {}
 
 
-def workspace(n: int, device, cfg: SBRConfig, iters: int, lean_from: int = None) -> DeviceSBR:
+def workspace(n: int, device, cfg: SBRConfig, iters: int, lean_from: int = None, xgate: bool = False) -> DeviceSBR:
     from .. import config
 
     key = (n, str(device), cfg.block, cfg.block_sweeps, cfg.thr_fac, cfg.ns_iters, cfg.damp_tau, cfg.tol, cfg.ns_kappa,
            cfg.damp_kappa, cfg.t4_kappa, cfg.near_only, cfg.theta0, cfg.theta_kappa, int(iters), lean_from,
-           bool(config.get("sbr_prepermute")), float(config.get("sbr_sweep_tol")))
+           bool(config.get("sbr_prepermute")), float(config.get("sbr_sweep_tol")), int(config.get("sbr_recover")),
+           int(config.get("sbr_lean_guard")), bool(xgate))
     if key not in _WS:
-        _WS[key] = DeviceSBR(n, device, cfg, iters, lean_from)
+        _WS[key] = DeviceSBR(n, device, cfg, iters, lean_from, xgate)
     return _WS[key]
 
 
@@ -209,9 +215,18 @@ def eigh_device(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None, it
         # lean tail slots only in a schedule that does not start cold (CMA-ES's cold-start
         # variant passes a longer schedule with every slot full)
         lean = config.get("sbr_full_slots") if iters < config.get("sbr_cold_iters") else None
+        # larger matrices stay above the damping / Newton–Schulz thresholds for more iterations
+        # (d = 2000: the lean-slot guard capped warm solves at slot 5): every slot full there
+        if C.shape[0] > int(config.get("sbr_lean_max_n")):
+            lean = None
     else:
         lean = None
-    return workspace(C.shape[0], C.device, cfg, iters, lean).solve(C, B_prev)
+    # the bounds-gated damping: everywhere (1) or in the cold-start schedule only (2): the
+    # large generators of a cold start are where an undamped step diverged (d = 2000), and in
+    # settled solves the extra power iterations cost ≈3 % of a generation (profiles/r5_eigh_recover.txt)
+    xg = int(config.get("sbr_xgate"))
+    xgate = xg == 1 or (xg == 2 and iters >= config.get("sbr_cold_iters"))
+    return workspace(C.shape[0], C.device, cfg, iters, lean, xgate).solve(C, B_prev)
 
 
 def all_histories():

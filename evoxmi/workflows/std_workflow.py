@@ -365,6 +365,10 @@ class StdWorkflow(Workflow):
             v = gv(g0 + k) if gv is not None else None
             if v not in variants:
                 variants.append(v)
+        vs = getattr(self.algorithm, "graph_variant_set", None)
+        for v in (vs() if vs is not None else ()):
+            if v not in variants:
+                variants.append(v)
         for v in variants:
             if v not in self._graphs:
                 self._capture(state, v)
@@ -391,6 +395,9 @@ class StdWorkflow(Workflow):
                 state = self._step_graph(state)
         else:
             state = self._step_eager(state)
+        hook = getattr(self.algorithm, "after_step", None)
+        if hook is not None:
+            hook(int(state.generation))
         for m in self.registered_hooks["post_step"]:
             m.post_step(state)
         k = config.get("check_replicas_every")

@@ -135,3 +135,113 @@ def test_cmaes_default_schedule_converges_every_generation_from_cold_start():
     assert float(h[:, 3].sum()) == 0.0
     assert set(wf._graphs) == ({"cold", None, "late"} if 0 < config.get("sbr_late_gens") < 200 else {"cold", None})
     assert int(h[:, 2].max()) <= max(config.get("sbr_device_iters"), config.get("sbr_cold_iters"))
+
+
+def _long_run(func: int, d: int, pop: int, gens: int, seed: int = 2024, init_stdev: float = 20.0):
+    """(histories, workflow, algorithm) of a graph-captured CMA-ES run of ``gens`` generations
+    from a cold start (C = I) with the default device schedule."""
+    from evoxmi import random as rnd
+    from evoxmi.algorithms import CMAES
+    from evoxmi.problems.numerical import CEC2022TestSuit
+    from evoxmi.workflows import StdWorkflow
+
+    center = (torch.rand(d, generator=torch.Generator().manual_seed(1)) * 160 - 80).cuda()
+    algo = CMAES(center_init=center, init_stdev=init_stdev, pop_size=pop)
+    wf = StdWorkflow(algo, CEC2022TestSuit.create(func), graph=True)
+    st = wf.init(rnd.PRNGKey(seed, device=torch.device("cuda")))
+    snap = sbr_device.snapshot_counts()
+    st = wf.step(st)
+    st = wf.prepare_graphs(st, gens - 1)
+    for _ in range(gens - 1):
+        st = wf.step(st)
+    torch.cuda.synchronize()
+    return sbr_device.histories_since(snap), wf, algo
+
+
+@pytest.mark.parametrize("func,d", [(4, 1000), (6, 1000), (12, 1000), (1, 200), (1, 2000)])
+def test_cmaes_default_schedule_converges_on_other_functions_and_dims(func, d):
+    """200 generations from a cold start with the default schedule on CEC'22 F4 / F6 / F12 at
+    d = 1000 and F1 at d = 200 / 2000 (λ = 4 + ⌊3 ln d⌋·… is replaced by the flagship's
+    λ = 10 000): every solve within tolerance, none capped, none fallen back — the schedule is
+    not tuned to the one F1 d = 1000 trajectory."""
+    from evoxmi import config
+
+    # F1 at d = 200: the run itself leaves f32 after ≈135 generations (σ grows while the
+    # smallest axis of C shrinks below 1e-7 of the largest on the quartic Zakharov term, then C
+    # turns NaN; profiles/r5_eigh_recover.txt) — its test stops at 120
+    gens = 120 if (func, d) == (1, 200) else 200
+    h, _, algo = _long_run(func, d, 10000, gens)
+    assert h.shape[0] >= gens - 1
+    tol = config.get("eigh_tol")
+    bad = h[(h[:, 0] > tol) | (h[:, 3] != 0)]
+    assert bad.shape[0] == 0, bad
+    assert int((h[:, 1].long() & 1).sum()) == 0  # no capped solve
+    assert algo.__dict__.get("_esc_count", 0) == 0
+
+
+def test_sim8_trajectory_recovers_from_divergence():
+    """bench.py --simulate-rank 0 --world 8 (rank 0's rows tiled ×8: a covariance with a
+    massively degenerate spectrum) diverged in round 4 — the cold-start solves of generations
+    0-2 and the warm solve of generation 12 fell back to the warm-start basis
+    (profiles/r5_eigh_recover.txt).  With the forced damped recovery none falls back and
+    generations 0-13 all converge."""
+    from evoxmi import config
+    from evoxmi import random as rnd
+    from evoxmi.algorithms import CMAES
+    from evoxmi.parallel.context import SimulatedDistContext
+    from evoxmi.problems.numerical import CEC2022TestSuit
+    from evoxmi.workflows import StdWorkflow
+
+    center = (torch.rand(1000, generator=torch.Generator().manual_seed(1)) * 160 - 80).cuda()
+    algo = CMAES(center_init=center, init_stdev=20.0, pop_size=10000)
+    wf = StdWorkflow(algo, CEC2022TestSuit.create(1), graph=False)
+    st = wf.init(rnd.PRNGKey(2024, device=torch.device("cuda")))
+    st = wf.enable_distributed(st, context=SimulatedDistContext(0, 8, algorithm=algo))
+    snap = sbr_device.snapshot_counts()
+    for _ in range(14):
+        st = wf.step(st)
+    h = sbr_device.histories_since(snap)
+    assert h.shape[0] == 14
+    assert float(h[:, 3].sum()) == 0.0, h
+    assert float(h[:, 0].max()) <= config.get("eigh_tol"), h
+    assert int((h[:, 1].long() & 2).sum()) > 0  # the recovery path did run
+
+
+def test_capped_late_solves_escalate_the_schedule_without_device_syncs(monkeypatch):
+    """sbr_late_iters = 2 (3 full slots clipped to 2): the late schedule cannot converge, its
+    solves report themselves capped, and the host — reading each solve's health two steps
+    later from the pinned ring, never through .item() or a device synchronize — switches to
+    the 8-slot schedule within ESC_LAG generations of the first late generation."""
+    from evoxmi import config
+    from evoxmi import random as rnd
+    from evoxmi.algorithms import CMAES
+    from evoxmi.problems.numerical import CEC2022TestSuit
+    from evoxmi.workflows import StdWorkflow
+
+    with config.override(sbr_late_gens=12, sbr_late_iters=2, sbr_late_full_slots=2):
+        center = (torch.rand(1000, generator=torch.Generator().manual_seed(1)) * 160 - 80).cuda()
+        algo = CMAES(center_init=center, init_stdev=20.0, pop_size=10000)
+        wf = StdWorkflow(algo, CEC2022TestSuit.create(1), graph=True)
+        st = wf.init(rnd.PRNGKey(2024, device=torch.device("cuda")))
+        st = wf.step(st)
+        st = wf.prepare_graphs(st, 40)
+        assert set(wf._graphs) == {"cold", None, "late"}
+
+        def forbidden(*a, **k):
+            raise AssertionError("device sync on the step path")
+
+        variants = []
+        with monkeypatch.context() as m:
+            m.setattr(torch.cuda, "synchronize", forbidden)
+            m.setattr(torch.Tensor, "item", forbidden)
+            for _ in range(24):
+                variants.append(algo.graph_variant(int(st.generation)))
+                st = wf.step(st)
+        torch.cuda.synchronize()
+    late = [i + 1 for i, v in enumerate(variants) if v == "late"]
+    assert late, variants
+    first_late = late[0]
+    # generation first_late replays the late graph; its capped solve is read ESC_LAG steps on
+    esc = [g for g, v in enumerate(variants, start=1) if g > first_late and v is None]
+    assert esc and esc[0] <= first_late + CMAES.ESC_LAG + 1, variants
+    assert algo.__dict__.get("_esc_count", 0) >= 1
