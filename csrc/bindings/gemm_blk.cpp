@@ -104,30 +104,32 @@ at::Tensor gemm_blk(const at::Tensor& A, int64_t M, const at::Tensor& B, int64_t
   return C;
 }
 
-void check_h3(const at::Tensor& t, const at::Tensor& rinv, int64_t rows, int64_t K, const char* what) {
+void check_h3(const at::Tensor& t, const at::Tensor& rinv, int64_t rows, int64_t K, const char* what, int64_t ncomp = 1) {
   CHECK_DEV(t); CHECK_DEV(rinv);
-  TORCH_CHECK(t.scalar_type() == at::kShort && t.is_contiguous() && t.numel() >= evx_h3_elems(rows, (int)K) &&
+  TORCH_CHECK(ncomp >= 1, what, ": ncomp >= 1");
+  TORCH_CHECK(t.scalar_type() == at::kShort && t.is_contiguous() && t.numel() >= ncomp * evx_h3_elems(rows, (int)K) &&
                   reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
-              what, ": f16x3 planes int16[", evx_h3_elems(rows, (int)K), "] for ", rows, " x ", K);
-  TORCH_CHECK(rinv.scalar_type() == at::kFloat && rinv.is_contiguous() && rinv.numel() >= evx_blk_rows(rows), what,
-              ": row scales float32[", evx_blk_rows(rows), "]");
+              what, ": f16x3 planes int16[", ncomp, " x ", evx_h3_elems(rows, (int)K), "] for ", rows, " x ", K);
+  TORCH_CHECK(rinv.scalar_type() == at::kFloat && rinv.is_contiguous() && rinv.numel() >= ncomp * evx_blk_rows(rows), what,
+              ": row scales float32[", ncomp, " x ", evx_blk_rows(rows), "]");
 }
 
 std::vector<at::Tensor> h3_alloc(const at::Tensor& like, int64_t rows, int64_t K, const c10::optional<at::Tensor>& out,
-                                 const c10::optional<at::Tensor>& rinv_out, const char* what) {
+                                 const c10::optional<at::Tensor>& rinv_out, const char* what, int64_t ncomp = 1) {
   at::Tensor o, r;
   if (out.has_value() && out->defined()) {
     TORCH_CHECK(rinv_out.has_value() && rinv_out->defined(), what, ": out and rinv_out together");
     o = *out;
     r = *rinv_out;
-    check_h3(o, r, rows, K, what);
+    check_h3(o, r, rows, K, what, ncomp);
   } else {
-    o = at::empty({evx_h3_elems(rows, (int)K)}, like.options().dtype(at::kShort));
-    r = at::empty({evx_blk_rows(rows)}, like.options().dtype(at::kFloat));
+    o = at::empty({ncomp * evx_h3_elems(rows, (int)K)}, like.options().dtype(at::kShort));
+    r = at::empty({ncomp * evx_blk_rows(rows)}, like.options().dtype(at::kFloat));
   }
   return {o, r};
 }
 
+// sub_k: a K-vector, or an ncomp × K matrix (row c shifts plane set c: one read of X)
 std::vector<at::Tensor> h3_split(const at::Tensor& X, const c10::optional<at::Tensor>& sub_k, const c10::optional<at::Tensor>& colscale,
                                  const c10::optional<at::Tensor>& out, const c10::optional<at::Tensor>& rinv_out) {
   CHECK_DEV(X); CHECK_F32(X);
@@ -135,9 +137,20 @@ std::vector<at::Tensor> h3_split(const at::Tensor& X, const c10::optional<at::Te
   const int64_t rows = X.size(0), K = X.size(1);
   TORCH_CHECK(rows > 0 && K > 0, "h3_split: empty");
   c10::DeviceGuard g(X.device());
-  auto v = h3_alloc(X, rows, K, out, rinv_out, "h3_split");
-  evx_split_h3(X.data_ptr<float>(), X.stride(0), rows, (int)K, opt_vec(sub_k, K, "sub_k"), opt_vec(colscale, K, "colscale"),
-               reinterpret_cast<uint16_t*>(v[0].data_ptr<int16_t>()), v[1].data_ptr<float>(), cur_stream());
+  int64_t ncomp = 1, sub_ld = 0;
+  const float* sub = nullptr;
+  if (sub_k.has_value() && sub_k->defined() && sub_k->dim() == 2) {
+    CHECK_DEV(*sub_k); CHECK_F32(*sub_k);
+    TORCH_CHECK(sub_k->size(1) >= K && sub_k->stride(1) == 1 && sub_k->size(0) >= 1, "h3_split: sub_k ncomp x K, unit inner stride");
+    ncomp = sub_k->size(0);
+    sub_ld = sub_k->stride(0);
+    sub = sub_k->data_ptr<float>();
+  } else {
+    sub = opt_vec(sub_k, K, "sub_k");
+  }
+  auto v = h3_alloc(X, rows, K, out, rinv_out, "h3_split", ncomp);
+  evx_split_h3(X.data_ptr<float>(), X.stride(0), rows, (int)K, sub, opt_vec(colscale, K, "colscale"),
+               reinterpret_cast<uint16_t*>(v[0].data_ptr<int16_t>()), v[1].data_ptr<float>(), cur_stream(), (int)ncomp, sub_ld);
   return v;
 }
 
@@ -155,9 +168,13 @@ std::vector<at::Tensor> h3_philox_normal(const at::Tensor& key, int64_t rows, in
 
 at::Tensor gemm_h3(const at::Tensor& A, const at::Tensor& a_rinv, int64_t M, const at::Tensor& B, const at::Tensor& b_rinv, int64_t N,
                    int64_t K, double alpha, const c10::optional<at::Tensor>& alpha_ptr, const c10::optional<at::Tensor>& bias_n,
-                   const c10::optional<at::Tensor>& out, const c10::optional<at::Tensor>& skip) {
+                   const c10::optional<at::Tensor>& out, const c10::optional<at::Tensor>& skip, int64_t sub_cols) {
   TORCH_CHECK(M > 0 && N > 0 && K > 0, "gemm_h3: shape");
-  check_h3(A, a_rinv, M, K, "gemm_h3 A");
+  // stacked A (sub_cols > 0): one plane set per sub_cols-wide output column block
+  TORCH_CHECK(sub_cols >= 0 && sub_cols % evx_gemm_blk_tile_n() == 0, "gemm_h3: sub_cols a multiple of the tile width ",
+              evx_gemm_blk_tile_n());
+  const int64_t ncomp = sub_cols > 0 ? (N + sub_cols - 1) / sub_cols : 1;
+  check_h3(A, a_rinv, M, K, "gemm_h3 A", ncomp);
   check_h3(B, b_rinv, N, K, "gemm_h3 B");
   c10::DeviceGuard g(A.device());
   at::Tensor C;
@@ -183,6 +200,8 @@ at::Tensor gemm_h3(const at::Tensor& A, const at::Tensor& a_rinv, int64_t M, con
   a.alpha = (float)alpha;
   a.alpha_ptr = opt_vec(alpha_ptr, 1, "alpha_ptr");
   a.bias_n = opt_vec(bias_n, N, "bias_n");
+  a.sub_cols = (int)sub_cols;
+  a.a_comp_stride = evx_h3_elems(M, (int)K);
   if (skip.has_value() && skip->defined()) {
     CHECK_DEV(*skip);
     TORCH_CHECK(skip->scalar_type() == at::kInt, "gemm_h3: skip int32");
@@ -209,7 +228,7 @@ TORCH_LIBRARY_FRAGMENT(evoxmi, m) {
   m.def("h3_split(Tensor X, Tensor? sub_k=None, Tensor? colscale=None, Tensor(a!)? out=None, Tensor(b!)? rinv_out=None) -> Tensor[]");
   m.def("h3_philox_normal(Tensor key, int rows, int d, int row0=0, Tensor(a!)? out=None, Tensor(b!)? rinv_out=None) -> Tensor[]");
   m.def("gemm_h3(Tensor A, Tensor a_rinv, int M, Tensor B, Tensor b_rinv, int N, int K, float alpha=1., Tensor? alpha_ptr=None, "
-        "Tensor? bias_n=None, Tensor(a!)? out=None, Tensor? skip=None) -> Tensor");
+        "Tensor? bias_n=None, Tensor(a!)? out=None, Tensor? skip=None, int sub_cols=0) -> Tensor");
   m.def("h3_elems(int rows, int K) -> int");
   m.def("blk_rows(int rows) -> int");
   m.def("gemm_blk_tile(int which) -> int");

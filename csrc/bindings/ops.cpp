@@ -39,6 +39,16 @@ int64_t key_batch(const at::Tensor& key, const char* op) {
   return key.size(0);
 }
 
+at::Tensor philox_window(const at::Tensor& key, int64_t rows, int64_t dtot, int64_t col0, int64_t own, int64_t row0, int64_t dist) {
+  TORCH_CHECK(key.is_cuda() && key.scalar_type() == at::kLong && key.numel() == 2, "philox_window: one device key");
+  TORCH_CHECK(rows >= 0 && own >= 0 && col0 >= 0 && col0 + own <= dtot && row0 >= 0, "philox_window: window outside the matrix");
+  c10::DeviceGuard g(key.device());
+  auto out = at::empty({rows, own}, key.options().dtype(at::kFloat));
+  if (rows > 0 && own > 0)
+    evx_philox_window(out.data_ptr<float>(), key.contiguous().data_ptr<int64_t>(), rows, dtot, col0, own, row0, (int)dist, cur_stream());
+  return out;
+}
+
 at::Tensor philox_fill(const at::Tensor& key, int64_t n, int64_t dist, int64_t offset) {
   const int64_t B = key_batch(key, "philox_fill");
   TORCH_CHECK(offset % 4 == 0, "offset must be a multiple of 4");
@@ -644,6 +654,50 @@ at::Tensor cec_basic(const at::Tensor& Z, int64_t fid, const c10::optional<at::T
   if (Z.size(0) > 0)
     evx_cec_basic(Z.data_ptr<float>(), Z.stride(0), (int)Z.size(0), (int)fid, pp, (int)start, (int)L, optf(sub), (float)scale,
                   yp, ldy, (int)ystart, (int)yperm, out.data_ptr<float>(), cur_stream(), (float)clamp);
+  return out;
+}
+
+// composition functions in one pass (cec2022.hip: cec_compose_kernel); Z: the stacked rotation
+// GEMM output (parts with zcol < 0 read x − Os[comp] instead)
+at::Tensor cec_compose(const c10::optional<at::Tensor>& Z, const at::Tensor& X, const at::Tensor& Os, at::IntArrayRef fid,
+                       at::IntArrayRef zcol, at::IntArrayRef comp, at::ArrayRef<double> scale, at::ArrayRef<double> sigma,
+                       at::ArrayRef<double> lamb, at::ArrayRef<double> bias, double thr) {
+  CHECK_DEV(X); CHECK_F32(X); CHECK_DEV(Os); CHECK_F32(Os);
+  TORCH_CHECK(X.dim() == 2 && X.stride(1) == 1, "cec_compose: X 2-D row-major");
+  const int64_t N = X.size(0), D = X.size(1), n = (int64_t)fid.size();
+  TORCH_CHECK(n >= 1 && n <= kEvxCecMaxParts, "cec_compose: 1..", kEvxCecMaxParts, " parts");
+  TORCH_CHECK((int64_t)zcol.size() == n && (int64_t)comp.size() == n && (int64_t)scale.size() == n && (int64_t)sigma.size() == n &&
+                  (int64_t)lamb.size() == n && (int64_t)bias.size() == n,
+              "cec_compose: one entry per part");
+  TORCH_CHECK(Os.dim() == 2 && Os.stride(1) == 1 && Os.size(0) >= n && Os.size(1) >= D, "cec_compose: Os (>= parts) x D");
+  EvxCecCompose c{};
+  c.n = (int)n;
+  const float* zp = nullptr;
+  int64_t ldz = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    TORCH_CHECK(fid[i] != 2, "cec_compose: SCHAFFERF7 is a hybrid-only component");
+    TORCH_CHECK(comp[i] >= 0 && comp[i] < Os.size(0), "cec_compose: comp index");
+    c.fid[i] = (int)fid[i];
+    c.zcol[i] = (int)zcol[i];
+    c.comp[i] = (int)comp[i];
+    c.scale[i] = (float)scale[i];
+    c.sigma[i] = (float)sigma[i];
+    c.lamb[i] = (float)lamb[i];
+    c.bias[i] = (float)bias[i];
+    if (zcol[i] >= 0) {
+      TORCH_CHECK(Z.has_value() && Z->defined(), "cec_compose: rotated parts need Z");
+      CHECK_DEV(*Z); CHECK_F32(*Z);
+      TORCH_CHECK(Z->dim() == 2 && Z->stride(1) == 1 && Z->size(0) == N && zcol[i] + D <= Z->size(1), "cec_compose: Z block");
+      zp = Z->data_ptr<float>();
+      ldz = Z->stride(0);
+    }
+  }
+  c.os = Os.data_ptr<float>();
+  c.ldo = Os.stride(0);
+  c.thr = (float)thr;
+  c10::DeviceGuard g(X.device());
+  auto out = at::empty({N}, X.options());
+  evx_cec_compose(zp, ldz, X.data_ptr<float>(), X.stride(0), (int)N, (int)D, c, out.data_ptr<float>(), cur_stream());
   return out;
 }
 
@@ -1379,27 +1433,31 @@ at::Tensor nsga_select(const at::Tensor& rank, const at::Tensor& f, int64_t N, i
 }  // namespace
 
 // OpenES gradient with Philox-regenerated noise: g[j] = Σ_i w[i] ε(row0 + i, j)
-at::Tensor es_population(const at::Tensor& key, const at::Tensor& center, double sigma, int64_t rows, int64_t half, int64_t row0) {
+at::Tensor es_population(const at::Tensor& key, const at::Tensor& center, double sigma, int64_t rows, int64_t half, int64_t row0,
+                         int64_t col0, int64_t dtot) {
   CHECK_DEV(key); CHECK_DEV(center); CHECK_F32(center); CHECK_CONTIG(center);
   TORCH_CHECK(key.scalar_type() == at::kLong && key.numel() == 2 && key.is_contiguous(), "es_population: key int64[2]");
-  TORCH_CHECK(center.dim() == 1 && rows >= 0 && half >= 0 && row0 >= 0, "es_population: center (d,)");
+  TORCH_CHECK(center.dim() == 1 && rows >= 0 && half >= 0 && row0 >= 0 && col0 >= 0 && (dtot == 0 || col0 + center.size(0) <= dtot),
+              "es_population: center (d,), window [col0, col0 + d) inside dtot");
   c10::DeviceGuard g(center.device());
   const int64_t d = center.size(0);
   auto out = at::empty({rows, d}, center.options());
   if (rows > 0 && d > 0)
-    evx_es_population(key.data_ptr<int64_t>(), center.data_ptr<float>(), (float)sigma, rows, d, half, row0, out.data_ptr<float>(), cur_stream());
+    evx_es_population(key.data_ptr<int64_t>(), center.data_ptr<float>(), (float)sigma, rows, d, half, row0, out.data_ptr<float>(), cur_stream(),
+                      col0, dtot);
   return out;
 }
 
-at::Tensor es_noise_grad(const at::Tensor& key, const at::Tensor& w, int64_t d, int64_t row0) {
+at::Tensor es_noise_grad(const at::Tensor& key, const at::Tensor& w, int64_t d, int64_t row0, int64_t col0, int64_t dtot) {
   check_key(key);
   CHECK_DEV(w); CHECK_F32(w); CHECK_CONTIG(w);
-  TORCH_CHECK(w.dim() == 1 && d >= 1 && row0 >= 0, "es_noise_grad: w (rows,), d >= 1");
+  TORCH_CHECK(w.dim() == 1 && d >= 1 && row0 >= 0 && col0 >= 0 && (dtot == 0 || col0 + d <= dtot), "es_noise_grad: w (rows,), d >= 1, window");
   const int64_t rows = w.size(0);
   const int chunks = (int)std::max<int64_t>(1, std::min<int64_t>(64, rows / 64));
   c10::DeviceGuard g(w.device());
   auto partial = at::empty({chunks, d}, w.options());
-  if (rows > 0) evx_es_noise_grad(key.data_ptr<int64_t>(), w.data_ptr<float>(), rows, d, row0, chunks, partial.data_ptr<float>(), cur_stream());
+  if (rows > 0)
+    evx_es_noise_grad(key.data_ptr<int64_t>(), w.data_ptr<float>(), rows, d, row0, chunks, partial.data_ptr<float>(), cur_stream(), col0, dtot);
   else partial.zero_();
   return partial.sum(0);
 }
@@ -1443,17 +1501,20 @@ at::Tensor hv_contrib(const at::Tensor& S, const at::Tensor& P, const at::Tensor
 }
 
 TORCH_LIBRARY(evoxmi, m) {
-  m.def("es_noise_grad(Tensor key, Tensor w, int d, int row0) -> Tensor");
-  m.def("es_population(Tensor key, Tensor center, float sigma, int rows, int half, int row0) -> Tensor");
+  m.def("es_noise_grad(Tensor key, Tensor w, int d, int row0, int col0=0, int dtot=0) -> Tensor");
+  m.def("es_population(Tensor key, Tensor center, float sigma, int rows, int half, int row0, int col0=0, int dtot=0) -> Tensor");
   m.def("knn(Tensor X, Tensor Y, int T) -> Tensor[]");
   m.def("hv_count(Tensor S, Tensor P, int strict) -> Tensor");
   m.def("hv_contrib(Tensor S, Tensor P, Tensor count, Tensor alpha) -> Tensor");
   m.def("philox_fill(Tensor key, int n, int dist, int offset) -> Tensor");
+  m.def("philox_window(Tensor key, int rows, int dtot, int col0, int own, int row0, int dist) -> Tensor");
   m.def("argsort_f32(Tensor keys, int descending) -> Tensor[]");
   m.def("radix_argsort_f32(Tensor keys, int descending) -> Tensor[]");
   m.def("rank_argsort_f32(Tensor keys, int descending) -> Tensor[]");
   m.def("merge_argsort_f32(Tensor keys, int descending) -> Tensor[]");
   m.def("cec_basic(Tensor Z, int fid, Tensor? perm, int start, int L, Tensor? sub, float scale, Tensor? Y, int ystart, int yperm, float clamp=0.0) -> Tensor");
+  m.def("cec_compose(Tensor? Z, Tensor X, Tensor Os, int[] fid, int[] zcol, int[] comp, float[] scale, float[] sigma, float[] lamb, "
+        "float[] bias, float thr) -> Tensor");
   m.def("jacobi_sweeps(Tensor A, Tensor B, Tensor sched, int sweeps, float tol, float inner_tol, int max_inner, int fused=2) -> Tensor[]");
   m.def("philox_words(Tensor key, int nblocks, int domain, int offset) -> Tensor");
   m.def("weighted_rowsum(Tensor X, Tensor? idx, Tensor w, Tensor? sub, int K) -> Tensor");
@@ -1543,6 +1604,7 @@ TORCH_LIBRARY_IMPL(evoxmi, CompositeExplicitAutograd, m) {
 TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
   m.impl("cec_rotated_rowterms", &cec_rotated_rowterms);
   m.impl("philox_fill", &philox_fill);
+  m.impl("philox_window", &philox_window);
   m.impl("classic_eval", &classic_eval);
   m.impl("sbx", &sbx);
   m.impl("pm", &pm);
@@ -1555,6 +1617,7 @@ TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
   m.impl("weighted_rowsum", &weighted_rowsum);
   m.impl("jacobi_sweeps", &jacobi_sweeps);
   m.impl("cec_basic", &cec_basic);
+  m.impl("cec_compose", &cec_compose);
   m.impl("argsort_f32", &argsort_f32);
   m.impl("radix_argsort_f32", &radix_argsort_f32);
   m.impl("rank_argsort_f32", &rank_argsort_f32);

@@ -4,6 +4,8 @@
 #include <stdint.h>
 
 void evx_philox_fill(float* out, int64_t n, const int64_t* key, int dist, int64_t elem_offset, hipStream_t s, int batch = 1);
+void evx_philox_window(float* out, const int64_t* key, int64_t rows, int64_t dtot, int64_t col0, int64_t own, int64_t row0, int dist,
+                       hipStream_t s);
 void evx_classic_eval(const float* X, float* out, int N, int D, int func, float a, float b, float c, hipStream_t s);
 void evx_pso_update(const float* pop, const float* vel, const float* lbl, const float* lbf, const float* fit,
                     const float* gbl, const int64_t* kp, const int64_t* kg, float w, float phip, float phig,
@@ -102,6 +104,8 @@ struct EvxGemmBlk {
   int tiles_m, tiles_n;  // set by the launcher
   const float* a_rinv;   // f16x3 only: per-row inverse scales of A (M) and B (N)
   const float* b_rinv;
+  int sub_cols;           // f16x3 stacked operands: output column block c·sub_cols reads A's plane
+  int64_t a_comp_stride;  // set c (a_comp_stride uint16 elements and a_rows row scales apart)
 };
 void evx_gemm_blk(const EvxGemmBlk& a, hipStream_t s);
 int evx_gemm_blk_tile_m();
@@ -114,7 +118,7 @@ void evx_split_blk(const float* X, int64_t ld, int64_t rows, int K, const float*
 // f16x3 planes (gemm_blk.hip): f16 [ceil(K/16)][Rp][2][16] + per-row inverse scales rinv[Rp]
 int64_t evx_h3_elems(int64_t rows, int K);
 void evx_split_h3(const float* X, int64_t ld, int64_t rows, int K, const float* sub_k, const float* colscale, uint16_t* out,
-                  float* rinv, hipStream_t s);
+                  float* rinv, hipStream_t s, int ncomp = 1, int64_t sub_ld = 0);
 void evx_philox_h3(const int64_t* key, int64_t rows, int d, int64_t row0, uint16_t* out, float* rinv, hipStream_t s);
 void evx_gemm_h3(const EvxGemmBlk& a, hipStream_t s);
 // blocked planes of rows [row0, row0 + rows) of normal(key, (·, d)) (d % 4 == 0)
@@ -125,6 +129,20 @@ void evx_split_planes(const float* X, int64_t ld, int64_t rows, int K, const flo
 void evx_philox_normal_planes(const int64_t* key, int64_t rows, int d, int64_t row0, uint16_t* out, int64_t kp, hipStream_t s);
 int evx_gemm_ks_tiles_n(int M, int N, int mode);  // column tiles of a launch (row-terms partial count)
 void evx_cec_rowterms_final(const float* parts, int tiles_n, int M, int fid, float* out, hipStream_t s);
+// one-pass composition (F9–F12): per part i the basic function fid[i] on z = Z[:, zcol[i] : +D]·scale[i]
+// (zcol ≥ 0, the stacked rotation GEMM's block) or (x − os[comp[i]])·scale[i] (zcol < 0), the distance
+// ‖x − os[i]‖², weights from sigma, f = Σ w̃ (lamb·f_i + bias), clamped below thr
+constexpr int kEvxCecMaxParts = 8;
+struct EvxCecCompose {
+  int n;
+  int fid[kEvxCecMaxParts], zcol[kEvxCecMaxParts], comp[kEvxCecMaxParts];
+  float scale[kEvxCecMaxParts], sigma[kEvxCecMaxParts], lamb[kEvxCecMaxParts], bias[kEvxCecMaxParts];
+  const float* os;  // shift rows (≥ n rows, ldo apart)
+  int64_t ldo;
+  float thr;
+};
+void evx_cec_compose(const float* Z, int64_t ldz, const float* X, int64_t ldx, int N, int D, const EvxCecCompose& c, float* out,
+                     hipStream_t s);
 int evx_gemm_ks_grid(int M, int N, int mode);  // workgroups of a launch (stat_part length)
 int evx_gemm_ks_tile(int M, int N, int mode);
 void evx_gemm_ks_set_tile(int t);
@@ -157,9 +175,9 @@ void evx_jacobi_apply_solve(float* A, float* B, int np, const int* sched_t, cons
 void evx_jacobi_check(const float* A, int np, double* part, int* flag, double tol2, double* last_off, hipStream_t s);
 int evx_jacobi_parts();
 void evx_es_population(const int64_t* key, const float* center, float sigma, int64_t rows, int64_t d, int64_t half, int64_t row0, float* out,
-                       hipStream_t s);
+                       hipStream_t s, int64_t col0 = 0, int64_t dtot = 0);
 void evx_es_noise_grad(const int64_t* key, const float* w, int64_t rows, int64_t d, int64_t row0, int chunks, float* partial,
-                       hipStream_t s);
+                       hipStream_t s, int64_t col0 = 0, int64_t dtot = 0);
 void evx_philox_words(const int64_t* key, int64_t nblocks, uint32_t domain, int64_t offset, int64_t* out, hipStream_t s,
                       int batch = 1);
 void evx_colsum(const float* partial, int chunks, int D, float* out, hipStream_t s);

@@ -7,6 +7,7 @@
 // composition weights are applied by the caller.  Function ids match
 // evoxmi/problems/numerical/cec2022.py.
 #include "evoxmi_common.h"
+#include "evoxmi_launchers.h"
 
 namespace {
 
@@ -29,15 +30,10 @@ struct RowView {
   }
 };
 
-__global__ void __launch_bounds__(256) cec_basic_kernel(const float* __restrict__ Z, int64_t ld, int N, int fid,
-                                                        const int32_t* __restrict__ perm, int start, int L,
-                                                        const float* __restrict__ sub, float scale,
-                                                        const float* __restrict__ Y, int64_t ldy, int ystart, int yperm,
-                                                        float* __restrict__ out, float clamp) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (row >= N) return;
-  RowView z{Z + (int64_t)row * ld, perm, sub, start, scale};
+// f of one row (wave64: every lane returns the same value).  SCHAFFERF7's y pairs come from Y
+// (a separate row), the permuted Z row (yperm) or z itself.
+__device__ __forceinline__ float basic_row(const RowView& z, int fid, int L, int lane, const float* __restrict__ yr,
+                                           const float* __restrict__ zrow, const int32_t* __restrict__ perm, int yperm) {
   float a = 0.f, b = 0.f, p = 1.f;
   const float fL = (float)L;
   switch (fid) {
@@ -54,8 +50,8 @@ __global__ void __launch_bounds__(256) cec_basic_kernel(const float* __restrict_
     case SCHAFFERF7:
       for (int j = lane; j < L - 1; j += 64) {
         float y0, y1;
-        if (Y) { const float* yr = Y + (int64_t)row * ldy + ystart; y0 = yr[j]; y1 = yr[j + 1]; }
-        else if (yperm) { const float* zr = Z + (int64_t)row * ld; y0 = zr[perm[j]]; y1 = zr[perm[j + 1]]; }
+        if (yr) { y0 = yr[j]; y1 = yr[j + 1]; }
+        else if (yperm) { y0 = zrow[perm[j]]; y1 = zrow[perm[j + 1]]; }
         else { y0 = z(j); y1 = z(j + 1); }
         float s = sqrtf(y0 * y0 + y1 * y1);
         float t = sinf(50.f * powf(s, 0.2f));
@@ -147,20 +143,92 @@ __global__ void __launch_bounds__(256) cec_basic_kernel(const float* __restrict_
   b = evx::wave_sum(b);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) p *= __shfl_xor(p, o, 64);
-  if (lane != 0) return;
-  float f;
   switch (fid) {
-    case ZAKHAROV: f = a + b * b + b * b * b * b; break;
-    case SCHAFFERF7: f = a * a / (fL - 1.f) / (fL - 1.f); break;
-    case HGBAT: f = sqrtf(fabsf(a * a - b * b)) + (0.5f * a + b) / fL + 0.5f; break;
-    case HAPPYCAT: f = powf(fabsf(a - fL), 0.25f) + (0.5f * a + b) / fL + 0.5f; break;
-    case KATSUURA: { float c = 10.f / fL / fL; f = p * c - c; break; }
-    case ACKLEY: f = -20.f * expf(-0.2f * sqrtf(a / fL)) - expf(b / fL) + 20.f + 2.718281828459045f; break;
-    case SCHWEFEL: f = a + 4.189828872724338e2f * fL; break;
-    case GRIEWANK: f = a / 4000.f - p + 1.f; break;
-    default: f = a; break;
+    case ZAKHAROV: return a + b * b + b * b * b * b;
+    case SCHAFFERF7: return a * a / (fL - 1.f) / (fL - 1.f);
+    case HGBAT: return sqrtf(fabsf(a * a - b * b)) + (0.5f * a + b) / fL + 0.5f;
+    case HAPPYCAT: return powf(fabsf(a - fL), 0.25f) + (0.5f * a + b) / fL + 0.5f;
+    case KATSUURA: { float c = 10.f / fL / fL; return p * c - c; }
+    case ACKLEY: return -20.f * expf(-0.2f * sqrtf(a / fL)) - expf(b / fL) + 20.f + 2.718281828459045f;
+    case SCHWEFEL: return a + 4.189828872724338e2f * fL;
+    case GRIEWANK: return a / 4000.f - p + 1.f;
+    default: return a;
   }
-  out[row] = (clamp > 0.f && f < clamp) ? 0.f : f;  // the CEC'22 f < 1e-8 -> 0 clamp when clamp > 0 (NaN stays NaN)
+}
+
+__global__ void __launch_bounds__(256) cec_basic_kernel(const float* __restrict__ Z, int64_t ld, int N, int fid,
+                                                        const int32_t* __restrict__ perm, int start, int L,
+                                                        const float* __restrict__ sub, float scale,
+                                                        const float* __restrict__ Y, int64_t ldy, int ystart, int yperm,
+                                                        float* __restrict__ out, float clamp) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= N) return;
+  const float* zrow = Z + (int64_t)row * ld;
+  RowView z{zrow, perm, sub, start, scale};
+  const float f = basic_row(z, fid, L, lane, Y ? Y + (int64_t)row * ldy + ystart : nullptr, zrow, perm, yperm);
+  if (lane == 0) out[row] = (clamp > 0.f && f < clamp) ? 0.f : f;  // the CEC'22 f < 1e-8 -> 0 clamp when clamp > 0 (NaN stays NaN)
+}
+
+// Composition functions (F9–F12) in one pass: wave per row computes every component's basic
+// function — from its block of the stacked rotation GEMM output (zcol ≥ 0) or from x − o
+// (zcol < 0) — and every ‖x − o_i‖² from one read of the x row, then the weighted sum
+// f = Σ w̃_i (λ_i f_i + bias_i) with w_i = exp(−d_i²/(2 D σ_i²)) / d_i (a zero distance selects its
+// component(s)), and the f < thr → 0 clamp.  Replaces 2n + ~15 launches per evaluation.
+__global__ void __launch_bounds__(256) cec_compose_kernel(const float* __restrict__ Z, int64_t ldz, const float* __restrict__ X,
+                                                          int64_t ldx, int N, int D, EvxCecCompose c, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= N) return;
+  const float* xrow = X + (int64_t)row * ldx;
+  float d2[kEvxCecMaxParts];
+#pragma unroll
+  for (int i = 0; i < kEvxCecMaxParts; ++i) d2[i] = 0.f;
+  for (int j = lane; j < D; j += 64) {
+    const float x = xrow[j];
+#pragma unroll
+    for (int i = 0; i < kEvxCecMaxParts; ++i)
+      if (i < c.n) {
+        const float t = x - c.os[(int64_t)i * c.ldo + j];
+        d2[i] += t * t;
+      }
+  }
+  float fsum = 0.f, wsum = 0.f, zsum = 0.f;
+  int nzero = 0;
+  float w[kEvxCecMaxParts], g[kEvxCecMaxParts];
+#pragma unroll
+  for (int i = 0; i < kEvxCecMaxParts; ++i) {
+    w[i] = 0.f;
+    g[i] = 0.f;
+    if (i < c.n) {
+      d2[i] = evx::wave_sum(d2[i]);
+      const bool rot = c.zcol[i] >= 0;
+      RowView z{rot ? Z + (int64_t)row * ldz + c.zcol[i] : xrow, nullptr, rot ? nullptr : c.os + (int64_t)c.comp[i] * c.ldo, 0,
+                c.scale[i]};
+      const float f = basic_row(z, c.fid[i], D, lane, nullptr, nullptr, nullptr, 0);
+      g[i] = c.lamb[i] * f + c.bias[i];
+      const float t1 = 1.f / sqrtf(d2[i]);
+      w[i] = t1 * expf(-0.5f * d2[i] / (c.sigma[i] * c.sigma[i] * (float)D));
+      if (!isfinite(t1)) ++nzero;
+    }
+  }
+  if (lane != 0) return;
+#pragma unroll
+  for (int i = 0; i < kEvxCecMaxParts; ++i)
+    if (i < c.n) {
+      wsum += w[i];
+      if (!isfinite(1.f / sqrtf(d2[i]))) zsum += g[i];
+    }
+  float f;
+  if (nzero > 0) {
+    f = zsum / (float)nzero;
+  } else {
+#pragma unroll
+    for (int i = 0; i < kEvxCecMaxParts; ++i)
+      if (i < c.n) fsum += (w[i] / wsum) * g[i];
+    f = fsum;
+  }
+  out[row] = f < c.thr ? 0.f : f;
 }
 
 }  // namespace
@@ -188,6 +256,12 @@ __global__ void cec_rowterms_final_kernel(const float* __restrict__ parts, int t
   out[row] = f < 1e-8f ? 0.f : f;
 }
 }  // namespace
+
+void evx_cec_compose(const float* Z, int64_t ldz, const float* X, int64_t ldx, int N, int D, const EvxCecCompose& c, float* out,
+                     hipStream_t s) {
+  if (N <= 0) return;
+  cec_compose_kernel<<<(N + 3) / 4, 256, 0, s>>>(Z, ldz, X, ldx, N, D, c, out);
+}
 
 void evx_cec_rowterms_final(const float* parts, int tiles_n, int M, int fid, float* out, hipStream_t s) {
   cec_rowterms_final_kernel<<<(M + 255) / 256, 256, 0, s>>>(parts, tiles_n, M, fid, out);

@@ -467,17 +467,20 @@ __global__ void __launch_bounds__(256) split_h2_kernel(const float* __restrict__
 // row's loads at once (4 float4 per lane), stages the shifted / scaled row in LDS and reduces
 // its max |x| to the row scale.  Phase 2: thread (record, slot) computes one 16-byte slot (8
 // values of the h or m plane) from LDS — 16 consecutive threads write the 4 rows' records of
-// one 16-k block, 256 contiguous bytes.
+// one 16-k block, 256 contiguous bytes.  ncomp > 1: one plane set per shift row of sub_k
+// (sub_ld apart; sets pstride elements and Rp row scales apart) from ONE read of X — the
+// stacked composition GEMM's per-component operands (x − o_c).
 __global__ void __launch_bounds__(256) split_h4_kernel(const float* __restrict__ X, int64_t ld, int64_t rows, int K,
                                                        const float* __restrict__ sub_k, const float* __restrict__ colscale,
-                                                       uint16_t* __restrict__ out, float* __restrict__ rinv, int64_t Rp, int KB, int vec) {
+                                                       uint16_t* __restrict__ out, float* __restrict__ rinv, int64_t Rp, int KB, int vec,
+                                                       int64_t sub_ld, int ncomp, int64_t pstride) {
   __shared__ __attribute__((aligned(16))) float s_row[4][1024 + 16];
   __shared__ float s_sc[4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t r0 = (int64_t)blockIdx.x * 4;
+  float4 f[4];
   {
     const int64_t row = r0 + w;
-    float4 f[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int k = 4 * lane + 256 * c;
@@ -493,51 +496,59 @@ __global__ void __launch_bounds__(256) split_h4_kernel(const float* __restrict__
         }
       }
     }
-    float mx = 0.f;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int k = 4 * lane + 256 * c;
-      float t[4] = {f[c].x, f[c].y, f[c].z, f[c].w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const bool in = k + e < K && row < rows;
-        if (sub_k && in) t[e] -= sub_k[k + e];
-        if (colscale && in) t[e] *= colscale[k + e];
-        if (!in) t[e] = 0.f;
-        mx = fmaxf(mx, fabsf(t[e]));
-      }
-      *reinterpret_cast<float4*>(&s_row[w][k]) = make_float4(t[0], t[1], t[2], t[3]);
-    }
-    mx = evx::wave_max(mx);
-    if (lane == 0) {
-      const float sc = row < rows ? row_scale(mx) : 1.f;
-      s_sc[w] = sc;
-      if (row < Rp) rinv[row] = row < rows ? 1.f / sc : 0.f;
-    }
   }
-  __syncthreads();
-  const int rl = (threadIdx.x >> 2) & 3, pos = threadIdx.x & 3;
-  const int64_t row = r0 + rl;
-  const float sc = s_sc[rl];
-  const int sw = (int)((row >> 2) & 3), slot = pos ^ sw, plane = slot >> 1, kh = slot & 1;
-  for (int kb = threadIdx.x >> 4; kb < KB; kb += 16) {
-    const float* src = &s_row[rl][16 * kb + 8 * kh];
-    const float4 f0 = *reinterpret_cast<const float4*>(src);
-    const float4 f1 = *reinterpret_cast<const float4*>(src + 4);
-    const float v[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
-    unsigned o[4];
+  for (int comp = 0; comp < ncomp; ++comp) {
+    const float* sub = sub_k ? sub_k + comp * sub_ld : nullptr;
+    if (comp) __syncthreads();  // the previous component's phase 2 is done with s_row / s_sc
+    {
+      const int64_t row = r0 + w;
+      float mx = 0.f;
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const float a0 = v[2 * p] * sc, a1 = v[2 * p + 1] * sc;
-      const f16x2 hb = __builtin_convertvector(f32x2{a0, a1}, f16x2);
-      if (plane == 0) {
-        o[p] = __builtin_bit_cast(unsigned, hb);
-      } else {
-        const f32x2 hf = __builtin_convertvector(hb, f32x2);
-        o[p] = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{a0 - hf.x, a1 - hf.y}, f16x2));
+      for (int c = 0; c < 4; ++c) {
+        const int k = 4 * lane + 256 * c;
+        float t[4] = {f[c].x, f[c].y, f[c].z, f[c].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool in = k + e < K && row < rows;
+          if (sub && in) t[e] -= sub[k + e];
+          if (colscale && in) t[e] *= colscale[k + e];
+          if (!in) t[e] = 0.f;
+          mx = fmaxf(mx, fabsf(t[e]));
+        }
+        *reinterpret_cast<float4*>(&s_row[w][k]) = make_float4(t[0], t[1], t[2], t[3]);
+      }
+      mx = evx::wave_max(mx);
+      if (lane == 0) {
+        const float sc = row < rows ? row_scale(mx) : 1.f;
+        s_sc[w] = sc;
+        if (row < Rp) rinv[comp * Rp + row] = row < rows ? 1.f / sc : 0.f;
       }
     }
-    *reinterpret_cast<uint4*>(out + (((int64_t)kb * Rp + row) * 4 + pos) * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+    __syncthreads();
+    const int rl = (threadIdx.x >> 2) & 3, pos = threadIdx.x & 3;
+    const int64_t row = r0 + rl;
+    const float sc = s_sc[rl];
+    const int sw = (int)((row >> 2) & 3), slot = pos ^ sw, plane = slot >> 1, kh = slot & 1;
+    uint16_t* o_c = out + comp * pstride;
+    for (int kb = threadIdx.x >> 4; kb < KB; kb += 16) {
+      const float* src = &s_row[rl][16 * kb + 8 * kh];
+      const float4 f0 = *reinterpret_cast<const float4*>(src);
+      const float4 f1 = *reinterpret_cast<const float4*>(src + 4);
+      const float v[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+      unsigned o[4];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const float a0 = v[2 * p] * sc, a1 = v[2 * p + 1] * sc;
+        const f16x2 hb = __builtin_convertvector(f32x2{a0, a1}, f16x2);
+        if (plane == 0) {
+          o[p] = __builtin_bit_cast(unsigned, hb);
+        } else {
+          const f32x2 hf = __builtin_convertvector(hb, f32x2);
+          o[p] = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{a0 - hf.x, a1 - hf.y}, f16x2));
+        }
+      }
+      *reinterpret_cast<uint4*>(o_c + (((int64_t)kb * Rp + row) * 4 + pos) * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
   }
 }
 
@@ -613,7 +624,12 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_h3_kernel(EvxGemmBlk p) {
   const int wm = w / WN, wn = w % WN;
   const int r = lane & 31, h2 = lane >> 5;
 
-  const unsigned char* a_base = reinterpret_cast<const unsigned char*>(p.A) + (int64_t)m0 * kRowH + lane * 16;
+  // stacked operands (sub_cols > 0): column block n0 / sub_cols reads A's plane set of that
+  // component (a tile never straddles two blocks: sub_cols is a multiple of BN)
+  const int comp = p.sub_cols > 0 ? n0 / p.sub_cols : 0;
+  const unsigned char* a_base =
+      reinterpret_cast<const unsigned char*>(p.A + comp * p.a_comp_stride) + (int64_t)m0 * kRowH + lane * 16;
+  const float* a_rinv = p.a_rinv + (int64_t)comp * p.a_rows;
   const unsigned char* b_base = reinterpret_cast<const unsigned char*>(p.B) + (int64_t)n0 * kRowH + lane * 16;
   const int64_t a_ks = p.a_rows * kRowH, b_ks = p.b_rows * kRowH;
   auto issue = [&](int kb, int buf) {
@@ -759,7 +775,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_h3_kernel(EvxGemmBlk p) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int row = m0 + (wm * TMW + i) * 32 + 8 * q + 4 * h2;
-      ra[i][q] = row < p.M ? *reinterpret_cast<const float4*>(p.a_rinv + row) : make_float4(0.f, 0.f, 0.f, 0.f);
+      ra[i][q] = row < p.M ? *reinterpret_cast<const float4*>(a_rinv + row) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
   for (int j = 0; j < TNW; ++j) {
@@ -845,16 +861,22 @@ void evx_philox_blk(const int64_t* key, int64_t rows, int d, int64_t row0, uint1
 int64_t evx_h3_elems(int64_t rows, int K) { return ((int64_t)((K + 15) / 16) * evx_blk_rows(rows) + kEvxBlkSlackRows) * 32; }
 
 void evx_split_h3(const float* X, int64_t ld, int64_t rows, int K, const float* sub_k, const float* colscale, uint16_t* out,
-                  float* rinv, hipStream_t s) {
+                  float* rinv, hipStream_t s, int ncomp, int64_t sub_ld) {
   const int KB = (K + 15) / 16;
-  const int64_t Rp = evx_blk_rows(rows);
+  const int64_t Rp = evx_blk_rows(rows), pstride = evx_h3_elems(rows, K);
   const int vec = (reinterpret_cast<uintptr_t>(X) % 16 == 0) && (ld % 4 == 0);
+  if (ncomp < 1) ncomp = 1;
   if (K <= 1024) {
-    split_h4_kernel<<<(unsigned)(Rp / 4), 256, 0, s>>>(X, ld, rows, K, sub_k, colscale, out, rinv, Rp, KB, vec);
-  } else if (reinterpret_cast<uintptr_t>(X) % 16 == 0) {
-    split_h2_kernel<<<(unsigned)(Rp / 16), 256, 0, s>>>(X, ld, rows, K, sub_k, colscale, out, rinv, Rp, KB);
-  } else {
-    split_h_kernel<<<(unsigned)((Rp + 3) / 4), 256, 0, s>>>(X, ld, rows, K, sub_k, colscale, out, rinv, Rp, KB, 0);
+    split_h4_kernel<<<(unsigned)(Rp / 4), 256, 0, s>>>(X, ld, rows, K, sub_k, colscale, out, rinv, Rp, KB, vec, sub_ld, ncomp,
+                                                        pstride);
+    return;
+  }
+  for (int c = 0; c < ncomp; ++c) {  // long rows: one pass per component
+    const float* sub = sub_k ? sub_k + c * sub_ld : nullptr;
+    if (reinterpret_cast<uintptr_t>(X) % 16 == 0)
+      split_h2_kernel<<<(unsigned)(Rp / 16), 256, 0, s>>>(X, ld, rows, K, sub, colscale, out + c * pstride, rinv + c * Rp, Rp, KB);
+    else
+      split_h_kernel<<<(unsigned)((Rp + 3) / 4), 256, 0, s>>>(X, ld, rows, K, sub, colscale, out + c * pstride, rinv + c * Rp, Rp, KB, 0);
   }
 }
 

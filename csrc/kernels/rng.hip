@@ -47,6 +47,56 @@ void evx_philox_fill(float* out, int64_t n, const int64_t* key, int dist, int64_
     philox_fill_kernel<1><<<grid, 256, 0, s>>>(out, n, key, elem_offset >> 2);
 }
 
+// A column window of a Philox matrix: out[i][c] = element (row0 + i)·dtot + col0 + c of the
+// uniform (DIST 0) / normal (DIST 1) stream — the block a decision-axis-sharded rank owns,
+// bitwise equal to those columns of philox_fill over the whole (·, dtot) matrix.  One thread
+// per 4 outputs; 16-B loads of the Philox block when the window is 4-aligned.
+namespace {
+template <int DIST>
+__global__ void __launch_bounds__(256) philox_window_kernel(float* __restrict__ out, const int64_t* __restrict__ key, int64_t rows,
+                                                            int64_t dtot, int64_t col0, int64_t own, int64_t row0) {
+  uint32_t k0, k1;
+  evx::load_key(key, k0, k1);
+  const bool v4 = (own & 3) == 0 && (col0 & 3) == 0 && (dtot & 3) == 0;
+  const int64_t per_row = v4 ? own >> 2 : own;
+  const int64_t total = rows * per_row;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = t / per_row, c = t - i * per_row;
+    if (v4) {
+      const int64_t j = c << 2;
+      const evx::u4 w = evx::philox_block((uint64_t)(((row0 + i) * dtot + col0 + j) >> 2), k0, k1);
+      const float4 v = DIST == 0 ? make_float4(evx::u24(w.x), evx::u24(w.y), evx::u24(w.z), evx::u24(w.w)) : evx::normal4(w);
+      *reinterpret_cast<float4*>(out + i * own + j) = v;
+    } else {
+      const uint64_t e = (uint64_t)((row0 + i) * dtot + col0 + c);
+      const evx::u4 w = evx::philox_block(e >> 2, k0, k1);
+      const int q = (int)(e & 3);
+      float v;
+      if (DIST == 0) {
+        v = evx::u24(q == 0 ? w.x : (q == 1 ? w.y : (q == 2 ? w.z : w.w)));
+      } else {
+        const float4 n4 = evx::normal4(w);
+        v = q == 0 ? n4.x : (q == 1 ? n4.y : (q == 2 ? n4.z : n4.w));
+      }
+      out[i * own + c] = v;
+    }
+  }
+}
+}  // namespace
+
+void evx_philox_window(float* out, const int64_t* key, int64_t rows, int64_t dtot, int64_t col0, int64_t own, int64_t row0, int dist,
+                       hipStream_t s) {
+  const bool v4 = (own & 3) == 0 && (col0 & 3) == 0 && (dtot & 3) == 0;
+  const int64_t total = rows * (v4 ? own >> 2 : own);
+  int64_t g = (total + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  if (dist == 0)
+    philox_window_kernel<0><<<(unsigned)g, 256, 0, s>>>(out, key, rows, dtot, col0, own, row0);
+  else
+    philox_window_kernel<1><<<(unsigned)g, 256, 0, s>>>(out, key, rows, dtot, col0, own, row0);
+}
+
 // Raw Philox words for small key-management ops (split / fold_in / bits): one launch
 // instead of ~80 int64 elementwise kernels.  out[b][w] = word w of block (offset + b)
 // with counter (b_lo, b_hi, 0, domain).  Words are stored as int64 (uint32 values).
@@ -84,8 +134,11 @@ void evx_philox_words(const int64_t* key, int64_t nblocks, uint32_t domain, int6
 // the N×P noise matrix.  One column per thread, chunks of rows per grid.y (partials summed
 // in a fixed order on the host side: deterministic).
 namespace {
+// (col0, dtot): the column window [col0, col0 + d) of a (·, dtot) noise matrix (decision-axis
+// sharding: each rank reduces only its own columns)
 __global__ void __launch_bounds__(256) es_noise_grad_kernel(const int64_t* __restrict__ key, const float* __restrict__ w, int64_t rows,
-                                                            int64_t d, int64_t row0, int64_t per, float* __restrict__ partial) {
+                                                            int64_t d, int64_t row0, int64_t per, float* __restrict__ partial,
+                                                            int64_t col0, int64_t dtot) {
   uint32_t k0, k1;
   evx::load_key(key, k0, k1);
   const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -94,7 +147,7 @@ __global__ void __launch_bounds__(256) es_noise_grad_kernel(const int64_t* __res
   const int64_t i0 = c * per, i1 = min(rows, i0 + per);
   float acc = 0.f;
   for (int64_t i = i0; i < i1; ++i) {
-    const uint64_t e = (uint64_t)((row0 + i) * d + j);
+    const uint64_t e = (uint64_t)((row0 + i) * dtot + col0 + j);
     const evx::u4 b = evx::philox_block(e >> 2, k0, k1);
     // the Box–Muller pair of element e only (same operations as evx::normal4)
     const int q = (int)(e & 3);
@@ -108,10 +161,10 @@ __global__ void __launch_bounds__(256) es_noise_grad_kernel(const int64_t* __res
 }  // namespace
 
 void evx_es_noise_grad(const int64_t* key, const float* w, int64_t rows, int64_t d, int64_t row0, int chunks, float* partial,
-                       hipStream_t s) {
+                       hipStream_t s, int64_t col0, int64_t dtot) {
   const int64_t per = (rows + chunks - 1) / chunks;
   const dim3 grid((unsigned)((d + 255) / 256), (unsigned)chunks);
-  es_noise_grad_kernel<<<grid, 256, 0, s>>>(key, w, rows, d, row0, per, partial);
+  es_noise_grad_kernel<<<grid, 256, 0, s>>>(key, w, rows, d, row0, per, partial, col0, dtot > 0 ? dtot : d);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -121,14 +174,16 @@ void evx_es_noise_grad(const int64_t* key, const float* w, int64_t rows, int64_t
 // f32 noise matrix, its mirrored copy and their concatenation are never written.  The sum is
 // c + (s·σ)·ε with two roundings: bitwise the torch expression it replaces.
 namespace {
+// (col0, dtot): columns [col0, col0 + d) of the (·, dtot) rows, center holding those d columns
 __global__ void __launch_bounds__(256) es_population_kernel(const int64_t* __restrict__ key, const float* __restrict__ center, float sigma,
-                                                            int64_t rows, int64_t d, int64_t half, int64_t row0, float* __restrict__ out) {
+                                                            int64_t rows, int64_t d, int64_t half, int64_t row0, float* __restrict__ out,
+                                                            int64_t col0, int64_t dtot) {
   // two roundings (σ·ε, then + c) like the torch expression: no FMA contraction in this scope
   // (plain operators: the pragma does not reach the __fmul_rn / __fadd_rn header definitions)
 #pragma clang fp contract(off)
   uint32_t k0, k1;
   evx::load_key(key, k0, k1);
-  const bool v4 = (d & 3) == 0;
+  const bool v4 = (d & 3) == 0 && (col0 & 3) == 0 && (dtot & 3) == 0;
   const int64_t per_row = v4 ? d >> 2 : d;
   const int64_t total = rows * per_row;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
@@ -139,7 +194,7 @@ __global__ void __launch_bounds__(256) es_population_kernel(const int64_t* __res
     const float ss = neg ? -sigma : sigma;
     if (v4) {
       const int64_t j = c << 2;
-      const float4 n = evx::normal4(evx::philox_block((uint64_t)((r * d + j) >> 2), k0, k1));
+      const float4 n = evx::normal4(evx::philox_block((uint64_t)((r * dtot + col0 + j) >> 2), k0, k1));
       const float4 ce = *reinterpret_cast<const float4*>(center + j);
       float4 o;
       o.x = ce.x + ss * n.x;
@@ -148,7 +203,7 @@ __global__ void __launch_bounds__(256) es_population_kernel(const int64_t* __res
       o.w = ce.w + ss * n.w;
       *reinterpret_cast<float4*>(out + i * d + j) = o;
     } else {
-      const uint64_t e = (uint64_t)(r * d + c);
+      const uint64_t e = (uint64_t)(r * dtot + col0 + c);
       const evx::u4 b = evx::philox_block(e >> 2, k0, k1);
       const float4 n4 = evx::normal4(b);
       const int q = (int)(e & 3);
@@ -160,10 +215,12 @@ __global__ void __launch_bounds__(256) es_population_kernel(const int64_t* __res
 }  // namespace
 
 void evx_es_population(const int64_t* key, const float* center, float sigma, int64_t rows, int64_t d, int64_t half, int64_t row0, float* out,
-                       hipStream_t s) {
-  const int64_t total = rows * ((d & 3) == 0 ? d >> 2 : d);
+                       hipStream_t s, int64_t col0, int64_t dtot) {
+  if (dtot <= 0) dtot = d;
+  const bool v4 = (d & 3) == 0 && (col0 & 3) == 0 && (dtot & 3) == 0;
+  const int64_t total = rows * (v4 ? d >> 2 : d);
   int64_t g = (total + 255) / 256;
   if (g > 8192) g = 8192;
   if (g < 1) g = 1;
-  es_population_kernel<<<(unsigned)g, 256, 0, s>>>(key, center, sigma, rows, d, half, row0, out);
+  es_population_kernel<<<(unsigned)g, 256, 0, s>>>(key, center, sigma, rows, d, half, row0, out, col0, dtot);
 }

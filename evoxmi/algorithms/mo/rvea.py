@@ -16,6 +16,10 @@ from .common import MOAlgorithm
 
 
 class RVEA(MOAlgorithm):
+    # decision-axis state sharding (P2): SBX + PM per global column (ColumnVariation), the
+    # APD selection and the reference-vector adaptation use the replicated objectives only
+    column_separable = True
+
     def __init__(self, lb, ub, n_objs, pop_size, alpha=2, fr=0.1, max_gen=100, selection_op=None, mutation_op=None, crossover_op=None):
         super().__init__(lb, ub, n_objs, pop_size, mutation_op, crossover_op)
         self.alpha, self.fr, self.max_gen = alpha, fr, max_gen

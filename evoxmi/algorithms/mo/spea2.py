@@ -63,6 +63,10 @@ def truncation_predicated(obj, k, mask, max_k: int):
 
 
 class SPEA2(MOAlgorithm):
+    # decision-axis state sharding (P2): variation per global column, tournament and
+    # truncation from the replicated objectives
+    column_separable = True
+
     def __init__(self, lb, ub, n_objs, pop_size, mutation_op=None, crossover_op=None):
         super().__init__(lb, ub, n_objs, pop_size, mutation_op, crossover_op)
         self.selection = selection.Tournament(n_round=pop_size)
@@ -70,7 +74,7 @@ class SPEA2(MOAlgorithm):
     def ask(self, state):
         key, sel_key, x_key, mut_key = rnd.split(state.key, 4)
         selected, _ = self.selection(sel_key, state.population, cal_fitness(state.fitness))
-        off = self.mutation(mut_key, self.crossover(x_key, selected))
+        off = self._variation(x_key, mut_key, selected, clip=False)
         return off, state.update(next_generation=off, key=key)
 
     def tell(self, state, fitness):

@@ -38,6 +38,10 @@ def theta_nd_sort(obj, w, mask):
 
 
 class TDEA(MOAlgorithm):
+    # decision-axis state sharding (P2): variation per global column, θ-dominance selection
+    # from the replicated objectives
+    column_separable = True
+
     def __init__(self, lb, ub, n_objs, pop_size, mutation_op=None, crossover_op=None):
         super().__init__(lb, ub, n_objs, pop_size, mutation_op, crossover_op)
         self.sample = UniformSampling(pop_size, n_objs)
@@ -58,7 +62,7 @@ class TDEA(MOAlgorithm):
     def ask(self, state):
         key, sel_key, x_key, mut_key = rnd.split(state.key, 4)
         pool = rnd.randint(sel_key, (self.pop_size,), 0, self.pop_size).to(state.population.device)
-        off = self.mutation(mut_key, self.crossover(x_key, state.population[pool]))
+        off = self._variation(x_key, mut_key, state.population[pool], clip=False)
         return off, state.update(next_generation=off, key=key)
 
     def tell(self, state, fitness):

@@ -23,12 +23,19 @@ from __future__ import annotations
 
 import torch
 
+from ....parallel.dim_sharded import ColumnSeparable
 from ....core import Algorithm
 from ....ops import random as rnd
 from . import common as C
 
 
-class LSHADE(Algorithm):
+class LSHADE(ColumnSeparable, Algorithm):
+    # decision-axis state sharding (P2) for the whole family (iL-SHADE, jSO, LSHADE-RSP only
+    # override hooks): trials per global column, the shrinking population's row moves and the
+    # memories from the replicated fitness
+    column_separable = True
+    dim_fields = ("population", "trial_vectors", "archive", "worst_solution")
+
     memory_F_init = 0.5
     memory_CR_init = 0.5
 
@@ -107,9 +114,10 @@ class LSHADE(Algorithm):
         CR = self._adjust_CR(CR, state, prog)
         cur = torch.arange(N, device=dev)
         red = state.pop_size_reduced
+        c0, own, d = self.cols()
         trials, _ = C.generate_trials(k_trial, state.population, state.fitness, state.best_index, cur, C.current2pbest_1_bin, F,
-                                      CR, self.diff_padding_num, self.lb, self.ub, p=state.p, reduced=red,
-                                      Fw=self._Fw(prog), repair="midpoint", **self._diff_mode(state))
+                                      CR, self.diff_padding_num, self.col_vec(self.lb), self.col_vec(self.ub), p=state.p, reduced=red,
+                                      Fw=self._Fw(prog), repair="midpoint", cols=(c0, d), **self._diff_mode(state))
         live = cur < red
         trials = torch.where(live[:, None], trials, state.worst_solution)
         return trials, state.update(trial_vectors=trials, key=key, F_vect=F, CR_vect=CR)

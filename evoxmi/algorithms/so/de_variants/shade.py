@@ -9,12 +9,17 @@ from __future__ import annotations
 
 import torch
 
+from ....parallel.dim_sharded import ColumnSeparable
 from ....core import Algorithm
 from ....ops import random as rnd
 from . import common as C
 
 
-class SHADE(Algorithm):
+class SHADE(ColumnSeparable, Algorithm):
+    # decision-axis state sharding (P2): see JaDE
+    column_separable = True
+    dim_fields = ("population", "trial_vectors", "archive")
+
     def __init__(self, lb, ub, pop_size=100, diff_padding_num=3, differential_weight=None, cross_probability=None,
                  with_archive=1, p=0.05):
         super().__init__()
@@ -45,9 +50,10 @@ class SHADE(Algorithm):
         F = torch.clamp(rnd.cauchy(k_f, (N,)).to(dev) * 0.1 + state.Memory_F[ids], 0, 1)
         CR = torch.clamp(rnd.normal(k_cr, (N,)).to(dev) * 0.1 + state.Memory_CR[ids], 0, 1)
         cur = torch.arange(N, device=dev)
+        c0, own, d = self.cols()
         trials, _ = C.generate_trials(k_trial, state.population, state.fitness, state.best_index, cur, C.current2pbest_1_bin, F,
-                                      CR, self.diff_padding_num, self.lb, self.ub, p=state.p,
-                                      archive=state.archive if self.with_archive else None)
+                                      CR, self.diff_padding_num, self.col_vec(self.lb), self.col_vec(self.ub), p=state.p,
+                                      archive=state.archive if self.with_archive else None, cols=(c0, d))
         return trials, state.update(trial_vectors=trials, key=key, F_vect=F, CR_vect=CR)
 
     def tell(self, state, trial_fitness):

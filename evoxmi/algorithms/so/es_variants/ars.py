@@ -5,10 +5,17 @@ import torch
 
 from ....core import Algorithm, State, use_state
 from ....ops import random as rnd
+from ....parallel.dim_sharded import ColumnSeparable
 from ._common import make_optimizer
 
 
-class ARS(Algorithm):
+class ARS(ColumnSeparable, Algorithm):
+    # decision-axis state sharding (P2): centre, population, noise and Adam's moments are column
+    # blocks; elite choice and the fitness scale come from the replicated fitness
+    column_separable = True
+    dim_fields = ("center", "population", "noise")
+    dim_child_fields = {"optimizer": ("opt_state",)}
+
     def __init__(self, pop_size, center_init, elite_ratio=0.1, optimizer="adam", lr=0.05, sigma=0.03):
         super().__init__()
         assert not pop_size & 1
@@ -29,7 +36,7 @@ class ARS(Algorithm):
 
     def ask(self, state):
         key, _ = rnd.split(state.key)
-        z_plus = rnd.normal(state.key, (self.pop_size // 2, self.dim)).to(state.center.device)
+        z_plus = self.normal_cols(state.key, self.pop_size // 2, state.center.device)
         z = torch.cat([z_plus, -z_plus])
         x = state.center + self.sigma * z
         return x, state.update(key=key, population=x, noise=z)

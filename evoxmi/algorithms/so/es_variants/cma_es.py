@@ -38,6 +38,7 @@ from ....runtime import host_phase
 from ....utils import profiling
 from .... import config
 from ....ops import linalg
+from ....parallel.dim_sharded import ColumnSeparable
 from ....ops.linalg import Operand, gemm, mm, plain_nt
 from ....ops.reduce import weighted_rowsum
 from ....ops.sort import argsort, argsort_i32
@@ -459,8 +460,16 @@ class CMAES(Algorithm):
         return self._finish_tell(state, buf[:d], buf[d:].reshape(d, d))
 
 
-class SepCMAES(CMAES):
-    """Separable CMA-ES (diagonal covariance, linear time/space)."""
+class SepCMAES(ColumnSeparable, CMAES):
+    """Separable CMA-ES (diagonal covariance, linear time/space).
+
+    Decision-axis state sharding (P2): mean, paths, diag(C) and the population are column
+    blocks; the noise is drawn per global column (normal_cols) and the one cross-column
+    quantity, ‖p_σ‖, is an all-reduced sum of squares (col_sum) — the collective GSPMD
+    inserts for the same norm over a sharded axis."""
+
+    column_separable = True
+    dim_fields = ("pc", "ps", "C", "mean", "population")
 
     def setup(self, key):
         dev = self.center_init.device
@@ -480,7 +489,7 @@ class SepCMAES(CMAES):
 
     def ask(self, state):
         key, sample_key = rnd.split(state.key)
-        noise = rnd.normal(sample_key, (self.pop_size, self.dim)).to(state.mean.device)
+        noise = self.normal_cols(sample_key, self.pop_size, state.mean.device)
         population = state.mean + state.sigma * torch.sqrt(state.C) * noise
         return population, state.update(population=population, count_iter=state.count_iter + 1, key=key)
 
@@ -491,11 +500,12 @@ class SepCMAES(CMAES):
         delta_mean = mean - state.mean
         ps = (1 - self.cs) * state.ps + math.sqrt(self.cs * (2 - self.cs) * self.mueff) * delta_mean / torch.sqrt(state.C) / state.sigma
         count = state.count_iter.to(torch.float32)
-        hsig = (torch.linalg.norm(ps) / torch.sqrt(1 - (1 - self.cs) ** (2 * count)) < (1.4 + 2 / (self.dim + 1)) * self.chiN).to(torch.float32)
+        ps_norm = torch.sqrt(self.col_sum((ps * ps).sum()))
+        hsig = (ps_norm / torch.sqrt(1 - (1 - self.cs) ** (2 * count)) < (1.4 + 2 / (self.dim + 1)) * self.chiN).to(torch.float32)
         pc = (1 - self.cc) * state.pc + hsig * math.sqrt(self.cc * (2 - self.cc) * self.mueff) * delta_mean / state.sigma
         y = (sel - state.mean) / state.sigma
         C = (1 - self.c1 - self.cmu) * state.C + self.c1 * (pc**2 + (1 - hsig) * self.cc * (2 - self.cc) * state.C) + self.cmu * (self.weights @ (y**2))
-        sigma = state.sigma * torch.exp((self.cs / self.damps) * (torch.linalg.norm(ps) / self.chiN - 1))
+        sigma = state.sigma * torch.exp((self.cs / self.damps) * (ps_norm / self.chiN - 1))
         return state.update(mean=mean, ps=ps, pc=pc, C=C, sigma=sigma)
 
 

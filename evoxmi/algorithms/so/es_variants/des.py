@@ -5,6 +5,7 @@ import torch
 
 from ....core import Algorithm, State
 from ....ops import random as rnd
+from ....parallel.dim_sharded import ColumnSeparable
 
 
 def get_des_weights(popsize: int, temperature: float = 12.5):
@@ -12,10 +13,15 @@ def get_des_weights(popsize: int, temperature: float = 12.5):
     return torch.softmax(-20 * torch.sigmoid(temperature * ranks), 0)
 
 
-class DES(Algorithm):
+class DES(ColumnSeparable, Algorithm):
+    # decision-axis state sharding (P2): centre, σ and the samples are column blocks
+    column_separable = True
+    dim_fields = ("sigma", "center", "x")
+
     def __init__(self, pop_size, center_init, temperature=12.5, sigma_init=0.1, mean_decay=0.0):
         super().__init__()
         self.num_dims = center_init.shape[0]
+        self.dim = self.num_dims
         self.center_init = center_init
         self.popsize = pop_size
         self.sigma_init = sigma_init
@@ -31,7 +37,7 @@ class DES(Algorithm):
 
     def ask(self, state):
         key, _ = rnd.split(state.key)
-        z = rnd.normal(state.key, (self.popsize, self.num_dims)).to(state.center.device)
+        z = self.normal_cols(state.key, self.popsize, state.center.device)
         x = state.center + z * state.sigma[None, :]
         return x, state.update(key=key, x=x)
 

@@ -36,12 +36,16 @@ def _normal_rows(key, rows: int, d: int, row0: int, dev):
     return rnd.normal(key, (rows, d), offset=row0 * d).to(dev)
 
 
-def _noise_grad(key, w, d: int, row0: int, dev):
-    """Σ_i w[i] · normal(key)[row0 + i, :] without materialising the rows on the device."""
+def _noise_grad(key, w, d: int, row0: int, dev, cols=None):
+    """Σ_i w[i] · normal(key)[row0 + i, :] without materialising the rows on the device;
+    ``cols = (col0, own)``: only the column window [col0, col0 + own) of the d columns."""
+    c0, own = cols if cols is not None else (0, d)
     if w.numel() == 0:
-        return torch.zeros(d, device=dev)
+        return torch.zeros(own, device=dev)
     if dev.type == "cuda":
-        return _ext.ops().es_noise_grad(key.to(dev).contiguous(), w.to(torch.float32).contiguous(), int(d), int(row0))
+        return _ext.ops().es_noise_grad(key.to(dev).contiguous(), w.to(torch.float32).contiguous(), int(own), int(row0), int(c0), int(d))
+    if cols is not None:
+        return rnd.normal_window(key, w.shape[0], d, c0, own, row0, dev).T @ w.to(torch.float32)
     return _normal_rows(key, w.shape[0], d, row0, dev).T @ w.to(torch.float32)
 
 
@@ -49,7 +53,8 @@ class OpenES(ColumnSeparable, Algorithm):
     rank_local_fields = ("population",)
     # decision-axis state sharding (StdWorkflow.enable_multi_devices(shard_state=True)): the
     # centre, the population and an element-wise optimiser's state are column blocks; every
-    # rank regenerates its columns of the (virtual) Philox noise and reduces εᵀf over them
+    # rank draws only its columns of the (virtual) Philox noise (es_population / es_noise_grad
+    # with a column window) and reduces εᵀf over them
     column_separable = True
     dim_fields = ("population", "center")
     dim_child_fields = {"optimizer": ("opt_state",)}
@@ -84,45 +89,47 @@ class OpenES(ColumnSeparable, Algorithm):
         dev = state.center.device
         if self._cols is None:
             population = self._population_rows(noise_key, state.center, 0, self.pop_size)
-        else:  # column block of a decision-axis-sharded state
-            noise = self.col_vec(self._noise_rows(noise_key, 0, self.pop_size, dev))
-            population = state.center[None, :] + self.noise_stdev * noise
+        else:  # column block of a decision-axis-sharded state: only this rank's noise columns are drawn
+            population = self._population_rows(noise_key, state.center, 0, self.pop_size, cols=self.cols())
         return population, state.update(population=population, key=key, noise_key=noise_key.to(state.noise_key.device))
 
-    def _population_rows(self, noise_key, center, start: int, size: int):
+    def _population_rows(self, noise_key, center, start: int, size: int, cols=None):
         """Rows [start, start + size) of center + σ·ε (mirrored: −ε for the second half).  On the
         device ONE kernel (rng.hip: es_population_kernel) draws the same Philox noise as
         :meth:`_noise_rows` and writes the rows; the noise matrix, its negated copy and their
         concatenation are never materialised."""
+        c0, own, dtot = cols if cols is not None else (0, center.shape[0], center.shape[0])
         if center.is_cuda and center.dtype == torch.float32:
             half = self.pop_size // 2 if self.mirrored_sampling else 0
             return _ext.ops().es_population(noise_key.to(center.device).contiguous(), center.contiguous(), float(self.noise_stdev),
-                                            int(size), int(half), int(start))
-        return center[None, :] + self.noise_stdev * self._noise_rows(noise_key, start, size, center.device)
+                                            int(size), int(half), int(start), int(c0), int(dtot))
+        noise = self._noise_rows(noise_key, start, size, center.device)
+        return center[None, :] + self.noise_stdev * (noise[:, c0 : c0 + own] if cols is not None else noise)
 
-    def _grad_rows(self, noise_key, fitness, start: int, size: int, dev):
-        """Σ over global rows [start, start + size) of f_g ε_g (f indexed by global row)."""
+    def _grad_rows(self, noise_key, fitness, start: int, size: int, dev, cols=None):
+        """Σ over global rows [start, start + size) of f_g ε_g (f indexed by global row);
+        ``cols = (col0, own)``: only that column window of ε."""
         d = self.dim
+        width = cols[1] if cols is not None else d
         f = fitness.to(torch.float32)
         if not self.mirrored_sampling:
-            return _noise_grad(noise_key, f[start : start + size], d, start, dev)
+            return _noise_grad(noise_key, f[start : start + size], d, start, dev, cols)
         h = self.pop_size // 2
-        g = torch.zeros(d, device=dev)
+        g = torch.zeros(width, device=dev)
         a0, a1 = start, min(start + size, h)
         b0, b1 = max(start, h), start + size
         if a1 > a0 and b0 == h and b1 - h == a1 - a0 and a0 == 0:
             # whole population on one rank: mirrored pairs folded into one pass
-            return _noise_grad(noise_key, f[:h] - f[h:], d, 0, dev)
+            return _noise_grad(noise_key, f[:h] - f[h:], d, 0, dev, cols)
         if a1 > a0:
-            g = g + _noise_grad(noise_key, f[a0:a1], d, a0, dev)
+            g = g + _noise_grad(noise_key, f[a0:a1], d, a0, dev, cols)
         if b1 > b0:
-            g = g - _noise_grad(noise_key, f[b0:b1], d, b0 - h, dev)
+            g = g - _noise_grad(noise_key, f[b0:b1], d, b0 - h, dev, cols)
         return g
 
     def tell(self, state, fitness):
-        grad = self._grad_rows(state.noise_key, fitness, 0, self.pop_size, state.center.device) / self.pop_size / self.noise_stdev
-        if self._cols is not None:
-            grad = self.col_vec(grad).contiguous()
+        cols = (self.cols()[0], self.cols()[1]) if self._cols is not None else None
+        grad = self._grad_rows(state.noise_key, fitness, 0, self.pop_size, state.center.device, cols) / self.pop_size / self.noise_stdev
         if self.optimizer is None:
             center = state.center - self.learning_rate * grad
         else:

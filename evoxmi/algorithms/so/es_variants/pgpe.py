@@ -12,6 +12,7 @@ import torch
 from ....core import Algorithm, State, Stateful, use_state
 from ....ops import random as rnd
 from ....utils import optim
+from ....parallel.dim_sharded import ColumnSeparable
 
 
 def _l2(x):
@@ -29,14 +30,26 @@ class ClipUp(Stateful):
     def setup(self, key):
         return State(velocity=torch.zeros_like(self.params))
 
+    _col_sum = None  # set under decision-axis sharding: the norms sum squares over every rank's columns
+
+    def _norm(self, x):
+        sq = (x * x).sum()
+        return torch.sqrt(self._col_sum(sq) if self._col_sum is not None else sq)
+
     def update(self, state, gradient, _params=None):
-        velocity = self.momentum * state.velocity + self.step_size * gradient / _l2(gradient)
-        vn = _l2(velocity)
+        velocity = self.momentum * state.velocity + self.step_size * gradient / self._norm(gradient)
+        vn = self._norm(velocity)
         velocity = torch.where(vn > self.max_speed, self.max_speed * velocity / vn, velocity)
         return -velocity, state.update(velocity=velocity)
 
 
-class PGPE(Algorithm):
+class PGPE(ColumnSeparable, Algorithm):
+    # decision-axis state sharding (P2): centre, stdev and noise are column blocks (noise drawn
+    # per global column), the optimiser's state too; ClipUp's two norms all-reduce their sums
+    # of squares (col_sum)
+    column_separable = True
+    dim_fields = ("center", "stdev", "noise")
+
     def __init__(self, pop_size, center_init, optimizer, stdev_init=0.1, center_learning_rate=0.15, stdev_learning_rate=0.1,
                  stdev_max_change=0.2):
         super().__init__()
@@ -60,6 +73,16 @@ class PGPE(Algorithm):
             raise TypeError(f"{optimizer} is not supported right now")
         self.optimizer = optimizer
 
+    def dim_shard(self, state, col0: int, own: int):
+        if isinstance(self.optimizer, ClipUp):
+            self.dim_child_fields = {"optimizer": ("velocity",)}
+            self.optimizer._col_sum = self.col_sum
+        elif isinstance(self.optimizer, optim.OptaxWrapper):
+            self.dim_child_fields = {"optimizer": ("opt_state",)}
+        else:
+            raise ValueError("PGPE column sharding needs ClipUp or an element-wise optax-style optimiser")
+        return super().dim_shard(state, col0, own)
+
     def setup(self, key):
         dev = self.center_init.device
         return State(center=self.center_init.clone(), stdev=torch.full((self.dim,), float(self.stdev_init), device=dev), key=key,
@@ -67,7 +90,7 @@ class PGPE(Algorithm):
 
     def ask(self, state):
         key, sub = rnd.split(state.key)
-        noise = rnd.normal(sub, (self.pop_size // 2, self.dim)).to(state.center.device) * state.stdev
+        noise = self.normal_cols(sub, self.pop_size // 2, state.center.device) * state.stdev
         return torch.cat([state.center + noise, state.center - noise], 0), state.update(key=key, noise=noise)
 
     def tell(self, state, fitness):

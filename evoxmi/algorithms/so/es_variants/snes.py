@@ -6,6 +6,7 @@ import math
 import torch
 
 from ....core import Algorithm, State
+from ....parallel.dim_sharded import ColumnSeparable
 from ....ops import random as rnd
 
 
@@ -19,10 +20,17 @@ def get_temp_weights(popsize: int, temperature: float):
     return torch.softmax(-temperature * ranks, 0)
 
 
-class SNES(Algorithm):
+class SNES(ColumnSeparable, Algorithm):
+    # decision-axis state sharding (P2): centre, σ, noise and population are column blocks;
+    # each rank draws only its columns of the Philox noise (normal_cols), the update weights
+    # come from the replicated fitness ranks
+    column_separable = True
+    dim_fields = ("sigma", "center", "noise", "population")
+
     def __init__(self, pop_size, center_init, sigma=1.0, lrate_mean=1.0, temperature=0.0, init_min=0.0, init_max=0.0):
         super().__init__()
         self.num_dims = center_init.shape[0]
+        self.dim = self.num_dims
         self.center_init = center_init
         self.popsize = pop_size
         self.sigma = sigma
@@ -40,7 +48,7 @@ class SNES(Algorithm):
 
     def ask(self, state):
         key, _ = rnd.split(state.key)
-        noise = rnd.normal(key, (self.popsize, self.num_dims)).to(state.center.device)
+        noise = self.normal_cols(key, self.popsize, state.center.device)
         x = state.center + noise * state.sigma[None, :]
         return x, state.update(key=key, noise=noise, population=x)
 

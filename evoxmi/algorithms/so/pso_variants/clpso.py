@@ -5,10 +5,16 @@ import torch
 
 from ....core import Algorithm, State
 from ....ops import random as rnd
+from ....parallel.dim_sharded import ColumnSeparable
 from .utils import init_swarm, min_by
 
 
-class CLPSO(Algorithm):
+class CLPSO(ColumnSeparable, Algorithm):
+    # decision-axis state sharding (P2): positions, velocities and the personal / global bests
+    # are column blocks; exemplar choice and the best updates use the replicated fitness only
+    column_separable = True
+    dim_fields = ("population", "velocity", "pbest_position", "gbest_position")
+
     def __init__(self, lb, ub, pop_size, inertia_weight, const_coefficient, learning_probability):
         super().__init__()
         self.dim = lb.shape[0]
@@ -30,7 +36,7 @@ class CLPSO(Algorithm):
         key, k_coef, k1, k2, k_rand = rnd.split(state.key, 5)
         dev = fitness.device
         N, d = self.pop_size, self.dim
-        coef = rnd.uniform(k_coef, (N, d)).to(dev)
+        coef = self.uniform_cols(k_coef, N, dev)
         better = state.pbest_fitness > fitness
         pbest_position = torch.where(better[:, None], state.population, state.pbest_position)
         pbest_fitness = torch.minimum(state.pbest_fitness, fitness)
@@ -42,6 +48,6 @@ class CLPSO(Algorithm):
         rp = rnd.uniform(k_rand, (N,)).to(dev)
         pbest = torch.where((rp < self.P_c)[:, None], learning_pbest, state.pbest_position)
         velocity = self.w * state.velocity + self.c * coef * (pbest - state.population)
-        population = torch.clamp(state.population + velocity, self.lb, self.ub)
+        population = torch.clamp(state.population + velocity, self.col_vec(self.lb), self.col_vec(self.ub))
         return state.update(population=population, velocity=velocity, pbest_position=pbest_position, pbest_fitness=pbest_fitness,
                             gbest_position=gpos, gbest_fitness=gfit.reshape(1), key=key)

@@ -10,9 +10,16 @@ import torch
 
 from ....core import Algorithm, State
 from ....ops import random as rnd
+from ....parallel.dim_sharded import ColumnSeparable
 
 
-class CSO(Algorithm):
+class CSO(ColumnSeparable, Algorithm):
+    # decision-axis state sharding (P2): positions and velocities are column blocks, the
+    # pairing comes from the replicated fitness, the learning coefficients are drawn per
+    # global column and the swarm centre is a per-column mean
+    column_separable = True
+    dim_fields = ("population", "velocity")
+
     def __init__(self, lb, ub, pop_size, phi=0.0, mean=None, stdev=None):
         super().__init__()
         self.lb, self.ub, self.pop_size, self.phi = lb, ub, pop_size, phi
@@ -44,11 +51,11 @@ class CSO(Algorithm):
         mask = state.fitness[perm[0]] < state.fitness[perm[1]]
         teachers = torch.where(mask, perm[0], perm[1])
         students = torch.where(mask, perm[1], perm[0])
-        l1, l2, l3 = (rnd.uniform(k, (h, self.dim)).to(dev) for k in (k1, k2, k3))
+        l1, l2, l3 = (self.uniform_cols(k, h, dev) for k in (k1, k2, k3))
         center = state.population.mean(0)
         ps = state.population[students]
         v = l1 * state.velocity[students] + l2 * (state.population[teachers] - ps) + self.phi * l3 * (center - ps)
-        cand = torch.clamp(ps + v, self.lb, self.ub)
+        cand = torch.clamp(ps + v, self.col_vec(self.lb), self.col_vec(self.ub))
         pop = state.population.index_copy(0, students, cand)
         vel = state.velocity.index_copy(0, students, v)
         return cand, state.update(population=pop, velocity=vel, students=students, key=key)

@@ -65,6 +65,7 @@ KNOBS: Dict[str, Knob] = {
     "sbr_xgate": Knob("EVOXMI_SBR_XGATE", 2, int, "device eigensolver: the damping's power iteration also follows free bounds of the generator (the X² GEMM's diagonal stats): skipped when ‖X‖₂ ≤ τ is proven, run when a row of X is longer than τ/2 whatever κ says — 1 in every schedule, 2 in the cold-start schedule only (where an undamped step on a large generator diverged the d = 2000 cold start; in settled solves it costs ≈3 % of a generation), 0 off"),
     "sbr_fused_damping": Knob("EVOXMI_SBR_FUSED_DAMPING", 0, int, "device-controlled eigensolver: the step-size damping (3 power steps + final) as one grid-barrier launch (1) or four launches (0, default: the grid barriers' agent-scope fences cost more than the three launch boundaries they remove — 1.939 vs 1.888 ms/gen, profiles/NOTES.md)"),
     "cec_stack": Knob("EVOXMI_CEC_STACK", 1, int, "CEC'22 compositions (F9–F12) on the device: every rotated component from ONE GEMM over the stacked rotations with per-block exact shifts (1) or one GEMM per component (0)"),
+    "cec_compose_fused": Knob("EVOXMI_CEC_COMPOSE_FUSED", 1, int, "CEC'22 compositions on the device: every component's basic function, the distances and the weighted sum in one kernel after the stacked GEMM (cec2022.hip: cec_compose_kernel) (1) or per-component launches (0)"),
     "cec_fused": Knob("EVOXMI_CEC_FUSED", 0, int, "CEC'22 F1 / F4 on the device: 1 = row terms from the rotation GEMM's epilogue (rotated population never written), 0 = GEMM + basic-function kernel (default: the fused epilogue measured 7 µs slower at pop 10 000 × d 1000, profiles/r3_cec_fused_epilogue.txt)"),
     "gemm_prec": Knob("EVOXMI_GEMM_PREC", "x6", str, "framework f32 GEMMs (gemm_ks.hip): 'x6' — each f32 operand split exactly into three bf16 parts, six bf16 MFMA products (f32-accurate, 3/8 of the f32 MFMA time) — or 'f32' (v_mfma_f32_16x16x4_f32)"),
     "gemm_nw8_tiles": Knob("EVOXMI_GEMM_NW8_TILES", 384, int, "gemm_ks: grids of at most this many 64×64 (or smaller) tiles with K ≥ 3072 run 8-wave workgroups (K split 8 ways, two waves per SIMD: one wave's loads overlap the other's MFMAs; the rank-μ product 55.8 → 47.8 µs); 0 = always 4 waves"),

@@ -375,12 +375,13 @@ class H3Planes:
     h + m (RNE; |x − h − m| ≤ 2⁻²²|x|), stored as f16 [ceil(K/16)][Rp][2][16] 64-byte records
     with the row's inverse scale in ``rinv``.  The product keeps h·h + h·m + m·h (three
     v_mfma_f32_32x32x16_f16 per 32 × 32 block and 16-k block).  On the CPU ``t`` is the f32
-    matrix and ``rinv`` is None."""
+    matrix (``ncomp`` × rows × K when stacked) and ``rinv`` is None.  ``ncomp`` > 1: one plane set
+    per shift row (:func:`h3_planes` with a 2-D ``sub_k``), for :func:`mm_h3` ``sub_cols``."""
 
-    __slots__ = ("t", "rinv", "rows", "K")
+    __slots__ = ("t", "rinv", "rows", "K", "ncomp")
 
-    def __init__(self, t: torch.Tensor, rinv: Optional[torch.Tensor], rows: int, K: int):
-        self.t, self.rinv, self.rows, self.K = t, rinv, int(rows), int(K)
+    def __init__(self, t: torch.Tensor, rinv: Optional[torch.Tensor], rows: int, K: int, ncomp: int = 1):
+        self.t, self.rinv, self.rows, self.K, self.ncomp = t, rinv, int(rows), int(K), int(ncomp)
 
     @property
     def is_cuda(self) -> bool:
@@ -390,18 +391,20 @@ class H3Planes:
 def h3_planes(X: torch.Tensor, sub_k: Optional[torch.Tensor] = None, colscale: Optional[torch.Tensor] = None,
               out: Optional[H3Planes] = None) -> H3Planes:
     """f16x3 planes of ``(X − sub_k[None, :])·diag(colscale)`` (shift and scale fused into the
-    split pass; ``out``: planes of the same shape from an earlier call, overwritten)."""
+    split pass; ``out``: planes of the same shape from an earlier call, overwritten).  A 2-D
+    ``sub_k`` (ncomp × K) gives one plane set per shift row from one read of X."""
     rows, K = X.shape
+    ncomp = sub_k.shape[0] if sub_k is not None and sub_k.dim() == 2 else 1
     if X.is_cuda:
         X_ = X if X.stride(-1) == 1 else X.contiguous()
         t, r = _ext.ops().h3_split(X_, _c(sub_k), _c(colscale), None if out is None else out.t, None if out is None else out.rinv)
-        return H3Planes(t, r, rows, K)
+        return H3Planes(t, r, rows, K, ncomp)
     Y = X.to(torch.float32)
     if sub_k is not None:
-        Y = Y - sub_k[None, :K]
+        Y = Y - (sub_k[None, :K] if sub_k.dim() == 1 else sub_k[:, None, :K])
     if colscale is not None:
         Y = Y * colscale[None, :K]
-    return H3Planes(Y, None, rows, K)
+    return H3Planes(Y, None, rows, K, ncomp)
 
 
 def normal_h3_planes(key: torch.Tensor, rows: int, d: int, row0: int = 0, out: Optional[H3Planes] = None) -> H3Planes:
@@ -418,13 +421,25 @@ def normal_h3_planes(key: torch.Tensor, rows: int, d: int, row0: int = 0, out: O
 
 def mm_h3(A: H3Planes, B: H3Planes, *, alpha: float = 1.0, alpha_ptr: Optional[torch.Tensor] = None,
           bias_n: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
-          skip: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``alpha·(*alpha_ptr)·A·Bᵀ (+ bias_n)`` for f16x3-planes operands (A: M × K, B: N × K)."""
+          skip: Optional[torch.Tensor] = None, sub_cols: int = 0) -> torch.Tensor:
+    """``alpha·(*alpha_ptr)·A·Bᵀ (+ bias_n)`` for f16x3-planes operands (A: M × K, B: N × K).
+    ``sub_cols`` > 0: A is stacked (``A.ncomp`` plane sets) and output columns
+    [c·sub_cols, (c+1)·sub_cols) use set c — e.g. (x − o_c)·M_cᵀ for every component c of a
+    composition function in one launch."""
     if A.K != B.K:
         raise ValueError(f"mm_h3: K mismatch {A.K} vs {B.K}")
+    if sub_cols:
+        if A.ncomp < -(-B.rows // sub_cols):
+            raise ValueError(f"mm_h3: {B.rows} columns in blocks of {sub_cols} need {-(-B.rows // sub_cols)} plane sets, A has {A.ncomp}")
+    elif A.ncomp != 1:
+        raise ValueError("mm_h3: stacked A needs sub_cols")
     if A.is_cuda:
-        return _ext.ops().gemm_h3(A.t, A.rinv, A.rows, B.t, B.rinv, B.rows, A.K, float(alpha), _c(alpha_ptr), _c(bias_n), out, skip)
-    C = alpha * (A.t @ B.t.T)
+        return _ext.ops().gemm_h3(A.t, A.rinv, A.rows, B.t, B.rinv, B.rows, A.K, float(alpha), _c(alpha_ptr), _c(bias_n), out, skip,
+                                  int(sub_cols))
+    if sub_cols:
+        C = alpha * torch.cat([A.t[c] @ B.t[c * sub_cols : (c + 1) * sub_cols].T for c in range(-(-B.rows // sub_cols))], 1)
+    else:
+        C = alpha * (A.t @ B.t.T)
     if alpha_ptr is not None:
         C = C * alpha_ptr.reshape(())
     if bias_n is not None:

@@ -180,6 +180,30 @@ def normal(key, shape=(), dtype=torch.float32, offset: int = 0) -> torch.Tensor:
     return z.reshape(-1)[:n].reshape(shape).to(dtype)
 
 
+def _window(key, rows, dtot, col0, own, row0, device, dist):
+    dev = torch.device(device) if device is not None else key.device
+    if dev.type == "cuda":
+        return _ext().ops().philox_window(key.to(dev).contiguous(), int(rows), int(dtot), int(col0), int(own), int(row0), int(dist))
+    fn = normal if dist else uniform
+    if own == dtot and col0 == 0:
+        return fn(key, (rows, dtot), offset=row0 * dtot).to(dev)
+    if not rows:
+        return torch.zeros(0, own, device=dev)
+    return torch.stack([fn(key, (own,), offset=(row0 + r) * dtot + col0) for r in range(rows)]).to(dev)
+
+
+def normal_window(key, rows: int, dtot: int, col0: int, own: int, row0: int = 0, device=None) -> torch.Tensor:
+    """Columns [col0, col0 + own) of rows [row0, row0 + rows) of ``normal(key, (·, dtot))`` —
+    the block a decision-axis-sharded rank owns, bitwise equal to slicing the full matrix.  On a
+    GPU one kernel draws only the block (rng.hip: philox_window_kernel)."""
+    return _window(key, rows, dtot, col0, own, row0, device, 1)
+
+
+def uniform_window(key, rows: int, dtot: int, col0: int, own: int, row0: int = 0, device=None) -> torch.Tensor:
+    """The same column window of ``uniform(key, (·, dtot))``."""
+    return _window(key, rows, dtot, col0, own, row0, device, 0)
+
+
 def randint(key, shape, minval: int, maxval: int, dtype=torch.int64) -> torch.Tensor:
     """Integers in ``[minval, maxval)`` (reference ``jax.random.randint``)."""
     shape = _as_shape(shape)

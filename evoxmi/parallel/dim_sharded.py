@@ -165,6 +165,39 @@ class ColumnSeparable:
         c0, own, _ = self.cols()
         return v[..., c0 : c0 + own]
 
+    def normal_cols(self, key, rows: int, device, row0: int = 0):
+        """This rank's columns of rows [row0, row0 + rows) of ``normal(key, (·, dim))`` — the
+        full matrix when the state is not sharded (every split draws the same numbers)."""
+        from ..ops import random as rnd
+
+        c0, own, d = self.cols()
+        if own == d and torch.device(device).type != "cuda":
+            return rnd.normal(key, (rows, d), offset=row0 * d).to(device)
+        # on a GPU every split (one rank included) draws through the same window kernel: bitwise
+        # equal blocks for any world size
+        return rnd.normal_window(key, rows, d, c0, own, row0, device)
+
+    def uniform_cols(self, key, rows: int, device, row0: int = 0):
+        """This rank's columns of ``uniform(key, (rows, dim))`` (see :meth:`normal_cols`)."""
+        from ..ops import random as rnd
+
+        c0, own, d = self.cols()
+        if own == d and torch.device(device).type != "cuda":
+            return rnd.uniform(key, (rows, d), offset=row0 * d).to(device)
+        # on a GPU every split (one rank included) draws through the same window kernel: bitwise
+        # equal blocks for any world size
+        return rnd.uniform_window(key, rows, d, c0, own, row0, device)
+
+    def col_sum(self, x: torch.Tensor) -> torch.Tensor:
+        """``x`` summed over the ranks of the decision-axis shard group (identity when the state
+        is not sharded): the per-column partial of a reduction over all decision variables,
+        e.g. ‖p_σ‖² — GSPMD inserts the same all-reduce for a sum over a sharded axis."""
+        if self._cols is None or self._cols[1] == self._cols[2] or not (dist.is_available() and dist.is_initialized()):
+            return x
+        x = x.contiguous().clone()
+        dist.all_reduce(x, group=getattr(self, "_dim_group", None))
+        return x
+
     def dim_gather(self, state, group=None):
         """The state with every ``dim_fields`` array reassembled to full width on every rank
         (one all-gather per field; for checkpoints, monitors and final results)."""

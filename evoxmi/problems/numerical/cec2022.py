@@ -554,7 +554,16 @@ class _Composition(_CEC2022):
             slot = {i: comps.index(comp) for i, (fid, comp, scale, rotate) in enumerate(self.parts) if rotate}
             st = self._cache[key] = (Ms, Osh, slot)
         Ms, Osh, slot = st
-        Z = linalg.mm_nt(X, Ms, a_sub_k=Osh, sub_cols=self.STACK)
+        if linalg.tall_nt_ok(X.shape[0], Ms.shape[0], D, X.device):
+            # f16x3 LDS-staged GEMM: X read once into one (x − o_c) plane set per component,
+            # the stacked rotations split once (cached), one launch over every component
+            bkey = ("stack_h3", D, str(X.device))
+            Bp = self._cache.get(bkey)
+            if Bp is None:
+                Bp = self._cache[bkey] = linalg.h3_planes(Ms)
+            Z = linalg.mm_h3(linalg.h3_planes(X, sub_k=Osh), Bp, sub_cols=self.STACK)
+        else:
+            Z = linalg.mm_nt(X, Ms, a_sub_k=Osh, sub_cols=self.STACK)
         return Z, slot
 
     def _evaluate(self, X, c):
@@ -563,6 +572,16 @@ class _Composition(_CEC2022):
         M = c["M"]
         fs = []
         stacked = self._stacked(X, c)
+        from ... import config
+
+        if stacked is not None and config.get("cec_compose_fused"):
+            # every component's basic function, distances and the weighted sum in one kernel
+            Z, slot = stacked
+            p = self.parts
+            return _ext.ops().cec_compose(
+                Z, X, c["Os"], [fid for fid, _, _, _ in p], [slot[i] * self.STACK if rot else -1 for i, (_, _, _, rot) in enumerate(p)],
+                [comp for _, comp, _, _ in p], [float(sc) for _, _, sc, _ in p], [float(v) for v in self.sigma],
+                [float(v) for v in self.lamb], [float(v) for v in self.bias], float(self._thr(D)))
         for i, (fid, comp, scale, rotate) in enumerate(self.parts):
             o = Os[comp]
             if rotate and stacked is not None:

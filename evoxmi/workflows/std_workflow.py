@@ -127,12 +127,20 @@ class StdWorkflow(Workflow):
 
     def _evaluate(self, state, transformed):
         if self._dim_shard_group is not None:
-            from ..parallel.dim_sharded import dim_sharded_fitness, dim_sharded_fitness_local
+            from ..parallel.dim_sharded import _gather_cols, dim_sharded_fitness, dim_sharded_fitness_local, supports_dim_sharding
 
+            if not torch.is_tensor(transformed):
+                raise TypeError("decision-axis sharding evaluates a (pop, dim) tensor; got " + type(transformed).__name__)
+            grp = self._dim_shard_group[0]
+            if not supports_dim_sharding(self.problem):
+                # no partial terms: the problem evaluates the replicated full rows through its own
+                # state (Brax / EnvPool keys, episode counters advance identically on every rank)
+                X = _gather_cols(transformed, self._dim_shard_group[2], grp) if len(self._dim_shard_group) > 1 else transformed
+                return use_state(self.problem.evaluate)(state, X)
             if len(self._dim_shard_group) > 1:  # state-sharded: `transformed` is this rank's column block
                 _, col0, d = self._dim_shard_group
-                return dim_sharded_fitness_local(self.problem, transformed, col0, d, self._dim_shard_group[0]), state
-            return dim_sharded_fitness(self.problem, transformed, self._dim_shard_group[0]), state
+                return dim_sharded_fitness_local(self.problem, transformed, col0, d, grp), state
+            return dim_sharded_fitness(self.problem, transformed, grp), state
         if self.jit_problem:
             return use_state(self.problem.evaluate)(state, transformed)
         fitness, state = use_state(self.problem.evaluate)(state, transformed)
@@ -491,6 +499,11 @@ class StdWorkflow(Workflow):
                           "(partial_terms / combine_terms / dim_halo); sharding the population instead "
                           "(shard_state=True keeps the decision axis sharded and all-gathers the rows to evaluate)")
             return self.enable_distributed(state)
+        if shard_state and self.sol_transforms:
+            # a solution transform maps whole decision vectors; under state sharding it would see
+            # this rank's column block
+            raise ValueError("enable_multi_devices(shard_state=True): sol_transforms act on whole decision vectors; "
+                             "use shard_state=False (the population stays replicated) or enable_distributed")
         ctx = DistContext(group=devices if isinstance(devices, torch.distributed.ProcessGroup) else None)
         state = ctx.broadcast_state(state)
         if shard_state:
@@ -502,6 +515,7 @@ class StdWorkflow(Workflow):
             col0, own = balanced_slices(d, world)[rank]
             alg = state.get_child_state("algorithm")
             state = state.update_child("algorithm", self.algorithm.dim_shard(alg, col0, own))
+            self.algorithm._dim_group = ctx.group
             self._dim_shard_group = (ctx.group, col0, d)
         else:
             self._dim_shard_group = (ctx.group,)

@@ -70,6 +70,8 @@ def test_enable_multi_devices_gloo_matches_single_process():
     for _ in range(20):
         st = wf.step(st)
     ref = st.get_child_state("algorithm")
+    if st.has_child("problem") and "count" in st.get_child_state("problem").keys():
+        ref = {**{k: ref[k] for k in ref.keys()}, "problem_count": st.get_child_state("problem")["count"]}
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
@@ -117,6 +119,8 @@ def test_state_sharded_de_gloo_matches_single_process(world, cls):
     for _ in range(15):
         st = wf.step(st)
     ref = st.get_child_state("algorithm")
+    if st.has_child("problem") and "count" in st.get_child_state("problem").keys():
+        ref = {**{k: ref[k] for k in ref.keys()}, "problem_count": st.get_child_state("problem")["count"]}
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_de_worker, args=(world, _free_port(), out, cls), nprocs=world, join=True)
@@ -156,6 +160,8 @@ def test_state_sharded_pso_gloo_matches_single_process(world):
     for _ in range(20):
         st = wf.step(st)
     ref = st.get_child_state("algorithm")
+    if st.has_child("problem") and "count" in st.get_child_state("problem").keys():
+        ref = {**{k: ref[k] for k in ref.keys()}, "problem_count": st.get_child_state("problem")["count"]}
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_worker, args=(world, _free_port(), out, True), nprocs=world, join=True)
@@ -263,6 +269,21 @@ def _make_coupled():
     return Coupled()
 
 
+def _make_counting():
+    """A stateful problem without partial terms: its state counts evaluations and its fitness
+    depends on that count (state must be threaded through the decision-axis evaluation)."""
+    from evoxmi.core import Problem, State
+
+    class Counting(Problem):
+        def setup(self, key):
+            return State(count=torch.zeros((), dtype=torch.int64))
+
+        def evaluate(self, state, X):
+            return (X * X).sum(1) + 0.01 * state.count.to(X.dtype), state.update(count=state.count + 1)
+
+    return Counting()
+
+
 def _generic_worker(rank, world, port, out, algo):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     torch.set_num_threads(1)
@@ -275,7 +296,9 @@ def _generic_worker(rank, world, port, out, algo):
     for _ in range(8):
         st = wf.step(st)
     full = wf.gather_state(st).get_child_state("algorithm")
-    out[rank] = {k: full[k].clone() for k in ("population", "center", "fitness") if k in full.keys()}
+    out[rank] = {k: full[k].clone() for k in ("population", "center", "mean", "sigma", "stdev", "C", "velocity", "pbest_position", "fitness") if k in full.keys()}
+    if st.has_child("problem") and "count" in st.get_child_state("problem").keys():
+        out[rank] = {**out[rank], "problem_count": st.get_child_state("problem")["count"].clone()}
     destroy()
 
 
@@ -284,37 +307,66 @@ def _make_generic(algo):
     from evoxmi.problems.numerical import Sphere
 
     d = 24
-    if algo in ("nsga2", "nsga3", "ibea", "hype"):
+    if algo in ("nsga2", "nsga3", "ibea", "hype", "rvea", "spea2", "tdea"):
         from evoxmi.problems.numerical import DTLZ2
 
-        cls = {"nsga2": A.NSGA2, "nsga3": A.NSGA3, "ibea": A.IBEA, "hype": A.HypE}[algo]
+        cls = {"nsga2": A.NSGA2, "nsga3": A.NSGA3, "ibea": A.IBEA, "hype": A.HypE, "rvea": A.RVEA, "spea2": A.SPEA2, "tdea": A.TDEA}[algo]
         kw = {"n_sample": 500} if algo == "hype" else {}
         return StdWorkflow(cls(torch.zeros(d), torch.ones(d), 3, 32, **kw), DTLZ2(d=d, m=3))
+    lb, ub = torch.full((d,), -5.0), torch.full((d,), 5.0)
     if algo == "de":
-        return StdWorkflow(A.DE(torch.full((d,), -5.0), torch.full((d,), 5.0), 32), _make_coupled())
+        return StdWorkflow(A.DE(lb, ub, 32), _make_coupled())
+    if algo in ("jade", "shade", "lshade", "jso"):
+        cls = {"jade": A.JaDE, "shade": A.SHADE, "lshade": A.LSHADE, "jso": A.JSO}[algo]
+        return StdWorkflow(cls(lb, ub, 32), _make_coupled())
+    if algo == "cso":
+        return StdWorkflow(A.CSO(lb, ub, 32, phi=0.1), _make_coupled())
+    if algo == "clpso":
+        return StdWorkflow(A.CLPSO(lb, ub, 32, 0.5, 1.5, 0.3), _make_coupled())
+    if algo in ("pgpe", "pgpe_adam"):
+        return StdWorkflow(A.PGPE(32, torch.full((d,), 2.0), "clipup" if algo == "pgpe" else "adam"), Sphere())
+    if algo == "ars":
+        return StdWorkflow(A.ARS(32, torch.full((d,), 2.0)), Sphere())
+    if algo == "des":
+        return StdWorkflow(A.DES(32, torch.full((d,), 2.0)), Sphere())
+    if algo == "snes":
+        return StdWorkflow(A.SNES(32, torch.full((d,), 2.0), sigma=0.5), Sphere())
+    if algo == "sepcmaes":
+        return StdWorkflow(A.SepCMAES(torch.full((d,), 2.0), 0.5, pop_size=32), _make_coupled())
+    if algo == "openes_stateful":
+        return StdWorkflow(A.OpenES(torch.full((d,), 2.0), 32, 0.05, 0.1), _make_counting())
     opt = "adam" if algo == "openes_adam" else None
     return StdWorkflow(A.OpenES(torch.full((d,), 2.0), 32, 0.05, 0.1, optimizer=opt), Sphere())
 
 
-@pytest.mark.parametrize("algo", ["de", "openes", "openes_adam", "nsga2", "nsga3", "ibea", "hype"])
-def test_state_sharded_generic_gloo_matches_single_process(algo):
-    """Generic decision-axis state sharding: DE on a problem without partial terms (rows
-    all-gathered for the evaluation), OpenES (SGD and Adam: centre, population and the
-    optimiser's moments as column blocks) on Sphere's terms, the SBX + PM MOEAs (operators
-    drawn per global column, selection from the replicated objectives) on DTLZ2's terms —
-    world 3 reproduces one process."""
+@pytest.mark.parametrize("algo", ["de", "jade", "shade", "lshade", "jso", "openes", "openes_adam", "openes_stateful", "snes",
+                                  "pgpe", "pgpe_adam", "ars", "des", "cso", "clpso", "sepcmaes", "nsga2",
+                                  "nsga3", "ibea", "hype", "rvea", "spea2", "tdea"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_state_sharded_generic_gloo_matches_single_process(algo, world):
+    """Generic decision-axis state sharding: the DE family (JaDE / SHADE / L-SHADE / jSO:
+    trials drawn per global column, the archive as column blocks) on a problem without partial
+    terms (rows all-gathered for the evaluation), OpenES (SGD and Adam: centre, population and
+    the optimiser's moments as column blocks), SNES, PGPE (ClipUp's norms all-reduced), ARS and
+    DES on Sphere's terms, CSO / CLPSO (coefficients drawn per global column), Sep-CMA-ES (‖p_σ‖
+    all-reduced), the SBX + PM MOEAs (operators drawn per global column, selection from the
+    replicated objectives) on DTLZ2's terms (whose state carries a key), and a stateful problem
+    without terms (its state advances through the all-gathered evaluation) — worlds 2 and 3
+    reproduce one process."""
     wf = _make_generic(algo)
     st = wf.init(rnd.PRNGKey(5))
     for _ in range(8):
         st = wf.step(st)
     ref = st.get_child_state("algorithm")
+    if st.has_child("problem") and "count" in st.get_child_state("problem").keys():
+        ref = {**{k: ref[k] for k in ref.keys()}, "problem_count": st.get_child_state("problem")["count"]}
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_generic_worker, args=(3, _free_port(), out, algo), nprocs=3, join=True)
+    mp.spawn(_generic_worker, args=(world, _free_port(), out, algo), nprocs=world, join=True)
+    assert set(out[0].keys()) <= set(ref.keys())
     for k, v in out[0].items():
-        assert torch.allclose(v, ref[k], rtol=1e-4, atol=1e-4), k
-        assert all(torch.equal(out[r][k], v) for r in range(3))
-
+        assert torch.allclose(v.double(), ref[k].double(), rtol=1e-4, atol=1e-4, equal_nan=True), k
+        assert all(torch.equal(out[r][k].nan_to_num(1e30), v.nan_to_num(1e30)) for r in range(world))
 
 
 def test_mo_column_sharding_rejects_operators_without_column_blocks():
@@ -364,3 +416,21 @@ def test_maf_partial_terms_reproduce_full_evaluation(name, world):
     for col0, own in balanced_slices(d, min(world, d)):
         T = T + p.partial_terms(X[:, col0 : col0 + own], col0, d, own)
     torch.testing.assert_close(p.combine_terms(T, d), full, rtol=1e-10, atol=1e-10)
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+@pytest.mark.parametrize("rows,d,c0,own,row0", [(37, 1000, 0, 334, 0), (37, 1000, 334, 333, 5), (64, 24, 8, 8, 3), (9, 30, 7, 11, 2),
+                                                (5, 7, 3, 1, 0)])
+def test_philox_windows_equal_full_matrix_columns(device, rows, d, c0, own, row0):
+    """normal_window / uniform_window (GPU: rng.hip philox_window_kernel, 4-aligned and ragged
+    windows) are bitwise the columns of the full matrix drawn at the same row offset."""
+    key = rnd.PRNGKey(17, device=device)
+    for win, full in ((rnd.normal_window, rnd.normal), (rnd.uniform_window, rnd.uniform)):
+        F = full(key, (rows, d), offset=row0 * d)
+        W = win(key, rows, d, c0, own, row0, device)
+        assert W.shape == (rows, own) and W.device.type == device
+        if device == "cuda" and rows * d < 4096 and win is rnd.normal_window:
+            # small GPU draws of rnd.normal take the torch Box–Muller (its own sin / cos): ulps
+            assert torch.allclose(W, F[:, c0 : c0 + own], rtol=1e-6, atol=1e-6)
+        else:
+            assert torch.equal(W, F[:, c0 : c0 + own]), (win.__name__, float((W - F[:, c0 : c0 + own]).abs().max()))

@@ -121,3 +121,30 @@ def test_h3_row_scaling_keeps_relative_accuracy():
     R = A @ Bm.double().t()
     tol = 2e-6 * (A.abs() @ Bm.double().abs().t()) + 1e-300
     assert ((C - R).abs() <= tol).all(), float(((C - R).abs() / tol).max())
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+@pytest.mark.parametrize("M,K,ncomp,sub", [(700, 1000, 5, 1024), (333, 200, 3, 256), (64, 37, 2, 128), (1000, 1200, 2, 1280)])
+def test_h3_stacked_components_match_fp64(device, M, K, ncomp, sub):
+    """Stacked operands: one split of X into ncomp plane sets (x − o_c), one launch whose column
+    block c uses set c — the composition functions' (x − o_c)·M_cᵀ for every component (K > 1024
+    takes the per-component split passes)."""
+    g = torch.Generator().manual_seed(M + K + ncomp)
+    X = torch.randn(M, K, generator=g) * 50
+    O = torch.randn(ncomp, K, generator=g) * 50
+    Ms = torch.zeros(ncomp * sub, K)
+    for c in range(ncomp):
+        Ms[c * sub : c * sub + min(sub, K)] = torch.randn(min(sub, K), K, generator=g)
+    Ap = linalg.h3_planes(X.to(device), sub_k=O.to(device))
+    assert Ap.ncomp == ncomp
+    C = linalg.mm_h3(Ap, linalg.h3_planes(Ms.to(device)), sub_cols=sub).cpu().double()
+    assert C.shape == (M, ncomp * sub)
+    for c in range(ncomp):
+        A = (X - O[c]).double()
+        Bc = Ms[c * sub : (c + 1) * sub].double()
+        R = A @ Bc.t()
+        tol = 2e-6 * (A.abs() @ Bc.abs().t()) + 1e-30
+        err = (C[:, c * sub : (c + 1) * sub] - R).abs()
+        assert (err <= tol).all(), (c, float((err / tol).max()))
+    with pytest.raises(ValueError):
+        linalg.mm_h3(Ap, linalg.h3_planes(Ms.to(device)))

@@ -141,6 +141,30 @@ def test_cec2022_gpu_matches_cpu(f, D):
     assert torch.allclose(out.cpu(), ref, rtol=2e-3, atol=1e-3), (f, D, out[:3], ref[:3])
 
 
+@pytest.mark.parametrize("f", [9, 10, 11, 12])
+def test_cec2022_compositions_d1000_fused_path(f):
+    """d = 1000 at a population that takes the stacked f16x3 GEMM (one split of X into every
+    component's x − o_c planes) and the one-pass composition kernel: equal to the CPU
+    evaluation and to the per-component device path; rows at / near a component's optimum
+    exercise the zero-distance selection and the weights."""
+    from evoxmi import config
+    from evoxmi.problems.numerical import CEC2022TestSuit
+
+    p = CEC2022TestSuit.create(f)
+    g = torch.Generator().manual_seed(f)
+    X = torch.rand(2048, 1000, generator=g) * 200 - 100
+    Os = p._consts(1000, torch.device("cpu"))["Os"]
+    X[0] = Os[0, :1000]
+    X[1] = Os[1, :1000] + 1e-3 * torch.randn(1000, generator=g)
+    X[2] = Os[0, :1000] + 1.0
+    ref, _ = p.evaluate(None, X)
+    out, _ = p.evaluate(None, X.cuda())
+    with config.override(cec_compose_fused=0):
+        unfused, _ = p.evaluate(None, X.cuda())
+    assert torch.allclose(out.cpu(), ref, rtol=2e-3, atol=1e-3), (f, out[:3], ref[:3])
+    assert torch.allclose(out.cpu(), unfused.cpu(), rtol=1e-4, atol=1e-4)
+
+
 def test_pso_kernel_matches_cpu():
     from evoxmi.ops.pso import pso_update
 
