@@ -257,6 +257,9 @@ at::Tensor gemm_ks(const at::Tensor& A, int64_t a_kc, const at::Tensor& B, int64
     a.stat_diag_only = (int)stat_diag_only;
   }
   a.c_vec4 = vec4_ok(C) ? 1 : 0;
+  // the partials' length (gemm_ks_grid) assumed the square-product kernel for this shape
+  TORCH_CHECK(!a.stat_part || !evx_gemm_ks_sq_shape((int)M, (int)N, (int)mode) || evx_gemm_ks_routes_sq(a),
+              "gemm_ks: stats partials of a square product need 16-byte aligned operands (gemm_sq)");
   evx_gemm_ks(a, cur_stream());
   return C;
 }
@@ -373,6 +376,7 @@ at::Tensor philox_normal_planes(const at::Tensor& key, int64_t rows, int64_t d, 
 void gemm_ks_set_tile(int64_t t) { evx_gemm_ks_set_tile((int)t); }
 void gemm_ks_set_prec(int64_t p) { evx_gemm_ks_set_prec((int)p); }
 void gemm_ks_set_nw8(int64_t t) { evx_gemm_ks_set_nw8((int)t); }
+void gemm_sq_enable(int64_t on) { evx_gemm_sq_enable((int)on); }
 
 at::Tensor gemm_ks_new(const at::Tensor& A, int64_t a_kc, const at::Tensor& B, int64_t b_kc, int64_t M, int64_t N, int64_t K,
                        int64_t mode, double alpha, const c10::optional<at::Tensor>& alpha_ptr,
@@ -518,7 +522,8 @@ void sbr_damping_out(const at::Tensor& X2, const at::Tensor& V, double tau, at::
 }
 
 void sbr_dev_prep(const at::Tensor& X, const at::Tensor& X2, const at::Tensor& X3, at::Tensor& alpha, at::Tensor& P, at::Tensor& MT,
-                  const at::Tensor& ctrl, const c10::optional<at::Tensor>& work, double tau, const c10::optional<at::Tensor>& xpart) {
+                  const at::Tensor& ctrl, const c10::optional<at::Tensor>& work, double tau, const c10::optional<at::Tensor>& xpart,
+                  const c10::optional<at::Tensor>& copy_src, const c10::optional<at::Tensor>& copy_dst) {
   for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&X, &X2, &X3, &P, &MT}) {
     CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t);
     TORCH_CHECK(t->sizes() == X.sizes(), "sbr_dev_prep: n×n");
@@ -535,8 +540,20 @@ void sbr_dev_prep(const at::Tensor& X, const at::Tensor& X2, const at::Tensor& X
   }
   int64_t np = 0;
   const double* xp = xpart_ptr(xpart, np);
+  // near-only iterations' basis copy (copy_src → copy_dst when ctrl[1] && !ctrl[7])
+  const float* cs = nullptr;
+  float* cd = nullptr;
+  if (copy_src.has_value() && copy_src->defined()) {
+    TORCH_CHECK(copy_dst.has_value() && copy_dst->defined(), "sbr_dev_prep: copy_src with copy_dst");
+    for (const at::Tensor* t : {&*copy_src, &*copy_dst}) {
+      CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t);
+      TORCH_CHECK(t->sizes() == X.sizes() && reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "sbr_dev_prep: copy n×n, 16-B aligned");
+    }
+    cs = copy_src->data_ptr<float>();
+    cd = copy_dst->data_ptr<float>();
+  }
   evx_sbr_dev_prep(X.data_ptr<float>(), X2.data_ptr<float>(), X3.data_ptr<float>(), (int)X.size(0), alpha.data_ptr<float>(),
-                   P.data_ptr<float>(), MT.data_ptr<float>(), ctrl.data_ptr<int>(), cur_stream(), v2, v3, (float)tau, xp, (int)np);
+                   P.data_ptr<float>(), MT.data_ptr<float>(), ctrl.data_ptr<int>(), cur_stream(), v2, v3, (float)tau, xp, (int)np, cs, cd);
 }
 
 void sbr_dev_copy(const at::Tensor& src, at::Tensor& dst, const at::Tensor& skip) {
@@ -670,6 +687,7 @@ at::Tensor cec_compose(const c10::optional<at::Tensor>& Z, const at::Tensor& X, 
                   (int64_t)lamb.size() == n && (int64_t)bias.size() == n,
               "cec_compose: one entry per part");
   TORCH_CHECK(Os.dim() == 2 && Os.stride(1) == 1 && Os.size(0) >= n && Os.size(1) >= D, "cec_compose: Os (>= parts) x D");
+  TORCH_CHECK(D >= 2, "cec_compose: D >= 2");
   EvxCecCompose c{};
   c.n = (int)n;
   const float* zp = nullptr;
@@ -1538,12 +1556,13 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("sbr16_far_out(Tensor A, Tensor perm, Tensor Q, Tensor dq, Tensor stats, float thr_fac, Tensor theta, Tensor(a!) X, int sb, Tensor skip) -> ()");
   m.def("sbr16_bq_out(Tensor B, Tensor perm, Tensor Q, Tensor(a!) Bq, int sb, Tensor skip) -> ()");
   m.def("sbr_damping_out(Tensor X2, Tensor V, float tau, Tensor(a!) alpha, Tensor(b!) work, Tensor skip, Tensor(c!)? bar=None, bool no_final=False, Tensor? xpart=None) -> ()");
-  m.def("sbr_dev_prep(Tensor X, Tensor X2, Tensor X3, Tensor(c!) alpha, Tensor(a!) P, Tensor(b!) MT, Tensor ctrl, Tensor? work=None, float tau=1.0, Tensor? xpart=None) -> ()");
+  m.def("sbr_dev_prep(Tensor X, Tensor X2, Tensor X3, Tensor(c!) alpha, Tensor(a!) P, Tensor(b!) MT, Tensor ctrl, Tensor? work=None, float tau=1.0, Tensor? xpart=None, Tensor? copy_src=None, Tensor(d!)? copy_dst=None) -> ()");
   m.def("sbr_dev_copy(Tensor src, Tensor(a!) dst, Tensor skip) -> ()");
   m.def("sbr_dev_ctrl(Tensor part, int nparts, int j, int K, Tensor(a!) hist, Tensor(b!) alpha, Tensor(c!) theta, Tensor(d!) ctrl, Tensor(e!) st, float[] prm, int ns_iters, Tensor A, Tensor(f!) w_out, Tensor(g!) eig_stats, Tensor(h!) w_init, Tensor(i!) log, Tensor(j!) log_count) -> ()");
   m.def("gemm_ks_set_tile(int t) -> ()");
   m.def("gemm_ks_set_prec(int prec) -> ()");
   m.def("gemm_ks_set_nw8(int tiles) -> ()");
+  m.def("gemm_sq_enable(int on) -> ()");
   m.def("gemm_ks_pl(Tensor? A, Tensor? a_pl, Tensor? B, Tensor? b_pl, int M, int N, int K, float alpha, Tensor? alpha_ptr, Tensor? bias_n, Tensor(a!)? out, Tensor? a_sub_k, int sub_cols=0, int sub_ld=0) -> Tensor");
   m.def("split_planes(Tensor X, Tensor? colscale) -> Tensor");
   m.def("philox_normal_planes(Tensor key, int rows, int d, int row0) -> Tensor");
@@ -1589,6 +1608,7 @@ TORCH_LIBRARY_IMPL(evoxmi, CompositeExplicitAutograd, m) {
   m.impl("gemm_ks_set_tile", &gemm_ks_set_tile);
   m.impl("gemm_ks_set_prec", &gemm_ks_set_prec);
   m.impl("gemm_ks_set_nw8", &gemm_ks_set_nw8);
+  m.impl("gemm_sq_enable", &gemm_sq_enable);
   m.impl("gemm_ks_pl", &gemm_ks_pl);
   m.impl("split_planes", &split_planes);
   m.impl("philox_normal_planes", &philox_normal_planes);

@@ -144,6 +144,14 @@ struct EvxCecCompose {
 void evx_cec_compose(const float* Z, int64_t ldz, const float* X, int64_t ldx, int N, int D, const EvxCecCompose& c, float* out,
                      hipStream_t s);
 int evx_gemm_ks_grid(int M, int N, int mode);  // workgroups of a launch (stat_part length)
+// LDS-staged bf16x6 kernel for square products (gemm_sq.hip), routed to by evx_gemm_ks
+bool evx_gemm_sq_shape(int M, int N, int mode);
+void evx_gemm_sq_enable(int on);
+int evx_gemm_sq_grid(int M, int N, int mode);
+bool evx_gemm_sq_ok(const EvxGemmKs& a);
+void evx_gemm_sq(const EvxGemmKs& a, hipStream_t s);
+bool evx_gemm_ks_routes_sq(const EvxGemmKs& a);
+bool evx_gemm_ks_sq_shape(int M, int N, int mode);  // a bf16x6 product of this shape goes to gemm_sq
 int evx_gemm_ks_tile(int M, int N, int mode);
 void evx_gemm_ks_set_tile(int t);
 // 1: bf16x6 split products on the bf16 matrix pipe (default), 0: f32 MFMA
@@ -272,7 +280,7 @@ void evx_linear_gp_fit(const double* a, const double* b, const double* c, const 
 // device-controlled SBR schedule (eigh_sbr_dev.hip)
 void evx_sbr_dev_prep(const float* X, const float* X2, const float* X3, int n, float* alpha, float* P, float* MT, const int* ctrl,
                       hipStream_t s, const float* V2 = nullptr, const float* V3 = nullptr,
-                      float tau = 1.f, const double* xpart = nullptr, int nparts = 0);
+                      float tau = 1.f, const double* xpart = nullptr, int nparts = 0, const float* copy_src = nullptr, float* copy_dst = nullptr);
 void evx_sbr_dev_copy(const float* src, float* dst, int64_t n, const int* skip, hipStream_t s);
 void evx_sbr_report(const double* stats, int* seq, double* ring, int R, hipStream_t s);
 void evx_sbr_dev_ctrl(const double* part, int nparts, int j, int K, double* hist, float* alpha, float* theta, int* ctrl, int* st,

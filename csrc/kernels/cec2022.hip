@@ -110,7 +110,8 @@ __device__ __forceinline__ float basic_row(const RowView& z, int fid, int L, int
       }
       break;
     case ELLIPTIC:
-      for (int j = lane; j < L; j += 64) { float v = z(j); a += powf(10.f, 6.f * (float)j / (fL - 1.f)) * v * v; }
+      // 10^(6j/(L−1)) as exp2 (powf's special-case handling is most of the loop's instructions)
+      for (int j = lane; j < L; j += 64) { float v = z(j); a += exp2f(6.f * (float)j / (fL - 1.f) * 3.3219280948873623f) * v * v; }
       break;
     case DISCUS:
       for (int j = lane; j < L; j += 64) { float v = z(j); a += (j == 0 ? 1e6f : 1.f) * v * v; }
@@ -172,60 +173,61 @@ __global__ void __launch_bounds__(256) cec_basic_kernel(const float* __restrict_
 
 // Composition functions (F9–F12) in one pass: wave per row computes every component's basic
 // function — from its block of the stacked rotation GEMM output (zcol ≥ 0) or from x − o
-// (zcol < 0) — and every ‖x − o_i‖² from one read of the x row, then the weighted sum
-// f = Σ w̃_i (λ_i f_i + bias_i) with w_i = exp(−d_i²/(2 D σ_i²)) / d_i (a zero distance selects its
-// component(s)), and the f < thr → 0 clamp.  Replaces 2n + ~15 launches per evaluation.
-__global__ void __launch_bounds__(256) cec_compose_kernel(const float* __restrict__ Z, int64_t ldz, const float* __restrict__ X,
-                                                          int64_t ldx, int N, int D, EvxCecCompose c, float* __restrict__ out) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (row >= N) return;
+// (zcol < 0) — and every ‖x − o_i‖² from one read of the x row (held in registers), then the
+// weighted sum f = Σ w̃_i (λ_i f_i + bias_i) with w_i = exp(−d_i²/(2 D σ_i²)) / d_i (a zero
+// distance selects its component(s)), and the f < thr → 0 clamp.  Replaces 2n + ~15 launches
+// per evaluation.  The part loop is NOT unrolled (one copy of the basic-function switch: the
+// unrolled form spilled and thrashed the instruction cache); per-part results go through LDS.
+constexpr int kComposeRows = 4;  // rows (waves) per workgroup
+__global__ void __launch_bounds__(64 * kComposeRows) cec_compose_kernel(const float* __restrict__ Z, int64_t ldz,
+                                                                        const float* __restrict__ X, int64_t ldx, int N, int D,
+                                                                        EvxCecCompose c, float* __restrict__ out) {
+  __shared__ float s_d2[kComposeRows][kEvxCecMaxParts], s_g[kComposeRows][kEvxCecMaxParts];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int row = blockIdx.x * kComposeRows + w;
+  if (row >= N) return;  // whole waves: no barrier below
   const float* xrow = X + (int64_t)row * ldx;
-  float d2[kEvxCecMaxParts];
-#pragma unroll
-  for (int i = 0; i < kEvxCecMaxParts; ++i) d2[i] = 0.f;
-  for (int j = lane; j < D; j += 64) {
-    const float x = xrow[j];
-#pragma unroll
-    for (int i = 0; i < kEvxCecMaxParts; ++i)
-      if (i < c.n) {
-        const float t = x - c.os[(int64_t)i * c.ldo + j];
-        d2[i] += t * t;
-      }
+#pragma unroll 1
+  for (int i = 0; i < c.n; ++i) {
+    // ‖x − o_i‖²: the x row re-read per part stays in L1 (a register copy of it halved the
+    // occupancy: 97 VGPRs, 4 waves per SIMD, for a latency-bound row loop)
+    const float* o = c.os + (int64_t)i * c.ldo;
+    float a = 0.f;
+    for (int j = lane; j < D; j += 64) {
+      const float t = xrow[j] - o[j];
+      a = fmaf(t, t, a);
+    }
+    a = evx::wave_sum(a);
+    const bool rot = c.zcol[i] >= 0;
+    RowView z{rot ? Z + (int64_t)row * ldz + c.zcol[i] : xrow, nullptr, rot ? nullptr : c.os + (int64_t)c.comp[i] * c.ldo, 0,
+              c.scale[i]};
+    const float f = basic_row(z, c.fid[i], D, lane, nullptr, nullptr, nullptr, 0);
+    if (lane == 0) {
+      s_d2[w][i] = a;
+      s_g[w][i] = c.lamb[i] * f + c.bias[i];
+    }
   }
-  float fsum = 0.f, wsum = 0.f, zsum = 0.f;
+  if (lane != 0) return;  // lane 0 wrote every part's results itself
+  float wsum = 0.f, zsum = 0.f, fsum = 0.f;
   int nzero = 0;
-  float w[kEvxCecMaxParts], g[kEvxCecMaxParts];
-#pragma unroll
-  for (int i = 0; i < kEvxCecMaxParts; ++i) {
-    w[i] = 0.f;
-    g[i] = 0.f;
-    if (i < c.n) {
-      d2[i] = evx::wave_sum(d2[i]);
-      const bool rot = c.zcol[i] >= 0;
-      RowView z{rot ? Z + (int64_t)row * ldz + c.zcol[i] : xrow, nullptr, rot ? nullptr : c.os + (int64_t)c.comp[i] * c.ldo, 0,
-                c.scale[i]};
-      const float f = basic_row(z, c.fid[i], D, lane, nullptr, nullptr, nullptr, 0);
-      g[i] = c.lamb[i] * f + c.bias[i];
-      const float t1 = 1.f / sqrtf(d2[i]);
-      w[i] = t1 * expf(-0.5f * d2[i] / (c.sigma[i] * c.sigma[i] * (float)D));
-      if (!isfinite(t1)) ++nzero;
+  for (int i = 0; i < c.n; ++i) {
+    const float d2 = s_d2[w][i];
+    const float t1 = 1.f / sqrtf(d2);
+    if (!isfinite(t1)) {
+      ++nzero;
+      zsum += s_g[w][i];
     }
+    wsum += t1 * expf(-0.5f * d2 / (c.sigma[i] * c.sigma[i] * (float)D));
   }
-  if (lane != 0) return;
-#pragma unroll
-  for (int i = 0; i < kEvxCecMaxParts; ++i)
-    if (i < c.n) {
-      wsum += w[i];
-      if (!isfinite(1.f / sqrtf(d2[i]))) zsum += g[i];
-    }
   float f;
   if (nzero > 0) {
     f = zsum / (float)nzero;
   } else {
-#pragma unroll
-    for (int i = 0; i < kEvxCecMaxParts; ++i)
-      if (i < c.n) fsum += (w[i] / wsum) * g[i];
+    for (int i = 0; i < c.n; ++i) {
+      const float d2 = s_d2[w][i];
+      const float wi = (1.f / sqrtf(d2)) * expf(-0.5f * d2 / (c.sigma[i] * c.sigma[i] * (float)D));
+      fsum += (wi / wsum) * s_g[w][i];
+    }
     f = fsum;
   }
   out[row] = f < c.thr ? 0.f : f;
@@ -260,7 +262,7 @@ __global__ void cec_rowterms_final_kernel(const float* __restrict__ parts, int t
 void evx_cec_compose(const float* Z, int64_t ldz, const float* X, int64_t ldx, int N, int D, const EvxCecCompose& c, float* out,
                      hipStream_t s) {
   if (N <= 0) return;
-  cec_compose_kernel<<<(N + 3) / 4, 256, 0, s>>>(Z, ldz, X, ldx, N, D, c, out);
+  cec_compose_kernel<<<(N + kComposeRows - 1) / kComposeRows, 64 * kComposeRows, 0, s>>>(Z, ldz, X, ldx, N, D, c, out);
 }
 
 void evx_cec_rowterms_final(const float* parts, int tiles_n, int M, int fid, float* out, hipStream_t s) {

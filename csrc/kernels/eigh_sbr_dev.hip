@@ -73,8 +73,21 @@ __global__ void __launch_bounds__(256) sbr_dev_prep_kernel(const float* __restri
                                                            const float* __restrict__ X3, int n, float* __restrict__ alpha,
                                                            float* __restrict__ P, float* __restrict__ MT, const int* __restrict__ ctrl,
                                                            const float* __restrict__ V2, const float* __restrict__ V3, float tau,
-                                                           const double* __restrict__ xpart, int nparts) {
-  if (ctrl[1]) return;
+                                                           const double* __restrict__ xpart, int nparts,
+                                                           const float* __restrict__ copy_src, float* __restrict__ copy_dst) {
+  if (ctrl[1]) {
+    // no far step this iteration: a near-only iteration (ctrl[7] == 0) takes the block-rotated
+    // basis Bq as the new basis — the copy runs here, in the launch the schedule makes anyway
+    if (copy_src && ctrl[7] == 0) {
+      const int64_t n4 = (int64_t)n * n / 4;
+      const float4* s4 = reinterpret_cast<const float4*>(copy_src);
+      float4* d4 = reinterpret_cast<float4*>(copy_dst);
+      const int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x, stride = (int64_t)gridDim.x * blockDim.x;
+      for (int64_t e = g; e < n4; e += stride) d4[e] = s4[e];
+      for (int64_t e = 4 * n4 + g; e < (int64_t)n * n; e += stride) copy_dst[e] = copy_src[e];
+    }
+    return;
+  }
   const bool six = ctrl[4] != 0;
   float a;
   if (xpart) {
@@ -353,13 +366,14 @@ void evx_sbr_report(const double* stats, int* seq, double* ring, int R, hipStrea
 }
 
 void evx_sbr_dev_prep(const float* X, const float* X2, const float* X3, int n, float* alpha, float* P, float* MT, const int* ctrl,
-                      hipStream_t s, const float* V2, const float* V3, float tau, const double* xpart, int nparts) {
+                      hipStream_t s, const float* V2, const float* V3, float tau, const double* xpart, int nparts, const float* copy_src,
+                      float* copy_dst) {
   // a grid-stride loop over 256 workgroups: the schedule skips this kernel in most
   // iterations, and an empty launch costs in proportion to its workgroup count
   const int64_t total = (int64_t)n * n;
   int g = (int)((total + 255) / 256);
   if (g > 256) g = 256;
-  sbr_dev_prep_kernel<<<g, 256, 0, s>>>(X, X2, X3, n, alpha, P, MT, ctrl, V2, V3, tau, xpart, nparts);
+  sbr_dev_prep_kernel<<<g, 256, 0, s>>>(X, X2, X3, n, alpha, P, MT, ctrl, V2, V3, tau, xpart, nparts, copy_src, copy_dst);
 }
 
 void evx_sbr_dev_copy(const float* src, float* dst, int64_t n, const int* skip, hipStream_t s) {

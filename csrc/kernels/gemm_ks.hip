@@ -825,12 +825,25 @@ int evx_gemm_ks_prec() { return g_ks_prec; }
 
 int evx_gemm_ks_tile(int M, int N, int mode) { return evx_host::gemm_ks_tile(M, N, mode, g_ks_tile_override); }
 
-int evx_gemm_ks_grid(int M, int N, int mode) { return (int)evx_host::gemm_ks_grid(M, N, mode, g_ks_tile_override); }
+// square bf16x6 products go to the LDS-staged kernel (gemm_sq.hip) unless a tile or the
+// precision is forced (probes): its grid then sizes the stats partials
+bool evx_gemm_ks_sq_shape(int M, int N, int mode) { return g_ks_prec == 1 && g_ks_tile_override == 0 && evx_gemm_sq_shape(M, N, mode); }
+
+int evx_gemm_ks_grid(int M, int N, int mode) {
+  if (evx_gemm_ks_sq_shape(M, N, mode)) return evx_gemm_sq_grid(M, N, mode);
+  return (int)evx_host::gemm_ks_grid(M, N, mode, g_ks_tile_override);
+}
+
+bool evx_gemm_ks_routes_sq(const EvxGemmKs& a) { return !a.force_tile && evx_gemm_ks_sq_shape(a.M, a.N, a.mode) && evx_gemm_sq_ok(a); }
 
 int evx_gemm_ks_tiles_n(int M, int N, int mode) { return (int)evx_host::gemm_ks_tiles_n(M, N, mode, g_ks_tile_override); }
 
 void evx_gemm_ks(const EvxGemmKs& a, hipStream_t s) {
   if (a.M <= 0 || a.N <= 0) return;
+  if (evx_gemm_ks_routes_sq(a)) {
+    evx_gemm_sq(a, s);
+    return;
+  }
   switch (a.force_tile ? a.force_tile : evx_gemm_ks_tile(a.M, a.N, a.mode)) {
     case 2: launch_tile<2, 2>(a, s); break;
     case 3: launch_tile<3, 3>(a, s); break;

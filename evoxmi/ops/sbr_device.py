@@ -143,8 +143,10 @@ class DeviceSBR:
             # order 6 only: X³ = X²·X = −X²·Xᵀ (skew)
             mm(self.X2, self.X, tb=True, mode=2, alpha=-1.0, out=self.X3, skip=sk_x3)
         damp_here = cfg.damp_tau > 0 and full and self.bar is None
+        # near-only iterations (no far step): the block-rotated basis is the new basis — Bq → B
+        # copied by this launch (it returns at once otherwise), no copy launch of its own
         ops.sbr_dev_prep(self.X, self.X2, self.X3, self.alpha[j + 1 : j + 2], self.P, self.VT, c, self.work if damp_here else None,
-                         float(cfg.damp_tau), self.part2)
+                         float(cfg.damp_tau), self.part2, self.Bq, self.B)
         # Vᵀ = M(−α) + X²·Pᵀ (order 4) or M(−α) − X³·Pᵀ (order 6): the control word selects
         mm(self.X2, self.P, tb=True, alpha=1.0, beta=1.0, Cin=self.VT, out=self.VT, skip=sk_far, sel=sel6, A2=self.X3, alpha2=-1.0)
         # B·V → B, or into T when Newton–Schulz follows
@@ -152,8 +154,6 @@ class DeviceSBR:
         if full:
             mm(self.T, self.T, ta=True, mode=1, out=self.G, skip=sk_ns)
             mm(self.T, self.G, tb=True, alpha=-0.5, beta=1.5, Cin=self.T, out=self.B, skip=sk_ns)
-        # near-only iteration: the block-rotated basis is the new basis
-        ops.sbr_dev_copy(self.Bq, self.B, sk_copy)
         self._btcb(C, sk_all)
         self._ctrl(j, C)
 

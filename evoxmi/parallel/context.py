@@ -181,13 +181,11 @@ class SimulatedDistContext(DistContext):
         counters (those calls repeat on every replay without running Python again)."""
         c = self.counters
         if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
-            from .wire import WireCounters
-
-            if c.captured is None or not getattr(c, "_capturing", False):
-                c.captured = WireCounters()
-                c._capturing = True
+            # the workflow opened this variant's counters (begin_capture) before capturing; a
+            # capture it did not announce gets counters of its own
+            if c.captured is None:
+                c.begin_capture(None)
             return c.captured
-        c._capturing = False
         return c
 
     def _count(self, kind: str, nbytes: int):

@@ -65,18 +65,49 @@ class WireCounters:
     wire_us: float = 0.0                # modelled wire time of the recorded collectives
     per_call: Dict[str, int] = field(default_factory=dict)
 
-    captured: object = None              # counters of the one step captured into a hipGraph
+    captured: object = None              # counters of the most recently captured step
+    # per graph variant (Algorithm.graph_variant): the captured step's counters (every segment of a
+    # segmented capture adds into its variant's), and how many replays of it the counters cover
+    captured_by: Dict[object, "WireCounters"] = field(default_factory=dict)
+    replays: Dict[object, int] = field(default_factory=dict)
 
     def reset(self):
-        """Zero the host counters and the device peer-row count (in place: a captured graph keeps
-        accumulating into the same tensor on every replay)."""
-        pr, cap, rb = self.peer_rows, self.captured, self.row_bytes
+        """Zero the host counters, the replay counts and the device peer-row count (in place: a
+        captured graph keeps accumulating into the same tensor on every replay); the captured
+        steps' counters stay (the graphs are not re-captured)."""
+        pr, cap, rb, by = self.peer_rows, self.captured, self.row_bytes, self.captured_by
         self.__init__()
         if pr is not None:
             pr.zero_()
             self.peer_rows = pr
         self.captured = cap
+        self.captured_by = by
         self.row_bytes = rb  # a property of the problem (bytes of one decision row), not a count
+
+    def begin_capture(self, key) -> "WireCounters":
+        """Fresh counters for the capture of graph variant ``key`` (its segments all add into them)."""
+        c = self.captured_by[key] = WireCounters()
+        self.captured = c
+        return c
+
+    def note_replay(self, key) -> None:
+        self.replays[key] = self.replays.get(key, 0) + 1
+
+    def _replayed_total(self) -> "WireCounters":
+        """The host counters of every replay: each variant's captured step × its replay count."""
+        t = WireCounters()
+        for key, n in self.replays.items():
+            c = self.captured_by.get(key)
+            if c is None:
+                continue
+            t.all_reduce_calls += n * c.all_reduce_calls
+            t.all_reduce_bytes += n * c.all_reduce_bytes
+            t.all_gather_calls += n * c.all_gather_calls
+            t.all_gather_bytes += n * c.all_gather_bytes
+            t.peer_gathers += n * c.peer_gathers
+            t.wire_us += n * c.wire_us
+            t.row_bytes = t.row_bytes or c.row_bytes
+        return t
 
     def summary(self, steps: int, model: WireModel, world: int, graph: bool = False) -> Dict[str, float]:
         """Per-generation volumes over ``steps`` generations.  ``graph``: the generations were
@@ -84,6 +115,13 @@ class WireCounters:
         counters of that captured step stand for every replay; the device peer-row count
         accumulated on every replay."""
         steps = max(1, int(steps))
+        if graph and self.replays and self.captured_by:
+            # replays of several variants (e.g. CMA-ES's cold / 8-slot / late eigensolver
+            # schedules), each weighted by how many generations replayed it
+            t = self._replayed_total()
+            t.peer_rows = 0.0 if self.peer_rows is None else float(self.peer_rows)
+            t.row_bytes = self.row_bytes or t.row_bytes
+            return WireCounters.summary(t, sum(self.replays.values()), model, world)
         if graph and self.captured is not None:
             # one generation = the captured step's host counters, with the device peer-row count
             # (accumulated over `steps` replays) averaged to one generation

@@ -277,6 +277,9 @@ class StdWorkflow(Workflow):
             # CMA-ES eigensolver's convergence checks) split the graph at host phases
             g = SegmentedGraph()
             record = {}
+            counters = getattr(self._dist, "counters", None) if self._dist is not None else None
+            if counters is not None and hasattr(counters, "begin_capture"):
+                counters.begin_capture(variant)  # this variant's wire counters (all its segments)
 
             def body():
                 out = self._proto_step(False, static, record=record)
@@ -340,6 +343,9 @@ class StdWorkflow(Workflow):
                 self._load_static(static, state)
         with self._phase("graph_replay"):
             self._graph.replay()
+        counters = getattr(self._dist, "counters", None) if self._dist is not None else None
+        if counters is not None and hasattr(counters, "note_replay"):
+            counters.note_replay(variant)
         gen = state.generation + 1
         out = static.update(generation=gen)
         self._static = out
@@ -379,25 +385,37 @@ class StdWorkflow(Workflow):
                 variants.append(v)
         for v in variants:
             if v not in self._graphs:
-                self._capture(state, v)
+                if self.graph == "auto":
+                    try:
+                        self._capture(state, v)
+                    except (RuntimeError, torch.AcceleratorError) as e:
+                        self._give_up_graphs(e)
+                        return state
+                else:
+                    self._capture(state, v)
         return state
+
+    def _give_up_graphs(self, e):
+        """graph='auto': a capture failed (host sync / H2D copy / data-dependent shape) — the
+        input state is untouched; every generation runs eagerly from now on."""
+        self._graph_failed = True
+        self._graph = None
+        self._graphs = {}
+        self._static = None
+        torch.cuda.synchronize()
+        warnings.warn(f"graph='auto': {type(self.algorithm).__name__} step is not capturable ({str(e).splitlines()[0]}); running eagerly")
 
     def step(self, state: State) -> State:
         for m in self.registered_hooks["pre_step"]:
             m.pre_step(state)
         if self.graph and not self._graph_failed and not (self._has_init_ask and state.generation == 0):
-            if self.graph == "auto" and self._graph is None:
+            if self.graph == "auto" and (self._graph is None or self._variant(state) not in self._graphs):
+                # a capture is due (the first one, or a graph variant not captured yet — e.g.
+                # CMA-ES's late eigensolver schedule): a capture-unsafe step falls back to eager
                 try:
                     state = self._step_graph(state)
                 except (RuntimeError, torch.AcceleratorError) as e:
-                    # capture-unsafe step (host sync / H2D copy / data-dependent shape):
-                    # the capture was invalidated, the input state is untouched — run eagerly from now on
-                    self._graph_failed = True
-                    self._graph = None
-                    self._graphs = {}
-                    self._static = None
-                    torch.cuda.synchronize()
-                    warnings.warn(f"graph='auto': {type(self.algorithm).__name__} step is not capturable ({str(e).splitlines()[0]}); running eagerly")
+                    self._give_up_graphs(e)
                     state = self._step_eager(state)
             else:
                 state = self._step_graph(state)

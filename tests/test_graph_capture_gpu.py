@@ -102,3 +102,37 @@ def test_cec2022_generation_captures_and_replays(func):
 
     a, b = run(True), run(False)
     assert torch.allclose(a.mean, b.mean, rtol=1e-4, atol=1e-4)
+
+
+def test_graph_auto_falls_back_when_a_later_variant_is_not_capturable():
+    """graph='auto': a graph variant first needed after the first capture (CMA-ES's late
+    eigensolver schedule is one) whose step cannot be captured falls back to eager too, with
+    the same result as an eager run, instead of raising to the caller."""
+    from evoxmi.problems.numerical import Sphere
+
+    class LateHostSync(A.PSO):
+        late = False
+
+        def graph_variant(self, generation):
+            self.late = generation >= 3
+            return "late" if self.late else None
+
+        def tell(self, state, fitness):
+            if self.late:
+                fitness.sum().item()  # a host read: not capturable
+            return super().tell(state, fitness)
+
+    def run(graph):
+        lb, ub = -torch.ones(8, device="cuda"), torch.ones(8, device="cuda")
+        wf = StdWorkflow(LateHostSync(lb, ub, 64), Sphere(), graph=graph)
+        st = wf.init(rnd.PRNGKey(4, device="cuda"))
+        for _ in range(6):
+            st = wf.step(st)
+        torch.cuda.synchronize()
+        return wf, st.get_child_state("algorithm")
+
+    _, a = run(False)
+    with pytest.warns(UserWarning, match="not capturable"):
+        wf, b = run("auto")
+    assert wf._graph_failed
+    assert torch.allclose(a.population, b.population, rtol=1e-6, atol=1e-6)

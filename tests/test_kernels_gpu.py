@@ -161,8 +161,10 @@ def test_cec2022_compositions_d1000_fused_path(f):
     out, _ = p.evaluate(None, X.cuda())
     with config.override(cec_compose_fused=0):
         unfused, _ = p.evaluate(None, X.cuda())
-    assert torch.allclose(out.cpu(), ref, rtol=2e-3, atol=1e-3), (f, out[:3], ref[:3])
-    assert torch.allclose(out.cpu(), unfused.cpu(), rtol=1e-4, atol=1e-4)
+    # atol: a row at a Schwefel optimum is Σ of 1000 terms of ±419 cancelling to ~0 (f32
+    # summation-order noise ~1e-2 between kernels / the CPU)
+    assert torch.allclose(out.cpu(), ref, rtol=2e-3, atol=5e-2), (f, out[:3], ref[:3])
+    assert torch.allclose(out.cpu(), unfused.cpu(), rtol=1e-4, atol=5e-2), (f, out[:3], unfused[:3])
 
 
 def test_pso_kernel_matches_cpu():

@@ -48,3 +48,28 @@ def test_graph_summary_uses_the_captured_step_and_averages_device_rows():
     assert s["peer_bytes_per_gen"] == pytest.approx(120 * 4000)
     assert s["wire_ms_per_gen"] == pytest.approx((cap.wire_us + m.peer_read_us(120 * 4000, 8)) / 1e3)
     assert cap.peer_rows is None  # the captured counters are not mutated
+
+
+def test_graph_summary_weights_every_captured_variant_by_its_replays():
+    """Per-variant captured counters (CMA-ES replays a cold, an 8-slot and a late graph): the
+    graph summary is Σ_v replays_v × counters_v per replayed generation, and a segmented capture's
+    segments all add into their variant's counters."""
+    from evoxmi.parallel.wire import WireCounters, WireModel
+
+    c = WireCounters()
+    a = c.begin_capture("cold")
+    a.all_reduce_calls, a.all_reduce_bytes, a.wire_us = 2, 4000, 20.0
+    a.all_reduce_calls += 1  # a second segment of the same capture
+    a.all_reduce_bytes += 1000
+    b = c.begin_capture("late")
+    b.all_gather_calls, b.all_gather_bytes, b.wire_us = 1, 8000, 10.0
+    for _ in range(3):
+        c.note_replay("cold")
+    c.note_replay("late")
+    s = c.summary(4, WireModel(), 8, graph=True)
+    assert s["all_reduce_per_gen"] == 3 * 3 / 4 and s["all_gather_per_gen"] == 1 / 4
+    assert abs(s["wire_ms_per_gen"] - (3 * 20.0 + 10.0) / 4 / 1e3) < 1e-12
+    c.reset()  # timed window: replay counts restart, the captured counters stay
+    assert c.replays == {} and set(c.captured_by) == {"cold", "late"}
+    c.note_replay("late")
+    assert c.summary(1, WireModel(), 8, graph=True)["all_gather_per_gen"] == 1
