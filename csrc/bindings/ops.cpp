@@ -715,7 +715,8 @@ at::Tensor cec_compose(const c10::optional<at::Tensor>& Z, const at::Tensor& X, 
   c.thr = (float)thr;
   c10::DeviceGuard g(X.device());
   auto out = at::empty({N}, X.options());
-  evx_cec_compose(zp, ldz, X.data_ptr<float>(), X.stride(0), (int)N, (int)D, c, out.data_ptr<float>(), cur_stream());
+  auto part = at::empty({N * n * 2}, X.options());
+  evx_cec_compose(zp, ldz, X.data_ptr<float>(), X.stride(0), (int)N, (int)D, c, part.data_ptr<float>(), out.data_ptr<float>(), cur_stream());
   return out;
 }
 

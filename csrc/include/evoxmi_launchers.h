@@ -129,7 +129,7 @@ void evx_split_planes(const float* X, int64_t ld, int64_t rows, int K, const flo
 void evx_philox_normal_planes(const int64_t* key, int64_t rows, int d, int64_t row0, uint16_t* out, int64_t kp, hipStream_t s);
 int evx_gemm_ks_tiles_n(int M, int N, int mode);  // column tiles of a launch (row-terms partial count)
 void evx_cec_rowterms_final(const float* parts, int tiles_n, int M, int fid, float* out, hipStream_t s);
-// one-pass composition (F9–F12): per part i the basic function fid[i] on z = Z[:, zcol[i] : +D]·scale[i]
+// composition (F9–F12) in two launches: per part i the basic function fid[i] on z = Z[:, zcol[i] : +D]·scale[i]
 // (zcol ≥ 0, the stacked rotation GEMM's block) or (x − os[comp[i]])·scale[i] (zcol < 0), the distance
 // ‖x − os[i]‖², weights from sigma, f = Σ w̃ (lamb·f_i + bias), clamped below thr
 constexpr int kEvxCecMaxParts = 8;
@@ -141,8 +141,8 @@ struct EvxCecCompose {
   int64_t ldo;
   float thr;
 };
-void evx_cec_compose(const float* Z, int64_t ldz, const float* X, int64_t ldx, int N, int D, const EvxCecCompose& c, float* out,
-                     hipStream_t s);
+void evx_cec_compose(const float* Z, int64_t ldz, const float* X, int64_t ldx, int N, int D, const EvxCecCompose& c, float* part,
+                     float* out, hipStream_t s);  // part: float[N · n · 2] scratch
 int evx_gemm_ks_grid(int M, int N, int mode);  // workgroups of a launch (stat_part length)
 // LDS-staged bf16x6 kernel for square products (gemm_sq.hip), routed to by evx_gemm_ks
 bool evx_gemm_sq_shape(int M, int N, int mode);

@@ -32,23 +32,39 @@ struct RowView {
 
 // f of one row (wave64: every lane returns the same value).  SCHAFFERF7's y pairs come from Y
 // (a separate row), the permuted Z row (yperm) or z itself.
+// the row loop of a basic function: lanes stride the row by 64; rows of ≤ 1024 (every CEC'22
+// dimension and the synthetic d = 1000) fully unrolled, so a lane's 16 independent loads issue
+// together instead of one memory latency per iteration
+template <class F>
+__device__ __forceinline__ void for_row(int L, int lane, F&& f) {
+  if (L <= 1024) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int j = lane + 64 * q;
+      if (j < L) f(j);
+    }
+  } else {
+    for (int j = lane; j < L; j += 64) f(j);
+  }
+}
+
 __device__ __forceinline__ float basic_row(const RowView& z, int fid, int L, int lane, const float* __restrict__ yr,
                                            const float* __restrict__ zrow, const int32_t* __restrict__ perm, int yperm) {
   float a = 0.f, b = 0.f, p = 1.f;
   const float fL = (float)L;
   switch (fid) {
     case ZAKHAROV:
-      for (int j = lane; j < L; j += 64) { float v = z(j); a += v * v; b += 0.5f * (float)(j + 1) * v; }
+      for_row(L, lane, [&](int j) { float v = z(j); a += v * v; b += 0.5f * (float)(j + 1) * v; });
       break;
     case ROSENBROCK:
-      for (int j = lane; j < L - 1; j += 64) {
+      for_row(L - 1, lane, [&](int j) {
         float v = z(j) + 1.f, w = z(j + 1) + 1.f;
         float t = v * v - w, u = 1.f - v;
         a += 100.f * t * t + u * u;
-      }
+      });
       break;
     case SCHAFFERF7:
-      for (int j = lane; j < L - 1; j += 64) {
+      for_row(L - 1, lane, [&](int j) {
         float y0, y1;
         if (yr) { y0 = yr[j]; y1 = yr[j + 1]; }
         else if (yperm) { y0 = zrow[perm[j]]; y1 = zrow[perm[j + 1]]; }
@@ -57,29 +73,29 @@ __device__ __forceinline__ float basic_row(const RowView& z, int fid, int L, int
         float t = sinf(50.f * powf(s, 0.2f));
         float r = sqrtf(s);
         a += r + r * t * t;
-      }
+      });
       break;
     case RASTRIGIN:
-      for (int j = lane; j < L; j += 64) { float v = z(j) * 0.0512f; a += v * v - 10.f * cosf(2.f * PI_F * v) + 10.f; }
+      for_row(L, lane, [&](int j) { float v = z(j) * 0.0512f; a += v * v - 10.f * cosf(2.f * PI_F * v) + 10.f; });
       break;
     case LEVY:
-      for (int j = lane; j < L; j += 64) {
+      for_row(L, lane, [&](int j) {
         float w = 1.f + z(j) * 0.25f;
         if (j == 0) { float s0 = sinf(PI_F * w); a += s0 * s0; }
         if (j < L - 1) { float s = sinf(PI_F * w + 1.f); a += (w - 1.f) * (w - 1.f) * (1.f + 10.f * s * s); }
         else { float s = sinf(2.f * PI_F * w); a += (w - 1.f) * (w - 1.f) * (1.f + s * s); }
-      }
+      });
       break;
     case BENTCIGAR:
-      for (int j = lane; j < L; j += 64) { float v = z(j); a += (j == 0 ? 1.f : 1e6f) * v * v; }
+      for_row(L, lane, [&](int j) { float v = z(j); a += (j == 0 ? 1.f : 1e6f) * v * v; });
       break;
     case HGBAT:
     case HAPPYCAT:
-      for (int j = lane; j < L; j += 64) { float v = z(j) * 0.05f - 1.f; a += v * v; b += v; }
+      for_row(L, lane, [&](int j) { float v = z(j) * 0.05f - 1.f; a += v * v; b += v; });
       break;
     case KATSUURA: {
       const float ex = 10.f / powf(fL, 1.2f);
-      for (int j = lane; j < L; j += 64) {
+      for_row(L, lane, [&](int j) {
         float v = z(j) * 0.05f, temp = 0.f, t1 = 1.f;
         for (int k = 1; k <= 32; ++k) {
           t1 *= 2.f;
@@ -87,14 +103,14 @@ __device__ __forceinline__ float basic_row(const RowView& z, int fid, int L, int
           temp += fabsf(t2 - floorf(t2 + 0.5f)) / t1;
         }
         p *= powf(1.f + (float)(j + 1) * temp, ex);
-      }
+      });
       break;
     }
     case ACKLEY:
-      for (int j = lane; j < L; j += 64) { float v = z(j); a += v * v; b += cosf(2.f * PI_F * v); }
+      for_row(L, lane, [&](int j) { float v = z(j); a += v * v; b += cosf(2.f * PI_F * v); });
       break;
     case SCHWEFEL:
-      for (int j = lane; j < L; j += 64) {
+      for_row(L, lane, [&](int j) {
         float v = z(j) * 10.f + 4.209687462275036e2f;
         if (v > 500.f) {
           float m = 500.f - fmodf(v, 500.f);
@@ -107,37 +123,37 @@ __device__ __forceinline__ float basic_row(const RowView& z, int fid, int L, int
         } else {
           a += -v * sinf(sqrtf(fabsf(v)));
         }
-      }
+      });
       break;
     case ELLIPTIC:
       // 10^(6j/(L−1)) as exp2 (powf's special-case handling is most of the loop's instructions)
-      for (int j = lane; j < L; j += 64) { float v = z(j); a += exp2f(6.f * (float)j / (fL - 1.f) * 3.3219280948873623f) * v * v; }
+      for_row(L, lane, [&](int j) { float v = z(j); a += exp2f(6.f * (float)j / (fL - 1.f) * 3.3219280948873623f) * v * v; });
       break;
     case DISCUS:
-      for (int j = lane; j < L; j += 64) { float v = z(j); a += (j == 0 ? 1e6f : 1.f) * v * v; }
+      for_row(L, lane, [&](int j) { float v = z(j); a += (j == 0 ? 1e6f : 1.f) * v * v; });
       break;
     case EXPSCHAFFER:
-      for (int j = lane; j < L; j += 64) {
+      for_row(L, lane, [&](int j) {
         float v = z(j), u = z(j == 0 ? L - 1 : j - 1);
         float sq = v * v + u * u;
         float s = sinf(sqrtf(sq));
         float d = 1.f + 0.001f * sq;
         a += 0.5f + (s * s - 0.5f) / (d * d);
-      }
+      });
       break;
     case EXPGRIEROSEN:
-      for (int j = lane; j < L; j += 64) {
+      for_row(L, lane, [&](int j) {
         float v = z(j) * 0.05f + 1.f, w = z(j == L - 1 ? 0 : j + 1) * 0.05f + 1.f;
         float t1 = v * v - w, t2 = v - 1.f;
         float temp = 100.f * t1 * t1 + t2 * t2;
         a += temp * temp / 4000.f - cosf(temp) + 1.f;
-      }
+      });
       break;
     case GRIEWANK:
-      for (int j = lane; j < L; j += 64) { float v = z(j); a += v * v; p *= cosf(v / sqrtf((float)(j + 1))); }
+      for_row(L, lane, [&](int j) { float v = z(j); a += v * v; p *= cosf(v / sqrtf((float)(j + 1))); });
       break;
     default:  // SPHERE
-      for (int j = lane; j < L; j += 64) { float v = z(j); a += v * v; }
+      for_row(L, lane, [&](int j) { float v = z(j); a += v * v; });
       break;
   }
   a = evx::wave_sum(a);
@@ -171,62 +187,58 @@ __global__ void __launch_bounds__(256) cec_basic_kernel(const float* __restrict_
   if (lane == 0) out[row] = (clamp > 0.f && f < clamp) ? 0.f : f;  // the CEC'22 f < 1e-8 -> 0 clamp when clamp > 0 (NaN stays NaN)
 }
 
-// Composition functions (F9–F12) in one pass: wave per row computes every component's basic
-// function — from its block of the stacked rotation GEMM output (zcol ≥ 0) or from x − o
-// (zcol < 0) — and every ‖x − o_i‖² from one read of the x row (held in registers), then the
-// weighted sum f = Σ w̃_i (λ_i f_i + bias_i) with w_i = exp(−d_i²/(2 D σ_i²)) / d_i (a zero
-// distance selects its component(s)), and the f < thr → 0 clamp.  Replaces 2n + ~15 launches
-// per evaluation.  The part loop is NOT unrolled (one copy of the basic-function switch: the
-// unrolled form spilled and thrashed the instruction cache); per-part results go through LDS.
-constexpr int kComposeRows = 4;  // rows (waves) per workgroup
-__global__ void __launch_bounds__(64 * kComposeRows) cec_compose_kernel(const float* __restrict__ Z, int64_t ldz,
-                                                                        const float* __restrict__ X, int64_t ldx, int N, int D,
-                                                                        EvxCecCompose c, float* __restrict__ out) {
-  __shared__ float s_d2[kComposeRows][kEvxCecMaxParts], s_g[kComposeRows][kEvxCecMaxParts];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int row = blockIdx.x * kComposeRows + w;
-  if (row >= N) return;  // whole waves: no barrier below
+// Composition functions (F9–F12) in two launches instead of 2n + ~15: (1) wave (row, part i) —
+// grid.y = part — computes the component's basic function from its block of the stacked rotation
+// GEMM output (zcol ≥ 0) or from x − o (zcol < 0), and ‖x − o_i‖² from the same pass over the x
+// row, writing (λ_i f_i + bias_i, d_i²); (2) one thread per row forms the weights
+// w_i = exp(−d_i²/(2 D σ_i²)) / d_i (a zero distance selects its component(s)), the weighted sum
+// and the f < thr → 0 clamp.  The part index is uniform per workgroup, so each wave runs one
+// case of the basic-function switch at full occupancy (a per-row loop over parts in one kernel
+// held 76-189 VGPRs and ran at 2-4 waves per SIMD: 238 µs at F9, 10 000 × 1000).
+__global__ void __launch_bounds__(256) cec_compose_parts_kernel(const float* __restrict__ Z, int64_t ldz, const float* __restrict__ X,
+                                                                int64_t ldx, int N, int D, EvxCecCompose c, float* __restrict__ part) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int i = blockIdx.y;
+  if (row >= N) return;
   const float* xrow = X + (int64_t)row * ldx;
-#pragma unroll 1
-  for (int i = 0; i < c.n; ++i) {
-    // ‖x − o_i‖²: the x row re-read per part stays in L1 (a register copy of it halved the
-    // occupancy: 97 VGPRs, 4 waves per SIMD, for a latency-bound row loop)
-    const float* o = c.os + (int64_t)i * c.ldo;
-    float a = 0.f;
-    for (int j = lane; j < D; j += 64) {
-      const float t = xrow[j] - o[j];
-      a = fmaf(t, t, a);
-    }
-    a = evx::wave_sum(a);
-    const bool rot = c.zcol[i] >= 0;
-    RowView z{rot ? Z + (int64_t)row * ldz + c.zcol[i] : xrow, nullptr, rot ? nullptr : c.os + (int64_t)c.comp[i] * c.ldo, 0,
-              c.scale[i]};
-    const float f = basic_row(z, c.fid[i], D, lane, nullptr, nullptr, nullptr, 0);
-    if (lane == 0) {
-      s_d2[w][i] = a;
-      s_g[w][i] = c.lamb[i] * f + c.bias[i];
-    }
-  }
-  if (lane != 0) return;  // lane 0 wrote every part's results itself
+  const float* o = c.os + (int64_t)i * c.ldo;
+  float a = 0.f;
+  for_row(D, lane, [&](int j) {
+    const float t = xrow[j] - o[j];
+    a = fmaf(t, t, a);
+  });
+  a = evx::wave_sum(a);
+  const bool rot = c.zcol[i] >= 0;
+  RowView z{rot ? Z + (int64_t)row * ldz + c.zcol[i] : xrow, nullptr, rot ? nullptr : c.os + (int64_t)c.comp[i] * c.ldo, 0, c.scale[i]};
+  const float f = basic_row(z, c.fid[i], D, lane, nullptr, nullptr, nullptr, 0);
+  if (lane == 0) *reinterpret_cast<float2*>(part + ((int64_t)row * c.n + i) * 2) = make_float2(c.lamb[i] * f + c.bias[i], a);
+}
+
+__global__ void __launch_bounds__(256) cec_compose_final_kernel(const float* __restrict__ part, int N, int D, EvxCecCompose c,
+                                                                float* __restrict__ out) {
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= N) return;
+  const float2* pr = reinterpret_cast<const float2*>(part) + (int64_t)row * c.n;
   float wsum = 0.f, zsum = 0.f, fsum = 0.f;
   int nzero = 0;
   for (int i = 0; i < c.n; ++i) {
-    const float d2 = s_d2[w][i];
-    const float t1 = 1.f / sqrtf(d2);
+    const float2 gd = pr[i];
+    const float t1 = 1.f / sqrtf(gd.y);
     if (!isfinite(t1)) {
       ++nzero;
-      zsum += s_g[w][i];
+      zsum += gd.x;
     }
-    wsum += t1 * expf(-0.5f * d2 / (c.sigma[i] * c.sigma[i] * (float)D));
+    wsum += t1 * expf(-0.5f * gd.y / (c.sigma[i] * c.sigma[i] * (float)D));
   }
   float f;
   if (nzero > 0) {
     f = zsum / (float)nzero;
   } else {
     for (int i = 0; i < c.n; ++i) {
-      const float d2 = s_d2[w][i];
-      const float wi = (1.f / sqrtf(d2)) * expf(-0.5f * d2 / (c.sigma[i] * c.sigma[i] * (float)D));
-      fsum += (wi / wsum) * s_g[w][i];
+      const float2 gd = pr[i];
+      const float wi = (1.f / sqrtf(gd.y)) * expf(-0.5f * gd.y / (c.sigma[i] * c.sigma[i] * (float)D));
+      fsum += (wi / wsum) * gd.x;
     }
     f = fsum;
   }
@@ -259,10 +271,11 @@ __global__ void cec_rowterms_final_kernel(const float* __restrict__ parts, int t
 }
 }  // namespace
 
-void evx_cec_compose(const float* Z, int64_t ldz, const float* X, int64_t ldx, int N, int D, const EvxCecCompose& c, float* out,
-                     hipStream_t s) {
+void evx_cec_compose(const float* Z, int64_t ldz, const float* X, int64_t ldx, int N, int D, const EvxCecCompose& c, float* part,
+                     float* out, hipStream_t s) {
   if (N <= 0) return;
-  cec_compose_kernel<<<(N + kComposeRows - 1) / kComposeRows, 64 * kComposeRows, 0, s>>>(Z, ldz, X, ldx, N, D, c, out);
+  cec_compose_parts_kernel<<<dim3((N + 3) / 4, c.n), 256, 0, s>>>(Z, ldz, X, ldx, N, D, c, part);
+  cec_compose_final_kernel<<<(N + 255) / 256, 256, 0, s>>>(part, N, D, c, out);
 }
 
 void evx_cec_rowterms_final(const float* parts, int tiles_n, int M, int fid, float* out, hipStream_t s) {
