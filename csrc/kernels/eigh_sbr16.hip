@@ -557,8 +557,10 @@ __global__ void __launch_bounds__(256) sbr_power_step_kernel(const float* __rest
   } else if (skip && *skip) {
     return;
   }
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (row >= n) return;
+  const int lane = threadIdx.x & 63;
+  // rows stride over a small grid: most launches are skipped (the device schedule or the ‖X‖
+  // bound says α = 1), and an empty launch costs in proportion to its workgroup count
+  for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < n; row += gridDim.x * 4) {
   const float* x = X2 + (int64_t)row * ldx;
   float acc[8] = {};
   for (int j = lane; j < n; j += 64) {
@@ -578,6 +580,7 @@ __global__ void __launch_bounds__(256) sbr_power_step_kernel(const float* __rest
   if (lane == 0) {
     *(float4*)(Vout + (int64_t)row * 8) = make_float4(-acc[0], -acc[1], -acc[2], -acc[3]);
     *(float4*)(Vout + (int64_t)row * 8 + 4) = make_float4(-acc[4], -acc[5], -acc[6], -acc[7]);
+  }
   }
 }
 
@@ -794,7 +797,7 @@ void evx_sbr_damping(const float* X2, int n, int64_t ldx, const float* V, float*
   float* V1 = work;
   float* V2 = work + (int64_t)n * 8;
   float* V3 = work + (int64_t)n * 16;
-  const int g = (n + 3) / 4;
+  const int g = (n + 3) / 4 < 64 ? (n + 3) / 4 : 64;
   const float t2 = tau * tau;
   sbr_power_step_kernel<<<g, 256, 0, s>>>(X2, n, ldx, V, V1, skip, xpart, nparts, t2);
   sbr_power_step_kernel<<<g, 256, 0, s>>>(X2, n, ldx, V1, V2, skip, xpart, nparts, t2);
