@@ -558,8 +558,7 @@ __global__ void __launch_bounds__(256) sbr_power_step_kernel(const float* __rest
     return;
   }
   const int lane = threadIdx.x & 63;
-  // rows stride over a small grid: most launches are skipped (the device schedule or the ‖X‖
-  // bound says α = 1), and an empty launch costs in proportion to its workgroup count
+  // rows stride over the grid (n > 1024)
   for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < n; row += gridDim.x * 4) {
   const float* x = X2 + (int64_t)row * ldx;
   float acc[8] = {};
@@ -797,7 +796,9 @@ void evx_sbr_damping(const float* X2, int n, int64_t ldx, const float* V, float*
   float* V1 = work;
   float* V2 = work + (int64_t)n * 8;
   float* V3 = work + (int64_t)n * 16;
-  const int g = (n + 3) / 4 < 64 ? (n + 3) / 4 : 64;
+  // one row per wave up to n = 1024 (a 64-workgroup grid made an executed step 12 vs 5.5 µs —
+  // profiles/r5_pmc_flagship.txt — for ≈1 µs less per empty launch)
+  const int g = (n + 3) / 4 < 256 ? (n + 3) / 4 : 256;
   const float t2 = tau * tau;
   sbr_power_step_kernel<<<g, 256, 0, s>>>(X2, n, ldx, V, V1, skip, xpart, nparts, t2);
   sbr_power_step_kernel<<<g, 256, 0, s>>>(X2, n, ldx, V1, V2, skip, xpart, nparts, t2);
