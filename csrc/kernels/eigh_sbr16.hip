@@ -115,32 +115,14 @@ __device__ __forceinline__ float3 rot16(float app, float aqq, float apq) {
 // transposes: S stays symmetric; pair u's own block set exactly), and every lane rotates a
 // 2×2 block of Q' = Q J (rows 2(L/8)+{0,1}, column pair L mod 8).  All updates are in place:
 // the 2×2 blocks of one round partition S and Q.
-// FR (fused rank, n ≤ kFuseMax, opt-in EVOXMI_SBR_FUSED_RANK=1): every workgroup sorts the
-// (diagonal key, index) pairs itself — a bitonic network over the padded keys in LDS, the same
-// strict total order as sbr16_rank_kernel — takes its members from the shifted sorted order and
-// writes its segment of perm for the far / Bq kernels: one launch per refinement slot fewer, but
-// the 55-stage network (one barrier each) made an executed block solve 42 µs instead of 27 + 8
-// for the two launches (profiles/r4_kstats_fused_rank.txt), so it is off by default.
+// FR (fused rank, n ≤ kFuseMax, opt-in EVOXMI_SBR_FUSED_RANK=1): every workgroup ranks the
+// (diagonal key, index) pairs itself by counting over the keys in LDS — the strict total order
+// of sbr16_rank_kernel — takes its members from the shifted order and writes its segment of perm
+// for the far / Bq kernels: one launch per refinement slot fewer, but each of the 32 workgroups
+// then counts all n² pairs with 8 waves (the rank kernel spreads them over 16 workgroups of 16
+// waves): the flagship measured 1.867 vs 1.689 ms (round 5); round 4's bitonic form was slower
+// still (42 µs per executed solve instead of 27 + 8, profiles/r4_kstats_fused_rank.txt).
 constexpr int kFuseMax = 2048;
-
-__device__ __forceinline__ void bitonic_kv(float* k, int* v, int np) {
-  for (int size = 2; size <= np; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int t = threadIdx.x; t < (np >> 1); t += blockDim.x) {
-        const int i = 2 * t - (t & (stride - 1)), j = i + stride;
-        const bool up = (i & size) == 0;
-        const float ki = k[i], kj = k[j];
-        const int vi = v[i], vj = v[j];
-        const bool gt = ki > kj || (ki == kj && vi > vj);
-        if (gt == up) {
-          k[i] = kj; k[j] = ki;
-          v[i] = vj; v[j] = vi;
-        }
-      }
-      __syncthreads();
-    }
-  }
-}
 
 // Threads: 2·SB²/4 — the first SB²/4 (waves 0-3 for SB = 32) rotate Q, the others (the
 // SB/2·(SB/2+1)/2 items {u ≤ v}) update S, so the two updates of a round run side by side on
@@ -162,22 +144,31 @@ __global__ void __launch_bounds__(SB * SB / 2) sbr16_block_kernel(const float* _
   const int s0 = blockIdx.x * SB, m = min(SB, n - s0);
   for (int e = tid; e < (SB - 1) * NH; e += nthr) ptab[e] = rr16<SB>(e / NH, e % NH);
   if constexpr (FR) {
-    __shared__ float skey[kFuseMax];
-    __shared__ int sidx[kFuseMax];
-    int np = 2;
-    while (np < n) np <<= 1;
-    for (int i = tid; i < np; i += nthr) {
-      skey[i] = i < n ? sort_key(A[(int64_t)i * lda + i]) : INFINITY;  // padding: +inf, after every real key
-      sidx[i] = i;
-    }
+    // every workgroup ranks ALL the diagonal keys by counting (the strict total order of
+    // sbr16_rank_kernel: NaN keys as +inf, ties by index) and takes the indices whose shifted
+    // position falls in its block — one launch per slot fewer than rank + block
+    __shared__ __attribute__((aligned(16))) float skey[kFuseMax];
+    const int np = (n + 3) & ~3;  // padded with +inf: never below a real key
+    for (int i = tid; i < np; i += nthr) skey[i] = i < n ? sort_key(A[(int64_t)i * lda + i]) : INFINITY;
+    if (tid < SB) members[tid] = -1;
     __syncthreads();
-    bitonic_kv(skey, sidx, np);
-    if (tid < SB) {
-      int r = s0 + tid + shift;
-      if (r >= n) r -= n;
-      const int idx = tid < m ? sidx[r] : -1;
-      members[tid] = idx;
-      if (tid < m) perm[s0 + tid] = idx;
+    for (int i = tid; i < n; i += nthr) {
+      const float ki = skey[i];
+      int cnt = 0;
+#pragma unroll 4
+      for (int j = 0; j < np; j += 4) {
+        const float4 k4 = *reinterpret_cast<const float4*>(skey + j);  // same address across the wave: broadcast
+        cnt += (k4.x < ki) | ((k4.x == ki) & (j < i));
+        cnt += (k4.y < ki) | ((k4.y == ki) & (j + 1 < i));
+        cnt += (k4.z < ki) | ((k4.z == ki) & (j + 2 < i));
+        cnt += (k4.w < ki) | ((k4.w == ki) & (j + 3 < i));
+      }
+      int pos = cnt - shift;
+      if (pos < 0) pos += n;
+      if (pos >= s0 && pos < s0 + m) {
+        members[pos - s0] = i;
+        perm[pos] = i;
+      }
     }
   } else {
     if (tid < SB) members[tid] = tid < m ? perm[s0 + tid] : -1;
