@@ -211,6 +211,39 @@ at::Tensor gemm_h3(const at::Tensor& A, const at::Tensor& a_rinv, int64_t M, con
   return C;
 }
 
+// CEC'22 F1 / F4 on the f16x3 rotation: the GEMM epilogue reduces each row's basic-function terms
+// over its 128-column tile (the rotated population is never written), one finishing kernel sums
+// the tiles in order and applies the f < 1e-8 clamp
+at::Tensor gemm_h3_rowterms(const at::Tensor& A, const at::Tensor& a_rinv, int64_t M, const at::Tensor& B, const at::Tensor& b_rinv,
+                            int64_t N, int64_t K, double alpha, int64_t fid) {
+  TORCH_CHECK(M > 0 && N > 0 && K > 0, "gemm_h3_rowterms: shape");
+  TORCH_CHECK(fid == 0 || fid == 3, "gemm_h3_rowterms: Zakharov (0) or Rastrigin (3)");
+  check_h3(A, a_rinv, M, K, "gemm_h3_rowterms A");
+  check_h3(B, b_rinv, N, K, "gemm_h3_rowterms B");
+  c10::DeviceGuard g(A.device());
+  const int tn = evx_gemm_h3_tiles_n((int)N);
+  auto parts = at::empty({tn, M, 2}, A.options().dtype(at::kFloat));
+  auto out = at::empty({M}, A.options().dtype(at::kFloat));
+  EvxGemmBlk a{};
+  a.A = reinterpret_cast<const uint16_t*>(A.data_ptr<int16_t>());
+  a.a_rows = evx_blk_rows(M);
+  a.B = reinterpret_cast<const uint16_t*>(B.data_ptr<int16_t>());
+  a.b_rows = evx_blk_rows(N);
+  a.a_rinv = a_rinv.data_ptr<float>();
+  a.b_rinv = b_rinv.data_ptr<float>();
+  a.KB = (int)((K + 15) / 16);
+  a.M = (int)M;
+  a.N = (int)N;
+  a.C = parts.data_ptr<float>();  // not written in row-terms mode
+  a.ldc = N;
+  a.alpha = (float)alpha;
+  a.row_terms = parts.data_ptr<float>();
+  a.row_fid = (int)fid;
+  evx_gemm_h3(a, cur_stream());
+  evx_cec_rowterms_final(parts.data_ptr<float>(), tn, (int)M, (int)fid, out.data_ptr<float>(), cur_stream());
+  return out;
+}
+
 int64_t h3_elems(int64_t rows, int64_t K) { return evx_h3_elems(rows, (int)K); }
 
 int64_t blk_elems(int64_t rows, int64_t K) { return evx_blk_elems(rows, (int)K); }
@@ -229,6 +262,7 @@ TORCH_LIBRARY_FRAGMENT(evoxmi, m) {
   m.def("h3_philox_normal(Tensor key, int rows, int d, int row0=0, Tensor(a!)? out=None, Tensor(b!)? rinv_out=None) -> Tensor[]");
   m.def("gemm_h3(Tensor A, Tensor a_rinv, int M, Tensor B, Tensor b_rinv, int N, int K, float alpha=1., Tensor? alpha_ptr=None, "
         "Tensor? bias_n=None, Tensor(a!)? out=None, Tensor? skip=None, int sub_cols=0) -> Tensor");
+  m.def("gemm_h3_rowterms(Tensor A, Tensor a_rinv, int M, Tensor B, Tensor b_rinv, int N, int K, float alpha, int fid) -> Tensor");
   m.def("h3_elems(int rows, int K) -> int");
   m.def("blk_rows(int rows) -> int");
   m.def("gemm_blk_tile(int which) -> int");
@@ -239,6 +273,7 @@ TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
   m.impl("blk_philox_normal", &blk_philox_normal);
   m.impl("gemm_blk", &gemm_blk);
   m.impl("h3_split", &h3_split);
+  m.impl("gemm_h3_rowterms", &gemm_h3_rowterms);
   m.impl("h3_philox_normal", &h3_philox_normal);
   m.impl("gemm_h3", &gemm_h3);
 }

@@ -106,10 +106,16 @@ struct EvxGemmBlk {
   const float* b_rinv;
   int sub_cols;           // f16x3 stacked operands: output column block c·sub_cols reads A's plane
   int64_t a_comp_stride;  // set c (a_comp_stride uint16 elements and a_rows row scales apart)
+  // f16x3 row-terms epilogue (CEC'22 F1 Zakharov fid 0 / F4 Rastrigin fid 3): C is not written;
+  // per 128-column tile and row the basic function's two additive terms go to
+  // row_terms[(tn · M + row) · 2 + {0, 1}] (finished by evx_cec_rowterms_final)
+  float* row_terms;
+  int row_fid;
 };
 void evx_gemm_blk(const EvxGemmBlk& a, hipStream_t s);
 int evx_gemm_blk_tile_m();
 int evx_gemm_blk_tile_n();
+int evx_gemm_h3_tiles_n(int N);  // 128-column tiles of gemm_h3 (row-terms partial count)
 int64_t evx_blk_rows(int64_t rows);
 int64_t evx_blk_elems(int64_t rows, int K);  // uint16 elements of a blocked-planes buffer
 // blocked planes of (X[r][k] − sub_k[k])·colscale[k] (sub_k / colscale may be null)

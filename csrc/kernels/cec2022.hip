@@ -16,38 +16,41 @@ constexpr float PI_F = 3.14159265358979323846f;
 enum { ZAKHAROV = 0, ROSENBROCK, SCHAFFERF7, RASTRIGIN, LEVY, BENTCIGAR, HGBAT, KATSUURA, ACKLEY, SCHWEFEL, HAPPYCAT,
        ELLIPTIC, DISCUS, EXPSCHAFFER, EXPGRIEROSEN, GRIEWANK, SPHERE };
 
-struct RowView {
+// PERM / SUB are template flags (not per-element pointer tests): with a runtime test in the
+// unrolled row loop the compiler kept every load behind its own vmcnt(0) wait (one memory
+// latency per element); specialised, a lane's 16 loads issue together
+template <bool PERM, bool SUB>
+struct RowViewT {
   const float* z;
   const int32_t* perm;
   const float* sub;
   int start;
   float scale;
   __device__ __forceinline__ float operator()(int j) const {
-    int i = perm ? perm[start + j] : start + j;
+    const int i = PERM ? perm[start + j] : start + j;
     float v = z[i];
-    if (sub) v -= sub[i];
+    if (SUB) v -= sub[i];
     return v * scale;
   }
 };
 
 // f of one row (wave64: every lane returns the same value).  SCHAFFERF7's y pairs come from Y
 // (a separate row), the permuted Z row (yperm) or z itself.
-// the row loop of a basic function: lanes stride the row by 64; rows of ≤ 1024 (every CEC'22
-// dimension and the synthetic d = 1000) fully unrolled, so a lane's 16 independent loads issue
-// together instead of one memory latency per iteration
+// the row loop of a basic function: lanes stride the row by 64.  The iterations in which every
+// lane is in range run without a guard, unrolled by 8, so a lane's loads of a chunk issue
+// together (behind a per-element `j < L` test the compiler kept each load behind its own
+// vmcnt(0) wait: one memory latency per element); the ragged last iteration is guarded
 template <class F>
 __device__ __forceinline__ void for_row(int L, int lane, F&& f) {
-  if (L <= 1024) {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int j = lane + 64 * q;
-      if (j < L) f(j);
-    }
-  } else {
-    for (int j = lane; j < L; j += 64) f(j);
-  }
+  const int full = L >> 6;
+  int q = 0;
+#pragma unroll 8
+  for (; q < full; ++q) f(lane + 64 * q);
+  const int j = lane + 64 * full;
+  if (j < L) f(j);
 }
 
+template <class RowView>
 __device__ __forceinline__ float basic_row(const RowView& z, int fid, int L, int lane, const float* __restrict__ yr,
                                            const float* __restrict__ zrow, const int32_t* __restrict__ perm, int yperm) {
   float a = 0.f, b = 0.f, p = 1.f;
@@ -182,8 +185,15 @@ __global__ void __launch_bounds__(256) cec_basic_kernel(const float* __restrict_
   const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (row >= N) return;
   const float* zrow = Z + (int64_t)row * ld;
-  RowView z{zrow, perm, sub, start, scale};
-  const float f = basic_row(z, fid, L, lane, Y ? Y + (int64_t)row * ldy + ystart : nullptr, zrow, perm, yperm);
+  const float* yr = Y ? Y + (int64_t)row * ldy + ystart : nullptr;
+  float f;
+  if (perm) {
+    if (sub) f = basic_row(RowViewT<true, true>{zrow, perm, sub, start, scale}, fid, L, lane, yr, zrow, perm, yperm);
+    else f = basic_row(RowViewT<true, false>{zrow, perm, sub, start, scale}, fid, L, lane, yr, zrow, perm, yperm);
+  } else {
+    if (sub) f = basic_row(RowViewT<false, true>{zrow, perm, sub, start, scale}, fid, L, lane, yr, zrow, perm, yperm);
+    else f = basic_row(RowViewT<false, false>{zrow, perm, sub, start, scale}, fid, L, lane, yr, zrow, perm, yperm);
+  }
   if (lane == 0) out[row] = (clamp > 0.f && f < clamp) ? 0.f : f;  // the CEC'22 f < 1e-8 -> 0 clamp when clamp > 0 (NaN stays NaN)
 }
 
@@ -209,9 +219,11 @@ __global__ void __launch_bounds__(256) cec_compose_parts_kernel(const float* __r
     a = fmaf(t, t, a);
   });
   a = evx::wave_sum(a);
-  const bool rot = c.zcol[i] >= 0;
-  RowView z{rot ? Z + (int64_t)row * ldz + c.zcol[i] : xrow, nullptr, rot ? nullptr : c.os + (int64_t)c.comp[i] * c.ldo, 0, c.scale[i]};
-  const float f = basic_row(z, c.fid[i], D, lane, nullptr, nullptr, nullptr, 0);
+  const bool rot = c.zcol[i] >= 0;  // uniform per workgroup
+  const float f = rot ? basic_row(RowViewT<false, false>{Z + (int64_t)row * ldz + c.zcol[i], nullptr, nullptr, 0, c.scale[i]}, c.fid[i], D,
+                                  lane, nullptr, nullptr, nullptr, 0)
+                      : basic_row(RowViewT<false, true>{xrow, nullptr, c.os + (int64_t)c.comp[i] * c.ldo, 0, c.scale[i]}, c.fid[i], D,
+                                  lane, nullptr, nullptr, nullptr, 0);
   if (lane == 0) *reinterpret_cast<float2*>(part + ((int64_t)row * c.n + i) * 2) = make_float2(c.lamb[i] * f + c.bias[i], a);
 }
 

@@ -553,6 +553,7 @@ __global__ void __launch_bounds__(256) sbr_power_step_kernel(const float* __rest
   for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < n; row += gridDim.x * 4) {
   const float* x = X2 + (int64_t)row * ldx;
   float acc[8] = {};
+#pragma unroll 4
   for (int j = lane; j < n; j += 64) {
     const float a = x[j];
     const float4 v0 = *(const float4*)(Vin + (int64_t)j * 8), v1 = *(const float4*)(Vin + (int64_t)j * 8 + 4);

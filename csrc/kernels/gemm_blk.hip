@@ -766,6 +766,78 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_h3_kernel(EvxGemmBlk p) {
     return;
   }
   const float s = p.alpha * (p.alpha_ptr ? p.alpha_ptr[0] : 1.f);
+  if (p.row_terms) {
+    // CEC'22 basic-function row terms of z = this tile's columns (Zakharov: Σ z², Σ ½(j+1) z;
+    // Rastrigin: Σ y² − 10 cos 2πy + 10 with y = 0.0512 z, 0): per 32-column block a
+    // transposing butterfly over the 32 lanes of each half (16 values → one sum per lane pair,
+    // 16 shuffles instead of 80), then the WN column blocks through LDS, one write per row
+    static_assert(TNW == 1, "row terms: one 32-column block per wave");
+    float* part = reinterpret_cast<float*>(lds);  // [WN][BM][2], the stages are free now
+    __syncthreads();
+    const int col = n0 + wn * 32 + r;
+    const bool cin = col < p.N;
+    const float cs = cin ? s * p.b_rinv[col] : 0.f;
+    const float cj = 0.5f * (float)(col + 1);
+    const bool zak = p.row_fid == 0;
+#pragma unroll
+    for (int i = 0; i < TMW; ++i) {
+      const int rowb = m0 + (wm * TMW + i) * 32 + 4 * h2;
+      float t1[16], t2[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = rowb + (e & 3) + 8 * (e >> 2);
+        const float rv = row < p.M ? p.a_rinv[row] : 0.f;
+        const float z = cs * rv * acc[i][0][e];
+        if (zak) {
+          t1[e] = z * z;
+          t2[e] = cj * z;
+        } else {  // v_cos takes revolutions: cos(2πy)
+          const float y = 0.0512f * z;
+          t1[e] = cin ? y * y - 10.f * __builtin_amdgcn_cosf(y) + 10.f : 0.f;
+          t2[e] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int w2 = 16; w2 >= 1; w2 >>= 1) {  // 16 → 8 → 4 → 2 → 1 values per lane
+        const bool hi = (r & w2) != 0;
+        const int nv = w2 == 1 ? 1 : w2 / 2;  // values kept after this step (xor 1: the final sum)
+        if (w2 == 1) {
+          t1[0] += __shfl_xor(t1[0], 1);
+          t2[0] += __shfl_xor(t2[0], 1);
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            if (k < nv) {
+              const float s1 = hi ? t1[k] : t1[k + nv], s2 = hi ? t2[k] : t2[k + nv];
+              const float k1 = hi ? t1[k + nv] : t1[k], k2 = hi ? t2[k + nv] : t2[k];
+              t1[k] = k1 + __shfl_xor(s1, w2);
+              t2[k] = k2 + __shfl_xor(s2, w2);
+            }
+          }
+        }
+      }
+      // lane (r even, h2) holds the 32-column sums of value e = (r >> 1) & 15
+      if ((r & 1) == 0) {
+        const int e = (r >> 1) & 15;
+        const int lr = (wm * TMW + i) * 32 + 4 * h2 + (e & 3) + 8 * (e >> 2);
+        part[(wn * BM + lr) * 2] = t1[0];
+        part[(wn * BM + lr) * 2 + 1] = t2[0];
+      }
+    }
+    __syncthreads();
+    for (int lr = threadIdx.x; lr < BM; lr += 64 * NW) {
+      const int row = m0 + lr;
+      if (row >= p.M) continue;
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int q = 0; q < WN; ++q) {  // fixed order: deterministic
+        a += part[(q * BM + lr) * 2];
+        b += part[(q * BM + lr) * 2 + 1];
+      }
+      *reinterpret_cast<float2*>(p.row_terms + ((int64_t)tn * p.M + row) * 2) = make_float2(a, b);
+    }
+    return;
+  }
   // the lane's 16 rows of a 32-row block are 4 runs of 4 (rows 8q + 4·h2 … +3): their row
   // scales arrive as 4 float4 loads per block, all issued before the first store
   // (rinv has Rp ≥ the tile's rows rounded to 64 entries; rows past M read zeros / slack)
@@ -906,6 +978,7 @@ void evx_gemm_h3(const EvxGemmBlk& a, hipStream_t s) {
 }
 
 int evx_gemm_blk_tile_m() { return 320; }
+int evx_gemm_h3_tiles_n(int N) { return (N + 127) / 128; }
 int evx_gemm_blk_tile_n() { return 128; }
 
 void evx_gemm_blk(const EvxGemmBlk& a, hipStream_t s) {

@@ -67,6 +67,7 @@ KNOBS: Dict[str, Knob] = {
     "cec_stack": Knob("EVOXMI_CEC_STACK", 1, int, "CEC'22 compositions (F9–F12) on the device: every rotated component from ONE GEMM over the stacked rotations with per-block exact shifts (1) or one GEMM per component (0)"),
     "cec_compose_fused": Knob("EVOXMI_CEC_COMPOSE_FUSED", 1, int, "CEC'22 compositions on the device: every component's basic function, the distances and the weighted sum in one kernel after the stacked GEMM (cec2022.hip: cec_compose_kernel) (1) or per-component launches (0)"),
     "cec_fused": Knob("EVOXMI_CEC_FUSED", 0, int, "CEC'22 F1 / F4 on the device: 1 = row terms from the rotation GEMM's epilogue (rotated population never written), 0 = GEMM + basic-function kernel (default: the fused epilogue measured 7 µs slower at pop 10 000 × d 1000, profiles/r3_cec_fused_epilogue.txt)"),
+    "cec_rowterms_h3": Knob("EVOXMI_CEC_ROWTERMS_H3", 1, int, "CEC'22 F1 / F4 on the device with the f16x3 rotation: the basic function's row terms reduced in the GEMM epilogue (1; the rotated population is never written) or the GEMM + basic-function kernel (0)"),
     "gemm_prec": Knob("EVOXMI_GEMM_PREC", "x6", str, "framework f32 GEMMs (gemm_ks.hip): 'x6' — each f32 operand split exactly into three bf16 parts, six bf16 MFMA products (f32-accurate, 3/8 of the f32 MFMA time) — or 'f32' (v_mfma_f32_16x16x4_f32)"),
     "gemm_nw8_tiles": Knob("EVOXMI_GEMM_NW8_TILES", 384, int, "gemm_ks: grids of at most this many 64×64 (or smaller) tiles with K ≥ 3072 run 8-wave workgroups (K split 8 ways, two waves per SIMD: one wave's loads overlap the other's MFMAs; the rank-μ product 55.8 → 47.8 µs); 0 = always 4 waves"),
     "gemm_planes": Knob("EVOXMI_GEMM_PLANES", 0, int, "x6 GEMMs: the d×d operand that is constant (CEC rotations) or produced once per generation (CMA-ES B·D) pre-split into bf16 fragment planes (1) — alone 162.6 vs 174.3 µs for the 10k sampling GEMM, but in the flagship generation 175.8 vs 172.6 µs (the planes leave L2 between calls) and 1.825 vs 1.811 ms/gen, so off by default; 2 also generates the CMA-ES noise into planes (205 µs); 0 splits both inside the GEMM (profiles/r4_gemm_planes.log)"),

@@ -289,7 +289,7 @@ class _CEC2022(Problem):
         return self._evaluate(X, c), state
 
 
-def _rowterms(X, o, M, s, fid):
+def _rowterms(X, o, M, s, fid, cache=None):
     """K6 fused: f of every row of z = s·(X − o)·Mᵀ straight from the rotation GEMM's epilogue
     (per column tile additive terms + one finishing kernel) — the rotated population is never
     written.  None when the device path does not apply (CPU, odd shapes, a tile layout other
@@ -298,10 +298,20 @@ def _rowterms(X, o, M, s, fid):
         return None
     from ... import config
 
-    if config.get("plain_gemm") == "blas" or not config.get("cec_fused"):
-        return None
     N, D = X.shape
     ops = _ext.ops()
+    if cache is not None and config.get("cec_rowterms_h3") and linalg.tall_nt_ok(N, D, D, X.device) and M.shape == (D, D):
+        # f16x3 rotation with the terms reduced in the GEMM epilogue (gemm_blk.hip): the rotated
+        # population is never written, no basic-function pass over it; the constant rotation's
+        # planes are the problem's cached ones (the _ssr path's)
+        key = ("h3", M.data_ptr(), M.shape)
+        pl = cache.get(key)
+        if pl is None:
+            pl = cache[key] = linalg.h3_planes(M)
+        Ap = linalg.h3_planes(X, sub_k=o.contiguous())
+        return ops.gemm_h3_rowterms(Ap.t, Ap.rinv, N, pl.t, pl.rinv, D, D, float(s), int(fid))
+    if config.get("plain_gemm") == "blas" or not config.get("cec_fused"):
+        return None
     if D % 4 or int(ops.gemm_ks_tile(N, D, 0)) not in (4, 8) or X.stride(1) != 1 or X.stride(0) % 4 or X.data_ptr() % 16:
         return None
     o = o.contiguous()
@@ -334,7 +344,7 @@ class F1_CEC2022(_RowSharded, _CEC2022):
 
     def _evaluate(self, X, c):
         D = X.shape[1]
-        f = _rowterms(X, c["Os"][:D], c["M"], 1.0, ZAKHAROV)
+        f = _rowterms(X, c["Os"][:D], c["M"], 1.0, ZAKHAROV, self._cache)
         if f is not None:
             return f
         Z = self._ssr(X, c["Os"][:D], c["M"], 1.0)
@@ -399,7 +409,7 @@ class F4_CEC2022(_RowSharded, _CEC2022):
 
     def _evaluate(self, X, c):
         D = X.shape[1]
-        f = _rowterms(X, c["Os"][:D], c["M"], 1.0, RASTRIGIN)
+        f = _rowterms(X, c["Os"][:D], c["M"], 1.0, RASTRIGIN, self._cache)
         if f is not None:
             return f
         return self._basic(self._ssr(X, c["Os"][:D], c["M"], 1.0), RASTRIGIN, clamp=1e-8)

@@ -167,6 +167,31 @@ def test_cec2022_compositions_d1000_fused_path(f):
     assert torch.allclose(out.cpu(), unfused.cpu(), rtol=1e-4, atol=5e-2), (f, out[:3], unfused[:3])
 
 
+@pytest.mark.parametrize("f", [1, 4])
+def test_cec2022_rowterms_in_the_h3_epilogue(f):
+    """F1 (Zakharov) / F4 (Rastrigin) at d = 1000 on the f16x3 rotation with the row terms reduced
+    in the GEMM epilogue (transposing butterfly over each 32-column block, the 128-column tiles
+    summed in order): equal to the CPU evaluation and to GEMM + basic-function kernel; rows at
+    the optimum give 0 (the < 1e-8 clamp)."""
+    from evoxmi import config
+    from evoxmi.problems.numerical import CEC2022TestSuit
+
+    p = CEC2022TestSuit.create(f)
+    g = torch.Generator().manual_seed(40 + f)
+    X = torch.rand(2050, 1000, generator=g) * 200 - 100
+    Os = p._consts(1000, torch.device("cpu"))["Os"]
+    X[0] = Os[0, :1000]
+    X[1] = Os[0, :1000] + 1e-2 * torch.randn(1000, generator=g)
+    ref, _ = p.evaluate(None, X)
+    out, _ = p.evaluate(None, X.cuda())
+    with config.override(cec_rowterms_h3=0):
+        plain, _ = p.evaluate(None, X.cuda())
+    assert float(out[0]) == 0.0
+    # Zakharov's (Σ ½(j+1) z)⁴ term amplifies the sum's relative rounding (a cancelling sum) ×4
+    assert torch.allclose(out.cpu(), ref, rtol=1e-3, atol=1e-3), (f, out[:3], ref[:3])
+    assert torch.allclose(out.cpu(), plain.cpu(), rtol=1e-4, atol=1e-3)
+
+
 def test_pso_kernel_matches_cpu():
     from evoxmi.ops.pso import pso_update
 
