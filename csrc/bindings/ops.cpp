@@ -508,13 +508,7 @@ void sbr_damping_out(const at::Tensor& X2, const at::Tensor& V, double tau, at::
                      const c10::optional<at::Tensor>& bar, bool no_final, const c10::optional<at::Tensor>& xpart) {
   const int64_t n = X2.size(0);
   TORCH_CHECK(V.numel() >= n * 8 && work.numel() >= n * 24 && alpha.numel() >= 1, "sbr_damping_out: shapes");
-  if (bar.has_value() && bar->defined()) {  // one persistent launch (grid barriers), see eigh_sbr16.hip
-    CHECK_DEV(*bar);
-    TORCH_CHECK(bar->scalar_type() == at::kInt && bar->numel() >= 3 && bar->is_contiguous(), "sbr_damping_out: bar int32[3]");
-    evx_sbr_damping_fused(X2.data_ptr<float>(), (int)n, X2.stride(0), V.data_ptr<float>(), work.data_ptr<float>(), (float)tau,
-                          alpha.data_ptr<float>(), cur_stream(), skip.data_ptr<int>(), reinterpret_cast<uint32_t*>(bar->data_ptr<int>()));
-    return;
-  }
+  TORCH_CHECK(!(bar.has_value() && bar->defined()), "sbr_damping_out: the grid-barrier damping was removed (round 5)");
   int64_t np = 0;
   const double* xp = xpart_ptr(xpart, np);
   evx_sbr_damping(X2.data_ptr<float>(), (int)n, X2.stride(0), V.data_ptr<float>(), work.data_ptr<float>(), (float)tau,

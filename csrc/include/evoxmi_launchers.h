@@ -256,8 +256,6 @@ int evx_sbr16_max_n();
 void evx_sbr_taylor4_prep(const float* X, const float* X2, int n, const float* alpha, float* P, float* M, hipStream_t s, int mt = 0);
 void evx_sbr_damping(const float* X2, int n, int64_t ldx, const float* V, float* work, float tau, float* alpha, hipStream_t s,
                      const int* skip = nullptr, int no_final = 0, const double* xpart = nullptr, int nparts = 0);
-void evx_sbr_damping_fused(const float* X2, int n, int64_t ldx, const float* V, float* work, float tau, float* alpha, hipStream_t s,
-                           const int* skip, uint32_t* bar);
 void evx_sbr16_block(const float* A, int n, int64_t lda, int shift, int sweeps, int* perm, float* Q, float* dq, int sb, hipStream_t s,
                      const int* skip = nullptr, float skip_tol = 0.f);
 void evx_sbr16_far(const float* A, int n, int64_t lda, const int* perm, const float* Q, const float* dq, const double* stats,

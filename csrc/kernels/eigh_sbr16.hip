@@ -583,121 +583,6 @@ __global__ void __launch_bounds__(256) sbr_damping_final_kernel(const float* __r
 }
 
 
-// The damping above as ONE launch (device-controlled schedule): the three power steps are
-// separated by grid barriers (every workgroup co-resident: ⌈n/4⌉ ≤ 256 workgroups of 4 waves on
-// the 256 CUs; the schedule's stream order leaves the chip empty at launch), workgroup 0 forms
-// α after the last one.  A skipped damping — most iterations — then costs one launch boundary
-// instead of four.  bar: [count, generation, error] (zeroed once; count returns to 0 after
-// every barrier).  A barrier that times out leaves α = 1 and sets bar[2].
-constexpr int kDampSpin = 1 << 22;
-
-__device__ __forceinline__ bool damp_barrier(uint32_t* bar, uint32_t nblocks, uint32_t& gen) {
-  __syncthreads();
-  __shared__ int ok;
-  if (threadIdx.x == 0) {
-    ok = 1;
-    __threadfence();
-    const uint32_t arrived = __hip_atomic_fetch_add(&bar[0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1;
-    if (arrived == nblocks) {
-      __hip_atomic_store(&bar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&bar[1], gen + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      int spins = 0;
-      while (__hip_atomic_load(&bar[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == gen) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins > kDampSpin) {
-          __hip_atomic_store(&bar[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          ok = 0;
-          break;
-        }
-      }
-    }
-    __threadfence();
-  }
-  __syncthreads();
-  gen += 1;
-  return ok;
-}
-
-__device__ __forceinline__ void power_rows(const float* __restrict__ X2, int n, int64_t ldx, const float* __restrict__ Vin,
-                                           float* __restrict__ Vout) {
-  const int lane = threadIdx.x & 63;
-  for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < n; row += gridDim.x * 4) {
-    const float* x = X2 + (int64_t)row * ldx;
-    float acc[8] = {};
-    for (int j = lane; j < n; j += 64) {
-      const float a = x[j];
-      const float4 v0 = *(const float4*)(Vin + (int64_t)j * 8), v1 = *(const float4*)(Vin + (int64_t)j * 8 + 4);
-      acc[0] = fmaf(a, v0.x, acc[0]);
-      acc[1] = fmaf(a, v0.y, acc[1]);
-      acc[2] = fmaf(a, v0.z, acc[2]);
-      acc[3] = fmaf(a, v0.w, acc[3]);
-      acc[4] = fmaf(a, v1.x, acc[4]);
-      acc[5] = fmaf(a, v1.y, acc[5]);
-      acc[6] = fmaf(a, v1.z, acc[6]);
-      acc[7] = fmaf(a, v1.w, acc[7]);
-    }
-#pragma unroll
-    for (int c = 0; c < 8; ++c) acc[c] = evx::wave_sum(acc[c]);
-    if (lane == 0) {
-      *(float4*)(Vout + (int64_t)row * 8) = make_float4(-acc[0], -acc[1], -acc[2], -acc[3]);
-      *(float4*)(Vout + (int64_t)row * 8 + 4) = make_float4(-acc[4], -acc[5], -acc[6], -acc[7]);
-    }
-  }
-}
-
-__global__ void __launch_bounds__(256) sbr_damping_fused_kernel(const float* __restrict__ X2, int n, int64_t ldx,
-                                                                const float* __restrict__ V, float* __restrict__ work, float tau,
-                                                                float* __restrict__ alpha, const int* __restrict__ skip,
-                                                                uint32_t* __restrict__ bar) {
-  if (skip && *skip) return;
-  float* V1 = work;
-  float* V2 = work + (int64_t)n * 8;
-  float* V3 = work + (int64_t)n * 16;
-  uint32_t gen = __hip_atomic_load(&bar[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-  const uint32_t nb = gridDim.x;
-  power_rows(X2, n, ldx, V, V1);
-  bool ok = damp_barrier(bar, nb, gen);
-  if (ok) power_rows(X2, n, ldx, V1, V2);
-  ok = ok && damp_barrier(bar, nb, gen);
-  if (ok) power_rows(X2, n, ldx, V2, V3);
-  ok = ok && damp_barrier(bar, nb, gen);
-  if (blockIdx.x != 0) return;
-  if (!ok) {
-    if (threadIdx.x == 0) alpha[0] = 1.f;
-    return;
-  }
-  __shared__ float red[2][8][4];
-  float s2[8] = {}, s3[8] = {};
-  for (int j = threadIdx.x; j < n; j += blockDim.x) {
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const float a = V2[(int64_t)j * 8 + c], b = V3[(int64_t)j * 8 + c];
-      s2[c] = fmaf(a, a, s2[c]);
-      s3[c] = fmaf(b, b, s3[c]);
-    }
-  }
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    s2[c] = evx::wave_sum(s2[c]);
-    s3[c] = evx::wave_sum(s3[c]);
-    if (lane == 0) {
-      red[0][c][w] = s2[c];
-      red[1][c][w] = s3[c];
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float lam = 0.f;
-    for (int c = 0; c < 8; ++c) {
-      const float a = red[0][c][0] + red[0][c][1] + red[0][c][2] + red[0][c][3];
-      const float b = red[1][c][0] + red[1][c][1] + red[1][c][2] + red[1][c][3];
-      lam = fmaxf(lam, sqrtf(b) / fmaxf(sqrtf(a), 1e-30f));
-    }
-    alpha[0] = fminf(1.f, tau / sqrtf(fmaxf(lam, 1e-30f)));
-  }
-}
 
 // Taylor-4 operands: exp(αX) ≈ M + X²·P with M = I + αX + α²X²/2, P = α²(αX/6 + α²X²/24)
 __global__ void __launch_bounds__(256) sbr_taylor4_prep_kernel(const float* __restrict__ X, const float* __restrict__ X2, int n,
@@ -777,11 +662,6 @@ void evx_sbr16_far_bq(const float* A, int n, int64_t lda, const int* perm, const
                                                  skip_bq, pre);
 }
 
-void evx_sbr_damping_fused(const float* X2, int n, int64_t ldx, const float* V, float* work, float tau, float* alpha, hipStream_t s,
-                           const int* skip, uint32_t* bar) {
-  const int g = (n + 3) / 4 < 256 ? (n + 3) / 4 : 256;  // co-resident on 256 CUs; rows stride over the grid
-  sbr_damping_fused_kernel<<<g, 256, 0, s>>>(X2, n, ldx, V, work, tau, alpha, skip, bar);
-}
 
 void evx_sbr_damping(const float* X2, int n, int64_t ldx, const float* V, float* work, float tau, float* alpha, hipStream_t s,
                      const int* skip, int no_final, const double* xpart, int nparts) {

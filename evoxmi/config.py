@@ -50,7 +50,7 @@ KNOBS: Dict[str, Knob] = {
     "sbr_cold_gens": Knob("EVOXMI_SBR_COLD_GENS", 4, int, "CMA-ES device eigensolver: the first generations that use the cold-start schedule (their own hipGraph; the generation index is host-known)"),
     "sbr_cold_iters": Knob("EVOXMI_SBR_COLD_ITERS", 16, int, "CMA-ES device eigensolver: refinement slots of the cold-start schedule"),
     "sbr_late_gens": Knob("EVOXMI_SBR_LATE_GENS", 24, int, "CMA-ES: generations from this index on replay a shorter 'late' eigensolver graph of sbr_late_iters slots (0: off) — at the bench config every solve from generation ≈22 to ≈305 converges in 4 iterations (5-7 before; profiles/r4_iters_per_gen_300.txt), so 6 slots keep a margin of 2"),
-    "sbr_late_iters": Knob("EVOXMI_SBR_LATE_ITERS", 6, int, "refinement slots of the late-generation eigensolver schedule"),
+    "sbr_late_iters": Knob("EVOXMI_SBR_LATE_ITERS", 5, int, "refinement slots of the late-generation eigensolver schedule (settled solves take 4; a capped solve escalates the schedule two generations later — round 5: 6 → 5 slots, 1.439 → 1.424 ms over 50 steps)"),
     "sbr_late_full_slots": Knob("EVOXMI_SBR_LATE_FULL_SLOTS", 3, int, "late-generation eigensolver schedule: slots that carry the damping / Newton–Schulz / order-6 kernels (the rest are lean); settled generations need them in slots 0-2 only (profiles/r4_near_only_ab.txt detail)"),
     "sbr_full_slots": Knob("EVOXMI_SBR_FULL_SLOTS", 5, int, "sbr device schedule (warm, 8 slots): slots past this carry no damping / Newton–Schulz / X³ kernels (those variants are chosen only in the first iterations of a warm-started solve), so a skipped tail slot costs 7 launches fewer"),
     "sbr_near_only": Knob("EVOXMI_SBR_NEAR_ONLY", 1.5, float, "sbr: a refinement iteration skips the far step once off_rel ≤ near_only·tol (after a far iteration).  1.5: with 3.0 a near-only step taken at off_rel 1.5-3e-5 often barely helped (far pairs left) and cost a further far iteration — 20 / 50-step bench 1.830 / 1.686 vs 1.850 / 1.694 ms, mean iterations 4.75 vs 5.0 (profiles/r4_near_only_ab.txt)"),
@@ -63,7 +63,6 @@ KNOBS: Dict[str, Knob] = {
     "sbr_escalate_gens": Knob("EVOXMI_SBR_ESCALATE_GENS", 8, int, "CMA-ES device eigensolver: after a solve reports itself capped or fell back (seen by the host one generation late through a pinned copy + event query), this many generations replay the next longer schedule (late → 8-slot → cold)"),
     "sbr_lean_max_n": Knob("EVOXMI_SBR_LEAN_MAX_N", 1024, int, "device eigensolver: lean tail slots only for matrices up to this order (larger ones keep the damping / Newton–Schulz kernels in every slot)"),
     "sbr_xgate": Knob("EVOXMI_SBR_XGATE", 2, int, "device eigensolver: the damping's power iteration also follows free bounds of the generator (the X² GEMM's diagonal stats): skipped when ‖X‖₂ ≤ τ is proven, run when a row of X is longer than τ/2 whatever κ says — 1 in every schedule, 2 in the cold-start schedule only (where an undamped step on a large generator diverged the d = 2000 cold start; in settled solves it costs ≈3 % of a generation), 0 off"),
-    "sbr_fused_damping": Knob("EVOXMI_SBR_FUSED_DAMPING", 0, int, "device-controlled eigensolver: the step-size damping (3 power steps + final) as one grid-barrier launch (1) or four launches (0, default: the grid barriers' agent-scope fences cost more than the three launch boundaries they remove — 1.939 vs 1.888 ms/gen, profiles/NOTES.md)"),
     "cec_stack": Knob("EVOXMI_CEC_STACK", 1, int, "CEC'22 compositions (F9–F12) on the device: every rotated component from ONE GEMM over the stacked rotations with per-block exact shifts (1) or one GEMM per component (0)"),
     "cec_compose_fused": Knob("EVOXMI_CEC_COMPOSE_FUSED", 1, int, "CEC'22 compositions on the device: every component's basic function, the distances and the weighted sum in one kernel after the stacked GEMM (cec2022.hip: cec_compose_kernel) (1) or per-component launches (0)"),
     "cec_fused": Knob("EVOXMI_CEC_FUSED", 0, int, "CEC'22 F1 / F4 on the device: 1 = row terms from the rotation GEMM's epilogue (rotated population never written), 0 = GEMM + basic-function kernel (default: the fused epilogue measured 7 µs slower at pop 10 000 × d 1000, profiles/r3_cec_fused_epilogue.txt)"),

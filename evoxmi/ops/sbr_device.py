@@ -37,12 +37,6 @@ from .sbr import SBRConfig, _probe_vectors
 LOG_LEN = 4096
 
 
-def config_fused_damping() -> bool:
-    from .. import config
-
-    return bool(config.get("sbr_fused_damping"))
-
-
 class DeviceSBR:
     """Persistent buffers + the fixed iteration schedule for one (n, device, config)."""
 
@@ -86,8 +80,6 @@ class DeviceSBR:
         self.ctrl = torch.ones(8 * max(K, 1), dtype=torch.int32, device=dev)
         self.st = torch.zeros(8, dtype=torch.int32, device=dev)
         self.never = torch.zeros(1, dtype=torch.int32, device=dev)
-        # grid-barrier words of the one-launch damping ([count, generation, error])
-        self.bar = torch.zeros(4, dtype=torch.int32, device=dev) if config_fused_damping() else None
         self.V = _probe_vectors(n, str(dev))
         self.work = torch.zeros(24 * n, device=dev)
         self.w = torch.zeros(n, device=dev)
@@ -137,12 +129,12 @@ class DeviceSBR:
         if cfg.damp_tau > 0 and full:
             # three power-step launches (they return at once when the free Frobenius bound already
             # gives α = 1); α itself is formed by the prep kernel below (no_final)
-            ops.sbr_damping_out(self.X2, self.V, float(cfg.damp_tau), self.alpha[j + 1 : j + 2], self.work, sk_damp, self.bar,
-                                self.bar is None, self.part2 if self.bar is None else None)
+            ops.sbr_damping_out(self.X2, self.V, float(cfg.damp_tau), self.alpha[j + 1 : j + 2], self.work, sk_damp, None, True,
+                                self.part2)
         if full:
             # order 6 only: X³ = X²·X = −X²·Xᵀ (skew)
             mm(self.X2, self.X, tb=True, mode=2, alpha=-1.0, out=self.X3, skip=sk_x3)
-        damp_here = cfg.damp_tau > 0 and full and self.bar is None
+        damp_here = cfg.damp_tau > 0 and full
         # near-only iterations (no far step): the block-rotated basis is the new basis — Bq → B
         # copied by this launch (it returns at once otherwise), no copy launch of its own
         ops.sbr_dev_prep(self.X, self.X2, self.X3, self.alpha[j + 1 : j + 2], self.P, self.VT, c, self.work if damp_here else None,
