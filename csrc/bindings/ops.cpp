@@ -986,12 +986,15 @@ std::vector<at::Tensor> sbr_taylor_prep(const at::Tensor& X, const at::Tensor& X
   return {P, M};
 }
 
-at::Tensor philox_words(const at::Tensor& key, int64_t nblocks, int64_t domain, int64_t offset) {
+// words = 4: every word of each block; 2: the first two (a key split's (num, 2) keys, one launch)
+at::Tensor philox_words(const at::Tensor& key, int64_t nblocks, int64_t domain, int64_t offset, int64_t words) {
   const int64_t B = key_batch(key, "philox_words");
+  TORCH_CHECK(words == 2 || words == 4, "philox_words: words 2 or 4");
   c10::DeviceGuard g(key.device());
-  auto out = B ? at::empty({B, nblocks, 4}, key.options()) : at::empty({nblocks, 4}, key.options());
+  auto out = B ? at::empty({B, nblocks, words}, key.options()) : at::empty({nblocks, words}, key.options());
   if (nblocks > 0)
-    evx_philox_words(key.data_ptr<int64_t>(), nblocks, (uint32_t)domain, offset, out.data_ptr<int64_t>(), cur_stream(), B ? (int)B : 1);
+    evx_philox_words(key.data_ptr<int64_t>(), nblocks, (uint32_t)domain, offset, out.data_ptr<int64_t>(), cur_stream(), B ? (int)B : 1,
+                     (int)words);
   return out;
 }
 
@@ -1529,7 +1532,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("cec_compose(Tensor? Z, Tensor X, Tensor Os, int[] fid, int[] zcol, int[] comp, float[] scale, float[] sigma, float[] lamb, "
         "float[] bias, float thr) -> Tensor");
   m.def("jacobi_sweeps(Tensor A, Tensor B, Tensor sched, int sweeps, float tol, float inner_tol, int max_inner, int fused=2) -> Tensor[]");
-  m.def("philox_words(Tensor key, int nblocks, int domain, int offset) -> Tensor");
+  m.def("philox_words(Tensor key, int nblocks, int domain, int offset, int words=4) -> Tensor");
   m.def("weighted_rowsum(Tensor X, Tensor? idx, Tensor w, Tensor? sub, int K) -> Tensor");
   m.def("gemm_set_config(int cfg) -> ()");
   m.def("sbx(Tensor x, Tensor keys, float pro_c, float dis_c, int type, int col0=0, int dtot=0) -> Tensor");

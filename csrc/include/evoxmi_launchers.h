@@ -193,7 +193,7 @@ void evx_es_population(const int64_t* key, const float* center, float sigma, int
 void evx_es_noise_grad(const int64_t* key, const float* w, int64_t rows, int64_t d, int64_t row0, int chunks, float* partial,
                        hipStream_t s, int64_t col0 = 0, int64_t dtot = 0);
 void evx_philox_words(const int64_t* key, int64_t nblocks, uint32_t domain, int64_t offset, int64_t* out, hipStream_t s,
-                      int batch = 1);
+                      int batch = 1, int words = 4);
 void evx_colsum(const float* partial, int chunks, int D, float* out, hipStream_t s);
 void evx_weighted_rowsum(const float* X, int64_t ldx, const int32_t* idx, const float* w, const float* sub, int K, int D,
                          float* partial, int chunks, hipStream_t s);

@@ -101,30 +101,37 @@ void evx_philox_window(float* out, const int64_t* key, int64_t rows, int64_t dto
 // instead of ~80 int64 elementwise kernels.  out[b][w] = word w of block (offset + b)
 // with counter (b_lo, b_hi, 0, domain).  Words are stored as int64 (uint32 values).
 namespace {
+// W = words kept per block (4, or 2 for key splits: the (num, 2) keys written directly)
+template <int W>
 __global__ void philox_words_kernel(const int64_t* __restrict__ key, int64_t nblocks, uint32_t domain, int64_t offset,
                                     int64_t* __restrict__ out) {
   key += 2 * (int64_t)blockIdx.y;
-  out += 4 * nblocks * (int64_t)blockIdx.y;
+  out += W * nblocks * (int64_t)blockIdx.y;
   uint32_t k0, k1;
   evx::load_key(key, k0, k1);
   for (int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; b < nblocks; b += (int64_t)gridDim.x * blockDim.x) {
     uint64_t c = (uint64_t)(b + offset);
     evx::u4 w = evx::philox4x32_10(evx::u4{(uint32_t)c, (uint32_t)(c >> 32), 0u, domain}, k0, k1);
-    out[4 * b + 0] = w.x;
-    out[4 * b + 1] = w.y;
-    out[4 * b + 2] = w.z;
-    out[4 * b + 3] = w.w;
+    out[W * b + 0] = w.x;
+    out[W * b + 1] = w.y;
+    if (W == 4) {
+      out[W * b + 2] = w.z;
+      out[W * b + 3] = w.w;
+    }
   }
 }
 }  // namespace
 
 void evx_philox_words(const int64_t* key, int64_t nblocks, uint32_t domain, int64_t offset, int64_t* out, hipStream_t s,
-                      int batch) {
+                      int batch, int words) {
   int gx = (int)((nblocks + 255) / 256);
   if (gx > 1024) gx = 1024;
   if (gx < 1) gx = 1;
   const dim3 grid(gx, batch);
-  philox_words_kernel<<<grid, 256, 0, s>>>(key, nblocks, domain, offset, out);
+  if (words == 2)
+    philox_words_kernel<2><<<grid, 256, 0, s>>>(key, nblocks, domain, offset, out);
+  else
+    philox_words_kernel<4><<<grid, 256, 0, s>>>(key, nblocks, domain, offset, out);
 }
 
 // ---------------------------------------------------------------------------------------

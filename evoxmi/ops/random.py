@@ -90,6 +90,9 @@ def _blocks(key: torch.Tensor, nblocks: int, domain: int, offset: int = 0):
 def split(key: torch.Tensor, num: int = 2) -> torch.Tensor:
     """``num`` new keys, shape ``(num, 2)`` (reference ``jax.random.split``)."""
     _check_key(key)
+    if key.is_cuda and key.dim() == 1:
+        # the (num, 2) keys straight from one launch (no stacking copy)
+        return _ext().ops().philox_words(key.contiguous(), int(num), int(_DOMAIN_SPLIT), 0, 2)
     w0, w1, _, _ = _blocks(key, num, _DOMAIN_SPLIT)
     return torch.stack([w0, w1], dim=1)
 

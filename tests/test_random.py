@@ -76,3 +76,17 @@ def test_gpu_philox_bit_exact():
     assert torch.allclose(zc, zg, atol=1e-5, rtol=1e-5)
     part = rnd.normal(key.cuda(), (4096,), offset=4096).cpu()
     assert torch.allclose(zc[4096:8192], part, atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("num", [1, 2, 5, 300])
+def test_split_on_the_device_matches_the_host(num):
+    """rnd.split on a GPU key writes the (num, 2) keys from one launch (philox_words, 2 words
+    per block): bitwise the host keys; fold_in and the bits of a split key agree too."""
+    for seed in (0, 7, 2**40 + 3):
+        kc = rnd.PRNGKey(seed)
+        kg = kc.cuda()
+        sc, sg = rnd.split(kc, num), rnd.split(kg, num)
+        assert sg.shape == (num, 2) and sg.is_contiguous()
+        assert torch.equal(sc, sg.cpu())
+        assert torch.equal(rnd.bits(sc[-1], (37,)), rnd.bits(sg[-1], (37,)).cpu())
