@@ -46,7 +46,8 @@ KNOBS: Dict[str, Knob] = {
     "sbr_sweeps": Knob("EVOXMI_SBR_SWEEPS", 2, int, "sbr: cyclic Jacobi sweeps of the near-pair block solve per refinement iteration"),
     "sbr_block": Knob("EVOXMI_SBR_BLOCK", 32, int, "sbr: near-pair block size — 32 or 16 (blocks in a shifted sorted order, eigh_sbr16.hip; 32 converges in fewer iterations on the bench matrices) or 64 (eigh_sbr.hip)"),
     "sbr_mode": Knob("EVOXMI_SBR_MODE", "device", str, "sbr: 'device' — fixed device-controlled iteration schedule inside the generation's graph (ops/sbr_device.py, no host read); 'host' — host-driven iterations with planned solves as a host phase between graph segments (ops/sbr.py)"),
-    "sbr_device_iters": Knob("EVOXMI_SBR_DEVICE_ITERS", 8, int, "sbr device mode: refinement iterations in the fixed schedule (kernels of iterations past convergence return at once)"),
+    "sbr_device_iters": Knob("EVOXMI_SBR_DEVICE_ITERS", 7, int, "sbr device mode: refinement iterations in the fixed (warm) schedule (kernels of iterations past convergence return at once; round 5: 8 → 7 slots, 1.644-1.656 → 1.630 ms at 20 steps — warm solves at d ≤ 1000 take at most 6 iterations on F1 / F4 / F6 / F12 over 200 generations, and a capped solve escalates the schedule)"),
+    "sbr_large_n_iters": Knob("EVOXMI_SBR_LARGE_N_ITERS", 8, int, "device eigensolver: least warm-schedule slots for matrices larger than sbr_lean_max_n"),
     "sbr_cold_gens": Knob("EVOXMI_SBR_COLD_GENS", 4, int, "CMA-ES device eigensolver: the first generations that use the cold-start schedule (their own hipGraph; the generation index is host-known)"),
     "sbr_cold_iters": Knob("EVOXMI_SBR_COLD_ITERS", 16, int, "CMA-ES device eigensolver: refinement slots of the cold-start schedule"),
     "sbr_late_gens": Knob("EVOXMI_SBR_LATE_GENS", 24, int, "CMA-ES: generations from this index on replay a shorter 'late' eigensolver graph of sbr_late_iters slots (0: off) — at the bench config every solve from generation ≈22 to ≈305 converges in 4 iterations (5-7 before; profiles/r4_iters_per_gen_300.txt), so 6 slots keep a margin of 2"),

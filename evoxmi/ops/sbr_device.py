@@ -208,9 +208,12 @@ def eigh_device(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None, it
         # variant passes a longer schedule with every slot full)
         lean = config.get("sbr_full_slots") if iters < config.get("sbr_cold_iters") else None
         # larger matrices stay above the damping / Newton–Schulz thresholds for more iterations
-        # (d = 2000: the lean-slot guard capped warm solves at slot 5): every slot full there
+        # (d = 2000: the lean-slot guard capped warm solves at slot 5): every slot full there,
+        # and at least sbr_large_n_iters slots (a 7-slot warm schedule capped one d = 2000 solve
+        # at 7 iterations, off_rel 1.39e-5)
         if C.shape[0] > int(config.get("sbr_lean_max_n")):
             lean = None
+            iters = max(iters, int(config.get("sbr_large_n_iters")))
     else:
         lean = None
     # the bounds-gated damping: everywhere (1) or in the cold-start schedule only (2): the
