@@ -182,8 +182,11 @@ __global__ void __launch_bounds__(SB * SB / 2) sbr16_block_kernel(const float* _
   }
   __syncthreads();
   const bool qlane = tid < NT;
-  // Q lanes: rows qr, qr+1, column pair qv
-  const int qr = (tid / NH) * 2, qv = tid % NH;
+  // Q lanes: row qrow, column pairs qv0 and qv0 + SB/4 — the 32 lanes of a half-wave share one
+  // pair and cover 32 rows, so their Q reads and writes hit 32 distinct banks (row pitch ≡ 1 mod
+  // 32); the round-4 map (two rows × 16 pairs per half-wave) conflicted whenever two pairs' columns
+  // differed by the row offset (SQ_LDS_BANK_CONFLICT 48 %, profiles/r5_pmc_flagship.txt)
+  const int qrow = tid % SB, qv0 = tid / SB;
   // S lanes: item {u ≤ v}
   int u = 0, rem = tid - NT;
   while (u < NH - 1 && rem >= NH - u) {
@@ -235,14 +238,15 @@ __global__ void __launch_bounds__(SB * SB / 2) sbr16_block_kernel(const float* _
     }
     __syncthreads();
     if (qlane) {
-      const int2 pq = pr[qv];
-      const float4 rq = rot[qv];
-      const float x0 = Qm[qr * SP + pq.x], y0 = Qm[qr * SP + pq.y];
-      const float x1 = Qm[(qr + 1) * SP + pq.x], y1 = Qm[(qr + 1) * SP + pq.y];
-      Qm[qr * SP + pq.x] = rq.x * x0 - rq.y * y0;
-      Qm[qr * SP + pq.y] = rq.y * x0 + rq.x * y0;
-      Qm[(qr + 1) * SP + pq.x] = rq.x * x1 - rq.y * y1;
-      Qm[(qr + 1) * SP + pq.y] = rq.y * x1 + rq.x * y1;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int qv = qv0 + h * (SB / 4);
+        const int2 pq = pr[qv];
+        const float4 rq = rot[qv];
+        const float x0 = Qm[qrow * SP + pq.x], y0 = Qm[qrow * SP + pq.y];
+        Qm[qrow * SP + pq.x] = rq.x * x0 - rq.y * y0;
+        Qm[qrow * SP + pq.y] = rq.y * x0 + rq.x * y0;
+      }
     } else if (item) {
       const int2 pu = pr[u], pv = pr[v];
       const float4 ru = rot[u], rv = rot[v];
