@@ -441,6 +441,295 @@ __device__ __forceinline__ void load_body(AntBody& s, AntLeg& g, const float* __
   init_momenta(s, g);
 }
 
+// ---------------------------------------------------------------- packed-f32 sub-step
+// The same sub-step written on register pairs for the lone-wave regime (pop ≤ #SIMDs: one wave
+// owns its SIMD and the step is VALU-issue bound).  A v_pk_fma_f32 issues at about the cost of a
+// v_fma_f32 (tools/probe_pk_f32.hip) but does two FMAs, so every 3-vector keeps (x, y) in an
+// aligned pair and z apart, the two hinges of a leg share pairs (hip, signed ankle), and the
+// rotation R is held both as column pairs (R v) and row pairs (Rᵀ v).  The compiler's SLP
+// vectoriser found pairs too but paid ~400 v_mov for them (1139 vs 913 instructions, 9.8 vs
+// 8.3 ms at pop 1024, profiles/r5_ant_packed.txt); the swizzles here ride on op_sel / neg
+// modifiers of hand-written VOP3P instructions instead.  Signed ankle variables (a = sg·aq,
+// its rate and momentum) make every leg's equations identical; sg appears only at the
+// observation and the actuator.
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2 lo2(float s) {  // s in the low dword of a pair (the high dword unused)
+  f2 r;
+  r.x = s;
+  return r;
+}
+// perp(a) = (−a.y, a.x) = e_z × a
+__device__ __forceinline__ f2 perp_mul(f2 a, float s) {  // perp(a)·s
+  f2 d;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,0] neg_lo:[1,0]" : "=v"(d) : "v"(a), "v"(lo2(s)));
+  return d;
+}
+__device__ __forceinline__ f2 perp_fma(f2 a, float s, f2 c) {  // perp(a)·s + c
+  f2 d;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,0,1] neg_lo:[1,0,0]" : "=v"(d) : "v"(a), "v"(lo2(s)), "v"(c));
+  return d;
+}
+__device__ __forceinline__ f2 perp_fms(f2 a, float s, f2 c) {  // perp(a)·s − c
+  f2 d;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,0,1] neg_lo:[1,0,1] neg_hi:[0,0,1]" : "=v"(d) : "v"(a), "v"(lo2(s)), "v"(c));
+  return d;
+}
+__device__ __forceinline__ float cross2(f2 a, f2 b) { return a.x * b.y - a.y * b.x; }
+__device__ __forceinline__ float dot2(f2 a, f2 b) { return a.x * b.x + a.y * b.y; }
+
+struct V3 {
+  f2 xy;
+  float z;
+};
+__device__ __forceinline__ V3 mk3(f2 xy, float z) {
+  V3 r;
+  r.xy = xy;
+  r.z = z;
+  return r;
+}
+// a × b = (a.z·perp(b) − b.z·perp(a), a.x b.y − a.y b.x)
+__device__ __forceinline__ V3 crs(const V3& a, const V3& b) { return mk3(perp_fms(b.xy, a.z, perp_mul(a.xy, b.z)), cross2(a.xy, b.xy)); }
+// a × b with b.z = 0
+__device__ __forceinline__ V3 crs_b0(const V3& a, f2 b) { return mk3(perp_mul(b, a.z), cross2(a.xy, b)); }
+__device__ __forceinline__ float dot3v(const V3& a, const V3& b) { return fmaf(a.z, b.z, dot2(a.xy, b.xy)); }
+
+struct PkRot {  // R (row-major r0..r8) as column pairs (r0,r3) (r1,r4) (r2,r5) and row pairs (r0,r1) (r3,r4) (r6,r7)
+  f2 c0, c1, c2, w0, w1, w2;
+  float r2, r5, r6, r7, r8;
+};
+__device__ __forceinline__ PkRot pk_rot(f2 qwx, f2 qyz) {
+  const float w = qwx.x, x = qwx.y, y = qyz.x, z = qyz.y;
+  PkRot R;
+  const float r0 = 1.f - 2.f * (y * y + z * z), r1 = 2.f * (x * y - w * z), r2 = 2.f * (x * z + w * y);
+  const float r3 = 2.f * (x * y + w * z), r4 = 1.f - 2.f * (x * x + z * z), r5 = 2.f * (y * z - w * x);
+  const float r6 = 2.f * (x * z - w * y), r7 = 2.f * (y * z + w * x), r8 = 1.f - 2.f * (x * x + y * y);
+  R.c0 = f2{r0, r3};
+  R.c1 = f2{r1, r4};
+  R.c2 = f2{r2, r5};
+  R.w0 = f2{r0, r1};
+  R.w1 = f2{r3, r4};
+  R.w2 = f2{r6, r7};
+  R.r2 = r2;
+  R.r5 = r5;
+  R.r6 = r6;
+  R.r7 = r7;
+  R.r8 = r8;
+  return R;
+}
+__device__ __forceinline__ V3 rmul(const PkRot& R, const V3& v) {  // R v
+  return mk3(R.c0 * v.xy.x + R.c1 * v.xy.y + R.c2 * v.z, R.r6 * v.xy.x + R.r7 * v.xy.y + R.r8 * v.z);
+}
+__device__ __forceinline__ V3 rtmul(const PkRot& R, const V3& v) {  // Rᵀ v
+  return mk3(R.w0 * v.xy.x + R.w1 * v.xy.y + R.w2 * v.z, R.r2 * v.xy.x + R.r5 * v.xy.y + R.r8 * v.z);
+}
+
+struct PkBody {
+  V3 p, v, w, P, L;
+  f2 qwx, qyz;
+};
+struct PkLeg {
+  f2 ang, rate, mom;  // (hip, signed ankle) angle, rate, momentum
+  f2 h;          // hip position in the torso frame
+  float sg, base;
+};
+__device__ __forceinline__ void pk_from(const AntBody& s, const AntLeg& g, PkBody& b, PkLeg& l) {
+  b.p = mk3(f2{s.p[0], s.p[1]}, s.p[2]);
+  b.v = mk3(f2{s.v[0], s.v[1]}, s.v[2]);
+  b.w = mk3(f2{s.w[0], s.w[1]}, s.w[2]);
+  b.P = mk3(f2{s.P[0], s.P[1]}, s.P[2]);
+  b.L = mk3(f2{s.L[0], s.L[1]}, s.L[2]);
+  b.qwx = f2{s.q[0], s.q[1]};
+  b.qyz = f2{s.q[2], s.q[3]};
+  l.ang = f2{g.hq, g.aq * g.sg};
+  l.rate = f2{g.hqd, g.aqd * g.sg};
+  l.mom = f2{g.pih, g.pik * g.sg};
+  l.h = f2{g.hx, g.hy};
+  l.sg = g.sg;
+  l.base = g.base;
+}
+
+// cap_contact on pairs: contact force (torso frame) on a capsule end-cap at torso point x moving with vb
+__device__ __forceinline__ V3 pk_contact(const PkBody& s, const PkRot& R, const V3& x, const V3& vb) {
+  const V3 vw = rmul(R, vb);
+  const float pz = s.p.z + R.r6 * x.xy.x + R.r7 * x.xy.y + R.r8 * x.z;
+  const float pen = fmaxf(RAD - pz, 0.f);
+  const float fn = fmaxf(KC * pen - CC * vw.z * (pen > 0.f ? 1.f : 0.f), 0.f);
+  const float ivn = rsqrtf(dot2(vw.xy, vw.xy) + EPSV * EPSV);
+  return rtmul(R, mk3(vw.xy * (-MU * fn * ivn), fn));
+}
+
+// Ant._substep on pairs; tq = (hip torque, sg · ankle torque)
+__device__ __forceinline__ void art_substep_pk(PkBody& s, PkLeg& g, f2 tq) {
+  // 1. positions with the current velocities
+  s.p.xy += DT * s.v.xy;
+  s.p.z += DT * s.v.z;
+  {
+    const float w = s.qwx.x, x = s.qwx.y, y = s.qyz.x, z = s.qyz.y;
+    const float ox = s.w.xy.x, oy = s.w.xy.y, oz = s.w.z;
+    const f2 n0 = s.qwx + (DT * 0.5f) * f2{-ox * x - oy * y - oz * z, ox * w + oy * z - oz * y};
+    const f2 n1 = s.qyz + (DT * 0.5f) * f2{oy * w + oz * x - ox * z, oz * w + ox * y - oy * x};
+    const float in = rsqrtf(dot2(n0, n0) + dot2(n1, n1));
+    s.qwx = n0 * in;
+    s.qyz = n1 * in;
+  }
+  g.ang += DT * g.rate;
+  // 2. forces and velocity-product terms at the new pose, old velocities
+  const PkRot R = pk_rot(s.qwx, s.qyz);
+  const V3 vB = rtmul(R, s.v), wB = rtmul(R, s.w);
+  const float cphi = __cosf(g.base + g.ang.x), sphi = __sinf(g.base + g.ang.x), ca = __cosf(g.ang.y), sa = __sinf(g.ang.y);
+  const f2 er = f2{cphi, sphi}, ep = f2{-sphi, cphi};
+  const V3 d = mk3(er * ca, -sa), dd = mk3(er * (-sa), -ca);
+  const f2 c1 = g.h + (0.5f * L1) * er, K = g.h + L1 * er;  // z = 0
+  const V3 c2 = mk3(K + (0.5f * L2) * d.xy, -0.5f * L2 * sa), F = mk3(K + L2 * d.xy, -L2 * sa);
+  const float r2c = L1 + 0.5f * L2 * ca;
+  const f2 t1 = (0.5f * L1) * ep, t2 = r2c * ep;  // z = 0
+  const V3 s2 = mk3((0.5f * L2) * dd.xy, -0.5f * L2 * ca);
+  const float phid = g.rate.x, ad = g.rate.y;
+  // link velocities and rod-inertia angular momenta (leg_vel)
+  const V3 a1 = crs_b0(wB, c1), a2 = crs(wB, c2);
+  const V3 V1 = mk3(vB.xy + a1.xy + t1 * phid, vB.z + a1.z);
+  const V3 V2 = mk3(vB.xy + a2.xy + t2 * phid + s2.xy * ad, vB.z + a2.z + s2.z * ad);
+  const float Oz = wB.z + phid;
+  const V3 O2 = mk3(wB.xy + ep * ad, Oz);
+  const float e1 = (IA1 - IP1) * dot2(er, wB.xy), e2 = (IA2 - IP2) * dot3v(d, O2);
+  const V3 IO1 = mk3(IP1 * wB.xy + e1 * er, IP1 * Oz);
+  const V3 IO2 = mk3(IP2 * O2.xy + e2 * d.xy, IP2 * Oz + e2 * d.z);
+  // contacts at the knee (K) and the foot (F)
+  const V3 wK = crs_b0(wB, K), wF = crs(wB, F);
+  const f2 vlin = vB.xy + (L1 * phid) * ep;
+  const V3 vk = mk3(vlin + wK.xy, vB.z + wK.z);
+  const V3 vf = mk3(vlin + wF.xy + (L2 * phid * ca) * ep + (L2 * ad) * dd.xy, vB.z + wF.z + L2 * ad * dd.z);
+  const V3 fK = pk_contact(s, R, mk3(K, 0.f), vk), fF = pk_contact(s, R, F, vf);
+  const V3 gB = mk3(R.w2 * (-GRAV), -GRAV * R.r8);
+  // contact moments about the hip, the legs' first mass moment S1 = m1 c1 + m2 c2
+  const f2 kh = L1 * er;  // K − h (z = 0)
+  const V3 fh = mk3(kh + L2 * d.xy, F.z);
+  const V3 tka = mk3(perp_mul(kh, -fK.z), cross2(kh, fK.xy)), tkb = crs(fh, fF);
+  const V3 Tk = mk3(tka.xy + tkb.xy, tka.z + tkb.z);
+  const V3 S1 = mk3(M1 * c1 + M2 * c2.xy, M2 * c2.z);
+  const V3 fs = mk3(fK.xy + fF.xy, fK.z + fF.z);
+  const float Qphi = cross2(S1.xy - (M1 + M2) * g.h, gB.xy) + Tk.z;
+  const V3 hg = mk3((0.5f * M2) * gB.xy + fF.xy, 0.5f * M2 * gB.z + fF.z);
+  const float Qa = L2 * dot3v(dd, hg);
+  float dphi, da;
+  {
+    const V3 r2 = mk3(L1 * er + (0.5f * L2) * d.xy, -0.5f * L2 * sa);
+    const float wz = wB.z;
+    const float wr1 = 0.5f * L1 * dot2(wB.xy, er), wr2 = dot3v(wB, r2);
+    const float a2c = (L1 + 0.5f * L2 * ca) * phid, b2 = 0.5f * L2 * ad * sa;
+    const V3 q1 = mk3(er * (-0.5f * L1 * (wz + phid)), wr1);
+    const V3 q2 = mk3(r2.xy * (-wz) - a2c * er - b2 * ep, wr2 - r2.z * wz);
+    const f2 IO = IO1.xy + IO2.xy;
+    dphi = M1 * dot3v(V1, q1) + M2 * dot3v(V2, q2) - cross2(wB.xy, IO);
+    const V3 ws2 = crs(wB, s2);
+    const V3 dc2 = mk3(ws2.xy + (0.5f * L2) * (ep * (-phid * sa) - d.xy * ad), ws2.z - 0.5f * L2 * ad * d.z);
+    da = M2 * dot3v(V2, dc2) + (IA2 - IP2) * dot3v(O2, dd) * dot3v(O2, d);
+  }
+  // limit springs: max(lo − q, 0) − max(q − hi, 0) = clamp(q, lo, hi) − q
+  const f2 lim = f2{__builtin_amdgcn_fmed3f(g.ang.x, HIP_LO, HIP_HI), __builtin_amdgcn_fmed3f(g.ang.y, ANK_LO, ANK_HI)} - g.ang;
+  g.mom += DT * (tq - JD * g.rate + LIMK * lim + f2{Qphi + dphi, Qa + da});
+  // external wrench on the system: contacts and the legs' weight about the torso origin
+  {
+    const V3 hf = mk3(perp_mul(g.h, -fs.z), cross2(g.h, fs.xy));
+    const V3 sg_ = crs(S1, gB);
+    const V3 X0 = mk3(f2{quad_sum(fs.xy.x), quad_sum(fs.xy.y)}, quad_sum(fs.z));
+    const V3 X1 = mk3(f2{quad_sum(Tk.xy.x + hf.xy.x + sg_.xy.x), quad_sum(Tk.xy.y + hf.xy.y + sg_.xy.y)}, quad_sum(Tk.z + hf.z + sg_.z));
+    V3 FW = rmul(R, X0);
+    FW.xy -= LDAMP * s.v.xy;
+    FW.z += -MTOT * GRAV - LDAMP * s.v.z;
+    const V3 TW = rmul(R, X1), pxF = crs(s.p, FW);
+    s.P.xy += DT * FW.xy;
+    s.P.z += DT * FW.z;
+    s.L.xy += DT * (TW.xy + pxF.xy - ADAMP * s.w.xy);
+    s.L.z += DT * (TW.z + pxF.z - ADAMP * s.w.z);
+  }
+  // 3. velocities from the momenta at the new pose (solve_velocities)
+  // hinge columns of M_bj (leg_columns): bphi = (M1 t1 + M2 t2 | M1 c1×t1 + M2 c2×t2 − cz d + (IP1+IP2) e_z),
+  // ba = (M2 s2 | M2 c2×s2 + IP2 ep); stored as pairs (0,1) (2,3) (4,5) of the 6-vector
+  const float cz = (IA2 - IP2) * sa;
+  const V3 x2 = crs_b0(c2, t2), x3 = crs(c2, s2);
+  const float x1z = cross2(c1, t1);
+  const f2 bp01 = M1 * t1 + M2 * t2;
+  const f2 bpA = M2 * x2.xy - cz * d.xy;  // angular x, y
+  const float bp5 = M1 * x1z + M2 * x2.z - cz * d.z + IP1 + IP2;
+  const f2 ba01 = M2 * s2.xy;
+  const float ba2 = M2 * s2.z;
+  const f2 baA = M2 * x3.xy + IP2 * ep;
+  const float ba5 = M2 * x3.z;
+  const float bphi[6] = {bp01.x, bp01.y, 0.f, bpA.x, bpA.y, bp5};
+  const float bav[6] = {ba01.x, ba01.y, ba2, baA.x, baA.y, ba5};
+  const float Hphi = M1 * dot2(t1, t1) + M2 * dot2(t2, t2) + IP1 + IP2 + (IA2 - IP2) * sa * sa + ARM;
+  const float Ha = M2 * dot3v(s2, s2) + IP2 + ARM;
+  const f2 iH = f2{__builtin_amdgcn_rcpf(Hphi), __builtin_amdgcn_rcpf(Ha)};
+  const V3 S1b = S1;
+  const float n1 = M1 * dot2(c1, c1) + M2 * dot3v(c2, c2) + IP1 + IP2;
+  float sp[6], sq[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    sp[i] = bphi[i] * iH.x;
+    sq[i] = bav[i] * iH.y;
+  }
+  const float c1v[3] = {c1.x, c1.y, 0.f}, c2v[3] = {c2.xy.x, c2.xy.y, c2.z}, erv[3] = {er.x, er.y, 0.f}, dv[3] = {d.xy.x, d.xy.y, d.z};
+  const float S1v[3] = {S1b.xy.x, S1b.xy.y, S1b.z};
+  // the Schur complement, row pairs (A[i][j], A[i][j+1]) for even j ≥ i − 1
+  f2 A2[6][3];
+  float b[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+#pragma unroll
+    for (int jp = 0; jp < 3; ++jp) {
+      if (2 * jp + 1 < i) continue;
+      float m[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int j = 2 * jp + h;
+        float mm = 0.f;
+        if (i >= 3 && j >= 3) {
+          const int r = i - 3, c = j - 3;
+          mm = (IA1 - IP1) * erv[r] * erv[c] + (IA2 - IP2) * dv[r] * dv[c] - M1 * c1v[r] * c1v[c] - M2 * c2v[r] * c2v[c];
+          if (r == c) mm += n1;
+        } else if (i < 3 && j >= 3) {  // −[S1]×
+          const int r = i, c = j - 3;
+          if (r == 0 && c == 1) mm = S1v[2];
+          if (r == 0 && c == 2) mm = -S1v[1];
+          if (r == 1 && c == 0) mm = -S1v[2];
+          if (r == 1 && c == 2) mm = S1v[0];
+          if (r == 2 && c == 0) mm = S1v[1];
+          if (r == 2 && c == 1) mm = -S1v[0];
+        }
+        m[h] = mm;
+      }
+      const f2 bpj = f2{bphi[2 * jp], bphi[2 * jp + 1]}, baj = f2{bav[2 * jp], bav[2 * jp + 1]};
+      const f2 e = f2{m[0], m[1]} - sp[i] * bpj - sq[i] * baj;
+      A2[i][jp] = f2{quad_sum(e.x), quad_sum(e.y)};
+    }
+    b[i] = quad_sum(-sp[i] * g.mom.x - sq[i] * g.mom.y);
+  }
+  float A[6][6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) A[i][j] = (j / 2 * 2 + 1 < i) ? 0.f : (j & 1 ? A2[i][j / 2].y : A2[i][j / 2].x);
+  A[0][0] += MTOT; A[1][1] += MTOT; A[2][2] += MTOT;
+  A[3][3] += I0; A[4][4] += I0; A[5][5] += I0;
+  {
+    const V3 hP = rtmul(R, s.P);
+    const V3 pxP = crs(s.p, s.P);
+    const V3 hL = rtmul(R, mk3(s.L.xy - pxP.xy, s.L.z - pxP.z));
+    b[0] += hP.xy.x; b[1] += hP.xy.y; b[2] += hP.z;
+    b[3] += hL.xy.x; b[4] += hL.xy.y; b[5] += hL.z;
+  }
+  float u[6];
+  solve6(A, b, u);
+  const f2 u01 = f2{u[0], u[1]}, u34 = f2{u[3], u[4]};
+  const f2 bu2 = bp01 * u01 + bpA * u34, au2 = ba01 * u01 + baA * u34;
+  const float bu = bu2.x + bu2.y + bp5 * u[5], au = au2.x + au2.y + ba2 * u[2] + ba5 * u[5];
+  g.rate = (g.mom - f2{bu, au}) * iH;
+  s.v = rmul(R, mk3(u01, u[2]));
+  s.w = rmul(R, mk3(u34, u[5]));
+}
+
 // layer sizes: in = 27, hidden h1, h2 (any, ≤ 256), out = 8; tanh everywhere
 __global__ void __launch_bounds__(256) ant_rollout_kernel(const float* __restrict__ W, int64_t P, int N, int h1, int h2,
                                                           const float* __restrict__ init, int cap, float* __restrict__ ret,
@@ -574,7 +863,7 @@ typedef float ant_f4 __attribute__((ext_vector_type(4)));
 // tools/k15_mfma_probe.hip measured the isolated 64x64 layer (one wave): VALU 1100 cycles, MFMA-only
 // 4x4x1 1078, 16x16x4 with the vector padded to 16 columns 2755, split 16 / 48 907
 // (profiles/r3_k15_mfma_probe.log).
-template <int KM>
+template <int KM, bool PK>
 __global__ void __launch_bounds__(64 * ANT_WAVES, 2) ant_rollout_reg_kernel(const float* __restrict__ W, int64_t P, int N, int h1, int h2,
                                                                           const float* __restrict__ init, int cap, float* __restrict__ ret,
                                                                           int* __restrict__ steps_out, int trace) {
@@ -608,24 +897,49 @@ __global__ void __launch_bounds__(64 * ANT_WAVES, 2) ant_rollout_reg_kernel(cons
   AntBody s;
   AntLeg g;
   load_body(s, g, init, leg);
+  PkBody pb;
+  PkLeg pl;
+  if constexpr (PK) pk_from(s, g, pb, pl);
   float total = 0.f;
   int t = 0;
   for (; t < cap; ++t) {
     float o[27];
-    o[0] = s.p[2];
+    if constexpr (PK) {
+      o[0] = pb.p.z;
+      o[1] = pb.qwx.x;
+      o[2] = pb.qwx.y;
+      o[3] = pb.qyz.x;
+      o[4] = pb.qyz.y;
+      const float aq = pl.ang.y * pl.sg, aqd = pl.rate.y * pl.sg;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) o[1 + i] = s.q[i];
+      for (int l = 0; l < 4; ++l) {
+        o[5 + 2 * l] = rl(pl.ang.x, l);
+        o[6 + 2 * l] = rl(aq, l);
+        o[19 + 2 * l] = rl(pl.rate.x, l);
+        o[20 + 2 * l] = rl(aqd, l);
+      }
+      o[13] = pb.v.xy.x;
+      o[14] = pb.v.xy.y;
+      o[15] = pb.v.z;
+      o[16] = pb.w.xy.x;
+      o[17] = pb.w.xy.y;
+      o[18] = pb.w.z;
+    } else {
+      o[0] = s.p[2];
 #pragma unroll
-    for (int l = 0; l < 4; ++l) {
-      o[5 + 2 * l] = rl(g.hq, l);
-      o[6 + 2 * l] = rl(g.aq, l);
-      o[19 + 2 * l] = rl(g.hqd, l);
-      o[20 + 2 * l] = rl(g.aqd, l);
+      for (int i = 0; i < 4; ++i) o[1 + i] = s.q[i];
+#pragma unroll
+      for (int l = 0; l < 4; ++l) {
+        o[5 + 2 * l] = rl(g.hq, l);
+        o[6 + 2 * l] = rl(g.aq, l);
+        o[19 + 2 * l] = rl(g.hqd, l);
+        o[20 + 2 * l] = rl(g.aqd, l);
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) o[13 + i] = s.v[i];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) o[16 + i] = s.w[i];
     }
-#pragma unroll
-    for (int i = 0; i < 3; ++i) o[13 + i] = s.v[i];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) o[16 + i] = s.w[i];
     float acc = b1;
 #pragma unroll
     for (int i = 0; i < 27; ++i) acc = fmaf(o[i], w1[i], acc);
@@ -695,13 +1009,25 @@ __global__ void __launch_bounds__(64 * ANT_WAVES, 2) ant_rollout_reg_kernel(cons
       tau[k] = GEAR * a;
       csum += a * a;
     }
-    const float x0 = s.p[0];
     const float th = sel4(leg, tau[0], tau[2], tau[4], tau[6]), ta = sel4(leg, tau[1], tau[3], tau[5], tau[7]);
-    #pragma unroll 1
-    for (int k = 0; k < SUB; ++k) art_substep(s, g, th, ta);
-    const bool healthy = (s.p[2] >= 0.2f) && (s.p[2] <= 1.0f);
+    float x0, x1, z1;
+    if constexpr (PK) {
+      x0 = pb.p.xy.x;
+      const f2 tq = f2{th, ta * pl.sg};
+#pragma unroll 1
+      for (int k = 0; k < SUB; ++k) art_substep_pk(pb, pl, tq);
+      x1 = pb.p.xy.x;
+      z1 = pb.p.z;
+    } else {
+      x0 = s.p[0];
+#pragma unroll 1
+      for (int k = 0; k < SUB; ++k) art_substep(s, g, th, ta);
+      x1 = s.p[0];
+      z1 = s.p[2];
+    }
+    const bool healthy = (z1 >= 0.2f) && (z1 <= 1.0f);
     if (!healthy) break;
-    total += (s.p[0] - x0) * (1.f / (DT * SUB)) + 1.f - 0.5f * csum;
+    total += (x1 - x0) * (1.f / (DT * SUB)) + 1.f - 0.5f * csum;
   }
   if (lane == 0) {
     ret[ind] = total;
@@ -734,14 +1060,24 @@ void evx_ant_rollout(const float* W, int64_t P, int N, int h1, int h2, const flo
       return e ? atoi(e) : 16;
     }();
     const dim3 grid((N + ANT_WAVES - 1) / ANT_WAVES), block(64 * ANT_WAVES);
-    if (km >= 32)
-      ant_rollout_reg_kernel<32><<<grid, block, 0, s>>>(W, P, N, h1, h2, init, cap, ret, steps, trace);
+    // EVOXMI_ANT_PACKED: the packed-f32 sub-step (art_substep_pk); 0 = the scalar one
+    static const int pk = [] {
+      const char* e = getenv("EVOXMI_ANT_PACKED");
+      return e ? atoi(e) : 1;
+    }();
+    if (pk) {
+      if (km >= 16)
+        ant_rollout_reg_kernel<16, true><<<grid, block, 0, s>>>(W, P, N, h1, h2, init, cap, ret, steps, trace);
+      else
+        ant_rollout_reg_kernel<0, true><<<grid, block, 0, s>>>(W, P, N, h1, h2, init, cap, ret, steps, trace);
+    } else if (km >= 32)
+      ant_rollout_reg_kernel<32, false><<<grid, block, 0, s>>>(W, P, N, h1, h2, init, cap, ret, steps, trace);
     else if (km >= 16)
-      ant_rollout_reg_kernel<16><<<grid, block, 0, s>>>(W, P, N, h1, h2, init, cap, ret, steps, trace);
+      ant_rollout_reg_kernel<16, false><<<grid, block, 0, s>>>(W, P, N, h1, h2, init, cap, ret, steps, trace);
     else if (km >= 8)
-      ant_rollout_reg_kernel<8><<<grid, block, 0, s>>>(W, P, N, h1, h2, init, cap, ret, steps, trace);
+      ant_rollout_reg_kernel<8, false><<<grid, block, 0, s>>>(W, P, N, h1, h2, init, cap, ret, steps, trace);
     else
-      ant_rollout_reg_kernel<0><<<grid, block, 0, s>>>(W, P, N, h1, h2, init, cap, ret, steps, trace);
+      ant_rollout_reg_kernel<0, false><<<grid, block, 0, s>>>(W, P, N, h1, h2, init, cap, ret, steps, trace);
     return;
   }
   const int64_t per = (P + 32 + h1 + h2 + 8) * 4;
