@@ -55,8 +55,9 @@ __device__ __forceinline__ void cross(const float* a, const float* b, float* o) 
 __device__ __forceinline__ float dot3(const float* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 
 __device__ __forceinline__ float quad_sum(float v) {
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));  // xor 1
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));  // xor 2
+  // bound_ctrl DPP movs (no "old" operand to initialise): both stages fuse into v_add_f32_dpp
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));  // xor 1
+  v = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, true)) + v;  // xor 2
   return v;
 }
 // tanh via one v_exp and one v_rcp (|error| ~1e-7 near 0, saturates exactly)
@@ -520,6 +521,9 @@ __device__ __forceinline__ PkRot pk_rot(f2 qwx, f2 qyz) {
 __device__ __forceinline__ V3 rmul(const PkRot& R, const V3& v) {  // R v
   return mk3(R.c0 * v.xy.x + R.c1 * v.xy.y + R.c2 * v.z, R.r6 * v.xy.x + R.r7 * v.xy.y + R.r8 * v.z);
 }
+__device__ __forceinline__ V3 rmul3(const PkRot& R, float x, float y, float z) {  // R (x, y, z)
+  return mk3(R.c0 * x + R.c1 * y + R.c2 * z, R.r6 * x + R.r7 * y + R.r8 * z);
+}
 __device__ __forceinline__ V3 rtmul(const PkRot& R, const V3& v) {  // Rᵀ v
   return mk3(R.w0 * v.xy.x + R.w1 * v.xy.y + R.w2 * v.z, R.r2 * v.xy.x + R.r5 * v.xy.y + R.r8 * v.z);
 }
@@ -633,101 +637,115 @@ __device__ __forceinline__ void art_substep_pk(PkBody& s, PkLeg& g, f2 tq) {
   {
     const V3 hf = mk3(perp_mul(g.h, -fs.z), cross2(g.h, fs.xy));
     const V3 sg_ = crs(S1, gB);
-    const V3 X0 = mk3(f2{quad_sum(fs.xy.x), quad_sum(fs.xy.y)}, quad_sum(fs.z));
-    const V3 X1 = mk3(f2{quad_sum(Tk.xy.x + hf.xy.x + sg_.xy.x), quad_sum(Tk.xy.y + hf.xy.y + sg_.xy.y)}, quad_sum(Tk.z + hf.z + sg_.z));
-    V3 FW = rmul(R, X0);
+    // quad sums stay scalars (a sum written into half of a pair does not fuse into v_add_f32_dpp)
+    const f2 tx = Tk.xy + hf.xy + sg_.xy;
+    V3 FW = rmul3(R, quad_sum(fs.xy.x), quad_sum(fs.xy.y), quad_sum(fs.z));
     FW.xy -= LDAMP * s.v.xy;
     FW.z += -MTOT * GRAV - LDAMP * s.v.z;
-    const V3 TW = rmul(R, X1), pxF = crs(s.p, FW);
+    const V3 TW = rmul3(R, quad_sum(tx.x), quad_sum(tx.y), quad_sum(Tk.z + hf.z + sg_.z)), pxF = crs(s.p, FW);
     s.P.xy += DT * FW.xy;
     s.P.z += DT * FW.z;
     s.L.xy += DT * (TW.xy + pxF.xy - ADAMP * s.w.xy);
     s.L.z += DT * (TW.z + pxF.z - ADAMP * s.w.z);
   }
-  // 3. velocities from the momenta at the new pose (solve_velocities)
+  // 3. velocities from the momenta at the new pose (solve_velocities), in the permuted basis
+  // (lin x, lin y | ang x, ang y | lin z, ang z) so that every pair of the 6-vectors and of the
+  // Schur-complement rows is an (x, y) pair of the 3-vector algebra.
   // hinge columns of M_bj (leg_columns): bphi = (M1 t1 + M2 t2 | M1 c1×t1 + M2 c2×t2 − cz d + (IP1+IP2) e_z),
-  // ba = (M2 s2 | M2 c2×s2 + IP2 ep); stored as pairs (0,1) (2,3) (4,5) of the 6-vector
+  // ba = (M2 s2 | M2 c2×s2 + IP2 ep)
   const float cz = (IA2 - IP2) * sa;
   const V3 x2 = crs_b0(c2, t2), x3 = crs(c2, s2);
   const float x1z = cross2(c1, t1);
-  const f2 bp01 = M1 * t1 + M2 * t2;
-  const f2 bpA = M2 * x2.xy - cz * d.xy;  // angular x, y
-  const float bp5 = M1 * x1z + M2 * x2.z - cz * d.z + IP1 + IP2;
-  const f2 ba01 = M2 * s2.xy;
-  const float ba2 = M2 * s2.z;
-  const f2 baA = M2 * x3.xy + IP2 * ep;
-  const float ba5 = M2 * x3.z;
-  const float bphi[6] = {bp01.x, bp01.y, 0.f, bpA.x, bpA.y, bp5};
-  const float bav[6] = {ba01.x, ba01.y, ba2, baA.x, baA.y, ba5};
+  f2 Bp[3], Ba[3];
+  Bp[0] = M1 * t1 + M2 * t2;
+  Bp[1] = M2 * x2.xy - cz * d.xy;
+  Bp[2] = f2{0.f, M1 * x1z + M2 * x2.z - cz * d.z + IP1 + IP2};  // lin z of bphi is 0
+  Ba[0] = M2 * s2.xy;
+  Ba[1] = M2 * x3.xy + IP2 * ep;
+  Ba[2] = f2{M2 * s2.z, M2 * x3.z};
   const float Hphi = M1 * dot2(t1, t1) + M2 * dot2(t2, t2) + IP1 + IP2 + (IA2 - IP2) * sa * sa + ARM;
   const float Ha = M2 * dot3v(s2, s2) + IP2 + ARM;
   const f2 iH = f2{__builtin_amdgcn_rcpf(Hphi), __builtin_amdgcn_rcpf(Ha)};
-  const V3 S1b = S1;
   const float n1 = M1 * dot2(c1, c1) + M2 * dot3v(c2, c2) + IP1 + IP2;
-  float sp[6], sq[6];
+  f2 Sp[3], Sq[3];
 #pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    sp[i] = bphi[i] * iH.x;
-    sq[i] = bav[i] * iH.y;
+  for (int q = 0; q < 3; ++q) {
+    Sp[q] = Bp[q] * iH.x;
+    Sq[q] = Ba[q] * iH.y;
   }
-  const float c1v[3] = {c1.x, c1.y, 0.f}, c2v[3] = {c2.xy.x, c2.xy.y, c2.z}, erv[3] = {er.x, er.y, 0.f}, dv[3] = {d.xy.x, d.xy.y, d.z};
-  const float S1v[3] = {S1b.xy.x, S1b.xy.y, S1b.z};
-  // the Schur complement, row pairs (A[i][j], A[i][j+1]) for even j ≥ i − 1
+  // composite-inertia block (ang, ang) rows x, y over columns (x, y): er_r ER + d_r DD − c1_r C1 − c2_r C2
+  const f2 ER = (IA1 - IP1) * er, DD = (IA2 - IP2) * d.xy, C1 = M1 * c1, C2 = M2 * c2.xy;
+  const float DDz = (IA2 - IP2) * d.z, C2z = M2 * c2.z;
+  f2 M[6][3];  // the leg's m(i, pair) before the Schur terms; only pairs with 2·jp + 1 ≥ i are used
+  M[0][0] = f2{0.f, 0.f};
+  M[0][1] = f2{0.f, S1.z};
+  M[0][2] = f2{0.f, -S1.xy.y};
+  M[1][0] = f2{0.f, 0.f};
+  M[1][1] = f2{-S1.z, 0.f};
+  M[1][2] = f2{0.f, S1.xy.x};
+  M[2][1] = er.x * ER + d.xy.x * DD - c1.x * C1 - c2.xy.x * C2;
+  M[2][1].x += n1;
+  M[2][2] = f2{S1.xy.y, d.xy.x * DDz - c2.xy.x * C2z};
+  M[3][1] = er.y * ER + d.xy.y * DD - c1.y * C1 - c2.xy.y * C2;
+  M[3][1].y += n1;
+  M[3][2] = f2{-S1.xy.x, d.xy.y * DDz - c2.xy.y * C2z};
+  M[4][2] = f2{0.f, 0.f};
+  M[5][2] = f2{0.f, d.z * DDz - c2.z * C2z + n1};
   f2 A2[6][3];
   float b[6];
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
+    const float spi = (i & 1) ? Sp[i / 2].y : Sp[i / 2].x, sqi = (i & 1) ? Sq[i / 2].y : Sq[i / 2].x;
 #pragma unroll
-    for (int jp = 0; jp < 3; ++jp) {
-      if (2 * jp + 1 < i) continue;
-      float m[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int j = 2 * jp + h;
-        float mm = 0.f;
-        if (i >= 3 && j >= 3) {
-          const int r = i - 3, c = j - 3;
-          mm = (IA1 - IP1) * erv[r] * erv[c] + (IA2 - IP2) * dv[r] * dv[c] - M1 * c1v[r] * c1v[c] - M2 * c2v[r] * c2v[c];
-          if (r == c) mm += n1;
-        } else if (i < 3 && j >= 3) {  // −[S1]×
-          const int r = i, c = j - 3;
-          if (r == 0 && c == 1) mm = S1v[2];
-          if (r == 0 && c == 2) mm = -S1v[1];
-          if (r == 1 && c == 0) mm = -S1v[2];
-          if (r == 1 && c == 2) mm = S1v[0];
-          if (r == 2 && c == 0) mm = S1v[1];
-          if (r == 2 && c == 1) mm = -S1v[0];
-        }
-        m[h] = mm;
-      }
-      const f2 bpj = f2{bphi[2 * jp], bphi[2 * jp + 1]}, baj = f2{bav[2 * jp], bav[2 * jp + 1]};
-      const f2 e = f2{m[0], m[1]} - sp[i] * bpj - sq[i] * baj;
-      A2[i][jp] = f2{quad_sum(e.x), quad_sum(e.y)};
+    for (int jp = i / 2; jp < 3; ++jp) {
+      const f2 e = M[i][jp] - spi * Bp[jp] - sqi * Ba[jp];
+      A2[i][jp].y = quad_sum(e.y);
+      A2[i][jp].x = (2 * jp >= i) ? quad_sum(e.x) : 0.f;  // the pair's lower entry is never read
     }
-    b[i] = quad_sum(-sp[i] * g.mom.x - sq[i] * g.mom.y);
   }
-  float A[6][6];
 #pragma unroll
-  for (int i = 0; i < 6; ++i)
-#pragma unroll
-    for (int j = 0; j < 6; ++j) A[i][j] = (j / 2 * 2 + 1 < i) ? 0.f : (j & 1 ? A2[i][j / 2].y : A2[i][j / 2].x);
-  A[0][0] += MTOT; A[1][1] += MTOT; A[2][2] += MTOT;
-  A[3][3] += I0; A[4][4] += I0; A[5][5] += I0;
+  for (int q = 0; q < 3; ++q) {
+    const f2 e = -Sp[q] * g.mom.x - Sq[q] * g.mom.y;
+    b[2 * q] = quad_sum(e.x);
+    b[2 * q + 1] = quad_sum(e.y);
+  }
+  A2[0][0].x += MTOT; A2[1][0].y += MTOT; A2[4][2].x += MTOT;
+  A2[2][1].x += I0; A2[3][1].y += I0; A2[5][2].y += I0;
   {
     const V3 hP = rtmul(R, s.P);
     const V3 pxP = crs(s.p, s.P);
     const V3 hL = rtmul(R, mk3(s.L.xy - pxP.xy, s.L.z - pxP.z));
-    b[0] += hP.xy.x; b[1] += hP.xy.y; b[2] += hP.z;
-    b[3] += hL.xy.x; b[4] += hL.xy.y; b[5] += hL.z;
+    b[0] += hP.xy.x; b[1] += hP.xy.y; b[2] += hL.xy.x;
+    b[3] += hL.xy.y; b[4] += hP.z; b[5] += hL.z;
   }
-  float u[6];
-  solve6(A, b, u);
-  const f2 u01 = f2{u[0], u[1]}, u34 = f2{u[3], u[4]};
-  const f2 bu2 = bp01 * u01 + bpA * u34, au2 = ba01 * u01 + baA * u34;
-  const float bu = bu2.x + bu2.y + bp5 * u[5], au = au2.x + au2.y + ba2 * u[2] + ba5 * u[5];
-  g.rate = (g.mom - f2{bu, au}) * iH;
-  s.v = rmul(R, mk3(u01, u[2]));
-  s.w = rmul(R, mk3(u34, u[5]));
+  // Gaussian elimination on the upper triangle (solve6), the row updates as pair FMAs
+  float inv[6], u[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    inv[k] = __builtin_amdgcn_rcpf((k & 1) ? A2[k][k / 2].y : A2[k][k / 2].x);
+    f2 Fp[3];
+#pragma unroll
+    for (int jp = (k + 1) / 2; jp < 3; ++jp) Fp[jp] = A2[k][jp] * inv[k];
+#pragma unroll
+    for (int i = k + 1; i < 6; ++i) {
+      const float f = (i & 1) ? Fp[i / 2].y : Fp[i / 2].x;
+#pragma unroll
+      for (int jp = i / 2; jp < 3; ++jp) A2[i][jp] -= f * A2[k][jp];
+      b[i] -= f * b[k];
+    }
+  }
+#pragma unroll
+  for (int k = 5; k >= 0; --k) {
+    float r = b[k];
+#pragma unroll
+    for (int j = k + 1; j < 6; ++j) r -= ((j & 1) ? A2[k][j / 2].y : A2[k][j / 2].x) * u[j];
+    u[k] = r * inv[k];
+  }
+  const f2 U0 = f2{u[0], u[1]}, U1 = f2{u[2], u[3]}, U2 = f2{u[4], u[5]};
+  const f2 bu2 = Bp[0] * U0 + Bp[1] * U1 + Bp[2] * U2, au2 = Ba[0] * U0 + Ba[1] * U1 + Ba[2] * U2;
+  g.rate = (g.mom - f2{bu2.x + bu2.y, au2.x + au2.y}) * iH;
+  s.v = rmul(R, mk3(U0, u[4]));
+  s.w = rmul(R, mk3(U1, u[5]));
 }
 
 // layer sizes: in = 27, hidden h1, h2 (any, ≤ 256), out = 8; tanh everywhere
