@@ -476,6 +476,21 @@ __device__ __forceinline__ f2 perp_fms(f2 a, float s, f2 c) {  // perp(a)·s −
   asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,0,1] neg_lo:[1,0,1] neg_hi:[0,0,1]" : "=v"(d) : "v"(a), "v"(lo2(s)), "v"(c));
   return d;
 }
+__device__ __forceinline__ f2 negx_fma(f2 a, float s, f2 c) {  // (−a.x, a.y)·s + c
+  f2 d;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1] neg_lo:[1,0,0]" : "=v"(d) : "v"(a), "v"(lo2(s)), "v"(c));
+  return d;
+}
+__device__ __forceinline__ f2 nswap_fma(f2 a, float s, f2 c) {  // −(a.y, a.x)·s + c
+  f2 d;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,0,1] neg_lo:[1,0,0] neg_hi:[1,0,0]" : "=v"(d) : "v"(a), "v"(lo2(s)), "v"(c));
+  return d;
+}
+__device__ __forceinline__ f2 nperp_fma_hi(f2 a, f2 t, f2 c) {  // −perp(a)·t.y + c = (a.y, −a.x)·t.y + c
+  f2 d;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[1,0,0]" : "=v"(d) : "v"(a), "v"(t), "v"(c));
+  return d;
+}
 __device__ __forceinline__ float cross2(f2 a, f2 b) { return a.x * b.y - a.y * b.x; }
 __device__ __forceinline__ float dot2(f2 a, f2 b) { return a.x * b.x + a.y * b.y; }
 
@@ -569,10 +584,13 @@ __device__ __forceinline__ void art_substep_pk(PkBody& s, PkLeg& g, f2 tq) {
   s.p.xy += DT * s.v.xy;
   s.p.z += DT * s.v.z;
   {
-    const float w = s.qwx.x, x = s.qwx.y, y = s.qyz.x, z = s.qyz.y;
-    const float ox = s.w.xy.x, oy = s.w.xy.y, oz = s.w.z;
-    const f2 n0 = s.qwx + (DT * 0.5f) * f2{-ox * x - oy * y - oz * z, ox * w + oy * z - oz * y};
-    const f2 n1 = s.qyz + (DT * 0.5f) * f2{oy * w + oz * x - ox * z, oz * w + ox * y - oy * x};
+    // q += ½ dt · ω ⊗ q on the pairs (w, x), (y, z):
+    // (w, x) += hox (−x, w) + hoy (−y, z) − hoz (z, y);  (y, z) += hox (−z, y) + w (hoy, hoz) + x (hoz, −hoy)
+    const f2 ho = (DT * 0.5f) * s.w.xy;
+    const float hoz = (DT * 0.5f) * s.w.z;
+    const f2 n0 = nswap_fma(s.qyz, hoz, negx_fma(s.qyz, ho.y, perp_fma(s.qwx, ho.x, s.qwx)));
+    const f2 hyz = f2{ho.y, hoz};
+    const f2 n1 = nperp_fma_hi(hyz, s.qwx, hyz * s.qwx.x + perp_fma(s.qyz, ho.x, s.qyz));
     const float in = rsqrtf(dot2(n0, n0) + dot2(n1, n1));
     s.qwx = n0 * in;
     s.qyz = n1 * in;
@@ -677,19 +695,23 @@ __device__ __forceinline__ void art_substep_pk(PkBody& s, PkLeg& g, f2 tq) {
   const f2 ER = (IA1 - IP1) * er, DD = (IA2 - IP2) * d.xy, C1 = M1 * c1, C2 = M2 * c2.xy;
   const float DDz = (IA2 - IP2) * d.z, C2z = M2 * c2.z;
   f2 M[6][3];  // the leg's m(i, pair) before the Schur terms; only pairs with 2·jp + 1 ≥ i are used
-  M[0][0] = f2{0.f, 0.f};
-  M[0][1] = f2{0.f, S1.z};
-  M[0][2] = f2{0.f, -S1.xy.y};
-  M[1][0] = f2{0.f, 0.f};
-  M[1][1] = f2{-S1.z, 0.f};
-  M[1][2] = f2{0.f, S1.xy.x};
+  // −[S1]× (lin rows, ang columns) and its transpose enter as scalar adds on single halves
+  // (i, jp, half) → term; every index is a compile-time constant after unrolling
+  auto sterm = [&](int i, int jp, int h, float v) -> float {
+    if (i == 0 && jp == 1 && h == 1) return v + S1.z;
+    if (i == 0 && jp == 2 && h == 1) return v - S1.xy.y;
+    if (i == 1 && jp == 1 && h == 0) return v - S1.z;
+    if (i == 1 && jp == 2 && h == 1) return v + S1.xy.x;
+    if (i == 2 && jp == 2 && h == 0) return v + S1.xy.y;
+    if (i == 3 && jp == 2 && h == 0) return v - S1.xy.x;
+    return v;
+  };
   M[2][1] = er.x * ER + d.xy.x * DD - c1.x * C1 - c2.xy.x * C2;
   M[2][1].x += n1;
-  M[2][2] = f2{S1.xy.y, d.xy.x * DDz - c2.xy.x * C2z};
+  M[2][2] = f2{0.f, d.xy.x * DDz - c2.xy.x * C2z};
   M[3][1] = er.y * ER + d.xy.y * DD - c1.y * C1 - c2.xy.y * C2;
   M[3][1].y += n1;
-  M[3][2] = f2{-S1.xy.x, d.xy.y * DDz - c2.xy.y * C2z};
-  M[4][2] = f2{0.f, 0.f};
+  M[3][2] = f2{0.f, d.xy.y * DDz - c2.xy.y * C2z};
   M[5][2] = f2{0.f, d.z * DDz - c2.z * C2z + n1};
   f2 A2[6][3];
   float b[6];
@@ -698,9 +720,11 @@ __device__ __forceinline__ void art_substep_pk(PkBody& s, PkLeg& g, f2 tq) {
     const float spi = (i & 1) ? Sp[i / 2].y : Sp[i / 2].x, sqi = (i & 1) ? Sq[i / 2].y : Sq[i / 2].x;
 #pragma unroll
     for (int jp = i / 2; jp < 3; ++jp) {
-      const f2 e = M[i][jp] - spi * Bp[jp] - sqi * Ba[jp];
-      A2[i][jp].y = quad_sum(e.y);
-      A2[i][jp].x = (2 * jp >= i) ? quad_sum(e.x) : 0.f;  // the pair's lower entry is never read
+      const bool mz = i < 2 || i == 4;  // rows whose M pairs are zero
+      const f2 e0 = mz ? -spi * Bp[jp] : M[i][jp] - spi * Bp[jp];
+      const f2 e = e0 - sqi * Ba[jp];
+      A2[i][jp].y = quad_sum(sterm(i, jp, 1, e.y));
+      A2[i][jp].x = (2 * jp >= i) ? quad_sum(sterm(i, jp, 0, e.x)) : 0.f;  // the pair's lower entry is never read
     }
   }
 #pragma unroll
@@ -718,6 +742,7 @@ __device__ __forceinline__ void art_substep_pk(PkBody& s, PkLeg& g, f2 tq) {
     b[0] += hP.xy.x; b[1] += hP.xy.y; b[2] += hL.xy.x;
     b[3] += hL.xy.y; b[4] += hP.z; b[5] += hL.z;
   }
+  f2 bv[3] = {f2{b[0], b[1]}, f2{b[2], b[3]}, f2{b[4], b[5]}};
   // Gaussian elimination on the upper triangle (solve6), the row updates as pair FMAs
   float inv[6], u[6];
 #pragma unroll
@@ -731,12 +756,16 @@ __device__ __forceinline__ void art_substep_pk(PkBody& s, PkLeg& g, f2 tq) {
       const float f = (i & 1) ? Fp[i / 2].y : Fp[i / 2].x;
 #pragma unroll
       for (int jp = i / 2; jp < 3; ++jp) A2[i][jp] -= f * A2[k][jp];
-      b[i] -= f * b[k];
     }
+    // b_i −= f_i b_k: whole pairs when both entries are below row k
+    const float bk = (k & 1) ? bv[k / 2].y : bv[k / 2].x;
+    if (!(k & 1)) bv[k / 2].y -= Fp[k / 2].y * bk;
+#pragma unroll
+    for (int jp = k / 2 + 1; jp < 3; ++jp) bv[jp] -= Fp[jp] * bk;
   }
 #pragma unroll
   for (int k = 5; k >= 0; --k) {
-    float r = b[k];
+    float r = (k & 1) ? bv[k / 2].y : bv[k / 2].x;
 #pragma unroll
     for (int j = k + 1; j < 6; ++j) r -= ((j & 1) ? A2[k][j / 2].y : A2[k][j / 2].x) * u[j];
     u[k] = r * inv[k];
