@@ -171,10 +171,12 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "fp32",
-            # the framework GEMM's arithmetic (gemm_ks.hip): an exact 3-way bf16 split with six
-            # bf16 MFMA products, f32-accurate (tests/test_gemm_ks.py: the 2e-6·Σ|ab| bound)
-            "gemm_precision": {"x6": "bf16x6 (f32-accurate)", "x6w": "bf16x6 32x32 (f32-accurate)",
-                               "f32": "f32 MFMA"}.get(config.get("gemm_prec"), config.get("gemm_prec")),
+            # the framework GEMMs' arithmetic: square products on gemm_ks.hip (an exact 3-way bf16
+            # split with six bf16 MFMA products), the tall 10 000-row products on gemm_blk.hip (per-row
+            # scaled f16 pairs, three f16 MFMA products); both f32-accurate (tests/test_gemm_ks.py,
+            # tests/test_gemm_blk.py: the 2e-6·Σ|ab| bound)
+            "gemm_precision": ({"x6": "bf16x6", "x6w": "bf16x6 32x32", "f32": "f32 MFMA"}.get(config.get("gemm_prec"), config.get("gemm_prec"))
+                               + (" square / f16x3 tall" if config.get("gemm_tall") == "h3" else "") + " (f32-accurate)"),
             "data": f"synthetic (seeded CEC'22 F{args.func} shift + Haar rotation at d={args.dim}; random init mean)",
             "generations_per_sec": round(gens_per_s, 3),
             "config": {
