@@ -31,10 +31,10 @@ def _front(x, bdim, B):
     return x.movedim(bdim, 0).contiguous()
 
 
-def _philox_words(info, in_dims, key, nblocks, domain, offset):
+def _philox_words(info, in_dims, key, nblocks, domain, offset, words=4):
     if in_dims[0] is None:
-        return _ext.ops().philox_words(key, nblocks, domain, offset), None
-    return _ext.ops().philox_words(_front(key, in_dims[0], info.batch_size), nblocks, domain, offset), 0
+        return _ext.ops().philox_words(key, nblocks, domain, offset, words), None
+    return _ext.ops().philox_words(_front(key, in_dims[0], info.batch_size), nblocks, domain, offset, words), 0
 
 
 def _philox_fill(info, in_dims, key, n, dist, offset):
