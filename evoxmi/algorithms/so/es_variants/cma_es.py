@@ -280,8 +280,9 @@ class CMAES(Algorithm):
         return population, state.update(population=population, count_iter=state.count_iter + 1, key=key)
 
     # ------------------------------------------------------------------ tell
-    def _weighted_stats(self, state, population, order_i32, K: int, wvec, gather: bool):
-        """(Σ wᵢ(xᵢ − m), Σ wᵢ yᵢ yᵢᵀ) with yᵢ = (xᵢ − m)/σ."""
+    def _weighted_stats(self, state, population, order_i32, K: int, wvec, gather: bool, s_out=None):
+        """(Σ wᵢ(xᵢ − m), Σ wᵢ yᵢ yᵢᵀ) with yᵢ = (xᵢ − m)/σ; ``s_out``: a (d, d) buffer the
+        framework GEMM writes S into (the sharded tell's all-reduce buffer)."""
         d = self.dim
         if population.is_cuda:
             rows = order_i32 if gather else None
@@ -300,7 +301,7 @@ class CMAES(Algorithm):
                                                 wvec.contiguous())
                 if config.get("plain_gemm") == "blas":
                     return dm, torch.mm(Yw.t(), Yw)
-                return dm, mm(Yw, Yw, ta=True, mode=1)
+                return dm, mm(Yw, Yw, ta=True, mode=1, out=s_out)
             splits = max(1, min(16, K // 256))
             S = gemm(
                 Operand(population, rc=True, gather=rows, sub=state.mean, kw=wvec, sscale=one_over, sscale_inv=True),
@@ -452,12 +453,18 @@ class CMAES(Algorithm):
             _, lorder = argsort(floc)
         lsel = lorder[:K].contiguous()
         wsel = wfull[start : start + size].index_select(0, lsel.long()).contiguous()
-        dm, S = self._weighted_stats(state, state.population, lsel, K, wsel, gather=True)
-        buf = torch.cat([dm.reshape(-1), S.reshape(-1)])
+        d = self.dim
+        # one (d² + d) buffer for the all-reduce: S (first, so its rows stay 16-byte aligned) is
+        # written into it by the GEMM, no 4 MB concatenation
+        buf = torch.empty(d * d + d, dtype=torch.float32, device=fitness.device)
+        Sv = buf[: d * d].view(d, d)
+        dm, S = self._weighted_stats(state, state.population, lsel, K, wsel, gather=True, s_out=Sv)
+        buf[d * d :].copy_(dm.reshape(-1))
+        if S.data_ptr() != Sv.data_ptr():
+            Sv.copy_(S)
         with profiling.phase("all_reduce"):
             dist.all_reduce_(buf)
-        d = self.dim
-        return self._finish_tell(state, buf[:d], buf[d:].reshape(d, d))
+        return self._finish_tell(state, buf[d * d :], Sv)
 
 
 class SepCMAES(ColumnSeparable, CMAES):
