@@ -5,6 +5,8 @@
 //  * ant_rollout_reg_kernel (h1, h2 <= 64): weights in VGPRs, lane j = hidden unit j;
 //  * ant_rollout_kernel (larger layers): weights in LDS, lanes stride over units
 //    ((in, out) row-major, so a row read is contiguous across lanes).
+// Both integrate with the packed-f32 sub-step (art_substep_pk below); the scalar art_substep
+// stays as its readable form and as the register kernel's EVOXMI_ANT_PACKED=0 A/B path.
 //
 // Physics (mirrors evoxmi/problems/neuroevolution/reinforcement_learning/envs.py:Ant, the CPU
 // oracle; constants below must match ANT / ant_derived there): the free-floating 14-DOF tree
@@ -800,32 +802,41 @@ __global__ void __launch_bounds__(256) ant_rollout_kernel(const float* __restric
   const float* B2 = W2 + h1 * h2;
   const float* W3 = B2 + h2;
   const float* B3 = W3 + h2 * 8;
-  AntBody s;
-  AntLeg g;
+  AntBody s0;
+  AntLeg g0;
   const int leg = lane & 3;
-  load_body(s, g, init, leg);
+  load_body(s0, g0, init, leg);
+  // the packed-f32 sub-step (art_substep_pk), as in the register-resident kernel
+  PkBody s;
+  PkLeg g;
+  pk_from(s0, g0, s, g);
   float total = 0.f;
   int t = 0;
   for (; t < cap; ++t) {
     // observation → LDS (the joints come from the leg-owning lanes 0-3)
     float jq[8], jqd[8];
+    const float aq = g.ang.y * g.sg, aqd = g.rate.y * g.sg;
 #pragma unroll
     for (int l = 0; l < 4; ++l) {
-      jq[2 * l] = rl(g.hq, l);
-      jq[2 * l + 1] = rl(g.aq, l);
-      jqd[2 * l] = rl(g.hqd, l);
-      jqd[2 * l + 1] = rl(g.aqd, l);
+      jq[2 * l] = rl(g.ang.x, l);
+      jq[2 * l + 1] = rl(aq, l);
+      jqd[2 * l] = rl(g.rate.x, l);
+      jqd[2 * l + 1] = rl(aqd, l);
     }
     if (lane == 0) {
-      a0[0] = s.p[2];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) a0[1 + i] = s.q[i];
+      a0[0] = s.p.z;
+      a0[1] = s.qwx.x;
+      a0[2] = s.qwx.y;
+      a0[3] = s.qyz.x;
+      a0[4] = s.qyz.y;
 #pragma unroll
       for (int i = 0; i < 8; ++i) a0[5 + i] = jq[i];
-#pragma unroll
-      for (int i = 0; i < 3; ++i) a0[13 + i] = s.v[i];
-#pragma unroll
-      for (int i = 0; i < 3; ++i) a0[16 + i] = s.w[i];
+      a0[13] = s.v.xy.x;
+      a0[14] = s.v.xy.y;
+      a0[15] = s.v.z;
+      a0[16] = s.w.xy.x;
+      a0[17] = s.w.xy.y;
+      a0[18] = s.w.z;
 #pragma unroll
       for (int i = 0; i < 8; ++i) a0[19 + i] = jqd[i];
     }
@@ -857,12 +868,13 @@ __global__ void __launch_bounds__(256) ant_rollout_kernel(const float* __restric
       csum += act[j] * act[j];
     }
     __builtin_amdgcn_wave_barrier();  // a0..a3 are rewritten next step
-    const float x0 = s.p[0];
+    const float x0 = s.p.xy.x;
     const float th = sel4(leg, tau[0], tau[2], tau[4], tau[6]), ta = sel4(leg, tau[1], tau[3], tau[5], tau[7]);
-    for (int k = 0; k < SUB; ++k) art_substep(s, g, th, ta);
-    const bool healthy = (s.p[2] >= 0.2f) && (s.p[2] <= 1.0f);
+    const f2 tq = f2{th, ta * g.sg};
+    for (int k = 0; k < SUB; ++k) art_substep_pk(s, g, tq);
+    const bool healthy = (s.p.z >= 0.2f) && (s.p.z <= 1.0f);
     if (!healthy) break;  // sticky done: the terminating step earns nothing
-    total += (s.p[0] - x0) * (1.f / (DT * SUB)) + 1.f - 0.5f * csum;
+    total += (s.p.xy.x - x0) * (1.f / (DT * SUB)) + 1.f - 0.5f * csum;
   }
   if (lane == 0) {
     ret[ind] = total;
