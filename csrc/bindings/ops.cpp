@@ -562,7 +562,7 @@ void sbr_dev_ctrl(const at::Tensor& part, int64_t nparts, int64_t j, int64_t K, 
                   at::Tensor& ctrl, at::Tensor& st, std::vector<double> prm, int64_t ns_iters, const at::Tensor& A, at::Tensor& w_out,
                   at::Tensor& eig_stats, at::Tensor& w_init, at::Tensor& log, at::Tensor& log_count) {
   TORCH_CHECK(log.scalar_type() == at::kDouble && log.is_contiguous() && log_count.scalar_type() == at::kInt, "sbr_dev_ctrl: log");
-  TORCH_CHECK(prm.size() >= 8, "sbr_dev_ctrl: params [tol, ns_kappa, damp_kappa, t4_kappa, near_only, theta0, theta_kappa, lean_from, (recover, lean_guard)]");
+  TORCH_CHECK(prm.size() >= 8, "sbr_dev_ctrl: params [tol, ns_kappa, damp_kappa, t4_kappa, near_only, theta0, theta_kappa, lean_from, (recover, lean_guard, xgate, damp_from)]");
   TORCH_CHECK(hist.scalar_type() == at::kDouble && hist.numel() >= 4 * (K + 1) && ctrl.numel() >= 8 * K && alpha.numel() >= K + 1 &&
                   theta.numel() >= K && st.numel() >= 8 && part.numel() >= 4 * nparts, "sbr_dev_ctrl: buffers");
   float p6[7] = {(float)prm[0], (float)prm[1], (float)prm[2], (float)prm[3], (float)prm[4], (float)prm[5], (float)prm[6]};
@@ -570,7 +570,8 @@ void sbr_dev_ctrl(const at::Tensor& part, int64_t nparts, int64_t j, int64_t K, 
                    theta.data_ptr<float>(), ctrl.data_ptr<int>(), st.data_ptr<int>(), p6, (int)ns_iters, A.data_ptr<float>(), A.stride(0),
                    (int)A.size(0), w_out.data_ptr<float>(), eig_stats.data_ptr<double>(), w_init.data_ptr<float>(),
                    log.data_ptr<double>(), (int)(log.numel() / 4), log_count.data_ptr<int>(), cur_stream(), (int)prm[7],
-                   prm.size() > 8 ? (int)prm[8] : 0, prm.size() > 9 ? (int)prm[9] : 0, prm.size() > 10 ? (int)prm[10] : 0);
+                   prm.size() > 8 ? (int)prm[8] : 0, prm.size() > 9 ? (int)prm[9] : 0, prm.size() > 10 ? (int)prm[10] : 0,
+                   prm.size() > 11 ? (int)prm[11] : -1);
 }
 
 std::vector<at::Tensor> argsort_f32(const at::Tensor& keys, int64_t descending) {

@@ -289,7 +289,7 @@ void evx_sbr_dev_copy(const float* src, float* dst, int64_t n, const int* skip, 
 void evx_sbr_report(const double* stats, int* seq, double* ring, int R, hipStream_t s);
 void evx_sbr_dev_ctrl(const double* part, int nparts, int j, int K, double* hist, float* alpha, float* theta, int* ctrl, int* st,
                       const float* prm6, int ns_iters, const float* A, int64_t lda, int n, float* w_out, double* eig_stats, float* w_init,
-                      double* log, int log_len, int* log_count, hipStream_t s, int lean_from = 1 << 30, int recover = 0, int lean_guard = 0, int xgate = 0);
+                      double* log, int log_len, int* log_count, hipStream_t s, int lean_from = 1 << 30, int recover = 0, int lean_guard = 0, int xgate = 0, int damp_from = -1);
 // far generator + Bq in one launch (skip_far / skip_bq: their control words)
 void evx_sbr16_far_bq(const float* A, int n, int64_t lda, const int* perm, const float* Q, const float* dq, const double* stats,
                       float thr_fac, const float* theta_ptr, float* X, int64_t ldx, const float* B, int rows, int64_t ldb, float* Bq,

@@ -48,6 +48,7 @@ struct SbrDevParams {
   int recover;    // divergences recovered by a forced damped step before the solve gives up (0: stop at the first)
   int lean_guard; // 1: a lean slot whose step would need damping / Newton–Schulz / order 6 stops the solve (capped)
   int xgate;      // 1: the damping kernels are scheduled for every full-slot far step and gate themselves (sbr_dev_prep)
+  int damp_from;  // slots ≥ damp_from carry no damping kernels (≤ lean_from; the late schedule keeps them in slot 0 only)
 };
 
 __device__ __forceinline__ void rel_kappa(const double* h, double& r, double& k) {
@@ -270,6 +271,7 @@ __global__ void __launch_bounds__(256) sbr_dev_ctrl_kernel(const double* __restr
     if (nx < K) {
       int* c = ctrl + 8 * nx;
       const bool lean = nx >= prm.lean_from;
+      const bool nodamp = nx >= prm.damp_from;  // no damping kernels in this slot (lean slots have none either)
       if (!st[0]) {
         // step size of the iteration just run (1 at the start); a lean slot's step is bounded
         // to a negligible Taylor remainder (sbr_dev_prep), so its α < 1 asks for no Newton–Schulz
@@ -286,7 +288,7 @@ __global__ void __launch_bounds__(256) sbr_dev_ctrl_kernel(const double* __restr
         // (a lean slot still takes an order-4 step where the rules would pick order 6: the
         // truncation is O(‖X‖⁵/120) and stays orthogonal to that order; damping and
         // Newton–Schulz are the safety steps it cannot skip)
-        if (lean && far && prm.lean_guard && (ns || damp)) {
+        if (far && prm.lean_guard && ((lean && (ns || damp)) || (nodamp && damp))) {
           // the lean slot has no damping / Newton–Schulz / order-6 kernels: taking its plain
           // order-4 step here is unguarded — stop, capped (the host escalates the schedule)
           st[7] |= 2;
@@ -295,7 +297,7 @@ __global__ void __launch_bounds__(256) sbr_dev_ctrl_kernel(const double* __restr
           c[0] = 0;
           c[1] = far ? 0 : 1;
           // 0: damp (κ rule), 2: the generator's free bounds decide (xgate), 1: no damping
-          c[2] = (far && !lean) ? (damp ? 0 : (prm.xgate ? 2 : 1)) : 1;
+          c[2] = (far && !lean && !nodamp) ? (damp ? 0 : (prm.xgate ? 2 : 1)) : 1;
           c[3] = (far && six && !lean) ? 0 : 1;
           c[4] = (six && !lean) ? 1 : 0;
           c[5] = (far && ns && !lean) ? 0 : 1;
@@ -385,8 +387,10 @@ void evx_sbr_dev_copy(const float* src, float* dst, int64_t n, const int* skip, 
 
 void evx_sbr_dev_ctrl(const double* part, int nparts, int j, int K, double* hist, float* alpha, float* theta, int* ctrl, int* st,
                       const float* prm6, int ns_iters, const float* A, int64_t lda, int n, float* w_out, double* eig_stats, float* w_init,
-                      double* log, int log_len, int* log_count, hipStream_t s, int lean_from, int recover, int lean_guard, int xgate) {
-  SbrDevParams p{prm6[0], prm6[1], prm6[2], prm6[3], prm6[4], prm6[5], prm6[6], ns_iters, lean_from, recover, lean_guard, xgate};
+                      double* log, int log_len, int* log_count, hipStream_t s, int lean_from, int recover, int lean_guard, int xgate,
+                      int damp_from) {
+  SbrDevParams p{prm6[0], prm6[1], prm6[2], prm6[3], prm6[4], prm6[5], prm6[6], ns_iters, lean_from, recover, lean_guard, xgate,
+                 damp_from < 0 ? lean_from : min(damp_from, lean_from)};
   sbr_dev_ctrl_kernel<<<1, 256, 0, s>>>(part, nparts, j, K, hist, alpha, theta, ctrl, st, p, A, lda, n, w_out, eig_stats, w_init, log,
                                         log_len, log_count);
 }

@@ -223,9 +223,11 @@ class CMAES(Algorithm):
             return config.override(sbr_device_iters=int(config.get("sbr_cold_iters")))
         if variant == "late":
             # settled generations: damping / Newton–Schulz / order-6 kernels only in the first
-            # sbr_late_full_slots slots (their κ falls below the order-4 threshold by slot 2)
+            # sbr_late_full_slots slots (their κ falls below the order-4 threshold by slot 2), the
+            # damping power steps only in the first sbr_late_damp_slots
             return config.override(sbr_device_iters=int(config.get("sbr_late_iters")),
-                                   sbr_full_slots=int(config.get("sbr_late_full_slots")))
+                                   sbr_full_slots=int(config.get("sbr_late_full_slots")),
+                                   sbr_damp_slots=int(config.get("sbr_late_damp_slots")))
         return super().graph_variant_context(variant)
 
     # ------------------------------------------------------------------ sampling

@@ -40,7 +40,8 @@ LOG_LEN = 4096
 class DeviceSBR:
     """Persistent buffers + the fixed iteration schedule for one (n, device, config)."""
 
-    def __init__(self, n: int, device, cfg: SBRConfig, iters: int, lean_from: int = None, xgate: bool = None):
+    def __init__(self, n: int, device, cfg: SBRConfig, iters: int, lean_from: int = None, xgate: bool = None,
+                 damp_from: int = None):
         if cfg.block not in (16, 32):
             raise ValueError("the device schedule uses the shifted-layout blocks (16 / 32)")
         self.n, self.cfg, self.K = n, cfg, int(iters)
@@ -48,6 +49,10 @@ class DeviceSBR:
         # only chosen in the first iterations of a warm-started solve): a skipped lean slot
         # costs 7 launch boundaries fewer
         self.lean_from = self.K if lean_from is None else min(int(lean_from), self.K)
+        # slots ≥ damp_from launch no damping power steps (the late schedule keeps them in slot 0:
+        # in settled solves they return at once, ≈6 launches per generation); the control kernel
+        # stops the solve (capped, escalated by the host) where the κ rule would damp there
+        self.damp_from = self.lean_from if damp_from is None else min(int(damp_from), self.lean_from)
         dev = torch.device(device)
         ops = _ext.ops()
 
@@ -89,7 +94,7 @@ class DeviceSBR:
         self.log_count = torch.zeros(1, dtype=torch.int32, device=dev)
         self.prm = [float(cfg.tol), float(cfg.ns_kappa), float(cfg.damp_kappa), float(cfg.t4_kappa), float(cfg.near_only),
                     float(cfg.theta0), float(cfg.theta_kappa), float(self.lean_from), float(config.get("sbr_recover")),
-                    float(config.get("sbr_lean_guard")), float(self.xgate)]
+                    float(config.get("sbr_lean_guard")), float(self.xgate), float(self.damp_from)]
 
     # ------------------------------------------------------------------ pieces
     def _btcb(self, C, skip):
@@ -113,6 +118,7 @@ class DeviceSBR:
         sk_all, sk_far, sk_damp, sk_x3, sel6, sk_ns, sel_ns, sk_copy = (c[i : i + 1] for i in range(8))
         shift = (j % 2) * (sb // 2)
         full = j < self.lean_from
+        damp_slot = j < self.damp_from
         ops.sbr16_block_out(self.A, shift, int(cfg.block_sweeps), sb, self.perm, self.Q, self.dq, sk_all, self.sweep_tol)
         # far generator X and Bq = B[:, perm]·blockdiag(Q) in one launch
         if self.prepermute:
@@ -126,7 +132,7 @@ class DeviceSBR:
                                  self.theta[j : j + 1], self.X, self.B, self.Bq, sb, sk_far, sk_all)
         # X skew ⇒ X² = −X·Xᵀ, symmetric (upper tiles only)
         mm(self.X, self.X, tb=True, mode=1, alpha=-1.0, out=self.X2, skip=sk_far, stat_part=self.part2, stat_diag_only=True)
-        if cfg.damp_tau > 0 and full:
+        if cfg.damp_tau > 0 and damp_slot:
             # three power-step launches (they return at once when the free Frobenius bound already
             # gives α = 1); α itself is formed by the prep kernel below (no_final)
             ops.sbr_damping_out(self.X2, self.V, float(cfg.damp_tau), self.alpha[j + 1 : j + 2], self.work, sk_damp, None, True,
@@ -134,7 +140,7 @@ class DeviceSBR:
         if full:
             # order 6 only: X³ = X²·X = −X²·Xᵀ (skew)
             mm(self.X2, self.X, tb=True, mode=2, alpha=-1.0, out=self.X3, skip=sk_x3)
-        damp_here = cfg.damp_tau > 0 and full
+        damp_here = cfg.damp_tau > 0 and damp_slot
         # near-only iterations (no far step): the block-rotated basis is the new basis — Bq → B
         # copied by this launch (it returns at once otherwise), no copy launch of its own
         ops.sbr_dev_prep(self.X, self.X2, self.X3, self.alpha[j + 1 : j + 2], self.P, self.VT, c, self.work if damp_here else None,
@@ -180,15 +186,16 @@ class DeviceSBR:
 _WS = {}
 
 
-def workspace(n: int, device, cfg: SBRConfig, iters: int, lean_from: int = None, xgate: bool = False) -> DeviceSBR:
+def workspace(n: int, device, cfg: SBRConfig, iters: int, lean_from: int = None, xgate: bool = False,
+              damp_from: int = None) -> DeviceSBR:
     from .. import config
 
     key = (n, str(device), cfg.block, cfg.block_sweeps, cfg.thr_fac, cfg.ns_iters, cfg.damp_tau, cfg.tol, cfg.ns_kappa,
            cfg.damp_kappa, cfg.t4_kappa, cfg.near_only, cfg.theta0, cfg.theta_kappa, int(iters), lean_from,
            bool(config.get("sbr_prepermute")), float(config.get("sbr_sweep_tol")), int(config.get("sbr_recover")),
-           int(config.get("sbr_lean_guard")), bool(xgate))
+           int(config.get("sbr_lean_guard")), bool(xgate), damp_from)
     if key not in _WS:
-        _WS[key] = DeviceSBR(n, device, cfg, iters, lean_from, xgate)
+        _WS[key] = DeviceSBR(n, device, cfg, iters, lean_from, xgate, damp_from)
     return _WS[key]
 
 
@@ -221,7 +228,9 @@ def eigh_device(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None, it
     # settled solves the extra power iterations cost ≈3 % of a generation (profiles/r5_eigh_recover.txt)
     xg = int(config.get("sbr_xgate"))
     xgate = xg == 1 or (xg == 2 and iters >= config.get("sbr_cold_iters"))
-    return workspace(C.shape[0], C.device, cfg, iters, lean, xgate).solve(C, B_prev)
+    ds = int(config.get("sbr_damp_slots"))
+    damp_from = ds if (lean is not None and ds > 0) else None
+    return workspace(C.shape[0], C.device, cfg, iters, lean, xgate, damp_from).solve(C, B_prev)
 
 
 def all_histories():
