@@ -71,6 +71,26 @@ def test_device_schedule_cap_reports_unconverged():
     assert math.isclose(float(st[0]), _offrel(A), rel_tol=5e-2)
 
 
+def test_slots_without_damping_kernels_stop_where_the_kappa_rule_damps():
+    """damp_from (the late schedule keeps the damping power steps in slot 0 only): a later slot
+    whose step the κ rule would damp is not taken undamped — the solve stops there (capped, the
+    lean-slot guard's status bit), keeping an orthogonal basis better than the warm start."""
+    C, B = _cma_like(1000, 1, seed=1, dev="cuda")
+    A0 = B.T.double() @ C.double() @ B.double()
+    ws = sbr_device.workspace(1000, C.device, sbr.SBRConfig(), 8, lean_from=8, damp_from=1)
+    w, Bn, st = ws.solve(C, B)
+    st = st.cpu()
+    assert int(st[1]) & 4, st  # stopped by the guard
+    assert int(st[1]) & 1, st  # reported unconverged (capped), so the host escalates
+    A = Bn.T.double() @ C.double() @ Bn.double()
+    assert _offrel(A) < _offrel(A0)
+    I = torch.eye(1000, device="cuda", dtype=torch.float64)
+    assert float(torch.linalg.matrix_norm(Bn.T.double() @ Bn.double() - I)) < 1e-3
+    # the same schedule with the damping kernels in every slot takes those steps (no guard stop)
+    w2, B2, st2 = sbr_device.workspace(1000, C.device, sbr.SBRConfig(), 8, lean_from=8).solve(C, B)
+    assert not (int(st2.cpu()[1]) & 4) and int(st2.cpu()[2]) > int(st[2])
+
+
 def test_cmaes_device_mode_checkpoint_resume_is_bitwise(tmp_path):
     from evoxmi import config
     from evoxmi import random as rnd
