@@ -455,6 +455,9 @@ __device__ __forceinline__ void load_body(AntBody& s, AntLeg& g, const float* __
 // modifiers of hand-written VOP3P instructions instead.  Signed ankle variables (a = sg·aq,
 // its rate and momentum) make every leg's equations identical; sg appears only at the
 // observation and the actuator.
+// rsqrtf's subnormal guard (compare, two scalings, two selects) is 5 instructions around each
+// v_rsq_f32: the arguments here (|q|² ≈ 1, |v|² + EPSV²) are never subnormal, so the bare
+// instruction gives the same result.
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ f2 lo2(float s) {  // s in the low dword of a pair (the high dword unused)
@@ -576,7 +579,7 @@ __device__ __forceinline__ V3 pk_contact(const PkBody& s, const PkRot& R, const 
   const float pz = s.p.z + R.r6 * x.xy.x + R.r7 * x.xy.y + R.r8 * x.z;
   const float pen = fmaxf(RAD - pz, 0.f);
   const float fn = fmaxf(KC * pen - CC * vw.z * (pen > 0.f ? 1.f : 0.f), 0.f);
-  const float ivn = rsqrtf(dot2(vw.xy, vw.xy) + EPSV * EPSV);
+  const float ivn = __builtin_amdgcn_rsqf(dot2(vw.xy, vw.xy) + EPSV * EPSV);
   return rtmul(R, mk3(vw.xy * (-MU * fn * ivn), fn));
 }
 
@@ -593,7 +596,7 @@ __device__ __forceinline__ void art_substep_pk(PkBody& s, PkLeg& g, f2 tq) {
     const f2 n0 = nswap_fma(s.qyz, hoz, negx_fma(s.qyz, ho.y, perp_fma(s.qwx, ho.x, s.qwx)));
     const f2 hyz = f2{ho.y, hoz};
     const f2 n1 = nperp_fma_hi(hyz, s.qwx, hyz * s.qwx.x + perp_fma(s.qyz, ho.x, s.qyz));
-    const float in = rsqrtf(dot2(n0, n0) + dot2(n1, n1));
+    const float in = __builtin_amdgcn_rsqf(dot2(n0, n0) + dot2(n1, n1));
     s.qwx = n0 * in;
     s.qyz = n1 * in;
   }
