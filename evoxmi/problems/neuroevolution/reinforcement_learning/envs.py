@@ -13,19 +13,14 @@ that keeps each individual's MLP weights in LDS for the whole episode.
 * ``mountain_car_continuous`` — gymnasium MountainCarContinuous-v0.
 * ``ant`` — **articulated Brax-style** quadruped (documented as such, not bit-compatible
   with Brax/MuJoCo): a torso rigid body and 4 legs of two massive capsule links each
-  (thigh on a hip yaw joint, shin on an ankle pitch joint), 8 actuators (gear 150) on a
-  joint-space model with armature, damping and limit springs.  Per leg the 2×2 joint-space
-  inertia (diagonal for this geometry) and its Coriolis/centrifugal terms come from the
-  links' masses and inertias; gravity on the links and ground contacts enter as generalized
-  forces through the leg Jacobian.  The torso is the base of a composite body: it moves
-  under gravity on the total mass, the contact forces and the legs' momentum exchange —
-  d/dt of the legs' relative linear and angular momentum (finite differences of the
-  semi-implicit update) act on it, so joint torques react on the torso through the moving
-  links.  Contacts: penalty spring-damper with smooth Coulomb friction at the end-cap
-  spheres of each shin capsule (knee and foot).  5 semi-implicit sub-steps of 10 ms per
-  50 ms control step.  Simplifications against a full articulated-body solver: the
-  torso's rotation does not feed back into the joint equations (no base-acceleration
-  coupling), and the composite rotational inertia is a constant scalar (nominal pose).
+  (thigh on a hip yaw joint, shin on an ankle pitch joint), 8 actuators (gear 150) with
+  armature, damping and limit springs; penalty spring-damper contacts with smooth Coulomb
+  friction at the knee and foot end-cap spheres.  The exact equations of motion of the
+  free-floating 14-DOF tree in momentum form (composite inertia of the current pose,
+  base-acceleration coupling, closed-form Coriolis / centrifugal terms, a 6×6 Schur-complement
+  solve per sub-step; see :class:`Ant`), 5 sub-steps of 10 ms per 50 ms control step; total
+  momentum is conserved to rounding with no external forces.  The fused kernel integrates the
+  same model on packed-f32 register pairs (``neuro.hip: art_substep_pk``).
   Observation (27) = torso z, orientation quaternion, 8 joint angles, torso linear and
   angular velocity, 8 joint velocities (Brax ``qpos[2:] ++ qvel``).  Reward = forward
   velocity + 1 (healthy) − 0.5‖a‖²; the episode ends when torso z leaves [0.2, 1.0].
