@@ -227,7 +227,8 @@ class CMAES(Algorithm):
             # damping power steps only in the first sbr_late_damp_slots
             return config.override(sbr_device_iters=int(config.get("sbr_late_iters")),
                                    sbr_full_slots=int(config.get("sbr_late_full_slots")),
-                                   sbr_damp_slots=int(config.get("sbr_late_damp_slots")))
+                                   sbr_damp_slots=int(config.get("sbr_late_damp_slots")),
+                                   sbr_ns_iters=int(config.get("sbr_late_ns_iters")))
         return super().graph_variant_context(variant)
 
     # ------------------------------------------------------------------ sampling

@@ -208,7 +208,7 @@ def eigh_device(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None, it
                            theta0=config.get("sbr_theta0"), theta_kappa=config.get("sbr_theta_kappa"),
                            thr_fac=config.get("sbr_thr_fac"), block_sweeps=config.get("sbr_sweeps"),
                            damp_tau=config.get("sbr_damp_tau"), damp_kappa=config.get("sbr_damp_kappa"),
-                           ns_kappa=config.get("sbr_ns_kappa"))
+                           ns_kappa=config.get("sbr_ns_kappa"), ns_iters=config.get("sbr_ns_iters"))
     if iters is None:
         iters = config.get("sbr_device_iters")
         # lean tail slots only in a schedule that does not start cold (CMA-ES's cold-start
