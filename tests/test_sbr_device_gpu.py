@@ -200,10 +200,10 @@ def test_cmaes_default_schedule_converges_on_other_functions_and_dims(func, d):
 
 
 def test_cmaes_basis_stays_orthogonal_over_600_generations():
-    """The late schedule re-orthonormalises B (Newton–Schulz) in its first slot only: over 600
-    generations of the flagship run the basis error stays bounded (‖BᵀB − I‖_F ≈ 2e-5; with no
-    forced Newton–Schulz step it grows linearly to 3.8e-3, profiles/r5_late_ns_orthogonality.txt)
-    and B still diagonalises C."""
+    """Over 600 generations of the flagship run the basis error stays bounded (‖BᵀB − I‖_F
+    ≈ 1.4e-5 with the default two forced Newton–Schulz steps per settled generation, 2e-5 with
+    one; with none it grows linearly to 3.8e-3, profiles/r5_late_ns_orthogonality.txt) and B
+    still diagonalises C."""
     from evoxmi import random as rnd
     from evoxmi.algorithms import CMAES
     from evoxmi.problems.numerical import CEC2022TestSuit
