@@ -230,7 +230,10 @@ def main():
                 "capped": int((dev_hist[:, 1].long() & 1).sum()),
                 "recovered": int(((dev_hist[:, 1].long() & 2) != 0).sum()),
                 "lean_guard_stops": int(((dev_hist[:, 1].long() & 4) != 0).sum()),
-                "schedule_escalations": int(algo.__dict__.get("_esc_count", 0)),
+                "schedule_escalations": int(getattr(algo, "schedule_escalations", 0)),
+                # eigensolver schedule each timed generation replayed (L late / W warm / C cold),
+                # chosen from the measured convergence of the solve two generations back
+                "schedule_per_gen": algo.schedule_levels(args.steps) if hasattr(algo, "schedule_levels") else None,
                 # refinement iterations of each timed generation, in order
                 "iters_per_gen": "".join(str(min(int(v), 9)) if v < 10 else "+" for v in dev_hist[:, 2].tolist()),
             }

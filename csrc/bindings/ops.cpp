@@ -171,7 +171,7 @@ at::Tensor gemm_ks(const at::Tensor& A, int64_t a_kc, const at::Tensor& B, int64
                    const c10::optional<at::Tensor>& a_sub_k, const c10::optional<at::Tensor>& sel = c10::nullopt,
                    const c10::optional<at::Tensor>& A2 = c10::nullopt, double alpha2 = 0.0,
                    const c10::optional<at::Tensor>& C2 = c10::nullopt, const c10::optional<at::Tensor>& stat_part = c10::nullopt,
-                   int64_t stat_diag_only = 0) {
+                   int64_t stat_diag_only = 0, int64_t prec = 0, double diag_add = 0.0) {
   CHECK_DEV(A); CHECK_F32(A); CHECK_DEV(B); CHECK_F32(B);
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.stride(1) == 1 && B.stride(1) == 1, "gemm_ks: 2-D operands with unit inner stride");
   TORCH_CHECK(M > 0 && N > 0 && K > 0, "gemm_ks: empty shape");
@@ -256,6 +256,10 @@ at::Tensor gemm_ks(const at::Tensor& A, int64_t a_kc, const at::Tensor& B, int64
     a.stat_part = stat_part->data_ptr<double>();
     a.stat_diag_only = (int)stat_diag_only;
   }
+  TORCH_CHECK(prec == 0 || prec == 3, "gemm_ks: prec 0 (process default) or 3 (bf16x3)");
+  TORCH_CHECK(diag_add == 0.0 || M == N, "gemm_ks: diag_add needs a square output");
+  a.prec = (int)prec;
+  a.diag_add = (float)diag_add;
   a.c_vec4 = vec4_ok(C) ? 1 : 0;
   // the partials' length (gemm_ks_grid) assumed the square-product kernel for this shape
   TORCH_CHECK(!a.stat_part || !evx_gemm_ks_sq_shape((int)M, (int)N, (int)mode) || evx_gemm_ks_routes_sq(a),
@@ -389,9 +393,10 @@ void gemm_ks_out(const at::Tensor& A, int64_t a_kc, const at::Tensor& B, int64_t
                  int64_t mode, double alpha, const c10::optional<at::Tensor>& alpha_ptr, const c10::optional<at::Tensor>& bias_n,
                  double beta, const c10::optional<at::Tensor>& Cin, const at::Tensor& out, const c10::optional<at::Tensor>& skip,
                  const c10::optional<at::Tensor>& a_sub_k, const c10::optional<at::Tensor>& sel, const c10::optional<at::Tensor>& A2,
-                 double alpha2, const c10::optional<at::Tensor>& C2, const c10::optional<at::Tensor>& stat_part, int64_t stat_diag_only) {
+                 double alpha2, const c10::optional<at::Tensor>& C2, const c10::optional<at::Tensor>& stat_part, int64_t stat_diag_only,
+                 int64_t prec, double diag_add) {
   gemm_ks(A, a_kc, B, b_kc, M, N, K, mode, alpha, alpha_ptr, bias_n, beta, Cin, out, skip, a_sub_k, sel, A2, alpha2, C2, stat_part,
-          stat_diag_only);
+          stat_diag_only, prec, diag_add);
 }
 
 int64_t gemm_ks_grid(int64_t M, int64_t N, int64_t mode) { return evx_gemm_ks_grid((int)M, (int)N, (int)mode); }
@@ -517,7 +522,7 @@ void sbr_damping_out(const at::Tensor& X2, const at::Tensor& V, double tau, at::
 
 void sbr_dev_prep(const at::Tensor& X, const at::Tensor& X2, const at::Tensor& X3, at::Tensor& alpha, at::Tensor& P, at::Tensor& MT,
                   const at::Tensor& ctrl, const c10::optional<at::Tensor>& work, double tau, const c10::optional<at::Tensor>& xpart,
-                  const c10::optional<at::Tensor>& copy_src, const c10::optional<at::Tensor>& copy_dst) {
+                  const c10::optional<at::Tensor>& copy_src, const c10::optional<at::Tensor>& copy_dst, int64_t minus_id) {
   for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&X, &X2, &X3, &P, &MT}) {
     CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t);
     TORCH_CHECK(t->sizes() == X.sizes(), "sbr_dev_prep: n×n");
@@ -547,7 +552,7 @@ void sbr_dev_prep(const at::Tensor& X, const at::Tensor& X2, const at::Tensor& X
     cd = copy_dst->data_ptr<float>();
   }
   evx_sbr_dev_prep(X.data_ptr<float>(), X2.data_ptr<float>(), X3.data_ptr<float>(), (int)X.size(0), alpha.data_ptr<float>(),
-                   P.data_ptr<float>(), MT.data_ptr<float>(), ctrl.data_ptr<int>(), cur_stream(), v2, v3, (float)tau, xp, (int)np, cs, cd);
+                   P.data_ptr<float>(), MT.data_ptr<float>(), ctrl.data_ptr<int>(), cur_stream(), v2, v3, (float)tau, xp, (int)np, cs, cd, (int)minus_id);
 }
 
 void sbr_dev_copy(const at::Tensor& src, at::Tensor& dst, const at::Tensor& skip) {
@@ -1547,7 +1552,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("classic_eval(Tensor X, int func, float a, float b, float c) -> Tensor");
   m.def("gemm_f32(Tensor A, int a_rc, Tensor? a_gather, Tensor? a_sub, int a_sub_on_k, Tensor? a_kscale, Tensor? a_kw, Tensor? a_sscale, int a_sscale_inv, Tensor B, int b_rc, Tensor? b_gather, Tensor? b_sub, int b_sub_on_k, Tensor? b_kscale, Tensor? b_kw, Tensor? b_sscale, int b_sscale_inv, Tensor? alpha_ptr, Tensor? bias_n, float beta, Tensor? Cin, int M, int N, int K, int splits, float alpha) -> Tensor");
   m.def("gemm_ks(Tensor A, int a_kc, Tensor B, int b_kc, int M, int N, int K, int mode, float alpha, Tensor? alpha_ptr, Tensor? bias_n, float beta, Tensor? Cin, Tensor? skip, Tensor? a_sub_k=None) -> Tensor");
-  m.def("gemm_ks_out(Tensor A, int a_kc, Tensor B, int b_kc, int M, int N, int K, int mode, float alpha, Tensor? alpha_ptr, Tensor? bias_n, float beta, Tensor? Cin, Tensor(a!) out, Tensor? skip, Tensor? a_sub_k=None, Tensor? sel=None, Tensor? A2=None, float alpha2=0., Tensor(b!)? C2=None, Tensor(c!)? stat_part=None, int stat_diag_only=0) -> ()");
+  m.def("gemm_ks_out(Tensor A, int a_kc, Tensor B, int b_kc, int M, int N, int K, int mode, float alpha, Tensor? alpha_ptr, Tensor? bias_n, float beta, Tensor? Cin, Tensor(a!) out, Tensor? skip, Tensor? a_sub_k=None, Tensor? sel=None, Tensor? A2=None, float alpha2=0., Tensor(b!)? C2=None, Tensor(c!)? stat_part=None, int stat_diag_only=0, int prec=0, float diag_add=0.) -> ()");
   m.def("gemm_ks_grid(int M, int N, int mode) -> int");
   m.def("gemm_ks_tile(int M, int N, int mode) -> int");
   m.def("cec_rotated_rowterms(Tensor X, Tensor Mrot, Tensor o, float alpha, int fid) -> Tensor");
@@ -1555,7 +1560,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("sbr16_far_out(Tensor A, Tensor perm, Tensor Q, Tensor dq, Tensor stats, float thr_fac, Tensor theta, Tensor(a!) X, int sb, Tensor skip) -> ()");
   m.def("sbr16_bq_out(Tensor B, Tensor perm, Tensor Q, Tensor(a!) Bq, int sb, Tensor skip) -> ()");
   m.def("sbr_damping_out(Tensor X2, Tensor V, float tau, Tensor(a!) alpha, Tensor(b!) work, Tensor skip, Tensor(c!)? bar=None, bool no_final=False, Tensor? xpart=None) -> ()");
-  m.def("sbr_dev_prep(Tensor X, Tensor X2, Tensor X3, Tensor(c!) alpha, Tensor(a!) P, Tensor(b!) MT, Tensor ctrl, Tensor? work=None, float tau=1.0, Tensor? xpart=None, Tensor? copy_src=None, Tensor(d!)? copy_dst=None) -> ()");
+  m.def("sbr_dev_prep(Tensor X, Tensor X2, Tensor X3, Tensor(c!) alpha, Tensor(a!) P, Tensor(b!) MT, Tensor ctrl, Tensor? work=None, float tau=1.0, Tensor? xpart=None, Tensor? copy_src=None, Tensor(d!)? copy_dst=None, int minus_id=0) -> ()");
   m.def("sbr_dev_copy(Tensor src, Tensor(a!) dst, Tensor skip) -> ()");
   m.def("sbr_dev_ctrl(Tensor part, int nparts, int j, int K, Tensor(a!) hist, Tensor(b!) alpha, Tensor(c!) theta, Tensor(d!) ctrl, Tensor(e!) st, float[] prm, int ns_iters, Tensor A, Tensor(f!) w_out, Tensor(g!) eig_stats, Tensor(h!) w_init, Tensor(i!) log, Tensor(j!) log_count) -> ()");
   m.def("gemm_ks_set_tile(int t) -> ()");

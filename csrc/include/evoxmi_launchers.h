@@ -82,6 +82,11 @@ struct EvxGemmKs {
   int sub_cols;
   int64_t sub_ld;
   int force_tile;  // tile code for this launch (0: the shape heuristic)
+  // 0: the process-wide precision (evx_gemm_ks_set_prec); 3: bf16x3 (hh + hm + mh, ≈16-bit
+  // products — the eigensolver's correction products, gemm_ks.hip split2)
+  int prec;
+  // added to the diagonal of the result (after alpha / Cin): Bᵀ B − I for Newton–Schulz
+  float diag_add;
 };
 void evx_gemm_ks(const EvxGemmKs& a, hipStream_t s);
 // LDS-staged bf16x6 GEMM on "blocked planes" (gemm_blk.hip): an f32 matrix rows × K stored as
@@ -284,7 +289,7 @@ void evx_linear_gp_fit(const double* a, const double* b, const double* c, const 
 // device-controlled SBR schedule (eigh_sbr_dev.hip)
 void evx_sbr_dev_prep(const float* X, const float* X2, const float* X3, int n, float* alpha, float* P, float* MT, const int* ctrl,
                       hipStream_t s, const float* V2 = nullptr, const float* V3 = nullptr,
-                      float tau = 1.f, const double* xpart = nullptr, int nparts = 0, const float* copy_src = nullptr, float* copy_dst = nullptr);
+                      float tau = 1.f, const double* xpart = nullptr, int nparts = 0, const float* copy_src = nullptr, float* copy_dst = nullptr, int minus_id = 0);
 void evx_sbr_dev_copy(const float* src, float* dst, int64_t n, const int* skip, hipStream_t s);
 void evx_sbr_report(const double* stats, int* seq, double* ring, int R, hipStream_t s);
 void evx_sbr_dev_ctrl(const double* part, int nparts, int j, int K, double* hist, float* alpha, float* theta, int* ctrl, int* st,

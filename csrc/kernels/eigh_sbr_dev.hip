@@ -75,7 +75,8 @@ __global__ void __launch_bounds__(256) sbr_dev_prep_kernel(const float* __restri
                                                            float* __restrict__ P, float* __restrict__ MT, const int* __restrict__ ctrl,
                                                            const float* __restrict__ V2, const float* __restrict__ V3, float tau,
                                                            const double* __restrict__ xpart, int nparts,
-                                                           const float* __restrict__ copy_src, float* __restrict__ copy_dst) {
+                                                           const float* __restrict__ copy_src, float* __restrict__ copy_dst,
+                                                           int minus_id) {
   if (ctrl[1]) {
     // no far step this iteration: a near-only iteration (ctrl[7] == 0) takes the block-rotated
     // basis Bq as the new basis — the copy runs here, in the launch the schedule makes anyway
@@ -131,7 +132,9 @@ __global__ void __launch_bounds__(256) sbr_dev_prep_kernel(const float* __restri
       for (int q = 0; q < 4; ++q) {
         const int j = c * w + q;
         const float x = a * xs[q], x2 = a2 * x2s[q];
-        const float id = i == j ? 1.f : 0.f;
+        // minus_id: M − I (the caller adds the exact basis itself: B·V = Bq + Bq·(V − I), whose
+        // correction product then runs at bf16x3)
+        const float id = (i == j && !minus_id) ? 1.f : 0.f;
         if (six) {
           const float x3 = a3 * x3s[q];
           ps[q] = a3 * (x * (1.f / 24.f) + x2 * (1.f / 120.f) + x3 * (1.f / 720.f));
@@ -369,13 +372,14 @@ void evx_sbr_report(const double* stats, int* seq, double* ring, int R, hipStrea
 
 void evx_sbr_dev_prep(const float* X, const float* X2, const float* X3, int n, float* alpha, float* P, float* MT, const int* ctrl,
                       hipStream_t s, const float* V2, const float* V3, float tau, const double* xpart, int nparts, const float* copy_src,
-                      float* copy_dst) {
+                      float* copy_dst, int minus_id) {
   // a grid-stride loop over 256 workgroups: the schedule skips this kernel in most
   // iterations, and an empty launch costs in proportion to its workgroup count
   const int64_t total = (int64_t)n * n;
   int g = (int)((total + 255) / 256);
   if (g > 256) g = 256;
-  sbr_dev_prep_kernel<<<g, 256, 0, s>>>(X, X2, X3, n, alpha, P, MT, ctrl, V2, V3, tau, xpart, nparts, copy_src, copy_dst);
+  sbr_dev_prep_kernel<<<g, 256, 0, s>>>(X, X2, X3, n, alpha, P, MT, ctrl, V2, V3, tau, xpart, nparts, copy_src, copy_dst,
+                                        minus_id);
 }
 
 void evx_sbr_dev_copy(const float* src, float* dst, int64_t n, const int* skip, hipStream_t s) {

@@ -265,8 +265,13 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_blk_kernel(EvxGemmBlk p) {
 // ============================================================================ f16x3 planes
 // An f32 value split into two f16 (11-bit significand) parts with round-to-nearest-even,
 // after a per-row power-of-two scale that puts the row's largest |x| at ≤ 2¹⁵:
-//   x·2^e = h + m + ε,  |m| ≤ 2⁻¹¹|x·2^e|,  |ε| ≤ 2⁻²²|x·2^e|
-// (the 13 low bits of the remainder x − h are exact in f32 and m keeps 11 of them).  A
+//   x·2^e = h + m + ε,  |m| ≤ 2⁻¹¹|x·2^e|,  |ε| ≤ max(2⁻²²|x·2^e|, 2⁻²⁴ · 2⁻¹⁴)
+// (the 13 low bits of the remainder x − h are exact in f32 and m keeps 11 of them, as long as
+// m is a normal f16: for elements more than ≈2¹⁸ below the row max, m falls into the f16
+// subnormals and the error is bounded absolutely instead, |ε| ≤ 2⁻⁴⁰·rowmax·2^e after the
+// scale).  The scale exponent is clamped (e ≤ 125) so a row of tiny magnitude never scales
+// to inf; the Σ|ab| bound below holds either way (tests/test_gemm_blk.py, tiny and
+// wide-range rows).  A
 // product a·b is kept as h_a h_b + h_a m_b + m_a h_b — three v_mfma_f32_32x32x16_f16, each
 // product of two f16 exact in the f32 accumulator — with the dropped m_a m_b ≤ 2⁻²²|ab|: at
 // most ≈3·2⁻²² ≈ 7e-7 |a·b| per product in the worst case, unbiased (RNE), inside the
@@ -305,12 +310,13 @@ __device__ __forceinline__ void split16h_store(const float (&v)[16], float sc, i
   dst[3 ^ sw] = make_uint4(M[4], M[5], M[6], M[7]);
 }
 
-// 2^e with e = 15 − ⌈log₂ max⌉ (max > 0, finite), else 1
+// 2^e with e = 15 − ⌈log₂ max⌉ (max > 0, finite), else 1; e ≤ 125 (a row whose max is below
+// ≈2⁻¹¹⁰ would otherwise get a scale past 2¹²⁸ = inf and NaN planes)
 __device__ __forceinline__ float row_scale(float mx) {
   if (!(mx > 0.f) || !(mx < 3.0e38f)) return 1.f;
   int ex;
   frexpf(mx, &ex);  // mx = f·2^ex, f ∈ [0.5, 1): mx < 2^ex
-  return ldexpf(1.f, 15 - ex);
+  return ldexpf(1.f, 15 - max(ex, -110));
 }
 
 // one wave per row: lane j owns the 16-k blocks j, j + 64, …; row max → scale → split

@@ -108,6 +108,35 @@ __device__ __forceinline__ void split3(const float4& v0, const float4& v1, bf16x
   l = __builtin_bit_cast(bf16x8, L);
 }
 
+// ---- bf16x3: correction products (PREC = 3) ----
+// a = h + m + ε with two RNE bf16 parts (|ε| ≤ 2⁻¹⁸|a|); a·b ≈ hh + hm + mh drops m·m and the
+// split remainders: ≤ ≈3·2⁻¹⁸ ≈ 1.1e-5 |a·b| per product.  Used for the eigensolver products
+// that form a SMALL correction (exp(αX) − I, its Taylor terms, Newton–Schulz T·(BᵀB − I)): the
+// result carries ≈16 good bits relative to the correction's own size (‖X‖ ≈ 1e-3 in settled
+// solves ⇒ ≈1e-8 of the basis), while the residual products (Bᵀ C B, BᵀB) stay bf16x6.  Half
+// the MFMAs of bf16x6 and two instead of three conversions per operand element.
+__device__ __forceinline__ void split2(const float4& v0, const float4& v1, bf16x8& h, bf16x8& m) {
+  u32x4 H, M;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const float4& q = p < 2 ? v0 : v1;
+    const float a0 = (p & 1) ? q.z : q.x, a1 = (p & 1) ? q.w : q.y;
+    const bf16x2 hb = __builtin_convertvector(f32x2{a0, a1}, bf16x2);
+    const f32x2 hf = __builtin_convertvector(hb, f32x2);
+    const bf16x2 mb = __builtin_convertvector(f32x2{a0 - hf.x, a1 - hf.y}, bf16x2);
+    H[p] = __builtin_bit_cast(unsigned, hb);
+    M[p] = __builtin_bit_cast(unsigned, mb);
+  }
+  h = __builtin_bit_cast(bf16x8, H);
+  m = __builtin_bit_cast(bf16x8, M);
+}
+
+__device__ __forceinline__ f32x4 mfma_x3(const bf16x8& ah, const bf16x8& am, const bf16x8& bh, const bf16x8& bm, f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bm, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, c, 0, 0, 0);
+}
+
 __device__ __forceinline__ f32x16 mfma_x6w(const bf16x8& ah, const bf16x8& am, const bf16x8& al, const bf16x8& bh,
                                            const bf16x8& bm, const bf16x8& bl, f32x16 c) {
   // v_mfma_f32_32x32x16_bf16: 32 cycles, holds vector issue for 8 of them (24 free cycles per
@@ -215,7 +244,8 @@ __device__ __forceinline__ void decode_tile(int bid, int tiles_m, int tiles_n, i
   tm = tn = 0;
 }
 
-// PREC 0: f32 MFMA (16x16x4, KH float4 per lane and 16-row block per k-group);
+// PREC 0: f32 MFMA (16x16x4, KH float4 per lane and 16-row block per k-group); PREC 3: bf16x3
+// (the PREC 1 fragment map with two bf16 parts and three products);
 // PREC 1: bf16x6 (KH = 2: a 32-k group is one 16x16x32 bf16 step — lane (r, q) holds
 // fragment element j ↔ k = 32·group + 16·(j >> 2) + 4q + (j & 3), the same k map for A and B,
 // so the f32 path's loads are reused unchanged).
@@ -227,6 +257,7 @@ __global__ void __launch_bounds__(64 * NW) gemm_ks_kernel(EvxGemmKs p) {
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   static_assert(PREC == 0 || KH == 2, "bf16x6 groups hold two float4 per lane and block");
   static_assert(PL == 0 || (PREC == 1 && AKC && BKC), "fragment planes: bf16x6 on 16x16x32, K-contiguous operands");
+  static_assert(PREC != 3 || PL == 0, "bf16x3 splits in registers");
   constexpr bool APL = PL & 1, BPL = PL & 2;
   static_assert(PREC != 2 || (TM % 2 == 0 && TN % 2 == 0), "32x32 MFMA tiles need even 16-blocks");
   if (p.skip && *p.skip) return;
@@ -364,7 +395,18 @@ __global__ void __launch_bounds__(64 * NW) gemm_ks_kernel(EvxGemmKs p) {
           xa[h][i].w -= xs[h].w;
         }
     }
-    if constexpr (PREC >= 1) {
+    if constexpr (PREC == 3) {
+      bf16x8 bh[NB], bm[NB];
+#pragma unroll
+      for (int j = 0; j < NB; ++j) split2(xb[0][j], xb[1][j], bh[j], bm[j]);
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        bf16x8 ah, am;
+        split2(xa[0][i], xa[1][i], ah, am);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) acc[i][j] = mfma_x3(ah, am, bh[j], bm[j], acc[i][j]);
+      }
+    } else if constexpr (PREC >= 1) {
       bf16x8 bh[NB], bm[NB], bl[NB];
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
@@ -578,6 +620,15 @@ __global__ void __launch_bounds__(64 * NW) gemm_ks_kernel(EvxGemmKs p) {
           if (gc + 2 < p.N) t.z += p.beta * cin[gc + 2];
           if (gc + 3 < p.N) t.w += p.beta * cin[gc + 3];
         }
+        if (p.diag_add != 0.f) {
+          // the diagonal element of this float4, if any (explicit selects: HIP's float4 members
+          // are accessor objects, not an indexable array)
+          const int dd = gr - gc;
+          if (dd == 0) t.x += p.diag_add;
+          else if (dd == 1) t.y += p.diag_add;
+          else if (dd == 2) t.z += p.diag_add;
+          else if (dd == 3) t.w += p.diag_add;
+        }
         if (MODE != 0 && tm == tn) {
           // diagonal tile: only its upper triangle is stored here (the mirror pass writes the
           // lower one from it), so the output is exactly (skew-)symmetric; skew diagonal = 0
@@ -719,6 +770,7 @@ void launch_layout(const EvxGemmKs& a, int tiles, hipStream_t s) {
       else gemm_ks_kernel<TM, TN, 2, true, true, MODE, 1, 2><<<grid, block, 0, s>>>(a);
       return;
     }
+    if (a.prec == 3) return launch_prec<TM, TN, MODE, 3>(a, tiles, s);
     if constexpr (TM % 2 == 0 && TN % 2 == 0) {
       if (g_ks_prec == 2) return launch_prec<TM, TN, MODE, 2>(a, tiles, s);
     }
@@ -834,7 +886,7 @@ int evx_gemm_ks_grid(int M, int N, int mode) {
   return (int)evx_host::gemm_ks_grid(M, N, mode, g_ks_tile_override);
 }
 
-bool evx_gemm_ks_routes_sq(const EvxGemmKs& a) { return !a.force_tile && evx_gemm_ks_sq_shape(a.M, a.N, a.mode) && evx_gemm_sq_ok(a); }
+bool evx_gemm_ks_routes_sq(const EvxGemmKs& a) { return !a.force_tile && a.prec != 3 && a.diag_add == 0.f && evx_gemm_ks_sq_shape(a.M, a.N, a.mode) && evx_gemm_sq_ok(a); }
 
 int evx_gemm_ks_tiles_n(int M, int N, int mode) { return (int)evx_host::gemm_ks_tiles_n(M, N, mode, g_ks_tile_override); }
 

@@ -95,6 +95,7 @@ class CMAES(Algorithm):
     def setup(self, key):
         dev = self.center_init.device
         d = self.dim
+        self._sched_reset()
         B = torch.eye(d, device=dev)
         C = torch.eye(d, device=dev)
         return State(
@@ -119,62 +120,87 @@ class CMAES(Algorithm):
         return (self.center_init.is_cuda and self.decomp_per_iter == 1 and config.get("cma_fused") and config.get("eigh") == "sbr"
                 and config.get("sbr_mode") == "device" and self.dim % 4 == 0 and self.dim <= 8192)
 
-    def graph_variant(self, generation: int):
-        """The first ``sbr_cold_gens`` generations decompose with the longer cold-start
-        schedule (``sbr_cold_iters`` refinement slots): the warm start is C ≈ I there, the
-        damped steps need ≈10–12 iterations, and later generations converge in 4–7 within the
-        default 8-slot schedule (profiles/r4_sbr_threshold_variants.txt).  The generation
-        index is host-known, so the choice costs no device read.
+    # ------------------------------------------------------------------ eigensolver schedule
+    # The device eigensolver runs a fixed number of refinement slots per generation (a skipped
+    # slot still costs its launch boundaries), in three captured graph variants: "cold"
+    # (sbr_cold_iters slots — the first solves from C = I need 10-12 iterations), None (the warm
+    # schedule, sbr_device_iters) and "late" (sbr_late_iters, lean: settled solves take 4).
+    # Which one a generation replays is chosen from MEASURED convergence, not from the
+    # generation index (round 6; round 5 switched at fixed generations 4 and 24 tuned on one
+    # trajectory):
+    #
+    # * each solve writes [off_rel, status, iterations, fallback, seq] into a host-mapped pinned
+    #   ring inside the generation (one single-thread kernel of its graph) and an event is
+    #   recorded after the step; choosing the variant of a step reads the solve of the step
+    #   ESC_LAG = 2 back (waiting on that step's event never idles the GPU while the step after
+    #   it is queued; no .item(), no device synchronize) — a fixed lag, so the choice and the
+    #   run are deterministic;
+    # * a solve that capped or fell back, or that converged only in its schedule's last slot,
+    #   moves the schedule one level up from the level it ran at (late → warm → cold); a solve
+    #   that would not fit the current level with one slot to spare moves it back to the
+    #   level it ran at (the "first slow solve" rule);
+    # * DOWN_STREAK consecutive solves at the current level that would have fitted the next
+    #   shorter schedule with one slot to spare move it one level down.
+    LEVELS = ("late", None, "cold")
+    ESC_LAG = 2
+    ESC_RING = 16
+    DOWN_STREAK = 2
 
-        Escalation (round 5): each solve writes its ``eig_stats`` into a host-mapped pinned ring
-        inside the generation (one single-thread kernel of its graph) and an event is recorded
-        after the step (:meth:`after_step`).  Choosing the schedule of a step reads the solve of
-        the step ``ESC_LAG`` = 2 back — waiting for that step's event, which never idles the
-        GPU while the step after it is queued (no ``.item()``, no device synchronize) — and,
-        when that solve reports itself capped (not converged) or fell back to the warm-start
-        basis, replays the next longer schedule (late → 8-slot → cold) for
-        ``sbr_escalate_gens`` generations.  The fixed lag keeps the choice, and so the run,
-        deterministic."""
+    def _sched(self):
+        sc = self.__dict__.get("_sched_state")
+        if sc is None:
+            sc = self._sched_state = self._sched_fresh()
+        return sc
+
+    @staticmethod
+    def _sched_fresh():
+        from collections import deque
+
+        return {"level": 2, "streak": 0, "enqueued": 0, "checked": -1, "pending": deque(), "last": 2, "escalations": 0,
+                "history": [], "levels": []}
+
+    def _sched_reset(self):
+        """A new run (``setup``): the schedule starts cold again and forgets the previous run's
+        solves; the device report counter and ring are re-based so slot k again holds solve k."""
+        self._sched_state = self._sched_fresh()
+        if self.__dict__.get("_eig_seq") is not None:
+            self._eig_seq.zero_()
+            self._eig_ring.fill_(-1.0)
+
+    def _level_slots(self, level: int) -> int:
+        from ....ops.sbr_device import schedule_iters
+
+        variant_iters = {0: config.get("sbr_late_iters"), 1: config.get("sbr_device_iters"), 2: config.get("sbr_cold_iters")}[level]
+        return schedule_iters(self.dim, int(variant_iters))
+
+    def graph_variant(self, generation: int):
+        """The eigensolver schedule of the next step (see the class comment above): one of
+        ``LEVELS``, chosen from the measured convergence of the solve ``ESC_LAG`` steps back."""
         if not self._device_eigh():
             return None
-        self._poll_eig_health(generation)
-        if generation < int(config.get("sbr_cold_gens")):
-            base = "cold"
-        else:
-            late = int(config.get("sbr_late_gens"))
-            # settled runs converge in ≤ 5 iterations: a shorter schedule drops the launch
-            # boundaries of the always-skipped tail slots
-            base = "late" if late > 0 and generation >= late else None
-        esc = self.__dict__.get("_esc")
-        if esc is not None and generation < esc[0]:
-            order = ["late", None, "cold"]
-            return order[min(order.index(base) + esc[1], 2)]
-        return base
+        sc = self._sched()
+        self._poll_eig_health(sc)
+        sc["last"] = sc["level"]
+        return self.LEVELS[sc["level"]]
 
     def graph_variant_set(self):
         if not self._device_eigh():
             return ()
-        return ("cold", None, "late") if int(config.get("sbr_late_gens")) > 0 else ("cold", None)
-
-    # fixed lag (in steps) at which the schedule choice reads a solve's health: the step two
-    # back has completed whenever one step is still queued, so the wait below never idles the
-    # GPU, and the same solves decide the same schedules in every run (deterministic)
-    ESC_LAG = 2
-    ESC_RING = 16
+        return self.LEVELS
 
     def after_step(self, generation: int) -> None:
         if self.__dict__.get("_eig_ring") is None or not torch.cuda.is_available():
             return
-        from collections import deque
-
-        pend = self.__dict__.setdefault("_eig_pending", deque())
+        sc = self._sched()
         ev = torch.cuda.Event()
         ev.record()
-        k = self.__dict__.get("_eig_enqueued", 0)
-        pend.append((k, ev))
-        self._eig_enqueued = k + 1
-        while len(pend) > self.ESC_RING // 2:
-            pend.popleft()
+        k = sc["enqueued"]
+        sc["pending"].append((k, ev, sc["last"]))
+        sc["levels"].append(sc["last"])
+        del sc["levels"][:-4096]
+        sc["enqueued"] = k + 1
+        while len(sc["pending"]) > self.ESC_RING // 2:
+            sc["pending"].popleft()
 
     def _stats_to_host(self, eig_stats: torch.Tensor) -> None:
         """This solve's [off_rel, status, iterations, fallback] into a host-mapped pinned ring,
@@ -197,26 +223,51 @@ class CMAES(Algorithm):
 
         _ext.ops().sbr_report(eig_stats, self._eig_seq, self._eig_ring)
 
-    def _poll_eig_health(self, generation: int) -> None:
-        n = self.__dict__.get("_eig_enqueued", 0)
-        target = n - self.ESC_LAG
-        if target < 0 or target <= self.__dict__.get("_eig_checked", -1):
+    def _poll_eig_health(self, sc) -> None:
+        target = sc["enqueued"] - self.ESC_LAG
+        if target < 0 or target <= sc["checked"]:
             return
-        self._eig_checked = target
-        pend = self.__dict__.get("_eig_pending")
+        sc["checked"] = target
+        pend = sc["pending"]
         while pend and pend[0][0] < target:
             pend.popleft()
         if not pend or pend[0][0] != target:
             return
-        pend[0][1].synchronize()  # the step two back: the GPU still holds the one after it
+        _, ev, lvl = pend[0]
+        ev.synchronize()  # the step two back: the GPU still holds the one after it
         row = self._eig_ring[target % self.ESC_RING].tolist()
         if int(row[4]) != target:
             return
-        if (int(row[1]) & 1) or row[3]:
-            esc = self.__dict__.get("_esc")
-            level = 1 if esc is None or generation >= esc[0] else min(esc[1] + 1, 2)
-            self._esc = (generation + int(config.get("sbr_escalate_gens")), level)
-            self._esc_count = self.__dict__.get("_esc_count", 0) + 1
+        iters, capped = int(row[2]), bool((int(row[1]) & 1) or row[3])
+        sc["history"].append((target, lvl, iters, capped))
+        del sc["history"][:-64]
+        level = sc["level"]
+        if capped or iters >= self._level_slots(lvl):
+            up = min(lvl + 1, 2)
+            if capped:
+                sc["escalations"] += 1
+        elif iters >= self._level_slots(level):
+            up = lvl
+        else:
+            up = level
+        if up > level:
+            sc["level"], sc["streak"] = up, 0
+            return
+        if lvl == level and level > 0:
+            fits = iters <= self._level_slots(level - 1) - 1
+            sc["streak"] = sc["streak"] + 1 if fits else 0
+            if sc["streak"] >= self.DOWN_STREAK:
+                sc["level"], sc["streak"] = level - 1, 0
+
+    @property
+    def schedule_escalations(self) -> int:
+        return int(self._sched()["escalations"])
+
+    def schedule_levels(self, last: int = None) -> str:
+        """The schedule each recent step replayed: L (late), W (warm), C (cold)."""
+        lv = self._sched()["levels"]
+        lv = lv if last is None else lv[-int(last):]
+        return "".join("LWC"[v] for v in lv)
 
     def graph_variant_context(self, variant):
         if variant == "cold":
@@ -480,6 +531,17 @@ class SepCMAES(ColumnSeparable, CMAES):
 
     column_separable = True
     dim_fields = ("pc", "ps", "C", "mean", "population")
+
+    # no eigensolver: one graph, no schedule variants (ADVICE r5 — the inherited ones captured
+    # three identical graphs)
+    def _device_eigh(self) -> bool:
+        return False
+
+    def graph_variant(self, generation: int):
+        return None
+
+    def graph_variant_set(self):
+        return ()
 
     def setup(self, key):
         dev = self.center_init.device

@@ -48,10 +48,8 @@ KNOBS: Dict[str, Knob] = {
     "sbr_mode": Knob("EVOXMI_SBR_MODE", "device", str, "sbr: 'device' — fixed device-controlled iteration schedule inside the generation's graph (ops/sbr_device.py, no host read); 'host' — host-driven iterations with planned solves as a host phase between graph segments (ops/sbr.py)"),
     "sbr_device_iters": Knob("EVOXMI_SBR_DEVICE_ITERS", 7, int, "sbr device mode: refinement iterations in the fixed (warm) schedule (kernels of iterations past convergence return at once; round 5: 8 → 7 slots, 1.644-1.656 → 1.630 ms at 20 steps — warm solves at d ≤ 1000 take at most 6 iterations on F1 / F4 / F6 / F12 over 200 generations, and a capped solve escalates the schedule)"),
     "sbr_large_n_iters": Knob("EVOXMI_SBR_LARGE_N_ITERS", 8, int, "device eigensolver: least warm-schedule slots for matrices larger than sbr_lean_max_n"),
-    "sbr_cold_gens": Knob("EVOXMI_SBR_COLD_GENS", 4, int, "CMA-ES device eigensolver: the first generations that use the cold-start schedule (their own hipGraph; the generation index is host-known)"),
-    "sbr_cold_iters": Knob("EVOXMI_SBR_COLD_ITERS", 16, int, "CMA-ES device eigensolver: refinement slots of the cold-start schedule"),
-    "sbr_late_gens": Knob("EVOXMI_SBR_LATE_GENS", 24, int, "CMA-ES: generations from this index on replay a shorter 'late' eigensolver graph of sbr_late_iters slots (0: off) — at the bench config every solve from generation ≈22 to ≈305 converges in 4 iterations (5-7 before; profiles/r4_iters_per_gen_300.txt), so 6 slots keep a margin of 2"),
-    "sbr_late_iters": Knob("EVOXMI_SBR_LATE_ITERS", 5, int, "refinement slots of the late-generation eigensolver schedule (settled solves take 4; a capped solve escalates the schedule two generations later — round 5: 6 → 5 slots, 1.439 → 1.424 ms over 50 steps)"),
+    "sbr_cold_iters": Knob("EVOXMI_SBR_COLD_ITERS", 16, int, "CMA-ES device eigensolver: refinement slots of the cold-start schedule (every run starts on it; CMAES moves down to the warm / late schedules after consecutive solves that fit them with a slot to spare)"),
+    "sbr_late_iters": Knob("EVOXMI_SBR_LATE_ITERS", 5, int, "refinement slots of the late (settled) eigensolver schedule (settled solves take 4; a capped or slow solve moves the run back up two generations later — round 5: 6 → 5 slots, 1.439 → 1.424 ms over 50 steps)"),
     "sbr_late_full_slots": Knob("EVOXMI_SBR_LATE_FULL_SLOTS", 3, int, "late-generation eigensolver schedule: slots that carry the damping / Newton–Schulz / order-6 kernels (the rest are lean); settled generations need them in slots 0-2 only (profiles/r4_near_only_ab.txt detail)"),
     "sbr_late_damp_slots": Knob("EVOXMI_SBR_LATE_DAMP_SLOTS", 1, int, "late-generation eigensolver schedule: slots that carry the damping power steps (slot 0 always damps by the κ rule; in settled solves the later slots' power steps return at once — 6 launches per generation; a later slot whose step the κ rule would damp stops the solve, capped, and the host escalates)"),
     "sbr_damp_slots": Knob("EVOXMI_SBR_DAMP_SLOTS", 0, int, "device eigensolver: slots that carry the damping power steps in a schedule with lean slots (0: every full slot; the late CMA-ES variant sets sbr_late_damp_slots)"),
@@ -62,10 +60,10 @@ KNOBS: Dict[str, Knob] = {
     "sbr_theta0": Knob("EVOXMI_SBR_THETA0", 1.0, float, "sbr: local far-pair threshold factor θ in every iteration whose κ ≤ sbr_theta_kappa (0: switched on only after a stalled far iteration). θ = 1 keeps steady-state CMA-ES solves at 4 iterations where θ = 0 stalls at ≈1.3e-5 for tens of generations (profiles/r4_sbr_threshold_variants.txt)"),
     "sbr_theta_kappa": Knob("EVOXMI_SBR_THETA_KAPPA", 0.05, float, "sbr: κ below which the local far threshold θ applies (larger far steps with it diverged in cold-start solves)"),
     "sbr_thr_fac": Knob("EVOXMI_SBR_THR_FAC", 0.3, float, "sbr: global far-pair threshold factor (gap > thr_fac·(block/2)·spread/n)"),
+    "sbr_corr_prec": Knob("EVOXMI_SBR_CORR_PREC", "x3", str, "device eigensolver: precision of the correction products (X², X³, the Taylor terms of exp(αX) − I, Bq·(V − I), Newton–Schulz T·(TᵀT − I)) — 'x3' (bf16x3, ≈1e-5 of the correction's size; the residual products Bᵀ C B and TᵀT stay bf16x6) or 'x6' (every product f32-accurate, the round-5 solver)"),
     "cma_fused": Knob("EVOXMI_CMA_FUSED", 1, int, "CMA-ES tell epilogue as the fused cmaes.hip kernels (0: reference-shaped torch ops)"),
     "sbr_recover": Knob("EVOXMI_SBR_RECOVER", 2, int, "device eigensolver: divergences (off-norm up > 1.5× in one iteration) answered by a forced damped + re-orthonormalised step from the current basis before the solve gives up and keeps the better of the current and the warm-start basis (0: give up at the first, the round-4 behaviour)"),
     "sbr_lean_guard": Knob("EVOXMI_SBR_LEAN_GUARD", 1, int, "device eigensolver: a lean slot (no damping / Newton–Schulz / order-6 kernels) whose step the full rules would damp, re-orthonormalise or take to order 6 stops the solve as capped instead of taking an unguarded order-4 step (the host then escalates the schedule)"),
-    "sbr_escalate_gens": Knob("EVOXMI_SBR_ESCALATE_GENS", 8, int, "CMA-ES device eigensolver: after a solve reports itself capped or fell back (seen by the host one generation late through a pinned copy + event query), this many generations replay the next longer schedule (late → 8-slot → cold)"),
     "sbr_lean_max_n": Knob("EVOXMI_SBR_LEAN_MAX_N", 1024, int, "device eigensolver: lean tail slots only for matrices up to this order (larger ones keep the damping / Newton–Schulz kernels in every slot)"),
     "sbr_xgate": Knob("EVOXMI_SBR_XGATE", 2, int, "device eigensolver: the damping's power iteration also follows free bounds of the generator (the X² GEMM's diagonal stats): skipped when ‖X‖₂ ≤ τ is proven, run when a row of X is longer than τ/2 whatever κ says — 1 in every schedule, 2 in the cold-start schedule only (where an undamped step on a large generator diverged the d = 2000 cold start; in settled solves it costs ≈3 % of a generation), 0 off"),
     "cec_stack": Knob("EVOXMI_CEC_STACK", 1, int, "CEC'22 compositions (F9–F12) on the device: every rotated component from ONE GEMM over the stacked rotations with per-block exact shifts (1) or one GEMM per component (0)"),

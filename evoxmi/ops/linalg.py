@@ -155,7 +155,8 @@ def mm(A: torch.Tensor, B: torch.Tensor, *, ta: bool = False, tb: bool = False, 
        Cin: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
        skip: Optional[torch.Tensor] = None, a_sub_k: Optional[torch.Tensor] = None, sel: Optional[torch.Tensor] = None,
        A2: Optional[torch.Tensor] = None, alpha2: Optional[float] = None, C2: Optional[torch.Tensor] = None,
-       stat_part: Optional[torch.Tensor] = None, stat_diag_only: bool = False) -> torch.Tensor:
+       stat_part: Optional[torch.Tensor] = None, stat_diag_only: bool = False, prec: Optional[str] = None,
+       diag_add: float = 0.0) -> torch.Tensor:
     """``alpha·(*alpha_ptr)·op(A)·op(B) (+ bias_n) (+ beta·Cin)`` with ``op(X) = Xᵀ`` when
     ``ta`` / ``tb`` (transposes are layouts, never copies).  ``mode`` 1 / 2: the result is
     symmetric / skew-symmetric by construction of the caller (Bᵀ C B, X·X for skew X, …);
@@ -168,6 +169,10 @@ def mm(A: torch.Tensor, B: torch.Tensor, *, ta: bool = False, tb: bool = False, 
     ``stat_part`` (mode 1): float64 partials of [Σ offdiag², Σ diag², min diag, max diag] per
     workgroup (``sbr_stats_final`` layout; length ``4·gemm_ks_grid``); ``stat_diag_only``: the
     diagonal's terms only (Σ offdiag² left 0 — the cheaper epilogue of the eigensolver's X²).
+    ``prec="x3"`` (device, with ``out``): bf16x3 products (≈1e-5 relative per product) for
+    results that are a small correction of something held exactly (the eigensolver's
+    exp(αX) − I terms); default: the process-wide f32-accurate precision.  ``diag_add``: added
+    to the result's diagonal (``out=`` only; Bᵀ B − I).
 
     On a GPU this is always the framework kernel (no vendor GEMM); shapes the kernel does
     not take (K % 4 ≠ 0 with a K-contiguous operand) go to :func:`gemm`."""
@@ -186,10 +191,11 @@ def mm(A: torch.Tensor, B: torch.Tensor, *, ta: bool = False, tb: bool = False, 
                     float(beta), Cin)
             if out is not None:
                 a2 = float(alpha if alpha2 is None else alpha2)
-                _ext.ops().gemm_ks_out(*args, out, skip, a_sub_k, sel, A2, a2, C2, stat_part, int(stat_diag_only))
+                _ext.ops().gemm_ks_out(*args, out, skip, a_sub_k, sel, A2, a2, C2, stat_part, int(stat_diag_only),
+                                       3 if prec == "x3" else 0, float(diag_add))
                 return out
-            if sel is not None or stat_part is not None:
-                raise ValueError("mm: sel / stat_part need out=")
+            if sel is not None or stat_part is not None or prec is not None or diag_add:
+                raise ValueError("mm: sel / stat_part / prec / diag_add need out=")
             return _ext.ops().gemm_ks(*args, skip, a_sub_k)
         if skip is not None or sel is not None or stat_part is not None:
             raise ValueError("mm: skip / sel / stat_part need a shape the gemm_ks kernel takes")
@@ -210,6 +216,8 @@ def mm(A: torch.Tensor, B: torch.Tensor, *, ta: bool = False, tb: bool = False, 
         C = C + bias_n[None, :N]
     if Cin is not None:
         C = C + beta * Cin[:M, :N]
+    if diag_add:
+        C = C + diag_add * torch.eye(M, N, dtype=C.dtype)
     if skip is not None and int(skip.reshape(-1)[0]) != 0:
         return out if out is not None else torch.zeros(M, N, dtype=torch.float32)
     if out is not None:

@@ -92,6 +92,11 @@ class DeviceSBR:
         self.eig_stats = torch.zeros(4, dtype=torch.float64, device=dev)
         self.log = torch.zeros(LOG_LEN, 4, dtype=torch.float64, device=dev)
         self.log_count = torch.zeros(1, dtype=torch.int32, device=dev)
+        # precision tiers (round 6): the residual products (Bᵀ C B, BᵀB) stay f32-accurate
+        # (bf16x6); the products that only form a correction of an exactly held matrix —
+        # X², X³ and the Taylor terms of exp(αX) − I, the basis update Bq + Bq·(V − I), and
+        # Newton–Schulz's T − ½T·(TᵀT − I) — run at bf16x3 (≈1e-5 of the correction's own size)
+        self.corr = "x3" if config.get("sbr_corr_prec") == "x3" else None
         self.prm = [float(cfg.tol), float(cfg.ns_kappa), float(cfg.damp_kappa), float(cfg.t4_kappa), float(cfg.near_only),
                     float(cfg.theta0), float(cfg.theta_kappa), float(self.lean_from), float(config.get("sbr_recover")),
                     float(config.get("sbr_lean_guard")), float(self.xgate), float(self.damp_from)]
@@ -130,8 +135,10 @@ class DeviceSBR:
         else:
             ops.sbr16_far_bq_out(self.A, self.perm, self.Q, self.dq, self.hist[4 * j : 4 * j + 4], float(cfg.thr_fac),
                                  self.theta[j : j + 1], self.X, self.B, self.Bq, sb, sk_far, sk_all)
+        corr = self.corr
         # X skew ⇒ X² = −X·Xᵀ, symmetric (upper tiles only)
-        mm(self.X, self.X, tb=True, mode=1, alpha=-1.0, out=self.X2, skip=sk_far, stat_part=self.part2, stat_diag_only=True)
+        mm(self.X, self.X, tb=True, mode=1, alpha=-1.0, out=self.X2, skip=sk_far, stat_part=self.part2, stat_diag_only=True,
+           prec=corr)
         if cfg.damp_tau > 0 and damp_slot:
             # three power-step launches (they return at once when the free Frobenius bound already
             # gives α = 1); α itself is formed by the prep kernel below (no_final)
@@ -139,19 +146,30 @@ class DeviceSBR:
                                 self.part2)
         if full:
             # order 6 only: X³ = X²·X = −X²·Xᵀ (skew)
-            mm(self.X2, self.X, tb=True, mode=2, alpha=-1.0, out=self.X3, skip=sk_x3)
+            mm(self.X2, self.X, tb=True, mode=2, alpha=-1.0, out=self.X3, skip=sk_x3, prec=corr)
         damp_here = cfg.damp_tau > 0 and damp_slot
         # near-only iterations (no far step): the block-rotated basis is the new basis — Bq → B
         # copied by this launch (it returns at once otherwise), no copy launch of its own
         ops.sbr_dev_prep(self.X, self.X2, self.X3, self.alpha[j + 1 : j + 2], self.P, self.VT, c, self.work if damp_here else None,
-                         float(cfg.damp_tau), self.part2, self.Bq, self.B)
+                         float(cfg.damp_tau), self.part2, self.Bq, self.B, int(corr is not None))
         # Vᵀ = M(−α) + X²·Pᵀ (order 4) or M(−α) − X³·Pᵀ (order 6): the control word selects
-        mm(self.X2, self.P, tb=True, alpha=1.0, beta=1.0, Cin=self.VT, out=self.VT, skip=sk_far, sel=sel6, A2=self.X3, alpha2=-1.0)
+        # (with the tiered precision the prep wrote M − I, so this is Vᵀ − I)
+        mm(self.X2, self.P, tb=True, alpha=1.0, beta=1.0, Cin=self.VT, out=self.VT, skip=sk_far, sel=sel6, A2=self.X3, alpha2=-1.0,
+           prec=corr)
         # B·V → B, or into T when Newton–Schulz follows
-        mm(self.Bq, self.VT, tb=True, out=self.B, skip=sk_far, sel=sel_ns, C2=self.T)
+        if corr is not None:
+            # Bq + Bq·(V − I): the exact basis plus an x3 correction product
+            mm(self.Bq, self.VT, tb=True, beta=1.0, Cin=self.Bq, out=self.B, skip=sk_far, sel=sel_ns, C2=self.T, prec=corr)
+        else:
+            mm(self.Bq, self.VT, tb=True, out=self.B, skip=sk_far, sel=sel_ns, C2=self.T)
         if full:
-            mm(self.T, self.T, ta=True, mode=1, out=self.G, skip=sk_ns)
-            mm(self.T, self.G, tb=True, alpha=-0.5, beta=1.5, Cin=self.T, out=self.B, skip=sk_ns)
+            if corr is not None:
+                # E = TᵀT − I at full precision (the orthogonality residual), then T − ½T·E
+                mm(self.T, self.T, ta=True, mode=1, out=self.G, skip=sk_ns, diag_add=-1.0)
+                mm(self.T, self.G, tb=True, alpha=-0.5, beta=1.0, Cin=self.T, out=self.B, skip=sk_ns, prec=corr)
+            else:
+                mm(self.T, self.T, ta=True, mode=1, out=self.G, skip=sk_ns)
+                mm(self.T, self.G, tb=True, alpha=-0.5, beta=1.5, Cin=self.T, out=self.B, skip=sk_ns)
         self._btcb(C, sk_all)
         self._ctrl(j, C)
 
@@ -193,10 +211,20 @@ def workspace(n: int, device, cfg: SBRConfig, iters: int, lean_from: int = None,
     key = (n, str(device), cfg.block, cfg.block_sweeps, cfg.thr_fac, cfg.ns_iters, cfg.damp_tau, cfg.tol, cfg.ns_kappa,
            cfg.damp_kappa, cfg.t4_kappa, cfg.near_only, cfg.theta0, cfg.theta_kappa, int(iters), lean_from,
            bool(config.get("sbr_prepermute")), float(config.get("sbr_sweep_tol")), int(config.get("sbr_recover")),
-           int(config.get("sbr_lean_guard")), bool(xgate), damp_from)
+           int(config.get("sbr_lean_guard")), bool(xgate), damp_from, config.get("sbr_corr_prec"))
     if key not in _WS:
         _WS[key] = DeviceSBR(n, device, cfg, iters, lean_from, xgate, damp_from)
     return _WS[key]
+
+
+def schedule_iters(n: int, iters: int) -> int:
+    """Refinement slots a schedule of ``iters`` slots actually runs at order ``n`` (larger
+    matrices get at least ``sbr_large_n_iters``; see :func:`eigh_device`)."""
+    from .. import config
+
+    if n > int(config.get("sbr_lean_max_n")) and iters < int(config.get("sbr_cold_iters")):
+        return max(int(iters), int(config.get("sbr_large_n_iters")))
+    return int(iters)
 
 
 def eigh_device(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None, iters: int = None):

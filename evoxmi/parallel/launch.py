@@ -11,7 +11,8 @@ process per GPU over RCCL, so a launch without ``torchrun`` spawns the ranks its
   initialising HIP: ``torch.cuda.device_count()`` does not on this image), spawns N fresh
   child processes with the torchrun environment (``RANK`` / ``LOCAL_RANK`` / ``WORLD_SIZE``,
   ``MASTER_ADDR=127.0.0.1``, a free ``MASTER_PORT``), forwards their output and exits with the
-  first non-zero child status.  The parent never touches the GPU, so no HIP context is forked
+  status of the first child to fail — the other ranks are then terminated (they would block in
+  a collective with the dead rank), and so are all of them when the parent is interrupted.  The parent never touches the GPU, so no HIP context is forked
   or exec'd.
 * ``device="cpu"``: the ranks run on gloo (tests of the launcher on a GPU-less host).
 """
@@ -40,31 +41,72 @@ def visible_devices() -> int:
     return int(torch.cuda.device_count())
 
 
-def spawn_ranks(n: int, argv: List[str], device: str = "cuda", env: Optional[dict] = None, timeout: Optional[float] = None) -> int:
-    """Run ``python argv…`` as N ranks of one job; returns the job's exit status (0 when
-    every rank exited 0, else the first non-zero status in rank order)."""
+def _stop(procs, grace: float = 5.0) -> None:
+    """Terminate every live child, then kill whatever is still running after ``grace`` s."""
+    import time
+
+    live = [p for p in procs if p.poll() is None]
+    for p in live:
+        p.terminate()
+    t_end = time.monotonic() + grace
+    for p in live:
+        try:
+            p.wait(timeout=max(0.0, t_end - time.monotonic()))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+
+
+def spawn_ranks(n: int, argv: List[str], device: str = "cuda", env: Optional[dict] = None, timeout: Optional[float] = None,
+                poll_s: float = 0.05) -> int:
+    """Run ``python argv…`` as N ranks of one job; returns the job's exit status: 0 when every
+    rank exited 0, else the status of the FIRST rank to fail (in time, not rank order).
+
+    All children are polled together: when one exits non-zero the others are terminated at
+    once (a surviving rank would otherwise block forever in a collective with the dead one),
+    and a ``timeout`` (seconds) or an interrupt of the parent (SIGINT / SIGTERM) ends every
+    child too, so no rank is left holding a GPU."""
+    import signal
+    import time
+
     base = dict(os.environ if env is None else env)
     base.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                 EVOXMI_LAUNCHED="1")
     procs = []
-    for r in range(n):
-        e = dict(base, RANK=str(r), LOCAL_RANK=str(r), GROUP_RANK="0")
-        if device == "cpu":
-            e["EVOXMI_DIST_BACKEND"] = "gloo"
-        procs.append(subprocess.Popen([sys.executable] + list(argv), env=e))
-    codes = []
-    for p in procs:
+
+    def _on_signal(signum, _frame):
+        _stop(procs)
+        raise SystemExit(128 + signum)
+
+    old = {}
+    for sig in (signal.SIGINT, signal.SIGTERM):
         try:
-            codes.append(p.wait(timeout=timeout))
-        except subprocess.TimeoutExpired:
-            for q in procs:
-                if q.poll() is None:
-                    q.kill()
-            codes.append(124)
-    for c in codes:
-        if c != 0:
-            return c
-    return 0
+            old[sig] = signal.signal(sig, _on_signal)
+        except ValueError:  # not the main thread: the finally below still cleans up
+            pass
+    try:
+        for r in range(n):
+            e = dict(base, RANK=str(r), LOCAL_RANK=str(r), GROUP_RANK="0")
+            if device == "cpu":
+                e["EVOXMI_DIST_BACKEND"] = "gloo"
+            procs.append(subprocess.Popen([sys.executable] + list(argv), env=e))
+        t_end = None if timeout is None else time.monotonic() + timeout
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c is not None and c != 0]
+            if bad:
+                _stop(procs)
+                return bad[0]
+            if all(c == 0 for c in codes):
+                return 0
+            if t_end is not None and time.monotonic() > t_end:
+                _stop(procs)
+                return 124
+            time.sleep(poll_s)
+    finally:
+        _stop(procs)
+        for sig, h in old.items():
+            signal.signal(sig, h)
 
 
 def ensure_ranks(n: int, device: str = "cuda", argv: Optional[List[str]] = None) -> None:

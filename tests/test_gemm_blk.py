@@ -123,6 +123,28 @@ def test_h3_row_scaling_keeps_relative_accuracy():
     assert ((C - R).abs() <= tol).all(), float(((C - R).abs() / tol).max())
 
 
+@pytest.mark.gpu
+def test_h3_tiny_and_wide_range_rows_stay_finite_and_bounded():
+    """a row whose max is below ≈2⁻¹¹⁰ used to get a scale of 2^e > 2¹²⁸ = inf (NaN
+    planes); the exponent is clamped.  A row spanning 20 decades keeps the Σ|ab| bound (its small
+    elements fall into f16 subnormals of m, bounded absolutely by the row max)."""
+    g = torch.Generator().manual_seed(11)
+    M, N, K = 8, 64, 1000
+    X = torch.randn(M, K, generator=g)
+    X[0] *= 1e-36
+    X[1] *= 5e-35
+    X[2] = X[2] * torch.logspace(0, -20, K, dtype=torch.float64).float()
+    X[3, :] = 0.0
+    X[3, 17] = 1e-37
+    Bm = torch.randn(N, K, generator=g)
+    C = linalg.mm_h3(linalg.h3_planes(X.cuda()), linalg.h3_planes(Bm.cuda())).cpu().double()
+    assert torch.isfinite(C).all()
+    R = X.double() @ Bm.double().t()
+    # f32 output resolution near the subnormal range: one ulp of the smallest normal
+    tol = 2e-6 * (X.double().abs() @ Bm.double().abs().t()) + 2e-45
+    assert ((C - R).abs() <= tol).all(), float(((C - R).abs() / tol).max())
+
+
 @pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
 @pytest.mark.parametrize("M,K,ncomp,sub", [(700, 1000, 5, 1024), (333, 200, 3, 256), (64, 37, 2, 128), (1000, 1200, 2, 1280)])
 def test_h3_stacked_components_match_fp64(device, M, K, ncomp, sub):

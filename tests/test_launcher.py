@@ -65,3 +65,38 @@ def test_spawn_ranks_reports_first_failure(tmp_path):
     script = tmp_path / "r.py"
     script.write_text("import os, sys\nsys.exit(3 if os.environ['RANK'] == '1' else 0)\n")
     assert spawn_ranks(3, [str(script)], device="cpu") == 3
+
+
+def test_spawn_ranks_stops_ranks_blocked_on_a_dead_peer(tmp_path):
+    """Rank 1 exits non-zero after rendezvous while rank 0 waits in a barrier: the launcher
+    returns rank 1's status promptly and terminates rank 0 (no hang, no orphan)."""
+    import time
+
+    from evoxmi.parallel.launch import spawn_ranks
+
+    pidfile = tmp_path / "pid0"
+    script = tmp_path / "r.py"
+    script.write_text(
+        "import os, sys, datetime\n"
+        "import torch.distributed as dist\n"
+        "dist.init_process_group('gloo', timeout=datetime.timedelta(seconds=600))\n"
+        "if dist.get_rank() == 1:\n"
+        "    sys.exit(5)\n"
+        f"open({str(pidfile)!r}, 'w').write(str(os.getpid()))\n"
+        "dist.barrier()\n"
+    )
+    t0 = time.monotonic()
+    assert spawn_ranks(2, [str(script)], device="cpu", timeout=300) == 5
+    assert time.monotonic() - t0 < 120
+    if pidfile.exists():
+        pid = int(pidfile.read_text())
+        with pytest.raises(ProcessLookupError):
+            os.kill(pid, 0)  # reaped: no process left behind
+
+
+def test_spawn_ranks_timeout_kills_every_rank(tmp_path):
+    from evoxmi.parallel.launch import spawn_ranks
+
+    script = tmp_path / "r.py"
+    script.write_text("import time\ntime.sleep(600)\n")
+    assert spawn_ranks(2, [str(script)], device="cpu", timeout=2) == 124

@@ -127,8 +127,9 @@ def test_cmaes_device_mode_checkpoint_resume_is_bitwise(tmp_path):
 def test_cmaes_default_schedule_converges_every_generation_from_cold_start():
     """The north-star configuration (d = 1000, λ = 10 000, CEC'22 F1) with the DEFAULT
     device schedule for 200 generations from a cold start (C = I): the first generations
-    replay the cold-start graph variant (CMAES.graph_variant), then the 8-slot schedule, from
-    generation sbr_late_gens on the shorter late schedule, and every logged solve reaches the tolerance — no capped, no fallen-back decomposition
+    replay the cold-start graph variant (CMAES.graph_variant), then — chosen from the measured
+    convergence of the solves two generations back — the warm schedule and the shorter late
+    one, and every logged solve reaches the tolerance — no capped, no fallen-back decomposition
     (the reference decomposes exactly every generation, cma_es.py:155-160,193-198)."""
     from evoxmi import config
     from evoxmi import random as rnd
@@ -153,8 +154,11 @@ def test_cmaes_default_schedule_converges_every_generation_from_cold_start():
     tol = config.get("eigh_tol")
     assert float(h[:, 0].max()) <= tol, h[h[:, 0] > tol]
     assert float(h[:, 3].sum()) == 0.0
-    assert set(wf._graphs) == ({"cold", None, "late"} if 0 < config.get("sbr_late_gens") < 200 else {"cold", None})
+    assert set(wf._graphs) == {"cold", None, "late"}
     assert int(h[:, 2].max()) <= max(config.get("sbr_device_iters"), config.get("sbr_cold_iters"))
+    lv = wf.algorithm.schedule_levels()
+    assert lv.startswith("CC") and "W" in lv and lv.endswith("L" * 100), lv  # settled runs end on the late schedule
+    assert wf.algorithm.schedule_escalations == 0
 
 
 def _long_run(func: int, d: int, pop: int, gens: int, seed: int = 2024, init_stdev: float = 20.0):
@@ -196,7 +200,7 @@ def test_cmaes_default_schedule_converges_on_other_functions_and_dims(func, d):
     bad = h[(h[:, 0] > tol) | (h[:, 3] != 0)]
     assert bad.shape[0] == 0, bad
     assert int((h[:, 1].long() & 1).sum()) == 0  # no capped solve
-    assert algo.__dict__.get("_esc_count", 0) == 0
+    assert algo.schedule_escalations == 0
 
 
 def test_cmaes_basis_stays_orthogonal_over_600_generations():
@@ -254,17 +258,17 @@ def test_sim8_trajectory_recovers_from_divergence():
 
 
 def test_capped_late_solves_escalate_the_schedule_without_device_syncs(monkeypatch):
-    """sbr_late_iters = 2 (3 full slots clipped to 2): the late schedule cannot converge, its
-    solves report themselves capped, and the host — reading each solve's health two steps
-    later from the pinned ring, never through .item() or a device synchronize — switches to
-    the 8-slot schedule within ESC_LAG generations of the first late generation."""
+    """sbr_late_iters = 2 (2 full slots): once the run is put on the late schedule its solves
+    cannot converge, report themselves capped, and the host — reading each solve's health two
+    steps later from the pinned ring, never through .item() or a device synchronize — moves
+    the run back to the warm schedule ESC_LAG generations after the first late one."""
     from evoxmi import config
     from evoxmi import random as rnd
     from evoxmi.algorithms import CMAES
     from evoxmi.problems.numerical import CEC2022TestSuit
     from evoxmi.workflows import StdWorkflow
 
-    with config.override(sbr_late_gens=12, sbr_late_iters=2, sbr_late_full_slots=2):
+    with config.override(sbr_late_iters=2, sbr_late_full_slots=2):
         center = (torch.rand(1000, generator=torch.Generator().manual_seed(1)) * 160 - 80).cuda()
         algo = CMAES(center_init=center, init_stdev=20.0, pop_size=10000)
         wf = StdWorkflow(algo, CEC2022TestSuit.create(1), graph=True)
@@ -272,22 +276,23 @@ def test_capped_late_solves_escalate_the_schedule_without_device_syncs(monkeypat
         st = wf.step(st)
         st = wf.prepare_graphs(st, 40)
         assert set(wf._graphs) == {"cold", None, "late"}
+        for _ in range(11):
+            st = wf.step(st)
+        # a 2-slot late schedule never fits "with a slot to spare": force the run onto it
+        algo._sched()["level"] = 0
 
         def forbidden(*a, **k):
             raise AssertionError("device sync on the step path")
 
-        variants = []
         with monkeypatch.context() as m:
             m.setattr(torch.cuda, "synchronize", forbidden)
             m.setattr(torch.Tensor, "item", forbidden)
-            for _ in range(24):
-                variants.append(algo.graph_variant(int(st.generation)))
+            for _ in range(12):
                 st = wf.step(st)
         torch.cuda.synchronize()
-    late = [i + 1 for i, v in enumerate(variants) if v == "late"]
-    assert late, variants
-    first_late = late[0]
-    # generation first_late replays the late graph; its capped solve is read ESC_LAG steps on
-    esc = [g for g, v in enumerate(variants, start=1) if g > first_late and v is None]
-    assert esc and esc[0] <= first_late + CMAES.ESC_LAG + 1, variants
-    assert algo.__dict__.get("_esc_count", 0) >= 1
+    lv = algo.schedule_levels(12)
+    # the first forced step replays the late graph; the solves read after it (still the warm
+    # ones in flight, then the capped late one) move the run back within ESC_LAG + 1 steps
+    assert lv[0] == "L" and "W" in lv[1 : CMAES.ESC_LAG + 2] and lv.endswith("W" * 6), lv
+    assert "C" not in lv  # the capped solves still in flight do not push the run to cold
+    assert algo.schedule_escalations >= 1

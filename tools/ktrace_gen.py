@@ -12,6 +12,7 @@ ap.add_argument("trace")
 ap.add_argument("--marker", default="philox_fill")
 ap.add_argument("--show", type=int, default=-2)
 ap.add_argument("--quiet", action="store_true")
+ap.add_argument("--agg", type=int, default=0)
 a = ap.parse_args()
 rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
 idx = [i for i, r in enumerate(rows) if a.marker in r["Kernel_Name"]]
@@ -30,3 +31,22 @@ if not a.quiet and gens:
         s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
         print(f"{(s - t0) / 1e3:8.1f} gap {(s - prev) / 1e3:6.1f} dur {(e - s) / 1e3:6.1f}  {r['Kernel_Name'][:90]}")
         prev = e
+
+# --agg N: per-kernel totals over the last N full generations (µs per generation)
+import sys as _sys
+
+if "--agg" in _sys.argv:
+    n = int(_sys.argv[_sys.argv.index("--agg") + 1])
+    sel = gens[-n:]
+    agg = {}
+    for g0, g1, _, _ in sel:
+        for r in rows[g0:g1]:
+            nm = r["Kernel_Name"][:110]
+            d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+            c, t = agg.get(nm, (0, 0.0))
+            agg[nm] = (c + 1, t + d)
+    walls = sum(g[2] for g in sel) / len(sel)
+    busy = sum(g[3] for g in sel) / len(sel)
+    print(f"=== last {len(sel)} generations: wall {walls:.1f} us, busy {busy:.1f} us per generation")
+    for nm, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+        print(f"{t / len(sel):9.1f} us/gen  calls/gen {c / len(sel):5.1f}  avg {t / c:7.2f} us  {nm}")
