@@ -261,9 +261,6 @@ at::Tensor gemm_ks(const at::Tensor& A, int64_t a_kc, const at::Tensor& B, int64
   a.prec = (int)prec;
   a.diag_add = (float)diag_add;
   a.c_vec4 = vec4_ok(C) ? 1 : 0;
-  // the partials' length (gemm_ks_grid) assumed the square-product kernel for this shape
-  TORCH_CHECK(!a.stat_part || !evx_gemm_ks_sq_shape((int)M, (int)N, (int)mode) || evx_gemm_ks_routes_sq(a),
-              "gemm_ks: stats partials of a square product need 16-byte aligned operands (gemm_sq)");
   evx_gemm_ks(a, cur_stream());
   return C;
 }
@@ -276,7 +273,7 @@ at::Tensor gemm_ks_pl(const c10::optional<at::Tensor>& A, const c10::optional<at
                       const c10::optional<at::Tensor>& out, const c10::optional<at::Tensor>& a_sub_k, int64_t sub_cols, int64_t sub_ld) {
   const bool ha = A.has_value() && A->defined(), hap = a_pl.has_value() && a_pl->defined();
   const bool hb = B.has_value() && B->defined(), hbp = b_pl.has_value() && b_pl->defined();
-  TORCH_CHECK(ha != hap && hb != hbp, "gemm_ks_pl: give each operand as f32 or as planes");
+  TORCH_CHECK(ha && hb && !hap && !hbp, "gemm_ks_pl: f32 operands (fragment planes were removed in round 6)");
   TORCH_CHECK(M > 0 && N > 0 && K > 0 && K % 4 == 0, "gemm_ks_pl: shape (K % 4 == 0)");
   const int64_t kp = (K + 31) / 32 * 32;
   auto vec4_ok = [](const at::Tensor& t) { return (reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0) && (t.stride(0) % 4 == 0); };
@@ -348,39 +345,9 @@ at::Tensor gemm_ks_pl(const c10::optional<at::Tensor>& A, const c10::optional<at
   return C;
 }
 
-at::Tensor split_planes(const at::Tensor& X, const c10::optional<at::Tensor>& colscale) {
-  CHECK_DEV(X); CHECK_F32(X);
-  TORCH_CHECK(X.dim() == 2 && X.stride(1) == 1, "split_planes: 2-D, unit inner stride");
-  const int64_t rows = X.size(0), K = X.size(1), kp = (K + 31) / 32 * 32;
-  const float* cs = nullptr;
-  if (colscale.has_value() && colscale->defined()) {
-    CHECK_DEV(*colscale); CHECK_F32(*colscale); CHECK_CONTIG(*colscale);
-    TORCH_CHECK(colscale->numel() >= K, "split_planes: colscale length");
-    cs = colscale->data_ptr<float>();
-  }
-  c10::DeviceGuard g(X.device());
-  at::Tensor out = at::empty({3, rows, kp}, X.options().dtype(at::kShort));
-  evx_split_planes(X.data_ptr<float>(), X.stride(0), rows, (int)K, cs, reinterpret_cast<uint16_t*>(out.data_ptr<int16_t>()), kp,
-                   cur_stream());
-  return out;
-}
-
-at::Tensor philox_normal_planes(const at::Tensor& key, int64_t rows, int64_t d, int64_t row0) {
-  CHECK_DEV(key);
-  TORCH_CHECK(key.scalar_type() == at::kLong && key.numel() >= 2 && key.is_contiguous(), "philox_normal_planes: key int64[2]");
-  TORCH_CHECK(d % 4 == 0 && rows > 0, "philox_normal_planes: d % 4 == 0");
-  const int64_t kp = (d + 31) / 32 * 32;
-  c10::DeviceGuard g(key.device());
-  at::Tensor out = at::empty({3, rows, kp}, key.options().dtype(at::kShort));
-  evx_philox_normal_planes(key.data_ptr<int64_t>(), rows, (int)d, row0, reinterpret_cast<uint16_t*>(out.data_ptr<int16_t>()), kp,
-                           cur_stream());
-  return out;
-}
-
 void gemm_ks_set_tile(int64_t t) { evx_gemm_ks_set_tile((int)t); }
 void gemm_ks_set_prec(int64_t p) { evx_gemm_ks_set_prec((int)p); }
 void gemm_ks_set_nw8(int64_t t) { evx_gemm_ks_set_nw8((int)t); }
-void gemm_sq_enable(int64_t on) { evx_gemm_sq_enable((int)on); }
 
 at::Tensor gemm_ks_new(const at::Tensor& A, int64_t a_kc, const at::Tensor& B, int64_t b_kc, int64_t M, int64_t N, int64_t K,
                        int64_t mode, double alpha, const c10::optional<at::Tensor>& alpha_ptr,
@@ -478,20 +445,6 @@ void sbr16_far_bq_out(const at::Tensor& A, const at::Tensor& perm, const at::Ten
                    skip_bq.data_ptr<int>(), pre);
 }
 
-void sbr16_permute_out(const at::Tensor& A, const at::Tensor& perm, const at::Tensor& B, at::Tensor& Ap, at::Tensor& Bp,
-                       const at::Tensor& skip_a, const at::Tensor& skip_b) {
-  const int64_t n = A.size(0);
-  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&A, &B, &Ap, &Bp}) {
-    CHECK_DEV(*t); CHECK_F32(*t);
-    TORCH_CHECK(t->dim() == 2 && t->size(1) == n && t->stride(1) == 1, "sbr16_permute_out: (·, n) row-major");
-  }
-  TORCH_CHECK(A.size(0) == n && Ap.size(0) == n && Ap.stride(0) == n && Bp.sizes() == B.sizes() && Bp.stride(0) == n &&
-                  n <= evx_sbr16_max_n() && perm.scalar_type() == at::kInt && perm.numel() >= n,
-              "sbr16_permute_out: shapes");
-  TORCH_CHECK(skip_a.scalar_type() == at::kInt && skip_b.scalar_type() == at::kInt, "sbr16_permute_out: skip words int32");
-  evx_sbr16_permute(A.data_ptr<float>(), (int)n, A.stride(0), perm.data_ptr<int>(), B.data_ptr<float>(), (int)B.size(0), B.stride(0),
-                    Ap.data_ptr<float>(), Bp.data_ptr<float>(), cur_stream(), skip_a.data_ptr<int>(), skip_b.data_ptr<int>());
-}
 void sbr16_bq_out(const at::Tensor& B, const at::Tensor& perm, const at::Tensor& Q, at::Tensor& Bq, int64_t sb, const at::Tensor& skip) {
   const int64_t n = B.size(1);
   TORCH_CHECK(Bq.sizes() == B.sizes() && Bq.stride(1) == 1 && B.stride(1) == 1, "sbr16_bq_out: shapes");
@@ -1259,6 +1212,13 @@ void moead_halo_gather(at::Tensor& pop, const at::Tensor& slots, const at::Tenso
                         starts.data_ptr<int>(), (int)peer.numel(), (int)pop.size(1), cur_stream(), fp, nf);
 }
 
+// writer side of the peer-buffer contract (parallel/peer.py): a system-scope release on the
+// current stream after the kernels that wrote a peer-visible buffer
+void peer_release(int64_t device) {
+  c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device));
+  evx_peer_release(cur_stream());
+}
+
 // hipMalloc'd buffer (an allocation base, so its IPC handle maps exactly this tensor)
 at::Tensor ipc_alloc(int64_t numel, int64_t device) {
   c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device));
@@ -1365,6 +1325,39 @@ at::Tensor cma_center_rows(const at::Tensor& pop, const c10::optional<at::Tensor
   evx_cma_center_rows(pop.data_ptr<float>(), pop.stride(0), rp, mean.data_ptr<float>(), sigma.contiguous().data_ptr<float>(),
                       w.data_ptr<float>(), (int)K, (int)d, Y.data_ptr<float>(), cur_stream());
   return Y;
+}
+
+// sharded tell: this rank's rows of the global top μ, compacted (see cmaes.hip local_select_kernel)
+void cma_local_select(const at::Tensor& order, int64_t mu, const at::Tensor& w, int64_t start, int64_t size, at::Tensor& rows,
+                      at::Tensor& wk) {
+  CHECK_DEV(order); CHECK_DEV(w); CHECK_DEV(rows); CHECK_DEV(wk); CHECK_F32(w); CHECK_F32(wk);
+  TORCH_CHECK(order.scalar_type() == at::kInt && order.is_contiguous() && order.numel() >= mu, "cma_local_select: order int32[>= mu]");
+  TORCH_CHECK(w.is_contiguous() && w.numel() >= mu, "cma_local_select: w (mu,)");
+  TORCH_CHECK(rows.scalar_type() == at::kInt && rows.is_contiguous() && wk.is_contiguous() && wk.numel() == rows.numel(),
+              "cma_local_select: rows int32[K], wk float[K]");
+  TORCH_CHECK(start >= 0 && size >= 0 && rows.numel() >= std::min<int64_t>(mu, size), "cma_local_select: K >= min(mu, size)");
+  c10::DeviceGuard g(order.device());
+  evx_cma_local_select(order.data_ptr<int32_t>(), (int)mu, w.data_ptr<float>(), (int)start, (int)size, (int)rows.numel(),
+                       rows.data_ptr<int32_t>(), wk.data_ptr<float>(), cur_stream());
+}
+
+// d × d symmetric ↔ packed upper triangle (d(d+1)/2 floats)
+void sym_pack(const at::Tensor& S, at::Tensor& P) {
+  CHECK_DEV(S); CHECK_F32(S); CHECK_DEV(P); CHECK_F32(P);
+  TORCH_CHECK(S.dim() == 2 && S.size(0) == S.size(1) && S.stride(1) == 1, "sym_pack: square row-major S");
+  const int64_t d = S.size(0);
+  TORCH_CHECK(P.is_contiguous() && P.numel() >= d * (d + 1) / 2, "sym_pack: P float[d(d+1)/2]");
+  c10::DeviceGuard g(S.device());
+  evx_sym_pack(S.data_ptr<float>(), S.stride(0), (int)d, P.data_ptr<float>(), cur_stream());
+}
+
+void sym_unpack(const at::Tensor& P, at::Tensor& S) {
+  CHECK_DEV(S); CHECK_F32(S); CHECK_DEV(P); CHECK_F32(P);
+  TORCH_CHECK(S.dim() == 2 && S.size(0) == S.size(1) && S.stride(1) == 1, "sym_unpack: square row-major S");
+  const int64_t d = S.size(0);
+  TORCH_CHECK(P.is_contiguous() && P.numel() >= d * (d + 1) / 2, "sym_unpack: P float[d(d+1)/2]");
+  c10::DeviceGuard g(S.device());
+  evx_sym_unpack(P.data_ptr<float>(), (int)d, S.data_ptr<float>(), S.stride(0), cur_stream());
 }
 
 std::vector<at::Tensor> cma_delta_gemv(const at::Tensor& M, const at::Tensor& mean, const at::Tensor& dm, double cm) {
@@ -1566,15 +1559,14 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("gemm_ks_set_tile(int t) -> ()");
   m.def("gemm_ks_set_prec(int prec) -> ()");
   m.def("gemm_ks_set_nw8(int tiles) -> ()");
-  m.def("gemm_sq_enable(int on) -> ()");
   m.def("gemm_ks_pl(Tensor? A, Tensor? a_pl, Tensor? B, Tensor? b_pl, int M, int N, int K, float alpha, Tensor? alpha_ptr, Tensor? bias_n, Tensor(a!)? out, Tensor? a_sub_k, int sub_cols=0, int sub_ld=0) -> Tensor");
-  m.def("split_planes(Tensor X, Tensor? colscale) -> Tensor");
-  m.def("philox_normal_planes(Tensor key, int rows, int d, int row0) -> Tensor");
   m.def("sbr16_far_bq_out(Tensor A, Tensor perm, Tensor Q, Tensor dq, Tensor stats, float thr_fac, Tensor theta, Tensor(a!) X, Tensor B, Tensor(b!) Bq, int sb, Tensor skip_far, Tensor skip_bq, bool pre=False) -> ()");
-  m.def("sbr16_permute_out(Tensor A, Tensor perm, Tensor B, Tensor(a!) Ap, Tensor(b!) Bp, Tensor skip_a, Tensor skip_b) -> ()");
   m.def("lsmop_g(Tensor X, int[] start, int[] sublen, int[] func, int nk, int cosine) -> Tensor");
   m.def("cma_delta_gemv(Tensor M, Tensor mean, Tensor dm, float cm) -> Tensor[]");
   m.def("cma_center_rows(Tensor pop, Tensor? rows, Tensor mean, Tensor sigma, Tensor w) -> Tensor");
+  m.def("cma_local_select(Tensor order, int mu, Tensor w, int start, int size, Tensor(a!) rows, Tensor(b!) wk) -> ()");
+  m.def("sym_pack(Tensor S, Tensor(a!) P) -> ()");
+  m.def("sym_unpack(Tensor P, Tensor(a!) S) -> ()");
   m.def("cma_paths(Tensor ps, Tensor pc, Tensor y, Tensor delta, Tensor sigma, Tensor count_iter, float[] consts) -> Tensor[]");
   m.def("cma_cov_pad(Tensor C, Tensor S, Tensor pc, Tensor a, float c1, float cmu, Tensor Bprev, int np, Tensor? Cn_out=None, bool want_bp=True) -> Tensor[]");
   m.def("cma_eig_out(Tensor Bp, Tensor w, int d, Tensor? B_out=None) -> Tensor[]");
@@ -1583,6 +1575,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("moead_variation(Tensor pop, Tensor p0, Tensor p1, Tensor kx, Tensor km, Tensor lb, Tensor ub, float pro_c, float dis_c, float pro_m, float dis_m, int nm, int row0=0, int rows=0, Tensor? win=None, Tensor(a!)? out=None) -> Tensor");
   m.def("moead_halo_replace(Tensor(a!) obj, Tensor off_obj, Tensor W, Tensor z, Tensor zmax, Tensor rowptr, Tensor owner, Tensor slots, int func, Tensor(b!) win_h) -> ()");
   m.def("moead_halo_gather(Tensor(a!) pop, Tensor slots, Tensor win_h, Tensor peer, Tensor starts, Tensor(b!)? first=None) -> ()");
+  m.def("peer_release(int device) -> ()");
   m.def("ipc_alloc(int numel, int device) -> Tensor");
   m.def("ipc_handle(Tensor t) -> Tensor");
   m.def("ipc_open(Tensor handle, int device) -> int");
@@ -1612,14 +1605,11 @@ TORCH_LIBRARY_IMPL(evoxmi, CompositeExplicitAutograd, m) {
   m.impl("gemm_ks_set_tile", &gemm_ks_set_tile);
   m.impl("gemm_ks_set_prec", &gemm_ks_set_prec);
   m.impl("gemm_ks_set_nw8", &gemm_ks_set_nw8);
-  m.impl("gemm_sq_enable", &gemm_sq_enable);
   m.impl("gemm_ks_pl", &gemm_ks_pl);
-  m.impl("split_planes", &split_planes);
-  m.impl("philox_normal_planes", &philox_normal_planes);
   m.impl("sbr16_far_bq_out", &sbr16_far_bq_out);
-  m.impl("sbr16_permute_out", &sbr16_permute_out);
   m.impl("gemm_ks_grid", &gemm_ks_grid);
   m.impl("gemm_ks_tile", &gemm_ks_tile);
+  m.impl("peer_release", &peer_release);
   m.impl("ipc_alloc", &ipc_alloc);
   m.impl("ipc_open", &ipc_open);
   m.impl("ipc_close", &ipc_close);
@@ -1663,6 +1653,9 @@ TORCH_LIBRARY_IMPL(evoxmi, CUDA, m) {
   m.impl("lsmop_g", &lsmop_g);
   m.impl("cma_delta_gemv", &cma_delta_gemv);
   m.impl("cma_center_rows", &cma_center_rows);
+  m.impl("cma_local_select", &cma_local_select);
+  m.impl("sym_pack", &sym_pack);
+  m.impl("sym_unpack", &sym_unpack);
   m.impl("cma_paths", &cma_paths);
   m.impl("cma_cov_pad", &cma_cov_pad);
   m.impl("cma_eig_out", &cma_eig_out);

@@ -135,9 +135,7 @@ void evx_gemm_h3(const EvxGemmBlk& a, hipStream_t s);
 // blocked planes of rows [row0, row0 + rows) of normal(key, (·, d)) (d % 4 == 0)
 void evx_philox_blk(const int64_t* key, int64_t rows, int d, int64_t row0, uint16_t* out, hipStream_t s);
 // fragment planes of X (rows × K, K-contiguous, row stride ld), X[r][k]·colscale[k] when colscale
-void evx_split_planes(const float* X, int64_t ld, int64_t rows, int K, const float* colscale, uint16_t* out, int64_t kp, hipStream_t s);
 // fragment planes of rows [row0, row0 + rows) of the virtual normal matrix normal(key, (·, d)) (d % 4 == 0)
-void evx_philox_normal_planes(const int64_t* key, int64_t rows, int d, int64_t row0, uint16_t* out, int64_t kp, hipStream_t s);
 int evx_gemm_ks_tiles_n(int M, int N, int mode);  // column tiles of a launch (row-terms partial count)
 void evx_cec_rowterms_final(const float* parts, int tiles_n, int M, int fid, float* out, hipStream_t s);
 // composition (F9–F12) in two launches: per part i the basic function fid[i] on z = Z[:, zcol[i] : +D]·scale[i]
@@ -155,20 +153,16 @@ struct EvxCecCompose {
 void evx_cec_compose(const float* Z, int64_t ldz, const float* X, int64_t ldx, int N, int D, const EvxCecCompose& c, float* part,
                      float* out, hipStream_t s);  // part: float[N · n · 2] scratch
 int evx_gemm_ks_grid(int M, int N, int mode);  // workgroups of a launch (stat_part length)
-// LDS-staged bf16x6 kernel for square products (gemm_sq.hip), routed to by evx_gemm_ks
-bool evx_gemm_sq_shape(int M, int N, int mode);
-void evx_gemm_sq_enable(int on);
-int evx_gemm_sq_grid(int M, int N, int mode);
-bool evx_gemm_sq_ok(const EvxGemmKs& a);
-void evx_gemm_sq(const EvxGemmKs& a, hipStream_t s);
-bool evx_gemm_ks_routes_sq(const EvxGemmKs& a);
-bool evx_gemm_ks_sq_shape(int M, int N, int mode);  // a bf16x6 product of this shape goes to gemm_sq
 int evx_gemm_ks_tile(int M, int N, int mode);
 void evx_gemm_ks_set_tile(int t);
 // 1: bf16x6 split products on the bf16 matrix pipe (default), 0: f32 MFMA
 void evx_gemm_ks_set_prec(int prec);
 void evx_gemm_ks_set_nw8(int tiles);  // 8-wave workgroups for grids of at most this many tiles
 int evx_gemm_ks_prec();
+void evx_cma_local_select(const int32_t* order, int mu, const float* w, int start, int size, int K, int32_t* rows, float* wk,
+                          hipStream_t s);
+void evx_sym_pack(const float* S, int64_t lds, int d, float* P, hipStream_t s);
+void evx_sym_unpack(const float* P, int d, float* S, int64_t lds, hipStream_t s);
 void evx_cma_center_rows(const float* pop, int64_t ldp, const int32_t* rows, const float* mean, const float* sigma, const float* w, int K,
                          int d, float* Y, hipStream_t s);
 void evx_radix_argsort(const float* keys, int n, int descending, float* out_keys, int32_t* out_idx, hipStream_t s, int batch);
@@ -299,12 +293,11 @@ void evx_sbr_dev_ctrl(const double* part, int nparts, int j, int K, double* hist
 void evx_sbr16_far_bq(const float* A, int n, int64_t lda, const int* perm, const float* Q, const float* dq, const double* stats,
                       float thr_fac, const float* theta_ptr, float* X, int64_t ldx, const float* B, int rows, int64_t ldb, float* Bq,
                       int64_t ldq, int sb, hipStream_t s, const int* skip_far, const int* skip_bq, bool pre = false);
-void evx_sbr16_permute(const float* A, int n, int64_t lda, const int* perm, const float* B, int rows, int64_t ldb, float* Ap, float* Bp,
-                       hipStream_t s, const int* skip_a, const int* skip_b);
 
 // owner-computes MOEA/D (moead.hip)
 void evx_moead_halo_replace(float* obj, const float* off_obj, const float* W, const float* z, const float* zmax, const int32_t* rowptr,
                             const int32_t* owner, const int32_t* slots, int H, int M, int func, int32_t* win_h, hipStream_t s);
+void evx_peer_release(hipStream_t s);
 void evx_moead_halo_gather(float* pop, const int32_t* slots, const int32_t* win_h, int H, const int64_t* peer, const int32_t* starts,
                            int world, int d, hipStream_t s, int32_t* first = nullptr,
                            int N = 0);

@@ -153,7 +153,85 @@ __global__ void __launch_bounds__(256) center_rows_kernel(const float* __restric
   }
 }
 
+// Sharded tell (round 6): this rank's rows among the global top μ, compacted in global-rank
+// order — rows_out[k] = local index, w_out[k] = its recombination weight, for k < count; the
+// slots [count, K) get row 0 with weight 0, so the rank-μ partial sum keeps the static
+// K = min(μ, local rows) a hipGraph needs.  One workgroup: a ballot / popcount scan over
+// order[0, μ) in chunks of 1024.  Replaces a second (local) argsort, an index_copy_ and an
+// index_select of the round-5 sharded tell.
+__global__ void __launch_bounds__(1024) local_select_kernel(const int32_t* __restrict__ order, int mu, const float* __restrict__ w,
+                                                            int start, int size, int K, int32_t* __restrict__ rows_out,
+                                                            float* __restrict__ w_out) {
+  __shared__ int wave_tot[16];
+  __shared__ int base_s;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid == 0) base_s = 0;
+  __syncthreads();
+  for (int c0 = 0; c0 < mu; c0 += 1024) {
+    const int i = c0 + tid;
+    int g = -1;
+    if (i < mu) g = order[i] - start;
+    const bool p = g >= 0 && g < size;
+    const unsigned long long b = __ballot(p);
+    const int pre = __popcll(b & ((1ull << lane) - 1ull));
+    if (lane == 0) wave_tot[wv] = __popcll(b);
+    __syncthreads();
+    int off = base_s;
+    for (int k = 0; k < wv; ++k) off += wave_tot[k];
+    if (p && off + pre < K) {
+      rows_out[off + pre] = g;
+      w_out[off + pre] = w[i];
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int t = 0;
+      for (int k = 0; k < 16; ++k) t += wave_tot[k];
+      base_s += t;
+    }
+    __syncthreads();
+  }
+  for (int k = base_s + tid; k < K; k += 1024) {
+    rows_out[k] = 0;
+    w_out[k] = 0.f;
+  }
+}
+
+// Symmetric d × d ↔ packed upper triangle (row i holds columns i..d−1 at i·d − i(i−1)/2): the
+// sharded tell all-reduces the rank-μ partial sums in this form — d(d+1)/2 + d floats, half the
+// bytes of the full matrix on the wire.  One workgroup per row.
+__device__ __forceinline__ int64_t packed_off(int64_t i, int64_t d) { return i * d - i * (i - 1) / 2; }
+
+__global__ void __launch_bounds__(256) sym_pack_kernel(const float* __restrict__ S, int64_t lds, int d, float* __restrict__ P) {
+  const int i = blockIdx.x;
+  const float* row = S + (int64_t)i * lds;
+  float* o = P + packed_off(i, d) - i;
+  for (int j = i + threadIdx.x; j < d; j += blockDim.x) o[j] = row[j];
+}
+
+__global__ void __launch_bounds__(256) sym_unpack_kernel(const float* __restrict__ P, int d, float* __restrict__ S, int64_t lds) {
+  const int i = blockIdx.x;
+  const float* o = P + packed_off(i, d) - i;
+  for (int j = i + threadIdx.x; j < d; j += blockDim.x) {
+    const float v = o[j];
+    S[(int64_t)i * lds + j] = v;
+    S[(int64_t)j * lds + i] = v;
+  }
+}
+
 }  // namespace
+
+void evx_cma_local_select(const int32_t* order, int mu, const float* w, int start, int size, int K, int32_t* rows, float* wk,
+                          hipStream_t s) {
+  local_select_kernel<<<1, 1024, 0, s>>>(order, mu, w, start, size, K, rows, wk);
+}
+
+void evx_sym_pack(const float* S, int64_t lds, int d, float* P, hipStream_t s) {
+  if (d > 0) sym_pack_kernel<<<d, 256, 0, s>>>(S, lds, d, P);
+}
+
+void evx_sym_unpack(const float* P, int d, float* S, int64_t lds, hipStream_t s) {
+  if (d > 0) sym_unpack_kernel<<<d, 256, 0, s>>>(P, d, S, lds);
+}
 
 void evx_cma_delta_gemv(const float* M, const float* mean, const float* dm, float cm, int d, float* mean_out, float* delta, float* y,
                         hipStream_t s) {

@@ -115,20 +115,15 @@ __device__ __forceinline__ float3 rot16(float app, float aqq, float apq) {
 // transposes: S stays symmetric; pair u's own block set exactly), and every lane rotates a
 // 2×2 block of Q' = Q J (rows 2(L/8)+{0,1}, column pair L mod 8).  All updates are in place:
 // the 2×2 blocks of one round partition S and Q.
-// FR (fused rank, n ≤ kFuseMax, opt-in EVOXMI_SBR_FUSED_RANK=1): every workgroup ranks the
-// (diagonal key, index) pairs itself by counting over the keys in LDS — the strict total order
-// of sbr16_rank_kernel — takes its members from the shifted order and writes its segment of perm
-// for the far / Bq kernels: one launch per refinement slot fewer, but each of the 32 workgroups
-// then counts all n² pairs with 8 waves (the rank kernel spreads them over 16 workgroups of 16
-// waves): the flagship measured 1.867 vs 1.689 ms (round 5); round 4's bitonic form was slower
-// still (42 µs per executed solve instead of 27 + 8, profiles/r4_kstats_fused_rank.txt).
-constexpr int kFuseMax = 2048;
+// (A fused-rank variant — every workgroup ranking the keys itself, one launch per slot fewer —
+// measured slower: 1.867 vs 1.689 ms per flagship generation in round 5, 42 vs 27 + 8 µs per
+// executed solve in round 4; removed in round 6, profiles/NOTES.md.)
 
 // Threads: 2·SB²/4 — the first SB²/4 (waves 0-3 for SB = 32) rotate Q, the others (the
 // SB/2·(SB/2+1)/2 items {u ≤ v}) update S, so the two updates of a round run side by side on
 // different SIMDs instead of one after the other in every lane; the round-robin pairs come from
 // a table built once in LDS (the index arithmetic was a third of the round's instructions).
-template <int SB, bool FR>
+template <int SB>
 __global__ void __launch_bounds__(SB * SB / 2) sbr16_block_kernel(const float* __restrict__ A, int n, int64_t lda,
                                                                  int* __restrict__ perm, int sweeps, float* __restrict__ Q_out,
                                                                  float* __restrict__ dq_out, const int* __restrict__ skip, int shift,
@@ -143,36 +138,7 @@ __global__ void __launch_bounds__(SB * SB / 2) sbr16_block_kernel(const float* _
   const int tid = threadIdx.x, nthr = blockDim.x;
   const int s0 = blockIdx.x * SB, m = min(SB, n - s0);
   for (int e = tid; e < (SB - 1) * NH; e += nthr) ptab[e] = rr16<SB>(e / NH, e % NH);
-  if constexpr (FR) {
-    // every workgroup ranks ALL the diagonal keys by counting (the strict total order of
-    // sbr16_rank_kernel: NaN keys as +inf, ties by index) and takes the indices whose shifted
-    // position falls in its block — one launch per slot fewer than rank + block
-    __shared__ __attribute__((aligned(16))) float skey[kFuseMax];
-    const int np = (n + 3) & ~3;  // padded with +inf: never below a real key
-    for (int i = tid; i < np; i += nthr) skey[i] = i < n ? sort_key(A[(int64_t)i * lda + i]) : INFINITY;
-    if (tid < SB) members[tid] = -1;
-    __syncthreads();
-    for (int i = tid; i < n; i += nthr) {
-      const float ki = skey[i];
-      int cnt = 0;
-#pragma unroll 4
-      for (int j = 0; j < np; j += 4) {
-        const float4 k4 = *reinterpret_cast<const float4*>(skey + j);  // same address across the wave: broadcast
-        cnt += (k4.x < ki) | ((k4.x == ki) & (j < i));
-        cnt += (k4.y < ki) | ((k4.y == ki) & (j + 1 < i));
-        cnt += (k4.z < ki) | ((k4.z == ki) & (j + 2 < i));
-        cnt += (k4.w < ki) | ((k4.w == ki) & (j + 3 < i));
-      }
-      int pos = cnt - shift;
-      if (pos < 0) pos += n;
-      if (pos >= s0 && pos < s0 + m) {
-        members[pos - s0] = i;
-        perm[pos] = i;
-      }
-    }
-  } else {
-    if (tid < SB) members[tid] = tid < m ? perm[s0 + tid] : -1;
-  }
+  if (tid < SB) members[tid] = tid < m ? perm[s0 + tid] : -1;
   __syncthreads();
   for (int e = tid; e < SB * SB; e += nthr) {
     const int a = e / SB, c = e % SB;
@@ -495,30 +461,9 @@ __global__ void __launch_bounds__(256) sbr16_bq_kernel(const float* __restrict__
 // far generator and Bq in ONE launch (device schedule): both read only the block solve's
 // perm / Q, so the (nt × nt) far tiles and the (row tiles × nt) Bq tiles run side by side —
 // one launch boundary fewer per refinement iteration, and the Bq tiles fill the CUs the far
-// tiles leave idle.  skip_far / skip_bq: the two parts' own control words.
-// Ap = A[perm, perm] and Bp = B[:, perm] (the shifted sorted order of this iteration), one row
-// per workgroup: the source row is read once, coalesced, into LDS and gathered from there, so the
-// generator / Bq tiles read contiguous 64×64 tiles instead of 64 scattered columns per row (each
-// touching ≈28 of a 4 KB row's 32 cache lines: ≈14× the useful bytes).
-__global__ void __launch_bounds__(256) sbr16_permute_kernel(const float* __restrict__ A, int n, int64_t lda, const int* __restrict__ perm,
-                                                            const float* __restrict__ B, int rows, int64_t ldb, float* __restrict__ Ap,
-                                                            float* __restrict__ Bp, const int* __restrict__ skip_a,
-                                                            const int* __restrict__ skip_b) {
-  __shared__ __attribute__((aligned(16))) float row[kRankMax];
-  const int i = blockIdx.x;
-  const bool isA = i < n;
-  if (isA ? (skip_a && *skip_a) : (skip_b && *skip_b)) return;
-  const float* src = isA ? A + (int64_t)perm[i] * lda : B + (int64_t)(i - n) * ldb;
-  float* dst = isA ? Ap + (int64_t)i * n : Bp + (int64_t)(i - n) * n;
-  if ((n & 3) == 0 && ((isA ? lda : ldb) & 3) == 0) {
-    for (int c = threadIdx.x; c < (n >> 2); c += blockDim.x) reinterpret_cast<float4*>(row)[c] = reinterpret_cast<const float4*>(src)[c];
-  } else {
-    for (int c = threadIdx.x; c < n; c += blockDim.x) row[c] = src[c];
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < n; c += blockDim.x) dst[c] = row[perm[c]];
-}
-
+// tiles leave idle.  skip_far / skip_bq: the two parts' own control words.  (A row-wise
+// pre-permutation of A and B before the tiles measured no faster — far+Bq 30.0 vs 28 µs plus 6 µs
+// for the gather — and was removed in round 6; the `pre` path reads already-permuted operands.)
 template <int SB>
 __global__ void __launch_bounds__(256) sbr16_far_bq_kernel(const float* __restrict__ A, int n, int64_t lda, const int* __restrict__ perm,
                                                            const float* __restrict__ Q, const float* __restrict__ dq,
@@ -611,22 +556,11 @@ int evx_sbr16_max_n() { return kRankMax; }
 
 void evx_sbr16_block(const float* A, int n, int64_t lda, int shift, int sweeps, int* perm, float* Q, float* dq, int sb, hipStream_t s,
                      const int* skip, float skip_tol) {
-  static const bool fuse = [] {  // EVOXMI_SBR_FUSED_RANK=1: the rank inside the block kernel (see sbr16_block_kernel)
-    const char* e = getenv("EVOXMI_SBR_FUSED_RANK");
-    return e && atoi(e) != 0;
-  }();
-  if (fuse && n <= kFuseMax) {
-    if (sb == 32)
-      sbr16_block_kernel<32, true><<<(n + 31) / 32, 512, 0, s>>>(A, n, lda, perm, sweeps, Q, dq, skip, shift, skip_tol);
-    else
-      sbr16_block_kernel<16, true><<<(n + 15) / 16, 128, 0, s>>>(A, n, lda, perm, sweeps, Q, dq, skip, shift, skip_tol);
-    return;
-  }
   sbr16_rank_kernel<<<(n + 63) / 64, 64 * kRankWaves, 0, s>>>(A, n, lda, shift, perm, skip);
   if (sb == 32)
-    sbr16_block_kernel<32, false><<<(n + 31) / 32, 512, 0, s>>>(A, n, lda, perm, sweeps, Q, dq, skip, shift, skip_tol);
+    sbr16_block_kernel<32><<<(n + 31) / 32, 512, 0, s>>>(A, n, lda, perm, sweeps, Q, dq, skip, shift, skip_tol);
   else
-    sbr16_block_kernel<16, false><<<(n + 15) / 16, 128, 0, s>>>(A, n, lda, perm, sweeps, Q, dq, skip, shift, skip_tol);
+    sbr16_block_kernel<16><<<(n + 15) / 16, 128, 0, s>>>(A, n, lda, perm, sweeps, Q, dq, skip, shift, skip_tol);
 }
 
 void evx_sbr16_far(const float* A, int n, int64_t lda, const int* perm, const float* Q, const float* dq, const double* stats,
@@ -648,10 +582,6 @@ void evx_sbr16_bq(const float* B, int rows, int n, int64_t ldb, const int* perm,
     sbr16_bq_kernel<16><<<dim3(nt, (rows + BQR - 1) / BQR), 256, 0, s>>>(B, rows, n, ldb, perm, Q, Bq, ldq, skip);
 }
 
-void evx_sbr16_permute(const float* A, int n, int64_t lda, const int* perm, const float* B, int rows, int64_t ldb, float* Ap, float* Bp,
-                       hipStream_t s, const int* skip_a, const int* skip_b) {
-  sbr16_permute_kernel<<<n + rows, 256, 0, s>>>(A, n, lda, perm, B, rows, ldb, Ap, Bp, skip_a, skip_b);
-}
 
 void evx_sbr16_far_bq(const float* A, int n, int64_t lda, const int* perm, const float* Q, const float* dq, const double* stats,
                       float thr_fac, const float* theta_ptr, float* X, int64_t ldx, const float* B, int rows, int64_t ldb, float* Bq,

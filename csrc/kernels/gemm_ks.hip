@@ -252,6 +252,8 @@ __device__ __forceinline__ void decode_tile(int bid, int tiles_m, int tiles_n, i
 // NW: waves per workgroup, each owning 1/NW of K.  8 for grids that cannot fill the chip twice
 // (the 1000³ eigensolver products: 256 tiles for 256 CUs): two waves per SIMD, so one wave's loads
 // are in flight while the other computes; the first 4 waves then run the 4-wave epilogue.
+// PL (operands as pre-split bf16x6 fragment planes) is no longer launched: the round-4 opt-in
+// measured no gain inside the generation (profiles/NOTES.md); the template keeps PL = 0.
 template <int TM, int TN, int KH, bool AKC, bool BKC, int MODE, int PREC, int PL = 0, int NW = 4>
 __global__ void __launch_bounds__(64 * NW) gemm_ks_kernel(EvxGemmKs p) {
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
@@ -763,13 +765,6 @@ void launch_prec(const EvxGemmKs& a, int tiles, hipStream_t s) {
 template <int TM, int TN, int MODE>
 void launch_layout(const EvxGemmKs& a, int tiles, hipStream_t s) {
   {
-    if (a.a_pl || a.b_pl) {  // fragment planes: bf16x6 on 16x16x32, K-contiguous operands
-      const dim3 grid(tiles), block(256);
-      if (a.a_pl && a.b_pl) gemm_ks_kernel<TM, TN, 2, true, true, MODE, 1, 3><<<grid, block, 0, s>>>(a);
-      else if (a.a_pl) gemm_ks_kernel<TM, TN, 2, true, true, MODE, 1, 1><<<grid, block, 0, s>>>(a);
-      else gemm_ks_kernel<TM, TN, 2, true, true, MODE, 1, 2><<<grid, block, 0, s>>>(a);
-      return;
-    }
     if (a.prec == 3) return launch_prec<TM, TN, MODE, 3>(a, tiles, s);
     if constexpr (TM % 2 == 0 && TN % 2 == 0) {
       if (g_ks_prec == 2) return launch_prec<TM, TN, MODE, 2>(a, tiles, s);
@@ -788,67 +783,6 @@ void launch_tile(EvxGemmKs a, hipStream_t s) {
   else launch_layout<TM, TN, 2>(a, a.tiles_m * (a.tiles_m + 1) / 2, s);
 }
 
-// fragment planes (see EvxGemmKs::a_pl): thread (row, group, q) splits the 8 values
-// k = 32·group + 16h + 4q + c (h = 0, 1; c = 0..3) and stores each part's 16 bytes
-__global__ void __launch_bounds__(256) split_planes_kernel(const float* __restrict__ X, int64_t ld, int64_t rows, int K,
-                                                           const float* __restrict__ colscale, uint16_t* __restrict__ out, int64_t kp) {
-  const int64_t ng = kp / 32, total = rows * ng * 4, plane = rows * kp;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    const int q = (int)(t & 3);
-    const int64_t rg = t >> 2, r = rg / ng, g = rg - r * ng;
-    float v[8];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int k = (int)(32 * g) + 16 * h + 4 * q;
-      const float* x = X + r * ld + k;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const bool in = k + c < K;
-        float a = in ? x[c] : 0.f;
-        if (colscale && in) a *= colscale[k + c];
-        v[4 * h + c] = a;
-      }
-    }
-    bf16x8 hh, mm, ll;
-    split3(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), hh, mm, ll);
-    uint16_t* o = out + r * kp + 32 * g + 8 * q;
-    *reinterpret_cast<uint4*>(o) = __builtin_bit_cast(uint4, hh);
-    *reinterpret_cast<uint4*>(o + plane) = __builtin_bit_cast(uint4, mm);
-    *reinterpret_cast<uint4*>(o + 2 * plane) = __builtin_bit_cast(uint4, ll);
-  }
-}
-
-// the same planes of rows [row0, row0 + rows) of normal(key, (·, d)) (rng.hip's philox_fill
-// arithmetic: element e of the virtual matrix is word (e mod 4) of Philox block e / 4, Box–Muller
-// on word pairs), generated in place: the f32 noise matrix is never written
-__global__ void __launch_bounds__(256) philox_normal_planes_kernel(const int64_t* __restrict__ key, int64_t rows, int d, int64_t row0,
-                                                                   uint16_t* __restrict__ out, int64_t kp) {
-  uint32_t k0, k1;
-  evx::load_key(key, k0, k1);
-  const int64_t ng = kp / 32, total = rows * ng * 4, plane = rows * kp;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    const int q = (int)(t & 3);
-    const int64_t rg = t >> 2, r = rg / ng, g = rg - r * ng;
-    float4 v[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int k = (int)(32 * g) + 16 * h + 4 * q;
-      if (k < d) {  // d % 4 == 0: the four values are one Philox block
-        const int64_t e = (row0 + r) * (int64_t)d + k;
-        v[h] = evx::normal4(evx::philox_block((uint64_t)(e >> 2), k0, k1));
-      } else {
-        v[h] = make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-    }
-    bf16x8 hh, mm, ll;
-    split3(v[0], v[1], hh, mm, ll);
-    uint16_t* o = out + r * kp + 32 * g + 8 * q;
-    *reinterpret_cast<uint4*>(o) = __builtin_bit_cast(uint4, hh);
-    *reinterpret_cast<uint4*>(o + plane) = __builtin_bit_cast(uint4, mm);
-    *reinterpret_cast<uint4*>(o + 2 * plane) = __builtin_bit_cast(uint4, ll);
-  }
-}
-
 int g_ks_tile_override = 0;
 
 }  // namespace
@@ -859,43 +793,16 @@ void evx_gemm_ks_set_prec(int prec) { g_ks_prec = prec; }
 
 void evx_gemm_ks_set_nw8(int tiles) { g_ks_nw8_tiles = tiles; }
 
-void evx_split_planes(const float* X, int64_t ld, int64_t rows, int K, const float* colscale, uint16_t* out, int64_t kp, hipStream_t s) {
-  const int64_t total = rows * (kp / 32) * 4;
-  int g = (int)((total + 255) / 256);
-  if (g > 4096) g = 4096;
-  if (g > 0) split_planes_kernel<<<g, 256, 0, s>>>(X, ld, rows, K, colscale, out, kp);
-}
-
-void evx_philox_normal_planes(const int64_t* key, int64_t rows, int d, int64_t row0, uint16_t* out, int64_t kp, hipStream_t s) {
-  const int64_t total = rows * (kp / 32) * 4;
-  int g = (int)((total + 255) / 256);
-  if (g > 8192) g = 8192;
-  if (g > 0) philox_normal_planes_kernel<<<g, 256, 0, s>>>(key, rows, d, row0, out, kp);
-}
-
 int evx_gemm_ks_prec() { return g_ks_prec; }
 
 int evx_gemm_ks_tile(int M, int N, int mode) { return evx_host::gemm_ks_tile(M, N, mode, g_ks_tile_override); }
 
-// square bf16x6 products go to the LDS-staged kernel (gemm_sq.hip) unless a tile or the
-// precision is forced (probes): its grid then sizes the stats partials
-bool evx_gemm_ks_sq_shape(int M, int N, int mode) { return g_ks_prec == 1 && g_ks_tile_override == 0 && evx_gemm_sq_shape(M, N, mode); }
-
-int evx_gemm_ks_grid(int M, int N, int mode) {
-  if (evx_gemm_ks_sq_shape(M, N, mode)) return evx_gemm_sq_grid(M, N, mode);
-  return (int)evx_host::gemm_ks_grid(M, N, mode, g_ks_tile_override);
-}
-
-bool evx_gemm_ks_routes_sq(const EvxGemmKs& a) { return !a.force_tile && a.prec != 3 && a.diag_add == 0.f && evx_gemm_ks_sq_shape(a.M, a.N, a.mode) && evx_gemm_sq_ok(a); }
+int evx_gemm_ks_grid(int M, int N, int mode) { return (int)evx_host::gemm_ks_grid(M, N, mode, g_ks_tile_override); }
 
 int evx_gemm_ks_tiles_n(int M, int N, int mode) { return (int)evx_host::gemm_ks_tiles_n(M, N, mode, g_ks_tile_override); }
 
 void evx_gemm_ks(const EvxGemmKs& a, hipStream_t s) {
   if (a.M <= 0 || a.N <= 0) return;
-  if (evx_gemm_ks_routes_sq(a)) {
-    evx_gemm_sq(a, s);
-    return;
-  }
   switch (a.force_tile ? a.force_tile : evx_gemm_ks_tile(a.M, a.N, a.mode)) {
     case 2: launch_tile<2, 2>(a, s); break;
     case 3: launch_tile<3, 3>(a, s); break;

@@ -375,6 +375,8 @@ __global__ void __launch_bounds__(256) halo_first_kernel(const int32_t* __restri
 // (deduplicated form) only the first halo slot taking an offspring reads it — an offspring that
 // wins several of this rank's halo slots crosses xGMI once — and dup_copy_kernel then fills the
 // other slots from that local row.
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
 __global__ void __launch_bounds__(256) halo_gather_kernel(float* __restrict__ pop, const int32_t* __restrict__ slots,
                                                           const int32_t* __restrict__ win_h, const int64_t* __restrict__ peer,
                                                           const int32_t* __restrict__ starts, int world, int d,
@@ -387,12 +389,18 @@ __global__ void __launch_bounds__(256) halo_gather_kernel(float* __restrict__ po
   while (q + 1 < world && starts[q + 1] <= w) ++q;
   const float* src = reinterpret_cast<const float*>(peer[q]) + (int64_t)(w - starts[q]) * d;
   float* dst = pop + (int64_t)slots[h] * d;
+  // peer-buffer contract (parallel/peer.py): system-scope ACQUIRE before the first peer load —
+  // lines of a peer buffer this GPU's L2 still holds from the previous generation's reads are
+  // invalidated, so the loads see what the owner released (peer_release) before the collective
+  // that ordered this kernel after it
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   if ((d & 3) == 0) {
     const int n4 = d >> 2;
+    // peer rows are read once: non-temporal, so they do not displace this rank's own data in L2
     for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < n4; c += gridDim.x * blockDim.x)
-      reinterpret_cast<float4*>(dst)[c] = reinterpret_cast<const float4*>(src)[c];
+      reinterpret_cast<f32x4v*>(dst)[c] = __builtin_nontemporal_load(reinterpret_cast<const f32x4v*>(src) + c);
   } else {
-    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < d; c += gridDim.x * blockDim.x) dst[c] = src[c];
+    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < d; c += gridDim.x * blockDim.x) dst[c] = __builtin_nontemporal_load(src + c);
   }
 }
 
@@ -468,6 +476,16 @@ void evx_moead_halo_replace(float* obj, const float* off_obj, const float* W, co
   else if (M == 2) halo_replace_kernel<2><<<g, 256, 0, s>>>(obj, off_obj, W, z, zmax, rowptr, owner, slots, H, M, func, win_h);
   else halo_replace_kernel<0><<<g, 256, 0, s>>>(obj, off_obj, W, z, zmax, rowptr, owner, slots, H, M, func, win_h);
 }
+
+// peer-buffer contract, writer side: one system-scope RELEASE after the kernels that wrote this
+// rank's peer-visible buffer (stream-ordered before the collective that publishes it): dirty L2
+// lines are written back to HBM, where peers' xGMI reads land (the memory-side caches are
+// coherent for them, the writer's L2 is not).  A single thread: the fence acts on the whole L2.
+__global__ void peer_release_kernel() {
+  if (threadIdx.x == 0 && blockIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+}
+
+void evx_peer_release(hipStream_t s) { peer_release_kernel<<<1, 64, 0, s>>>(); }
 
 void evx_moead_halo_gather(float* pop, const int32_t* slots, const int32_t* win_h, int H, const int64_t* peer, const int32_t* starts,
                            int world, int d, hipStream_t s, int32_t* first, int N) {

@@ -314,6 +314,7 @@ class MOEAD(Algorithm):
                                              self.lb, self.ub, c.pro_c, c.dis_c, m.pro_m, m.dis_m, row0=start, rows=size, out=buf)
             else:
                 off = buf.copy_(self._offspring_rows(state, parents, sel_key, mut_key, row0=start, rows=size))
+            ow["peer"].release()  # the peers read these rows after the next collective (peer.py contract)
         else:
             off = self._offspring_rows(state, parents, sel_key, mut_key, row0=start, rows=size)
         return off, state.update(next_generation=off, key=key, parents=parents, var_keys=torch.stack([sel_key, mut_key]))

@@ -170,8 +170,7 @@ class CMAES(Algorithm):
     def _level_slots(self, level: int) -> int:
         from ....ops.sbr_device import schedule_iters
 
-        variant_iters = {0: config.get("sbr_late_iters"), 1: config.get("sbr_device_iters"), 2: config.get("sbr_cold_iters")}[level]
-        return schedule_iters(self.dim, int(variant_iters))
+        return schedule_iters(self.dim, ("late", "warm", "cold")[level])
 
     def graph_variant(self, generation: int):
         """The eigensolver schedule of the next step (see the class comment above): one of
@@ -270,37 +269,18 @@ class CMAES(Algorithm):
         return "".join("LWC"[v] for v in lv)
 
     def graph_variant_context(self, variant):
-        if variant == "cold":
-            return config.override(sbr_device_iters=int(config.get("sbr_cold_iters")))
-        if variant == "late":
-            # settled generations: damping / Newton–Schulz / order-6 kernels only in the first
-            # sbr_late_full_slots slots (their κ falls below the order-4 threshold by slot 2), the
-            # damping power steps only in the first sbr_late_damp_slots
-            return config.override(sbr_device_iters=int(config.get("sbr_late_iters")),
-                                   sbr_full_slots=int(config.get("sbr_late_full_slots")),
-                                   sbr_damp_slots=int(config.get("sbr_late_damp_slots")),
-                                   sbr_ns_iters=int(config.get("sbr_late_ns_iters")))
+        """The eigensolver schedule of a graph variant (ops/sbr_device.py: ``schedule``): "cold"
+        — every slot full, bounds-gated damping; None — the warm schedule (lean tail slots);
+        "late" — settled solves: damping / Newton–Schulz / order-6 kernels in the first slots only."""
+        if variant in ("cold", "late"):
+            from ....ops.sbr_device import use_schedule
+
+            return use_schedule(variant)
         return super().graph_variant_context(variant)
 
     # ------------------------------------------------------------------ sampling
     def _sample(self, state, key, row0: int, rows: int):
         d = self.dim
-        if (state.B.is_cuda and config.get("gemm_planes") and config.get("gemm_prec") == "x6" and config.get("plain_gemm") == "evoxmi"
-                and d % 4 == 0):
-            # opt-in (gemm_planes ≥ 1): B·diag(D) pre-split into its bf16x6 fragment planes once per
-            # generation (one pass, D as the column scale), so the sampling GEMM splits only the noise
-            # on the fly — 162.6 vs 174.3 µs alone, but no gain inside the generation (175.8 vs
-            # 172.6 µs, profiles/r4_gemm_planes.log); gemm_planes = 2 also generates the noise straight
-            # into planes (the A side of the load-bound loop grows 1.5×: 205 µs)
-            from ....ops.linalg import mm_nt, normal_planes, split_planes
-
-            za = normal_planes(key.to(state.B.device), rows, d, row0) if config.get("gemm_planes") >= 2 else \
-                rnd.normal(key, (rows, d), offset=row0 * d)
-            bdp = split_planes(state.B, colscale=state.D)
-            buf = state.population
-            out = buf if (rows == self.pop_size and torch.cuda.is_current_stream_capturing() and buf.is_contiguous()
-                          and buf.shape == (rows, d)) else None
-            return mm_nt(za, bdp, alpha_ptr=state.sigma.reshape(1), bias_n=state.mean, out=out)
         if (state.B.is_cuda and d % 4 == 0 and config.get("gemm_prec") == "x6"
                 and linalg.tall_nt_ok(rows, d, d, state.B.device)):
             # tall sampling product on the f16x3 LDS-staged GEMM: the Philox noise is generated
@@ -486,39 +466,55 @@ class CMAES(Algorithm):
         return local, state.update(population=local, count_iter=state.count_iter + 1, key=key)
 
     def tell_sharded(self, state, fitness, dist):
-        """``fitness`` is the all-gathered (λ,) vector; ``state.population`` the local rows."""
+        """``fitness`` is the all-gathered (λ,) vector; ``state.population`` the local rows.
+
+        One global argsort; this rank's rows among the top μ are compacted in global-rank order
+        by one kernel (``cma_local_select``: at most K = min(μ, λ/N) of them — the same K = μ
+        GEMM as the unsharded tell on one rank, static for hipGraphs, padded with zero weights);
+        the rank-μ partial sum S (symmetric) goes on the wire as its packed upper triangle with
+        the weighted mean shift appended: d(d+1)/2 + d floats, half the bytes of round 5's
+        (d² + d) all-reduce.  Reference: ``cma_es.py:163-198`` (tell), whose ``Σ wᵢ yᵢ yᵢᵀ`` is
+        this sum over ranks."""
         start, size = dist.slice_of(self.pop_size)
+        d = self.dim
+        K = min(self.mu, size)
+        dev = fitness.device
         if fitness.is_cuda:
+            from ....ops import _ext
+
+            ops = _ext.ops()
             _, order = argsort_i32(fitness.contiguous())
-            order = order.long()
+            lsel = torch.empty(K, dtype=torch.int32, device=dev)
+            wsel = torch.empty(K, dtype=torch.float32, device=dev)
+            ops.cma_local_select(order, self.mu, self.weights, start, size, lsel, wsel)
         else:
             _, order = argsort(fitness)
-        # weight of every global row (0 outside the top μ).  A rank holds at most
-        # K = min(μ, λ/N) selected rows — its K best local rows — so the rank-μ partial sum
-        # gathers exactly those K rows (weight 0 for any that missed the global top μ):
-        # the same K = μ GEMM as the unsharded tell on one rank, fixed shapes for hipGraphs
-        wfull = torch.zeros(self.pop_size, dtype=torch.float32, device=fitness.device)
-        wfull.index_copy_(0, order[: self.mu], self.weights.to(fitness.device))
-        K = min(self.mu, size)
-        floc = fitness[start : start + size].contiguous()
-        if floc.is_cuda:
-            _, lorder = argsort_i32(floc)
+            top = order[: self.mu]
+            mine = (top >= start) & (top < start + size)
+            lsel = torch.zeros(K, dtype=torch.int64)
+            wsel = torch.zeros(K, dtype=torch.float32)
+            n = int(mine.sum())
+            lsel[:n] = top[mine] - start
+            wsel[:n] = self.weights.cpu()[mine]
+            lsel, wsel = lsel.to(dev), wsel.to(dev)
+        dm, S = self._weighted_stats(state, state.population, lsel, K, wsel, gather=True)
+        P = d * (d + 1) // 2
+        buf = torch.empty(P + d, dtype=torch.float32, device=dev)
+        if S.is_cuda:
+            ops.sym_pack(S, buf[:P])
         else:
-            _, lorder = argsort(floc)
-        lsel = lorder[:K].contiguous()
-        wsel = wfull[start : start + size].index_select(0, lsel.long()).contiguous()
-        d = self.dim
-        # one (d² + d) buffer for the all-reduce: S (first, so its rows stay 16-byte aligned) is
-        # written into it by the GEMM, no 4 MB concatenation
-        buf = torch.empty(d * d + d, dtype=torch.float32, device=fitness.device)
-        Sv = buf[: d * d].view(d, d)
-        dm, S = self._weighted_stats(state, state.population, lsel, K, wsel, gather=True, s_out=Sv)
-        buf[d * d :].copy_(dm.reshape(-1))
-        if S.data_ptr() != Sv.data_ptr():
-            Sv.copy_(S)
+            iu = torch.triu_indices(d, d)
+            buf[:P] = S[iu[0], iu[1]]
+        buf[P:].copy_(dm.reshape(-1))
         with profiling.phase("all_reduce"):
             dist.all_reduce_(buf)
-        return self._finish_tell(state, buf[d * d :], Sv)
+        if S.is_cuda:
+            ops.sym_unpack(buf[:P], S)
+        else:
+            S = torch.zeros(d, d, dtype=torch.float32)
+            S[iu[0], iu[1]] = buf[:P]
+            S = S + torch.triu(S, 1).T
+        return self._finish_tell(state, buf[P:], S)
 
 
 class SepCMAES(ColumnSeparable, CMAES):

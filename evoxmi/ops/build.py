@@ -81,8 +81,7 @@ def _run(cmd):
 # beside MFMAs costs ≈13 cycles more than two v_sub_f32)
 FILE_FLAGS = {"eigh_sbr.hip": ["-fno-slp-vectorize"], "mo_geom.hip": ["-ffp-contract=fast-honor-pragmas"],
               "rng.hip": ["-ffp-contract=fast-honor-pragmas"],
-              "neuro.hip": ["-fno-slp-vectorize"], "gemm_ks.hip": ["-fno-slp-vectorize"],
-              "gemm_sq.hip": ["-fno-slp-vectorize"]}
+              "neuro.hip": ["-fno-slp-vectorize"], "gemm_ks.hip": ["-fno-slp-vectorize"]}
 
 
 def build(verbose: bool = True, jobs: int = None) -> str:

@@ -18,6 +18,14 @@ from .linalg import matmul, matmul_tn
 from .. import config
 
 COLD_SWEEPS = 12
+# (round 6: fixed here instead of EVOXMI_JACOBI_* knobs)
+TOL_FACTOR = 4.0      # convergence: ‖offdiag‖ ≤ factor·eps_f32·sqrt(n)·‖diag‖
+INNER_TOL = 1e-6      # per-subproblem skip threshold of the solve kernel
+INNER = 1             # inner sweeps per 32×32 subproblem (2 / 3 do not speed the outer convergence)
+REORTHO = True        # Newton–Schulz re-orthonormalisation of the warm-start basis
+# round pipeline: 2 = B update of round t−1 inside round t's solve launch (default); 0 = split
+# solve / apply launches; 1 = fused apply + next solve (bit-identical, 27 vs 17.4 µs per round)
+FUSED = 2
 # convergence is judged against the f32 floor of ‖offdiag‖/‖diag‖ ≈ eps·sqrt(n)
 # (sweeps / tolerance / inner sweeps are evoxmi.config knobs: EVOXMI_JACOBI_*)
 
@@ -100,7 +108,8 @@ def _btcb(C: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
     return matmul_tn(B, matmul(C, B)).contiguous()
 
 
-def warm_eigh(C: torch.Tensor, B_prev: torch.Tensor = None, max_sweeps: int = None, tol: float = None, return_stats: bool = False):
+def warm_eigh(C: torch.Tensor, B_prev: torch.Tensor = None, max_sweeps: int = None, tol: float = None, return_stats: bool = False,
+              fused: int = None):
     n = C.shape[0]
     np_ = padded_size(n)
     dev = C.device
@@ -114,28 +123,28 @@ def warm_eigh(C: torch.Tensor, B_prev: torch.Tensor = None, max_sweeps: int = No
         A = Cp
         sweeps = COLD_SWEEPS if max_sweeps is None else max_sweeps
     else:
-        Bp[:n, :n] = reorthonormalize(B_prev) if config.get("jacobi_reortho") else B_prev
+        Bp[:n, :n] = reorthonormalize(B_prev) if REORTHO else B_prev
         Bp[n:, n:] = eye_pad
         if config.get("plain_gemm") == "blas":
             A = (Bp.t() @ (Cp @ Bp)).contiguous()
         else:
             A = _btcb(Cp, Bp)
         sweeps = config.get("jacobi_sweeps") if max_sweeps is None else max_sweeps
-    tol = tol or config.get("jacobi_tol_factor") * 1.1920929e-07 * max(n, 16) ** 0.5
+    tol = tol or TOL_FACTOR * 1.1920929e-07 * max(n, 16) ** 0.5
     w, stats = _ext.ops().jacobi_sweeps(A, Bp, schedule(np_ // 16, dev), int(sweeps), float(tol),
-                                        float(config.get("jacobi_inner_tol")), int(config.get("jacobi_inner")), int(config.get("jacobi_fused")))
+                                        float(INNER_TOL), int(INNER), int(FUSED if fused is None else fused))
     out = (w[:n].contiguous(), Bp[:n, :n].contiguous())
     return (*out, stats) if return_stats else out
 
 
-def warm_eigh_padded(Cp: torch.Tensor, Bp: torch.Tensor, n: int, max_sweeps: int = None, tol: float = None):
+def warm_eigh_padded(Cp: torch.Tensor, Bp: torch.Tensor, n: int, max_sweeps: int = None, tol: float = None, fused: int = None):
     """``warm_eigh`` on operands that are already padded to ``padded_size(n)`` with an
     identity block (``Cp`` symmetric; ``Bp`` the previous basis, e.g. from the fused
     CMA-ES epilogue).  Returns ``(w_padded, Bp_rotated)``; the first ``n`` entries /
     the leading n×n block are the decomposition of the unpadded matrix."""
     np_ = Cp.shape[0]
     assert np_ == padded_size(n) and Bp.shape == Cp.shape
-    if config.get("jacobi_reortho"):
+    if REORTHO:
         # Newton–Schulz on the padded basis: the identity block is a fixed point
         Bp = torch.addmm(Bp, Bp, Bp.t() @ Bp, beta=1.5, alpha=-0.5) if config.get("plain_gemm") == "blas" else reorthonormalize(Bp)
     if config.get("plain_gemm") == "blas":
@@ -144,9 +153,9 @@ def warm_eigh_padded(Cp: torch.Tensor, Bp: torch.Tensor, n: int, max_sweeps: int
         A = _btcb(Cp, Bp)
     Bp = Bp.contiguous()
     sweeps = config.get("jacobi_sweeps") if max_sweeps is None else max_sweeps
-    tol = tol or config.get("jacobi_tol_factor") * 1.1920929e-07 * max(n, 16) ** 0.5
+    tol = tol or TOL_FACTOR * 1.1920929e-07 * max(n, 16) ** 0.5
     w, _ = _ext.ops().jacobi_sweeps(A, Bp, schedule(np_ // 16, Cp.device), int(sweeps), float(tol),
-                                    float(config.get("jacobi_inner_tol")), int(config.get("jacobi_inner")), int(config.get("jacobi_fused")))
+                                    float(INNER_TOL), int(INNER), int(FUSED if fused is None else fused))
     return w, Bp
 
 

@@ -226,47 +226,9 @@ def mm(A: torch.Tensor, B: torch.Tensor, *, ta: bool = False, tb: bool = False, 
     return C
 
 
-# ---------------------------------------------------------------------------- fragment planes
-class Planes:
-    """An f32 matrix (rows × K, K-contiguous) pre-split for the bf16x6 GEMM: int16 [3, rows, kp]
-    high / middle / low bf16 parts, each 32-k group stored in the 16x16x32 MFMA fragment order
-    (``gemm_ks.hip: split_planes_kernel``).  A GEMM that reads planes does no split arithmetic
-    for that operand — worth it for an operand that is re-read by many output tiles and is
-    constant (a problem's rotation) or produced once per generation (CMA-ES's B·D, the
-    sampling noise).  On the CPU the object just holds the f32 matrix."""
-
-    __slots__ = ("t", "rows", "K")
-
-    def __init__(self, t: torch.Tensor, rows: int, K: int):
-        self.t, self.rows, self.K = t, int(rows), int(K)
-
-    @property
-    def is_cuda(self) -> bool:
-        return self.t.is_cuda
-
-
-def split_planes(X: torch.Tensor, colscale: Optional[torch.Tensor] = None) -> Planes:
-    """``Planes`` of ``X·diag(colscale)`` (the column scale fused into the split pass)."""
-    if X.is_cuda:
-        X_ = X if X.stride(-1) == 1 else X.contiguous()
-        return Planes(_ext.ops().split_planes(X_, None if colscale is None else colscale.contiguous()), X.shape[0], X.shape[1])
-    return Planes(X if colscale is None else X * colscale[None, :], X.shape[0], X.shape[1])
-
-
-def normal_planes(key: torch.Tensor, rows: int, d: int, row0: int = 0) -> Planes:
-    """``Planes`` of rows [row0, row0 + rows) of ``random.normal(key, (·, d))`` generated in
-    place (the f32 noise matrix is never written); d % 4 == 0 on the device."""
-    if key.is_cuda and d % 4 == 0:
-        return Planes(_ext.ops().philox_normal_planes(key.contiguous(), int(rows), int(d), int(row0)), rows, d)
-    from . import random as rnd
-
-    return Planes(rnd.normal(key, (rows, d), offset=row0 * d).to(key.device), rows, d)
-
-
 def mm_nt(A, B, *, alpha: float = 1.0, alpha_ptr: Optional[torch.Tensor] = None, bias_n: Optional[torch.Tensor] = None,
           out: Optional[torch.Tensor] = None, a_sub_k: Optional[torch.Tensor] = None, sub_cols: int = 0) -> torch.Tensor:
-    """``alpha·(*alpha_ptr)·(A − a_sub_k)·Bᵀ (+ bias_n)`` where A (M × K) and B (N × K) are f32
-    tensors or :class:`Planes` (bf16x6 fragment planes: no split work for that operand).
+    """``alpha·(*alpha_ptr)·(A − a_sub_k)·Bᵀ (+ bias_n)`` for f32 A (M × K) and B (N × K).
 
     ``sub_cols > 0``: ``a_sub_k`` is a (blocks, K) matrix and output columns
     [c·sub_cols, (c+1)·sub_cols) use shift row c — several shifted products that share A (the
@@ -276,23 +238,9 @@ def mm_nt(A, B, *, alpha: float = 1.0, alpha_ptr: Optional[torch.Tensor] = None,
             blocks = [((A - a_sub_k[c][None, :]) @ B[c * sub_cols : (c + 1) * sub_cols].T) for c in range(a_sub_k.shape[0])]
             C = alpha * torch.cat(blocks, 1)[:, : B.shape[0]]
             return C if alpha_ptr is None else C * alpha_ptr.reshape(())
-        N = B.rows if isinstance(B, Planes) else B.shape[0]
-        bp, bf = (B.t, None) if isinstance(B, Planes) else (None, B)
-        return _ext.ops().gemm_ks_pl(A, None, bf, bp, int(A.shape[0]), int(N), int(A.shape[1]), float(alpha), alpha_ptr, bias_n, out,
-                                     a_sub_k.contiguous(), int(sub_cols), int(a_sub_k.stride(0)))
-    if not isinstance(A, Planes) and not isinstance(B, Planes):
-        return mm(A, B, tb=True, alpha=alpha, alpha_ptr=alpha_ptr, bias_n=bias_n, out=out, a_sub_k=a_sub_k)
-    M = A.rows if isinstance(A, Planes) else A.shape[0]
-    N = B.rows if isinstance(B, Planes) else B.shape[0]
-    K = A.K if isinstance(A, Planes) else A.shape[1]
-    dev = A.is_cuda if isinstance(A, Planes) else A.is_cuda
-    if dev:
-        ap, af = (A.t, None) if isinstance(A, Planes) else (None, A)
-        bp, bf = (B.t, None) if isinstance(B, Planes) else (None, B)
-        return _ext.ops().gemm_ks_pl(af, ap, bf, bp, int(M), int(N), int(K), float(alpha), alpha_ptr, bias_n, out, a_sub_k)
-    Am = A.t if isinstance(A, Planes) else A
-    Bm = B.t if isinstance(B, Planes) else B
-    return mm(Am, Bm, tb=True, alpha=alpha, alpha_ptr=alpha_ptr, bias_n=bias_n, out=out, a_sub_k=a_sub_k)
+        return _ext.ops().gemm_ks_pl(A, None, B, None, int(A.shape[0]), int(B.shape[0]), int(A.shape[1]), float(alpha), alpha_ptr, bias_n,
+                                     out, a_sub_k.contiguous(), int(sub_cols), int(a_sub_k.stride(0)))
+    return mm(A, B, tb=True, alpha=alpha, alpha_ptr=alpha_ptr, bias_n=bias_n, out=out, a_sub_k=a_sub_k)
 
 
 # ---------------------------------------------------------------------------- blocked planes

@@ -623,10 +623,8 @@ def _jacobi_sweep(A, B, tol):
     if np_ > n:
         Ap[n:, n:] = torch.eye(np_ - n, device=dev)
         Bp[n:, n:] = torch.eye(np_ - n, device=dev)
-    from .. import config
-
-    _ext.ops().jacobi_sweeps(Ap, Bp, jacobi.schedule(np_ // 16, dev), 1, float(tol), float(config.get("jacobi_inner_tol")),
-                             int(config.get("jacobi_inner")), int(config.get("jacobi_fused")))
+    _ext.ops().jacobi_sweeps(Ap, Bp, jacobi.schedule(np_ // 16, dev), 1, float(tol), float(jacobi.INNER_TOL), int(jacobi.INNER),
+                             int(jacobi.FUSED))
     return Ap[:n, :n].contiguous(), Bp[:n, :n].contiguous()
 
 

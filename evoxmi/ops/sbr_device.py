@@ -28,6 +28,10 @@ also go to a device ring (:meth:`DeviceSBR.history`) that benches read after tim
 """
 from __future__ import annotations
 
+import contextlib
+from dataclasses import dataclass
+from typing import Optional
+
 import torch
 
 from . import _ext
@@ -35,6 +39,74 @@ from .linalg import mm
 from .sbr import SBRConfig, _probe_vectors
 
 LOG_LEN = 4096
+
+# ---------------------------------------------------------------------------- tuned constants
+# (round 6: fixed here instead of ~20 EVOXMI_SBR_* knobs; each value is the round-3..5
+# measurement recorded in profiles/NOTES.md)
+#
+# decision rules of the device control kernel (eigh_sbr_dev.hip):
+#   near_only 1.5   — a near-only step at 1.5-3e-5 often left far pairs: 1.5 saved 0.25 iterations
+#   theta0 1.0 / theta_kappa 0.05 — the local far threshold once κ ≤ 0.05 keeps settled solves at
+#                     4 iterations (without it they stall at ≈1.3e-5)
+#   thr_fac 0.3     — global far-pair threshold (0.2 / 0.5 measured slower)
+#   block_sweeps 2  — one sweep per block: 7 iterations per solve instead of 4.4
+#   damp_tau / damp_kappa 1.0, ns_kappa 0.3, ns_iters 2 — the damping / Newton–Schulz rules of
+#                     the round-2 solver (τ 1.5 / 2 fell back)
+DEVICE_CFG = dict(near_only=1.5, theta0=1.0, theta_kappa=0.05, thr_fac=0.3, block_sweeps=2, damp_tau=1.0, damp_kappa=1.0,
+                  ns_kappa=0.3, ns_iters=2)
+RECOVER = 2          # divergences answered by a forced damped + re-orthonormalised step
+LEAN_GUARD = 1       # a lean slot whose step needs damping / NS / order 6 stops the solve (capped)
+FULL_SLOTS = 5       # warm schedule: slots ≥ 5 are lean (no damping / NS / X³ kernels)
+LATE_FULL_SLOTS = 3  # late schedule: damping / NS / order-6 kernels in slots 0-2 only
+LATE_DAMP_SLOTS = 1  # late schedule: the damping power steps in slot 0 only (89 launches / generation)
+LATE_NS_ITERS = 2    # forced Newton–Schulz steps per late solve (1: trajectory parity 5.8 % > 5 % bound)
+LEAN_MAX_N = 1024    # larger matrices keep every slot full (d = 2000 capped in a lean slot)
+LARGE_N_ITERS = 8    # ... and get at least 8 slots (7 capped one d = 2000 solve)
+
+
+@dataclass(frozen=True)
+class Schedule:
+    """A fixed device schedule: ``iters`` refinement slots; slots ≥ ``lean_from`` carry no
+    damping / Newton–Schulz / X³ kernels, slots ≥ ``damp_from`` no damping power steps;
+    ``ns_iters`` forced Newton–Schulz iterations; ``xgate``: the damping also follows the
+    generator's free bounds (cold starts)."""
+
+    iters: int
+    lean_from: Optional[int] = None
+    damp_from: Optional[int] = None
+    ns_iters: int = 2
+    xgate: bool = False
+
+
+def schedule(level: str, n: int) -> Schedule:
+    """The schedule of a CMA-ES graph variant: ``"cold"`` (every slot full, bounds-gated
+    damping), ``"warm"`` or ``"late"`` (lean tail slots) at matrix order ``n``."""
+    from .. import config
+
+    if level == "cold":
+        return Schedule(int(config.get("sbr_cold_iters")), None, None, DEVICE_CFG["ns_iters"], True)
+    late = level == "late"
+    iters = int(config.get("sbr_late_iters" if late else "sbr_device_iters"))
+    if n > LEAN_MAX_N:
+        return Schedule(max(iters, LARGE_N_ITERS), None, None, DEVICE_CFG["ns_iters"], False)
+    if late:
+        return Schedule(iters, LATE_FULL_SLOTS, LATE_DAMP_SLOTS, LATE_NS_ITERS, False)
+    return Schedule(iters, FULL_SLOTS, None, DEVICE_CFG["ns_iters"], False)
+
+
+_LEVEL = ["warm"]
+
+
+@contextlib.contextmanager
+def use_schedule(level: str):
+    """Solves inside this context use :func:`schedule` (``level``) — the CMA-ES graph variants
+    (``CMAES.graph_variant_context``)."""
+    prev = _LEVEL[0]
+    _LEVEL[0] = level
+    try:
+        yield
+    finally:
+        _LEVEL[0] = prev
 
 
 class DeviceSBR:
@@ -63,11 +135,6 @@ class DeviceSBR:
          self.G) = (mat() for _ in range(11))
         from .. import config
 
-        # opt-in: A[perm, perm] and B[:, perm] gathered row-wise first (measured no faster)
-        self.prepermute = bool(config.get("sbr_prepermute"))
-        # a block already diagonal to this relative off-norm skips its remaining Jacobi sweeps
-        self.sweep_tol = float(config.get("sbr_sweep_tol"))
-        self.Ap, self.Bp = (mat(), mat()) if self.prepermute else (None, None)
         sb = cfg.block
         nb = -(-n // sb)
         self.perm = torch.zeros(n, dtype=torch.int32, device=dev)
@@ -76,7 +143,7 @@ class DeviceSBR:
         self.nparts = int(ops.gemm_ks_grid(n, n, 1))
         self.part = torch.zeros(4 * self.nparts, dtype=torch.float64, device=dev)
         # stats partials of X² = −X·Xᵀ: the free ‖X‖_F bound that gates every step size (sbr_dev_prep)
-        self.xgate = bool(config.get("sbr_xgate") == 1) if xgate is None else bool(xgate)
+        self.xgate = bool(xgate)
         self.part2 = torch.zeros(4 * self.nparts, dtype=torch.float64, device=dev) if self.xgate else None
         K = self.K
         self.hist = torch.zeros(4 * (K + 1), dtype=torch.float64, device=dev)
@@ -98,8 +165,8 @@ class DeviceSBR:
         # Newton–Schulz's T − ½T·(TᵀT − I) — run at bf16x3 (≈1e-5 of the correction's own size)
         self.corr = "x3" if config.get("sbr_corr_prec") == "x3" else None
         self.prm = [float(cfg.tol), float(cfg.ns_kappa), float(cfg.damp_kappa), float(cfg.t4_kappa), float(cfg.near_only),
-                    float(cfg.theta0), float(cfg.theta_kappa), float(self.lean_from), float(config.get("sbr_recover")),
-                    float(config.get("sbr_lean_guard")), float(self.xgate), float(self.damp_from)]
+                    float(cfg.theta0), float(cfg.theta_kappa), float(self.lean_from), float(RECOVER),
+                    float(LEAN_GUARD), float(self.xgate), float(self.damp_from)]
 
     # ------------------------------------------------------------------ pieces
     def _btcb(self, C, skip):
@@ -124,17 +191,10 @@ class DeviceSBR:
         shift = (j % 2) * (sb // 2)
         full = j < self.lean_from
         damp_slot = j < self.damp_from
-        ops.sbr16_block_out(self.A, shift, int(cfg.block_sweeps), sb, self.perm, self.Q, self.dq, sk_all, self.sweep_tol)
+        ops.sbr16_block_out(self.A, shift, int(cfg.block_sweeps), sb, self.perm, self.Q, self.dq, sk_all, 0.0)
         # far generator X and Bq = B[:, perm]·blockdiag(Q) in one launch
-        if self.prepermute:
-            # A[perm, perm] and B[:, perm] row by row first, so that the tiles read contiguous blocks —
-            # far+Bq 30.0 instead of 28 µs plus 6 µs for the gather (profiles/NOTES.md): off by default
-            ops.sbr16_permute_out(self.A, self.perm, self.B, self.Ap, self.Bp, sk_far, sk_all)
-            ops.sbr16_far_bq_out(self.Ap, self.perm, self.Q, self.dq, self.hist[4 * j : 4 * j + 4], float(cfg.thr_fac),
-                                 self.theta[j : j + 1], self.X, self.Bp, self.Bq, sb, sk_far, sk_all, True)
-        else:
-            ops.sbr16_far_bq_out(self.A, self.perm, self.Q, self.dq, self.hist[4 * j : 4 * j + 4], float(cfg.thr_fac),
-                                 self.theta[j : j + 1], self.X, self.B, self.Bq, sb, sk_far, sk_all)
+        ops.sbr16_far_bq_out(self.A, self.perm, self.Q, self.dq, self.hist[4 * j : 4 * j + 4], float(cfg.thr_fac),
+                             self.theta[j : j + 1], self.X, self.B, self.Bq, sb, sk_far, sk_all)
         corr = self.corr
         # X skew ⇒ X² = −X·Xᵀ, symmetric (upper tiles only)
         mm(self.X, self.X, tb=True, mode=1, alpha=-1.0, out=self.X2, skip=sk_far, stat_part=self.part2, stat_diag_only=True,
@@ -209,56 +269,40 @@ def workspace(n: int, device, cfg: SBRConfig, iters: int, lean_from: int = None,
     from .. import config
 
     key = (n, str(device), cfg.block, cfg.block_sweeps, cfg.thr_fac, cfg.ns_iters, cfg.damp_tau, cfg.tol, cfg.ns_kappa,
-           cfg.damp_kappa, cfg.t4_kappa, cfg.near_only, cfg.theta0, cfg.theta_kappa, int(iters), lean_from,
-           bool(config.get("sbr_prepermute")), float(config.get("sbr_sweep_tol")), int(config.get("sbr_recover")),
-           int(config.get("sbr_lean_guard")), bool(xgate), damp_from, config.get("sbr_corr_prec"))
+           cfg.damp_kappa, cfg.t4_kappa, cfg.near_only, cfg.theta0, cfg.theta_kappa, int(iters), lean_from, bool(xgate), damp_from,
+           config.get("sbr_corr_prec"))
     if key not in _WS:
         _WS[key] = DeviceSBR(n, device, cfg, iters, lean_from, xgate, damp_from)
     return _WS[key]
 
 
-def schedule_iters(n: int, iters: int) -> int:
-    """Refinement slots a schedule of ``iters`` slots actually runs at order ``n`` (larger
-    matrices get at least ``sbr_large_n_iters``; see :func:`eigh_device`)."""
+def schedule_iters(n: int, level: str) -> int:
+    """Refinement slots the ``level`` schedule runs at matrix order ``n``."""
+    return schedule(level, n).iters
+
+
+def device_config(ns_iters: int = None) -> SBRConfig:
     from .. import config
 
-    if n > int(config.get("sbr_lean_max_n")) and iters < int(config.get("sbr_cold_iters")):
-        return max(int(iters), int(config.get("sbr_large_n_iters")))
-    return int(iters)
+    kw = dict(DEVICE_CFG)
+    if ns_iters is not None:
+        kw["ns_iters"] = int(ns_iters)
+    return SBRConfig(tol=config.get("eigh_tol"), block=config.get("sbr_block"), **kw)
 
 
 def eigh_device(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None, iters: int = None):
     """Converged-or-capped eigendecomposition of symmetric ``C`` warm-started from
-    ``B_prev``, entirely on the device (see module docstring).  Returns ``(w, B, stats)``."""
+    ``B_prev``, entirely on the device (see module docstring).  Returns ``(w, B, stats)``.
+    ``iters``: an explicit schedule of that many slots, every slot full (tests, probes);
+    default: the schedule of the active level (:func:`use_schedule`, warm outside a context)."""
     from .. import config
 
-    cfg = cfg or SBRConfig(tol=config.get("eigh_tol"), block=config.get("sbr_block"), near_only=config.get("sbr_near_only"),
-                           theta0=config.get("sbr_theta0"), theta_kappa=config.get("sbr_theta_kappa"),
-                           thr_fac=config.get("sbr_thr_fac"), block_sweeps=config.get("sbr_sweeps"),
-                           damp_tau=config.get("sbr_damp_tau"), damp_kappa=config.get("sbr_damp_kappa"),
-                           ns_kappa=config.get("sbr_ns_kappa"), ns_iters=config.get("sbr_ns_iters"))
     if iters is None:
-        iters = config.get("sbr_device_iters")
-        # lean tail slots only in a schedule that does not start cold (CMA-ES's cold-start
-        # variant passes a longer schedule with every slot full)
-        lean = config.get("sbr_full_slots") if iters < config.get("sbr_cold_iters") else None
-        # larger matrices stay above the damping / Newton–Schulz thresholds for more iterations
-        # (d = 2000: the lean-slot guard capped warm solves at slot 5): every slot full there,
-        # and at least sbr_large_n_iters slots (a 7-slot warm schedule capped one d = 2000 solve
-        # at 7 iterations, off_rel 1.39e-5)
-        if C.shape[0] > int(config.get("sbr_lean_max_n")):
-            lean = None
-            iters = max(iters, int(config.get("sbr_large_n_iters")))
+        sch = schedule(_LEVEL[0], C.shape[0])
     else:
-        lean = None
-    # the bounds-gated damping: everywhere (1) or in the cold-start schedule only (2): the
-    # large generators of a cold start are where an undamped step diverged (d = 2000), and in
-    # settled solves the extra power iterations cost ≈3 % of a generation (profiles/r5_eigh_recover.txt)
-    xg = int(config.get("sbr_xgate"))
-    xgate = xg == 1 or (xg == 2 and iters >= config.get("sbr_cold_iters"))
-    ds = int(config.get("sbr_damp_slots"))
-    damp_from = ds if (lean is not None and ds > 0) else None
-    return workspace(C.shape[0], C.device, cfg, iters, lean, xgate, damp_from).solve(C, B_prev)
+        sch = Schedule(int(iters), None, None, DEVICE_CFG["ns_iters"], int(iters) >= int(config.get("sbr_cold_iters")))
+    cfg = cfg or device_config(sch.ns_iters)
+    return workspace(C.shape[0], C.device, cfg, sch.iters, sch.lean_from, sch.xgate, sch.damp_from).solve(C, B_prev)
 
 
 def all_histories():

@@ -9,10 +9,24 @@ rows straight out of the generating rank's memory is the "direct mesh" path of S
 host involvement (capturable, sizes decided on the device).  Handles are exchanged once
 through ``torch.distributed`` (``all_gather_object``).
 
-Ordering: a peer's buffer is complete once this rank's next collective with it has
-completed (the peer wrote it before entering that collective on its stream); it must not
-be rewritten before every reader is done — the owner calls :meth:`PeerBuffer.fence`
-(a one-float all-reduce) after its reads.  Backends without device IPC (CPU / gloo on
+Memory model (round 6: explicit, not left to cache side effects).  Peer buffers are plain
+``hipMalloc`` allocations (coarse-grained): peers read them over xGMI, and those reads are
+served from the owner's HBM through its memory-side cache, NOT from the owner's L2 — nor
+is a reader's L2 kept coherent with another GPU's writes.  So every exchange is:
+
+1. writer: the kernels that fill the owner's buffer, then :meth:`PeerBuffer.release` — a
+   one-thread kernel with a system-scope release fence (``peer_release``: the owner's dirty L2
+   lines are written back to HBM) — all on the owner's stream;
+2. a collective between writer and reader (the fitness all-gather / z_max all-reduce of the
+   same generation): RCCL orders the reader's later kernels after the owner's earlier ones;
+3. reader: the gather kernel issues a system-scope acquire fence before its first peer load
+   (``moead_halo_gather``: lines of the peer buffer left in the reader's L2 by the previous
+   generation are invalidated) and reads the rows non-temporally (read once);
+4. reuse: the owner must not rewrite the buffer before every reader is done — the owner calls
+   :meth:`PeerBuffer.fence` (a one-float all-reduce) after its reads.
+
+The fences cost one launch per generation on the writer and one invalidate per reading wave
+(measured in profiles/NOTES.md, round 6).  Backends without device IPC (CPU / gloo on
 CPU tensors) fall back to an all-gather of the full buffers (``peer_table`` returns
 ``None``); the single-process :class:`SimulatedDistContext` points every peer entry at the
 local buffer (same rows read from local HBM).
@@ -73,6 +87,14 @@ class PeerBuffer:
     def peer_table(self):
         """int64 device pointers of every rank's buffer (None: no device IPC)."""
         return self.table
+
+    def release(self):
+        """Writer side of the contract: system-scope release after this rank filled ``local``
+        (a no-op without device IPC — the all-gather fallback and the simulated rank read
+        through the normal stream order — except that the simulated rank runs the kernel, so
+        its cost is in the one-GPU projection)."""
+        if self.device.type == "cuda" and (self.ipc or getattr(self.ctx, "backend", "") == "simulated"):
+            _ext.ops().peer_release(self.device.index or 0)
 
     def fence(self):
         """All ranks have finished reading every peer buffer (before the owners rewrite them)."""

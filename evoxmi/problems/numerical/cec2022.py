@@ -220,14 +220,6 @@ class _CEC2022(Problem):
                 if pl is None:
                     pl = self._cache[key] = linalg.h3_planes(M)
                 return linalg.tall_nt(X, M, alpha=float(s), a_sub_k=o.contiguous(), b_planes=pl)
-            if config.get("gemm_planes") and config.get("gemm_prec") == "x6" and config.get("plain_gemm") == "evoxmi" and D % 4 == 0:
-                # the rotation is constant: its bf16x6 fragment planes are split once and reused
-                # by every evaluation (the GEMM splits only the population on the fly)
-                key = (M.data_ptr(), M.shape)
-                pl = self._cache.get(("planes",) + key)
-                if pl is None:
-                    pl = self._cache[("planes",) + key] = linalg.split_planes(M)
-                return linalg.mm_nt(X, pl, alpha=float(s), a_sub_k=o.contiguous())
             return linalg.plain_nt(X, M, alpha=float(s), a_sub_k=o.contiguous())
         return ((X - o) * s) @ M.T
 

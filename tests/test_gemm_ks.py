@@ -150,62 +150,6 @@ def test_gemm_ks_fused_shift_prologue(M, N, K):
     assert bool((Z0 == 0).all())
 
 
-def _planes_to_f32(P, K):
-    """Reassemble h + m + l from int16 fragment planes [3, rows, kp] (fragment order: position
-    p of a 32-k group holds k = 16·((p % 8) >> 2) + 4·(p // 8) + (p % 4))."""
-    p = torch.arange(P.shape[2])
-    g, r = p // 32, p % 32
-    q, j = r // 8, r % 8
-    k = 32 * g + 16 * (j >> 2) + 4 * q + (j & 3)
-    parts = (P.cpu().to(torch.int32) << 16).view(torch.float32)  # bf16 bits → f32
-    X = torch.zeros(P.shape[1], P.shape[2], dtype=torch.float64)
-    X[:, k] = parts.double().sum(0)
-    return X[:, :K]
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("rows,K", [(100, 1000), (33, 20), (7, 64)])
-def test_split_planes_exact(rows, K):
-    """The three bf16 parts of every element sum back to the f32 value exactly (column scale
-    applied first, padding columns zero)."""
-    g = torch.Generator().manual_seed(rows + K)
-    X = torch.randn(rows, K, generator=g) * torch.logspace(-6, 6, K)[None, :]
-    s = torch.rand(K, generator=g) + 0.5
-    P = linalg.split_planes(X.cuda(), s.cuda()).t
-    assert P.shape == (3, rows, (K + 31) // 32 * 32)
-    assert torch.equal(_planes_to_f32(P, K), (X * s).double())
-
-
-@pytest.mark.gpu
-def test_normal_planes_match_the_philox_normals():
-    from evoxmi import random as rnd
-
-    key = rnd.PRNGKey(7, device=torch.device("cuda"))
-    P = linalg.normal_planes(key, 50, 1000, row0=3).t
-    z = rnd.normal(key, (50, 1000), offset=3 * 1000)
-    assert torch.equal(_planes_to_f32(P, 1000), z.cpu().double())
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("M,N,K", [(10000, 1000, 1000), (257, 130, 72), (64, 48, 20)])
-@pytest.mark.parametrize("which", ["a", "b", "ab"])
-def test_gemm_planes_matches_fp64(M, N, K, which):
-    g = torch.Generator().manual_seed(M + N + K)
-    A, B = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g)
-    bias, ap = torch.randn(N, generator=g), torch.tensor([0.75])
-    Ad, Bd = A.cuda(), B.cuda()
-    a = linalg.split_planes(Ad) if "a" in which else Ad
-    b = linalg.split_planes(Bd) if "b" in which else Bd
-    C = linalg.mm_nt(a, b, alpha=2.0, alpha_ptr=ap.cuda(), bias_n=bias.cuda()).cpu().double()
-    R = _ref(A, B, False, True, 1.5, bias)
-    assert ((C - R).abs() <= 1.5 * _tol(A, B, False, True, K) + 1e-6).all()
-    if which == "b":  # the CEC form: shifted f32 population × constant rotation planes
-        o = torch.randn(K, generator=g)
-        Z = linalg.mm_nt(Ad, b, a_sub_k=o.cuda()).cpu().double()
-        ref = (A.double() - o.double()) @ B.double().t()
-        assert ((Z - ref).abs() <= 2e-6 * ((A - o).double().abs() @ B.double().abs().t()) + 1e-30).all()
-
-
 @pytest.mark.gpu
 def test_gemm_per_block_shifts():
     """Stacked shifted products in one launch: column block c uses shift row c (exact zero when

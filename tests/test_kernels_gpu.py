@@ -285,8 +285,7 @@ def test_jacobi_fused_apply_solve_is_bit_identical(n, sweeps):
     C = ((Q * lam) @ Q.T + (X + X.T)).float().cuda()
     outs = []
     for fused in (0, 1, 2):  # split launches / fused apply+solve / B update inside the next solve launch
-        with config.override(jacobi_fused=fused):
-            outs.append(jacobi.warm_eigh(C, Q.float().cuda(), max_sweeps=sweeps))
+        outs.append(jacobi.warm_eigh(C, Q.float().cuda(), max_sweeps=sweeps, fused=fused))
     for o in outs[1:]:
         assert torch.equal(outs[0][0], o[0]) and torch.equal(outs[0][1], o[1])
 

@@ -32,8 +32,9 @@ def test_device_schedule_converges_like_host_driver(gens):
     # the host driver (adaptive, no plans, no graphs) takes the same decisions
     from evoxmi import config
 
-    _, _, info = sbr.eigh_warm(C, B, sbr.SBRConfig(graphs=False, plan=False, theta0=config.get("sbr_theta0"),
-                                                  near_only=config.get("sbr_near_only"), thr_fac=config.get("sbr_thr_fac")))
+    dc = sbr_device.DEVICE_CFG
+    _, _, info = sbr.eigh_warm(C, B, sbr.SBRConfig(graphs=False, plan=False, theta0=dc["theta0"], near_only=dc["near_only"],
+                                                  thr_fac=dc["thr_fac"]))
     assert abs(int(st[2]) - info.refine_iters) <= 1, (int(st[2]), info.refine_iters)
 
 
@@ -268,7 +269,7 @@ def test_capped_late_solves_escalate_the_schedule_without_device_syncs(monkeypat
     from evoxmi.problems.numerical import CEC2022TestSuit
     from evoxmi.workflows import StdWorkflow
 
-    with config.override(sbr_late_iters=2, sbr_late_full_slots=2):
+    with config.override(sbr_late_iters=2):  # the late schedule's full slots are clipped to its 2 slots
         center = (torch.rand(1000, generator=torch.Generator().manual_seed(1)) * 160 - 80).cuda()
         algo = CMAES(center_init=center, init_stdev=20.0, pop_size=10000)
         wf = StdWorkflow(algo, CEC2022TestSuit.create(1), graph=True)

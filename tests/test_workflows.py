@@ -314,4 +314,4 @@ def test_simulated_rank_context_runs_one_rank_share():
     a = st.get_child_state("algorithm")
     assert a.population.shape == (10, 8)
     assert torch.isfinite(a.mean).all() and torch.isfinite(a.C).all()
-    assert ctx.bytes_all_reduce == 3 * (8 + 64) * 4
+    assert ctx.bytes_all_reduce == 3 * (8 + 8 * 9 // 2) * 4  # packed upper triangle of S + the mean shift

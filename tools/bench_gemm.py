@@ -84,13 +84,6 @@ def main():
                      "x6_tflops": round(flops / t["x6"] / 1e6, 1), "f32_tflops": round(flops / t["f32"] / 1e6, 1),
                      "torch_tflops": round(flops / t_t / 1e6, 1), "x6_vs_torch": round(t_t / t["x6"], 3)})
         print(json.dumps(rows[-1]), flush=True)
-    # fragment planes (pre-split operands: no split arithmetic in the GEMM) on the NT shapes
-    Ap, Bp, Zp = linalg.split_planes(A), linalg.split_planes(B), linalg.split_planes(Z)
-    for name, f in [("1000^3 NT planes A+B", lambda: linalg.mm_nt(Ap, Bp, out=out)),
-                    ("1000^3 NT planes B only", lambda: linalg.mm_nt(A, Bp, out=out)),
-                    ("10000x1000x1000 NT planes B only", lambda: linalg.mm_nt(Z, Bp, out=out_t)),
-                    ("10000x1000x1000 NT planes A+B", lambda: linalg.mm_nt(Zp, Bp, out=out_t))]:
-        print(json.dumps({"case": name, "x6_us": round(timeit(f, a.reps), 2)}), flush=True)
 
 
 if __name__ == "__main__":
