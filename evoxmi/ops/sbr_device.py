@@ -61,6 +61,11 @@ LATE_FULL_SLOTS = 3  # late schedule: damping / NS / order-6 kernels in slots 0-
 LATE_DAMP_SLOTS = 1  # late schedule: the damping power steps in slot 0 only (89 launches / generation)
 LATE_NS_ITERS = 2    # forced Newton–Schulz steps per late solve (1: trajectory parity 5.8 % > 5 % bound)
 LEAN_MAX_N = 1024    # larger matrices keep every slot full (d = 2000 capped in a lean slot)
+# order-2 steps (round 6): a far step whose generator is proven small (‖αX‖₂ ≤ 2e-3 from the X²
+# GEMM's free bound) takes exp(αX) − I ≈ αX + ½α²X² — truncation ≤ 1.4e-9, orthogonal to
+# ‖X‖⁴/4 — and skips the Taylor Vᵀ GEMM (0 disables)
+ORDER2_THR = 2e-3
+CW = 16              # control words per slot (eigh_sbr_dev.hip kCW)
 LARGE_N_ITERS = 8    # ... and get at least 8 slots (7 capped one d = 2000 solve)
 
 
@@ -142,14 +147,15 @@ class DeviceSBR:
         self.dq = torch.zeros(n, device=dev)
         self.nparts = int(ops.gemm_ks_grid(n, n, 1))
         self.part = torch.zeros(4 * self.nparts, dtype=torch.float64, device=dev)
-        # stats partials of X² = −X·Xᵀ: the free ‖X‖_F bound that gates every step size (sbr_dev_prep)
+        # stats partials of X² = −X·Xᵀ (its diagonal): free bounds of ‖X‖₂ — they gate the damping's
+        # power iteration in the cold schedule (xgate) and choose order-2 steps in every schedule
         self.xgate = bool(xgate)
-        self.part2 = torch.zeros(4 * self.nparts, dtype=torch.float64, device=dev) if self.xgate else None
+        self.part2 = torch.zeros(4 * self.nparts, dtype=torch.float64, device=dev)
         K = self.K
         self.hist = torch.zeros(4 * (K + 1), dtype=torch.float64, device=dev)
         self.alpha = torch.ones(K + 1, device=dev)
         self.theta = torch.zeros(max(K, 1), device=dev)
-        self.ctrl = torch.ones(8 * max(K, 1), dtype=torch.int32, device=dev)
+        self.ctrl = torch.ones(CW * max(K, 1), dtype=torch.int32, device=dev)
         self.st = torch.zeros(8, dtype=torch.int32, device=dev)
         self.never = torch.zeros(1, dtype=torch.int32, device=dev)
         self.V = _probe_vectors(n, str(dev))
@@ -186,8 +192,8 @@ class DeviceSBR:
         ops = _ext.ops()
         cfg = self.cfg
         sb = cfg.block
-        c = self.ctrl[8 * j : 8 * j + 8]
-        sk_all, sk_far, sk_damp, sk_x3, sel6, sk_ns, sel_ns, sk_copy = (c[i : i + 1] for i in range(8))
+        c = self.ctrl[CW * j : CW * j + CW]
+        sk_all, sk_far, sk_damp, sk_x3, sel6, sk_ns, sel_ns, sk_copy, sk_vt = (c[i : i + 1] for i in range(9))
         shift = (j % 2) * (sb // 2)
         full = j < self.lean_from
         damp_slot = j < self.damp_from
@@ -203,7 +209,7 @@ class DeviceSBR:
             # three power-step launches (they return at once when the free Frobenius bound already
             # gives α = 1); α itself is formed by the prep kernel below (no_final)
             ops.sbr_damping_out(self.X2, self.V, float(cfg.damp_tau), self.alpha[j + 1 : j + 2], self.work, sk_damp, None, True,
-                                self.part2)
+                                self.part2 if self.xgate else None)
         if full:
             # order 6 only: X³ = X²·X = −X²·Xᵀ (skew)
             mm(self.X2, self.X, tb=True, mode=2, alpha=-1.0, out=self.X3, skip=sk_x3, prec=corr)
@@ -211,11 +217,13 @@ class DeviceSBR:
         # near-only iterations (no far step): the block-rotated basis is the new basis — Bq → B
         # copied by this launch (it returns at once otherwise), no copy launch of its own
         ops.sbr_dev_prep(self.X, self.X2, self.X3, self.alpha[j + 1 : j + 2], self.P, self.VT, c, self.work if damp_here else None,
-                         float(cfg.damp_tau), self.part2, self.Bq, self.B, int(corr is not None))
+                         float(cfg.damp_tau), self.part2 if self.xgate else None, self.Bq, self.B, int(corr is not None),
+                         self.part2 if ORDER2_THR > 0 else None, float(ORDER2_THR))
         # Vᵀ = M(−α) + X²·Pᵀ (order 4) or M(−α) − X³·Pᵀ (order 6): the control word selects
-        # (with the tiered precision the prep wrote M − I, so this is Vᵀ − I)
-        mm(self.X2, self.P, tb=True, alpha=1.0, beta=1.0, Cin=self.VT, out=self.VT, skip=sk_far, sel=sel6, A2=self.X3, alpha2=-1.0,
-           prec=corr)
+        # (with the tiered precision the prep wrote M − I, so this is Vᵀ − I); skipped (sk_vt,
+        # written by the prep) for a near-only iteration or an order-2 step
+        mm(self.X2, self.P, tb=True, alpha=1.0, beta=1.0, Cin=self.VT, out=self.VT, skip=sk_vt if ORDER2_THR > 0 else sk_far, sel=sel6,
+           A2=self.X3, alpha2=-1.0, prec=corr)
         # B·V → B, or into T when Newton–Schulz follows
         if corr is not None:
             # Bq + Bq·(V − I): the exact basis plus an x3 correction product

@@ -19,14 +19,15 @@ is a reader's L2 kept coherent with another GPU's writes.  So every exchange is:
    lines are written back to HBM) — all on the owner's stream;
 2. a collective between writer and reader (the fitness all-gather / z_max all-reduce of the
    same generation): RCCL orders the reader's later kernels after the owner's earlier ones;
-3. reader: the gather kernel issues a system-scope acquire fence before its first peer load
-   (``moead_halo_gather``: lines of the peer buffer left in the reader's L2 by the previous
-   generation are invalidated) and reads the rows non-temporally (read once);
+3. reader: a system-scope acquire launch right before the gather kernel (``moead_halo_gather``:
+   lines of the peer buffer left in any XCD's caches by the previous generation's reads are
+   invalidated), then the gather reads the rows non-temporally (read once);
 4. reuse: the owner must not rewrite the buffer before every reader is done — the owner calls
    :meth:`PeerBuffer.fence` (a one-float all-reduce) after its reads.
 
-The fences cost one launch per generation on the writer and one invalidate per reading wave
-(measured in profiles/NOTES.md, round 6).  Backends without device IPC (CPU / gloo on
+Each fence is one lane of 64 workgroups (a fence acts on its CU's L1 and its XCD's L2; blocks are
+dealt round-robin over the 8 XCDs): one launch per generation on each side (cost measured in
+profiles/NOTES.md, round 6 — a fence in every reading wave instead cost 0.21 ms per generation).  Backends without device IPC (CPU / gloo on
 CPU tensors) fall back to an all-gather of the full buffers (``peer_table`` returns
 ``None``); the single-process :class:`SimulatedDistContext` points every peer entry at the
 local buffer (same rows read from local HBM).

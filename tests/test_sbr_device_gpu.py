@@ -279,8 +279,11 @@ def test_capped_late_solves_escalate_the_schedule_without_device_syncs(monkeypat
         assert set(wf._graphs) == {"cold", None, "late"}
         for _ in range(11):
             st = wf.step(st)
-        # a 2-slot late schedule never fits "with a slot to spare": force the run onto it
-        algo._sched()["level"] = 0
+        # a 2-slot late schedule never fits "with a slot to spare": force the run onto it, past
+        # the two warm solves still in flight (whose reads would move it straight back)
+        sc = algo._sched()
+        sc["level"] = 0
+        sc["checked"] = sc["enqueued"] - CMAES.ESC_LAG + 1
 
         def forbidden(*a, **k):
             raise AssertionError("device sync on the step path")
@@ -292,8 +295,7 @@ def test_capped_late_solves_escalate_the_schedule_without_device_syncs(monkeypat
                 st = wf.step(st)
         torch.cuda.synchronize()
     lv = algo.schedule_levels(12)
-    # the first forced step replays the late graph; the solves read after it (still the warm
-    # ones in flight, then the capped late one) move the run back within ESC_LAG + 1 steps
-    assert lv[0] == "L" and "W" in lv[1 : CMAES.ESC_LAG + 2] and lv.endswith("W" * 6), lv
+    # the first late solve is read ESC_LAG steps later: capped → the warm schedule from then on
+    assert lv.startswith("L" * CMAES.ESC_LAG) and lv[CMAES.ESC_LAG] == "W" and lv.endswith("W" * 6), lv
     assert "C" not in lv  # the capped solves still in flight do not push the run to cold
     assert algo.schedule_escalations >= 1

@@ -69,6 +69,16 @@ def main():
             row["err_" + (prec or "x6")] = err
         rows.append(row)
         print(json.dumps(row), flush=True)
+    # a rank's column block of the same products under a column-distributed eigensolver (W = 2 / 4 / 8):
+    # the 1000² output already holds one 64 × 64 tile per CU, so a narrower output keeps each tile's
+    # serial K loop and only idles CUs — the evidence for keeping the d = 1000 solve replicated
+    for w in (2, 4, 8):
+        nc = n // w
+        Bn = B[:, :nc].contiguous()
+        on = torch.empty(n, nc, device=dev)
+        for prec in (None, "x3"):
+            us = timeit(lambda: linalg.mm(A, Bn, out=on, prec=prec), a.reps)
+            print(json.dumps({"case": f"NN column block 1000x{nc}x1000 (W={w})", "prec": prec or "x6", "us": round(us, 2)}), flush=True)
     # diag_add: BᵀB − I on an orthogonal B
     Q, _ = torch.linalg.qr(torch.randn(n, n, device=dev, generator=g, dtype=torch.float64))
     Qf = Q.float()

@@ -55,7 +55,7 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu", action="store_true")
     ap.add_argument("--force-dist", action="store_true", help="sharded protocol even on one rank")
-    ap.add_argument("--simulate-rank", type=int, default=None,
+    ap.add_argument("--simulate-rank", type=int, default=None,  # -1 (MOEA/D): the rank with the largest halo
                     help="time rank R's share of a --world N sharded step on this one GPU (collectives → same-size local ops)")
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--shard", choices=["auto", "owner", "replica"], default="auto", help="MOEA/D sharded mode")
@@ -100,6 +100,12 @@ def main():
     if sim:
         from evoxmi.parallel.context import SimulatedDistContext
 
+        if args.simulate_rank < 0 and args.algo == "moead":
+            # the rank with the largest owner-computes halo: the one that sets the step time
+            a0 = st.get_child_state("algorithm")
+            fr = [algo.halo_fraction(a0, r, args.world) for r in range(args.world)]
+            args.simulate_rank = max(range(args.world), key=lambda r: fr[r])
+        args.simulate_rank = max(args.simulate_rank, 0)
         sim_ctx = SimulatedDistContext(args.simulate_rank, args.world, algorithm=algo)
         if args.link_gbps:
             sim_ctx.wire.link_gbps = args.link_gbps
