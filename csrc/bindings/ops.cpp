@@ -475,8 +475,7 @@ void sbr_damping_out(const at::Tensor& X2, const at::Tensor& V, double tau, at::
 
 void sbr_dev_prep(const at::Tensor& X, const at::Tensor& X2, const at::Tensor& X3, at::Tensor& alpha, at::Tensor& P, at::Tensor& MT,
                   const at::Tensor& ctrl, const c10::optional<at::Tensor>& work, double tau, const c10::optional<at::Tensor>& xpart,
-                  const c10::optional<at::Tensor>& copy_src, const c10::optional<at::Tensor>& copy_dst, int64_t minus_id,
-                  const c10::optional<at::Tensor>& xstat, double o2_thr) {
+                  const c10::optional<at::Tensor>& copy_src, const c10::optional<at::Tensor>& copy_dst, int64_t minus_id) {
   for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&X, &X2, &X3, &P, &MT}) {
     CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t);
     TORCH_CHECK(t->sizes() == X.sizes(), "sbr_dev_prep: n×n");
@@ -505,18 +504,8 @@ void sbr_dev_prep(const at::Tensor& X, const at::Tensor& X2, const at::Tensor& X
     cs = copy_src->data_ptr<float>();
     cd = copy_dst->data_ptr<float>();
   }
-  // order-2 decision (eigh_sbr_dev.hip sbr_dev_prep_kernel): the X² stats and the slot's 9th control word
-  int64_t nx = 0;
-  const double* xs = xpart_ptr(xstat, nx);
-  int* cw = nullptr;
-  if (xs) {
-    TORCH_CHECK(ctrl.numel() >= 9, "sbr_dev_prep: order 2 needs the slot's 9 control words");
-    if (np == 0) np = nx;
-    TORCH_CHECK(np == nx, "sbr_dev_prep: xpart / xstat sizes");
-    cw = const_cast<int*>(ctrl.data_ptr<int>());
-  }
   evx_sbr_dev_prep(X.data_ptr<float>(), X2.data_ptr<float>(), X3.data_ptr<float>(), (int)X.size(0), alpha.data_ptr<float>(),
-                   P.data_ptr<float>(), MT.data_ptr<float>(), ctrl.data_ptr<int>(), cur_stream(), v2, v3, (float)tau, xp, (int)np, cs, cd, (int)minus_id, xs, (float)(o2_thr * o2_thr), cw);
+                   P.data_ptr<float>(), MT.data_ptr<float>(), ctrl.data_ptr<int>(), cur_stream(), v2, v3, (float)tau, xp, (int)np, cs, cd, (int)minus_id);
 }
 
 void sbr_dev_copy(const at::Tensor& src, at::Tensor& dst, const at::Tensor& skip) {
@@ -532,7 +521,7 @@ void sbr_dev_ctrl(const at::Tensor& part, int64_t nparts, int64_t j, int64_t K, 
                   at::Tensor& eig_stats, at::Tensor& w_init, at::Tensor& log, at::Tensor& log_count) {
   TORCH_CHECK(log.scalar_type() == at::kDouble && log.is_contiguous() && log_count.scalar_type() == at::kInt, "sbr_dev_ctrl: log");
   TORCH_CHECK(prm.size() >= 8, "sbr_dev_ctrl: params [tol, ns_kappa, damp_kappa, t4_kappa, near_only, theta0, theta_kappa, lean_from, (recover, lean_guard, xgate, damp_from)]");
-  TORCH_CHECK(hist.scalar_type() == at::kDouble && hist.numel() >= 4 * (K + 1) && ctrl.numel() >= 16 * K && alpha.numel() >= K + 1 &&
+  TORCH_CHECK(hist.scalar_type() == at::kDouble && hist.numel() >= 4 * (K + 1) && ctrl.numel() >= 8 * K && alpha.numel() >= K + 1 &&
                   theta.numel() >= K && st.numel() >= 8 && part.numel() >= 4 * nparts, "sbr_dev_ctrl: buffers");
   float p6[7] = {(float)prm[0], (float)prm[1], (float)prm[2], (float)prm[3], (float)prm[4], (float)prm[5], (float)prm[6]};
   evx_sbr_dev_ctrl(part.data_ptr<double>(), (int)nparts, (int)j, (int)K, hist.data_ptr<double>(), alpha.data_ptr<float>(),
@@ -1564,7 +1553,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("sbr16_far_out(Tensor A, Tensor perm, Tensor Q, Tensor dq, Tensor stats, float thr_fac, Tensor theta, Tensor(a!) X, int sb, Tensor skip) -> ()");
   m.def("sbr16_bq_out(Tensor B, Tensor perm, Tensor Q, Tensor(a!) Bq, int sb, Tensor skip) -> ()");
   m.def("sbr_damping_out(Tensor X2, Tensor V, float tau, Tensor(a!) alpha, Tensor(b!) work, Tensor skip, Tensor(c!)? bar=None, bool no_final=False, Tensor? xpart=None) -> ()");
-  m.def("sbr_dev_prep(Tensor X, Tensor X2, Tensor X3, Tensor(c!) alpha, Tensor(a!) P, Tensor(b!) MT, Tensor ctrl, Tensor? work=None, float tau=1.0, Tensor? xpart=None, Tensor? copy_src=None, Tensor(d!)? copy_dst=None, int minus_id=0, Tensor? xstat=None, float o2_thr=0.) -> ()");
+  m.def("sbr_dev_prep(Tensor X, Tensor X2, Tensor X3, Tensor(c!) alpha, Tensor(a!) P, Tensor(b!) MT, Tensor ctrl, Tensor? work=None, float tau=1.0, Tensor? xpart=None, Tensor? copy_src=None, Tensor(d!)? copy_dst=None, int minus_id=0) -> ()");
   m.def("sbr_dev_copy(Tensor src, Tensor(a!) dst, Tensor skip) -> ()");
   m.def("sbr_dev_ctrl(Tensor part, int nparts, int j, int K, Tensor(a!) hist, Tensor(b!) alpha, Tensor(c!) theta, Tensor(d!) ctrl, Tensor(e!) st, float[] prm, int ns_iters, Tensor A, Tensor(f!) w_out, Tensor(g!) eig_stats, Tensor(h!) w_init, Tensor(i!) log, Tensor(j!) log_count) -> ()");
   m.def("gemm_ks_set_tile(int t) -> ()");

@@ -283,8 +283,7 @@ void evx_linear_gp_fit(const double* a, const double* b, const double* c, const 
 // device-controlled SBR schedule (eigh_sbr_dev.hip)
 void evx_sbr_dev_prep(const float* X, const float* X2, const float* X3, int n, float* alpha, float* P, float* MT, const int* ctrl,
                       hipStream_t s, const float* V2 = nullptr, const float* V3 = nullptr,
-                      float tau = 1.f, const double* xpart = nullptr, int nparts = 0, const float* copy_src = nullptr, float* copy_dst = nullptr, int minus_id = 0,
-                      const double* xstat = nullptr, float o2_thr2 = 0.f, int* ctrl_w = nullptr);
+                      float tau = 1.f, const double* xpart = nullptr, int nparts = 0, const float* copy_src = nullptr, float* copy_dst = nullptr, int minus_id = 0);
 void evx_sbr_dev_copy(const float* src, float* dst, int64_t n, const int* skip, hipStream_t s);
 void evx_sbr_report(const double* stats, int* seq, double* ring, int R, hipStream_t s);
 void evx_sbr_dev_ctrl(const double* part, int nparts, int j, int K, double* hist, float* alpha, float* theta, int* ctrl, int* st,

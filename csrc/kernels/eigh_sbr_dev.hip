@@ -39,9 +39,8 @@
 
 namespace {
 
-// control words per refinement slot (the first 8 documented above; 8: skip the Vᵀ Taylor GEMM —
-// written by the prep kernel itself, see sbr_dev_prep_kernel)
-constexpr int kCW = 16;
+// control words per refinement slot (documented above)
+constexpr int kCW = 8;
 
 struct SbrDevParams {
   float tol, ns_kappa, damp_kappa, t4_kappa, near_only;
@@ -80,15 +79,8 @@ __global__ void __launch_bounds__(256) sbr_dev_prep_kernel(const float* __restri
                                                            const float* __restrict__ V2, const float* __restrict__ V3, float tau,
                                                            const double* __restrict__ xpart, int nparts,
                                                            const float* __restrict__ copy_src, float* __restrict__ copy_dst,
-                                                           int minus_id, const double* __restrict__ xstat, float o2_thr2, int* __restrict__ ctrl_w) {
-  // order 2 (round 6): when the generator's free bound proves ‖αX‖₂² ≤ o2_thr2, exp(αX) − I is
-  // taken as αX + ½α²X² — the truncation X³/6 is below 1e-9 of the basis and (I + X + X²/2) is
-  // orthogonal to ‖X‖⁴/4 — and the Vᵀ GEMM that adds the X²·Pᵀ Taylor terms is skipped (its
-  // skip word ctrl[8], read by that GEMM after this kernel): one 1000³ product fewer per settled
-  // refinement iteration.  Every workgroup runs the bound (a block-wide reduction); block 0 writes
-  // the word.
+                                                           int minus_id) {
   if (ctrl[1]) {
-    if (ctrl_w && blockIdx.x == 0 && threadIdx.x == 0) ctrl_w[8] = 1;
     // no far step this iteration: a near-only iteration (ctrl[7] == 0) takes the block-rotated
     // basis Bq as the new basis — the copy runs here, in the launch the schedule makes anyway
     if (copy_src && ctrl[7] == 0) {
@@ -113,14 +105,6 @@ __global__ void __launch_bounds__(256) sbr_dev_prep_kernel(const float* __restri
   }
   if (xpart || (V2 && ctrl[2] == 0)) {
     if (blockIdx.x == 0 && threadIdx.x == 0) alpha[0] = a;
-  }
-  if (ctrl_w) {
-    bool o2 = false;
-    if (xstat && !six) {
-      const float2 b = evx_sbr_xbounds(xstat, nparts, n);
-      o2 = a * a * b.y <= o2_thr2;
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0) ctrl_w[8] = o2 ? 1 : 0;
   }
 
   const float a2 = a * a, a3 = a2 * a;
@@ -391,14 +375,14 @@ void evx_sbr_report(const double* stats, int* seq, double* ring, int R, hipStrea
 
 void evx_sbr_dev_prep(const float* X, const float* X2, const float* X3, int n, float* alpha, float* P, float* MT, const int* ctrl,
                       hipStream_t s, const float* V2, const float* V3, float tau, const double* xpart, int nparts, const float* copy_src,
-                      float* copy_dst, int minus_id, const double* xstat, float o2_thr2, int* ctrl_w) {
+                      float* copy_dst, int minus_id) {
   // a grid-stride loop over 256 workgroups: the schedule skips this kernel in most
   // iterations, and an empty launch costs in proportion to its workgroup count
   const int64_t total = (int64_t)n * n;
   int g = (int)((total + 255) / 256);
   if (g > 256) g = 256;
   sbr_dev_prep_kernel<<<g, 256, 0, s>>>(X, X2, X3, n, alpha, P, MT, ctrl, V2, V3, tau, xpart, nparts, copy_src, copy_dst,
-                                        minus_id, xstat, o2_thr2, ctrl_w);
+                                        minus_id);
 }
 
 void evx_sbr_dev_copy(const float* src, float* dst, int64_t n, const int* skip, hipStream_t s) {

@@ -122,9 +122,10 @@ class CMAES(Algorithm):
 
     # ------------------------------------------------------------------ eigensolver schedule
     # The device eigensolver runs a fixed number of refinement slots per generation (a skipped
-    # slot still costs its launch boundaries), in three captured graph variants: "cold"
-    # (sbr_cold_iters slots — the first solves from C = I need 10-12 iterations), None (the warm
-    # schedule, sbr_device_iters) and "late" (sbr_late_iters, lean: settled solves take 4).
+    # slot still costs its launch boundaries — ≈10 kernels, ≈45 µs in graph replay), in four captured
+    # graph variants: "cold" (sbr_cold_iters slots — the first solves from C = I need 10-12
+    # iterations), None (the warm schedule, sbr_device_iters), "warm6" (one slot fewer: most warm
+    # solves take 5) and "late" (sbr_late_iters, lean: settled solves take 4).
     # Which one a generation replays is chosen from MEASURED convergence, not from the
     # generation index (round 6; round 5 switched at fixed generations 4 and 24 tuned on one
     # trajectory):
@@ -141,7 +142,8 @@ class CMAES(Algorithm):
     #   level it ran at (the "first slow solve" rule);
     # * DOWN_STREAK consecutive solves at the current level that would have fitted the next
     #   shorter schedule with one slot to spare move it one level down.
-    LEVELS = ("late", None, "cold")
+    LEVELS = ("late", "warm6", None, "cold")
+    TOP = len(LEVELS) - 1
     ESC_LAG = 2
     ESC_RING = 16
     DOWN_STREAK = 2
@@ -156,7 +158,7 @@ class CMAES(Algorithm):
     def _sched_fresh():
         from collections import deque
 
-        return {"level": 2, "streak": 0, "enqueued": 0, "checked": -1, "pending": deque(), "last": 2, "escalations": 0,
+        return {"level": CMAES.TOP, "streak": 0, "enqueued": 0, "checked": -1, "pending": deque(), "last": CMAES.TOP, "escalations": 0,
                 "history": [], "levels": []}
 
     def _sched_reset(self):
@@ -170,7 +172,7 @@ class CMAES(Algorithm):
     def _level_slots(self, level: int) -> int:
         from ....ops.sbr_device import schedule_iters
 
-        return schedule_iters(self.dim, ("late", "warm", "cold")[level])
+        return schedule_iters(self.dim, ("late", "warm6", "warm", "cold")[level])
 
     def graph_variant(self, generation: int):
         """The eigensolver schedule of the next step (see the class comment above): one of
@@ -242,7 +244,7 @@ class CMAES(Algorithm):
         del sc["history"][:-64]
         level = sc["level"]
         if capped or iters >= self._level_slots(lvl):
-            up = min(lvl + 1, 2)
+            up = min(lvl + 1, self.TOP)
             if capped:
                 sc["escalations"] += 1
         elif iters >= self._level_slots(level):
@@ -263,16 +265,16 @@ class CMAES(Algorithm):
         return int(self._sched()["escalations"])
 
     def schedule_levels(self, last: int = None) -> str:
-        """The schedule each recent step replayed: L (late), W (warm), C (cold)."""
+        """The schedule each recent step replayed: L (late), V (warm, one slot fewer), W (warm), C (cold)."""
         lv = self._sched()["levels"]
         lv = lv if last is None else lv[-int(last):]
-        return "".join("LWC"[v] for v in lv)
+        return "".join("LVWC"[v] for v in lv)
 
     def graph_variant_context(self, variant):
         """The eigensolver schedule of a graph variant (ops/sbr_device.py: ``schedule``): "cold"
         — every slot full, bounds-gated damping; None — the warm schedule (lean tail slots);
         "late" — settled solves: damping / Newton–Schulz / order-6 kernels in the first slots only."""
-        if variant in ("cold", "late"):
+        if variant in ("cold", "late", "warm6"):
             from ....ops.sbr_device import use_schedule
 
             return use_schedule(variant)

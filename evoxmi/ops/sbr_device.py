@@ -61,11 +61,7 @@ LATE_FULL_SLOTS = 3  # late schedule: damping / NS / order-6 kernels in slots 0-
 LATE_DAMP_SLOTS = 1  # late schedule: the damping power steps in slot 0 only (89 launches / generation)
 LATE_NS_ITERS = 2    # forced Newton–Schulz steps per late solve (1: trajectory parity 5.8 % > 5 % bound)
 LEAN_MAX_N = 1024    # larger matrices keep every slot full (d = 2000 capped in a lean slot)
-# order-2 steps (round 6): a far step whose generator is proven small (‖αX‖₂ ≤ 2e-3 from the X²
-# GEMM's free bound) takes exp(αX) − I ≈ αX + ½α²X² — truncation ≤ 1.4e-9, orthogonal to
-# ‖X‖⁴/4 — and skips the Taylor Vᵀ GEMM (0 disables)
-ORDER2_THR = 2e-3
-CW = 16              # control words per slot (eigh_sbr_dev.hip kCW)
+CW = 8               # control words per slot (eigh_sbr_dev.hip kCW)
 LARGE_N_ITERS = 8    # ... and get at least 8 slots (7 capped one d = 2000 solve)
 
 
@@ -85,15 +81,20 @@ class Schedule:
 
 def schedule(level: str, n: int) -> Schedule:
     """The schedule of a CMA-ES graph variant: ``"cold"`` (every slot full, bounds-gated
-    damping), ``"warm"`` or ``"late"`` (lean tail slots) at matrix order ``n``."""
+    damping), ``"warm"``, ``"warm6"`` (one slot fewer) or ``"late"`` (lean tail slots) at matrix
+    order ``n``."""
     from .. import config
 
     if level == "cold":
         return Schedule(int(config.get("sbr_cold_iters")), None, None, DEVICE_CFG["ns_iters"], True)
     late = level == "late"
     iters = int(config.get("sbr_late_iters" if late else "sbr_device_iters"))
+    if level == "warm6":  # the warm schedule with one slot fewer
+        iters = max(iters - 1, int(config.get("sbr_late_iters")))
     if n > LEAN_MAX_N:
         return Schedule(max(iters, LARGE_N_ITERS), None, None, DEVICE_CFG["ns_iters"], False)
+    if iters >= int(config.get("sbr_cold_iters")):  # a schedule as long as the cold one keeps every slot full
+        return Schedule(iters, None, None, DEVICE_CFG["ns_iters"], False)
     if late:
         return Schedule(iters, LATE_FULL_SLOTS, LATE_DAMP_SLOTS, LATE_NS_ITERS, False)
     return Schedule(iters, FULL_SLOTS, None, DEVICE_CFG["ns_iters"], False)
@@ -147,10 +148,12 @@ class DeviceSBR:
         self.dq = torch.zeros(n, device=dev)
         self.nparts = int(ops.gemm_ks_grid(n, n, 1))
         self.part = torch.zeros(4 * self.nparts, dtype=torch.float64, device=dev)
-        # stats partials of X² = −X·Xᵀ (its diagonal): free bounds of ‖X‖₂ — they gate the damping's
-        # power iteration in the cold schedule (xgate) and choose order-2 steps in every schedule
+        # stats partials of X² = −X·Xᵀ (its diagonal): free bounds of ‖X‖₂ that gate the damping's
+        # power iteration in the cold schedule (xgate).  (Round 6 also tried them to choose order-2
+        # steps — exp(αX) − I ≈ αX + ½α²X² below ‖αX‖₂ ≤ 2e-3 — but settled solves' generators are
+        # 0.02-1.2 in 2-norm (tools/xnorm_probe.py): it never fired; removed.)
         self.xgate = bool(xgate)
-        self.part2 = torch.zeros(4 * self.nparts, dtype=torch.float64, device=dev)
+        self.part2 = torch.zeros(4 * self.nparts, dtype=torch.float64, device=dev) if self.xgate else None
         K = self.K
         self.hist = torch.zeros(4 * (K + 1), dtype=torch.float64, device=dev)
         self.alpha = torch.ones(K + 1, device=dev)
@@ -169,7 +172,13 @@ class DeviceSBR:
         # (bf16x6); the products that only form a correction of an exactly held matrix —
         # X², X³ and the Taylor terms of exp(αX) − I, the basis update Bq + Bq·(V − I), and
         # Newton–Schulz's T − ½T·(TᵀT − I) — run at bf16x3 (≈1e-5 of the correction's own size)
-        self.corr = "x3" if config.get("sbr_corr_prec") == "x3" else None
+        cp = config.get("sbr_corr_prec")
+        # "x3": the Taylor terms of exp(αX) − I only (X², X³, Vᵀ); "x3all": also the basis update and
+        # the Newton–Schulz correction (measured: moved tests/test_eigh_sbr.py's 5-seed trajectory-parity
+        # statistic to 5.2 % against its 5 % bound on seeds 7-11, 0.4 % / 1.9 % on seeds 12-16 / 17-21,
+        # x6 2.6 / 0.9 / 2.3 % — profiles/r6_parity_seed_sets.jsonl)
+        self.corr = "x3" if cp in ("x3", "x3all") else None
+        self.corr_basis = "x3" if cp == "x3all" else None
         self.prm = [float(cfg.tol), float(cfg.ns_kappa), float(cfg.damp_kappa), float(cfg.t4_kappa), float(cfg.near_only),
                     float(cfg.theta0), float(cfg.theta_kappa), float(self.lean_from), float(RECOVER),
                     float(LEAN_GUARD), float(self.xgate), float(self.damp_from)]
@@ -193,7 +202,7 @@ class DeviceSBR:
         cfg = self.cfg
         sb = cfg.block
         c = self.ctrl[CW * j : CW * j + CW]
-        sk_all, sk_far, sk_damp, sk_x3, sel6, sk_ns, sel_ns, sk_copy, sk_vt = (c[i : i + 1] for i in range(9))
+        sk_all, sk_far, sk_damp, sk_x3, sel6, sk_ns, sel_ns, sk_copy = (c[i : i + 1] for i in range(8))
         shift = (j % 2) * (sb // 2)
         full = j < self.lean_from
         damp_slot = j < self.damp_from
@@ -209,7 +218,7 @@ class DeviceSBR:
             # three power-step launches (they return at once when the free Frobenius bound already
             # gives α = 1); α itself is formed by the prep kernel below (no_final)
             ops.sbr_damping_out(self.X2, self.V, float(cfg.damp_tau), self.alpha[j + 1 : j + 2], self.work, sk_damp, None, True,
-                                self.part2 if self.xgate else None)
+                                self.part2)
         if full:
             # order 6 only: X³ = X²·X = −X²·Xᵀ (skew)
             mm(self.X2, self.X, tb=True, mode=2, alpha=-1.0, out=self.X3, skip=sk_x3, prec=corr)
@@ -217,24 +226,22 @@ class DeviceSBR:
         # near-only iterations (no far step): the block-rotated basis is the new basis — Bq → B
         # copied by this launch (it returns at once otherwise), no copy launch of its own
         ops.sbr_dev_prep(self.X, self.X2, self.X3, self.alpha[j + 1 : j + 2], self.P, self.VT, c, self.work if damp_here else None,
-                         float(cfg.damp_tau), self.part2 if self.xgate else None, self.Bq, self.B, int(corr is not None),
-                         self.part2 if ORDER2_THR > 0 else None, float(ORDER2_THR))
+                         float(cfg.damp_tau), self.part2, self.Bq, self.B, int(corr is not None))
         # Vᵀ = M(−α) + X²·Pᵀ (order 4) or M(−α) − X³·Pᵀ (order 6): the control word selects
-        # (with the tiered precision the prep wrote M − I, so this is Vᵀ − I); skipped (sk_vt,
-        # written by the prep) for a near-only iteration or an order-2 step
-        mm(self.X2, self.P, tb=True, alpha=1.0, beta=1.0, Cin=self.VT, out=self.VT, skip=sk_vt if ORDER2_THR > 0 else sk_far, sel=sel6,
-           A2=self.X3, alpha2=-1.0, prec=corr)
+        # (with the tiered precision the prep wrote M − I, so this is Vᵀ − I)
+        mm(self.X2, self.P, tb=True, alpha=1.0, beta=1.0, Cin=self.VT, out=self.VT, skip=sk_far, sel=sel6, A2=self.X3, alpha2=-1.0,
+           prec=corr)
         # B·V → B, or into T when Newton–Schulz follows
         if corr is not None:
-            # Bq + Bq·(V − I): the exact basis plus an x3 correction product
-            mm(self.Bq, self.VT, tb=True, beta=1.0, Cin=self.Bq, out=self.B, skip=sk_far, sel=sel_ns, C2=self.T, prec=corr)
+            # Bq + Bq·(V − I): the exact basis plus a correction product
+            mm(self.Bq, self.VT, tb=True, beta=1.0, Cin=self.Bq, out=self.B, skip=sk_far, sel=sel_ns, C2=self.T, prec=self.corr_basis)
         else:
             mm(self.Bq, self.VT, tb=True, out=self.B, skip=sk_far, sel=sel_ns, C2=self.T)
         if full:
             if corr is not None:
                 # E = TᵀT − I at full precision (the orthogonality residual), then T − ½T·E
                 mm(self.T, self.T, ta=True, mode=1, out=self.G, skip=sk_ns, diag_add=-1.0)
-                mm(self.T, self.G, tb=True, alpha=-0.5, beta=1.0, Cin=self.T, out=self.B, skip=sk_ns, prec=corr)
+                mm(self.T, self.G, tb=True, alpha=-0.5, beta=1.0, Cin=self.T, out=self.B, skip=sk_ns, prec=self.corr_basis)
             else:
                 mm(self.T, self.T, ta=True, mode=1, out=self.G, skip=sk_ns)
                 mm(self.T, self.G, tb=True, alpha=-0.5, beta=1.5, Cin=self.T, out=self.B, skip=sk_ns)

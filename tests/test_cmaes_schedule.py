@@ -42,17 +42,19 @@ def _run(a, solves):
 
 def test_schedule_starts_cold_and_moves_down_on_measured_convergence():
     a = _algo()
-    cold, warm, late = (a._level_slots(l) for l in (2, 1, 0))
-    assert (late, warm, cold) == (config.get("sbr_late_iters"), config.get("sbr_device_iters"), config.get("sbr_cold_iters"))
+    cold, warm, warm6, late = (a._level_slots(l) for l in (3, 2, 1, 0))
+    assert (late, warm6, warm, cold) == (config.get("sbr_late_iters"), config.get("sbr_device_iters") - 1, config.get("sbr_device_iters"),
+                                         config.get("sbr_cold_iters"))
     # cold-start solves need 10-12 iterations, then 5-6 (fit warm), then 4 (fit late)
     solves = [(12, False), (10, False), (6, False), (6, False), (6, False), (5, False), (5, False)] + [(4, False)] * 10
     lv = _run(a, solves)
-    assert lv[0] == 2 and lv[1] == 2
-    first_warm = lv.index(1)
+    assert lv[0] == 3 and lv[1] == 3
+    first_warm = lv.index(2)
     # two consecutive cold solves with ≤ warm − 1 iterations, read two steps late
     assert first_warm == 2 + 2 + 1
     first_late = lv.index(0)
     assert first_late > first_warm and all(v == 0 for v in lv[first_late:])
+    assert 1 in lv[first_warm:first_late]  # through the one-slot-shorter warm schedule
     assert a.schedule_escalations == 0
 
 
@@ -65,7 +67,7 @@ def test_capped_late_solve_escalates_once_and_slow_solve_returns_to_warm():
     # solve 3 capped at the late level → warm from step 3 + ESC_LAG on; the two capped solves
     # still in flight at the late level do not push it to cold
     assert lv[:5] == [0, 0, 0, 0, 0]
-    assert lv[5] == 1 and max(lv) == 1
+    assert lv[5] == 1 and max(lv) == 1  # one level up: the shorter warm schedule
     assert a.schedule_escalations == 2
     # a solve that converged only in the late schedule's last slot also moves the run up
     b = _algo()
@@ -80,4 +82,4 @@ def test_new_run_restarts_the_schedule():
     a._sched()["level"] = 0
     a.setup(torch.zeros(2, dtype=torch.int64))
     sc = a._sched()
-    assert sc["level"] == 2 and sc["enqueued"] == 0 and not sc["pending"] and a.schedule_escalations == 0
+    assert sc["level"] == CMAES.TOP and sc["enqueued"] == 0 and not sc["pending"] and a.schedule_escalations == 0
