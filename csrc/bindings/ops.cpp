@@ -518,8 +518,21 @@ void sbr_dev_copy(const at::Tensor& src, at::Tensor& dst, const at::Tensor& skip
 
 void sbr_dev_ctrl(const at::Tensor& part, int64_t nparts, int64_t j, int64_t K, at::Tensor& hist, at::Tensor& alpha, at::Tensor& theta,
                   at::Tensor& ctrl, at::Tensor& st, std::vector<double> prm, int64_t ns_iters, const at::Tensor& A, at::Tensor& w_out,
-                  at::Tensor& eig_stats, at::Tensor& w_init, at::Tensor& log, at::Tensor& log_count) {
+                  at::Tensor& eig_stats, at::Tensor& w_init, at::Tensor& log, at::Tensor& log_count,
+                  const c10::optional<at::Tensor>& rep_seq, const c10::optional<at::Tensor>& rep_ring) {
   TORCH_CHECK(log.scalar_type() == at::kDouble && log.is_contiguous() && log_count.scalar_type() == at::kInt, "sbr_dev_ctrl: log");
+  int* rs = nullptr;
+  double* rr = nullptr;
+  int rl = 0;
+  if (rep_seq.has_value() && rep_seq->defined()) {  // the last slot also reports into the host-mapped ring
+    TORCH_CHECK(rep_seq->is_cuda() && rep_seq->scalar_type() == at::kInt && rep_seq->numel() >= 1, "sbr_dev_ctrl: device int32 counter");
+    TORCH_CHECK(rep_ring.has_value() && !rep_ring->is_cuda() && rep_ring->is_pinned() && rep_ring->scalar_type() == at::kDouble &&
+                    rep_ring->is_contiguous() && rep_ring->dim() == 2 && rep_ring->size(1) == 5,
+                "sbr_dev_ctrl: pinned host float64 [R, 5] ring");
+    rs = rep_seq->data_ptr<int>();
+    rr = rep_ring->data_ptr<double>();
+    rl = (int)rep_ring->size(0);
+  }
   TORCH_CHECK(prm.size() >= 8, "sbr_dev_ctrl: params [tol, ns_kappa, damp_kappa, t4_kappa, near_only, theta0, theta_kappa, lean_from, (recover, lean_guard, xgate, damp_from)]");
   TORCH_CHECK(hist.scalar_type() == at::kDouble && hist.numel() >= 4 * (K + 1) && ctrl.numel() >= 8 * K && alpha.numel() >= K + 1 &&
                   theta.numel() >= K && st.numel() >= 8 && part.numel() >= 4 * nparts, "sbr_dev_ctrl: buffers");
@@ -529,7 +542,7 @@ void sbr_dev_ctrl(const at::Tensor& part, int64_t nparts, int64_t j, int64_t K, 
                    (int)A.size(0), w_out.data_ptr<float>(), eig_stats.data_ptr<double>(), w_init.data_ptr<float>(),
                    log.data_ptr<double>(), (int)(log.numel() / 4), log_count.data_ptr<int>(), cur_stream(), (int)prm[7],
                    prm.size() > 8 ? (int)prm[8] : 0, prm.size() > 9 ? (int)prm[9] : 0, prm.size() > 10 ? (int)prm[10] : 0,
-                   prm.size() > 11 ? (int)prm[11] : -1);
+                   prm.size() > 11 ? (int)prm[11] : -1, rs, rr, rl);
 }
 
 std::vector<at::Tensor> argsort_f32(const at::Tensor& keys, int64_t descending) {
@@ -1372,7 +1385,8 @@ std::vector<at::Tensor> cma_delta_gemv(const at::Tensor& M, const at::Tensor& me
 }
 
 std::vector<at::Tensor> cma_paths(const at::Tensor& ps, const at::Tensor& pc, const at::Tensor& y, const at::Tensor& delta,
-                                  const at::Tensor& sigma, const at::Tensor& count_iter, std::vector<double> consts) {
+                                  const at::Tensor& sigma, const at::Tensor& count_iter, std::vector<double> consts,
+                                  const c10::optional<at::Tensor>& count_eigen) {
   for (auto* t : {&ps, &pc, &y, &delta, &sigma}) { CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t); }
   CHECK_DEV(count_iter);
   TORCH_CHECK(count_iter.scalar_type() == at::kLong && count_iter.numel() == 1 && sigma.numel() == 1, "cma_paths: scalars");
@@ -1384,9 +1398,20 @@ std::vector<at::Tensor> cma_paths(const at::Tensor& ps, const at::Tensor& pc, co
   for (int i = 0; i < 9; ++i) k[i] = (float)consts[i];
   auto pso = at::empty_like(ps), pco = at::empty_like(pc);
   auto so = at::empty_like(sigma), ao = at::empty_like(sigma), ho = at::empty_like(sigma);
+  // count_eigen given: the kernel also advances both generation counters (returned as two more tensors)
+  const bool adv = count_eigen.has_value() && count_eigen->defined();
+  at::Tensor ci, ce;
+  if (adv) {
+    CHECK_DEV(*count_eigen);
+    TORCH_CHECK(count_eigen->scalar_type() == at::kLong && count_eigen->numel() == 1, "cma_paths: count_eigen int64 scalar");
+    ci = at::empty_like(count_iter);
+    ce = at::empty_like(*count_eigen);
+  }
   evx_cma_paths(ps.data_ptr<float>(), pc.data_ptr<float>(), y.data_ptr<float>(), delta.data_ptr<float>(), sigma.data_ptr<float>(),
                 count_iter.data_ptr<int64_t>(), (int)d, k, pso.data_ptr<float>(), pco.data_ptr<float>(), so.data_ptr<float>(),
-                ao.data_ptr<float>(), ho.data_ptr<float>(), cur_stream());
+                ao.data_ptr<float>(), ho.data_ptr<float>(), cur_stream(), adv ? count_eigen->data_ptr<int64_t>() : nullptr,
+                adv ? ci.data_ptr<int64_t>() : nullptr, adv ? ce.data_ptr<int64_t>() : nullptr);
+  if (adv) return {pso, pco, so, ao, ho, ci, ce};
   return {pso, pco, so, ao, ho};
 }
 
@@ -1555,7 +1580,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("sbr_damping_out(Tensor X2, Tensor V, float tau, Tensor(a!) alpha, Tensor(b!) work, Tensor skip, Tensor(c!)? bar=None, bool no_final=False, Tensor? xpart=None) -> ()");
   m.def("sbr_dev_prep(Tensor X, Tensor X2, Tensor X3, Tensor(c!) alpha, Tensor(a!) P, Tensor(b!) MT, Tensor ctrl, Tensor? work=None, float tau=1.0, Tensor? xpart=None, Tensor? copy_src=None, Tensor(d!)? copy_dst=None, int minus_id=0) -> ()");
   m.def("sbr_dev_copy(Tensor src, Tensor(a!) dst, Tensor skip) -> ()");
-  m.def("sbr_dev_ctrl(Tensor part, int nparts, int j, int K, Tensor(a!) hist, Tensor(b!) alpha, Tensor(c!) theta, Tensor(d!) ctrl, Tensor(e!) st, float[] prm, int ns_iters, Tensor A, Tensor(f!) w_out, Tensor(g!) eig_stats, Tensor(h!) w_init, Tensor(i!) log, Tensor(j!) log_count) -> ()");
+  m.def("sbr_dev_ctrl(Tensor part, int nparts, int j, int K, Tensor(a!) hist, Tensor(b!) alpha, Tensor(c!) theta, Tensor(d!) ctrl, Tensor(e!) st, float[] prm, int ns_iters, Tensor A, Tensor(f!) w_out, Tensor(g!) eig_stats, Tensor(h!) w_init, Tensor(i!) log, Tensor(j!) log_count, Tensor(k!)? rep_seq=None, Tensor(l!)? rep_ring=None) -> ()");
   m.def("gemm_ks_set_tile(int t) -> ()");
   m.def("gemm_ks_set_prec(int prec) -> ()");
   m.def("gemm_ks_set_nw8(int tiles) -> ()");
@@ -1567,7 +1592,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("cma_local_select(Tensor order, int mu, Tensor w, int start, int size, Tensor(a!) rows, Tensor(b!) wk) -> ()");
   m.def("sym_pack(Tensor S, Tensor(a!) P) -> ()");
   m.def("sym_unpack(Tensor P, Tensor(a!) S) -> ()");
-  m.def("cma_paths(Tensor ps, Tensor pc, Tensor y, Tensor delta, Tensor sigma, Tensor count_iter, float[] consts) -> Tensor[]");
+  m.def("cma_paths(Tensor ps, Tensor pc, Tensor y, Tensor delta, Tensor sigma, Tensor count_iter, float[] consts, Tensor? count_eigen=None) -> Tensor[]");
   m.def("cma_cov_pad(Tensor C, Tensor S, Tensor pc, Tensor a, float c1, float cmu, Tensor Bprev, int np, Tensor? Cn_out=None, bool want_bp=True) -> Tensor[]");
   m.def("cma_eig_out(Tensor Bp, Tensor w, int d, Tensor? B_out=None) -> Tensor[]");
   m.def("nsga_select(Tensor rank, Tensor f, int N, int mask_pos) -> Tensor");

@@ -22,26 +22,13 @@ void copy_d2h_async(const at::Tensor& src, at::Tensor& dst) {
   TORCH_CHECK(st == hipSuccess, "copy_d2h_async: ", hipGetErrorString(st));
 }
 
-// a device solve's stats into a host-mapped pinned ring (see eigh_sbr_dev.hip: sbr_report_kernel)
-void sbr_report(const at::Tensor& stats, at::Tensor& seq, at::Tensor& ring) {
-  TORCH_CHECK(stats.is_cuda() && stats.scalar_type() == at::kDouble && stats.numel() >= 4, "sbr_report: device float64[4] stats");
-  TORCH_CHECK(seq.is_cuda() && seq.scalar_type() == at::kInt && seq.numel() >= 1, "sbr_report: device int32 counter");
-  TORCH_CHECK(!ring.is_cuda() && ring.is_pinned() && ring.scalar_type() == at::kDouble && ring.is_contiguous() && ring.dim() == 2 &&
-                  ring.size(1) == 5,
-              "sbr_report: pinned host float64 [R, 5] ring");
-  c10::DeviceGuard g(stats.device());
-  evx_sbr_report(stats.data_ptr<double>(), seq.data_ptr<int>(), ring.data_ptr<double>(), (int)ring.size(0),
-                 c10::hip::getCurrentHIPStream().stream());
-}
 
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(evoxmi, m) {
   m.def("copy_d2h_async(Tensor src, Tensor(a!) dst) -> ()");
-  m.def("sbr_report(Tensor stats, Tensor(a!) seq, Tensor(b!) ring) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(evoxmi, CompositeExplicitAutograd, m) {
   m.impl("copy_d2h_async", &copy_d2h_async);
-  m.impl("sbr_report", &sbr_report);
 }

@@ -231,7 +231,8 @@ void evx_cma_delta_gemv(const float* M, const float* mean, const float* dm, floa
                         hipStream_t s);
 void evx_cma_paths(const float* ps, const float* pc, const float* y, const float* delta, const float* sigma, const int64_t* count_iter,
                    int d, const float* consts, float* ps_out, float* pc_out, float* sigma_out, float* a_out, float* hsig_out,
-                   hipStream_t s);
+                   hipStream_t s,
+                   const int64_t* count_eigen = nullptr, int64_t* count_iter_out = nullptr, int64_t* count_eigen_out = nullptr);
 void evx_cma_cov_pad(const float* C, const float* S, const float* pc, const float* a, float c1, float cmu, const float* Bprev, int d,
                      int np, float* Cn, float* Cp, float* Bp, hipStream_t s);
 void evx_cma_eig_out(const float* Bp, const float* w, int d, int np, float* B, float* D, float* BdivD, hipStream_t s);
@@ -285,10 +286,9 @@ void evx_sbr_dev_prep(const float* X, const float* X2, const float* X3, int n, f
                       hipStream_t s, const float* V2 = nullptr, const float* V3 = nullptr,
                       float tau = 1.f, const double* xpart = nullptr, int nparts = 0, const float* copy_src = nullptr, float* copy_dst = nullptr, int minus_id = 0);
 void evx_sbr_dev_copy(const float* src, float* dst, int64_t n, const int* skip, hipStream_t s);
-void evx_sbr_report(const double* stats, int* seq, double* ring, int R, hipStream_t s);
 void evx_sbr_dev_ctrl(const double* part, int nparts, int j, int K, double* hist, float* alpha, float* theta, int* ctrl, int* st,
                       const float* prm6, int ns_iters, const float* A, int64_t lda, int n, float* w_out, double* eig_stats, float* w_init,
-                      double* log, int log_len, int* log_count, hipStream_t s, int lean_from = 1 << 30, int recover = 0, int lean_guard = 0, int xgate = 0, int damp_from = -1);
+                      double* log, int log_len, int* log_count, hipStream_t s, int lean_from = 1 << 30, int recover = 0, int lean_guard = 0, int xgate = 0, int damp_from = -1, int* rep_seq = nullptr, double* rep_ring = nullptr, int rep_len = 0);
 // far generator + Bq in one launch (skip_far / skip_bq: their control words)
 void evx_sbr16_far_bq(const float* A, int n, int64_t lda, const int* perm, const float* Q, const float* dq, const double* stats,
                       float thr_fac, const float* theta_ptr, float* X, int64_t ldx, const float* B, int rows, int64_t ldb, float* Bq,

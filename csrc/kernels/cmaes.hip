@@ -55,7 +55,9 @@ __global__ void __launch_bounds__(1024) paths_kernel(const float* __restrict__ p
                                                      const float* __restrict__ y, const float* __restrict__ delta,
                                                      const float* __restrict__ sigma, const int64_t* __restrict__ count_iter, int d,
                                                      PathConsts k, float* __restrict__ ps_out, float* __restrict__ pc_out,
-                                                     float* __restrict__ sigma_out, float* __restrict__ a_out, float* __restrict__ hsig_out) {
+                                                     float* __restrict__ sigma_out, float* __restrict__ a_out, float* __restrict__ hsig_out,
+                                                     const int64_t* __restrict__ count_eigen, int64_t* __restrict__ count_iter_out,
+                                                     int64_t* __restrict__ count_eigen_out) {
   __shared__ float scratch[16];
   const float s = sigma[0];
   const float inv_s = 1.f / s;
@@ -66,13 +68,21 @@ __global__ void __launch_bounds__(1024) paths_kernel(const float* __restrict__ p
     nrm2 += v * v;
   }
   const float nrm = sqrtf(block_sum(nrm2, scratch));
-  const float count = (float)count_iter[0];
+  // with count_iter_out the generation counters advance here (count_iter + 1 used for this
+  // generation, as the reference's ask would have left it; count_eigen + 1): two one-element add
+  // launches fewer per captured generation
+  const int64_t cnt = count_iter[0] + (count_iter_out ? 1 : 0);
+  const float count = (float)cnt;
   const float hs = (nrm / sqrtf(1.f - powf(1.f - k.cs, 2.f * count)) < k.hs_thresh) ? 1.f : 0.f;
   for (int i = threadIdx.x; i < d; i += blockDim.x) pc_out[i] = (1.f - k.cc) * pc[i] + hs * k.c_pc * delta[i] * inv_s;
   if (threadIdx.x == 0) {
     sigma_out[0] = s * expf((k.cs / k.damps) * (nrm / k.chiN - 1.f));
     a_out[0] = (1.f - k.c1 - k.cmu) + k.c1 * (1.f - hs) * k.cc * (2.f - k.cc);
     hsig_out[0] = hs;
+    if (count_iter_out) {
+      count_iter_out[0] = cnt;
+      count_eigen_out[0] = count_eigen[0] + 1;
+    }
   }
 }
 
@@ -240,9 +250,10 @@ void evx_cma_delta_gemv(const float* M, const float* mean, const float* dm, floa
 
 void evx_cma_paths(const float* ps, const float* pc, const float* y, const float* delta, const float* sigma, const int64_t* count_iter,
                    int d, const float* consts, float* ps_out, float* pc_out, float* sigma_out, float* a_out, float* hsig_out,
-                   hipStream_t s) {
+                   hipStream_t s, const int64_t* count_eigen, int64_t* count_iter_out, int64_t* count_eigen_out) {
   PathConsts k{consts[0], consts[1], consts[2], consts[3], consts[4], consts[5], consts[6], consts[7], consts[8]};
-  paths_kernel<<<1, 1024, 0, s>>>(ps, pc, y, delta, sigma, count_iter, d, k, ps_out, pc_out, sigma_out, a_out, hsig_out);
+  paths_kernel<<<1, 1024, 0, s>>>(ps, pc, y, delta, sigma, count_iter, d, k, ps_out, pc_out, sigma_out, a_out, hsig_out, count_eigen,
+                                  count_iter_out, count_eigen_out);
 }
 
 void evx_cma_cov_pad(const float* C, const float* S, const float* pc, const float* a, float c1, float cmu, const float* Bprev, int d,

@@ -176,7 +176,8 @@ __global__ void __launch_bounds__(256) sbr_dev_ctrl_kernel(const double* __restr
                                                            SbrDevParams prm, const float* __restrict__ A, int64_t lda, int n,
                                                            float* __restrict__ w_out, double* __restrict__ eig_stats,
                                                            float* __restrict__ w_init, double* __restrict__ log, int log_len,
-                                                           int* __restrict__ log_count) {
+                                                           int* __restrict__ log_count, int* __restrict__ rep_seq, double* rep_ring,
+                                                           int rep_len) {
   __shared__ double s[4][4];
   __shared__ int s_keep;
   const int t = threadIdx.x;
@@ -330,7 +331,10 @@ __global__ void __launch_bounds__(256) sbr_dev_ctrl_kernel(const double* __restr
       eig_stats[1] = (double)((conv ? 0 : 1) | ((st[7] & 1) ? 2 : 0) | ((st[7] & 2) ? 4 : 0) | ((st[7] & 4) ? 8 : 0));
       eig_stats[2] = (double)st[2];
       eig_stats[3] = fb ? 1.0 : 0.0;
-      st[5] = fb ? 0 : 1;  // keep: the restore copy is skipped unless the refinement diverged
+      // keep: the restore copy (warm-start basis → output) is skipped unless the refinement
+      // diverged or no iteration ran at all (the solve then never wrote its output basis: the
+      // warm start is read directly by the first BᵀCB and the first iteration, no copy launch)
+      st[5] = (fb || st[2] == 0) ? 0 : 1;
       if (log && log_len > 0) {  // per-solve history ring (read by benches after the timed loop)
         const int c = *log_count;
         double* o = log + 4 * (int64_t)(c % log_len);
@@ -339,6 +343,17 @@ __global__ void __launch_bounds__(256) sbr_dev_ctrl_kernel(const double* __restr
         o[2] = eig_stats[2];
         o[3] = eig_stats[3];
         *log_count = c + 1;
+      }
+      if (rep_seq) {  // the solve's health into the host-mapped ring (CMAES schedule; was sbr_report_kernel)
+        const int q = *rep_seq;
+        double* o = rep_ring + 5 * (int64_t)(q % rep_len);
+        o[0] = eig_stats[0];
+        o[1] = eig_stats[1];
+        o[2] = eig_stats[2];
+        o[3] = eig_stats[3];
+        o[4] = (double)q;
+        __threadfence_system();
+        *rep_seq = q + 1;
       }
     }
     s_keep = st[1] ? 0 : 1;
@@ -350,28 +365,7 @@ __global__ void __launch_bounds__(256) sbr_dev_ctrl_kernel(const double* __restr
   }
 }
 
-// the solve's stats → slot (seq mod R) of a host-mapped pinned ring [R][5] ([off_rel, status,
-// iterations, fallback, seq]), then seq + 1: the host reads the slot of the solve it needs
-// after that step's event completed (CMAES.graph_variant: a fixed lag, so the schedule choice
-// is deterministic).  One thread, vector stores.
-__global__ void sbr_report_kernel(const double* __restrict__ stats, int* __restrict__ seq, double* ring, int R) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  const int q = *seq;
-  double* o = ring + 5 * (int64_t)(q % R);
-  o[0] = stats[0];
-  o[1] = stats[1];
-  o[2] = stats[2];
-  o[3] = stats[3];
-  o[4] = (double)q;
-  __threadfence_system();
-  *seq = q + 1;
-}
-
 }  // namespace
-
-void evx_sbr_report(const double* stats, int* seq, double* ring, int R, hipStream_t s) {
-  sbr_report_kernel<<<1, 64, 0, s>>>(stats, seq, ring, R);
-}
 
 void evx_sbr_dev_prep(const float* X, const float* X2, const float* X3, int n, float* alpha, float* P, float* MT, const int* ctrl,
                       hipStream_t s, const float* V2, const float* V3, float tau, const double* xpart, int nparts, const float* copy_src,
@@ -395,9 +389,9 @@ void evx_sbr_dev_copy(const float* src, float* dst, int64_t n, const int* skip, 
 void evx_sbr_dev_ctrl(const double* part, int nparts, int j, int K, double* hist, float* alpha, float* theta, int* ctrl, int* st,
                       const float* prm6, int ns_iters, const float* A, int64_t lda, int n, float* w_out, double* eig_stats, float* w_init,
                       double* log, int log_len, int* log_count, hipStream_t s, int lean_from, int recover, int lean_guard, int xgate,
-                      int damp_from) {
+                      int damp_from, int* rep_seq, double* rep_ring, int rep_len) {
   SbrDevParams p{prm6[0], prm6[1], prm6[2], prm6[3], prm6[4], prm6[5], prm6[6], ns_iters, lean_from, recover, lean_guard, xgate,
                  damp_from < 0 ? lean_from : min(damp_from, lean_from)};
   sbr_dev_ctrl_kernel<<<1, 256, 0, s>>>(part, nparts, j, K, hist, alpha, theta, ctrl, st, p, A, lda, n, w_out, eig_stats, w_init, log,
-                                        log_len, log_count);
+                                        log_len, log_count, j + 1 == K ? rep_seq : nullptr, rep_ring, rep_len);
 }

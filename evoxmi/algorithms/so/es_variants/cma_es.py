@@ -203,13 +203,11 @@ class CMAES(Algorithm):
         while len(sc["pending"]) > self.ESC_RING // 2:
             sc["pending"].popleft()
 
-    def _stats_to_host(self, eig_stats: torch.Tensor) -> None:
-        """This solve's [off_rel, status, iterations, fallback] into a host-mapped pinned ring,
-        slot (solve index mod R), by one single-thread kernel (captured into the graph)."""
+    def _report_buffers(self, device):
+        """(device counter, host-mapped pinned ring) the solve's last control kernel writes its
+        [off_rel, status, iterations, fallback, seq] into (captured into the graph)."""
         from ....core import in_capture_warmup
 
-        if not eig_stats.is_cuda:
-            return
         if self.__dict__.get("_eig_ring") is None:
             # allocated by the eager step or the capture's warm-up, never inside a capture
             # (no host allocation while capturing; a counter zeroed inside the graph would be
@@ -217,12 +215,10 @@ class CMAES(Algorithm):
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("CMAES: the eigensolver report ring must exist before a graph capture")
             self._eig_ring = torch.full((self.ESC_RING, 5), -1.0, dtype=torch.float64).pin_memory()
-            self._eig_seq = torch.zeros(1, dtype=torch.int32, device=eig_stats.device)
+            self._eig_seq = torch.zeros(1, dtype=torch.int32, device=device)
         if in_capture_warmup():
-            return
-        from ....ops import _ext
-
-        _ext.ops().sbr_report(eig_stats, self._eig_seq, self._eig_ring)
+            return None
+        return self._eig_seq, self._eig_ring
 
     def _poll_eig_health(self, sc) -> None:
         target = sc["enqueued"] - self.ESC_LAG
@@ -310,10 +306,19 @@ class CMAES(Algorithm):
             return mm(z, BD, tb=True, alpha_ptr=state.sigma.reshape(1), bias_n=state.mean)
         return state.mean + state.sigma * (state.D * z) @ state.B.T
 
+    def _counts_in_tell(self, state) -> bool:
+        """The fused device tell advances count_iter (and count_eigen) inside its paths kernel —
+        two one-element launches fewer per generation; ask then leaves count_iter as it is (the
+        tell uses count_iter + 1, as the reference's ask would have set it)."""
+        return self._fused_epilogue_ok(state)
+
+    def _advance(self, state):
+        return state if self._counts_in_tell(state) else state.update(count_iter=state.count_iter + 1)
+
     def ask(self, state):
         key, sample_key = rnd.split(state.key)
         population = self._sample(state, sample_key, 0, self.pop_size)
-        return population, state.update(population=population, count_iter=state.count_iter + 1, key=key)
+        return population, self._advance(state).update(population=population, key=key)
 
     # ------------------------------------------------------------------ tell
     def _weighted_stats(self, state, population, order_i32, K: int, wvec, gather: bool, s_out=None):
@@ -368,8 +373,9 @@ class CMAES(Algorithm):
         mean, delta, y = ops.cma_delta_gemv(state.invsqrtC.contiguous(), state.mean.contiguous(), dm.contiguous(), float(self.cm))
         consts = [self.cs, math.sqrt(self.cs * (2 - self.cs) * self.mueff), self.cc, math.sqrt(self.cc * (2 - self.cc) * self.mueff),
                   self.chiN, self.damps, self.c1, self.cmu, (1.4 + 2 / (d + 1)) * self.chiN]
-        ps, pc, sigma, a, _hsig = ops.cma_paths(state.ps.contiguous(), state.pc.contiguous(), y, delta, state.sigma.reshape(1).contiguous(),
-                                                state.count_iter.reshape(1).contiguous(), consts)
+        ps, pc, sigma, a, _hsig, count_iter, count_eigen = ops.cma_paths(
+            state.ps.contiguous(), state.pc.contiguous(), y, delta, state.sigma.reshape(1).contiguous(), state.count_iter.reshape(1).contiguous(),
+            consts, state.count_eigen.reshape(1).contiguous())
         eig_stats = state.eig_stats
         # hipGraph: C' and B go straight into the captured state buffers (no write-back copy of
         # 8 MB per generation): cov_pad reads each C element only where it writes it, and the
@@ -388,14 +394,12 @@ class CMAES(Algorithm):
                     # generation's graph, no host read (ops/sbr_device.py)
                     from ....ops.sbr_device import eigh_device
 
-                    w, Bn, eig_stats = eigh_device(Cp[:d, :d], state.B)
+                    w, Bn, eig_stats = eigh_device(Cp[:d, :d], state.B, report=self._report_buffers(state.B.device))
                 else:
                     # host-orchestrated solve: a host phase between hipGraph segments
                     w, Bn, eig_stats = host_phase(sbr_phase, Cp[:d, :d], state.B, self.__dict__.setdefault("_eig_plans", {}),
                                                   out_like=(state.D, state.B, state.eig_stats))
             B, D, BdivD = ops.cma_eig_out(Bn.contiguous(), w.contiguous(), d, b_out)
-            if config.get("sbr_mode") == "device" and d % 4 == 0 and d <= 8192:
-                self._stats_to_host(eig_stats)
         else:
             np_ = jacobi.padded_size(d)
             C, Cp, Bp = ops.cma_cov_pad(state.C.contiguous(), S.contiguous(), pc, a, float(self.c1), float(self.cmu), state.B.contiguous(), np_,
@@ -415,7 +419,8 @@ class CMAES(Algorithm):
         # outside a graph the stats buffer is the solver's own and is reused: the state keeps a copy
         # (under capture the state write-back is that copy)
         return state.update(mean=mean, ps=ps, pc=pc, C=C, sigma=sigma.reshape(state.sigma.shape), B=B, D=D, invsqrtC=invsqrtC,
-                            count_eigen=state.count_eigen + 1, eig_stats=eig_stats if capturing else eig_stats.clone())
+                            count_iter=count_iter.reshape(state.count_iter.shape), count_eigen=count_eigen.reshape(state.count_eigen.shape),
+                            eig_stats=eig_stats if capturing else eig_stats.clone())
 
     def _finish_tell(self, state, dm, S):
         if self._fused_epilogue_ok(state):
@@ -440,7 +445,20 @@ class CMAES(Algorithm):
 
     def _decomposition_C(self, C, B_prev):
         Cs = symmetrize_upper(C)
-        w, B = warm_eigh(Cs, B_prev, max_sweeps=self.eig_sweeps, plans=self.__dict__.setdefault("_eig_plans", {}))
+        d = self.dim
+        if (Cs.is_cuda and config.get("eigh") == "sbr" and config.get("sbr_mode") == "device" and d % 4 == 0 and d <= 8192
+                and self.eig_sweeps is None):
+            # decompositions every decomp_per_iter generations (small λ): the matrix moved by several
+            # updates since the last basis, so the device solver runs its long cold-start schedule
+            # (every slot full, bounds-gated damping) — the host driver's plain refinement diverged
+            # and fell back to Jacobi sweeps in 25 of 28 such solves at d = 1000, λ = 24
+            from ....ops.sbr_device import eigh_device, use_schedule
+
+            with use_schedule("cold"):
+                w, B, _ = eigh_device(Cs.contiguous(), B_prev.contiguous())
+            w, B = w.clone(), B.clone()
+        else:
+            w, B = warm_eigh(Cs, B_prev, max_sweeps=self.eig_sweeps, plans=self.__dict__.setdefault("_eig_plans", {}))
         B = B.contiguous()
         w = torch.clamp(w, min=1e-30)
         D = torch.sqrt(w)
@@ -465,7 +483,7 @@ class CMAES(Algorithm):
         start, size = dist.slice_of(self.pop_size)
         key, sample_key = rnd.split(state.key)
         local = self._sample(state, sample_key, start, size)
-        return local, state.update(population=local, count_iter=state.count_iter + 1, key=key)
+        return local, self._advance(state).update(population=local, key=key)
 
     def tell_sharded(self, state, fitness, dist):
         """``fitness`` is the all-gathered (λ,) vector; ``state.population`` the local rows.

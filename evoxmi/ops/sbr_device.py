@@ -184,20 +184,23 @@ class DeviceSBR:
                     float(LEAN_GUARD), float(self.xgate), float(self.damp_from)]
 
     # ------------------------------------------------------------------ pieces
-    def _btcb(self, C, skip):
+    def _btcb(self, C, skip, B=None):
         """A = Bᵀ C B (symmetric output, stats partials in the epilogue)."""
-        mm(self.B, C, ta=True, tb=True, out=self.W, skip=skip)
-        mm(self.W, self.B, mode=1, out=self.A, skip=skip, stat_part=self.part)
+        B = self.B if B is None else B
+        mm(B, C, ta=True, tb=True, out=self.W, skip=skip)
+        mm(self.W, B, mode=1, out=self.A, skip=skip, stat_part=self.part)
 
-    def _ctrl(self, j, C):
+    def _ctrl(self, j, C, report=None):
         from ..core import in_capture_warmup
 
         # a graph capture's warm-up step (on a copy of the state) is not a solve of the run: unlogged
-        log = self.log[:0] if in_capture_warmup() else self.log  # log_len 0: the ctrl kernel writes no row
+        warm = in_capture_warmup()
+        log = self.log[:0] if warm else self.log  # log_len 0: the ctrl kernel writes no row
+        seq, ring = (None, None) if (report is None or warm) else report
         _ext.ops().sbr_dev_ctrl(self.part, self.nparts, j, self.K, self.hist, self.alpha, self.theta, self.ctrl, self.st, self.prm,
-                                int(self.cfg.ns_iters), self.A, self.w, self.eig_stats, self.w_init, log, self.log_count)
+                                int(self.cfg.ns_iters), self.A, self.w, self.eig_stats, self.w_init, log, self.log_count, seq, ring)
 
-    def _iteration(self, j, C):
+    def _iteration(self, j, C, B_in=None, report=None):
         ops = _ext.ops()
         cfg = self.cfg
         sb = cfg.block
@@ -208,8 +211,9 @@ class DeviceSBR:
         damp_slot = j < self.damp_from
         ops.sbr16_block_out(self.A, shift, int(cfg.block_sweeps), sb, self.perm, self.Q, self.dq, sk_all, 0.0)
         # far generator X and Bq = B[:, perm]·blockdiag(Q) in one launch
+        # (iteration 0 reads the warm-start basis itself: no copy of it into the workspace)
         ops.sbr16_far_bq_out(self.A, self.perm, self.Q, self.dq, self.hist[4 * j : 4 * j + 4], float(cfg.thr_fac),
-                             self.theta[j : j + 1], self.X, self.B, self.Bq, sb, sk_far, sk_all)
+                             self.theta[j : j + 1], self.X, self.B if B_in is None else B_in, self.Bq, sb, sk_far, sk_all)
         corr = self.corr
         # X skew ⇒ X² = −X·Xᵀ, symmetric (upper tiles only)
         mm(self.X, self.X, tb=True, mode=1, alpha=-1.0, out=self.X2, skip=sk_far, stat_part=self.part2, stat_diag_only=True,
@@ -246,22 +250,23 @@ class DeviceSBR:
                 mm(self.T, self.T, ta=True, mode=1, out=self.G, skip=sk_ns)
                 mm(self.T, self.G, tb=True, alpha=-0.5, beta=1.5, Cin=self.T, out=self.B, skip=sk_ns)
         self._btcb(C, sk_all)
-        self._ctrl(j, C)
+        self._ctrl(j, C, report)
 
     # ------------------------------------------------------------------ solve
-    def solve(self, C: torch.Tensor, B_prev: torch.Tensor):
+    def solve(self, C: torch.Tensor, B_prev: torch.Tensor, report=None):
         """(w, B, eig_stats) with C ≈ B diag(w) Bᵀ — device buffers of this workspace, valid
-        until the next solve.  Nothing is read back; capturable into a hipGraph."""
+        until the next solve.  Nothing is read back; capturable into a hipGraph.  ``report``:
+        (int32 device counter, pinned host float64 [R, 5] ring) — the last slot's control kernel
+        writes the solve's [off_rel, status, iterations, fallback, seq] there (CMAES's schedule)."""
         ops = _ext.ops()
         n = self.n
         assert C.shape == (n, n) and B_prev.shape == (n, n)
         B_prev = B_prev if B_prev.is_contiguous() else B_prev.contiguous()
-        ops.sbr_dev_copy(B_prev, self.B, self.never)
-        self._btcb(C, self.never)
-        self._ctrl(-1, C)
+        self._btcb(C, self.never, B_prev)
+        self._ctrl(-1, C, report if self.K == 0 else None)
         for j in range(self.K):
-            self._iteration(j, C)
-        # the refinement diverged (st[5] = 0): back to the warm-start basis
+            self._iteration(j, C, B_prev if j == 0 else None, report if j == self.K - 1 else None)
+        # the refinement diverged, or no iteration ran (st[5] = 0): the warm-start basis is the result
         ops.sbr_dev_copy(B_prev, self.B, self.st[5:6])
         return self.w, self.B, self.eig_stats
 
@@ -305,7 +310,7 @@ def device_config(ns_iters: int = None) -> SBRConfig:
     return SBRConfig(tol=config.get("eigh_tol"), block=config.get("sbr_block"), **kw)
 
 
-def eigh_device(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None, iters: int = None):
+def eigh_device(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None, iters: int = None, report=None):
     """Converged-or-capped eigendecomposition of symmetric ``C`` warm-started from
     ``B_prev``, entirely on the device (see module docstring).  Returns ``(w, B, stats)``.
     ``iters``: an explicit schedule of that many slots, every slot full (tests, probes);
@@ -317,7 +322,7 @@ def eigh_device(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None, it
     else:
         sch = Schedule(int(iters), None, None, DEVICE_CFG["ns_iters"], int(iters) >= int(config.get("sbr_cold_iters")))
     cfg = cfg or device_config(sch.ns_iters)
-    return workspace(C.shape[0], C.device, cfg, sch.iters, sch.lean_from, sch.xgate, sch.damp_from).solve(C, B_prev)
+    return workspace(C.shape[0], C.device, cfg, sch.iters, sch.lean_from, sch.xgate, sch.damp_from).solve(C, B_prev, report)
 
 
 def all_histories():
