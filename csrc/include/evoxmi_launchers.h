@@ -282,7 +282,7 @@ void evx_linear_gp_fit(const double* a, const double* b, const double* c, const 
                        float* v, float* s2, hipStream_t s);
 
 // device-controlled SBR schedule (eigh_sbr_dev.hip)
-void evx_sbr_dev_prep(const float* X, const float* X2, const float* X3, int n, float* alpha, float* P, float* MT, const int* ctrl,
+void evx_sbr_dev_prep(const float* X, const float* X2, const float* X3, int n, float* alpha, float* P, float* MT, int* ctrl,
                       hipStream_t s, const float* V2 = nullptr, const float* V3 = nullptr,
                       float tau = 1.f, const double* xpart = nullptr, int nparts = 0, const float* copy_src = nullptr, float* copy_dst = nullptr, int minus_id = 0);
 void evx_sbr_dev_copy(const float* src, float* dst, int64_t n, const int* skip, hipStream_t s);

@@ -75,7 +75,7 @@ __device__ __forceinline__ void rel_kappa(const double* h, double& r, double& k)
 // pairs rotate at once.)
 __global__ void __launch_bounds__(256) sbr_dev_prep_kernel(const float* __restrict__ X, const float* __restrict__ X2,
                                                            const float* __restrict__ X3, int n, float* __restrict__ alpha,
-                                                           float* __restrict__ P, float* __restrict__ MT, const int* __restrict__ ctrl,
+                                                           float* __restrict__ P, float* __restrict__ MT, int* __restrict__ ctrl,
                                                            const float* __restrict__ V2, const float* __restrict__ V3, float tau,
                                                            const double* __restrict__ xpart, int nparts,
                                                            const float* __restrict__ copy_src, float* __restrict__ copy_dst,
@@ -104,7 +104,21 @@ __global__ void __launch_bounds__(256) sbr_dev_prep_kernel(const float* __restri
     a = alpha[0];
   }
   if (xpart || (V2 && ctrl[2] == 0)) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) alpha[0] = a;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      alpha[0] = a;
+      // the generator's bounds damped a step the κ rule had left undamped and without
+      // Newton–Schulz (xgate): near-degenerate spectra (κ small, gaps ≈ 1e-5 — a CMA-ES C after
+      // a few small-λ updates) give generators of 2-norm ≈ 5 and a damped step of ‖αX‖ = τ whose
+      // order-4 truncation, un-re-orthonormalised, grew the off-norm 100× and sent the solve
+      // into its divergence recovery (profiles/NOTES.md, round 6).  Re-orthonormalise this
+      // iteration too: the B·V product (launched after this kernel) reads sel_ns, and the
+      // Newton–Schulz kernels skip_ns, at run time; damping only runs in full slots, which
+      // carry the Newton–Schulz kernels.
+      if (xpart && a < 1.f && ctrl[5] != 0) {
+        ctrl[5] = 0;
+        ctrl[6] = 1;
+      }
+    }
   }
 
   const float a2 = a * a, a3 = a2 * a;
@@ -367,7 +381,7 @@ __global__ void __launch_bounds__(256) sbr_dev_ctrl_kernel(const double* __restr
 
 }  // namespace
 
-void evx_sbr_dev_prep(const float* X, const float* X2, const float* X3, int n, float* alpha, float* P, float* MT, const int* ctrl,
+void evx_sbr_dev_prep(const float* X, const float* X2, const float* X3, int n, float* alpha, float* P, float* MT, int* ctrl,
                       hipStream_t s, const float* V2, const float* V3, float tau, const double* xpart, int nparts, const float* copy_src,
                       float* copy_dst, int minus_id) {
   // a grid-stride loop over 256 workgroups: the schedule skips this kernel in most

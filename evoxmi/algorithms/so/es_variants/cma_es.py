@@ -449,12 +449,14 @@ class CMAES(Algorithm):
         if (Cs.is_cuda and config.get("eigh") == "sbr" and config.get("sbr_mode") == "device" and d % 4 == 0 and d <= 8192
                 and self.eig_sweeps is None):
             # decompositions every decomp_per_iter generations (small λ): the matrix moved by several
-            # updates since the last basis, so the device solver runs its long cold-start schedule
-            # (every slot full, bounds-gated damping) — the host driver's plain refinement diverged
-            # and fell back to Jacobi sweeps in 25 of 28 such solves at d = 1000, λ = 24
+            # updates since the last basis, so the device solver runs the cold-start rules (every slot
+            # full, bounds-gated damping) with twice the cold slots ("deep"): the host driver's plain
+            # refinement fell back to Jacobi sweeps in 25 of 28 such solves at d = 1000, λ = 24, and
+            # with the 16 cold slots 5 of 25 solves that recovered from a divergence were capped
+            # (damped steps after a recovery converge slowly; profiles/NOTES.md, round 6)
             from ....ops.sbr_device import eigh_device, use_schedule
 
-            with use_schedule("cold"):
+            with use_schedule("deep"):
                 w, B, _ = eigh_device(Cs.contiguous(), B_prev.contiguous())
             w, B = w.clone(), B.clone()
         else:

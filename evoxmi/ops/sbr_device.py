@@ -82,11 +82,14 @@ class Schedule:
 def schedule(level: str, n: int) -> Schedule:
     """The schedule of a CMA-ES graph variant: ``"cold"`` (every slot full, bounds-gated
     damping), ``"warm"``, ``"warm6"`` (one slot fewer) or ``"late"`` (lean tail slots) at matrix
-    order ``n``."""
+    order ``n``; ``"deep"`` is the cold schedule with twice the slots, for decompositions that
+    run only every few generations (``CMAES._decomposition_C``: the basis is several updates
+    old, a divergence recovery's damped steps are slow, and the cost is amortised)."""
     from .. import config
 
-    if level == "cold":
-        return Schedule(int(config.get("sbr_cold_iters")), None, None, DEVICE_CFG["ns_iters"], True)
+    if level in ("cold", "deep"):
+        return Schedule(int(config.get("sbr_cold_iters")) * (2 if level == "deep" else 1), None, None, DEVICE_CFG["ns_iters"],
+                        True)
     late = level == "late"
     iters = int(config.get("sbr_late_iters" if late else "sbr_device_iters"))
     if level == "warm6":  # the warm schedule with one slot fewer
