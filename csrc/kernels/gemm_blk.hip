@@ -32,6 +32,7 @@
 #include "evoxmi_common.h"
 #include "evoxmi_launchers.h"
 #include <cstdlib>
+#include <stdexcept>
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
@@ -565,11 +566,14 @@ __global__ void __launch_bounds__(256) philox_h_kernel(const int64_t* __restrict
                                                        uint16_t* __restrict__ out, float* __restrict__ rinv, int64_t Rp, int KB) {
   uint32_t k0, k1;
   evx::load_key(key, k0, k1);
-  const int64_t total = (int64_t)KB * Rp * 2;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+  // 32-bit record index (the launcher checks KB·Rp < 2³¹): a 64-bit division here was ≈ 10 %
+  // of this VALU-bound kernel's issue
+  const uint32_t total = (uint32_t)KB * (uint32_t)Rp * 2u, rp = (uint32_t)Rp;
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
     const int half = (int)(t & 1);
-    const int64_t rec = t >> 1, row = rec % Rp;
-    const int kb = (int)(rec / Rp);
+    const uint32_t rec = t >> 1, kb32 = rec / rp;
+    const int64_t row = rec - kb32 * rp;
+    const int kb = (int)kb32;
     float v[8];
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
@@ -594,7 +598,7 @@ __global__ void __launch_bounds__(256) philox_h_kernel(const int64_t* __restrict
       M[p] = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{a0 - hf.x, a1 - hf.y}, f16x2));
     }
     const int sw = (int)((row >> 2) & 3);
-    uint4* dst = reinterpret_cast<uint4*>(out + rec * 32);
+    uint4* dst = reinterpret_cast<uint4*>(out + (int64_t)rec * 32);
     dst[half ^ sw] = make_uint4(H[0], H[1], H[2], H[3]);
     dst[(2 + half) ^ sw] = make_uint4(M[0], M[1], M[2], M[3]);
     if (kb == 0 && half == 0) rinv[row] = row < rows ? 1.f / 8192.f : 0.f;
@@ -961,6 +965,7 @@ void evx_split_h3(const float* X, int64_t ld, int64_t rows, int K, const float* 
 void evx_philox_h3(const int64_t* key, int64_t rows, int d, int64_t row0, uint16_t* out, float* rinv, hipStream_t s) {
   const int KB = (d + 15) / 16;
   const int64_t Rp = evx_blk_rows(rows), total = (int64_t)KB * Rp * 2;
+  if (total >= (int64_t)1 << 31) throw std::runtime_error("evx_philox_h3: rows · d too large for the 32-bit record index");
   int g = (int)((total + 255) / 256);
   if (g > 8192) g = 8192;
   if (g > 0) philox_h_kernel<<<g, 256, 0, s>>>(key, rows, d, row0, out, rinv, Rp, KB);
