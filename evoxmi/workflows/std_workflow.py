@@ -502,7 +502,9 @@ class StdWorkflow(Workflow):
         ODE, …) keep only their column block of every ``dim_fields`` array on each rank; problems
         with halo-free terms evaluate that block (the only traffic is the (N, k) term all-reduce),
         every other problem evaluates the all-gathered rows (GSPMD's all-gather of a sharded
-        operand).  The state then holds column blocks: :meth:`gather_state` reassembles the
+        operand).  An algorithm that is not column-separable (CMA-ES and the other
+        full-covariance ES) keeps its state replicated, with a warning — the same results as
+        GSPMD's column-sharded matrices, which it would gather for every product.  The state then holds column blocks: :meth:`gather_state` reassembles the
         full arrays (the reference's sharded arrays stay logically global).  Default ``False``:
         a state read after the run has the reference's full shapes."""
         if not self.jit_problem:
@@ -512,6 +514,15 @@ class StdWorkflow(Workflow):
         from ..parallel.context import DistContext, balanced_slices
         from ..parallel.dim_sharded import supports_dim_sharding, supports_state_sharding
 
+        if shard_state and not supports_state_sharding(self.algorithm, self.problem):
+            # GSPMD would shard a full-covariance ES's d×d matrices by columns and gather them for
+            # every product; its results equal the unsharded run's, which is what the replicated
+            # state gives (at d ≤ 8192 the matrices are ≤ 256 MiB of a GPU's 288 GB, and the
+            # column-distributed eigensolver does not pay at d = 1000 — profiles/NOTES.md, round 6)
+            warnings.warn(f"enable_multi_devices(shard_state=True): {type(self.algorithm).__name__} is not column-separable "
+                          "(parallel.ColumnSeparable); its state stays replicated on every rank and only the "
+                          "evaluation is sharded")
+            shard_state = False
         if not supports_dim_sharding(self.problem) and not shard_state:
             warnings.warn(f"enable_multi_devices: {type(self.problem).__name__} has no dim-sharding terms "
                           "(partial_terms / combine_terms / dim_halo); sharding the population instead "
@@ -525,9 +536,6 @@ class StdWorkflow(Workflow):
         ctx = DistContext(group=devices if isinstance(devices, torch.distributed.ProcessGroup) else None)
         state = ctx.broadcast_state(state)
         if shard_state:
-            if not supports_state_sharding(self.algorithm, self.problem):
-                raise ValueError(f"state sharding needs a column-separable algorithm (parallel.ColumnSeparable); "
-                                 f"{type(self.algorithm).__name__} is not")
             d = int(self.algorithm.dim)
             rank, world = torch.distributed.get_rank(ctx.group), torch.distributed.get_world_size(ctx.group)
             col0, own = balanced_slices(d, world)[rank]

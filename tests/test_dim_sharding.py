@@ -434,3 +434,50 @@ def test_philox_windows_equal_full_matrix_columns(device, rows, d, c0, own, row0
             assert torch.allclose(W, F[:, c0 : c0 + own], rtol=1e-6, atol=1e-6)
         else:
             assert torch.equal(W, F[:, c0 : c0 + own]), (win.__name__, float((W - F[:, c0 : c0 + own]).abs().max()))
+
+
+def _make_cmaes():
+    from evoxmi.algorithms import CMAES
+
+    return StdWorkflow(CMAES(center_init=torch.full((16,), 3.0), init_stdev=1.0, pop_size=24), Ellipsoid())
+
+
+def _cmaes_worker(rank, world, port, out):
+    import warnings
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from evoxmi.parallel import destroy, init_distributed
+
+    init_distributed(backend="gloo")
+    wf = _make_cmaes()
+    st = wf.init(rnd.PRNGKey(5))
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        st = wf.enable_multi_devices(st, shard_state=True)
+    for _ in range(30):
+        st = wf.step(st)
+    a = st.get_child_state("algorithm")
+    out[rank] = (a.mean.clone(), a.C.clone(), a.sigma.clone(), [str(x.message) for x in w])
+    destroy()
+
+
+def test_full_covariance_es_under_state_sharding_keeps_replicated_state():
+    """CMA-ES is not column-separable: enable_multi_devices(shard_state=True) keeps its d×d state
+    replicated (warning) and shards the evaluation — the run equals the single-process one, as the
+    reference's GSPMD column-sharded matrices do (std_workflow.py:253-270)."""
+    wf = _make_cmaes()
+    st = wf.init(rnd.PRNGKey(5))
+    for _ in range(30):
+        st = wf.step(st)
+    ref = st.get_child_state("algorithm")
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_cmaes_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    m0, C0, s0, msgs = out[0]
+    m1, C1, s1, _ = out[1]
+    assert any("not column-separable" in m for m in msgs), msgs
+    assert torch.equal(m0, m1) and torch.equal(C0, C1) and torch.equal(s0, s1)
+    assert C0.shape == (16, 16)
+    assert torch.allclose(m0, ref.mean, rtol=1e-3, atol=1e-3)
+    assert torch.allclose(C0, ref.C, rtol=1e-3, atol=1e-4)
