@@ -89,7 +89,9 @@ def main():
         from evoxmi.monitors import EvalMonitor
 
         monitors = [EvalMonitor(full_fit_history=args.monitor != "best", history_to_host=args.monitor == "host")]
-    wf = StdWorkflow(algo, prob, graph=use_graph, monitors=monitors)
+    # "auto": a step that cannot be captured (e.g. a collective the communicator refuses to
+    # record) runs eagerly instead of ending the run; the JSON reports which one was timed
+    wf = StdWorkflow(algo, prob, graph="auto" if use_graph else False, monitors=monitors)
     state = wf.init(key)
     dist_on = (world > 1 or args.force_dist) and not sim
     if dist_on:
@@ -186,7 +188,7 @@ def main():
                 "parallelism": f"pop-shard{world}" if not sim else f"simulated-rank{args.simulate_rank}-of-{args.world}",
                 "pop_size": args.pop,
                 "dim": args.dim,
-                "hipgraph": use_graph,
+                "hipgraph": bool(use_graph and not getattr(wf, "_graph_failed", False)),
                 "eigh": config.get("eigh") + ("-" + config.get("sbr_mode") if config.get("eigh") == "sbr" else ""),
             },
         }
