@@ -1321,7 +1321,7 @@ at::Tensor lsmop_g(const at::Tensor& X, std::vector<int64_t> start, std::vector<
 // ---------------------------------------------------------------- CMA-ES tell epilogue (cmaes.hip)
 // Yw = (pop[rows] − mean)·sqrt(w)/σ (K×d), rows int32 (or none: the first K rows)
 at::Tensor cma_center_rows(const at::Tensor& pop, const c10::optional<at::Tensor>& rows, const at::Tensor& mean, const at::Tensor& sigma,
-                           const at::Tensor& w) {
+                           const at::Tensor& w, bool aug) {
   CHECK_DEV(pop); CHECK_F32(pop);
   TORCH_CHECK(pop.dim() == 2 && pop.stride(1) == 1, "cma_center_rows: pop must be row-major 2-D");
   const int64_t d = pop.size(1), K = w.numel();
@@ -1334,10 +1334,12 @@ at::Tensor cma_center_rows(const at::Tensor& pop, const c10::optional<at::Tensor
     TORCH_CHECK(K <= pop.size(0), "cma_center_rows: K > rows of pop");
   }
   c10::DeviceGuard g(pop.device());
-  auto Y = at::empty({K, d}, pop.options());
+  // aug: (K, d + 1) view of a (K, ld) buffer, ld = d + 1 rounded up to 4 (16-B rows), column d = σ·sqrt(wᵢ)
+  const int64_t ld = aug ? ((d + 1 + 3) & ~int64_t(3)) : d;
+  auto Yb = at::empty({K, ld}, pop.options());
   evx_cma_center_rows(pop.data_ptr<float>(), pop.stride(0), rp, mean.data_ptr<float>(), sigma.contiguous().data_ptr<float>(),
-                      w.data_ptr<float>(), (int)K, (int)d, Y.data_ptr<float>(), cur_stream());
-  return Y;
+                      w.data_ptr<float>(), (int)K, (int)d, Yb.data_ptr<float>(), cur_stream(), ld, aug ? 1 : 0);
+  return aug ? Yb.narrow(1, 0, d + 1) : Yb;
 }
 
 // sharded tell: this rank's rows of the global top μ, compacted (see cmaes.hip local_select_kernel)
@@ -1418,9 +1420,12 @@ std::vector<at::Tensor> cma_paths(const at::Tensor& ps, const at::Tensor& pc, co
 std::vector<at::Tensor> cma_cov_pad(const at::Tensor& C, const at::Tensor& S, const at::Tensor& pc, const at::Tensor& a, double c1,
                                     double cmu, const at::Tensor& Bprev, int64_t np, const c10::optional<at::Tensor>& Cn_out,
                                     bool want_bp) {
-  for (auto* t : {&C, &S, &pc, &a, &Bprev}) { CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t); }
+  for (auto* t : {&C, &pc, &a, &Bprev}) { CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t); }
+  CHECK_DEV(S); CHECK_F32(S);
   const int64_t d = pc.numel();
   TORCH_CHECK(C.dim() == 2 && C.size(0) == d && C.size(1) == d && S.sizes() == C.sizes() && Bprev.sizes() == C.sizes(), "cma_cov_pad: shapes");
+  // S may be the leading d × d block of the augmented rank-μ product (row stride ≥ d)
+  TORCH_CHECK(S.stride(1) == 1 && S.stride(0) >= d, "cma_cov_pad: S row-major (row stride >= d)");
   TORCH_CHECK(np >= d && np % 32 == 0 && a.numel() == 1, "cma_cov_pad: np must be a multiple of 32 and >= d");
   c10::DeviceGuard g(C.device());
   at::Tensor Cn;
@@ -1435,7 +1440,7 @@ std::vector<at::Tensor> cma_cov_pad(const at::Tensor& C, const at::Tensor& S, co
   auto Bp = want_bp ? at::empty({np, np}, C.options()) : at::empty({0}, C.options());
   evx_cma_cov_pad(C.data_ptr<float>(), S.data_ptr<float>(), pc.data_ptr<float>(), a.data_ptr<float>(), (float)c1, (float)cmu,
                   Bprev.data_ptr<float>(), (int)d, (int)np, Cn.data_ptr<float>(), Cp.data_ptr<float>(),
-                  want_bp ? Bp.data_ptr<float>() : nullptr, cur_stream());
+                  want_bp ? Bp.data_ptr<float>() : nullptr, cur_stream(), S.stride(0));
   return {Cn, Cp, Bp};
 }
 
@@ -1588,7 +1593,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("sbr16_far_bq_out(Tensor A, Tensor perm, Tensor Q, Tensor dq, Tensor stats, float thr_fac, Tensor theta, Tensor(a!) X, Tensor B, Tensor(b!) Bq, int sb, Tensor skip_far, Tensor skip_bq, bool pre=False) -> ()");
   m.def("lsmop_g(Tensor X, int[] start, int[] sublen, int[] func, int nk, int cosine) -> Tensor");
   m.def("cma_delta_gemv(Tensor M, Tensor mean, Tensor dm, float cm) -> Tensor[]");
-  m.def("cma_center_rows(Tensor pop, Tensor? rows, Tensor mean, Tensor sigma, Tensor w) -> Tensor");
+  m.def("cma_center_rows(Tensor pop, Tensor? rows, Tensor mean, Tensor sigma, Tensor w, bool aug=False) -> Tensor");
   m.def("cma_local_select(Tensor order, int mu, Tensor w, int start, int size, Tensor(a!) rows, Tensor(b!) wk) -> ()");
   m.def("sym_pack(Tensor S, Tensor(a!) P) -> ()");
   m.def("sym_unpack(Tensor P, Tensor(a!) S) -> ()");

@@ -164,7 +164,7 @@ void evx_cma_local_select(const int32_t* order, int mu, const float* w, int star
 void evx_sym_pack(const float* S, int64_t lds, int d, float* P, hipStream_t s);
 void evx_sym_unpack(const float* P, int d, float* S, int64_t lds, hipStream_t s);
 void evx_cma_center_rows(const float* pop, int64_t ldp, const int32_t* rows, const float* mean, const float* sigma, const float* w, int K,
-                         int d, float* Y, hipStream_t s);
+                         int d, float* Y, hipStream_t s, int64_t ldy = 0, int aug = 0);
 void evx_radix_argsort(const float* keys, int n, int descending, float* out_keys, int32_t* out_idx, hipStream_t s, int batch);
 int evx_argsort_max_n();
 void evx_argsort(const float* keys, int n, int descending, float* out_keys, int32_t* out_idx, hipStream_t s, int batch = 1);
@@ -234,7 +234,7 @@ void evx_cma_paths(const float* ps, const float* pc, const float* y, const float
                    hipStream_t s,
                    const int64_t* count_eigen = nullptr, int64_t* count_iter_out = nullptr, int64_t* count_eigen_out = nullptr);
 void evx_cma_cov_pad(const float* C, const float* S, const float* pc, const float* a, float c1, float cmu, const float* Bprev, int d,
-                     int np, float* Cn, float* Cp, float* Bp, hipStream_t s);
+                     int np, float* Cn, float* Cp, float* Bp, hipStream_t s, int64_t lds = 0);
 void evx_cma_eig_out(const float* Bp, const float* w, int d, int np, float* B, float* D, float* BdivD, hipStream_t s);
 
 // nsga_select.hip

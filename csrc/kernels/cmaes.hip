@@ -93,7 +93,7 @@ constexpr int TS = 32;
 // captured generation updates the state's covariance in place): a strictly upper tile also
 // writes its transpose into Cp's lower tile, so no workgroup reads another tile of C.
 // Bp (the padded warm-start basis) is optional: the device eigensolver reads B unpadded.
-__global__ void __launch_bounds__(256) cov_pad_kernel(const float* C, const float* __restrict__ S,
+__global__ void __launch_bounds__(256) cov_pad_kernel(const float* C, const float* __restrict__ S, int64_t lds,
                                                       const float* __restrict__ pc, const float* __restrict__ a_ptr, float c1, float cmu,
                                                       const float* __restrict__ Bprev, int d, int np, float* Cn,
                                                       float* __restrict__ Cp, float* __restrict__ Bp) {
@@ -107,7 +107,7 @@ __global__ void __launch_bounds__(256) cov_pad_kernel(const float* C, const floa
     const int i = ti * TS + r0 + rr, j = tj * TS + c;
     float v = (i == j) ? 1.f : 0.f, b = v;
     if (i < d && j < d) {
-      v = a * C[(int64_t)i * d + j] + c1 * pc[i] * pc[j] + cmu * S[(int64_t)i * d + j];
+      v = a * C[(int64_t)i * d + j] + c1 * pc[i] * pc[j] + cmu * S[(int64_t)i * lds + j];
       Cn[(int64_t)i * d + j] = v;
       if (Bp) b = Bprev[(int64_t)i * d + j];
     }
@@ -145,15 +145,21 @@ __global__ void __launch_bounds__(256) eig_out_kernel(const float* __restrict__ 
 // Rank-μ operand: Yw[i, :] = (pop[rows[i], :] − mean) · sqrt(w_i) / σ, so Σ wᵢ yᵢ yᵢᵀ = Ywᵀ Yw
 // is one plain GEMM (gather, centring, scaling in one pass instead of 4 library kernels).
 // One workgroup per selected row, float4 along d.
+// aug: the row also gets y[d] = σ·sqrt(wᵢ) and zeros up to ldy — the rank-μ product of these
+// rows then carries Σ wᵢ (xᵢ − m) = the weighted mean shift in its last row (round 6: the
+// separate weighted row sum and its column reduction, two launches, are gone)
 __global__ void __launch_bounds__(256) center_rows_kernel(const float* __restrict__ pop, int64_t ldp, const int32_t* __restrict__ rows,
                                                           const float* __restrict__ mean, const float* __restrict__ sigma,
-                                                          const float* __restrict__ w, int d, float* __restrict__ Y) {
+                                                          const float* __restrict__ w, int d, float* __restrict__ Y, int64_t ldy,
+                                                          int aug) {
   const int i = blockIdx.x;
   const int64_t src = rows ? rows[i] : i;
-  const float sc = sqrtf(w[i]) / sigma[0];
+  const float sw = sqrtf(w[i]), sc = sw / sigma[0];
   const float* x = pop + src * ldp;
-  float* y = Y + (int64_t)i * d;
-  if ((d & 3) == 0 && (ldp & 3) == 0) {
+  float* y = Y + (int64_t)i * ldy;
+  if (aug)
+    for (int c = d + (int)threadIdx.x; c < ldy; c += blockDim.x) y[c] = c == d ? sw * sigma[0] : 0.f;
+  if ((d & 3) == 0 && (ldp & 3) == 0 && (ldy & 3) == 0) {
     for (int c = threadIdx.x * 4; c < d; c += blockDim.x * 4) {
       const float4 a = *(const float4*)(x + c), m = *(const float4*)(mean + c);
       *(float4*)(y + c) = make_float4((a.x - m.x) * sc, (a.y - m.y) * sc, (a.z - m.z) * sc, (a.w - m.w) * sc);
@@ -257,9 +263,9 @@ void evx_cma_paths(const float* ps, const float* pc, const float* y, const float
 }
 
 void evx_cma_cov_pad(const float* C, const float* S, const float* pc, const float* a, float c1, float cmu, const float* Bprev, int d,
-                     int np, float* Cn, float* Cp, float* Bp, hipStream_t s) {
+                     int np, float* Cn, float* Cp, float* Bp, hipStream_t s, int64_t lds) {
   dim3 grid(np / TS, np / TS);
-  cov_pad_kernel<<<grid, 256, 0, s>>>(C, S, pc, a, c1, cmu, Bprev, d, np, Cn, Cp, Bp);
+  cov_pad_kernel<<<grid, 256, 0, s>>>(C, S, lds > 0 ? lds : d, pc, a, c1, cmu, Bprev, d, np, Cn, Cp, Bp);
 }
 
 void evx_cma_eig_out(const float* Bp, const float* w, int d, int np, float* B, float* D, float* BdivD, hipStream_t s) {
@@ -270,6 +276,7 @@ void evx_cma_eig_out(const float* Bp, const float* w, int d, int np, float* B, f
 }
 
 void evx_cma_center_rows(const float* pop, int64_t ldp, const int32_t* rows, const float* mean, const float* sigma, const float* w, int K,
-                         int d, float* Y, hipStream_t s) {
-  if (K > 0) center_rows_kernel<<<K, 256, 0, s>>>(pop, ldp, rows, mean, sigma, w, d, Y);
+                         int d, float* Y, hipStream_t s, int64_t ldy, int aug) {
+  if (ldy <= 0) ldy = d;
+  if (K > 0) center_rows_kernel<<<K, 256, 0, s>>>(pop, ldp, rows, mean, sigma, w, d, Y, ldy, aug);
 }

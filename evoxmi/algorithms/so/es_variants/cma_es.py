@@ -321,6 +321,23 @@ class CMAES(Algorithm):
         return population, self._advance(state).update(population=population, key=key)
 
     # ------------------------------------------------------------------ tell
+    def _aug_ok(self, population) -> bool:
+        return population.is_cuda and config.get("plain_gemm") == "evoxmi"
+
+    def _weighted_stats_aug(self, state, population, rows_i32, wvec):
+        """The (d+1) × (d+1) rank-μ product of the centred, weighted rows augmented by a column
+        σ·sqrt(wᵢ): its leading d × d block is Σ wᵢ yᵢ yᵢᵀ and its last row Σ wᵢ (xᵢ − m), the
+        weighted mean shift — one centring pass and one GEMM instead of a weighted row sum (two
+        launches) beside them (the (d+1)-wide product has the same tile grid as the d-wide one at
+        d = 1000).  A view into a (d+1) × ld buffer (16-B rows)."""
+        from ....ops import _ext
+
+        d = self.dim
+        Yw = _ext.ops().cma_center_rows(population, rows_i32, state.mean.contiguous(), state.sigma.reshape(1), wvec.contiguous(), True)
+        ld = (d + 1 + 3) // 4 * 4
+        S_aug = torch.empty(d + 1, ld, dtype=torch.float32, device=population.device)[:, : d + 1]
+        return mm(Yw, Yw, ta=True, mode=1, out=S_aug)
+
     def _weighted_stats(self, state, population, order_i32, K: int, wvec, gather: bool, s_out=None):
         """(Σ wᵢ(xᵢ − m), Σ wᵢ yᵢ yᵢᵀ) with yᵢ = (xᵢ − m)/σ; ``s_out``: a (d, d) buffer the
         framework GEMM writes S into (the sharded tell's all-reduce buffer)."""
@@ -385,8 +402,8 @@ class CMAES(Algorithm):
         b_out = state.B if capturing and state.B.is_contiguous() else None
         if config.get("eigh") == "sbr":
             np_ = jacobi.padded_size(d)
-            C, Cp, _ = ops.cma_cov_pad(state.C.contiguous(), S.contiguous(), pc, a, float(self.c1), float(self.cmu), state.B.contiguous(), np_,
-                                       c_out, False)
+            C, Cp, _ = ops.cma_cov_pad(state.C.contiguous(), S if S.stride(1) == 1 else S.contiguous(), pc, a, float(self.c1),
+                                       float(self.cmu), state.B.contiguous(), np_, c_out, False)
             # Cp[:d, :d] = triu(C) + triu(C, 1)ᵀ, the reference's symmetrisation (cma_es.py:193-195)
             with profiling.phase("eigh"):
                 if config.get("sbr_mode") == "device" and d % 4 == 0 and d <= 8192:
@@ -402,7 +419,8 @@ class CMAES(Algorithm):
             B, D, BdivD = ops.cma_eig_out(Bn.contiguous(), w.contiguous(), d, b_out)
         else:
             np_ = jacobi.padded_size(d)
-            C, Cp, Bp = ops.cma_cov_pad(state.C.contiguous(), S.contiguous(), pc, a, float(self.c1), float(self.cmu), state.B.contiguous(), np_,
+            C, Cp, Bp = ops.cma_cov_pad(state.C.contiguous(), S if S.stride(1) == 1 else S.contiguous(), pc, a, float(self.c1),
+                                        float(self.cmu), state.B.contiguous(), np_,
                                         c_out, True)
             with profiling.phase("eigh"):
                 w, Bp = jacobi.warm_eigh_padded(Cp, Bp, d, max_sweeps=self.eig_sweeps)
@@ -472,7 +490,12 @@ class CMAES(Algorithm):
 
     def tell(self, state, fitness):
         pop = state.population
-        if pop.is_cuda:
+        if self._aug_ok(pop):
+            _, order = argsort_i32(fitness.contiguous())
+            S_aug = self._weighted_stats_aug(state, pop, order[: self.mu].contiguous(), self.weights)
+            d = self.dim
+            dm, S = S_aug[d, :d], S_aug[:d, :d]
+        elif pop.is_cuda:
             _, order = argsort_i32(fitness.contiguous())
             dm, S = self._weighted_stats(state, pop, order[: self.mu].contiguous(), self.mu, self.weights, gather=True)
         else:
@@ -519,6 +542,20 @@ class CMAES(Algorithm):
             lsel[:n] = top[mine] - start
             wsel[:n] = self.weights.cpu()[mine]
             lsel, wsel = lsel.to(dev), wsel.to(dev)
+        if self._aug_ok(state.population):
+            # the augmented product's packed upper triangle carries the mean shift in its last
+            # column: (d+1)(d+2)/2 floats on the wire, one more than d(d+1)/2 + d
+            from ....ops import _ext
+
+            ops = _ext.ops()
+            S_aug = self._weighted_stats_aug(state, state.population, lsel, wsel)
+            Pa = (d + 1) * (d + 2) // 2
+            buf = torch.empty(Pa, dtype=torch.float32, device=dev)
+            ops.sym_pack(S_aug, buf)
+            with profiling.phase("all_reduce"):
+                dist.all_reduce_(buf)
+            ops.sym_unpack(buf, S_aug)
+            return self._finish_tell(state, S_aug[d, :d], S_aug[:d, :d])
         dm, S = self._weighted_stats(state, state.population, lsel, K, wsel, gather=True)
         P = d * (d + 1) // 2
         buf = torch.empty(P + d, dtype=torch.float32, device=dev)
