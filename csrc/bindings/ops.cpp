@@ -1444,7 +1444,8 @@ std::vector<at::Tensor> cma_cov_pad(const at::Tensor& C, const at::Tensor& S, co
   return {Cn, Cp, Bp};
 }
 
-std::vector<at::Tensor> cma_eig_out(const at::Tensor& Bp, const at::Tensor& w, int64_t d, const c10::optional<at::Tensor>& B_out) {
+std::vector<at::Tensor> cma_eig_out(const at::Tensor& Bp, const at::Tensor& w, int64_t d, const c10::optional<at::Tensor>& B_out,
+                                    const c10::optional<at::Tensor>& B_alt, const c10::optional<at::Tensor>& keep) {
   for (auto* t : {&Bp, &w}) { CHECK_DEV(*t); CHECK_F32(*t); CHECK_CONTIG(*t); }
   const int64_t np = Bp.size(0);
   TORCH_CHECK(Bp.dim() == 2 && Bp.size(1) == np && w.numel() >= d && d <= np, "cma_eig_out: shapes");
@@ -1458,8 +1459,18 @@ std::vector<at::Tensor> cma_eig_out(const at::Tensor& Bp, const at::Tensor& w, i
     B = at::empty({d, d}, Bp.options());
   }
   auto BD = at::empty({d, d}, Bp.options()), D = at::empty({d}, Bp.options());
+  const float* alt = nullptr;
+  const int* kp = nullptr;
+  if (B_alt.has_value() && B_alt->defined()) {  // the warm start, taken while *keep == 0 (device eigensolver)
+    CHECK_DEV(*B_alt); CHECK_F32(*B_alt); CHECK_CONTIG(*B_alt);
+    TORCH_CHECK(B_alt->dim() == 2 && B_alt->size(0) == d && B_alt->size(1) == d && keep.has_value() && keep->defined() &&
+                    keep->is_cuda() && keep->scalar_type() == at::kInt && keep->numel() >= 1,
+                "cma_eig_out: B_alt (d, d) with an int32 device keep word");
+    alt = B_alt->data_ptr<float>();
+    kp = keep->data_ptr<int>();
+  }
   if (d > 0) evx_cma_eig_out(Bp.data_ptr<float>(), w.data_ptr<float>(), (int)d, (int)np, B.data_ptr<float>(), D.data_ptr<float>(),
-                             BD.data_ptr<float>(), cur_stream());
+                             BD.data_ptr<float>(), cur_stream(), alt, kp);
   return {B, D, BD};
 }
 
@@ -1599,7 +1610,7 @@ TORCH_LIBRARY(evoxmi, m) {
   m.def("sym_unpack(Tensor P, Tensor(a!) S) -> ()");
   m.def("cma_paths(Tensor ps, Tensor pc, Tensor y, Tensor delta, Tensor sigma, Tensor count_iter, float[] consts, Tensor? count_eigen=None) -> Tensor[]");
   m.def("cma_cov_pad(Tensor C, Tensor S, Tensor pc, Tensor a, float c1, float cmu, Tensor Bprev, int np, Tensor? Cn_out=None, bool want_bp=True) -> Tensor[]");
-  m.def("cma_eig_out(Tensor Bp, Tensor w, int d, Tensor? B_out=None) -> Tensor[]");
+  m.def("cma_eig_out(Tensor Bp, Tensor w, int d, Tensor? B_out=None, Tensor? B_alt=None, Tensor? keep=None) -> Tensor[]");
   m.def("nsga_select(Tensor rank, Tensor f, int N, int mask_pos) -> Tensor");
   m.def("moead_parents(Tensor nb, Tensor key, int row0=0, int rows=0) -> Tensor[]");
   m.def("moead_variation(Tensor pop, Tensor p0, Tensor p1, Tensor kx, Tensor km, Tensor lb, Tensor ub, float pro_c, float dis_c, float pro_m, float dis_m, int nm, int row0=0, int rows=0, Tensor? win=None, Tensor(a!)? out=None) -> Tensor");

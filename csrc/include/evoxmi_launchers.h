@@ -235,7 +235,8 @@ void evx_cma_paths(const float* ps, const float* pc, const float* y, const float
                    const int64_t* count_eigen = nullptr, int64_t* count_iter_out = nullptr, int64_t* count_eigen_out = nullptr);
 void evx_cma_cov_pad(const float* C, const float* S, const float* pc, const float* a, float c1, float cmu, const float* Bprev, int d,
                      int np, float* Cn, float* Cp, float* Bp, hipStream_t s, int64_t lds = 0);
-void evx_cma_eig_out(const float* Bp, const float* w, int d, int np, float* B, float* D, float* BdivD, hipStream_t s);
+void evx_cma_eig_out(const float* Bp, const float* w, int d, int np, float* B, float* D, float* BdivD, hipStream_t s,
+                     const float* Balt = nullptr, const int* keep = nullptr);
 
 // nsga_select.hip
 void evx_nsga_select(const int32_t* rank, const float* f, int n, int m, int N, int mask_pos, int64_t* keep, hipStream_t s);

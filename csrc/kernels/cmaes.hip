@@ -128,16 +128,25 @@ __global__ void __launch_bounds__(256) cov_pad_kernel(const float* C, const floa
   }
 }
 
+// keep (device eigensolver, round 6): while *keep == 0 the solve diverged or ran no iteration and
+// the basis is the warm start Balt (d × d; may be the output buffer B itself — each element is
+// read and written by the same thread) — the solver's own restore-copy launch is gone.  Rows over
+// the grid, columns over the threads (no per-element 64-bit division).
 __global__ void __launch_bounds__(256) eig_out_kernel(const float* __restrict__ Bp, const float* __restrict__ w, int d, int np,
-                                                      float* __restrict__ B, float* __restrict__ D, float* __restrict__ BdivD) {
-  const int64_t total = (int64_t)d * d;
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    const int i = (int)(e / d), j = (int)(e - (int64_t)i * d);
-    const float dj = sqrtf(fmaxf(w[j], 1e-30f));
-    const float b = Bp[(int64_t)i * np + j];
-    B[e] = b;
-    BdivD[e] = b / dj;
-    if (i == 0) D[j] = dj;
+                                                      float* B, float* __restrict__ D, float* __restrict__ BdivD,
+                                                      const float* Balt, const int* __restrict__ keep) {
+  const bool alt = Balt && keep && *keep == 0;
+  const float* src = alt ? Balt : Bp;
+  const int64_t lds = alt ? d : np;
+  for (int i = blockIdx.x; i < d; i += gridDim.x) {
+    for (int j = threadIdx.x; j < d; j += blockDim.x) {
+      const float dj = sqrtf(fmaxf(w[j], 1e-30f));
+      const float b = src[(int64_t)i * lds + j];
+      const int64_t e = (int64_t)i * d + j;
+      B[e] = b;
+      BdivD[e] = b / dj;
+      if (i == 0) D[j] = dj;
+    }
   }
 }
 
@@ -268,11 +277,10 @@ void evx_cma_cov_pad(const float* C, const float* S, const float* pc, const floa
   cov_pad_kernel<<<grid, 256, 0, s>>>(C, S, lds > 0 ? lds : d, pc, a, c1, cmu, Bprev, d, np, Cn, Cp, Bp);
 }
 
-void evx_cma_eig_out(const float* Bp, const float* w, int d, int np, float* B, float* D, float* BdivD, hipStream_t s) {
-  const int64_t total = (int64_t)d * d;
-  int g = (int)((total + 255) / 256);
-  if (g > 4096) g = 4096;
-  eig_out_kernel<<<g, 256, 0, s>>>(Bp, w, d, np, B, D, BdivD);
+void evx_cma_eig_out(const float* Bp, const float* w, int d, int np, float* B, float* D, float* BdivD, hipStream_t s, const float* Balt,
+                     const int* keep) {
+  const int g = d < 4096 ? d : 4096;
+  if (g > 0) eig_out_kernel<<<g, 256, 0, s>>>(Bp, w, d, np, B, D, BdivD, Balt, keep);
 }
 
 void evx_cma_center_rows(const float* pop, int64_t ldp, const int32_t* rows, const float* mean, const float* sigma, const float* w, int K,

@@ -411,12 +411,17 @@ class CMAES(Algorithm):
                     # generation's graph, no host read (ops/sbr_device.py)
                     from ....ops.sbr_device import eigh_device
 
-                    w, Bn, eig_stats = eigh_device(Cp[:d, :d], state.B, report=self._report_buffers(state.B.device))
+                    # restore=False: a diverged solve's warm start is selected by cma_eig_out itself
+                    # (keep word), not copied back by a launch of its own
+                    w, Bn, eig_stats, keep = eigh_device(Cp[:d, :d], state.B, report=self._report_buffers(state.B.device),
+                                                         restore=False)
                 else:
                     # host-orchestrated solve: a host phase between hipGraph segments
                     w, Bn, eig_stats = host_phase(sbr_phase, Cp[:d, :d], state.B, self.__dict__.setdefault("_eig_plans", {}),
                                                   out_like=(state.D, state.B, state.eig_stats))
-            B, D, BdivD = ops.cma_eig_out(Bn.contiguous(), w.contiguous(), d, b_out)
+                    keep = None
+            B, D, BdivD = ops.cma_eig_out(Bn.contiguous(), w.contiguous(), d, b_out, state.B.contiguous() if keep is not None else None,
+                                          keep)
         else:
             np_ = jacobi.padded_size(d)
             C, Cp, Bp = ops.cma_cov_pad(state.C.contiguous(), S if S.stride(1) == 1 else S.contiguous(), pc, a, float(self.c1),

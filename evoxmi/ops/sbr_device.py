@@ -256,7 +256,7 @@ class DeviceSBR:
         self._ctrl(j, C, report)
 
     # ------------------------------------------------------------------ solve
-    def solve(self, C: torch.Tensor, B_prev: torch.Tensor, report=None):
+    def solve(self, C: torch.Tensor, B_prev: torch.Tensor, report=None, restore: bool = True):
         """(w, B, eig_stats) with C ≈ B diag(w) Bᵀ — device buffers of this workspace, valid
         until the next solve.  Nothing is read back; capturable into a hipGraph.  ``report``:
         (int32 device counter, pinned host float64 [R, 5] ring) — the last slot's control kernel
@@ -270,8 +270,15 @@ class DeviceSBR:
         for j in range(self.K):
             self._iteration(j, C, B_prev if j == 0 else None, report if j == self.K - 1 else None)
         # the refinement diverged, or no iteration ran (st[5] = 0): the warm-start basis is the result
-        ops.sbr_dev_copy(B_prev, self.B, self.st[5:6])
+        # (restore=False: the caller selects it itself from keep_word — CMA-ES's cma_eig_out)
+        if restore:
+            ops.sbr_dev_copy(B_prev, self.B, self.st[5:6])
         return self.w, self.B, self.eig_stats
+
+    @property
+    def keep_word(self) -> torch.Tensor:
+        """int32 device word: 0 ⇒ the last solve's basis is its warm start (not written to B)."""
+        return self.st[5:6]
 
     def history(self, last: int = None):
         """[off_rel, 0, refinement iterations, fallback] of the most recent solves (one
@@ -313,11 +320,13 @@ def device_config(ns_iters: int = None) -> SBRConfig:
     return SBRConfig(tol=config.get("eigh_tol"), block=config.get("sbr_block"), **kw)
 
 
-def eigh_device(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None, iters: int = None, report=None):
+def eigh_device(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None, iters: int = None, report=None, restore: bool = True):
     """Converged-or-capped eigendecomposition of symmetric ``C`` warm-started from
     ``B_prev``, entirely on the device (see module docstring).  Returns ``(w, B, stats)``.
     ``iters``: an explicit schedule of that many slots, every slot full (tests, probes);
-    default: the schedule of the active level (:func:`use_schedule`, warm outside a context)."""
+    default: the schedule of the active level (:func:`use_schedule`, warm outside a context).
+    ``restore=False``: no restore-copy launch; a fourth value, the keep word, tells the caller
+    whether B or B_prev is the basis (``ops.cma_eig_out(..., B_alt, keep)`` selects in-kernel)."""
     from .. import config
 
     if iters is None:
@@ -325,7 +334,10 @@ def eigh_device(C: torch.Tensor, B_prev: torch.Tensor, cfg: SBRConfig = None, it
     else:
         sch = Schedule(int(iters), None, None, DEVICE_CFG["ns_iters"], int(iters) >= int(config.get("sbr_cold_iters")))
     cfg = cfg or device_config(sch.ns_iters)
-    return workspace(C.shape[0], C.device, cfg, sch.iters, sch.lean_from, sch.xgate, sch.damp_from).solve(C, B_prev, report)
+    ws = workspace(C.shape[0], C.device, cfg, sch.iters, sch.lean_from, sch.xgate, sch.damp_from)
+    out = ws.solve(C, B_prev, report, restore)
+    # restore=False: (w, B, stats, keep) — B holds the result only while keep != 0, else it is B_prev
+    return out if restore else (*out, ws.keep_word)
 
 
 def all_histories():

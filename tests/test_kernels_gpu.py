@@ -1186,3 +1186,47 @@ def test_openes_population_kernel_matches_noise_rows(d, mirrored):
         ref = center[None, :] + es.noise_stdev * es._noise_rows(key, start, size, center.device)
         got = es._population_rows(key, center, start, size)
         assert torch.equal(got, ref), (start, size)
+
+
+@pytest.mark.parametrize("keep", [0, 1])
+def test_cma_eig_out_selects_the_warm_start_on_the_keep_word(keep):
+    """Round 6: the device eigensolver's restore copy is folded into cma_eig_out — while the keep
+    word is 0 (diverged / no iteration ran) the basis is the warm start B_alt (here the output
+    buffer itself, as under capture), else the solver's basis; D = sqrt(w), B/D by columns."""
+    d = 96
+    g = torch.Generator().manual_seed(3)
+    Bp = torch.randn(d, d, generator=g).cuda()
+    Bw = torch.randn(d, d, generator=g).cuda()
+    w = (torch.rand(d, generator=g) + 0.1).cuda()
+    out = Bw.clone()  # B_out aliases B_alt
+    kw = torch.full((1,), keep, dtype=torch.int32, device="cuda")
+    B, D, BD = _ext.ops().cma_eig_out(Bp, w, d, out, out, kw)
+    ref = Bp if keep else Bw
+    assert B.data_ptr() == out.data_ptr()
+    assert torch.equal(B, ref)
+    assert torch.allclose(D, w.sqrt())
+    assert torch.allclose(BD, ref / w.sqrt()[None, :], rtol=1e-6, atol=1e-7)
+
+
+def test_cma_center_rows_augmented_product_carries_the_mean_shift():
+    """Round 6: the rank-μ rows augmented by σ·sqrt(wᵢ) — the (d+1)-square product's last row is
+    Σ wᵢ (xᵢ − m) and its leading block Σ wᵢ yᵢ yᵢᵀ (fp64 reference)."""
+    from evoxmi.ops.linalg import mm
+
+    d, n, K = 1000, 300, 120
+    g = torch.Generator().manual_seed(4)
+    pop = (torch.randn(n, d, generator=g) * 3).cuda()
+    mean = torch.randn(d, generator=g).cuda()
+    sigma = torch.tensor([1.7]).cuda()
+    rows = torch.randperm(n, generator=g)[:K].to(torch.int32).cuda()
+    w = torch.rand(K, generator=g).cuda()
+    w = w / w.sum()
+    Yw = _ext.ops().cma_center_rows(pop, rows, mean, sigma, w, True)
+    assert Yw.shape == (K, d + 1) and Yw.stride(0) % 4 == 0
+    S = mm(Yw, Yw, ta=True, mode=1, out=torch.empty(d + 1, Yw.stride(0), device="cuda")[:, : d + 1])
+    x = pop[rows.long()].double() - mean.double()
+    dm = (w.double()[:, None] * x).sum(0)
+    y = x / 1.7
+    Sref = (y * w.double()[:, None]).T @ y
+    assert torch.allclose(S[d, :d].double(), dm, rtol=1e-5, atol=1e-5)
+    assert torch.allclose(S[:d, :d].double(), Sref, rtol=1e-5, atol=3e-5)
