@@ -722,7 +722,10 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_h3_kernel(EvxGemmBlk p) {
     // lgkmcnt(0) in front of the next MFMAs); the barrier is asm with a memory clobber so no
     // LDS read moves above it
     const int after = min(NS - 2, KB - 1 - t);
-    if (after >= 3 && NS >= 5) __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(3 * PMIN));
+    if (after >= 6 && NS >= 8) __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(6 * PMIN));
+    else if (after == 5 && NS >= 7) __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(5 * PMIN));
+    else if (after == 4 && NS >= 6) __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(4 * PMIN));
+    else if (after >= 3 && NS >= 5) __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(3 * PMIN));
     else if (after == 2 && NS >= 4) __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(2 * PMIN));
     else if (after == 1) __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(PMIN));
     else __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(0));
@@ -895,6 +898,7 @@ void launch_h3(EvxGemmBlk a, hipStream_t s, int var) {
 }
 
 int g_h3_ns = -1;
+int g_h3_cfg = -1;
 
 int g_blk_variant = -1;
 
@@ -980,6 +984,39 @@ void evx_gemm_h3(const EvxGemmBlk& a, hipStream_t s) {
   if (g_h3_ns < 0) {
     const char* e = getenv("EVOXMI_H3_NS");
     g_h3_ns = e ? atoi(e) : 5;
+  }
+  // Tile height by how the product fills 256 CUs: the shortest of 64 / 128 / 192 / 320 rows
+  // (× 128 columns, 8 waves) whose tiles fit in one wave of tiles — a population shard has
+  // fewer rows than the flagship's 10 000 (5000 at 2 ranks, 1250 at 8), and 320-row tiles
+  // would leave half / seven eighths of the chip idle.  Measured (eager, µs; tools/
+  // bench_gemm_blk.py --only-h3, profiles/r6_h3_tile_heights.jsonl) at × 1000 × 1000:
+  //   rows    320    192    128(NS6)  64     160×128 on 4 waves
+  //   10000   82.2   97.1   102.6     99.8   108.6
+  //    5000   72.0   52.8    67.8     60.4    58.1
+  //    2500   65.7   46.3    36.4     39.9    53.0
+  //    1250   66.8   44.0    33.7     29.7    51.2
+  // (64 rows with 8 stages, 128 with 4, 32 × 128 on 4 waves: no better — removed).
+  if (g_h3_cfg < 0) {
+    const char* e = getenv("EVOXMI_H3_CFG");  // probe override: 1 = 320, 2 = 192, 3 = 128, 4 = 64 rows
+    g_h3_cfg = e ? atoi(e) : 0;
+  }
+  int cfg = g_h3_cfg;
+  if (cfg < 1 || cfg > 4) {
+    const int64_t tn = (a.N + 127) / 128;
+    auto fits = [&](int bm) { return (int64_t)((a.M + bm - 1) / bm) * tn <= 256; };
+    cfg = fits(64) ? 4 : fits(128) ? 3 : fits(192) ? 2 : 1;
+  }
+  if (cfg == 2) {
+    launch_h3<2, 4, 3, 1, 5>(a, s, g_blk_variant);
+    return;
+  }
+  if (cfg == 3) {
+    launch_h3<2, 4, 2, 1, 6>(a, s, g_blk_variant);
+    return;
+  }
+  if (cfg == 4) {
+    launch_h3<2, 4, 1, 1, 5>(a, s, g_blk_variant);
+    return;
   }
   switch (g_h3_ns) {
     case 3: launch_h3<2, 4, 5, 1, 3>(a, s, g_blk_variant); break;

@@ -294,9 +294,15 @@ def blk_tile() -> tuple:
 
 
 def blk_worthwhile(M: int, N: int, n_cu: int = 256) -> bool:
-    """True when the 320 × 128-tile launch fills the chip (≥ ¾ of the CUs busy in its last
-    wave of tiles) — smaller products stay on the K-split ``gemm_ks``."""
+    """True when the f16x3 tall launch fills the chip: the 320 × 128-tile launch with ≥ ¾ of
+    the CUs busy in its last wave of tiles, or a population shard's product (M ≥ 1024 rows,
+    N ≥ 512: ``evx_gemm_h3`` then takes 160 × 128 or 64 × 128 tiles, ≥ 128 of them — the
+    sharded flagship's 5000 / 2500 / 1250 × 1000 × 1000 sampling and rotation products, which
+    on the K-split ``gemm_ks`` ran at 100 / 37 µs each, profiles/r6_phase_table_sim.md).
+    Smaller products stay on ``gemm_ks``."""
     tiles = -(-M // 320) * -(-N // 128)
+    if M >= 1024 and N >= 512:
+        return True
     if tiles < (3 * n_cu) // 4:
         return False
     rem = tiles % n_cu

@@ -32,7 +32,9 @@ def test_blk_cpu_semantics():
 @pytest.mark.gpu
 @pytest.mark.parametrize("fmt", sorted(FMTS))
 @pytest.mark.parametrize("M,N,K", [(10000, 1000, 1000), (1, 1, 1), (700, 130, 20), (333, 1000, 37), (2560, 256, 16),
-                                   (10240, 1024, 1008), (5000, 600, 1000), (321, 129, 17), (640, 256, 4096), (100, 64, 5000)])
+                                   (10240, 1024, 1008), (5000, 600, 1000), (321, 129, 17), (640, 256, 4096), (100, 64, 5000),
+                                   # population shards of the flagship: the 160 × 128 / 64 × 128-tile launches
+                                   (5000, 1000, 1000), (2500, 1000, 1000), (1250, 1000, 1000), (1111, 520, 999)])
 def test_gemm_blk_matches_fp64(M, N, K, fmt):
     split, _, mm = FMTS[fmt]
     g = torch.Generator().manual_seed(M + 3 * N + 7 * K)

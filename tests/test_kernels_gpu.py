@@ -141,6 +141,38 @@ def test_cec2022_gpu_matches_cpu(f, D):
     assert torch.allclose(out.cpu(), ref, rtol=2e-3, atol=1e-3), (f, D, out[:3], ref[:3])
 
 
+@pytest.mark.parametrize("f", [1, 2, 4])
+@pytest.mark.parametrize("rows", [1250, 5000])
+def test_cec2022_d1000_shard_rows_match_cpu(f, rows):
+    """A population shard of the flagship (λ = 10 000 over 8 / 2 ranks) evaluates its rows on the
+    f16x3 rotation with the fused row terms at the shorter tile heights (csrc/kernels/gemm_blk.hip
+    evx_gemm_h3): equal to the CPU evaluation; Zakharov (F1) against a float64 evaluation at the
+    bound of its conditioning — Σ ½·i·z cancels over 1000 terms of both signs and enters as its
+    fourth power, so the f32 CPU result itself is off by up to ~1e-2 on such rows."""
+    from evoxmi.ops import linalg
+    from evoxmi.problems.numerical import CEC2022TestSuit
+
+    assert linalg.tall_nt_ok(rows, 1000, 1000, torch.device("cuda"))
+    p = CEC2022TestSuit.create(f)
+    X = torch.rand(rows, 1000, generator=torch.Generator().manual_seed(f + rows)) * 200 - 100
+    out, _ = p.evaluate(None, X.cuda())
+    out = out.cpu().double()
+    if f == 1:
+        c = p._consts(1000, torch.device("cpu"))
+        z = (X.double() - c["Os"][:1000].double()) @ c["M"].double().t()
+        hi = 0.5 * torch.arange(1, 1001, dtype=torch.float64)
+        s2, a2 = (hi * z).sum(1), (hi * z).abs().sum(1)
+        ref = (z * z).sum(1) + s2 ** 2 + s2 ** 4
+        scale = (z * z).sum(1) + a2 ** 2 + a2 ** 4
+        cpu, _ = p.evaluate(None, X)
+        assert ((cpu.double() - ref).abs() <= 1e-4 * scale).all()  # the reference formula is the suite's
+        err = (out - ref).abs() / scale
+    else:
+        ref, _ = p.evaluate(None, X)
+        err = (out - ref.double()).abs() / ref.double().abs()
+    assert float(err.max()) <= 1e-4, (f, rows, float(err.max()))
+
+
 @pytest.mark.parametrize("f", [9, 10, 11, 12])
 def test_cec2022_compositions_d1000_fused_path(f):
     """d = 1000 at a population that takes the stacked f16x3 GEMM (one split of X into every

@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--shapes", default="10000x1000x1000,5000x1000x1000,10240x1024x1024")
     ap.add_argument("--only-blk", action="store_true")
+    ap.add_argument("--only-h3", action="store_true", help="time the f16x3 product only (with EVOXMI_H3_CFG: one tile config)")
     args = ap.parse_args()
     dev = torch.device("cuda")
     # clocks up before the first timed case
@@ -58,6 +59,10 @@ def main():
         Bh = linalg.h3_planes(B)
         res["h3_gemm_us"] = timeit(lambda: linalg.mm_h3(Ah, Bh, alpha_ptr=sig, bias_n=bias, out=out), args.reps)
         res["h3_pct_x3_ceiling"] = round(100 * 2.0 * M * N * K * 3 / (res["h3_gemm_us"] * 1e-6) / 2.5e15, 1)
+        if args.only_h3:
+            res["h3_cfg"] = os.environ.get("EVOXMI_H3_CFG", "auto")
+            print(json.dumps({k: (round(v, 2) if isinstance(v, float) else v) for k, v in res.items()}), flush=True)
+            continue
         res["blk_gemm_us"] = timeit(lambda: linalg.mm_blk(Ap, Bp, alpha_ptr=sig, bias_n=bias, out=out), args.reps)
         if args.only_blk:
             flops = 2.0 * M * N * K
