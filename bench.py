@@ -180,6 +180,7 @@ def main():
             "gemm_precision": ({"x6": "bf16x6", "x6w": "bf16x6 32x32", "f32": "f32 MFMA"}.get(config.get("gemm_prec"), config.get("gemm_prec"))
                                + (" square / f16x3 tall" if config.get("gemm_tall") == "h3" else "") + " (f32-accurate)"
                                + {"x3all": "; eigensolver corrections (exp(αX) − I terms, basis update, Newton–Schulz) bf16x3",
+                                  "x3late": "; eigensolver exp(αX) − I terms bf16x3, settled solves' basis corrections bf16x3",
                                   "x3": "; eigensolver exp(αX) − I terms bf16x3"}.get(config.get("sbr_corr_prec"), "")),
             "data": f"synthetic (seeded CEC'22 F{args.func} shift + Haar rotation at d={args.dim}; random init mean)",
             "generations_per_sec": round(gens_per_s, 3),

@@ -43,7 +43,7 @@ KNOBS: Dict[str, Knob] = {
     "sbr_device_iters": Knob("EVOXMI_SBR_DEVICE_ITERS", 7, int, "device eigensolver: refinement slots of the warm schedule (the tuned constants of the three schedules are in ops/sbr_device.py) (kernels of iterations past convergence return at once; round 5: 8 → 7 slots, 1.644-1.656 → 1.630 ms at 20 steps — warm solves at d ≤ 1000 take at most 6 iterations on F1 / F4 / F6 / F12 over 200 generations, and a capped solve escalates the schedule)"),
     "sbr_cold_iters": Knob("EVOXMI_SBR_COLD_ITERS", 16, int, "CMA-ES device eigensolver: refinement slots of the cold-start schedule (every run starts on it; CMAES moves down to the warm / late schedules after consecutive solves that fit them with a slot to spare)"),
     "sbr_late_iters": Knob("EVOXMI_SBR_LATE_ITERS", 5, int, "refinement slots of the late (settled) eigensolver schedule (settled solves take 4; a capped or slow solve moves the run back up two generations later — round 5: 6 → 5 slots, 1.439 → 1.424 ms over 50 steps)"),
-    "sbr_corr_prec": Knob("EVOXMI_SBR_CORR_PREC", "x3", str, "device eigensolver: precision of the correction products — 'x3' (default): the Taylor terms of exp(αX) − I (X², X³, the Vᵀ GEMM) as bf16x3 (≈1e-5 of the correction's own size; the basis update Bq + Bq·(V − I), Newton–Schulz and the residual products Bᵀ C B, TᵀT stay bf16x6); 'x3all': the basis update and Newton–Schulz's T·(TᵀT − I) too (2 % faster; trajectory parity over 15 seeds as good as x6, but one fallback in the degenerate-spectrum stress test tests/test_sbr_device_gpu.py::test_sim8_trajectory_recovers_from_divergence); 'x6': every product f32-accurate (the round-5 solver)"),
+    "sbr_corr_prec": Knob("EVOXMI_SBR_CORR_PREC", "x3late", str, "device eigensolver: precision of the correction products — 'x3': the Taylor terms of exp(αX) − I (X², X³, the Vᵀ GEMM) as bf16x3 (≈1e-5 of the correction's own size; the basis update Bq + Bq·(V − I), Newton–Schulz and the residual products Bᵀ C B, TᵀT stay bf16x6); 'x3late' (default): as 'x3', plus the basis update and Newton–Schulz correction at bf16x3 in the late (settled) schedule level only (50 steps 1.345 vs 1.363 ms; the eigensolver GPU tests pass unchanged); 'x3all': the basis update and Newton–Schulz's T·(TᵀT − I) at every level (2 % faster; trajectory parity over 15 seeds as good as x6, but one fallback in the degenerate-spectrum stress test tests/test_sbr_device_gpu.py::test_sim8_trajectory_recovers_from_divergence); 'x6': every product f32-accurate (the round-5 solver)"),
     "cma_fused": Knob("EVOXMI_CMA_FUSED", 1, int, "CMA-ES tell epilogue as the fused cmaes.hip kernels (0: reference-shaped torch ops)"),
     "cec_stack": Knob("EVOXMI_CEC_STACK", 1, int, "CEC'22 compositions (F9–F12) on the device: every rotated component from ONE GEMM over the stacked rotations with per-block exact shifts (1) or one GEMM per component (0)"),
     "cec_compose_fused": Knob("EVOXMI_CEC_COMPOSE_FUSED", 1, int, "CEC'22 compositions on the device: every component's basic function, the distances and the weighted sum in one kernel after the stacked GEMM (cec2022.hip: cec_compose_kernel) (1) or per-component launches (0)"),
