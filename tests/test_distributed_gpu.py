@@ -34,12 +34,15 @@ def _make(kind):
         d = 64
         alg = CMAES(torch.linspace(-3, 3, d, device="cuda"), init_stdev=2.0, pop_size=512)
         return StdWorkflow(alg, CEC2022TestSuit.create(1))
+    if kind == "flagship":  # bench.py's config: each of 2 ranks samples / evaluates 5000 rows (192-row f16x3 tiles)
+        center = (torch.rand(1000, generator=torch.Generator().manual_seed(1)) * 160 - 80).cuda()
+        return StdWorkflow(CMAES(center_init=center, init_stdev=20.0, pop_size=10000), CEC2022TestSuit.create(1))
     alg = OpenES(torch.full((40,), 1.0, device="cuda"), 256, learning_rate=0.05, noise_stdev=0.2, optimizer="adam")
     return StdWorkflow(alg, Sphere())
 
 
 def _field(kind):
-    return "mean" if kind == "cmaes" else "center"
+    return "mean" if kind in ("cmaes", "flagship") else "center"
 
 
 def _worker(rank, world, port, kind, gens, out, seed=3):
@@ -57,7 +60,7 @@ def _worker(rank, world, port, kind, gens, out, seed=3):
     torch.cuda.synchronize()
     alg = st.get_child_state("algorithm")
     out[rank] = alg[_field(kind)].cpu()
-    if kind == "cmaes":
+    if kind in ("cmaes", "flagship"):
         out[("sigma", rank)] = alg["sigma"].cpu()
     destroy()
 
@@ -65,7 +68,7 @@ def _worker(rank, world, port, kind, gens, out, seed=3):
 # CMA-ES: one generation (afterwards the Jacobi eigenbasis of the clustered spectrum
 # amplifies rounding-level differences of the all-reduced statistics into different
 # — equally valid — sample rotations, so longer runs are compared replica-to-replica only)
-@pytest.mark.parametrize("kind,gens", [("cmaes", 1), ("cmaes", 5), ("openes", 8)])
+@pytest.mark.parametrize("kind,gens", [("cmaes", 1), ("cmaes", 5), ("openes", 8), ("flagship", 1)])
 def test_sharded_two_ranks_on_gpu_match_single_process(kind, gens):
     from evoxmi import random as rnd
 
@@ -79,6 +82,12 @@ def test_sharded_two_ranks_on_gpu_match_single_process(kind, gens):
     mp.spawn(_worker, args=(2, _free_port(), kind, gens, out), nprocs=2, join=True)
     assert torch.equal(out[0], out[1])  # replicas stay bit-identical
     if kind == "cmaes" and gens > 1:
+        return
+    if kind == "flagship":
+        # the shard's 5000-row sampling / rotation products on the shorter f16x3 tiles, the packed
+        # rank-μ all-reduce: the same population rows (Philox row offsets), sums in another order
+        assert torch.equal(out[("sigma", 0)], out[("sigma", 1)])
+        assert torch.allclose(out[0], ref, rtol=1e-4, atol=1e-4), float((out[0] - ref).abs().max())
         return
     # reduction order differs from the single process (rank partial sums + all-reduce)
     assert torch.allclose(out[0], ref, rtol=1e-3, atol=1e-3)
