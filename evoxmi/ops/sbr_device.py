@@ -59,7 +59,9 @@ LEAN_GUARD = 1       # a lean slot whose step needs damping / NS / order 6 stops
 FULL_SLOTS = 5       # warm schedule: slots ≥ 5 are lean (no damping / NS / X³ kernels)
 LATE_FULL_SLOTS = 3  # late schedule: damping / NS / order-6 kernels in slots 0-2 only
 LATE_DAMP_SLOTS = 1  # late schedule: the damping power steps in slot 0 only (89 launches / generation)
-LATE_NS_ITERS = 2    # forced Newton–Schulz steps per late solve (1: trajectory parity 5.8 % > 5 % bound)
+LATE_NS_ITERS = 1    # forced Newton–Schulz steps per late solve: 1 since the end of round 6 (with x3late: 50 steps
+                     # 1.3325 vs 1.3499 ms, ‖BᵀB − I‖ bounded over 600 generations, 10-seed trajectory parity
+                     # passes; round 5 had kept 2 after the 5-seed parity statistic read 5.8 % > 5 %)
 LEAN_MAX_N = 1024    # larger matrices keep every slot full (d = 2000 capped in a lean slot)
 CW = 8               # control words per slot (eigh_sbr_dev.hip kCW)
 LARGE_N_ITERS = 8    # ... and get at least 8 slots (7 capped one d = 2000 solve)

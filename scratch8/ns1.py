@@ -1,0 +1,17 @@
+"""A/B probe: the late schedule with ONE forced Newton–Schulz step (sbr_device.LATE_NS_ITERS = 1)
+for the bench (argv: bench args) or pytest (argv[1] == 'pytest')."""
+import os
+import sys
+
+sys.path.insert(0, os.getcwd())
+import evoxmi.ops.sbr_device as sd  # noqa: E402
+
+sd.LATE_NS_ITERS = int(os.environ.get("NS_LATE", "1"))
+if len(sys.argv) > 1 and sys.argv[1] == "pytest":
+    import pytest
+
+    sys.exit(pytest.main(sys.argv[2:]))
+import bench  # noqa: E402
+
+sys.argv = ["bench.py"] + sys.argv[1:]
+bench.main()

@@ -206,8 +206,8 @@ def test_cmaes_default_schedule_converges_on_other_functions_and_dims(func, d):
 
 def test_cmaes_basis_stays_orthogonal_over_600_generations():
     """Over 600 generations of the flagship run the basis error stays bounded (‖BᵀB − I‖_F
-    ≈ 1.4e-5 with the default two forced Newton–Schulz steps per settled generation, 2e-5 with
-    one; with none it grows linearly to 3.8e-3, profiles/r5_late_ns_orthogonality.txt) and B
+    ≈ 1.4e-5 with two forced Newton–Schulz steps per settled generation, 2e-5 with one (the
+    default since the end of round 6); with none it grows linearly to 3.8e-3, profiles/r5_late_ns_orthogonality.txt) and B
     still diagonalises C."""
     from evoxmi import random as rnd
     from evoxmi.algorithms import CMAES
