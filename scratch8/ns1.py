@@ -6,7 +6,8 @@ import sys
 sys.path.insert(0, os.getcwd())
 import evoxmi.ops.sbr_device as sd  # noqa: E402
 
-sd.LATE_NS_ITERS = int(os.environ.get("NS_LATE", "1"))
+sd.LATE_NS_ITERS = int(os.environ.get("NS_LATE", str(sd.LATE_NS_ITERS)))
+sd.LATE_FULL_SLOTS = int(os.environ.get("LATE_FULL", str(sd.LATE_FULL_SLOTS)))
 if len(sys.argv) > 1 and sys.argv[1] == "pytest":
     import pytest
 
