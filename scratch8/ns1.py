@@ -8,6 +8,7 @@ import evoxmi.ops.sbr_device as sd  # noqa: E402
 
 sd.LATE_NS_ITERS = int(os.environ.get("NS_LATE", str(sd.LATE_NS_ITERS)))
 sd.LATE_FULL_SLOTS = int(os.environ.get("LATE_FULL", str(sd.LATE_FULL_SLOTS)))
+sd.DEVICE_CFG["ns_iters"] = int(os.environ.get("NS_WARM", str(sd.DEVICE_CFG["ns_iters"])))
 if len(sys.argv) > 1 and sys.argv[1] == "pytest":
     import pytest
 
