@@ -296,9 +296,10 @@ def blk_tile() -> tuple:
 def blk_worthwhile(M: int, N: int, n_cu: int = 256) -> bool:
     """True when the f16x3 tall launch fills the chip: the 320 × 128-tile launch with ≥ ¾ of
     the CUs busy in its last wave of tiles, or a population shard's product (M ≥ 1024 rows,
-    N ≥ 512: ``evx_gemm_h3`` then takes 160 × 128 or 64 × 128 tiles, ≥ 128 of them — the
-    sharded flagship's 5000 / 2500 / 1250 × 1000 × 1000 sampling and rotation products, which
-    on the K-split ``gemm_ks`` ran at 100 / 37 µs each, profiles/r6_phase_table_sim.md).
+    N ≥ 512: ``evx_gemm_h3`` then takes the shortest of 64 / 128 / 192-row tiles whose tiles fit
+    one wave of 256 — the sharded flagship's 5000 / 2500 / 1250 × 1000 × 1000 sampling and
+    rotation products, which on the K-split ``gemm_ks`` ran at 100 / 37 µs each,
+    profiles/r6_phase_table_sim.md).
     Smaller products stay on ``gemm_ks``."""
     tiles = -(-M // 320) * -(-N // 128)
     if M >= 1024 and N >= 512:
